@@ -1,0 +1,161 @@
+// Python bindings of the native layer: HIP kernel launchers + host runtime.
+// Every launcher validates shapes/dtypes/devices here (host side) before a kernel
+// is launched, so a wrong call fails loudly instead of faulting the GPU.
+#include <torch/extension.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <ATen/DeviceGuard.h>
+
+#include "ddl_gemm.h"
+#include "ddl_ops.h"
+
+namespace py = pybind11;
+using namespace ddl;
+
+namespace {
+
+inline hipStream_t cur_stream() { return at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+
+#define CHECK_CUDA(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
+#define CHECK_BF16(x) TORCH_CHECK((x).scalar_type() == at::kBFloat16, #x " must be bf16")
+#define CHECK_F32(x) TORCH_CHECK((x).scalar_type() == at::kFloat, #x " must be fp32")
+#define CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
+#define HIP_OK(expr)                                                                   \
+  do {                                                                                 \
+    int _e = (expr);                                                                   \
+    TORCH_CHECK(_e == 0, "HIP launch failed: ", hipGetErrorString((hipError_t)_e)); \
+  } while (0)
+
+void fill_geom(ConvGeom& g, const py::dict& d) {
+  g.n = d["n"].cast<int>();
+  g.hi = d["hi"].cast<int>();
+  g.wi = d["wi"].cast<int>();
+  g.c = d["c"].cast<int>();
+  g.ho = d["ho"].cast<int>();
+  g.wo = d["wo"].cast<int>();
+  g.sh = d["sh"].cast<int>();
+  g.sw = d["sw"].cast<int>();
+  g.tap_c = d["tap_c"].cast<int>();
+  auto dh = d["dh"].cast<std::vector<int>>();
+  auto dw = d["dw"].cast<std::vector<int>>();
+  std::vector<int> wt = d.contains("wt") ? d["wt"].cast<std::vector<int>>() : std::vector<int>(dh.size(), 0);
+  TORCH_CHECK(dh.size() == dw.size() && dh.size() <= (size_t)kMaxTaps && wt.size() == dh.size(), "bad tap table");
+  g.ntaps = (int)dh.size();
+  for (size_t i = 0; i < dh.size(); ++i) {
+    TORCH_CHECK(dh[i] >= -128 && dh[i] < 128 && dw[i] >= -128 && dw[i] < 128, "tap offset out of int8 range");
+    g.dh[i] = (int8_t)dh[i];
+    g.dw[i] = (int8_t)dw[i];
+    g.wt[i] = (int16_t)wt[i];
+  }
+}
+
+// C[m][n] = alpha * sum_k A(m,k) B(n,k) (+ epilogue).  Modes: see ddl_gemm.h.
+void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t M, int64_t N, int64_t K,
+          int64_t a_mode, int64_t b_mode, int64_t lda, int64_t ldb, int64_t ldc, int64_t epi, int64_t tile,
+          int64_t k_split, double alpha, double beta, c10::optional<at::Tensor> bias,
+          c10::optional<at::Tensor> resid, int64_t ldr, bool relu, c10::optional<py::dict> geom,
+          c10::optional<py::dict> outmap, int64_t b_kdiv, int64_t b_tap_stride,
+          c10::optional<at::Tensor> stats) {
+  CHECK_CUDA(a);
+  CHECK_CUDA(b);
+  CHECK_CUDA(c);
+  CHECK_BF16(a);
+  CHECK_BF16(b);
+  if (epi == EPI_BF16) { CHECK_BF16(c); } else { CHECK_F32(c); }
+  const bool k_vec = a_mode == OP_KC || a_mode == OP_KC_GATHER || b_mode == OP_KC;
+  TORCH_CHECK(!k_vec || K % 8 == 0, "gemm: K-contiguous operands need K % 8 == 0 (16-B vectors), got ", K);
+  if (a_mode == OP_KC) TORCH_CHECK(lda % 8 == 0, "gemm: lda must be a multiple of 8");
+  if (b_mode == OP_KC) TORCH_CHECK(ldb % 8 == 0, "gemm: ldb must be a multiple of 8");
+  if (a_mode == OP_RC) TORCH_CHECK(lda % 8 == 0, "gemm: lda must be a multiple of 8");
+  if (b_mode == OP_RC || b_mode == OP_RC_TAPS) TORCH_CHECK(ldb % 8 == 0, "gemm: ldb must be a multiple of 8");
+  TORCH_CHECK(((uintptr_t)a.data_ptr() % 16) == 0 && ((uintptr_t)b.data_ptr() % 16) == 0, "gemm: operands must be 16-B aligned");
+  TORCH_CHECK(k_split > 0 && k_split % 64 == 0, "gemm: k_split must be a positive multiple of 64");
+  TORCH_CHECK(tile >= 0 && tile <= 3, "gemm: bad tile id");
+  const int bm = (tile == 0 || tile == 1) ? 128 : 64;
+  const int bn = (tile == 0 || tile == 2) ? 128 : 64;
+  if (a_mode == OP_RC || a_mode == OP_RC_GATHER) TORCH_CHECK(M % 8 == 0, "gemm: row-contiguous A needs M % 8 == 0");
+  if (b_mode == OP_RC || b_mode == OP_RC_GATHER || b_mode == OP_RC_TAPS) TORCH_CHECK(N % 8 == 0, "gemm: row-contiguous B needs N % 8 == 0");
+  GemmParams p{};
+  p.a = a.data_ptr();
+  p.b = b.data_ptr();
+  p.c = c.data_ptr();
+  p.lda = lda;
+  p.ldb = ldb;
+  p.ldc = ldc;
+  p.M = (int)M;
+  p.N = (int)N;
+  p.K = (int)K;
+  p.k_split = (int)k_split;
+  p.a_mode = (int)a_mode;
+  p.b_mode = (int)b_mode;
+  p.b_kdiv = (int)b_kdiv;
+  p.b_tap_stride = b_tap_stride;
+  p.alpha = (float)alpha;
+  p.beta = (float)beta;
+  p.relu = relu ? 1 : 0;
+  p.ldr = ldr;
+  if (bias) {
+    CHECK_CUDA(*bias);
+    CHECK_F32(*bias);
+    TORCH_CHECK(bias->numel() >= N, "bias too short");
+    p.bias = bias->data_ptr<float>();
+  }
+  if (resid) {
+    CHECK_CUDA(*resid);
+    CHECK_BF16(*resid);
+    p.resid = resid->data_ptr();
+  }
+  if (geom) {
+    fill_geom(p.g, *geom);
+    if (a_mode == OP_KC_GATHER) TORCH_CHECK(p.g.tap_c % 64 == 0 && K == (int64_t)p.g.ntaps * p.g.tap_c, "conv A gather: tap_c % 64 and K = taps*C");
+    if (b_mode == OP_RC_GATHER) TORCH_CHECK(p.g.tap_c % bn == 0 && N == (int64_t)p.g.ntaps * p.g.tap_c, "conv B gather: tap_c % BN and N = taps*C");
+    if (b_mode == OP_RC_TAPS) TORCH_CHECK(b_kdiv % 64 == 0 && K == (int64_t)p.g.ntaps * b_kdiv, "conv B taps: kdiv % 64 and K = taps*kdiv");
+  } else {
+    TORCH_CHECK(a_mode <= OP_RC && b_mode <= OP_RC, "gather modes need a geometry");
+  }
+  if (outmap) {
+    const auto& d = *outmap;
+    p.om.enabled = 1;
+    p.om.gh = d["gh"].cast<int>();
+    p.om.gw = d["gw"].cast<int>();
+    p.om.hy = d["hy"].cast<int>();
+    p.om.wy = d["wy"].cast<int>();
+    p.om.so = d["so"].cast<int>();
+    p.om.oh = d["oh"].cast<int>();
+    p.om.ow = d["ow"].cast<int>();
+  }
+  if (stats) {
+    CHECK_CUDA(*stats);
+    CHECK_F32(*stats);
+    TORCH_CHECK(epi == EPI_BF16, "fused stats need the bf16 epilogue");
+    TORCH_CHECK(stats->numel() >= (int64_t)kStatShards * 2 * N, "stats workspace too small");
+    p.stats = stats->data_ptr<float>();
+  }
+  (void)bm;
+  at::DeviceGuard guard(a.device());
+  HIP_OK(launch_gemm_bf16(p, (int)epi, (int)tile, cur_stream()));
+}
+
+}  // namespace
+
+void register_ops(py::module& m);      // ops_bindings.cpp style registrations (elementwise, norms, ...)
+void register_runtime(py::module& m);  // host runtime (parameter server, ingest)
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "MI355X-native kernels and runtime of distributeddeeplearningspark_amd";
+  m.def("gemm", &gemm, "MFMA implicit-GEMM (bf16 in, fp32 accumulate)", py::arg("a"), py::arg("b"), py::arg("c"),
+        py::arg("M"), py::arg("N"), py::arg("K"), py::arg("a_mode"), py::arg("b_mode"), py::arg("lda"),
+        py::arg("ldb"), py::arg("ldc"), py::arg("epi"), py::arg("tile"), py::arg("k_split"), py::arg("alpha") = 1.0,
+        py::arg("beta") = 0.0, py::arg("bias") = py::none(), py::arg("resid") = py::none(), py::arg("ldr") = 0,
+        py::arg("relu") = false, py::arg("geom") = py::none(), py::arg("outmap") = py::none(),
+        py::arg("b_kdiv") = 0, py::arg("b_tap_stride") = 0, py::arg("stats") = py::none());
+  m.attr("OP_KC") = (int)OP_KC;
+  m.attr("OP_RC") = (int)OP_RC;
+  m.attr("OP_KC_GATHER") = (int)OP_KC_GATHER;
+  m.attr("OP_RC_GATHER") = (int)OP_RC_GATHER;
+  m.attr("OP_RC_TAPS") = (int)OP_RC_TAPS;
+  m.attr("EPI_BF16") = (int)EPI_BF16;
+  m.attr("EPI_F32") = (int)EPI_F32;
+  m.attr("EPI_F32_ATOMIC") = (int)EPI_F32_ATOMIC;
+  register_ops(m);
+  register_runtime(m);
+}

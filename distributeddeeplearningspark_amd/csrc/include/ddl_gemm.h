@@ -1,0 +1,77 @@
+// Host-visible parameter block for the MFMA implicit-GEMM kernel family.
+//
+// One kernel template covers every GEMM-shaped op of the framework:
+//   * plain GEMMs with either operand K-contiguous ("KC") or row-contiguous ("RC"),
+//     i.e. NT / NN / TN / TT in BLAS terms (Linear fwd / dgrad / wgrad, 1x1 conv);
+//   * NHWC implicit-GEMM convolution: forward and data-gradient gather the A
+//     operand through a tap table (KC_GATHER), weight-gradient gathers the B
+//     operand (RC_GATHER); the data-gradient reads the weights through a tap
+//     table (RC_TAPS) and can scatter its output to a strided grid (stride-2
+//     parity classes).
+// C[m][n] = sum_k A(m,k) * B(n,k)
+#pragma once
+#include <stdint.h>
+
+namespace ddl {
+
+enum OperandMode : int {
+  OP_KC = 0,         // addr = ptr + r*ld + k
+  OP_RC = 1,         // addr = ptr + k*ld + r
+  OP_KC_GATHER = 2,  // conv input gather: r = output pixel, k = tap*C + c
+  OP_RC_GATHER = 3,  // conv input gather: k = output pixel, r = tap*C + c
+  OP_RC_TAPS = 4,    // weight [co][tap][c]: r = c, k = tap*Co + co
+};
+
+enum EpilogueMode : int {
+  EPI_BF16 = 0,        // bf16 store of alpha*acc (+bias)(+resid)(relu)
+  EPI_F32 = 1,         // fp32 store of alpha*acc + beta*C
+  EPI_F32_ATOMIC = 2,  // fp32 atomicAdd of alpha*acc (split-K)
+};
+
+constexpr int kMaxTaps = 64;
+
+struct ConvGeom {
+  int n, hi, wi, c;   // gathered NHWC tensor
+  int ho, wo;         // iteration grid over pixels
+  int sh, sw;         // stride on that grid
+  int ntaps;
+  int tap_c;          // channels per tap inside the gathered dimension
+  int8_t dh[kMaxTaps];
+  int8_t dw[kMaxTaps];
+  int16_t wt[kMaxTaps];  // weight tap index (OP_RC_TAPS)
+};
+
+struct OutMap {       // scatter of output rows to a strided NHWC grid (dgrad parity classes)
+  int enabled;
+  int gh, gw;         // row grid (rows m -> (n, i, j))
+  int hy, wy;         // destination spatial dims
+  int so;             // destination stride
+  int oh, ow;         // destination offsets
+};
+
+struct GemmParams {
+  const void* a; long lda;
+  const void* b; long ldb;
+  void* c; long ldc;
+  int M, N, K;
+  int k_split;        // K elements per split (multiple of 64)
+  int a_mode, b_mode;
+  // RC_TAPS: k -> (tap = k / kdiv, co = k % kdiv); addr = ptr + co*ldb + wt[tap]*tap_stride + r
+  int b_kdiv; long b_tap_stride;
+  ConvGeom g;
+  OutMap om;
+  const float* bias;
+  const void* resid; long ldr;
+  float alpha, beta;
+  int relu;
+  // optional fused per-column batch statistics of the stored bf16 output:
+  // stats[shard][0][n] += sum, stats[shard][1][n] += sum of squares (shard = tile % kStatShards)
+  float* stats;
+};
+
+constexpr int kStatShards = 32;
+
+// host launcher (defined in gemm_bf16.hip); returns hipError_t as int
+int launch_gemm_bf16(const GemmParams& p, int epi, int tile, void* stream);
+
+}  // namespace ddl

@@ -1,0 +1,72 @@
+// Launchers of the non-GEMM kernels (normalisation, pooling, losses, optimizers,
+// data movement).  All tensors are NHWC / row-major, bf16 activations, fp32 statistics,
+// fp32 master weights.  Every launcher returns a hipError_t as int.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ddl {
+
+constexpr int kBnShards = 32;  // == kStatShards: sharded atomic accumulation of per-channel sums
+
+// ---------------- batch norm (x: [M, C] bf16, C % 8 == 0) ----------------
+// ws: [kBnShards][2][C] fp32, must be zero on entry (accumulates sum / sumsq)
+int bn_stats(const void* x, float* ws, long M, int C, hipStream_t s);
+// ws -> mean/invstd (saved for backward), scale/shift for apply, running stats update
+int bn_finalize(const float* ws, long M, int C, const float* gamma, const float* beta, float eps, float momentum,
+                float* running_mean, float* running_var, float* save_mean, float* save_invstd, float* scale,
+                float* shift, hipStream_t s);
+// y = relu?(x*scale[c] + shift[c] + resid)
+int bn_apply(const void* x, const float* scale, const float* shift, const void* resid, void* y, long M, int C,
+             int relu, hipStream_t s);
+// backward pass 1: dy' = dy * (y > 0 if relu) ; ws[shard][0][c] += sum dy', ws[shard][1][c] += sum dy'*xhat
+int bn_bwd_reduce(const void* dy, const void* x, const void* y, const float* mean, const float* invstd, float* ws,
+                  long M, int C, int relu, hipStream_t s);
+// pass 2: grads of gamma/beta (+=) and dx coefficients
+int bn_bwd_finalize(const float* ws, long M, int C, const float* gamma, const float* invstd, float* dgamma,
+                    float* dbeta, float* coef, hipStream_t s);
+// pass 3: dx = coef0[c]*(dy' - coef1[c] - xhat*coef2[c]);  optionally dres = dy' (masked)
+int bn_bwd_dx(const void* dy, const void* x, const void* y, const float* mean, const float* invstd,
+              const float* coef, void* dx, void* dres, long M, int C, int relu, hipStream_t s);
+
+// ---------------- pooling (NHWC) ----------------
+int maxpool_fwd(const void* x, void* y, uint8_t* argmax, int N, int H, int W, int C, int Ho, int Wo, int kh, int kw,
+                int sh, int sw, int ph, int pw, hipStream_t s);
+int maxpool_bwd(const void* dy, const uint8_t* argmax, void* dx, int N, int H, int W, int C, int Ho, int Wo, int kh,
+                int kw, int sh, int sw, int ph, int pw, hipStream_t s);
+int avgpool_global_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t s);
+int avgpool_global_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t s);
+
+// ---------------- losses ----------------
+// logits [B, K] (bf16 or fp32), target: class index (int64) OR probability rows (fp32 [B,K]).
+// loss_rows[b] = CE; dlogits = (softmax - target) * grad_scale  (same dtype as logits)
+int softmax_xent(const void* logits, int logits_bf16, const int64_t* labels, const float* target_probs,
+                 float* loss_rows, void* dlogits, int B, int K, float grad_scale, float label_smoothing,
+                 int ignore_index, hipStream_t s);
+
+// ---------------- elementwise ----------------
+int cast_f32_bf16(const float* x, void* y, long n, hipStream_t s);
+int cast_bf16_f32(const void* x, float* y, long n, hipStream_t s);
+int relu_bwd(const void* dy, const void* y, void* dx, long n, hipStream_t s);
+int add_bf16(const void* a, const void* b, void* y, long n, hipStream_t s);
+int bias_grad(const void* dy, float* db, long M, int N, int accumulate, hipStream_t s);  // db[n] (+)= sum_m dy[m][n]
+int im2col(const void* x, void* col, int n, int hi, int wi, int c, int ho, int wo, int sh, int sw, int ntaps,
+           const int* dh, const int* dw, int kpad, hipStream_t s);
+// ingest: uint8 NHWC images -> bf16 normalised, channel-padded NHWC (cpad >= c)
+int normalize_u8(const uint8_t* x, void* y, long npix, int c, int cpad, const float* mean, const float* invstd,
+                 hipStream_t s);
+
+// ---------------- optimizers over flat fp32 buffers (multi-tensor via the flat arena) ----------------
+// every kernel optionally writes the bf16 compute copy of the updated parameters (w16 != nullptr)
+int sgd_step(float* w, const float* g, float* mom, void* w16, long n, float lr, float momentum, float dampening,
+             float wd, int nesterov, float gscale, hipStream_t s);
+int adam_step(float* w, const float* g, float* m, float* v, void* w16, long n, float lr, float b1, float b2,
+              float eps, float wd, int adamw, float bc1, float bc2, float gscale, hipStream_t s);
+int adagrad_step(float* w, const float* g, float* acc, void* w16, long n, float lr, float eps, float wd, float gscale,
+                 hipStream_t s);
+int rmsprop_step(float* w, const float* g, float* acc, void* w16, long n, float lr, float rho, float eps, float wd,
+                 float gscale, hipStream_t s);
+// sum of squares of a flat fp32 buffer into out[0] (for grad-norm clipping / checksums); out must be zeroed
+int sumsq_f32(const float* x, long n, float* out, hipStream_t s);
+
+}  // namespace ddl

@@ -1,0 +1,285 @@
+// Batch normalisation for NHWC activations viewed as [M = N*H*W, C] (C % 8 == 0).
+// Training-mode statistics are accumulated per channel with sharded fp32 atomics
+// (kBnShards copies, so 1000+ workgroups do not serialise on one cache line), then a
+// per-channel finalize turns them into scale/shift.  The apply pass fuses the residual
+// add and ReLU of a ResNet block; the backward pass fuses the ReLU mask and writes the
+// masked gradient for the residual branch in the same sweep.
+// All sweeps move 16 B per lane (8 bf16) — these kernels are HBM-bound by design.
+#include "ddl_common.h"
+#include "ddl_ops.h"
+
+namespace ddl {
+
+__device__ __forceinline__ void unpack8(const uint4& u, float* f) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  return make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]), pack_bf16x2(f[6], f[7]));
+}
+
+struct ColGeom {  // thread -> (row-lane, column-vector) mapping for column reductions
+  int CV, CT, RT, ct, rt, cv;
+  bool active;
+  __device__ __forceinline__ ColGeom(int C) {
+    CV = C >> 3;
+    CT = CV < 256 ? CV : 256;
+    RT = 256 / CT;
+    ct = threadIdx.x % CT;
+    rt = threadIdx.x / CT;
+    cv = blockIdx.y * CT + ct;
+    active = rt < RT && cv < CV;
+  }
+};
+
+// Block reduction of 16 per-thread partials over the RT row-lanes, then sharded atomics.
+__device__ __forceinline__ void col_reduce_store(float (&acc)[16], const ColGeom& g, float* ws, int C) {
+  __shared__ float red[256 * 17];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) red[threadIdx.x * 17 + i] = acc[i];
+  __syncthreads();
+  if (g.rt == 0 && g.cv < g.CV) {
+    for (int r = 1; r < g.RT; ++r) {
+      const int t = r * g.CT + g.ct;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] += red[t * 17 + i];
+    }
+    float* dst = ws + (long)(blockIdx.x % kBnShards) * 2 * C + g.cv * 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      atomicAdd(dst + i, acc[i]);
+      atomicAdd(dst + C + i, acc[8 + i]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_stats_kernel(const uint4* __restrict__ x, float* ws, long M, int C) {
+  ColGeom g(C);
+  float acc[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  if (g.active) {
+    const long step = (long)gridDim.x * g.RT;
+    long r = (long)blockIdx.x * g.RT + g.rt;
+    for (; r + 3 * step < M; r += 4 * step) {  // 4 independent 16-B loads in flight
+      uint4 u[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) u[q] = x[(r + q * step) * g.CV + g.cv];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float f[8];
+        unpack8(u[q], f);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          acc[i] += f[i];
+          acc[8 + i] += f[i] * f[i];
+        }
+      }
+    }
+    for (; r < M; r += step) {
+      float f[8];
+      unpack8(x[r * g.CV + g.cv], f);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        acc[i] += f[i];
+        acc[8 + i] += f[i] * f[i];
+      }
+    }
+  }
+  col_reduce_store(acc, g, ws, C);
+}
+
+static dim3 col_grid(long M, int C) {
+  const int CV = C >> 3, CT = CV < 256 ? CV : 256, RT = 256 / CT;
+  const int gy = (CV + CT - 1) / CT;
+  long gx = (M + RT - 1) / RT;
+  const long cap = 2048 / gy > 1 ? 2048 / gy : 1;
+  if (gx > cap) gx = cap;
+  return dim3((unsigned)gx, (unsigned)gy);
+}
+
+int bn_stats(const void* x, float* ws, long M, int C, hipStream_t s) {
+  hipLaunchKernelGGL(bn_stats_kernel, col_grid(M, C), dim3(256), 0, s, (const uint4*)x, ws, M, C);
+  return (int)hipGetLastError();
+}
+
+__global__ void bn_finalize_kernel(const float* ws, long M, int C, const float* gamma, const float* beta, float eps,
+                                   float momentum, float* rmean, float* rvar, float* smean, float* sinv, float* scale,
+                                   float* shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s1 = 0.0, s2 = 0.0;
+  for (int k = 0; k < kBnShards; ++k) {
+    s1 += ws[(long)k * 2 * C + c];
+    s2 += ws[(long)k * 2 * C + C + c];
+  }
+  const double mean = s1 / (double)M;
+  double var = s2 / (double)M - mean * mean;
+  if (var < 0) var = 0;
+  const float inv = (float)(1.0 / sqrt(var + (double)eps));
+  const float g = gamma ? gamma[c] : 1.f;
+  const float b = beta ? beta[c] : 0.f;
+  if (smean) smean[c] = (float)mean;
+  if (sinv) sinv[c] = inv;
+  scale[c] = g * inv;
+  shift[c] = b - (float)mean * g * inv;
+  if (rmean) rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mean;
+  if (rvar) {
+    const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unb;
+  }
+}
+
+int bn_finalize(const float* ws, long M, int C, const float* gamma, const float* beta, float eps, float momentum,
+                float* running_mean, float* running_var, float* save_mean, float* save_invstd, float* scale,
+                float* shift, hipStream_t s) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, M, C, gamma, beta, eps, momentum,
+                     running_mean, running_var, save_mean, save_invstd, scale, shift);
+  return (int)hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void bn_apply_kernel(const uint4* __restrict__ x, const float* __restrict__ scale,
+                                                        const float* __restrict__ shift, const uint4* __restrict__ res,
+                                                        uint4* __restrict__ y, long nvec, int CV, int relu) {
+  for (long v = (long)blockIdx.x * 256 + threadIdx.x; v < nvec; v += (long)gridDim.x * 256) {
+    const int c = (int)(v % CV) * 8;
+    float f[8], r[8];
+    unpack8(x[v], f);
+    if (res) unpack8(res[v], r);
+    const float4 s0 = *reinterpret_cast<const float4*>(scale + c), s1 = *reinterpret_cast<const float4*>(scale + c + 4);
+    const float4 h0 = *reinterpret_cast<const float4*>(shift + c), h1 = *reinterpret_cast<const float4*>(shift + c + 4);
+    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float o = f[i] * sc[i] + sh[i];
+      if (res) o += r[i];
+      if (relu) o = fmaxf(o, 0.f);
+      f[i] = o;
+    }
+    y[v] = pack8(f);
+  }
+}
+
+static unsigned ew_grid(long nvec) {
+  long g = (nvec + 255) / 256;
+  if (g > 8192) g = 8192;
+  return (unsigned)(g > 0 ? g : 1);
+}
+
+int bn_apply(const void* x, const float* scale, const float* shift, const void* resid, void* y, long M, int C, int relu,
+             hipStream_t s) {
+  const long nvec = M * (C >> 3);
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(nvec)), dim3(256), 0, s, (const uint4*)x, scale, shift,
+                     (const uint4*)resid, (uint4*)y, nvec, C >> 3, relu);
+  return (int)hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint4* __restrict__ dy, const uint4* __restrict__ x,
+                                                             const uint4* __restrict__ y, const float* __restrict__ mean,
+                                                             float* ws, long M, int C, int relu) {
+  ColGeom g(C);
+  float acc[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  if (g.active) {
+    float mu[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) mu[i] = mean[g.cv * 8 + i];
+    const long step = (long)gridDim.x * g.RT;
+    for (long r = (long)blockIdx.x * g.RT + g.rt; r < M; r += step) {
+      const long idx = r * g.CV + g.cv;
+      float d[8], xv[8];
+      unpack8(dy[idx], d);
+      unpack8(x[idx], xv);
+      if (relu) {
+        float yv[8];
+        unpack8(y[idx], yv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) d[i] = yv[i] > 0.f ? d[i] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        acc[i] += d[i];
+        acc[8 + i] += d[i] * (xv[i] - mu[i]);
+      }
+    }
+  }
+  col_reduce_store(acc, g, ws, C);
+}
+
+int bn_bwd_reduce(const void* dy, const void* x, const void* y, const float* mean, const float* invstd, float* ws,
+                  long M, int C, int relu, hipStream_t s) {
+  (void)invstd;  // applied per channel in bn_bwd_finalize
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, col_grid(M, C), dim3(256), 0, s, (const uint4*)dy, (const uint4*)x,
+                     (const uint4*)y, mean, ws, M, C, relu);
+  return (int)hipGetLastError();
+}
+
+__global__ void bn_bwd_finalize_kernel(const float* ws, long M, int C, const float* gamma, const float* invstd,
+                                       float* dgamma, float* dbeta, float* coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s1 = 0.f, s2 = 0.f;
+  for (int k = 0; k < kBnShards; ++k) {
+    s1 += ws[(long)k * 2 * C + c];
+    s2 += ws[(long)k * 2 * C + C + c];
+  }
+  const float inv = invstd[c];
+  s2 *= inv;  // sum dy' * xhat
+  if (dbeta) dbeta[c] += s1;
+  if (dgamma) dgamma[c] += s2;
+  const float g = gamma ? gamma[c] : 1.f;
+  coef[c] = g * inv;
+  coef[C + c] = s1 / (float)M;
+  coef[2 * C + c] = s2 / (float)M;
+}
+
+int bn_bwd_finalize(const float* ws, long M, int C, const float* gamma, const float* invstd, float* dgamma,
+                    float* dbeta, float* coef, hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, M, C, gamma, invstd, dgamma,
+                     dbeta, coef);
+  return (int)hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const uint4* __restrict__ dy, const uint4* __restrict__ x,
+                                                         const uint4* __restrict__ y, const float* __restrict__ mean,
+                                                         const float* __restrict__ invstd,
+                                                         const float* __restrict__ coef, uint4* __restrict__ dx,
+                                                         uint4* __restrict__ dres, long nvec, int CV, int relu) {
+  const int C = CV * 8;
+  for (long v = (long)blockIdx.x * 256 + threadIdx.x; v < nvec; v += (long)gridDim.x * 256) {
+    const int c = (int)(v % CV) * 8;
+    float d[8], xv[8];
+    unpack8(dy[v], d);
+    unpack8(x[v], xv);
+    if (relu) {
+      float yv[8];
+      unpack8(y[v], yv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d[i] = yv[i] > 0.f ? d[i] : 0.f;
+    }
+    if (dres) dres[v] = pack8(d);
+    float o[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float xh = (xv[i] - mean[c + i]) * invstd[c + i];
+      o[i] = coef[c + i] * (d[i] - coef[C + c + i] - xh * coef[2 * C + c + i]);
+    }
+    dx[v] = pack8(o);
+  }
+}
+
+int bn_bwd_dx(const void* dy, const void* x, const void* y, const float* mean, const float* invstd, const float* coef,
+              void* dx, void* dres, long M, int C, int relu, hipStream_t s) {
+  const long nvec = M * (C >> 3);
+  hipLaunchKernelGGL(bn_bwd_dx_kernel, dim3(ew_grid(nvec)), dim3(256), 0, s, (const uint4*)dy, (const uint4*)x,
+                     (const uint4*)y, mean, invstd, coef, (uint4*)dx, (uint4*)dres, nvec, C >> 3, relu);
+  return (int)hipGetLastError();
+}
+
+}  // namespace ddl

@@ -1,0 +1,95 @@
+// Fused softmax + cross-entropy forward AND backward in one sweep per row:
+// a 256-thread block per row computes an online (max, sum-exp) over the row, then
+// writes the per-row loss and dlogits = (softmax - target) * grad_scale.
+// Targets are class indices (with label smoothing / ignore_index) or probability rows
+// (Keras categorical_crossentropy with one-hot label vectors).
+#include "ddl_common.h"
+#include "ddl_ops.h"
+
+namespace ddl {
+
+template <bool BF16>
+__device__ __forceinline__ float ld_logit(const void* p, long i) {
+  if constexpr (BF16) return bf2f(reinterpret_cast<const bf16_t*>(p)[i]);
+  else return reinterpret_cast<const float*>(p)[i];
+}
+
+template <bool BF16>
+__global__ __launch_bounds__(256) void softmax_xent_kernel(const void* __restrict__ logits,
+                                                            const int64_t* __restrict__ labels,
+                                                            const float* __restrict__ tprob, float* loss_rows,
+                                                            void* dlogits, int K, float gscale, float smooth,
+                                                            int ignore_index) {
+  const int b = blockIdx.x;
+  const long base = (long)b * K;
+  __shared__ float sm[2][4];
+  // pass 1: online max / sum-exp
+  float m = -INFINITY, s = 0.f;
+  for (int k = threadIdx.x; k < K; k += 256) {
+    const float x = ld_logit<BF16>(logits, base + k);
+    if (x > m) {
+      s = s * __expf(m - x) + 1.f;
+      m = x;
+    } else {
+      s += __expf(x - m);
+    }
+  }
+  // wave reduce (m, s)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(m, o, 64), os = __shfl_xor(s, o, 64);
+    const float nm = fmaxf(m, om);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + (om == -INFINITY ? 0.f : os * __expf(om - nm));
+    m = nm;
+  }
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) {
+    sm[0][wid] = m;
+    sm[1][wid] = s;
+  }
+  __syncthreads();
+  float M = sm[0][0];
+  for (int w = 1; w < 4; ++w) M = fmaxf(M, sm[0][w]);
+  float S = 0.f;
+  for (int w = 0; w < 4; ++w) S += sm[1][w] * __expf(sm[0][w] - M);
+  const float lse = M + __logf(S);
+  const int64_t lab = labels ? labels[b] : -1;
+  const bool ignored = labels && lab == (int64_t)ignore_index;
+  // pass 2: loss terms and gradient
+  float lpart = 0.f;
+  const float off = smooth / (float)K;
+  for (int k = threadIdx.x; k < K; k += 256) {
+    const float x = ld_logit<BF16>(logits, base + k);
+    const float p = __expf(x - lse);
+    float t;
+    if (tprob) t = tprob[base + k];
+    else t = (k == lab ? 1.f - smooth : 0.f) + off;
+    if (ignored) t = 0.f;
+    lpart += t * (lse - x);
+    const float g = ignored ? 0.f : (p - t) * gscale;
+    if (dlogits) {
+      if constexpr (BF16) reinterpret_cast<bf16_t*>(dlogits)[base + k] = f2bf(g);
+      else reinterpret_cast<float*>(dlogits)[base + k] = g;
+    }
+  }
+  lpart = warp_sum(lpart);
+  __syncthreads();
+  if (lane == 0) sm[0][wid] = lpart;
+  __syncthreads();
+  if (threadIdx.x == 0) loss_rows[b] = sm[0][0] + sm[0][1] + sm[0][2] + sm[0][3];
+}
+
+int softmax_xent(const void* logits, int logits_bf16, const int64_t* labels, const float* target_probs,
+                 float* loss_rows, void* dlogits, int B, int K, float grad_scale, float label_smoothing,
+                 int ignore_index, hipStream_t s) {
+  if (B <= 0) return 0;
+  if (logits_bf16)
+    hipLaunchKernelGGL(softmax_xent_kernel<true>, dim3(B), dim3(256), 0, s, logits, labels, target_probs, loss_rows,
+                       dlogits, K, grad_scale, label_smoothing, ignore_index);
+  else
+    hipLaunchKernelGGL(softmax_xent_kernel<false>, dim3(B), dim3(256), 0, s, logits, labels, target_probs, loss_rows,
+                       dlogits, K, grad_scale, label_smoothing, ignore_index);
+  return (int)hipGetLastError();
+}
+
+}  // namespace ddl

@@ -1,0 +1,140 @@
+// Data-movement kernels: casts, ReLU backward, adds, bias gradients, im2col for the
+// convolutions whose channel count does not fit the implicit-GEMM gather (C % 64 != 0,
+// e.g. the 3-channel stem and the MNIST CNN), and the fused ingest normaliser
+// (uint8 NHWC images -> bf16, channel padded) that runs right after the H2D copy.
+#include "ddl_common.h"
+#include "ddl_ops.h"
+
+namespace ddl {
+
+static unsigned mgrid(long n) {
+  long g = (n + 255) / 256;
+  if (g > 8192) g = 8192;
+  return (unsigned)(g > 0 ? g : 1);
+}
+
+#define GRID_LOOP(i, n) for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < (n); i += (long)gridDim.x * 256)
+
+__global__ void cast_f32_bf16_kernel(const float4* x, uint2* y, long n4) {
+  GRID_LOOP(i, n4) {
+    const float4 v = x[i];
+    y[i] = make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w));
+  }
+}
+__global__ void cast_f32_bf16_tail(const float* x, bf16_t* y, long start, long n) {
+  const long i = start + threadIdx.x;
+  if (i < n) y[i] = f2bf(x[i]);
+}
+
+int cast_f32_bf16(const float* x, void* y, long n, hipStream_t s) {
+  const long n4 = n / 4;
+  if (n4) hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(mgrid(n4)), dim3(256), 0, s, (const float4*)x, (uint2*)y, n4);
+  if (n % 4) hipLaunchKernelGGL(cast_f32_bf16_tail, dim3(1), dim3(4), 0, s, x, (bf16_t*)y, n4 * 4, n);
+  return (int)hipGetLastError();
+}
+
+__global__ void cast_bf16_f32_kernel(const bf16_t* x, float* y, long n) {
+  GRID_LOOP(i, n) y[i] = bf2f(x[i]);
+}
+
+int cast_bf16_f32(const void* x, float* y, long n, hipStream_t s) {
+  hipLaunchKernelGGL(cast_bf16_f32_kernel, dim3(mgrid(n)), dim3(256), 0, s, (const bf16_t*)x, y, n);
+  return (int)hipGetLastError();
+}
+
+__global__ void relu_bwd_kernel(const bf16_t* dy, const bf16_t* y, bf16_t* dx, long n) {
+  GRID_LOOP(i, n) dx[i] = bf2f(y[i]) > 0.f ? dy[i] : (bf16_t)0;
+}
+
+int relu_bwd(const void* dy, const void* y, void* dx, long n, hipStream_t s) {
+  hipLaunchKernelGGL(relu_bwd_kernel, dim3(mgrid(n)), dim3(256), 0, s, (const bf16_t*)dy, (const bf16_t*)y,
+                     (bf16_t*)dx, n);
+  return (int)hipGetLastError();
+}
+
+__global__ void add_bf16_kernel(const bf16_t* a, const bf16_t* b, bf16_t* y, long n) {
+  GRID_LOOP(i, n) y[i] = f2bf(bf2f(a[i]) + bf2f(b[i]));
+}
+
+int add_bf16(const void* a, const void* b, void* y, long n, hipStream_t s) {
+  hipLaunchKernelGGL(add_bf16_kernel, dim3(mgrid(n)), dim3(256), 0, s, (const bf16_t*)a, (const bf16_t*)b, (bf16_t*)y,
+                     n);
+  return (int)hipGetLastError();
+}
+
+// db[n] += sum_m dy[m][n]; grid (col blocks, row splits) with one atomic per column per block
+__global__ void bias_grad_kernel(const bf16_t* dy, float* db, long M, int N) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  float acc = 0.f;
+  for (long m = blockIdx.y; m < M; m += gridDim.y) acc += bf2f(dy[m * N + n]);
+  atomicAdd(db + n, acc);
+}
+
+int bias_grad(const void* dy, float* db, long M, int N, int accumulate, hipStream_t s) {
+  if (!accumulate) hipMemsetAsync(db, 0, sizeof(float) * N, s);
+  long ys = M / 64;
+  if (ys < 1) ys = 1;
+  if (ys > 256) ys = 256;
+  hipLaunchKernelGGL(bias_grad_kernel, dim3((N + 255) / 256, (unsigned)ys), dim3(256), 0, s, (const bf16_t*)dy, db, M,
+                     N);
+  return (int)hipGetLastError();
+}
+
+// im2col with a tap table: col[m][t*C + c] = x[n][i*sh + dh[t]][j*sw + dw[t]][c], zero padded to kpad columns
+struct Taps {
+  int dh[64];
+  int dw[64];
+};
+
+__global__ void im2col_kernel(const bf16_t* x, bf16_t* col, int N, int H, int W, int C, int Ho, int Wo, int sh, int sw,
+                              int T, Taps taps, int kpad) {
+  const long total = (long)N * Ho * Wo * kpad;
+  GRID_LOOP(idx, total) {
+    const int kk = (int)(idx % kpad);
+    const long m = idx / kpad;
+    bf16_t v = 0;
+    if (kk < T * C) {
+      const int t = kk / C, c = kk - t * C;
+      const int j = (int)(m % Wo);
+      const long q = m / Wo;
+      const int i = (int)(q % Ho);
+      const int n = (int)(q / Ho);
+      const int ih = i * sh + taps.dh[t], iw = j * sw + taps.dw[t];
+      if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) v = x[(((long)n * H + ih) * W + iw) * C + c];
+    }
+    col[idx] = v;
+  }
+}
+
+int im2col(const void* x, void* col, int n, int hi, int wi, int c, int ho, int wo, int sh, int sw, int ntaps,
+           const int* dh, const int* dw, int kpad, hipStream_t s) {
+  if (ntaps > 64) return (int)hipErrorInvalidValue;
+  Taps t;
+  for (int i = 0; i < ntaps; ++i) {
+    t.dh[i] = dh[i];
+    t.dw[i] = dw[i];
+  }
+  const long total = (long)n * ho * wo * kpad;
+  hipLaunchKernelGGL(im2col_kernel, dim3(mgrid(total)), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)col, n, hi, wi, c,
+                     ho, wo, sh, sw, ntaps, t, kpad);
+  return (int)hipGetLastError();
+}
+
+__global__ void normalize_u8_kernel(const uint8_t* x, bf16_t* y, long npix, int C, int CP, const float* mean,
+                                    const float* invstd) {
+  GRID_LOOP(idx, npix * CP) {
+    const int c = (int)(idx % CP);
+    const long p = idx / CP;
+    y[idx] = c < C ? f2bf(((float)x[p * C + c] - mean[c]) * invstd[c]) : (bf16_t)0;
+  }
+}
+
+int normalize_u8(const uint8_t* x, void* y, long npix, int c, int cpad, const float* mean, const float* invstd,
+                 hipStream_t s) {
+  hipLaunchKernelGGL(normalize_u8_kernel, dim3(mgrid(npix * cpad)), dim3(256), 0, s, x, (bf16_t*)y, npix, c, cpad,
+                     mean, invstd);
+  return (int)hipGetLastError();
+}
+
+}  // namespace ddl

@@ -1,0 +1,167 @@
+// Optimizer steps over the flat fp32 parameter arena: ONE launch updates every
+// parameter of the model (the arena makes "multi-tensor apply" a plain 1-D sweep),
+// and the same sweep writes the bf16 compute copy, so no separate cast pass exists.
+// float4 per lane; grad_scale folds the data-parallel 1/world averaging (or loss-scale)
+// into the update instead of a separate pass over the gradients.
+#include "ddl_common.h"
+#include "ddl_ops.h"
+
+namespace ddl {
+
+static unsigned ogrid(long n4) {
+  long g = (n4 + 255) / 256;
+  if (g > 4096) g = 4096;
+  return (unsigned)(g > 0 ? g : 1);
+}
+
+__device__ __forceinline__ void store_bf16x4(void* w16, long i4, const float4& w) {
+  uint2 o;
+  o.x = pack_bf16x2(w.x, w.y);
+  o.y = pack_bf16x2(w.z, w.w);
+  reinterpret_cast<uint2*>(w16)[i4] = o;
+}
+
+#define DDL_FLAT_FOR(i, n) for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < ((n) >> 2); i += (long)gridDim.x * 256)
+
+// ------------------------------ SGD (+momentum, nesterov, weight decay) ------------------------------
+__global__ __launch_bounds__(256) void sgd_kernel(float4* w, const float4* g, float4* mom, void* w16, long n, float lr,
+                                                   float mu, float damp, float wd, int nesterov, float gs) {
+  DDL_FLAT_FOR(i, n) {
+    float4 p = w[i], d = g[i];
+    float* pp = &p.x;
+    float* dd = &d.x;
+    float4 b = mom ? mom[i] : make_float4(0, 0, 0, 0);
+    float* bb = &b.x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float gg = dd[k] * gs + wd * pp[k];
+      if (mom) {
+        bb[k] = mu * bb[k] + (1.f - damp) * gg;
+        gg = nesterov ? gg + mu * bb[k] : bb[k];
+      }
+      pp[k] -= lr * gg;
+    }
+    w[i] = p;
+    if (mom) mom[i] = b;
+    if (w16) store_bf16x4(w16, i, p);
+  }
+}
+
+int sgd_step(float* w, const float* g, float* mom, void* w16, long n, float lr, float momentum, float dampening,
+             float wd, int nesterov, float gscale, hipStream_t s) {
+  if (n % 4) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(sgd_kernel, dim3(ogrid(n / 4)), dim3(256), 0, s, (float4*)w, (const float4*)g,
+                     momentum != 0.f ? (float4*)mom : nullptr, w16, n, lr, momentum, dampening, wd, nesterov, gscale);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------ Adam / AdamW ------------------------------
+// mode bit0: decoupled weight decay (AdamW); bit1: Keras epsilon placement
+//   PyTorch: w -= lr * (m/bc1) / (sqrt(v/bc2) + eps)
+//   Keras 2: w -= lr * sqrt(bc2)/bc1 * m / (sqrt(v) + eps)
+__global__ __launch_bounds__(256) void adam_kernel(float4* w, const float4* g, float4* m, float4* v, void* w16, long n,
+                                                    float lr, float b1, float b2, float eps, float wd, int mode,
+                                                    float bc1, float bc2, float gs) {
+  const float sbc2 = sqrtf(bc2);
+  DDL_FLAT_FOR(i, n) {
+    float4 p = w[i], d = g[i], mm = m[i], vv = v[i];
+    float *pp = &p.x, *dd = &d.x, *m_ = &mm.x, *v_ = &vv.x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float gg = dd[k] * gs;
+      if (mode & 1) pp[k] *= (1.f - lr * wd);
+      else gg += wd * pp[k];
+      m_[k] = b1 * m_[k] + (1.f - b1) * gg;
+      v_[k] = b2 * v_[k] + (1.f - b2) * gg * gg;
+      if (mode & 2) pp[k] -= lr * (sbc2 / bc1) * m_[k] / (sqrtf(v_[k]) + eps);
+      else pp[k] -= lr * (m_[k] / bc1) / (sqrtf(v_[k]) / sbc2 + eps);
+    }
+    w[i] = p;
+    m[i] = mm;
+    v[i] = vv;
+    if (w16) store_bf16x4(w16, i, p);
+  }
+}
+
+int adam_step(float* w, const float* g, float* m, float* v, void* w16, long n, float lr, float b1, float b2, float eps,
+              float wd, int adamw, float bc1, float bc2, float gscale, hipStream_t s) {
+  if (n % 4) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(adam_kernel, dim3(ogrid(n / 4)), dim3(256), 0, s, (float4*)w, (const float4*)g, (float4*)m,
+                     (float4*)v, w16, n, lr, b1, b2, eps, wd, adamw, bc1, bc2, gscale);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------ Adagrad (Keras 2 semantics) ------------------------------
+__global__ __launch_bounds__(256) void adagrad_kernel(float4* w, const float4* g, float4* acc, void* w16, long n,
+                                                       float lr, float eps, float wd, float gs) {
+  DDL_FLAT_FOR(i, n) {
+    float4 p = w[i], d = g[i], a = acc[i];
+    float *pp = &p.x, *dd = &d.x, *aa = &a.x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float gg = dd[k] * gs + wd * pp[k];
+      aa[k] += gg * gg;
+      pp[k] -= lr * gg / (sqrtf(aa[k]) + eps);
+    }
+    w[i] = p;
+    acc[i] = a;
+    if (w16) store_bf16x4(w16, i, p);
+  }
+}
+
+int adagrad_step(float* w, const float* g, float* acc, void* w16, long n, float lr, float eps, float wd, float gscale,
+                 hipStream_t s) {
+  if (n % 4) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(adagrad_kernel, dim3(ogrid(n / 4)), dim3(256), 0, s, (float4*)w, (const float4*)g, (float4*)acc,
+                     w16, n, lr, eps, wd, gscale);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------ RMSprop (Keras 2 semantics) ------------------------------
+__global__ __launch_bounds__(256) void rmsprop_kernel(float4* w, const float4* g, float4* acc, void* w16, long n,
+                                                       float lr, float rho, float eps, float wd, float gs) {
+  DDL_FLAT_FOR(i, n) {
+    float4 p = w[i], d = g[i], a = acc[i];
+    float *pp = &p.x, *dd = &d.x, *aa = &a.x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float gg = dd[k] * gs + wd * pp[k];
+      aa[k] = rho * aa[k] + (1.f - rho) * gg * gg;
+      pp[k] -= lr * gg / (sqrtf(aa[k]) + eps);
+    }
+    w[i] = p;
+    acc[i] = a;
+    if (w16) store_bf16x4(w16, i, p);
+  }
+}
+
+int rmsprop_step(float* w, const float* g, float* acc, void* w16, long n, float lr, float rho, float eps, float wd,
+                 float gscale, hipStream_t s) {
+  if (n % 4) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(rmsprop_kernel, dim3(ogrid(n / 4)), dim3(256), 0, s, (float4*)w, (const float4*)g, (float4*)acc,
+                     w16, n, lr, rho, eps, wd, gscale);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------ sum of squares ------------------------------
+__global__ __launch_bounds__(256) void sumsq_kernel(const float4* x, long n4, float* out) {
+  float acc = 0.f;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    const float4 v = x[i];
+    acc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  acc = warp_sum(acc);
+  __shared__ float sm[4];
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out, sm[0] + sm[1] + sm[2] + sm[3]);
+}
+
+int sumsq_f32(const float* x, long n, float* out, hipStream_t s) {
+  if (n % 4) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(sumsq_kernel, dim3(ogrid(n / 4) > 1024 ? 1024 : ogrid(n / 4)), dim3(256), 0, s, (const float4*)x,
+                     n / 4, out);
+  return (int)hipGetLastError();
+}
+
+}  // namespace ddl

@@ -1,0 +1,176 @@
+// NHWC pooling: max-pool with a byte-sized argmax (window index) so the backward is a
+// gather (each input pixel collects from the <= ceil(k/s)^2 windows that cover it; no
+// atomics), and global average pooling.  8 channels (16 B) per lane.
+#include "ddl_common.h"
+#include "ddl_ops.h"
+
+namespace ddl {
+
+__device__ __forceinline__ void unpack8p(const uint4& u, float* f) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ uint4 pack8p(const float* f) {
+  return make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]), pack_bf16x2(f[6], f[7]));
+}
+
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint4* __restrict__ x, uint4* __restrict__ y,
+                                                           uint2* __restrict__ am, int N, int H, int W, int CV, int Ho,
+                                                           int Wo, int kh, int kw, int sh, int sw, int ph, int pw) {
+  const long total = (long)N * Ho * Wo * CV;
+  for (long v = (long)blockIdx.x * 256 + threadIdx.x; v < total; v += (long)gridDim.x * 256) {
+    const int cv = (int)(v % CV);
+    long p = v / CV;
+    const int ow = (int)(p % Wo);
+    p /= Wo;
+    const int oh = (int)(p % Ho);
+    const int n = (int)(p / Ho);
+    float best[8];
+    uint8_t arg[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      best[i] = -INFINITY;
+      arg[i] = 0;
+    }
+    for (int r = 0; r < kh; ++r) {
+      const int ih = oh * sh - ph + r;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int s = 0; s < kw; ++s) {
+        const int iw = ow * sw - pw + s;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        float f[8];
+        unpack8p(x[(((long)n * H + ih) * W + iw) * CV + cv], f);
+        const uint8_t idx = (uint8_t)(r * kw + s);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (f[i] > best[i]) {
+            best[i] = f[i];
+            arg[i] = idx;
+          }
+      }
+    }
+    y[v] = pack8p(best);
+    uint2 a;
+    a.x = (uint32_t)arg[0] | ((uint32_t)arg[1] << 8) | ((uint32_t)arg[2] << 16) | ((uint32_t)arg[3] << 24);
+    a.y = (uint32_t)arg[4] | ((uint32_t)arg[5] << 8) | ((uint32_t)arg[6] << 16) | ((uint32_t)arg[7] << 24);
+    am[v] = a;
+  }
+}
+
+static unsigned pgrid(long n) {
+  long g = (n + 255) / 256;
+  if (g > 8192) g = 8192;
+  return (unsigned)(g > 0 ? g : 1);
+}
+
+int maxpool_fwd(const void* x, void* y, uint8_t* argmax, int N, int H, int W, int C, int Ho, int Wo, int kh, int kw,
+                int sh, int sw, int ph, int pw, hipStream_t s) {
+  const long total = (long)N * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(pgrid(total)), dim3(256), 0, s, (const uint4*)x, (uint4*)y,
+                     (uint2*)argmax, N, H, W, C / 8, Ho, Wo, kh, kw, sh, sw, ph, pw);
+  return (int)hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const uint4* __restrict__ dy, const uint2* __restrict__ am,
+                                                           uint4* __restrict__ dx, int N, int H, int W, int CV, int Ho,
+                                                           int Wo, int kh, int kw, int sh, int sw, int ph, int pw) {
+  const long total = (long)N * H * W * CV;
+  for (long v = (long)blockIdx.x * 256 + threadIdx.x; v < total; v += (long)gridDim.x * 256) {
+    const int cv = (int)(v % CV);
+    long p = v / CV;
+    const int w = (int)(p % W);
+    p /= W;
+    const int h = (int)(p % H);
+    const int n = (int)(p / H);
+    float acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+    // windows covering h: oh*sh - ph <= h <= oh*sh - ph + kh - 1
+    int oh0 = h + ph - kh + 1;
+    oh0 = oh0 <= 0 ? 0 : (oh0 + sh - 1) / sh;
+    const int oh1 = min(Ho - 1, (h + ph) / sh);
+    int ow0 = w + pw - kw + 1;
+    ow0 = ow0 <= 0 ? 0 : (ow0 + sw - 1) / sw;
+    const int ow1 = min(Wo - 1, (w + pw) / sw);
+    for (int oh = oh0; oh <= oh1; ++oh) {
+      for (int ow = ow0; ow <= ow1; ++ow) {
+        const int idx = (h + ph - oh * sh) * kw + (w + pw - ow * sw);
+        const long o = (((long)n * Ho + oh) * Wo + ow) * CV + cv;
+        const uint2 a = am[o];
+        float g[8];
+        unpack8p(dy[o], g);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const uint32_t word = i < 4 ? a.x : a.y;
+          const int ai = (word >> ((i & 3) * 8)) & 0xff;
+          if (ai == idx) acc[i] += g[i];
+        }
+      }
+    }
+    dx[v] = pack8p(acc);
+  }
+}
+
+int maxpool_bwd(const void* dy, const uint8_t* argmax, void* dx, int N, int H, int W, int C, int Ho, int Wo, int kh,
+                int kw, int sh, int sw, int ph, int pw, hipStream_t s) {
+  const long total = (long)N * H * W * (C / 8);
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(pgrid(total)), dim3(256), 0, s, (const uint4*)dy, (const uint2*)argmax,
+                     (uint4*)dx, N, H, W, C / 8, Ho, Wo, kh, kw, sh, sw, ph, pw);
+  return (int)hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void avgpool_fwd_kernel(const uint4* __restrict__ x, uint4* __restrict__ y, int N,
+                                                           int HW, int CV) {
+  const long total = (long)N * CV;
+  for (long v = (long)blockIdx.x * 256 + threadIdx.x; v < total; v += (long)gridDim.x * 256) {
+    const int cv = (int)(v % CV);
+    const long n = v / CV;
+    float acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+    for (int p = 0; p < HW; ++p) {
+      float f[8];
+      unpack8p(x[(n * HW + p) * CV + cv], f);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] += f[i];
+    }
+    const float inv = 1.f / (float)HW;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] *= inv;
+    y[v] = pack8p(acc);
+  }
+}
+
+int avgpool_global_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t s) {
+  const long total = (long)N * (C / 8);
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(pgrid(total)), dim3(256), 0, s, (const uint4*)x, (uint4*)y, N, HW, C / 8);
+  return (int)hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void avgpool_bwd_kernel(const uint4* __restrict__ dy, uint4* __restrict__ dx, int N,
+                                                           int HW, int CV) {
+  const long total = (long)N * HW * CV;
+  const float inv = 1.f / (float)HW;
+  for (long v = (long)blockIdx.x * 256 + threadIdx.x; v < total; v += (long)gridDim.x * 256) {
+    const int cv = (int)(v % CV);
+    const long n = v / ((long)CV * HW);
+    float f[8];
+    unpack8p(dy[n * CV + cv], f);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] *= inv;
+    dx[v] = pack8p(f);
+  }
+}
+
+int avgpool_global_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t s) {
+  const long total = (long)N * HW * (C / 8);
+  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(pgrid(total)), dim3(256), 0, s, (const uint4*)dy, (uint4*)dx, N, HW,
+                     C / 8);
+  return (int)hipGetLastError();
+}
+
+}  // namespace ddl

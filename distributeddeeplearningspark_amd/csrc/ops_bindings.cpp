@@ -1,0 +1,293 @@
+// pybind11 registrations of the non-GEMM kernels.  Host-side validation of every
+// pointer/shape/dtype happens here before the launch.
+#include <torch/extension.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <ATen/DeviceGuard.h>
+
+#include "ddl_ops.h"
+
+namespace py = pybind11;
+using namespace ddl;
+
+namespace {
+
+inline hipStream_t cur_stream() { return at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+
+#define CK(cond, ...) TORCH_CHECK(cond, __VA_ARGS__)
+#define GPU(x) CK((x).is_cuda(), #x " must be a GPU tensor")
+#define BF16(x) CK((x).scalar_type() == at::kBFloat16 && (x).is_contiguous(), #x " must be contiguous bf16")
+#define F32(x) CK((x).scalar_type() == at::kFloat && (x).is_contiguous(), #x " must be contiguous fp32")
+#define HIP_OK(expr)                                                                  \
+  do {                                                                                \
+    int _e = (expr);                                                                  \
+    CK(_e == 0, "HIP launch failed: ", hipGetErrorString((hipError_t)_e)); \
+  } while (0)
+
+template <class T>
+T* optr(const c10::optional<at::Tensor>& t) {
+  return t ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
+}
+
+// ---------------------------------------------------------------- batch norm
+void bn_stats_(const at::Tensor& x, const at::Tensor& ws, int64_t C) {
+  GPU(x); BF16(x); F32(ws);
+  CK(C % 8 == 0 && x.numel() % C == 0, "bn_stats: C % 8 and numel % C");
+  CK(ws.numel() >= (int64_t)kBnShards * 2 * C, "bn_stats: workspace too small");
+  at::DeviceGuard g(x.device());
+  HIP_OK(bn_stats(x.data_ptr(), ws.data_ptr<float>(), x.numel() / C, (int)C, cur_stream()));
+}
+
+void bn_finalize_(const at::Tensor& ws, int64_t M, int64_t C, c10::optional<at::Tensor> gamma,
+                  c10::optional<at::Tensor> beta, double eps, double momentum, c10::optional<at::Tensor> rmean,
+                  c10::optional<at::Tensor> rvar, const at::Tensor& smean, const at::Tensor& sinv,
+                  const at::Tensor& scale, const at::Tensor& shift) {
+  GPU(ws); F32(ws); F32(smean); F32(sinv); F32(scale); F32(shift);
+  CK(smean.numel() >= C && sinv.numel() >= C && scale.numel() >= C && shift.numel() >= C, "bn_finalize: sizes");
+  at::DeviceGuard g(ws.device());
+  HIP_OK(bn_finalize(ws.data_ptr<float>(), M, (int)C, optr<const float>(gamma), optr<const float>(beta), (float)eps,
+                     (float)momentum, optr<float>(rmean), optr<float>(rvar), smean.data_ptr<float>(),
+                     sinv.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(), cur_stream()));
+}
+
+void bn_apply_(const at::Tensor& x, const at::Tensor& scale, const at::Tensor& shift, c10::optional<at::Tensor> resid,
+               const at::Tensor& y, int64_t C, bool relu) {
+  GPU(x); BF16(x); BF16(y); F32(scale); F32(shift);
+  CK(C % 8 == 0 && x.numel() % C == 0 && y.numel() == x.numel(), "bn_apply: shapes");
+  if (resid) { BF16(*resid); CK(resid->numel() == x.numel(), "bn_apply: resid shape"); }
+  at::DeviceGuard g(x.device());
+  HIP_OK(bn_apply(x.data_ptr(), scale.data_ptr<float>(), shift.data_ptr<float>(), optr<const void>(resid), y.data_ptr(),
+                  x.numel() / C, (int)C, relu ? 1 : 0, cur_stream()));
+}
+
+void bn_bwd_reduce_(const at::Tensor& dy, const at::Tensor& x, c10::optional<at::Tensor> y, const at::Tensor& mean,
+                    const at::Tensor& ws, int64_t C) {
+  GPU(dy); BF16(dy); BF16(x); F32(mean); F32(ws);
+  CK(dy.numel() == x.numel() && x.numel() % C == 0 && C % 8 == 0, "bn_bwd_reduce: shapes");
+  if (y) { BF16(*y); CK(y->numel() == x.numel(), "bn_bwd_reduce: y shape"); }
+  CK(ws.numel() >= (int64_t)kBnShards * 2 * C, "bn_bwd_reduce: workspace too small");
+  at::DeviceGuard g(x.device());
+  HIP_OK(bn_bwd_reduce(dy.data_ptr(), x.data_ptr(), optr<const void>(y), mean.data_ptr<float>(), nullptr,
+                       ws.data_ptr<float>(), x.numel() / C, (int)C, y ? 1 : 0, cur_stream()));
+}
+
+void bn_bwd_finalize_(const at::Tensor& ws, int64_t M, int64_t C, c10::optional<at::Tensor> gamma,
+                      const at::Tensor& invstd, c10::optional<at::Tensor> dgamma, c10::optional<at::Tensor> dbeta,
+                      const at::Tensor& coef) {
+  GPU(ws); F32(ws); F32(invstd); F32(coef);
+  CK(coef.numel() >= 3 * C, "bn_bwd_finalize: coef size");
+  at::DeviceGuard g(ws.device());
+  HIP_OK(bn_bwd_finalize(ws.data_ptr<float>(), M, (int)C, optr<const float>(gamma), invstd.data_ptr<float>(),
+                         optr<float>(dgamma), optr<float>(dbeta), coef.data_ptr<float>(), cur_stream()));
+}
+
+void bn_bwd_dx_(const at::Tensor& dy, const at::Tensor& x, c10::optional<at::Tensor> y, const at::Tensor& mean,
+                const at::Tensor& invstd, const at::Tensor& coef, const at::Tensor& dx, c10::optional<at::Tensor> dres,
+                int64_t C) {
+  GPU(dy); BF16(dy); BF16(x); BF16(dx); F32(mean); F32(invstd); F32(coef);
+  CK(dy.numel() == x.numel() && dx.numel() == x.numel() && x.numel() % C == 0, "bn_bwd_dx: shapes");
+  if (y) BF16(*y);
+  if (dres) { BF16(*dres); CK(dres->numel() == x.numel(), "bn_bwd_dx: dres shape"); }
+  at::DeviceGuard g(x.device());
+  HIP_OK(bn_bwd_dx(dy.data_ptr(), x.data_ptr(), optr<const void>(y), mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                   coef.data_ptr<float>(), dx.data_ptr(), optr<void>(dres), x.numel() / C, (int)C, y ? 1 : 0,
+                   cur_stream()));
+}
+
+// ---------------------------------------------------------------- pooling
+void maxpool_fwd_(const at::Tensor& x, const at::Tensor& y, const at::Tensor& am, int64_t kh, int64_t kw, int64_t sh,
+                  int64_t sw, int64_t ph, int64_t pw) {
+  GPU(x); BF16(x); BF16(y);
+  CK(am.scalar_type() == at::kByte && am.is_contiguous(), "argmax must be uint8");
+  CK(x.dim() == 4 && y.dim() == 4, "maxpool: NHWC tensors");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), Ho = y.size(1), Wo = y.size(2);
+  CK(C % 8 == 0 && y.size(0) == N && y.size(3) == C && am.numel() == y.numel(), "maxpool: shapes");
+  CK(kh * kw <= 256, "maxpool: window too large for byte argmax");
+  at::DeviceGuard g(x.device());
+  HIP_OK(maxpool_fwd(x.data_ptr(), y.data_ptr(), am.data_ptr<uint8_t>(), N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw,
+                     cur_stream()));
+}
+
+void maxpool_bwd_(const at::Tensor& dy, const at::Tensor& am, const at::Tensor& dx, int64_t kh, int64_t kw, int64_t sh,
+                  int64_t sw, int64_t ph, int64_t pw) {
+  GPU(dy); BF16(dy); BF16(dx);
+  const int N = dx.size(0), H = dx.size(1), W = dx.size(2), C = dx.size(3), Ho = dy.size(1), Wo = dy.size(2);
+  CK(C % 8 == 0 && dy.size(3) == C && am.numel() == dy.numel(), "maxpool_bwd: shapes");
+  at::DeviceGuard g(dy.device());
+  HIP_OK(maxpool_bwd(dy.data_ptr(), am.data_ptr<uint8_t>(), dx.data_ptr(), N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw,
+                     cur_stream()));
+}
+
+void avgpool_fwd_(const at::Tensor& x, const at::Tensor& y) {
+  GPU(x); BF16(x); BF16(y);
+  CK(x.dim() == 4, "avgpool: NHWC");
+  const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
+  CK(C % 8 == 0 && y.numel() == (int64_t)N * C, "avgpool: shapes");
+  at::DeviceGuard g(x.device());
+  HIP_OK(avgpool_global_fwd(x.data_ptr(), y.data_ptr(), N, HW, C, cur_stream()));
+}
+
+void avgpool_bwd_(const at::Tensor& dy, const at::Tensor& dx) {
+  GPU(dy); BF16(dy); BF16(dx);
+  const int N = dx.size(0), HW = dx.size(1) * dx.size(2), C = dx.size(3);
+  CK(C % 8 == 0 && dy.numel() == (int64_t)N * C, "avgpool_bwd: shapes");
+  at::DeviceGuard g(dy.device());
+  HIP_OK(avgpool_global_bwd(dy.data_ptr(), dx.data_ptr(), N, HW, C, cur_stream()));
+}
+
+// ---------------------------------------------------------------- loss
+void softmax_xent_(const at::Tensor& logits, c10::optional<at::Tensor> labels, c10::optional<at::Tensor> probs,
+                   const at::Tensor& loss_rows, c10::optional<at::Tensor> dlogits, double grad_scale, double smoothing,
+                   int64_t ignore_index) {
+  GPU(logits);
+  CK(logits.dim() == 2 && logits.is_contiguous(), "softmax_xent: logits [B,K] contiguous");
+  const bool bf = logits.scalar_type() == at::kBFloat16;
+  CK(bf || logits.scalar_type() == at::kFloat, "softmax_xent: logits bf16/fp32");
+  const int B = logits.size(0), K = logits.size(1);
+  F32(loss_rows);
+  CK(loss_rows.numel() == B, "loss_rows size");
+  CK((labels.has_value()) != (probs.has_value()), "exactly one of labels/probs");
+  if (labels) CK(labels->scalar_type() == at::kLong && labels->numel() == B, "labels int64 [B]");
+  if (probs) { F32(*probs); CK(probs->numel() == (int64_t)B * K, "probs [B,K]"); }
+  if (dlogits) CK(dlogits->scalar_type() == logits.scalar_type() && dlogits->numel() == logits.numel(), "dlogits");
+  at::DeviceGuard g(logits.device());
+  HIP_OK(softmax_xent(logits.data_ptr(), bf ? 1 : 0, optr<const int64_t>(labels), optr<const float>(probs),
+                      loss_rows.data_ptr<float>(), optr<void>(dlogits), B, K, (float)grad_scale, (float)smoothing,
+                      (int)ignore_index, cur_stream()));
+}
+
+// ---------------------------------------------------------------- elementwise
+void cast_f32_bf16_(const at::Tensor& x, const at::Tensor& y) {
+  GPU(x); F32(x); BF16(y);
+  CK(x.numel() == y.numel(), "cast: sizes");
+  at::DeviceGuard g(x.device());
+  HIP_OK(cast_f32_bf16(x.data_ptr<float>(), y.data_ptr(), x.numel(), cur_stream()));
+}
+void cast_bf16_f32_(const at::Tensor& x, const at::Tensor& y) {
+  GPU(x); BF16(x); F32(y);
+  CK(x.numel() == y.numel(), "cast: sizes");
+  at::DeviceGuard g(x.device());
+  HIP_OK(cast_bf16_f32(x.data_ptr(), y.data_ptr<float>(), x.numel(), cur_stream()));
+}
+void relu_bwd_(const at::Tensor& dy, const at::Tensor& y, const at::Tensor& dx) {
+  GPU(dy); BF16(dy); BF16(y); BF16(dx);
+  CK(dy.numel() == y.numel() && dx.numel() == y.numel(), "relu_bwd: sizes");
+  at::DeviceGuard g(dy.device());
+  HIP_OK(relu_bwd(dy.data_ptr(), y.data_ptr(), dx.data_ptr(), dy.numel(), cur_stream()));
+}
+void add_bf16_(const at::Tensor& a, const at::Tensor& b, const at::Tensor& y) {
+  GPU(a); BF16(a); BF16(b); BF16(y);
+  CK(a.numel() == b.numel() && y.numel() == a.numel(), "add: sizes");
+  at::DeviceGuard g(a.device());
+  HIP_OK(add_bf16(a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(), cur_stream()));
+}
+void bias_grad_(const at::Tensor& dy, const at::Tensor& db, int64_t N, bool accumulate) {
+  GPU(dy); BF16(dy); F32(db);
+  CK(dy.numel() % N == 0 && db.numel() >= N, "bias_grad: shapes");
+  at::DeviceGuard g(dy.device());
+  HIP_OK(bias_grad(dy.data_ptr(), db.data_ptr<float>(), dy.numel() / N, (int)N, accumulate ? 1 : 0, cur_stream()));
+}
+void im2col_(const at::Tensor& x, const at::Tensor& col, int64_t ho, int64_t wo, int64_t sh, int64_t sw,
+             std::vector<int> dh, std::vector<int> dw, int64_t kpad) {
+  GPU(x); BF16(x); BF16(col);
+  CK(x.dim() == 4, "im2col: NHWC input");
+  CK(dh.size() == dw.size() && dh.size() <= 64, "im2col: taps");
+  const int N = x.size(0);
+  CK(col.numel() == (int64_t)N * ho * wo * kpad, "im2col: col size");
+  CK(kpad >= (int64_t)dh.size() * x.size(3), "im2col: kpad");
+  at::DeviceGuard g(x.device());
+  HIP_OK(im2col(x.data_ptr(), col.data_ptr(), N, x.size(1), x.size(2), x.size(3), ho, wo, sh, sw, (int)dh.size(),
+                dh.data(), dw.data(), (int)kpad, cur_stream()));
+}
+void normalize_u8_(const at::Tensor& x, const at::Tensor& y, const at::Tensor& mean, const at::Tensor& invstd,
+                   int64_t C, int64_t CP) {
+  GPU(x);
+  CK(x.scalar_type() == at::kByte && x.is_contiguous(), "normalize_u8: uint8 input");
+  BF16(y); F32(mean); F32(invstd);
+  CK(x.numel() % C == 0 && y.numel() == x.numel() / C * CP && CP >= C, "normalize_u8: shapes");
+  at::DeviceGuard g(x.device());
+  HIP_OK(normalize_u8(x.data_ptr<uint8_t>(), y.data_ptr(), x.numel() / C, (int)C, (int)CP, mean.data_ptr<float>(),
+                      invstd.data_ptr<float>(), cur_stream()));
+}
+
+// ---------------------------------------------------------------- optimizers
+#define OPT_CHECK(w, g)                                                        \
+  GPU(w); F32(w); F32(g);                                                      \
+  CK((w).numel() == (g).numel() && (w).numel() % 4 == 0, "optimizer: flat sizes (multiple of 4)")
+
+void sgd_step_(const at::Tensor& w, const at::Tensor& g, c10::optional<at::Tensor> mom, c10::optional<at::Tensor> w16,
+               double lr, double momentum, double dampening, double wd, bool nesterov, double gscale) {
+  OPT_CHECK(w, g);
+  if (mom) { F32(*mom); CK(mom->numel() == w.numel(), "momentum size"); }
+  if (w16) { BF16(*w16); CK(w16->numel() == w.numel(), "w16 size"); }
+  CK(momentum == 0.0 || mom.has_value(), "sgd: momentum buffer required");
+  at::DeviceGuard gd(w.device());
+  HIP_OK(sgd_step(w.data_ptr<float>(), g.data_ptr<float>(), optr<float>(mom), optr<void>(w16), w.numel(), (float)lr,
+                  (float)momentum, (float)dampening, (float)wd, nesterov ? 1 : 0, (float)gscale, cur_stream()));
+}
+void adam_step_(const at::Tensor& w, const at::Tensor& g, const at::Tensor& m, const at::Tensor& v,
+                c10::optional<at::Tensor> w16, double lr, double b1, double b2, double eps, double wd, int64_t mode,
+                double bc1, double bc2, double gscale) {
+  OPT_CHECK(w, g);
+  F32(m); F32(v);
+  CK(m.numel() == w.numel() && v.numel() == w.numel(), "adam: state sizes");
+  if (w16) { BF16(*w16); CK(w16->numel() == w.numel(), "w16 size"); }
+  at::DeviceGuard gd(w.device());
+  HIP_OK(adam_step(w.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), optr<void>(w16),
+                   w.numel(), (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (int)mode, (float)bc1,
+                   (float)bc2, (float)gscale, cur_stream()));
+}
+void adagrad_step_(const at::Tensor& w, const at::Tensor& g, const at::Tensor& acc, c10::optional<at::Tensor> w16,
+                   double lr, double eps, double wd, double gscale) {
+  OPT_CHECK(w, g);
+  F32(acc);
+  CK(acc.numel() == w.numel(), "adagrad: state size");
+  if (w16) BF16(*w16);
+  at::DeviceGuard gd(w.device());
+  HIP_OK(adagrad_step(w.data_ptr<float>(), g.data_ptr<float>(), acc.data_ptr<float>(), optr<void>(w16), w.numel(),
+                      (float)lr, (float)eps, (float)wd, (float)gscale, cur_stream()));
+}
+void rmsprop_step_(const at::Tensor& w, const at::Tensor& g, const at::Tensor& acc, c10::optional<at::Tensor> w16,
+                   double lr, double rho, double eps, double wd, double gscale) {
+  OPT_CHECK(w, g);
+  F32(acc);
+  CK(acc.numel() == w.numel(), "rmsprop: state size");
+  if (w16) BF16(*w16);
+  at::DeviceGuard gd(w.device());
+  HIP_OK(rmsprop_step(w.data_ptr<float>(), g.data_ptr<float>(), acc.data_ptr<float>(), optr<void>(w16), w.numel(),
+                      (float)lr, (float)rho, (float)eps, (float)wd, (float)gscale, cur_stream()));
+}
+void sumsq_(const at::Tensor& x, const at::Tensor& out) {
+  GPU(x); F32(x); F32(out);
+  CK(x.numel() % 4 == 0, "sumsq: multiple of 4");
+  at::DeviceGuard gd(x.device());
+  HIP_OK(sumsq_f32(x.data_ptr<float>(), x.numel(), out.data_ptr<float>(), cur_stream()));
+}
+
+}  // namespace
+
+void register_ops(py::module& m) {
+  m.attr("BN_SHARDS") = (int)kBnShards;
+  m.def("bn_stats", &bn_stats_);
+  m.def("bn_finalize", &bn_finalize_);
+  m.def("bn_apply", &bn_apply_);
+  m.def("bn_bwd_reduce", &bn_bwd_reduce_);
+  m.def("bn_bwd_finalize", &bn_bwd_finalize_);
+  m.def("bn_bwd_dx", &bn_bwd_dx_);
+  m.def("maxpool_fwd", &maxpool_fwd_);
+  m.def("maxpool_bwd", &maxpool_bwd_);
+  m.def("avgpool_fwd", &avgpool_fwd_);
+  m.def("avgpool_bwd", &avgpool_bwd_);
+  m.def("softmax_xent", &softmax_xent_);
+  m.def("cast_f32_bf16", &cast_f32_bf16_);
+  m.def("cast_bf16_f32", &cast_bf16_f32_);
+  m.def("relu_bwd", &relu_bwd_);
+  m.def("add_bf16", &add_bf16_);
+  m.def("bias_grad", &bias_grad_);
+  m.def("im2col", &im2col_);
+  m.def("normalize_u8", &normalize_u8_);
+  m.def("sgd_step", &sgd_step_);
+  m.def("adam_step", &adam_step_);
+  m.def("adagrad_step", &adagrad_step_);
+  m.def("rmsprop_step", &rmsprop_step_);
+  m.def("sumsq", &sumsq_);
+}

@@ -1,0 +1,486 @@
+"""Keras-compatible model API (``Sequential``, layers, ``compile/fit/train_on_batch/
+predict/get_weights/set_weights/summary/to_json``) on top of the MI355X op layer.
+
+The reference builds Keras 2 ``Sequential`` models (``ddl_mnist_aztk.py:180-199``,
+``ddl_nyiso_aztk.py:201-204,249-252``) and hands them to dist-keras trainers that
+serialise them as ``{'model': to_json(), 'weights': get_weights()}``.  This module
+keeps that surface: Keras weight layouts/ordering in ``get_weights`` and a
+Keras-shaped JSON config, while the storage underneath is the flat parameter arena
+(``params.py``) and every op dispatches to the HIP kernels on the GPU.
+
+Activations are NHWC; on the GPU they are bf16 with fp32 master weights.
+"""
+from __future__ import annotations
+
+import json
+import math
+import time
+from typing import Any, Sequence
+
+import numpy as np
+import torch
+
+from . import optimizers as optim_mod
+from .params import Param, ParamArena, to_numpy
+
+_LAYER_TYPES: dict[str, type] = {}
+_NAME_COUNTS: dict[str, int] = {}
+
+
+def _auto_name(prefix: str) -> str:
+    n = _NAME_COUNTS.get(prefix, 0) + 1
+    _NAME_COUNTS[prefix] = n
+    return f"{prefix}_{n}"
+
+
+def _snake(name: str) -> str:
+    out = []
+    for i, ch in enumerate(name):
+        if ch.isupper() and i and not name[i - 1].isupper():
+            out.append("_")
+        out.append(ch.lower())
+    return "".join(out)
+
+
+class Layer:
+    """Base layer.  Subclasses define ``build`` (create params with ``add_weight``),
+    ``call`` and ``compute_output_shape``; shapes exclude the batch dimension."""
+
+    def __init_subclass__(cls, **kw):
+        super().__init_subclass__(**kw)
+        _LAYER_TYPES[cls.__name__] = cls
+
+    def __init__(self, name: str | None = None, input_shape=None, input_dim=None, trainable: bool = True,
+                 batch_input_shape=None, **kwargs):
+        if kwargs:
+            unknown = set(kwargs) - {"dtype", "weights"}
+            if unknown:
+                raise TypeError(f"{type(self).__name__}: unexpected arguments {sorted(unknown)}")
+        self.name = name or _auto_name(_snake(type(self).__name__))
+        if batch_input_shape is not None:
+            input_shape = tuple(batch_input_shape[1:])
+        if input_shape is None and input_dim is not None:
+            input_shape = (int(input_dim),)
+        self._input_shape_arg = tuple(input_shape) if input_shape is not None else None
+        self.trainable = trainable
+        self.built = False
+        self._params: list[Param] = []
+        self._states: dict[str, torch.Tensor] = {}
+        self.input_shape = None
+        self.output_shape = None
+        self.grad_hook = None  # set by the data-parallel engine (fires when this layer's grads are final)
+        self._initial_weights = kwargs.get("weights")
+
+    # ------------------------------------------------------------------ params
+    def add_weight(self, name: str, shape, init, trainable: bool = True) -> Param:
+        p = Param(f"{self.name}/{name}", shape, init, trainable)
+        self._params.append(p)
+        return p
+
+    def add_state(self, name: str, value: torch.Tensor) -> torch.Tensor:
+        self._states[name] = value.to(torch.float32)
+        return self._states[name]
+
+    def sublayers(self) -> list["Layer"]:
+        return []
+
+    def all_params(self) -> list[Param]:
+        out = list(self._params)
+        for l in self.sublayers():
+            out.extend(l.all_params())
+        return out
+
+    def all_layers(self) -> list["Layer"]:
+        out = [self]
+        for l in self.sublayers():
+            out.extend(l.all_layers())
+        return out
+
+    def count_params(self) -> int:
+        return sum(p.numel for p in self.all_params())
+
+    # ------------------------------------------------------------------ lifecycle
+    def build(self, input_shape):
+        self.built = True
+
+    def ensure_built(self, input_shape):
+        if not self.built:
+            self.input_shape = tuple(input_shape)
+            self.build(tuple(input_shape))
+            self.built = True
+            self.output_shape = tuple(self.compute_output_shape(tuple(input_shape)))
+        return self.output_shape
+
+    def compute_output_shape(self, input_shape):
+        return input_shape
+
+    def call(self, x, training: bool = False):
+        raise NotImplementedError
+
+    def __call__(self, x, training: bool = False):
+        return self.call(x, training)
+
+    def states_to(self, device):
+        for k, v in list(self._states.items()):
+            self._states[k] = v.to(device)
+        for l in self.sublayers():
+            l.states_to(device)
+
+    # ------------------------------------------------------------------ keras weights
+    def keras_weight_params(self) -> list:
+        """Ordered entries of Keras ``get_weights()``: Param objects or state names."""
+        return list(self._params)
+
+    def get_keras_weights(self) -> list[np.ndarray]:
+        out = []
+        for e in self.keras_weight_params():
+            if isinstance(e, Param):
+                out.append(e.to_keras(to_numpy(e.master)))
+            else:
+                out.append(to_numpy(self._states[e]))
+        return out
+
+    def set_keras_weights(self, ws: Sequence[np.ndarray]):
+        ents = self.keras_weight_params()
+        if len(ws) != len(ents):
+            raise ValueError(f"{self.name}: expected {len(ents)} weight arrays, got {len(ws)}")
+        for e, w in zip(ents, ws):
+            if isinstance(e, Param):
+                arr = np.asarray(e.from_keras(np.asarray(w, dtype=np.float32)), dtype=np.float32).reshape(e.shape)
+                if e.master is None:
+                    e._initial = arr
+                else:
+                    e.master.copy_(torch.from_numpy(arr))
+            else:
+                self._states[e].copy_(torch.as_tensor(np.asarray(w), dtype=torch.float32))
+
+    # ------------------------------------------------------------------ config
+    def get_config(self) -> dict:
+        cfg = {"name": self.name, "trainable": self.trainable}
+        if self._input_shape_arg is not None:
+            cfg["batch_input_shape"] = [None, *self._input_shape_arg]
+        return cfg
+
+    @classmethod
+    def from_config(cls, cfg: dict):
+        cfg = dict(cfg)
+        return cls(**cfg)
+
+    def __repr__(self):
+        return f"<{type(self).__name__} {self.name}>"
+
+
+def layer_from_config(d: dict) -> Layer:
+    cls = _LAYER_TYPES.get(d["class_name"])
+    if cls is None:
+        raise ValueError(f"unknown layer class {d['class_name']!r}")
+    return cls.from_config(d["config"])
+
+
+# =========================================================================================
+#                                         Model
+# =========================================================================================
+_LOSS_ALIASES = {
+    "mse": "mean_squared_error",
+    "mae": "mean_absolute_error",
+    "categorical_crossentropy": "categorical_crossentropy",
+    "sparse_categorical_crossentropy": "sparse_categorical_crossentropy",
+    "binary_crossentropy": "binary_crossentropy",
+    "mean_squared_error": "mean_squared_error",
+    "mean_absolute_error": "mean_absolute_error",
+}
+
+
+class Model(Layer):
+    """A trainable network: owns the parameter arena, optimizer and loss."""
+
+    def __init__(self, name=None, **kw):
+        super().__init__(name=name, **kw)
+        self.arena: ParamArena | None = None
+        self.device = torch.device("cpu")
+        self.compute_dtype = torch.float32
+        self.optimizer = None
+        self.loss = None
+        self.metrics: list = []
+        self.history: list[float] = []
+        self.seed = 0
+
+    # ---------------------------------------------------------------- placement
+    def build_model(self):
+        raise NotImplementedError
+
+    def place(self, device=None, dtype=None, seed: int | None = None):
+        """Allocate the flat parameter arena on ``device`` (bf16 compute on GPU)."""
+        if device is None:
+            device = "cuda" if torch.cuda.is_available() else "cpu"
+        device = torch.device(device)
+        if dtype is None:
+            dtype = torch.bfloat16 if device.type == "cuda" else torch.float32
+        self.build_model()
+        old = None
+        if self.arena is not None:
+            old = self.arena.master.detach().cpu()
+        params = self.all_params()
+        self.arena = ParamArena(params, device, dtype, seed=self.seed if seed is None else seed)
+        if old is not None and old.numel() == self.arena.master.numel():
+            self.arena.set_flat(old)
+        self.states_to(device)
+        self.device, self.compute_dtype = device, dtype
+        if self.optimizer is not None:
+            self.optimizer.bind(self.arena)
+        return self
+
+    def _ensure_placed(self):
+        if self.arena is None:
+            self.place()
+
+    # ---------------------------------------------------------------- compile / train
+    def compile(self, optimizer="sgd", loss="mean_squared_error", metrics=None, **kw):
+        self.optimizer = optim_mod.get(optimizer)
+        if isinstance(loss, str):
+            if loss not in _LOSS_ALIASES:
+                raise ValueError(f"unknown loss {loss!r}")
+            loss = _LOSS_ALIASES[loss]
+        self.loss = loss
+        self.metrics = list(metrics or [])
+        if self.arena is not None:
+            self.optimizer.bind(self.arena)
+        return self
+
+    def to_input(self, x) -> torch.Tensor:
+        if isinstance(x, np.ndarray):
+            x = torch.from_numpy(np.ascontiguousarray(x))
+        x = torch.as_tensor(x)
+        if x.is_floating_point():
+            x = x.to(self.device, self.compute_dtype, non_blocking=True)
+        else:
+            x = x.to(self.device, non_blocking=True)
+        return x
+
+    def to_target(self, y) -> torch.Tensor:
+        if isinstance(y, np.ndarray):
+            y = torch.from_numpy(np.ascontiguousarray(y))
+        y = torch.as_tensor(y)
+        return y.to(self.device, non_blocking=True)
+
+    # subclasses: forward(x, training, logits=False)
+    def forward(self, x, training=False, logits=False):
+        raise NotImplementedError
+
+    def call(self, x, training=False):
+        return self.forward(x, training)
+
+    def ends_with_softmax(self) -> bool:
+        return False
+
+    def compute_loss(self, x, y, training=True):
+        from ..ops import loss as L
+
+        name = self.loss
+        if callable(name):
+            return name(self.forward(x, training), y)
+        if name in ("categorical_crossentropy", "sparse_categorical_crossentropy") and self.ends_with_softmax():
+            logits = self.forward(x, training, logits=True)
+            logits = logits.reshape(logits.shape[0], -1)
+            if name == "sparse_categorical_crossentropy" or not y.is_floating_point():
+                return L.softmax_cross_entropy(logits, labels=y.reshape(-1).long())
+            return L.softmax_cross_entropy(logits, probs=y.reshape(logits.shape))
+        out = self.forward(x, training).float()
+        yy = y.float().reshape(out.shape)
+        if name == "mean_squared_error":
+            return L.mean_squared_error(out, yy)
+        if name == "mean_absolute_error":
+            return L.mean_absolute_error(out, yy)
+        if name == "binary_crossentropy":
+            return L.binary_crossentropy(out, yy)
+        if name == "categorical_crossentropy":
+            return L.categorical_crossentropy_probs(out, yy)
+        if name == "sparse_categorical_crossentropy":
+            return torch.nn.functional.nll_loss(torch.log(out.clamp_min(1e-7)), y.long().reshape(-1))
+        raise ValueError(f"unsupported loss {name!r}")
+
+    def backward_step(self, x, y):
+        """zero grads -> forward -> loss -> backward (grads land in the arena). Returns loss tensor."""
+        self._ensure_placed()
+        self.arena.zero_grad()
+        loss = self.compute_loss(x, y, training=True)
+        loss.backward()
+        return loss
+
+    def train_on_batch(self, x, y, grad_sync=None, grad_scale: float = 1.0) -> float:
+        if self.optimizer is None:
+            raise RuntimeError("call compile() before training")
+        self._ensure_placed()
+        if self.optimizer.arena is not self.arena:
+            self.optimizer.bind(self.arena)
+        x, y = self.to_input(x), self.to_target(y)
+        loss = self.backward_step(x, y)
+        if grad_sync is not None:
+            grad_scale = grad_sync(self.arena) * grad_scale
+        self.optimizer.step(grad_scale)
+        return float(loss.detach())
+
+    def fit(self, x, y, batch_size=32, epochs=1, verbose=0, shuffle=True, drop_last=False):
+        x = np.asarray(x)
+        y = np.asarray(y)
+        n = x.shape[0]
+        rng = np.random.default_rng(self.seed)
+        hist = []
+        for ep in range(epochs):
+            idx = rng.permutation(n) if shuffle else np.arange(n)
+            losses = []
+            stop = n - (n % batch_size) if drop_last else n
+            for b in range(0, stop, batch_size):
+                sel = idx[b : b + batch_size]
+                losses.append(self.train_on_batch(x[sel], y[sel]))
+            hist.append(float(np.mean(losses)) if losses else float("nan"))
+            if verbose:
+                print(f"Epoch {ep + 1}/{epochs} - loss: {hist[-1]:.4f}")
+        self.history.extend(hist)
+        return {"loss": hist}
+
+    @torch.no_grad()
+    def predict(self, x, batch_size=256) -> np.ndarray:
+        self._ensure_placed()
+        x = np.asarray(x) if not isinstance(x, torch.Tensor) else x
+        outs = []
+        for b in range(0, x.shape[0], batch_size):
+            xb = self.to_input(x[b : b + batch_size])
+            outs.append(self.forward(xb, training=False).float().cpu())
+        if not outs:
+            return np.zeros((0,) + tuple(self.output_shape or ()), dtype=np.float32)
+        return torch.cat(outs).numpy()
+
+    @torch.no_grad()
+    def evaluate(self, x, y, batch_size=256) -> float:
+        self._ensure_placed()
+        tot, cnt = 0.0, 0
+        for b in range(0, len(x), batch_size):
+            xb, yb = self.to_input(np.asarray(x[b : b + batch_size])), self.to_target(np.asarray(y[b : b + batch_size]))
+            tot += float(self.compute_loss(xb, yb, training=False)) * xb.shape[0]
+            cnt += xb.shape[0]
+        return tot / max(cnt, 1)
+
+    # ---------------------------------------------------------------- weights / serialisation
+    def weight_layers(self) -> list[Layer]:
+        return [l for l in self.all_layers() if l is not self and (l._params or l._states)]
+
+    def get_weights(self) -> list[np.ndarray]:
+        self.build_model()
+        out = []
+        for l in self.weight_layers():
+            if l.keras_weight_params():
+                out.extend(l.get_keras_weights())
+        return out
+
+    def set_weights(self, weights: Sequence[np.ndarray]):
+        self.build_model()
+        weights = list(weights)
+        i = 0
+        for l in self.weight_layers():
+            n = len(l.keras_weight_params())
+            if n:
+                l.set_keras_weights(weights[i : i + n])
+                i += n
+        if i != len(weights):
+            raise ValueError(f"set_weights: expected {i} arrays, got {len(weights)}")
+        if self.arena is not None:
+            self.arena.sync_compute()
+
+    def get_flat_weights(self) -> torch.Tensor:
+        self._ensure_placed()
+        return self.arena.master
+
+    def to_json(self) -> str:
+        return json.dumps({"class_name": type(self).__name__, "config": self.get_config(),
+                           "backend": "distributeddeeplearningspark_amd", "keras_version": "2.1.6"})
+
+    def summary(self, print_fn=print):
+        self.build_model()
+        line = "_" * 65
+        print_fn(line)
+        print_fn(f"{'Layer (type)':<29}{'Output Shape':<25}{'Param #':<11}")
+        print_fn("=" * 65)
+        rows = self.summary_rows()
+        for i, (nm, shp, cnt) in enumerate(rows):
+            print_fn(f"{nm:<29}{shp:<25}{cnt:<11}")
+            print_fn("=" * 65 if i == len(rows) - 1 else line)
+        total = self.count_params()
+        print_fn(f"Total params: {total:,}")
+        print_fn(f"Trainable params: {total:,}")
+        print_fn("Non-trainable params: 0")
+        print_fn(line)
+
+    def summary_rows(self):
+        rows = []
+        for l in self.sublayers():
+            shp = "(None, " + ", ".join(str(s) for s in (l.output_shape or ())) + ")"
+            if l.output_shape is not None and len(l.output_shape) == 1:
+                shp = f"(None, {l.output_shape[0]})"
+            rows.append((f"{l.name} ({type(l).__name__})", shp, l.count_params()))
+        return rows
+
+
+class Sequential(Model):
+    """Keras ``Sequential``: ``add`` layers, the first carries ``input_shape``."""
+
+    def __init__(self, layers: Sequence[Layer] | None = None, name=None, **kw):
+        super().__init__(name=name or _auto_name("sequential"), **kw)
+        self.layers: list[Layer] = []
+        for l in layers or []:
+            self.add(l)
+
+    def add(self, layer: Layer):
+        if self.arena is not None:
+            raise RuntimeError("cannot add layers after the model was placed")
+        self.layers.append(layer)
+        self.built = False
+
+    def sublayers(self):
+        return list(self.layers)
+
+    def build_model(self):
+        if self.built:
+            return
+        if not self.layers:
+            raise ValueError("empty Sequential model")
+        shape = self.layers[0]._input_shape_arg or self._input_shape_arg
+        if shape is None:
+            raise ValueError("the first layer needs input_shape=")
+        self.input_shape = tuple(shape)
+        for l in self.layers:
+            shape = l.ensure_built(shape)
+        self.output_shape = tuple(shape)
+        self.built = True
+
+    def ends_with_softmax(self) -> bool:
+        last = self.layers[-1] if self.layers else None
+        return getattr(last, "activation_name", None) == "softmax"
+
+    def forward(self, x, training=False, logits=False):
+        n = len(self.layers)
+        for i, l in enumerate(self.layers):
+            if logits and i == n - 1 and getattr(l, "activation_name", None) == "softmax":
+                x = l.call(x, training, skip_activation=True) if hasattr(l, "supports_skip") else x
+                break
+            x = l.call(x, training)
+        return x
+
+    def get_config(self):
+        return {"name": self.name, "layers": [{"class_name": type(l).__name__, "config": l.get_config()}
+                                              for l in self.layers]}
+
+    @classmethod
+    def from_config(cls, cfg):
+        m = cls(name=cfg.get("name"))
+        for d in cfg["layers"]:
+            m.add(layer_from_config(d))
+        return m
+
+
+def model_from_json(s: str) -> Model:
+    d = json.loads(s)
+    cls = _LAYER_TYPES.get(d["class_name"])
+    if cls is None:
+        raise ValueError(f"unknown model class {d['class_name']!r}")
+    return cls.from_config(d["config"])

@@ -1,0 +1,169 @@
+"""Keras-style optimizers on the flat parameter arena (``worker_optimizer='adam'`` etc.).
+
+Defaults follow Keras 2 (the reference's per-worker optimizers, ``ddl_mnist_aztk.py:195``,
+``ddl_nyiso_aztk.py:207,255``): Adam(lr=1e-3, eps=1e-7, Keras epsilon placement),
+Adagrad(lr=1e-2, eps=1e-7), RMSprop(lr=1e-3, rho=0.9), SGD(lr=1e-2).
+Each optimizer's ``step`` is ONE kernel launch over the whole model on the GPU.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..ops import optim as K
+
+
+class Optimizer:
+    name = "optimizer"
+
+    def __init__(self, lr: float, weight_decay: float = 0.0, clipnorm: float | None = None):
+        self.lr = float(lr)
+        self.weight_decay = float(weight_decay)
+        self.clipnorm = clipnorm
+        self.iterations = 0
+        self.arena = None
+        self.state: dict[str, torch.Tensor] = {}
+
+    def bind(self, arena):
+        self.arena = arena
+        self.iterations = 0
+        self._alloc()
+        return self
+
+    def _alloc(self):
+        pass
+
+    def _zeros(self):
+        return torch.zeros_like(self.arena.master)
+
+    def get_config(self):
+        return {"name": self.name, "lr": self.lr, "weight_decay": self.weight_decay}
+
+    def state_dict(self):
+        return {"iterations": self.iterations, **{k: v.detach().cpu() for k, v in self.state.items()}}
+
+    def load_state_dict(self, sd):
+        self.iterations = int(sd.get("iterations", 0))
+        for k, v in sd.items():
+            if k in self.state:
+                self.state[k].copy_(v.to(self.state[k].device))
+
+    def _grad_scale(self, grad_scale):
+        if self.clipnorm is None:
+            return grad_scale
+        g = self.arena.grad
+        norm = float(torch.linalg.vector_norm(g)) * grad_scale
+        if norm > self.clipnorm:
+            return grad_scale * self.clipnorm / (norm + 1e-6)
+        return grad_scale
+
+    def step(self, grad_scale: float = 1.0):
+        self.iterations += 1
+        a = self.arena
+        w16 = None if a.compute is a.master else a.compute
+        self._apply(a.master, a.grad, w16, self._grad_scale(grad_scale))
+
+    def _apply(self, w, g, w16, gs):
+        raise NotImplementedError
+
+
+class SGD(Optimizer):
+    name = "sgd"
+
+    def __init__(self, lr=0.01, momentum=0.0, nesterov=False, dampening=0.0, weight_decay=0.0, clipnorm=None):
+        super().__init__(lr, weight_decay, clipnorm)
+        self.momentum, self.nesterov, self.dampening = float(momentum), bool(nesterov), float(dampening)
+
+    def _alloc(self):
+        if self.momentum:
+            self.state["momentum"] = self._zeros()
+
+    def _apply(self, w, g, w16, gs):
+        K.sgd_(w, g, self.state.get("momentum"), w16, lr=self.lr, momentum=self.momentum, dampening=self.dampening,
+               weight_decay=self.weight_decay, nesterov=self.nesterov, grad_scale=gs)
+
+    def get_config(self):
+        return {**super().get_config(), "momentum": self.momentum, "nesterov": self.nesterov}
+
+
+class Adam(Optimizer):
+    name = "adam"
+
+    def __init__(self, lr=0.001, beta_1=0.9, beta_2=0.999, epsilon=1e-7, weight_decay=0.0, decoupled=False,
+                 keras_eps=True, clipnorm=None):
+        super().__init__(lr, weight_decay, clipnorm)
+        self.b1, self.b2, self.eps = float(beta_1), float(beta_2), float(epsilon)
+        self.decoupled, self.keras_eps = bool(decoupled), bool(keras_eps)
+
+    def _alloc(self):
+        self.state["m"] = self._zeros()
+        self.state["v"] = self._zeros()
+
+    def _apply(self, w, g, w16, gs):
+        K.adam_(w, g, self.state["m"], self.state["v"], w16, lr=self.lr, beta1=self.b1, beta2=self.b2, eps=self.eps,
+                weight_decay=self.weight_decay, decoupled=self.decoupled, keras_eps=self.keras_eps,
+                step=self.iterations, grad_scale=gs)
+
+    def get_config(self):
+        return {**super().get_config(), "beta_1": self.b1, "beta_2": self.b2, "epsilon": self.eps}
+
+
+class AdamW(Adam):
+    name = "adamw"
+
+    def __init__(self, lr=0.001, beta_1=0.9, beta_2=0.999, epsilon=1e-8, weight_decay=0.01, clipnorm=None):
+        super().__init__(lr, beta_1, beta_2, epsilon, weight_decay, decoupled=True, keras_eps=False,
+                         clipnorm=clipnorm)
+
+
+class Adagrad(Optimizer):
+    name = "adagrad"
+
+    def __init__(self, lr=0.01, epsilon=1e-7, weight_decay=0.0, clipnorm=None):
+        super().__init__(lr, weight_decay, clipnorm)
+        self.eps = float(epsilon)
+
+    def _alloc(self):
+        self.state["acc"] = self._zeros()
+
+    def _apply(self, w, g, w16, gs):
+        K.adagrad_(w, g, self.state["acc"], w16, lr=self.lr, eps=self.eps, weight_decay=self.weight_decay,
+                   grad_scale=gs)
+
+
+class RMSprop(Optimizer):
+    name = "rmsprop"
+
+    def __init__(self, lr=0.001, rho=0.9, epsilon=1e-7, weight_decay=0.0, clipnorm=None):
+        super().__init__(lr, weight_decay, clipnorm)
+        self.rho, self.eps = float(rho), float(epsilon)
+
+    def _alloc(self):
+        self.state["acc"] = self._zeros()
+
+    def _apply(self, w, g, w16, gs):
+        K.rmsprop_(w, g, self.state["acc"], w16, lr=self.lr, rho=self.rho, eps=self.eps,
+                   weight_decay=self.weight_decay, grad_scale=gs)
+
+
+_BY_NAME = {"sgd": SGD, "adam": Adam, "adamw": AdamW, "adagrad": Adagrad, "rmsprop": RMSprop}
+
+
+def get(spec) -> Optimizer:
+    """Resolve a Keras optimizer spec: a name (``'adam'``), a config dict or an instance."""
+    if isinstance(spec, Optimizer):
+        return spec
+    if isinstance(spec, str):
+        key = spec.lower()
+        if key not in _BY_NAME:
+            raise ValueError(f"unknown optimizer {spec!r}; known: {sorted(_BY_NAME)}")
+        return _BY_NAME[key]()
+    if isinstance(spec, dict):
+        cfg = dict(spec)
+        name = cfg.pop("name")
+        return _BY_NAME[name.lower()](**cfg)
+    raise TypeError(f"bad optimizer spec {spec!r}")
+
+
+def clone(opt: Optimizer) -> Optimizer:
+    """Fresh optimizer with the same hyper-parameters (worker-local optimizer state)."""
+    return get(opt.get_config()) if isinstance(opt, Optimizer) else get(opt)

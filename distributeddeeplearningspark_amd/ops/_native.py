@@ -1,0 +1,54 @@
+"""Loader of the in-tree native extension (``_C.so``: HIP kernels for gfx950 + host runtime).
+
+On a GPU the HIP path is the ONLY path: if the extension is missing or stale an op
+raises instead of silently falling back to a PyTorch implementation.  CPU tensors use
+the reference implementations in the individual op modules (tests, CPU executors).
+``DDL_BACKEND=torch`` forces the reference path on GPU too (A/B benchmarking only).
+"""
+from __future__ import annotations
+
+import importlib
+import os
+
+_C = None
+_ERR: Exception | None = None
+
+
+def _load():
+    global _C, _ERR
+    if _C is not None or _ERR is not None:
+        return
+    try:
+        _C = importlib.import_module("distributeddeeplearningspark_amd._C")
+    except Exception as e:  # pragma: no cover - depends on build state
+        _ERR = e
+
+
+def has_native() -> bool:
+    _load()
+    return _C is not None
+
+
+def C():
+    """Return the native module or raise a loud error explaining how to build it."""
+    _load()
+    if _C is None:
+        raise RuntimeError(
+            "distributeddeeplearningspark_amd native extension (_C.so) is not available: "
+            f"{_ERR!r}. Build it with `python -m distributeddeeplearningspark_amd._build`."
+        )
+    return _C
+
+
+def force_reference() -> bool:
+    return os.environ.get("DDL_BACKEND", "").lower() == "torch"
+
+
+def use_native(t) -> bool:
+    """True when ``t`` lives on the GPU and the HIP path must be used."""
+    if not getattr(t, "is_cuda", False):
+        return False
+    if force_reference():
+        return False
+    C()  # raises if missing: no silent fallback on GPU
+    return True

@@ -1,0 +1,233 @@
+"""NHWC 2-D convolution on MFMA implicit GEMM.
+
+Layouts: activations ``[N, H, W, C]`` (bf16 on GPU), weights ``[Co, KH, KW, Ci]``
+(K-contiguous for the forward GEMM).  Parameter gradients are accumulated out of
+band into fp32 gradient-arena views (``gw``, ``gb``), so autograd only tracks
+activations and the data-parallel engine is told when each gradient is final.
+
+Decomposition (``ConvGeometry``):
+  forward  : M = N*Ho*Wo pixels, N = Co, K = taps*Ci.  1x1/stride-1 is a plain GEMM;
+             Ci % 64 == 0 gathers A through a tap table (implicit GEMM, zero padding
+             handled in the loader); other Ci (stem, MNIST) use an im2col pass.
+  dgrad    : the transposed convolution as implicit GEMM over dY with a flipped tap
+             table; stride s is split into s*s parity classes, each a stride-1 problem
+             whose rows scatter to a strided grid (OutMap) — no col2im, no atomics.
+  wgrad    : M = Co, N = taps*Ci, K = N*Ho*Wo with split-K and fp32 accumulation;
+             A = dY read row-contiguous, B = X gathered per tap.
+"""
+from __future__ import annotations
+
+import math
+from functools import lru_cache
+
+import torch
+import torch.nn.functional as F
+
+from . import gemm as G
+from ._native import C, use_native
+from ._ref import accumulate, ref_grads
+
+
+def _pair(v):
+    return (v, v) if isinstance(v, int) else tuple(v)
+
+
+class ConvGeometry:
+    def __init__(self, N, H, W, Ci, Co, KH, KW, stride, pad, dil):
+        self.N, self.H, self.W, self.Ci, self.Co, self.KH, self.KW = N, H, W, Ci, Co, KH, KW
+        self.sh, self.sw = stride
+        self.ph, self.pw = pad
+        self.dh, self.dw = dil
+        self.Ho = (H + 2 * self.ph - self.dh * (KH - 1) - 1) // self.sh + 1
+        self.Wo = (W + 2 * self.pw - self.dw * (KW - 1) - 1) // self.sw + 1
+        if self.Ho <= 0 or self.Wo <= 0:
+            raise ValueError(f"conv output would be empty: {(H, W)} k={(KH, KW)} s={stride} p={pad}")
+        self.T = KH * KW
+        self.M = N * self.Ho * self.Wo
+        self.taps_h = [r * self.dh - self.ph for r in range(KH) for s in range(KW)]
+        self.taps_w = [s * self.dw - self.pw for r in range(KH) for s in range(KW)]
+        self.is_pointwise = KH == 1 and KW == 1 and stride == (1, 1) and pad == (0, 0)
+        self.implicit_fwd = Ci % 64 == 0 and self.T <= 64
+        self.implicit_dgrad = Co % 64 == 0 and Ci % 8 == 0 and self.T <= 64
+        self.implicit_wgrad = Ci % 64 == 0 and Co % 8 == 0 and self.T <= 64
+        self.kpad = math.ceil(self.T * Ci / 8) * 8
+        self.fwd_geom = dict(n=N, hi=H, wi=W, c=Ci, ho=self.Ho, wo=self.Wo, sh=self.sh, sw=self.sw, tap_c=Ci,
+                             dh=self.taps_h, dw=self.taps_w)
+        # data-gradient parity classes
+        self.classes = []
+        for ph in range(self.sh):
+            for pw in range(self.sw):
+                Hc = -(-(H - ph) // self.sh)
+                Wc = -(-(W - pw) // self.sw)
+                if Hc <= 0 or Wc <= 0:
+                    continue
+                dh_, dw_, wt = [], [], []
+                for r in range(KH):
+                    nh = ph + self.ph - r * self.dh
+                    if nh % self.sh:
+                        continue
+                    for s in range(KW):
+                        nw = pw + self.pw - s * self.dw
+                        if nw % self.sw:
+                            continue
+                        dh_.append(nh // self.sh)
+                        dw_.append(nw // self.sw)
+                        wt.append(r * KW + s)
+                self.classes.append(dict(ph=ph, pw=pw, Hc=Hc, Wc=Wc, dh=dh_, dw=dw_, wt=wt))
+        self.dgrad_needs_zero = any(len(c["wt"]) == 0 for c in self.classes) or len(self.classes) < self.sh * self.sw
+
+
+@lru_cache(maxsize=4096)
+def geometry(N, H, W, Ci, Co, KH, KW, stride, pad, dil):
+    return ConvGeometry(N, H, W, Ci, Co, KH, KW, stride, pad, dil)
+
+
+# ------------------------------------------------------------------------------- native
+def _im2col(x, g: ConvGeometry, taps_h, taps_w, ho, wo, sh, sw, kpad):
+    col = torch.empty((x.shape[0] * ho * wo, kpad), dtype=torch.bfloat16, device=x.device)
+    C().im2col(x, col, ho, wo, sh, sw, list(taps_h), list(taps_w), kpad)
+    return col
+
+
+def conv_fwd_native(x, w, g: ConvGeometry, bias=None, relu=False, stats=None):
+    y = torch.empty((g.N, g.Ho, g.Wo, g.Co), dtype=torch.bfloat16, device=x.device)
+    y2 = y.view(g.M, g.Co)
+    if g.is_pointwise:
+        G.linear_fwd(x.view(g.M, g.Ci), w.view(g.Co, g.Ci), bias=bias, relu=relu, out=y2, stats=stats)
+    elif g.implicit_fwd:
+        G.gemm(x, w, y2, g.M, g.Co, g.T * g.Ci, G.KC_GATHER, G.KC, 0, g.T * g.Ci, g.Co, G.EPI_BF16, bias=bias,
+               relu=relu, geom=g.fwd_geom, stats=stats)
+    else:
+        col = _im2col(x, g, g.taps_h, g.taps_w, g.Ho, g.Wo, g.sh, g.sw, g.kpad)
+        w2 = w.reshape(g.Co, g.T * g.Ci)
+        if g.kpad != g.T * g.Ci:
+            w2 = F.pad(w2, (0, g.kpad - g.T * g.Ci))
+        G.linear_fwd(col, w2.contiguous(), bias=bias, relu=relu, out=y2, stats=stats)
+    return y
+
+
+def conv_dgrad_native(dy, w, g: ConvGeometry, resid=None):
+    """dx = conv^T(dy, w) (+ resid, fused into the epilogue when the layout allows)."""
+    dev = dy.device
+    if g.is_pointwise:
+        dx = torch.empty((g.N, g.H, g.W, g.Ci), dtype=torch.bfloat16, device=dev)
+        G.linear_dgrad(dy.view(g.M, g.Co), w.view(g.Co, g.Ci), out=dx.view(-1, g.Ci),
+                       resid=None if resid is None else resid.view(-1, g.Ci))
+        return dx
+    dx = (torch.zeros if g.dgrad_needs_zero else torch.empty)((g.N, g.H, g.W, g.Ci), dtype=torch.bfloat16, device=dev)
+    strided = g.sh > 1 or g.sw > 1
+    for cl in g.classes:
+        nt = len(cl["wt"])
+        if nt == 0:
+            continue
+        Mc = g.N * cl["Hc"] * cl["Wc"]
+        om = None
+        if strided:
+            om = dict(gh=cl["Hc"], gw=cl["Wc"], hy=g.H, wy=g.W, so=g.sh, oh=cl["ph"], ow=cl["pw"])
+        r = None if (resid is None or strided) else resid.view(-1, g.Ci)
+        if g.implicit_dgrad:
+            geom = dict(n=g.N, hi=g.Ho, wi=g.Wo, c=g.Co, ho=cl["Hc"], wo=cl["Wc"], sh=1, sw=1, tap_c=g.Co,
+                        dh=cl["dh"], dw=cl["dw"], wt=cl["wt"])
+            G.gemm(dy, w, dx, Mc, g.Ci, nt * g.Co, G.KC_GATHER, G.RC_TAPS, 0, g.T * g.Ci, g.Ci, G.EPI_BF16,
+                   geom=geom, outmap=om, b_kdiv=g.Co, b_tap_stride=g.Ci, resid=r, ldr=g.Ci if r is not None else 0)
+        else:
+            kp = math.ceil(nt * g.Co / 8) * 8
+            col = _im2col(dy, g, cl["dh"], cl["dw"], cl["Hc"], cl["Wc"], 1, 1, kp)
+            # wperm[ci][t][co] = w[co][wt[t]][ci]
+            wsel = w.reshape(g.Co, g.T, g.Ci)[:, cl["wt"], :]
+            wperm = wsel.permute(2, 1, 0).reshape(g.Ci, nt * g.Co)
+            if kp != nt * g.Co:
+                wperm = F.pad(wperm, (0, kp - nt * g.Co))
+            wperm = wperm.contiguous()
+            G.gemm(col, wperm, dx, Mc, g.Ci, kp, G.KC, G.KC, kp, kp, g.Ci, G.EPI_BF16, outmap=om, resid=r,
+                   ldr=g.Ci if r is not None else 0)
+    if resid is not None and strided:
+        C().add_bf16(dx, resid, dx)
+    return dx
+
+
+def conv_wgrad_native(dy, x, g: ConvGeometry, gw):
+    """gw[Co, KH, KW, Ci] (fp32) += dW."""
+    gw2 = gw.view(g.Co, g.T * g.Ci)
+    if g.is_pointwise:
+        G.linear_wgrad(dy.view(g.M, g.Co), x.view(g.M, g.Ci), gw2)
+    elif g.implicit_wgrad:
+        G.gemm(dy, x, gw2, g.Co, g.T * g.Ci, g.M, G.RC, G.RC_GATHER, g.Co, 0, g.T * g.Ci, G.EPI_F32, beta=1.0,
+               geom=g.fwd_geom, bn_cap=min(128, g.Ci))
+    else:
+        col = _im2col(x, g, g.taps_h, g.taps_w, g.Ho, g.Wo, g.sh, g.sw, g.kpad)
+        if g.kpad == g.T * g.Ci:
+            G.linear_wgrad(dy.view(g.M, g.Co), col, gw2)
+        else:
+            tmp = torch.zeros((g.Co, g.kpad), dtype=torch.float32, device=dy.device)
+            G.linear_wgrad(dy.view(g.M, g.Co), col, tmp)
+            gw2.add_(tmp[:, : g.T * g.Ci])
+
+
+# ------------------------------------------------------------------------------- reference
+def conv_ref(x, w, bias, stride, pad, dil, relu=False):
+    y = F.conv2d(x.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), bias, stride, pad, dil).permute(0, 2, 3, 1)
+    if relu:
+        y = torch.relu(y)
+    return y.contiguous()
+
+
+# ------------------------------------------------------------------------------- autograd
+class _Conv2dFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, gw, gb, cfg):
+        stride, pad, dil, relu, stats, hook = cfg
+        N, H, W, Ci = x.shape
+        Co, KH, KW, _ = w.shape
+        ctx.cfg = cfg
+        ctx.native = use_native(x)
+        if ctx.native:
+            g = geometry(N, H, W, Ci, Co, KH, KW, stride, pad, dil)
+            y = conv_fwd_native(x.contiguous(), w, g, bias=b, relu=relu, stats=stats)
+            ctx.g = g
+        else:
+            y = conv_ref(x, w.to(x.dtype), None if b is None else b.to(x.dtype), stride, pad, dil, relu)
+        ctx.gw, ctx.gb = gw, gb
+        ctx.save_for_backward(x, w, b, y if relu else None)
+        ctx.needs_dx = ctx.needs_input_grad[0]
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, b, y = ctx.saved_tensors
+        gw, gb = ctx.gw, ctx.gb
+        stride, pad, dil, relu, _, hook = ctx.cfg
+        dy = dy.contiguous()
+        dx = None
+        if ctx.native:
+            g = ctx.g
+            if relu:
+                d2 = torch.empty_like(dy)
+                C().relu_bwd(dy, y, d2)
+                dy = d2
+            if gb is not None:
+                C().bias_grad(dy, gb, g.Co, True)
+            if gw is not None:
+                conv_wgrad_native(dy, x, g, gw)
+            if ctx.needs_dx:
+                dx = conv_dgrad_native(dy, w, g)
+        else:
+            fn = lambda xx, ww, bb: conv_ref(xx, ww, bb, stride, pad, dil, relu)
+            bb = None if b is None else b.to(x.dtype)
+            gx, gww, gbb = ref_grads(fn, [x, w.to(x.dtype), bb], dy)
+            accumulate(gw, gww)
+            accumulate(gb, gbb)
+            dx = gx if ctx.needs_dx else None
+        if hook is not None:
+            hook()
+        return dx, None, None, None, None, None
+
+
+def conv2d(x, w, bias=None, *, stride=1, padding=0, dilation=1, relu=False, grad_w=None, grad_b=None, stats=None,
+           on_grad=None):
+    """NHWC conv.  ``w``: [Co, KH, KW, Ci] compute-dtype weights; ``grad_w``/``grad_b``:
+    fp32 buffers that receive ``+= dW``/``+= db`` in backward; ``stats``: optional
+    [32, 2, Co] fp32 workspace receiving fused per-channel sum / sum-of-squares
+    (GPU); ``on_grad``: callback fired once the parameter gradients are final."""
+    cfg = (_pair(stride), _pair(padding), _pair(dilation), bool(relu), stats, on_grad)
+    return _Conv2dFn.apply(x, w, bias, grad_w, grad_b, cfg)

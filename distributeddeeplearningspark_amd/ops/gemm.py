@@ -1,0 +1,115 @@
+"""Python front of the MFMA implicit-GEMM kernel family (``csrc/include/ddl_gemm_kernel.h``).
+
+Semantics: ``C[m][n] = alpha * sum_k A(m,k) * B(n,k)`` with each operand either
+K-contiguous (``KC``: ``ptr + r*ld + k``) or row-contiguous (``RC``: ``ptr + k*ld + r``).
+So  ``Y = X @ W.T`` (Linear fwd)   = KC x KC,
+    ``dX = dY @ W``   (Linear dgrad) = KC x RC,
+    ``dW = dY.T @ X`` (Linear wgrad) = RC x RC,
+without materialising any transpose: the kernel reads RC operands with
+``ds_read_b64_tr_b16`` (hardware LDS transpose).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ._native import C
+
+KC, RC, KC_GATHER, RC_GATHER, RC_TAPS = 0, 1, 2, 3, 4
+EPI_BF16, EPI_F32, EPI_F32_ATOMIC = 0, 1, 2
+_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64)}
+_CU = 256
+
+
+def choose_tile(M: int, N: int, bn_cap: int = 128) -> int:
+    bn = 128 if (N > 64 and bn_cap >= 128) else 64
+    bm = 128 if M > 64 else 64
+    if bm == 128 and bn == 128 and math.ceil(M / 128) * math.ceil(N / 128) < 2 * _CU:
+        # not enough tiles to fill 256 CUs twice: shrink the tile along the larger extent
+        bm = 64 if M <= N else 128
+        bn = 64 if M > N else 128
+    for tid, (tm, tn) in _TILES.items():
+        if (tm, tn) == (bm, bn):
+            return tid
+    return 3
+
+
+def choose_split(M: int, N: int, K: int, tile: int, allow: bool) -> int:
+    """Return k_split (elements, multiple of 64)."""
+    kfull = max(64, math.ceil(K / 64) * 64)
+    if not allow:
+        return kfull
+    bm, bn = _TILES[tile]
+    tiles = math.ceil(M / bm) * math.ceil(N / bn)
+    if tiles >= 2 * _CU or K < 1024:
+        return kfull
+    splits = min(math.ceil(4 * _CU / tiles), max(1, K // 512))
+    ks = math.ceil(K / splits / 64) * 64
+    return max(64, ks)
+
+
+def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, beta=0.0, bias=None, resid=None,
+         ldr=0, relu=False, geom=None, outmap=None, b_kdiv=0, b_tap_stride=0, stats=None, tile=None, k_split=None,
+         bn_cap=128):
+    """Raw launcher with automatic tile / split-K choice.
+
+    With ``epi == EPI_F32`` and a split-K decomposition the launch switches to the
+    atomic epilogue, which *accumulates* into ``c``: callers that need ``c = A@B``
+    must pass a zeroed ``c`` (the gradient arena is zeroed once per step) or
+    ``beta == 1`` semantics.
+    """
+    if tile is None:
+        tile = choose_tile(M, N, bn_cap)
+    if k_split is None:
+        k_split = choose_split(M, N, K, tile, allow=(epi != EPI_BF16))
+    if epi == EPI_F32 and k_split < K:
+        if beta not in (0.0, 1.0):
+            raise ValueError("split-K fp32 gemm supports beta in {0,1} (beta=0 needs a zeroed C)")
+        epi = EPI_F32_ATOMIC
+    C().gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, tile, k_split, alpha, beta, bias, resid, ldr,
+             relu, geom, outmap, b_kdiv, b_tap_stride, stats)
+    return c
+
+
+# ----------------------------------------------------------------------------------------
+# 2-D helpers (row-major tensors)
+# ----------------------------------------------------------------------------------------
+def linear_fwd(x2, w, bias=None, relu=False, out=None, resid=None, stats=None):
+    """y[M,N] = x2[M,K] @ w[N,K]^T (+bias)(+resid)(relu) -> bf16."""
+    M, K = x2.shape
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=x2.device)
+    return gemm(x2, w, out, M, N, K, KC, KC, x2.stride(0), w.stride(0), out.stride(0), EPI_BF16, bias=bias, relu=relu,
+                resid=resid, ldr=(resid.stride(0) if resid is not None else 0), stats=stats)
+
+
+def linear_dgrad(dy, w, out=None, resid=None):
+    """dx[M,K] = dy[M,N] @ w[N,K] -> bf16 (w read row-contiguous; no transpose copy)."""
+    M, N = dy.shape
+    K = w.shape[1]
+    if out is None:
+        out = torch.empty((M, K), dtype=torch.bfloat16, device=dy.device)
+    return gemm(dy, w, out, M, K, N, KC, RC, dy.stride(0), w.stride(0), out.stride(0), EPI_BF16, resid=resid,
+                ldr=(resid.stride(0) if resid is not None else 0))
+
+
+def linear_wgrad(dy, x2, gw):
+    """gw[N,K] += dy[M,N]^T @ x2[M,K]  (fp32 accumulation into the gradient arena)."""
+    M, N = dy.shape
+    K = x2.shape[1]
+    return gemm(dy, x2, gw, N, K, M, RC, RC, dy.stride(0), x2.stride(0), gw.stride(0), EPI_F32, beta=1.0)
+
+
+def matmul(a, b, trans_a=False, trans_b=False, out=None, alpha=1.0):
+    """General bf16 matmul op(a) @ op(b) -> bf16 using the KC/RC operand modes."""
+    M = a.shape[1] if trans_a else a.shape[0]
+    K = a.shape[0] if trans_a else a.shape[1]
+    N = b.shape[0] if trans_b else b.shape[1]
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    a_mode = RC if trans_a else KC
+    # B(n,k): op(b)[k][n]; trans_b -> b[n][k] is K-contiguous
+    b_mode = KC if trans_b else RC
+    return gemm(a, b, out, M, N, K, a_mode, b_mode, a.stride(0), b.stride(0), out.stride(0), EPI_BF16, alpha=alpha)

@@ -1,0 +1,76 @@
+"""Losses.  ``softmax_cross_entropy`` is ONE fused HIP kernel that returns the loss and
+stores dlogits during the forward sweep (the backward only hands them out)."""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from ._native import C, use_native
+
+
+class _SoftmaxXentFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, probs, smoothing, ignore_index):
+        B, K = logits.shape
+        if use_native(logits):
+            logits = logits.contiguous()
+            loss_rows = torch.empty(B, dtype=torch.float32, device=logits.device)
+            dl = torch.empty_like(logits)
+            if labels is not None:
+                valid = (labels != ignore_index).sum().clamp_min(1).to(torch.float32)
+                # grad scale 1/valid is data-dependent: use 1/B in-kernel, rescale below on host-free path
+                C().softmax_xent(logits, labels.to(torch.int64).contiguous(), None, loss_rows, dl, 1.0, smoothing,
+                                 ignore_index)
+                ctx.save_for_backward(dl, valid)
+                return loss_rows.sum() / valid
+            C().softmax_xent(logits, None, probs.to(torch.float32).contiguous(), loss_rows, dl, 1.0 / B, 0.0, -100)
+            ctx.save_for_backward(dl, None)
+            return loss_rows.mean()
+        with torch.enable_grad():
+            lg = logits.detach().requires_grad_(True)
+            lp = F.log_softmax(lg.float(), dim=-1)
+            if labels is not None:
+                loss = F.nll_loss(lp, labels.long(), ignore_index=ignore_index, reduction="none")
+                if smoothing > 0:
+                    sm = -lp.mean(dim=-1)
+                    loss = (1 - smoothing) * loss + smoothing * sm * (labels != ignore_index)
+                valid = (labels != ignore_index).sum().clamp_min(1)
+                out = loss.sum() / valid
+            else:
+                out = -(probs.float() * lp).sum(-1).mean()
+            (dl,) = torch.autograd.grad(out, [lg])
+        ctx.save_for_backward(dl, None)
+        return out.detach()
+
+    @staticmethod
+    def backward(ctx, g):
+        dl, valid = ctx.saved_tensors
+        scale = g if valid is None else g / valid
+        return (dl * scale.to(dl.dtype)).to(dl.dtype), None, None, None, None
+
+
+def softmax_cross_entropy(logits, labels=None, probs=None, label_smoothing=0.0, ignore_index=-100):
+    """Mean CE of softmax(logits) against class ``labels`` or target ``probs`` rows."""
+    if (labels is None) == (probs is None):
+        raise ValueError("pass exactly one of labels / probs")
+    return _SoftmaxXentFn.apply(logits, labels, probs, float(label_smoothing), int(ignore_index))
+
+
+def mean_squared_error(pred, target):
+    return ((pred.float() - target.float()) ** 2).mean()
+
+
+def mean_absolute_error(pred, target):
+    return (pred.float() - target.float()).abs().mean()
+
+
+def binary_crossentropy(pred, target, eps=1e-7):
+    p = pred.float().clamp(eps, 1 - eps)
+    t = target.float()
+    return -(t * torch.log(p) + (1 - t) * torch.log(1 - p)).mean()
+
+
+def categorical_crossentropy_probs(probs, target, eps=1e-7):
+    """Keras semantics on already-softmaxed outputs: -sum(y*log(clip(p)))."""
+    p = probs.float().clamp(eps, 1 - eps)
+    return -(target.float() * torch.log(p)).sum(-1).mean()

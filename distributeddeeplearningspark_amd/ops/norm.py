@@ -1,0 +1,133 @@
+"""Batch normalisation (NHWC, training statistics) with fused residual-add + ReLU.
+
+GPU path (csrc/kernels/bn.hip): statistics either come fused from the producing
+convolution's epilogue (``stats`` workspace filled by the GEMM) or from one
+``bn_stats`` sweep; a per-channel finalize yields scale/shift and updates running
+statistics; one apply sweep writes ``relu(x*scale + shift + residual)``.  Backward is
+reduce (masked dy, dy*xhat) -> finalize (dgamma/dbeta, coefficients) -> one dx sweep that
+also emits the masked gradient of the residual branch.
+"""
+from __future__ import annotations
+
+import torch
+
+from ._native import C, use_native
+from ._ref import accumulate, ref_grads
+
+SHARDS = 32
+
+
+def new_stats_workspace(C_, device):
+    return torch.zeros((SHARDS, 2, C_), dtype=torch.float32, device=device)
+
+
+def bn_ref(x, gamma, beta, mean, var, eps, resid=None, relu=False):
+    y = (x - mean) / torch.sqrt(var + eps)
+    if gamma is not None:
+        y = y * gamma
+    if beta is not None:
+        y = y + beta
+    if resid is not None:
+        y = y + resid
+    if relu:
+        y = torch.relu(y)
+    return y
+
+
+def _bn_train_ref(x, gamma, beta, eps, resid, relu):
+    dims = tuple(range(x.dim() - 1))
+    mean = x.mean(dims)
+    var = x.var(dims, unbiased=False)
+    return bn_ref(x, gamma, beta, mean, var, eps, resid, relu)
+
+
+class _BatchNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, resid, ggamma, gbeta, state):
+        rmean, rvar, momentum, eps, relu, training, stats, hook = state
+        Cc = x.shape[-1]
+        M = x.numel() // Cc
+        ctx.native = use_native(x)
+        ctx.relu, ctx.eps, ctx.hook, ctx.training = relu, eps, hook, training
+        ctx.has_resid = resid is not None
+        if ctx.native:
+            x = x.contiguous()
+            dev = x.device
+            scale = torch.empty(Cc, dtype=torch.float32, device=dev)
+            shift = torch.empty(Cc, dtype=torch.float32, device=dev)
+            mean = torch.empty(Cc, dtype=torch.float32, device=dev)
+            invstd = torch.empty(Cc, dtype=torch.float32, device=dev)
+            if training:
+                if stats is None:
+                    stats = new_stats_workspace(Cc, dev)
+                    C().bn_stats(x, stats, Cc)
+                C().bn_finalize(stats, M, Cc, gamma, beta, eps, momentum, rmean, rvar, mean, invstd, scale, shift)
+            else:
+                invstd = torch.rsqrt(rvar + eps)
+                mean = rmean.clone()
+                g = gamma if gamma is not None else torch.ones_like(rmean)
+                b = beta if beta is not None else torch.zeros_like(rmean)
+                scale = (g * invstd).contiguous()
+                shift = (b - rmean * scale).contiguous()
+            y = torch.empty_like(x)
+            C().bn_apply(x, scale, shift, None if resid is None else resid.contiguous(), y, Cc, relu)
+            ctx.gg, ctx.gbt = ggamma, gbeta
+            ctx.save_for_backward(x, y if relu else None, mean, invstd, gamma)
+            return y
+        # reference path
+        if training:
+            dims = tuple(range(x.dim() - 1))
+            with torch.no_grad():
+                bm = x.mean(dims)
+                bv = x.var(dims, unbiased=False)
+                if rmean is not None:
+                    n = x.numel() // Cc
+                    rmean.mul_(1 - momentum).add_(momentum * bm.to(rmean.dtype))
+                    rvar.mul_(1 - momentum).add_(momentum * (bv * n / max(n - 1, 1)).to(rvar.dtype))
+            y = _bn_train_ref(x, gamma, beta, eps, resid, relu)
+        else:
+            y = bn_ref(x, gamma, beta, rmean, rvar, eps, resid, relu)
+        ctx.gg, ctx.gbt, ctx.rstats = ggamma, gbeta, (rmean, rvar)
+        ctx.save_for_backward(x, resid, gamma, beta)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dres = None
+        if ctx.native:
+            x, y, mean, invstd, gamma = ctx.saved_tensors
+            ggamma, gbeta = ctx.gg, ctx.gbt
+            dy = dy.contiguous()
+            Cc = x.shape[-1]
+            M = x.numel() // Cc
+            ws = new_stats_workspace(Cc, x.device)
+            C().bn_bwd_reduce(dy, x, y, mean, ws, Cc)
+            coef = torch.empty(3 * Cc, dtype=torch.float32, device=x.device)
+            C().bn_bwd_finalize(ws, M, Cc, gamma, invstd, ggamma, gbeta, coef)
+            dx = torch.empty_like(x)
+            if ctx.has_resid:
+                dres = torch.empty_like(x)
+            C().bn_bwd_dx(dy, x, y, mean, invstd, coef, dx, dres, Cc)
+        else:
+            x, resid, gamma, beta = ctx.saved_tensors
+            ggamma, gbeta = ctx.gg, ctx.gbt
+            rmean, rvar = ctx.rstats
+            eps, relu = ctx.eps, ctx.relu
+            if ctx.training:
+                fn = lambda xx, gg, bb, rr: _bn_train_ref(xx, gg, bb, eps, rr, relu)
+            else:
+                fn = lambda xx, gg, bb, rr: bn_ref(xx, gg, bb, rmean, rvar, eps, rr, relu)
+            dx, dg, db, dres = ref_grads(fn, [x, gamma, beta, resid], dy)
+            accumulate(ggamma, dg)
+            accumulate(gbeta, db)
+        if ctx.hook is not None:
+            ctx.hook()
+        return dx, None, None, dres, None, None, None
+
+
+def batch_norm(x, gamma, beta, running_mean, running_var, *, training=True, momentum=0.1, eps=1e-5, resid=None,
+               relu=False, grad_gamma=None, grad_beta=None, stats=None, on_grad=None):
+    """NHWC batch norm over all but the last dim.  ``stats``: fused statistics workspace
+    already accumulated by the producer (GPU); ``resid``/``relu``: fused epilogue."""
+    state = (running_mean, running_var, momentum, eps, bool(relu), bool(training), stats, on_grad)
+    return _BatchNormFn.apply(x, gamma, beta, resid, grad_gamma, grad_beta, state)

@@ -1,0 +1,341 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op.
+
+Inputs are rounded to bf16 first, then the reference runs in fp32 on those exact
+values; tolerances reflect bf16 outputs (rel ~1e-2) and fp32 accumulation.
+Operands are asymmetric random data (catches transposed C/D maps).
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _C():
+    from distributeddeeplearningspark_amd.ops._native import C
+
+    return C()
+
+
+def rnd(*shape, scale=1.0, dtype=torch.bfloat16, seed=None):
+    g = torch.Generator(device="cpu")
+    g.manual_seed(seed if seed is not None else (hash(shape) & 0xFFFF))
+    return (torch.randn(*shape, generator=g) * scale).to(dtype).to(DEV)
+
+
+def close(a, b, rtol=2e-2, atol=2e-2, what=""):
+    a = a.float().cpu()
+    b = b.float().cpu()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    bad = (err > tol).float().mean().item()
+    rel = (err.norm() / (b.norm() + 1e-12)).item()
+    assert bad < 1e-3 and rel < 2e-2, f"{what}: frac_bad={bad:.2e} rel_l2={rel:.2e} max_err={err.max().item():.3e}"
+
+
+# ----------------------------------------------------------------------------- GEMM
+@pytest.mark.parametrize("M,N,K", [(256, 256, 256), (200, 72, 136), (1000, 384, 64), (64, 1000, 2048), (8, 16, 8)])
+@pytest.mark.parametrize("a_rc", [False, True])
+@pytest.mark.parametrize("b_rc", [False, True])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3])
+def test_gemm_layouts(M, N, K, a_rc, b_rc, tile):
+    from distributeddeeplearningspark_amd.ops import gemm as G
+
+    if (a_rc and M % 8) or (b_rc and N % 8):
+        pytest.skip("row-contiguous operands need a multiple of 8 rows")
+    A = rnd(M, K, seed=1)          # logical A [M,K]
+    B = rnd(N, K, seed=2)          # logical B [N,K]
+    ref = A.float() @ B.float().T
+    a_t = A.T.contiguous() if a_rc else A.contiguous()
+    b_t = B.T.contiguous() if b_rc else B.contiguous()
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    G.gemm(a_t, b_t, out, M, N, K, G.RC if a_rc else G.KC, G.RC if b_rc else G.KC, a_t.stride(0), b_t.stride(0), N,
+           G.EPI_BF16, tile=tile)
+    close(out, ref, what=f"gemm a_rc={a_rc} b_rc={b_rc} tile={tile}")
+
+
+def test_gemm_identity_asymmetric():
+    from distributeddeeplearningspark_amd.ops import gemm as G
+
+    n = 64
+    A = torch.eye(n, dtype=torch.bfloat16, device=DEV)
+    B = (torch.arange(n * n, device=DEV).reshape(n, n) % 97).to(torch.bfloat16)  # B[n][k], asymmetric
+    out = torch.empty(n, n, dtype=torch.bfloat16, device=DEV)
+    G.gemm(A, B, out, n, n, n, G.KC, G.KC, n, n, n, G.EPI_BF16)
+    assert torch.equal(out.float(), B.float().T), "C/D map transposed"
+
+
+def test_gemm_epilogues_and_splitk():
+    from distributeddeeplearningspark_amd.ops import gemm as G
+
+    M, N, K = 512, 192, 1024
+    A, B = rnd(M, K, seed=3), rnd(N, K, seed=4)
+    bias = torch.randn(N, device=DEV)
+    res = rnd(M, N, seed=5)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    G.gemm(A, B, out, M, N, K, G.KC, G.KC, K, K, N, G.EPI_BF16, bias=bias, resid=res, ldr=N, relu=True)
+    ref = torch.relu(A.float() @ B.float().T + bias + res.float())
+    close(out, ref, what="bias+resid+relu")
+    # fp32 split-K accumulate (wgrad-shaped: small M,N, huge K)
+    M2, N2, K2 = 64, 576, 50176
+    dy, x = rnd(K2, M2, seed=6), rnd(K2, N2, seed=7)
+    gw = torch.full((M2, N2), 0.5, device=DEV)
+    G.gemm(dy, x, gw, M2, N2, K2, G.RC, G.RC, M2, N2, N2, G.EPI_F32, beta=1.0)
+    ref2 = 0.5 + dy.float().T @ x.float()
+    close(gw, ref2, rtol=1e-3, atol=1e-2, what="split-K fp32 accumulate")
+
+
+def test_gemm_fused_stats():
+    from distributeddeeplearningspark_amd.ops import gemm as G
+
+    M, N, K = 3000, 128, 192
+    A, B = rnd(M, K, seed=8), rnd(N, K, seed=9)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    st = torch.zeros(32, 2, N, device=DEV)
+    G.gemm(A, B, out, M, N, K, G.KC, G.KC, K, K, N, G.EPI_BF16, stats=st)
+    s = st.sum(0)
+    o = out.float()
+    close(s[0], o.sum(0), rtol=1e-3, atol=1e-1, what="fused sum")
+    close(s[1], (o * o).sum(0), rtol=1e-3, atol=1e-1, what="fused sumsq")
+
+
+# ----------------------------------------------------------------------------- conv
+CONV_CASES = [
+    # N, H, W, Ci, Co, k, stride, pad
+    (2, 14, 14, 64, 64, 3, 1, 1),
+    (2, 15, 15, 64, 128, 3, 2, 1),
+    (2, 14, 14, 256, 512, 1, 2, 0),
+    (2, 7, 7, 128, 64, 1, 1, 0),
+    (2, 32, 32, 3, 64, 7, 2, 3),   # stem: im2col path
+    (4, 28, 28, 1, 32, 3, 1, 0),   # MNIST conv1
+    (4, 26, 26, 32, 32, 3, 1, 0),  # MNIST conv2 (im2col fwd / implicit-less dgrad)
+    (2, 9, 9, 128, 128, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_bwd(case):
+    from distributeddeeplearningspark_amd.ops.conv import conv2d
+
+    N, H, W, Ci, Co, k, s, p = case
+    x = rnd(N, H, W, Ci, seed=10)
+    w = rnd(Co, k, k, Ci, scale=1.0 / math.sqrt(k * k * Ci), seed=11)
+    b = torch.randn(Co, device=DEV) * 0.1
+    gw = torch.zeros(Co, k, k, Ci, device=DEV)
+    gb = torch.zeros(Co, device=DEV)
+    xg = x.clone().requires_grad_(True)
+    w_anchor = w.clone().requires_grad_(True)
+    y = conv2d(xg, w_anchor, b, stride=s, padding=p, grad_w=gw, grad_b=gb)
+    dy = rnd(*y.shape, seed=12)
+    y.backward(dy)
+    # fp32 reference on the same bf16 values
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = w.float().permute(0, 3, 1, 2).requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    yr = F.conv2d(xr, wr, br, s, p)
+    yr.backward(dy.float().permute(0, 3, 1, 2))
+    close(y, yr.permute(0, 2, 3, 1), what=f"conv fwd {case}")
+    close(xg.grad, xr.grad.permute(0, 2, 3, 1), what=f"conv dgrad {case}")
+    close(gw, wr.grad.permute(0, 2, 3, 1), rtol=1e-2, atol=1e-2, what=f"conv wgrad {case}")
+    close(gb, br.grad, rtol=1e-2, atol=1e-2, what=f"conv bgrad {case}")
+
+
+def test_conv_relu_fused():
+    from distributeddeeplearningspark_amd.ops.conv import conv2d
+
+    x = rnd(2, 10, 10, 64, seed=13)
+    w = rnd(64, 3, 3, 64, scale=0.05, seed=14)
+    xg = x.clone().requires_grad_(True)
+    y = conv2d(xg, w.clone().requires_grad_(True), None, stride=1, padding=1, relu=True)
+    dy = rnd(*y.shape, seed=15)
+    y.backward(dy)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = torch.relu(F.conv2d(xr, w.float().permute(0, 3, 1, 2), None, 1, 1))
+    yr.backward(dy.float().permute(0, 3, 1, 2))
+    close(y, yr.permute(0, 2, 3, 1), what="conv+relu fwd")
+    close(xg.grad, xr.grad.permute(0, 2, 3, 1), what="conv+relu dgrad")
+
+
+# ----------------------------------------------------------------------------- batch norm
+@pytest.mark.parametrize("resid,relu", [(False, False), (True, True), (False, True)])
+def test_batchnorm(resid, relu):
+    from distributeddeeplearningspark_amd.ops.norm import batch_norm
+
+    N, H, W, Cc = 8, 7, 7, 256
+    x = (rnd(N, H, W, Cc, seed=16).float() * 2 + 0.5).to(torch.bfloat16)
+    r = rnd(N, H, W, Cc, seed=17) if resid else None
+    g = torch.rand(Cc, device=DEV) + 0.5
+    b = torch.randn(Cc, device=DEV) * 0.1
+    rm, rv = torch.zeros(Cc, device=DEV), torch.ones(Cc, device=DEV)
+    gg, gbt = torch.zeros(Cc, device=DEV), torch.zeros(Cc, device=DEV)
+    xg = x.clone().requires_grad_(True)
+    rg = r.clone().requires_grad_(True) if resid else None
+    y = batch_norm(xg, g.clone().requires_grad_(True), b, rm, rv, training=True, momentum=0.1, eps=1e-5,
+                   resid=rg, relu=relu, grad_gamma=gg, grad_beta=gbt)
+    dy = rnd(*y.shape, seed=18)
+    y.backward(dy)
+    xr = x.float().requires_grad_(True)
+    gr, br = g.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    rr = r.float().requires_grad_(True) if resid else None
+    mean = xr.mean((0, 1, 2))
+    var = xr.var((0, 1, 2), unbiased=False)
+    yr = (xr - mean) / torch.sqrt(var + 1e-5) * gr + br
+    if resid:
+        yr = yr + rr
+    if relu:
+        yr = torch.relu(yr)
+    yr.backward(dy.float())
+    close(y, yr, what="bn fwd")
+    close(xg.grad, xr.grad, rtol=3e-2, atol=3e-2, what="bn dx")
+    close(gg, gr.grad, rtol=1e-2, atol=5e-2, what="bn dgamma")
+    close(gbt, br.grad, rtol=1e-2, atol=5e-2, what="bn dbeta")
+    if resid:
+        close(rg.grad, rr.grad, what="bn dresid")
+    n = N * H * W
+    close(rm, 0.1 * mean.detach(), rtol=1e-3, atol=1e-3, what="running mean")
+    close(rv, 0.9 + 0.1 * var.detach() * n / (n - 1), rtol=1e-3, atol=1e-3, what="running var")
+
+
+# ----------------------------------------------------------------------------- pooling
+@pytest.mark.parametrize("k,s,p,H", [(3, 2, 1, 16), (2, 2, 0, 24), (3, 2, 1, 15)])
+def test_maxpool(k, s, p, H):
+    from distributeddeeplearningspark_amd.ops.pool import max_pool2d
+
+    x = rnd(2, H, H, 64, seed=19)
+    xg = x.clone().requires_grad_(True)
+    y = max_pool2d(xg, k, s, p)
+    dy = rnd(*y.shape, seed=20)
+    y.backward(dy)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = F.max_pool2d(xr, k, s, p)
+    yr.backward(dy.float().permute(0, 3, 1, 2))
+    close(y, yr.permute(0, 2, 3, 1), what="maxpool fwd")
+    close(xg.grad, xr.grad.permute(0, 2, 3, 1), what="maxpool bwd")
+
+
+def test_global_avgpool():
+    from distributeddeeplearningspark_amd.ops.pool import global_avg_pool
+
+    x = rnd(4, 7, 7, 2048, seed=21)
+    xg = x.clone().requires_grad_(True)
+    y = global_avg_pool(xg)
+    dy = rnd(*y.shape, seed=22)
+    y.backward(dy)
+    close(y, x.float().mean((1, 2)), what="avgpool fwd")
+    close(xg.grad, (dy.float() / 49).view(4, 1, 1, 2048).expand_as(xg), what="avgpool bwd")
+
+
+# ----------------------------------------------------------------------------- loss
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_softmax_xent(dtype):
+    from distributeddeeplearningspark_amd.ops.loss import softmax_cross_entropy
+
+    B, K = 64, 1000
+    logits = rnd(B, K, scale=3.0, dtype=dtype, seed=23)
+    labels = torch.randint(0, K, (B,), device=DEV)
+    lg = logits.clone().requires_grad_(True)
+    loss = softmax_cross_entropy(lg, labels=labels)
+    loss.backward()
+    lr = logits.float().requires_grad_(True)
+    ref = F.cross_entropy(lr, labels)
+    ref.backward()
+    assert abs(loss.item() - ref.item()) < 1e-3 * max(1.0, ref.item())
+    close(lg.grad, lr.grad, rtol=2e-2, atol=1e-4, what="xent grad")
+    probs = F.one_hot(labels, K).float()
+    lg2 = logits.clone().requires_grad_(True)
+    loss2 = softmax_cross_entropy(lg2, probs=probs)
+    loss2.backward()
+    assert abs(loss2.item() - ref.item()) < 1e-3 * max(1.0, ref.item())
+    close(lg2.grad, lr.grad, rtol=2e-2, atol=1e-4, what="xent(probs) grad")
+
+
+# ----------------------------------------------------------------------------- optimizers
+@pytest.mark.parametrize("kind", ["sgd", "sgd_nesterov", "adam", "adamw", "adam_keras", "adagrad", "rmsprop"])
+def test_optimizers(kind):
+    from distributeddeeplearningspark_amd.ops import optim as O
+
+    n = 4096 + 64
+    w0 = torch.randn(n)
+    g = torch.randn(n)
+    outs = {}
+    for dev in ("cpu", DEV):
+        w = w0.clone().to(dev)
+        gd = g.to(dev)
+        s1, s2 = torch.zeros(n, device=dev), torch.zeros(n, device=dev)
+        w16 = torch.empty(n, dtype=torch.bfloat16, device=dev) if dev != "cpu" else None
+        for step in range(1, 4):
+            if kind.startswith("sgd"):
+                O.sgd_(w, gd, s1, w16, lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=kind == "sgd_nesterov",
+                       grad_scale=0.5)
+            elif kind == "adam":
+                O.adam_(w, gd, s1, s2, w16, lr=1e-3, weight_decay=1e-2, step=step)
+            elif kind == "adamw":
+                O.adam_(w, gd, s1, s2, w16, lr=1e-3, weight_decay=1e-2, decoupled=True, step=step)
+            elif kind == "adam_keras":
+                O.adam_(w, gd, s1, s2, w16, lr=1e-3, eps=1e-7, keras_eps=True, step=step)
+            elif kind == "adagrad":
+                O.adagrad_(w, gd, s1, w16, lr=1e-2)
+            else:
+                O.rmsprop_(w, gd, s1, w16, lr=1e-3)
+        outs[dev] = (w.cpu(), None if w16 is None else w16.float().cpu())
+    close(outs[DEV][0], outs["cpu"][0], rtol=1e-5, atol=1e-6, what=f"{kind} master")
+    close(outs[DEV][1], outs["cpu"][0], rtol=1e-2, atol=1e-2, what=f"{kind} bf16 copy")
+
+
+# ----------------------------------------------------------------------------- misc
+def test_normalize_u8_and_casts():
+    from distributeddeeplearningspark_amd.data.ingest import DeviceFeeder
+
+    x = torch.randint(0, 256, (2, 8, 8, 3), dtype=torch.uint8, device=DEV)
+    f = DeviceFeeder(DEV)
+    y = f.normalize(x)
+    ref = (x.float() - f.mean) * f.invstd
+    close(y, ref, what="normalize_u8")
+    a = torch.randn(1003, device=DEV)
+    b = torch.empty(1003, dtype=torch.bfloat16, device=DEV)
+    _C().cast_f32_bf16(a, b)
+    assert torch.equal(b, a.to(torch.bfloat16))
+
+
+def test_linear_layer_odd_sizes():
+    from distributeddeeplearningspark_amd.ops.linear import linear
+
+    for (M, K, N) in [(16, 4608, 225), (16, 225, 10), (32, 128, 1)]:
+        x = rnd(M, K, seed=24)
+        w = rnd(N, K, scale=1 / math.sqrt(K), seed=25)
+        b = torch.randn(N, device=DEV)
+        gw, gb = torch.zeros(N, K, device=DEV), torch.zeros(N, device=DEV)
+        xg = x.clone().requires_grad_(True)
+        y = linear(xg, w.clone().requires_grad_(True), b, relu=True, grad_w=gw, grad_b=gb)
+        dy = rnd(M, N, seed=26)
+        y.backward(dy)
+        xr, wr, br = x.float().requires_grad_(True), w.float().requires_grad_(True), b.clone().requires_grad_(True)
+        yr = torch.relu(xr @ wr.T + br)
+        yr.backward(dy.float())
+        close(y, yr, what=f"linear fwd {(M, K, N)}")
+        close(xg.grad, xr.grad, what=f"linear dgrad {(M, K, N)}")
+        close(gw, wr.grad, rtol=1e-2, atol=1e-2, what=f"linear wgrad {(M, K, N)}")
+        close(gb, br.grad, rtol=1e-2, atol=1e-2, what=f"linear bgrad {(M, K, N)}")
+
+
+def test_resnet50_step_matches_reference():
+    """Small ResNet-50 (64x64 input): GPU bf16 loss/grad-norm close to the CPU fp32 path."""
+    from distributeddeeplearningspark_amd.models import ResNet50
+
+    torch.manual_seed(0)
+    x = torch.randn(4, 64, 64, 3)
+    y = torch.randint(0, 10, (4,))
+    res = {}
+    for dev in ("cpu", DEV):
+        m = ResNet50(input_shape=(64, 64, 3), num_classes=10)
+        m.compile("sgd", "sparse_categorical_crossentropy")
+        m.place(dev, seed=3)
+        loss = m.backward_step(m.to_input(x), m.to_target(y))
+        res[dev] = (float(loss), m.arena.grad.norm().item())
+    (lc, gc), (lg, gg) = res["cpu"], res[DEV]
+    assert abs(lc - lg) < 0.05 * max(1.0, abs(lc)), (lc, lg)
+    assert abs(gc - gg) < 0.1 * gc, (gc, gg)
