@@ -8,6 +8,10 @@ Output: one JSON line per shape + a summary table (gpurun_out/conv_layers.json).
 from __future__ import annotations
 
 import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import json
 import statistics
 import time

@@ -7,6 +7,10 @@ used only to report how the hand-written kernels compare with the vendor librari
 from __future__ import annotations
 
 import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import json
 import time
 

@@ -61,7 +61,7 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
   CHECK_BF16(a);
   CHECK_BF16(b);
   if (epi == EPI_BF16) { CHECK_BF16(c); } else { CHECK_F32(c); }
-  const bool k_vec = a_mode == OP_KC || a_mode == OP_KC_GATHER || b_mode == OP_KC;
+  const bool k_vec = a_mode == OP_KC || a_mode == OP_KC_GATHER || a_mode == OP_KC_GATHER8 || b_mode == OP_KC;
   TORCH_CHECK(!k_vec || K % 8 == 0, "gemm: K-contiguous operands need K % 8 == 0 (16-B vectors), got ", K);
   if (a_mode == OP_KC) TORCH_CHECK(lda % 8 == 0, "gemm: lda must be a multiple of 8");
   if (b_mode == OP_KC) TORCH_CHECK(ldb % 8 == 0, "gemm: ldb must be a multiple of 8");
@@ -73,7 +73,8 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
   const int bm = (tile == 0 || tile == 1) ? 128 : 64;
   const int bn = (tile == 0 || tile == 2) ? 128 : 64;
   if (a_mode == OP_RC || a_mode == OP_RC_GATHER) TORCH_CHECK(M % 8 == 0, "gemm: row-contiguous A needs M % 8 == 0");
-  if (b_mode == OP_RC || b_mode == OP_RC_GATHER || b_mode == OP_RC_TAPS) TORCH_CHECK(N % 8 == 0, "gemm: row-contiguous B needs N % 8 == 0");
+  if (b_mode == OP_RC || b_mode == OP_RC_GATHER || b_mode == OP_RC_GATHER8 || b_mode == OP_RC_TAPS)
+    TORCH_CHECK(N % 8 == 0, "gemm: row-contiguous B needs N % 8 == 0");
   GemmParams p{};
   p.a = a.data_ptr();
   p.b = b.data_ptr();
@@ -109,6 +110,9 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
     if (a_mode == OP_KC_GATHER) TORCH_CHECK(p.g.tap_c % 64 == 0 && K == (int64_t)p.g.ntaps * p.g.tap_c, "conv A gather: tap_c % 64 and K = taps*C");
     if (b_mode == OP_RC_GATHER) TORCH_CHECK(p.g.tap_c % bn == 0 && N == (int64_t)p.g.ntaps * p.g.tap_c, "conv B gather: tap_c % BN and N = taps*C");
     if (b_mode == OP_RC_TAPS) TORCH_CHECK(b_kdiv % 64 == 0 && K == (int64_t)p.g.ntaps * b_kdiv, "conv B taps: kdiv % 64 and K = taps*kdiv");
+    if (a_mode == OP_KC_GATHER8) TORCH_CHECK(p.g.tap_c % 8 == 0 && K == (int64_t)p.g.ntaps * p.g.tap_c, "conv A gather8: tap_c % 8 and K = taps*C");
+    if (b_mode == OP_RC_GATHER8) TORCH_CHECK(p.g.tap_c % 8 == 0 && N == (int64_t)p.g.ntaps * p.g.tap_c, "conv B gather8: tap_c % 8 and N = taps*C");
+    if (a_mode == OP_KC_GATHER || a_mode == OP_KC_GATHER8) TORCH_CHECK(p.g.c == p.g.tap_c, "gather: c == tap_c");
   } else {
     TORCH_CHECK(a_mode <= OP_RC && b_mode <= OP_RC, "gather modes need a geometry");
   }
@@ -122,6 +126,7 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
     p.om.so = d["so"].cast<int>();
     p.om.oh = d["oh"].cast<int>();
     p.om.ow = d["ow"].cast<int>();
+    p.om.zero_siblings = d.contains("zero") ? d["zero"].cast<int>() : 0;
   }
   if (stats) {
     CHECK_CUDA(*stats);
@@ -153,6 +158,8 @@ PYBIND11_MODULE(_C, m) {
   m.attr("OP_KC_GATHER") = (int)OP_KC_GATHER;
   m.attr("OP_RC_GATHER") = (int)OP_RC_GATHER;
   m.attr("OP_RC_TAPS") = (int)OP_RC_TAPS;
+  m.attr("OP_KC_GATHER8") = (int)OP_KC_GATHER8;
+  m.attr("OP_RC_GATHER8") = (int)OP_RC_GATHER8;
   m.attr("EPI_BF16") = (int)EPI_BF16;
   m.attr("EPI_F32") = (int)EPI_F32;
   m.attr("EPI_F32_ATOMIC") = (int)EPI_F32_ATOMIC;

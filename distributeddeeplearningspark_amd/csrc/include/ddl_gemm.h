@@ -20,6 +20,8 @@ enum OperandMode : int {
   OP_KC_GATHER = 2,  // conv input gather: r = output pixel, k = tap*C + c
   OP_RC_GATHER = 3,  // conv input gather: k = output pixel, r = tap*C + c
   OP_RC_TAPS = 4,    // weight [co][tap][c]: r = c, k = tap*Co + co
+  OP_KC_GATHER8 = 5, // as KC_GATHER for small channel counts (C % 8 == 0): tap looked up per 16-B vector
+  OP_RC_GATHER8 = 6, // as RC_GATHER for C % 8 == 0
 };
 
 enum EpilogueMode : int {
@@ -47,6 +49,7 @@ struct OutMap {       // scatter of output rows to a strided NHWC grid (dgrad pa
   int hy, wy;         // destination spatial dims
   int so;             // destination stride
   int oh, ow;         // destination offsets
+  int zero_siblings;  // also write zeros to the other so*so-1 positions of each cell
 };
 
 struct GemmParams {

@@ -41,7 +41,7 @@ __device__ __forceinline__ uint4 ldg16(const void* p) { return *reinterpret_cast
 // ----------------------------------------------------------------------------------------
 template <int R, int MODE>
 struct Operand {
-  static constexpr bool KC = (MODE == OP_KC || MODE == OP_KC_GATHER);
+  static constexpr bool KC = (MODE == OP_KC || MODE == OP_KC_GATHER || MODE == OP_KC_GATHER8);
   static constexpr int V = R / 32;  // 16-B vectors per thread per K-tile (R*64*2/16/256)
   uint4 reg[V];
   // per-thread precomputed state
@@ -59,7 +59,7 @@ struct Operand {
     rows = rows_;
     r0 = r0_;
     K = K_;
-    if constexpr (MODE == OP_KC_GATHER) {
+    if constexpr (MODE == OP_KC_GATHER || MODE == OP_KC_GATHER8) {
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         const int idx = threadIdx.x + v * NTHREADS;
@@ -103,6 +103,33 @@ struct Operand {
         const int ih = hbase[v] + dh, iw = wbase[v] + dw;
         const bool ok = rvalid[v] && (unsigned)ih < (unsigned)g.hi && (unsigned)iw < (unsigned)g.wi;
         reg[v] = ok ? ldg16(ptr + ((long)(pixbase[v] + ih * g.wi + iw)) * g.c + c0 + kc * 8) : make_uint4(0, 0, 0, 0);
+      }
+    } else if constexpr (MODE == OP_KC_GATHER8) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const int idx = threadIdx.x + v * NTHREADS;
+        const int k = k0 + (idx & 7) * 8;
+        bool ok = rvalid[v] && k < K;
+        const int t = ok ? k / g.tap_c : 0;
+        const int c = k - t * g.tap_c;
+        const int ih = hbase[v] + g.dh[t], iw = wbase[v] + g.dw[t];
+        ok = ok && (unsigned)ih < (unsigned)g.hi && (unsigned)iw < (unsigned)g.wi;
+        reg[v] = ok ? ldg16(ptr + ((long)(pixbase[v] + ih * g.wi + iw)) * g.c + c) : make_uint4(0, 0, 0, 0);
+      }
+    } else if constexpr (MODE == OP_RC_GATHER8) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const int idx = threadIdx.x + v * NTHREADS;
+        const int krow = idx / (R / 8), rc = idx % (R / 8);
+        const int k = k0 + krow, r = r0 + rc * 8;
+        bool ok = k < K && r < rows;
+        const int t = ok ? r / g.tap_c : 0;
+        const int c = r - t * g.tap_c;
+        int n, i, j;
+        pix_decompose((uint32_t)(ok ? k : 0), g.ho, g.wo, n, i, j);
+        const int ih = i * g.sh + g.dh[t], iw = j * g.sw + g.dw[t];
+        ok = ok && (unsigned)ih < (unsigned)g.hi && (unsigned)iw < (unsigned)g.wi;
+        reg[v] = ok ? ldg16(ptr + ((long)((n * g.hi + ih) * g.wi + iw)) * g.c + c) : make_uint4(0, 0, 0, 0);
       }
     } else if constexpr (MODE == OP_RC_GATHER) {
       const int t = r0 / g.tap_c;  // block-uniform: tap_c % R == 0
@@ -231,7 +258,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams
 #pragma unroll
       for (int i = 0; i < RM; ++i)
 #pragma unroll
-        for (int j = 0; j < RN; ++j) acc[i][j] = mfma16x16x32(af[i], bf[j], acc[i][j]);
+        for (int j = 0; j < RN; ++j) acc[i][j] = mfma16x16x32(bf[j], af[i], acc[i][j]);  // D^T: 4 consecutive n per lane
     }
     if (more) {
       A.store(odd ? lds_a0 : lds_a1);
@@ -241,56 +268,133 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams
   }
 
   // ---------------------------------- epilogue ----------------------------------
-  const int col_l = lane & 15;
-  const int row_l = (lane >> 4) * 4;
+  // acc[i][j][e] = C[m = m0+wm0+16i+(lane&15)][n = n0+wn0+16j+4*(lane>>4)+e]: each lane owns
+  // 4 consecutive columns of one row -> 8-B (bf16x4) / 16-B (f32x4) vector stores.
+  const int mrow = lane & 15;
+  const int ncol = 4 * (lane >> 4);
+  float s1[RN][4], s2[RN][4];
 #pragma unroll
-  for (int j = 0; j < RN; ++j) {
-    const int n = n0 + wn0 + 16 * j + col_l;
-    const bool nok = n < p.N;
-    const float bias = (EPI == EPI_BF16 && p.bias && nok) ? p.bias[n] : 0.f;
-    float s1 = 0.f, s2 = 0.f;
+  for (int j = 0; j < RN; ++j)
 #pragma unroll
-    for (int i = 0; i < RM; ++i) {
+    for (int e = 0; e < 4; ++e) s1[j][e] = s2[j][e] = 0.f;
+  const bool vec_ok = (p.ldc % 4) == 0 && (!p.resid || (p.ldr % 4) == 0);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int m = m0 + wm0 + 16 * i + row_l + e;
-        if (m >= p.M || !nok) continue;
-        float v = acc[i][j][e] * p.alpha;
-        long off;
-        if (p.om.enabled) {
-          int nn, ii, jj;
-          pix_decompose((uint32_t)m, p.om.gh, p.om.gw, nn, ii, jj);
-          off = ((long)(nn * p.om.hy + ii * p.om.so + p.om.oh) * p.om.wy + jj * p.om.so + p.om.ow) * p.ldc + n;
-        } else {
-          off = (long)m * p.ldc + n;
+  for (int i = 0; i < RM; ++i) {
+    const int m = m0 + wm0 + 16 * i + mrow;
+    if (m >= p.M) continue;
+    long rowoff;
+    int nn = 0, ii = 0, jj = 0;
+    if (p.om.enabled) {
+      pix_decompose((uint32_t)m, p.om.gh, p.om.gw, nn, ii, jj);
+      rowoff = ((long)(nn * p.om.hy + ii * p.om.so + p.om.oh) * p.om.wy + jj * p.om.so + p.om.ow) * p.ldc;
+    } else {
+      rowoff = (long)m * p.ldc;
+    }
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      const int n = n0 + wn0 + 16 * j + ncol;
+      if (n >= p.N) continue;
+      const bool full = vec_ok && (n + 3 < p.N);
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * p.alpha;
+      if constexpr (EPI == EPI_BF16) {
+        if (p.bias) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += (n + e < p.N) ? p.bias[n + e] : 0.f;
         }
-        if constexpr (EPI == EPI_BF16) {
-          v += bias;
-          if (p.resid) v += bf2f(reinterpret_cast<const bf16_t*>(p.resid)[(long)m * p.ldr + n]);
-          if (p.relu) v = fmaxf(v, 0.f);
-          const bf16_t o = f2bf(v);
-          reinterpret_cast<bf16_t*>(p.c)[off] = o;
-          const float r = bf2f(o);
-          s1 += r;
-          s2 += r * r;
-        } else if constexpr (EPI == EPI_F32) {
-          float* c = reinterpret_cast<float*>(p.c);
-          c[off] = (p.beta != 0.f) ? v + p.beta * c[off] : v;
-        } else {
-          atomicAdd(reinterpret_cast<float*>(p.c) + off, v);
+        if (p.resid) {
+          const bf16_t* r = reinterpret_cast<const bf16_t*>(p.resid) + (long)m * p.ldr + n;
+          if (full) {
+            const uint2 rv = *reinterpret_cast<const uint2*>(r);
+            v[0] += __uint_as_float(rv.x << 16);
+            v[1] += __uint_as_float(rv.x & 0xffff0000u);
+            v[2] += __uint_as_float(rv.y << 16);
+            v[3] += __uint_as_float(rv.y & 0xffff0000u);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (n + e < p.N) v[e] += bf2f(r[e]);
+          }
         }
+        if (p.relu) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
+        bf16_t o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o[e] = f2bf(v[e]);
+          const float rr = (n + e < p.N) ? bf2f(o[e]) : 0.f;
+          s1[j][e] += rr;
+          s2[j][e] += rr * rr;
+        }
+        bf16_t* c = reinterpret_cast<bf16_t*>(p.c) + rowoff + n;
+        if (full) {
+          *reinterpret_cast<uint2*>(c) = make_uint2((uint32_t)o[0] | ((uint32_t)o[1] << 16),
+                                                    (uint32_t)o[2] | ((uint32_t)o[3] << 16));
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (n + e < p.N) c[e] = o[e];
+        }
+      } else if constexpr (EPI == EPI_F32) {
+        float* c = reinterpret_cast<float*>(p.c) + rowoff + n;
+        if (full && p.beta == 0.f) {
+          *reinterpret_cast<float4*>(c) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (n + e < p.N) c[e] = (p.beta != 0.f) ? v[e] + p.beta * c[e] : v[e];
+        }
+      } else {
+        float* c = reinterpret_cast<float*>(p.c) + rowoff + n;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (n + e < p.N) atomicAdd(c + e, v[e]);
       }
     }
     if constexpr (EPI == EPI_BF16) {
-      if (p.stats) {  // reduce over the 4 row-groups of the wave (lanes l, l^16, l^32, l^48)
-        s1 += __shfl_xor(s1, 16, 64);
-        s1 += __shfl_xor(s1, 32, 64);
-        s2 += __shfl_xor(s2, 16, 64);
-        s2 += __shfl_xor(s2, 32, 64);
-        if (lane < 16 && nok) {
-          float* st = p.stats + (long)(bid % kStatShards) * 2 * p.N;
-          atomicAdd(st + n, s1);
-          atomicAdd(st + p.N + n, s2);
+      if (p.om.enabled && p.om.zero_siblings) {  // this class is the only one with taps: zero the rest
+        bf16_t* cb = reinterpret_cast<bf16_t*>(p.c);
+        for (int a = 0; a < p.om.so; ++a) {
+          const int hy = ii * p.om.so + a;
+          if (hy >= p.om.hy) break;
+          for (int b = 0; b < p.om.so; ++b) {
+            const int wy = jj * p.om.so + b;
+            if (wy >= p.om.wy || (a == p.om.oh && b == p.om.ow)) continue;
+            bf16_t* z = cb + ((long)(nn * p.om.hy + hy) * p.om.wy + wy) * p.ldc;
+#pragma unroll
+            for (int j = 0; j < RN; ++j) {
+              const int n = n0 + wn0 + 16 * j + ncol;
+              if (n + 3 < p.N && vec_ok) *reinterpret_cast<uint2*>(z + n) = make_uint2(0, 0);
+              else
+                for (int e = 0; e < 4; ++e)
+                  if (n + e < p.N) z[n + e] = 0;
+            }
+          }
+        }
+      }
+    }
+  }
+  if constexpr (EPI == EPI_BF16) {
+    if (p.stats) {  // reduce over the 16 rows held by lanes sharing (lane>>4), then one atomic per column
+      float* st = p.stats + (long)(bid % kStatShards) * 2 * p.N;
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float a = s1[j][e], b = s2[j][e];
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) {
+            a += __shfl_xor(a, o, 64);
+            b += __shfl_xor(b, o, 64);
+          }
+          const int n = n0 + wn0 + 16 * j + ncol + e;
+          if (mrow == 0 && n < p.N) {
+            atomicAdd(st + n, a);
+            atomicAdd(st + p.N + n, b);
+          }
         }
       }
     }

@@ -19,15 +19,16 @@ int bn_finalize(const float* ws, long M, int C, const float* gamma, const float*
 // y = relu?(x*scale[c] + shift[c] + resid)
 int bn_apply(const void* x, const float* scale, const float* shift, const void* resid, void* y, long M, int C,
              int relu, hipStream_t s);
-// backward pass 1: dy' = dy * (y > 0 if relu) ; ws[shard][0][c] += sum dy', ws[shard][1][c] += sum dy'*xhat
-int bn_bwd_reduce(const void* dy, const void* x, const void* y, const float* mean, const float* invstd, float* ws,
-                  long M, int C, int relu, hipStream_t s);
-// pass 2: grads of gamma/beta (+=) and dx coefficients
-int bn_bwd_finalize(const float* ws, long M, int C, const float* gamma, const float* invstd, float* dgamma,
-                    float* dbeta, float* coef, hipStream_t s);
-// pass 3: dx = coef0[c]*(dy' - coef1[c] - xhat*coef2[c]);  optionally dres = dy' (masked)
-int bn_bwd_dx(const void* dy, const void* x, const void* y, const float* mean, const float* invstd,
-              const float* coef, void* dx, void* dres, long M, int C, int relu, hipStream_t s);
+// backward pass 1: dy' = dy * relu-mask ; ws[shard][0][c] += sum dy', ws[shard][1][c] += sum dy'*(x-mean)
+// mask mode: 0 none, 1 (y > 0) from the forward output, 2 (x*scale+shift > 0) recomputed from x
+int bn_bwd_reduce(const void* dy, const void* x, const void* y, const float* scale, const float* shift,
+                  const float* mean, float* ws, long M, int C, int mode, hipStream_t s);
+// pass 2: grads of gamma/beta (+=) and per-channel dx = A*dy' + B*x + K coefficients
+int bn_bwd_finalize(const float* ws, long M, int C, const float* gamma, const float* mean, const float* invstd,
+                    float* dgamma, float* dbeta, float* coef, hipStream_t s);
+// pass 3: dx = A*dy' + B*x + K;  optionally dres = dy' (masked gradient of the residual branch)
+int bn_bwd_dx(const void* dy, const void* x, const void* y, const float* scale, const float* shift,
+              const float* coef, void* dx, void* dres, long M, int C, int mode, hipStream_t s);
 
 // ---------------- pooling (NHWC) ----------------
 int maxpool_fwd(const void* x, void* y, uint8_t* argmax, int N, int H, int W, int C, int Ho, int Wo, int kh, int kw,

@@ -179,29 +179,68 @@ int bn_apply(const void* x, const float* scale, const float* shift, const void* 
   return (int)hipGetLastError();
 }
 
+// ReLU mask of the backward: mode 1 reads the forward output y (> 0), mode 2 recomputes
+// x*scale+shift > 0 from the BN input already in registers (no extra tensor read: the
+// forward computed the same fmaf on the same values).
+__device__ __forceinline__ void relu_mask(float* d, const float* xv, const uint4* __restrict__ y, long idx,
+                                          const float* sc, const float* sh, int mode) {
+  if (mode == 1) {
+    float yv[8];
+    unpack8(y[idx], yv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d[i] = yv[i] > 0.f ? d[i] : 0.f;
+  } else if (mode == 2) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d[i] = (xv[i] * sc[i] + sh[i]) > 0.f ? d[i] : 0.f;
+  }
+}
+
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint4* __restrict__ dy, const uint4* __restrict__ x,
-                                                             const uint4* __restrict__ y, const float* __restrict__ mean,
-                                                             float* ws, long M, int C, int relu) {
+                                                             const uint4* __restrict__ y, const float* __restrict__ scale,
+                                                             const float* __restrict__ shift,
+                                                             const float* __restrict__ mean, float* ws, long M, int C,
+                                                             int mode) {
   ColGeom g(C);
   float acc[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
   if (g.active) {
-    float mu[8];
+    float mu[8], sc[8], sh[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) mu[i] = mean[g.cv * 8 + i];
+    for (int i = 0; i < 8; ++i) {
+      mu[i] = mean[g.cv * 8 + i];
+      sc[i] = mode == 2 ? scale[g.cv * 8 + i] : 0.f;
+      sh[i] = mode == 2 ? shift[g.cv * 8 + i] : 0.f;
+    }
     const long step = (long)gridDim.x * g.RT;
-    for (long r = (long)blockIdx.x * g.RT + g.rt; r < M; r += step) {
+    long r = (long)blockIdx.x * g.RT + g.rt;
+    for (; r + step < M; r += 2 * step) {  // two rows of dy and x in flight per lane
+      const long i0 = r * g.CV + g.cv, i1 = (r + step) * g.CV + g.cv;
+      const uint4 d0 = dy[i0], x0 = x[i0], d1 = dy[i1], x1 = x[i1];
+      float d[8], xv[8];
+      unpack8(d0, d);
+      unpack8(x0, xv);
+      relu_mask(d, xv, y, i0, sc, sh, mode);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        acc[i] += d[i];
+        acc[8 + i] += d[i] * (xv[i] - mu[i]);
+      }
+      unpack8(d1, d);
+      unpack8(x1, xv);
+      relu_mask(d, xv, y, i1, sc, sh, mode);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        acc[i] += d[i];
+        acc[8 + i] += d[i] * (xv[i] - mu[i]);
+      }
+    }
+    for (; r < M; r += step) {
       const long idx = r * g.CV + g.cv;
       float d[8], xv[8];
       unpack8(dy[idx], d);
       unpack8(x[idx], xv);
-      if (relu) {
-        float yv[8];
-        unpack8(y[idx], yv);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) d[i] = yv[i] > 0.f ? d[i] : 0.f;
-      }
+      relu_mask(d, xv, y, idx, sc, sh, mode);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         acc[i] += d[i];
@@ -212,16 +251,17 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint4* __restr
   col_reduce_store(acc, g, ws, C);
 }
 
-int bn_bwd_reduce(const void* dy, const void* x, const void* y, const float* mean, const float* invstd, float* ws,
-                  long M, int C, int relu, hipStream_t s) {
-  (void)invstd;  // applied per channel in bn_bwd_finalize
+int bn_bwd_reduce(const void* dy, const void* x, const void* y, const float* scale, const float* shift,
+                  const float* mean, float* ws, long M, int C, int mode, hipStream_t s) {
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, col_grid(M, C), dim3(256), 0, s, (const uint4*)dy, (const uint4*)x,
-                     (const uint4*)y, mean, ws, M, C, relu);
+                     (const uint4*)y, scale, shift, mean, ws, M, C, mode);
   return (int)hipGetLastError();
 }
 
-__global__ void bn_bwd_finalize_kernel(const float* ws, long M, int C, const float* gamma, const float* invstd,
-                                       float* dgamma, float* dbeta, float* coef) {
+// coef[c] = A, coef[C+c] = B, coef[2C+c] = K with dx = A*dy' + B*x + K
+//   (= gamma*invstd * (dy' - mean(dy') - xhat * mean(dy'*xhat)))
+__global__ void bn_bwd_finalize_kernel(const float* ws, long M, int C, const float* gamma, const float* mean,
+                                       const float* invstd, float* dgamma, float* dbeta, float* coef) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   float s1 = 0.f, s2 = 0.f;
@@ -234,51 +274,61 @@ __global__ void bn_bwd_finalize_kernel(const float* ws, long M, int C, const flo
   if (dbeta) dbeta[c] += s1;
   if (dgamma) dgamma[c] += s2;
   const float g = gamma ? gamma[c] : 1.f;
-  coef[c] = g * inv;
-  coef[C + c] = s1 / (float)M;
-  coef[2 * C + c] = s2 / (float)M;
+  const float A = g * inv;
+  const float m1 = s1 / (float)M, m2 = s2 / (float)M;
+  coef[c] = A;
+  coef[C + c] = -A * m2 * inv;
+  coef[2 * C + c] = -A * m1 + A * m2 * inv * mean[c];
 }
 
-int bn_bwd_finalize(const float* ws, long M, int C, const float* gamma, const float* invstd, float* dgamma,
-                    float* dbeta, float* coef, hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, M, C, gamma, invstd, dgamma,
-                     dbeta, coef);
+int bn_bwd_finalize(const float* ws, long M, int C, const float* gamma, const float* mean, const float* invstd,
+                    float* dgamma, float* dbeta, float* coef, hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, M, C, gamma, mean, invstd,
+                     dgamma, dbeta, coef);
   return (int)hipGetLastError();
 }
 
 __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const uint4* __restrict__ dy, const uint4* __restrict__ x,
-                                                         const uint4* __restrict__ y, const float* __restrict__ mean,
-                                                         const float* __restrict__ invstd,
+                                                         const uint4* __restrict__ y, const float* __restrict__ scale,
+                                                         const float* __restrict__ shift,
                                                          const float* __restrict__ coef, uint4* __restrict__ dx,
-                                                         uint4* __restrict__ dres, long nvec, int CV, int relu) {
+                                                         uint4* __restrict__ dres, long nvec, int CV, int mode) {
   const int C = CV * 8;
   for (long v = (long)blockIdx.x * 256 + threadIdx.x; v < nvec; v += (long)gridDim.x * 256) {
     const int c = (int)(v % CV) * 8;
     float d[8], xv[8];
     unpack8(dy[v], d);
     unpack8(x[v], xv);
-    if (relu) {
-      float yv[8];
-      unpack8(y[v], yv);
+    if (mode) {
+      float sc[8], sh[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) d[i] = yv[i] > 0.f ? d[i] : 0.f;
+      for (int i = 0; i < 8; ++i) {
+        sc[i] = mode == 2 ? scale[c + i] : 0.f;
+        sh[i] = mode == 2 ? shift[c + i] : 0.f;
+      }
+      relu_mask(d, xv, y, v, sc, sh, mode);
     }
     if (dres) dres[v] = pack8(d);
+    const float4 a0 = *reinterpret_cast<const float4*>(coef + c), a1 = *reinterpret_cast<const float4*>(coef + c + 4);
+    const float4 b0 = *reinterpret_cast<const float4*>(coef + C + c),
+                 b1 = *reinterpret_cast<const float4*>(coef + C + c + 4);
+    const float4 k0 = *reinterpret_cast<const float4*>(coef + 2 * C + c),
+                 k1 = *reinterpret_cast<const float4*>(coef + 2 * C + c + 4);
+    const float A[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    const float B[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    const float K[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
     float o[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float xh = (xv[i] - mean[c + i]) * invstd[c + i];
-      o[i] = coef[c + i] * (d[i] - coef[C + c + i] - xh * coef[2 * C + c + i]);
-    }
+    for (int i = 0; i < 8; ++i) o[i] = A[i] * d[i] + B[i] * xv[i] + K[i];
     dx[v] = pack8(o);
   }
 }
 
-int bn_bwd_dx(const void* dy, const void* x, const void* y, const float* mean, const float* invstd, const float* coef,
-              void* dx, void* dres, long M, int C, int relu, hipStream_t s) {
+int bn_bwd_dx(const void* dy, const void* x, const void* y, const float* scale, const float* shift, const float* coef,
+              void* dx, void* dres, long M, int C, int mode, hipStream_t s) {
   const long nvec = M * (C >> 3);
   hipLaunchKernelGGL(bn_bwd_dx_kernel, dim3(ew_grid(nvec)), dim3(256), 0, s, (const uint4*)dy, (const uint4*)x,
-                     (const uint4*)y, mean, invstd, coef, (uint4*)dx, (uint4*)dres, nvec, C >> 3, relu);
+                     (const uint4*)y, scale, shift, coef, (uint4*)dx, (uint4*)dres, nvec, C >> 3, mode);
   return (int)hipGetLastError();
 }
 

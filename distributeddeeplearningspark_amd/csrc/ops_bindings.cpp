@@ -59,38 +59,45 @@ void bn_apply_(const at::Tensor& x, const at::Tensor& scale, const at::Tensor& s
                   x.numel() / C, (int)C, relu ? 1 : 0, cur_stream()));
 }
 
-void bn_bwd_reduce_(const at::Tensor& dy, const at::Tensor& x, c10::optional<at::Tensor> y, const at::Tensor& mean,
-                    const at::Tensor& ws, int64_t C) {
+// relu mask mode: 0 none; 1 from y (forward output); 2 recomputed from x*scale+shift
+void bn_bwd_reduce_(const at::Tensor& dy, const at::Tensor& x, c10::optional<at::Tensor> y,
+                    c10::optional<at::Tensor> scale, c10::optional<at::Tensor> shift, const at::Tensor& mean,
+                    const at::Tensor& ws, int64_t C, int64_t mode) {
   GPU(dy); BF16(dy); BF16(x); F32(mean); F32(ws);
   CK(dy.numel() == x.numel() && x.numel() % C == 0 && C % 8 == 0, "bn_bwd_reduce: shapes");
-  if (y) { BF16(*y); CK(y->numel() == x.numel(), "bn_bwd_reduce: y shape"); }
+  if (mode == 1) { CK(y.has_value(), "mode 1 needs y"); BF16(*y); CK(y->numel() == x.numel(), "bn_bwd_reduce: y shape"); }
+  if (mode == 2) { CK(scale.has_value() && shift.has_value(), "mode 2 needs scale/shift"); F32(*scale); F32(*shift); }
   CK(ws.numel() >= (int64_t)kBnShards * 2 * C, "bn_bwd_reduce: workspace too small");
   at::DeviceGuard g(x.device());
-  HIP_OK(bn_bwd_reduce(dy.data_ptr(), x.data_ptr(), optr<const void>(y), mean.data_ptr<float>(), nullptr,
-                       ws.data_ptr<float>(), x.numel() / C, (int)C, y ? 1 : 0, cur_stream()));
+  HIP_OK(bn_bwd_reduce(dy.data_ptr(), x.data_ptr(), optr<const void>(y), optr<const float>(scale),
+                       optr<const float>(shift), mean.data_ptr<float>(), ws.data_ptr<float>(), x.numel() / C, (int)C,
+                       (int)mode, cur_stream()));
 }
 
 void bn_bwd_finalize_(const at::Tensor& ws, int64_t M, int64_t C, c10::optional<at::Tensor> gamma,
-                      const at::Tensor& invstd, c10::optional<at::Tensor> dgamma, c10::optional<at::Tensor> dbeta,
-                      const at::Tensor& coef) {
-  GPU(ws); F32(ws); F32(invstd); F32(coef);
+                      const at::Tensor& mean, const at::Tensor& invstd, c10::optional<at::Tensor> dgamma,
+                      c10::optional<at::Tensor> dbeta, const at::Tensor& coef) {
+  GPU(ws); F32(ws); F32(mean); F32(invstd); F32(coef);
   CK(coef.numel() >= 3 * C, "bn_bwd_finalize: coef size");
   at::DeviceGuard g(ws.device());
-  HIP_OK(bn_bwd_finalize(ws.data_ptr<float>(), M, (int)C, optr<const float>(gamma), invstd.data_ptr<float>(),
-                         optr<float>(dgamma), optr<float>(dbeta), coef.data_ptr<float>(), cur_stream()));
+  HIP_OK(bn_bwd_finalize(ws.data_ptr<float>(), M, (int)C, optr<const float>(gamma), mean.data_ptr<float>(),
+                         invstd.data_ptr<float>(), optr<float>(dgamma), optr<float>(dbeta), coef.data_ptr<float>(),
+                         cur_stream()));
 }
 
-void bn_bwd_dx_(const at::Tensor& dy, const at::Tensor& x, c10::optional<at::Tensor> y, const at::Tensor& mean,
-                const at::Tensor& invstd, const at::Tensor& coef, const at::Tensor& dx, c10::optional<at::Tensor> dres,
-                int64_t C) {
-  GPU(dy); BF16(dy); BF16(x); BF16(dx); F32(mean); F32(invstd); F32(coef);
-  CK(dy.numel() == x.numel() && dx.numel() == x.numel() && x.numel() % C == 0, "bn_bwd_dx: shapes");
-  if (y) BF16(*y);
+void bn_bwd_dx_(const at::Tensor& dy, const at::Tensor& x, c10::optional<at::Tensor> y,
+                c10::optional<at::Tensor> scale, c10::optional<at::Tensor> shift, const at::Tensor& coef,
+                const at::Tensor& dx, c10::optional<at::Tensor> dres, int64_t C, int64_t mode) {
+  GPU(dy); BF16(dy); BF16(x); BF16(dx); F32(coef);
+  CK(dy.numel() == x.numel() && dx.numel() == x.numel() && x.numel() % C == 0 && C % 8 == 0, "bn_bwd_dx: shapes");
+  CK(coef.numel() >= 3 * C, "bn_bwd_dx: coef size");
+  if (mode == 1) { CK(y.has_value(), "mode 1 needs y"); BF16(*y); CK(y->numel() == x.numel(), "bn_bwd_dx: y shape"); }
+  if (mode == 2) { CK(scale.has_value() && shift.has_value(), "mode 2 needs scale/shift"); F32(*scale); F32(*shift); }
   if (dres) { BF16(*dres); CK(dres->numel() == x.numel(), "bn_bwd_dx: dres shape"); }
   at::DeviceGuard g(x.device());
-  HIP_OK(bn_bwd_dx(dy.data_ptr(), x.data_ptr(), optr<const void>(y), mean.data_ptr<float>(), invstd.data_ptr<float>(),
-                   coef.data_ptr<float>(), dx.data_ptr(), optr<void>(dres), x.numel() / C, (int)C, y ? 1 : 0,
-                   cur_stream()));
+  HIP_OK(bn_bwd_dx(dy.data_ptr(), x.data_ptr(), optr<const void>(y), optr<const float>(scale),
+                   optr<const float>(shift), coef.data_ptr<float>(), dx.data_ptr(), optr<void>(dres), x.numel() / C,
+                   (int)C, (int)mode, cur_stream()));
 }
 
 // ---------------------------------------------------------------- pooling

@@ -301,7 +301,10 @@ class Model(Layer):
 
     def backward_step(self, x, y):
         """zero grads -> forward -> loss -> backward (grads land in the arena). Returns loss tensor."""
+        from ..ops.norm import reset_workspaces
+
         self._ensure_placed()
+        reset_workspaces(self.device)
         self.arena.zero_grad()
         loss = self.compute_loss(x, y, training=True)
         loss.backward()

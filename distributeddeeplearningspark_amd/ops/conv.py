@@ -50,6 +50,8 @@ class ConvGeometry:
         self.implicit_fwd = Ci % 64 == 0 and self.T <= 64
         self.implicit_dgrad = Co % 64 == 0 and Ci % 8 == 0 and self.T <= 64
         self.implicit_wgrad = Ci % 64 == 0 and Co % 8 == 0 and self.T <= 64
+        self.gather8_fwd = (not self.implicit_fwd) and Ci % 8 == 0 and self.T <= 64
+        self.gather8_wgrad = (not self.implicit_wgrad) and Ci % 8 == 0 and Co % 8 == 0 and self.T <= 64
         self.kpad = math.ceil(self.T * Ci / 8) * 8
         self.fwd_geom = dict(n=N, hi=H, wi=W, c=Ci, ho=self.Ho, wo=self.Wo, sh=self.sh, sw=self.sw, tap_c=Ci,
                              dh=self.taps_h, dw=self.taps_w)
@@ -74,7 +76,13 @@ class ConvGeometry:
                         dw_.append(nw // self.sw)
                         wt.append(r * KW + s)
                 self.classes.append(dict(ph=ph, pw=pw, Hc=Hc, Wc=Wc, dh=dh_, dw=dw_, wt=wt))
-        self.dgrad_needs_zero = any(len(c["wt"]) == 0 for c in self.classes) or len(self.classes) < self.sh * self.sw
+        nonempty = [c for c in self.classes if c["wt"]]
+        # a single class with taps (1x1 / stride-s downsample): its epilogue zero-fills the
+        # other s*s-1 positions, so dX needs no separate memset
+        self.dgrad_zero_siblings = (len(nonempty) == 1 and (self.sh > 1 or self.sw > 1) and self.sh == self.sw
+                                    and len(self.classes) == self.sh * self.sw)
+        self.dgrad_needs_zero = (not self.dgrad_zero_siblings) and (
+            any(len(c["wt"]) == 0 for c in self.classes) or len(self.classes) < self.sh * self.sw)
 
 
 @lru_cache(maxsize=4096)
@@ -94,9 +102,9 @@ def conv_fwd_native(x, w, g: ConvGeometry, bias=None, relu=False, stats=None):
     y2 = y.view(g.M, g.Co)
     if g.is_pointwise:
         G.linear_fwd(x.view(g.M, g.Ci), w.view(g.Co, g.Ci), bias=bias, relu=relu, out=y2, stats=stats)
-    elif g.implicit_fwd:
-        G.gemm(x, w, y2, g.M, g.Co, g.T * g.Ci, G.KC_GATHER, G.KC, 0, g.T * g.Ci, g.Co, G.EPI_BF16, bias=bias,
-               relu=relu, geom=g.fwd_geom, stats=stats)
+    elif g.implicit_fwd or g.gather8_fwd:
+        G.gemm(x, w, y2, g.M, g.Co, g.T * g.Ci, G.KC_GATHER if g.implicit_fwd else G.KC_GATHER8, G.KC, 0,
+               g.T * g.Ci, g.Co, G.EPI_BF16, bias=bias, relu=relu, geom=g.fwd_geom, stats=stats)
     else:
         col = _im2col(x, g, g.taps_h, g.taps_w, g.Ho, g.Wo, g.sh, g.sw, g.kpad)
         w2 = w.reshape(g.Co, g.T * g.Ci)
@@ -123,7 +131,8 @@ def conv_dgrad_native(dy, w, g: ConvGeometry, resid=None):
         Mc = g.N * cl["Hc"] * cl["Wc"]
         om = None
         if strided:
-            om = dict(gh=cl["Hc"], gw=cl["Wc"], hy=g.H, wy=g.W, so=g.sh, oh=cl["ph"], ow=cl["pw"])
+            om = dict(gh=cl["Hc"], gw=cl["Wc"], hy=g.H, wy=g.W, so=g.sh, oh=cl["ph"], ow=cl["pw"],
+                      zero=int(g.dgrad_zero_siblings))
         r = None if (resid is None or strided) else resid.view(-1, g.Ci)
         if g.implicit_dgrad:
             geom = dict(n=g.N, hi=g.Ho, wi=g.Wo, c=g.Co, ho=cl["Hc"], wo=cl["Wc"], sh=1, sw=1, tap_c=g.Co,
@@ -154,6 +163,9 @@ def conv_wgrad_native(dy, x, g: ConvGeometry, gw):
     elif g.implicit_wgrad:
         G.gemm(dy, x, gw2, g.Co, g.T * g.Ci, g.M, G.RC, G.RC_GATHER, g.Co, 0, g.T * g.Ci, G.EPI_F32, beta=1.0,
                geom=g.fwd_geom, bn_cap=min(128, g.Ci))
+    elif g.gather8_wgrad:
+        G.gemm(dy, x, gw2, g.Co, g.T * g.Ci, g.M, G.RC, G.RC_GATHER8, g.Co, 0, g.T * g.Ci, G.EPI_F32, beta=1.0,
+               geom=g.fwd_geom)
     else:
         col = _im2col(x, g, g.taps_h, g.taps_w, g.Ho, g.Wo, g.sh, g.sw, g.kpad)
         if g.kpad == g.T * g.Ci:
@@ -181,9 +193,16 @@ class _Conv2dFn(torch.autograd.Function):
         Co, KH, KW, _ = w.shape
         ctx.cfg = cfg
         ctx.native = use_native(x)
+        ctx.ci = Ci
         if ctx.native:
+            x = x.contiguous()
+            if Ci % 8:  # 16-B vector granularity: pad channels (stem: 3 -> 8) with zeros
+                cp = -(-Ci // 8) * 8
+                x = F.pad(x, (0, cp - Ci))
+                w = F.pad(w.detach(), (0, cp - Ci))
+                Ci = cp
             g = geometry(N, H, W, Ci, Co, KH, KW, stride, pad, dil)
-            y = conv_fwd_native(x.contiguous(), w, g, bias=b, relu=relu, stats=stats)
+            y = conv_fwd_native(x, w, g, bias=b, relu=relu, stats=stats)
             ctx.g = g
         else:
             y = conv_ref(x, w.to(x.dtype), None if b is None else b.to(x.dtype), stride, pad, dil, relu)
@@ -207,10 +226,18 @@ class _Conv2dFn(torch.autograd.Function):
                 dy = d2
             if gb is not None:
                 C().bias_grad(dy, gb, g.Co, True)
+            padded = g.Ci != ctx.ci
             if gw is not None:
-                conv_wgrad_native(dy, x, g, gw)
+                if padded:
+                    tmp = torch.zeros((g.Co, g.KH, g.KW, g.Ci), dtype=torch.float32, device=dy.device)
+                    conv_wgrad_native(dy, x, g, tmp)
+                    gw.add_(tmp[..., : ctx.ci])
+                else:
+                    conv_wgrad_native(dy, x, g, gw)
             if ctx.needs_dx:
                 dx = conv_dgrad_native(dy, w, g)
+                if padded:
+                    dx = dx[..., : ctx.ci].contiguous()
         else:
             fn = lambda xx, ww, bb: conv_ref(xx, ww, bb, stride, pad, dil, relu)
             bb = None if b is None else b.to(x.dtype)

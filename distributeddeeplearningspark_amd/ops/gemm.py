@@ -16,7 +16,7 @@ import torch
 
 from ._native import C
 
-KC, RC, KC_GATHER, RC_GATHER, RC_TAPS = 0, 1, 2, 3, 4
+KC, RC, KC_GATHER, RC_GATHER, RC_TAPS, KC_GATHER8, RC_GATHER8 = 0, 1, 2, 3, 4, 5, 6
 EPI_BF16, EPI_F32, EPI_F32_ATOMIC = 0, 1, 2
 _TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64)}
 _CU = 256

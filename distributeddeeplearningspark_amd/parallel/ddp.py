@@ -134,7 +134,10 @@ class DataParallel:
                     self.pg.broadcast_(t, src)
 
     def train_step(self, x, y):
+        from ..ops.norm import reset_workspaces
+
         m = self.model
+        reset_workspaces(m.device)
         m.arena.zero_grad()
         if self.overlap:
             self._begin()
