@@ -258,7 +258,12 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams
 #pragma unroll
       for (int i = 0; i < RM; ++i)
 #pragma unroll
-        for (int j = 0; j < RN; ++j) acc[i][j] = mfma16x16x32(bf[j], af[i], acc[i][j]);  // D^T: 4 consecutive n per lane
+        for (int j = 0; j < RN; ++j) {
+          if constexpr (EPI == EPI_BF16)
+            acc[i][j] = mfma16x16x32(bf[j], af[i], acc[i][j]);  // D^T: 4 consecutive n per lane (vector stores)
+          else
+            acc[i][j] = mfma16x16x32(af[i], bf[j], acc[i][j]);  // D: 16 consecutive n per row (coalesced atomics)
+        }
     }
     if (more) {
       A.store(odd ? lds_a0 : lds_a1);
@@ -268,6 +273,28 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams
   }
 
   // ---------------------------------- epilogue ----------------------------------
+  if constexpr (EPI != EPI_BF16) {
+    // fp32 (weight-gradient) epilogue, D orientation: acc[i][j][e] = C[m0+wm0+16i+4(lane>>4)+e][n0+wn0+16j+(lane&15)]
+    // -> each atomic wave-instruction covers 4 rows x 64 contiguous bytes.
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      const int n = n0 + wn0 + 16 * j + (lane & 15);
+      if (n >= p.N) continue;
+#pragma unroll
+      for (int i = 0; i < RM; ++i) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int m = m0 + wm0 + 16 * i + 4 * (lane >> 4) + e;
+          if (m >= p.M) continue;
+          float* c = reinterpret_cast<float*>(p.c) + (long)m * p.ldc + n;
+          const float v = acc[i][j][e] * p.alpha;
+          if constexpr (EPI == EPI_F32) *c = (p.beta != 0.f) ? v + p.beta * *c : v;
+          else atomicAdd(c, v);
+        }
+      }
+    }
+    return;
+  }
   // acc[i][j][e] = C[m = m0+wm0+16i+(lane&15)][n = n0+wn0+16j+4*(lane>>4)+e]: each lane owns
   // 4 consecutive columns of one row -> 8-B (bf16x4) / 16-B (f32x4) vector stores.
   const int mrow = lane & 15;

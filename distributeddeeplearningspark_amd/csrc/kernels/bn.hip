@@ -142,40 +142,65 @@ int bn_finalize(const float* ws, long M, int C, const float* gamma, const float*
   return (int)hipGetLastError();
 }
 
+__device__ __forceinline__ void load8f(const float* p, float* f) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
+  f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+
+// Streaming sweeps use the column-fixed mapping of ColGeom: a lane keeps ONE 8-channel
+// vector (per-channel parameters live in registers, no per-element index division) and
+// walks rows; two rows are in flight per lane.
 __global__ __launch_bounds__(256) void bn_apply_kernel(const uint4* __restrict__ x, const float* __restrict__ scale,
                                                         const float* __restrict__ shift, const uint4* __restrict__ res,
-                                                        uint4* __restrict__ y, long nvec, int CV, int relu) {
-  for (long v = (long)blockIdx.x * 256 + threadIdx.x; v < nvec; v += (long)gridDim.x * 256) {
-    const int c = (int)(v % CV) * 8;
-    float f[8], r[8];
-    unpack8(x[v], f);
-    if (res) unpack8(res[v], r);
-    const float4 s0 = *reinterpret_cast<const float4*>(scale + c), s1 = *reinterpret_cast<const float4*>(scale + c + 4);
-    const float4 h0 = *reinterpret_cast<const float4*>(shift + c), h1 = *reinterpret_cast<const float4*>(shift + c + 4);
-    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      float o = f[i] * sc[i] + sh[i];
-      if (res) o += r[i];
-      if (relu) o = fmaxf(o, 0.f);
-      f[i] = o;
+                                                        uint4* __restrict__ y, long M, int C, int relu) {
+  ColGeom g(C);
+  if (!g.active) return;
+  float sc[8], sh[8];
+  load8f(scale + g.cv * 8, sc);
+  load8f(shift + g.cv * 8, sh);
+  const long step = (long)gridDim.x * g.RT;
+  for (long r = (long)blockIdx.x * g.RT + g.rt; r < M; r += 2 * step) {
+    const bool two = r + step < M;
+    const long i0 = r * g.CV + g.cv, i1 = (r + step) * g.CV + g.cv;
+    const uint4 x0 = x[i0];
+    const uint4 x1 = two ? x[i1] : x0;
+    uint4 r0 = x0, r1 = x0;
+    if (res) {
+      r0 = res[i0];
+      r1 = two ? res[i1] : r0;
     }
-    y[v] = pack8(f);
+    float f[8], q[8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1 && !two) break;
+      unpack8(h ? x1 : x0, f);
+      if (res) unpack8(h ? r1 : r0, q);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float o = f[i] * sc[i] + sh[i];
+        if (res) o += q[i];
+        if (relu) o = fmaxf(o, 0.f);
+        f[i] = o;
+      }
+      y[h ? i1 : i0] = pack8(f);
+    }
   }
 }
 
-static unsigned ew_grid(long nvec) {
-  long g = (nvec + 255) / 256;
-  if (g > 8192) g = 8192;
-  return (unsigned)(g > 0 ? g : 1);
+static dim3 stream_grid(long M, int C) {
+  const int CV = C >> 3, CT = CV < 256 ? CV : 256, RT = 256 / CT;
+  const int gy = (CV + CT - 1) / CT;
+  long gx = (M + 2 * RT - 1) / (2 * RT);
+  const long cap = 4096 / gy > 1 ? 4096 / gy : 1;
+  if (gx > cap) gx = cap;
+  return dim3((unsigned)(gx > 0 ? gx : 1), (unsigned)gy);
 }
 
 int bn_apply(const void* x, const float* scale, const float* shift, const void* resid, void* y, long M, int C, int relu,
              hipStream_t s) {
-  const long nvec = M * (C >> 3);
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(nvec)), dim3(256), 0, s, (const uint4*)x, scale, shift,
-                     (const uint4*)resid, (uint4*)y, nvec, C >> 3, relu);
+  hipLaunchKernelGGL(bn_apply_kernel, stream_grid(M, C), dim3(256), 0, s, (const uint4*)x, scale, shift,
+                     (const uint4*)resid, (uint4*)y, M, C, relu);
   return (int)hipGetLastError();
 }
 
@@ -292,43 +317,47 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const uint4* __restrict_
                                                          const uint4* __restrict__ y, const float* __restrict__ scale,
                                                          const float* __restrict__ shift,
                                                          const float* __restrict__ coef, uint4* __restrict__ dx,
-                                                         uint4* __restrict__ dres, long nvec, int CV, int mode) {
-  const int C = CV * 8;
-  for (long v = (long)blockIdx.x * 256 + threadIdx.x; v < nvec; v += (long)gridDim.x * 256) {
-    const int c = (int)(v % CV) * 8;
-    float d[8], xv[8];
-    unpack8(dy[v], d);
-    unpack8(x[v], xv);
-    if (mode) {
-      float sc[8], sh[8];
+                                                         uint4* __restrict__ dres, long M, int C, int mode) {
+  ColGeom g(C);
+  if (!g.active) return;
+  const int c = g.cv * 8;
+  float A[8], B[8], K[8], sc[8], sh[8];
+  load8f(coef + c, A);
+  load8f(coef + C + c, B);
+  load8f(coef + 2 * C + c, K);
+  if (mode == 2) {
+    load8f(scale + c, sc);
+    load8f(shift + c, sh);
+  } else {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        sc[i] = mode == 2 ? scale[c + i] : 0.f;
-        sh[i] = mode == 2 ? shift[c + i] : 0.f;
-      }
-      relu_mask(d, xv, y, v, sc, sh, mode);
+    for (int i = 0; i < 8; ++i) sc[i] = sh[i] = 0.f;
+  }
+  const long step = (long)gridDim.x * g.RT;
+  for (long r = (long)blockIdx.x * g.RT + g.rt; r < M; r += 2 * step) {
+    const bool two = r + step < M;
+    const long i0 = r * g.CV + g.cv, i1 = (r + step) * g.CV + g.cv;
+    const uint4 d0 = dy[i0], x0 = x[i0];
+    const uint4 d1 = two ? dy[i1] : d0, x1 = two ? x[i1] : x0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1 && !two) break;
+      const long idx = h ? i1 : i0;
+      float d[8], xv[8], o[8];
+      unpack8(h ? d1 : d0, d);
+      unpack8(h ? x1 : x0, xv);
+      relu_mask(d, xv, y, idx, sc, sh, mode);
+      if (dres) dres[idx] = pack8(d);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = A[i] * d[i] + B[i] * xv[i] + K[i];
+      dx[idx] = pack8(o);
     }
-    if (dres) dres[v] = pack8(d);
-    const float4 a0 = *reinterpret_cast<const float4*>(coef + c), a1 = *reinterpret_cast<const float4*>(coef + c + 4);
-    const float4 b0 = *reinterpret_cast<const float4*>(coef + C + c),
-                 b1 = *reinterpret_cast<const float4*>(coef + C + c + 4);
-    const float4 k0 = *reinterpret_cast<const float4*>(coef + 2 * C + c),
-                 k1 = *reinterpret_cast<const float4*>(coef + 2 * C + c + 4);
-    const float A[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-    const float B[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-    const float K[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
-    float o[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) o[i] = A[i] * d[i] + B[i] * xv[i] + K[i];
-    dx[v] = pack8(o);
   }
 }
 
 int bn_bwd_dx(const void* dy, const void* x, const void* y, const float* scale, const float* shift, const float* coef,
               void* dx, void* dres, long M, int C, int mode, hipStream_t s) {
-  const long nvec = M * (C >> 3);
-  hipLaunchKernelGGL(bn_bwd_dx_kernel, dim3(ew_grid(nvec)), dim3(256), 0, s, (const uint4*)dy, (const uint4*)x,
-                     (const uint4*)y, scale, shift, coef, (uint4*)dx, (uint4*)dres, nvec, C >> 3, mode);
+  hipLaunchKernelGGL(bn_bwd_dx_kernel, stream_grid(M, C), dim3(256), 0, s, (const uint4*)dy, (const uint4*)x,
+                     (const uint4*)y, scale, shift, coef, (uint4*)dx, (uint4*)dres, M, C, mode);
   return (int)hipGetLastError();
 }
 

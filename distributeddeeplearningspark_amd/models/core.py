@@ -370,6 +370,8 @@ class Model(Layer):
 
     def get_weights(self) -> list[np.ndarray]:
         self.build_model()
+        if self.arena is None:  # materialise the initial weights (host memory, no GPU touch)
+            self.place("cpu")
         out = []
         for l in self.weight_layers():
             if l.keras_weight_params():
@@ -461,12 +463,43 @@ class Sequential(Model):
         return getattr(last, "activation_name", None) == "softmax"
 
     def forward(self, x, training=False, logits=False):
-        n = len(self.layers)
-        for i, l in enumerate(self.layers):
+        """Runs the layers with graph-level fusions: Conv2D/Dense + Activation('relu') ->
+        ReLU epilogue; Conv2D -> BatchNormalization -> relu: BN statistics accumulated in
+        the conv epilogue and ReLU fused into the BN apply; final softmax skipped when the
+        loss is the fused softmax-cross-entropy (``logits=True``)."""
+        from ..ops._native import use_native
+        from ..ops.norm import new_stats_workspace
+        from .layers import Activation, BatchNormalization, Conv2D, Dense
+
+        L = self.layers
+        n = len(L)
+        i = 0
+        while i < n:
+            l = L[i]
+            nxt = L[i + 1] if i + 1 < n else None
+            nxt2 = L[i + 2] if i + 2 < n else None
             if logits and i == n - 1 and getattr(l, "activation_name", None) == "softmax":
-                x = l.call(x, training, skip_activation=True) if hasattr(l, "supports_skip") else x
+                if hasattr(l, "supports_skip"):
+                    x = l.call(x, training, skip_activation=True)
                 break
+            relu_next = isinstance(nxt, Activation) and nxt.activation_name == "relu"
+            if isinstance(l, Conv2D) and l.activation_name == "linear" and isinstance(nxt, BatchNormalization):
+                stats = new_stats_workspace(l.filters, x.device) if (training and use_native(x)) else None
+                y = l.call(x, training, stats=stats)
+                relu2 = isinstance(nxt2, Activation) and nxt2.activation_name == "relu"
+                x = nxt.call(y, training, relu=relu2, stats=stats)
+                i += 3 if relu2 else 2
+                continue
+            if relu_next and isinstance(l, (Conv2D, Dense)) and l.activation_name == "linear":
+                x = l.call(x, training, relu=True)
+                i += 2
+                continue
+            if relu_next and isinstance(l, BatchNormalization):
+                x = l.call(x, training, relu=True)
+                i += 2
+                continue
             x = l.call(x, training)
+            i += 1
         return x
 
     def get_config(self):

@@ -1,0 +1,160 @@
+"""Worker launcher: the Spark driver -> executor step of the reference, one OS process per
+data-parallel worker (one per MI355X on a GPU node).
+
+Three modes, chosen automatically:
+  * SPMD  — the job was started by ``torchrun`` (WORLD_SIZE > 1 in the env): every rank
+            already runs the driver program; each trains its own partition in-process.
+  * local — ``num_workers == 1``: run in the calling process (SingleTrainer, tests).
+  * spawn — the driver spawns ``num_workers`` fresh interpreters (multiprocessing
+            "spawn": a child process started with fork+exec, never an exec of the
+            driver itself), each binding GPU ``rank % n_gpus`` (RCCL) or the CPU (gloo),
+            rendezvousing on a TCP store at 127.0.0.1:<free port>.
+Failures in any worker abort the others and re-raise the worker traceback in the driver
+(Spark would retry the task; here a training job is all-or-nothing — see utils/fault.py
+for checkpoint-based restart).
+"""
+from __future__ import annotations
+
+import os
+import socket
+import time
+import traceback
+
+
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _gpu_count() -> int:
+    try:
+        import torch
+
+        return torch.cuda.device_count()  # does not initialise the HIP runtime on this image
+    except Exception:
+        return 0
+
+
+def plan_devices(num_workers: int, device: str | None = None) -> list[str]:
+    if device is None:
+        device = os.environ.get("DDL_DEVICE", "auto")
+    n = _gpu_count()
+    if device == "cpu" or (device == "auto" and n == 0):
+        return ["cpu"] * num_workers
+    if num_workers > n:
+        raise ValueError(f"{num_workers} workers requested but only {n} GPUs: one worker per MI355X "
+                         "(pass device='cpu' to run the workers on CPU executors)")
+    return [f"cuda:{i}" for i in range(num_workers)]
+
+
+def _child_main(payload_path: str, result_path: str):
+    """Entry point of a worker process (``python -m ...parallel.launcher payload result``)."""
+    import pickle
+
+    with open(payload_path, "rb") as f:
+        fn, rank, world, port, device, args, threads = pickle.load(f)
+    try:
+        import torch
+
+        torch.set_num_threads(max(1, threads))
+        from .comm import init_process_group
+
+        pg = init_process_group(rank, world, "127.0.0.1", port, device=device, timeout_s=600.0)
+        res = fn(rank, world, pg, *args)
+        out = ("ok", res)
+        pg.shutdown()
+    except BaseException:  # report every failure to the driver
+        out = ("error", traceback.format_exc())
+    tmp = result_path + ".tmp"
+    with open(tmp, "wb") as f:
+        pickle.dump(out, f, protocol=pickle.HIGHEST_PROTOCOL)
+    os.replace(tmp, result_path)
+
+
+def run_workers(fn, num_workers: int, args_per_rank, device: str | None = None, timeout_s: float = 3600.0):
+    """Run ``fn(rank, world, pg, *args_per_rank[rank])`` on ``num_workers`` workers, return results by rank."""
+    from . import comm
+
+    env_world = int(os.environ.get("WORLD_SIZE", "1"))
+    if env_world > 1:  # SPMD under torchrun
+        pg = comm.default_group() or comm.init_from_env()
+        if pg.world_size != num_workers:
+            raise ValueError(f"torchrun world size {pg.world_size} != num_workers {num_workers}")
+        res = fn(pg.rank, pg.world_size, pg, *args_per_rank[pg.rank])
+        return pg.all_gather_object(res)
+    devices = plan_devices(num_workers, device)
+    if num_workers == 1:
+        import torch
+
+        dev = torch.device(devices[0])
+        if dev.type == "cuda":
+            torch.cuda.set_device(dev)
+        pg = comm.ProcessGroup(0, 1, 0, dev, None)
+        return [fn(0, 1, pg, *args_per_rank[0])]
+    # Fresh interpreters started as child processes (no re-import of the driver's __main__,
+    # so reference-style scripts without an ``if __name__ == "__main__"`` guard work).
+    import pickle
+    import subprocess
+    import sys
+    import tempfile
+
+    port = free_port()
+    threads = max(1, (os.cpu_count() or 2) // num_workers)
+    tmpdir = tempfile.mkdtemp(prefix="ddl_workers_")
+    procs, res_paths = [], []
+    env = dict(os.environ)
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    for r in range(num_workers):
+        pp, rp = os.path.join(tmpdir, f"in{r}.pkl"), os.path.join(tmpdir, f"out{r}.pkl")
+        with open(pp, "wb") as f:
+            pickle.dump((fn, r, num_workers, port, devices[r], args_per_rank[r], threads), f,
+                        protocol=pickle.HIGHEST_PROTOCOL)
+        procs.append(subprocess.Popen([sys.executable, "-m", "distributeddeeplearningspark_amd.parallel.launcher",
+                                       pp, rp], env=env))
+        res_paths.append(rp)
+    results, errors = {}, {}
+    deadline = time.time() + timeout_s
+    try:
+        while len(results) + len(errors) < num_workers:
+            progressed = False
+            for r, (p, rp) in enumerate(zip(procs, res_paths)):
+                if r in results or r in errors:
+                    continue
+                if os.path.exists(rp):
+                    with open(rp, "rb") as f:
+                        status, payload = pickle.load(f)
+                    (results if status == "ok" else errors)[r] = payload
+                    progressed = True
+                elif p.poll() is not None:
+                    errors[r] = f"worker {r} exited with code {p.returncode} without a result"
+                    progressed = True
+            if errors:
+                break
+            if time.time() > deadline:
+                raise TimeoutError(f"workers did not finish within {timeout_s}s")
+            if not progressed:
+                time.sleep(0.05)
+    finally:
+        for p in procs:
+            if errors and p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=60)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        import shutil
+
+        shutil.rmtree(tmpdir, ignore_errors=True)
+    if errors:
+        r = sorted(errors)[0]
+        raise RuntimeError(f"worker {r} failed:\n{errors[r]}")
+    return [results[r] for r in range(num_workers)]
+
+
+if __name__ == "__main__":
+    import sys as _sys
+
+    _child_main(_sys.argv[1], _sys.argv[2])

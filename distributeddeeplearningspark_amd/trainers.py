@@ -1,0 +1,507 @@
+"""dist-keras trainers (``distkeras.trainers``) on MI355X data parallelism.
+
+Constructor kwargs and the observable surface are the reference's
+(``ddl_mnist_aztk.py:216-224``, ``ddl_nyiso_aztk.py:207-218``):
+``ADAG(keras_model, worker_optimizer, loss, num_workers, batch_size,
+communication_window, num_epoch, features_col, label_col).train(df)`` returns the
+trained model; ``trainer.parameter_server.num_updates`` and
+``trainer.get_training_time()`` are reported afterwards.
+
+Execution (MI355X-native, not a socket parameter server):
+  * ``train(df)`` repartitions the frame into ``num_workers`` shards and starts one
+    process per worker (= per GPU, ``parallel/launcher.py``).  Each worker rebuilds the
+    model from the serialised ``{'model', 'weights'}`` blob, keeps its shard resident in
+    HBM, and trains with its own worker-local optimizer on bf16 HIP kernels.
+  * The dist-keras commit/pull protocol becomes a synchronous **periodic delta
+    all-reduce over RCCL**: every ``communication_window`` mini-batches all workers
+    all-reduce their window-normalised weight delta and continue from the new center
+    variable.  ``num_updates`` follows the reference's update law
+    ``sum_w floor(num_epoch * floor(rows_w / batch_size) / communication_window)``
+    (1425 for the NYISO config); workers that run out of windows keep
+    joining the collective with a zero delta so shards of unequal size cannot deadlock.
+  * Semantics per algorithm (center c, worker weights W, window k, rank order r):
+      ADAG      c += sum_w (W_w - c) / k                       ; W <- c
+      DynSGD    c += sum_w (W_w - c) / (s_w + 1)               ; W <- c   (s_w = staleness
+                emulated as the number of workers committing before w in the round)
+      DOWNPOUR  c += sum_w (W_w - c)                           ; W <- c
+      (A)EASGD / EAMSGD  E_w = alpha (W_w - c); W_w -= E_w; c += sum_w E_w   (elastic)
+      AveragingTrainer   independent training, c = mean_w W_w at the end
+      EnsembleTrainer    independent models, all returned
+      SingleTrainer      one worker on the coalesced frame
+      SynchronousDataParallel (new)  per-step bucketed gradient all-reduce, overlapped
+    These are the synchronous equivalents of dist-keras' asynchronous commits
+    (documented deviation: no stale updates are applied).
+"""
+from __future__ import annotations
+
+import copy
+import time
+
+import numpy as np
+import torch
+
+from .models import optimizers as opt_mod
+from .parallel.launcher import run_workers
+from .utils import deserialize_keras_model, get_states, serialize_keras_model, set_states
+
+
+# =============================================================================================
+#                                    worker side
+# =============================================================================================
+def _to_device(a: np.ndarray, model):
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if t.is_floating_point():
+        return t.to(model.device, model.compute_dtype)
+    return t.to(model.device)
+
+
+class _Worker:
+    def __init__(self, cfg, model, pg, sizes):
+        self.cfg, self.model, self.pg, self.sizes = cfg, model, pg, sizes
+        bs, E = cfg["batch_size"], cfg["num_epoch"]
+        self.k = max(1, int(cfg.get("communication_window", 1)))
+        self.steps_all = [E * (s // bs) for s in sizes]
+        self.commits_all = [st // self.k for st in self.steps_all]
+        self.rounds = max(self.commits_all) if self.commits_all else 0
+        self.history: list[float] = []
+
+    @property
+    def arena(self):
+        return self.model.arena
+
+    def batches(self, X, Y):
+        bs = self.cfg["batch_size"]
+        n = X.shape[0] // bs  # trailing partial batch dropped (dist-keras worker behaviour)
+        for _ in range(self.cfg["num_epoch"]):
+            for b in range(n):
+                yield X[b * bs:(b + 1) * bs], Y[b * bs:(b + 1) * bs]
+
+    def num_updates(self) -> int:
+        return int(sum(self.commits_all))
+
+    def run(self, X, Y):
+        raise NotImplementedError
+
+
+class _CommitWorker(_Worker):
+    """Periodic commit rounds (ADAG / DynSGD / DOWNPOUR / EASGD family)."""
+
+    rule = "adag"
+
+    def run(self, X, Y):
+        a = self.arena
+        center = a.master.detach().clone()
+        it = rnd = 0
+        for xb, yb in self.batches(X, Y):
+            self.history.append(self.model.train_on_batch(xb, yb))
+            it += 1
+            if it % self.k == 0 and rnd < self.rounds:
+                self.commit(center, rnd)
+                rnd += 1
+        while rnd < self.rounds:  # my shard is exhausted: join the remaining rounds with a zero delta
+            self.commit(center, rnd)
+            rnd += 1
+        return center
+
+    def _contributors(self, rnd):
+        return [r for r, c in enumerate(self.commits_all) if rnd < c]
+
+    def commit(self, center, rnd):
+        a, pg = self.arena, self.pg
+        contrib = self._contributors(rnd)
+        mine = pg.rank in contrib
+        W = a.master.detach()
+        rule = self.rule
+        with torch.no_grad():
+            if rule in ("easgd", "aeasgd", "eamsgd"):
+                e = (W - center) * self.cfg["alpha"] if mine else torch.zeros_like(W)
+                if mine:
+                    W.sub_(e)
+                self._allreduce(e)
+                center.add_(e)
+                a.sync_compute()
+                return
+            d = (W - center) if mine else torch.zeros_like(W)
+            if rule == "adag":
+                d.div_(self.k)
+            elif rule == "dynsgd" and mine:
+                staleness = contrib.index(pg.rank)  # workers committing before me in this round
+                d.div_(staleness + 1)
+            self._allreduce(d)
+            center.add_(d)
+            W.copy_(center)
+            a.sync_compute()
+
+    def _allreduce(self, t):
+        if self.pg.distributed:
+            from .parallel.ddp import DataParallel
+
+            DataParallel.all_reduce_flat_(_FlatReducer(self.pg), t)
+
+
+class _FlatReducer:
+    """Minimal object to reuse DataParallel.all_reduce_flat_ without hooks."""
+
+    def __init__(self, pg):
+        self.pg = pg
+        self.bucket_bytes = 64 << 20
+
+
+class _AdagWorker(_CommitWorker):
+    rule = "adag"
+
+
+class _DynSGDWorker(_CommitWorker):
+    rule = "dynsgd"
+
+
+class _DownpourWorker(_CommitWorker):
+    rule = "downpour"
+
+
+class _EASGDWorker(_CommitWorker):
+    rule = "easgd"
+
+
+class _AveragingWorker(_Worker):
+    def num_updates(self):
+        return 1
+
+    def run(self, X, Y):
+        for xb, yb in self.batches(X, Y):
+            self.history.append(self.model.train_on_batch(xb, yb))
+        W = self.arena.master.detach()
+        with torch.no_grad():
+            if self.pg.distributed:
+                _CommitWorker._allreduce(self, W)
+                W.div_(self.pg.world_size)
+            self.arena.sync_compute()
+        return W.clone()
+
+
+class _EnsembleWorker(_Worker):
+    def num_updates(self):
+        return 0
+
+    def run(self, X, Y):
+        for xb, yb in self.batches(X, Y):
+            self.history.append(self.model.train_on_batch(xb, yb))
+        return self.arena.master.detach().clone()
+
+
+class _SyncDPWorker(_Worker):
+    """Per-step synchronous data parallelism (bucketed RCCL all-reduce overlapped with backward)."""
+
+    def __init__(self, cfg, model, pg, sizes):
+        super().__init__(cfg, model, pg, sizes)
+        self.steps = min(self.steps_all) if self.steps_all else 0
+
+    def num_updates(self):
+        return self.steps
+
+    def run(self, X, Y):
+        from .parallel.ddp import DataParallel
+
+        ddp = DataParallel(self.model, self.pg, bucket_mb=self.cfg.get("bucket_mb"))
+        ddp.broadcast_parameters()
+        it = 0
+        for xb, yb in self.batches(X, Y):
+            if it >= self.steps:
+                break
+            xb, yb = self.model.to_input(xb), self.model.to_target(yb)
+            self.history.append(float(ddp.train_step(xb, yb)))
+            it += 1
+        return self.arena.master.detach().clone()
+
+
+_WORKERS = {"adag": _AdagWorker, "dynsgd": _DynSGDWorker, "downpour": _DownpourWorker, "easgd": _EASGDWorker,
+            "aeasgd": _EASGDWorker, "eamsgd": _EASGDWorker, "averaging": _AveragingWorker,
+            "ensemble": _EnsembleWorker, "single": _EnsembleWorker, "syncdp": _SyncDPWorker}
+
+
+def _train_worker(rank, world, pg, cfg, blob, X, Y, sizes):
+    t0 = time.time()
+    model = deserialize_keras_model({k: v for k, v in blob.items() if k not in ("optimizer", "loss")})
+    opt = opt_mod.get(cfg["worker_optimizer"])
+    if cfg["algorithm"] == "eamsgd" and isinstance(opt, opt_mod.SGD) and not opt.momentum:
+        opt.momentum = cfg.get("momentum", 0.9)
+    model.compile(opt, cfg["loss"])
+    model.seed = cfg.get("seed", 0)
+    model.place(pg.device)
+    if blob.get("flat") is not None:
+        model.arena.set_flat(torch.from_numpy(blob["flat"]))
+    if blob.get("states"):
+        set_states(model, blob["states"])
+    Xd, Yd = _to_device(X, model), _to_device(Y, model)
+    w = _WORKERS[cfg["algorithm"]](cfg, model, pg, sizes)
+    final = w.run(Xd, Yd)
+    if model.device.type == "cuda":
+        torch.cuda.synchronize(model.device)
+    out = {"rank": rank, "history": w.history, "num_updates": w.num_updates(), "time": time.time() - t0}
+    if rank == 0 or cfg["algorithm"] == "ensemble":
+        out["flat"] = final.cpu().numpy().copy()
+        out["states"] = get_states(model)
+    return out
+
+
+# =============================================================================================
+#                                    driver side
+# =============================================================================================
+class ParameterServer:
+    """Facade of the reference's driver-resident parameter server: the center variable
+    and the update counter (``trainer.parameter_server.num_updates``)."""
+
+    def __init__(self, model_blob):
+        self.model_blob = model_blob
+        self.num_updates = 0
+        self.center = None
+        self.states = None
+
+    def get_model(self):
+        m = deserialize_keras_model({k: v for k, v in self.model_blob.items() if k not in ("optimizer", "loss")})
+        m.place("cpu")
+        if self.center is not None:
+            m.arena.set_flat(torch.from_numpy(self.center))
+        if self.states:
+            set_states(m, self.states)
+        return m
+
+
+class Trainer:
+    def __init__(self, keras_model, loss, worker_optimizer, metrics=None, loss_weights=None):
+        self.master_model = serialize_keras_model(keras_model)
+        self.loss = loss
+        self.worker_optimizer = worker_optimizer if not isinstance(worker_optimizer, opt_mod.Optimizer) \
+            else worker_optimizer.get_config()
+        self.metrics = metrics or ["accuracy"]
+        self.loss_weights = loss_weights
+        self.history = []
+        self.training_time_start = 0.0
+        self.training_time_end = 0.0
+        self.training_time = 0.0
+        self.max_mini_batches_prefetch = 100
+        self.parameter_server = ParameterServer(self.master_model)
+        self.device = None
+
+    def set_max_prefetch(self, max_mini_batches):
+        self.max_mini_batches_prefetch = max_mini_batches
+
+    def record_training_start(self):
+        self.training_time = 0.0
+        self.training_time_start = time.time()
+
+    def record_training_end(self):
+        self.training_time_end = time.time()
+        self.training_time = self.training_time_end - self.training_time_start
+
+    def get_training_time(self) -> float:
+        return self.training_time
+
+    def get_history(self):
+        return self.history
+
+    def get_averaged_history(self):
+        from .utils import history_executors_average
+
+        return history_executors_average(self.history)
+
+    def get_executor_history(self, executor_id):
+        return self.history[executor_id]
+
+    def train(self, dataframe, shuffle=False):
+        raise NotImplementedError
+
+
+class _ShardedTrainer(Trainer):
+    algorithm = "adag"
+
+    def __init__(self, keras_model, worker_optimizer, loss, metrics=None, num_workers=2, batch_size=32,
+                 features_col="features", label_col="label", num_epoch=1, communication_window=1,
+                 master_port=5000, loss_weights=None, device=None, seed=0, **extra):
+        super().__init__(keras_model, loss, worker_optimizer, metrics, loss_weights)
+        self.num_workers = int(num_workers)
+        self.batch_size = int(batch_size)
+        self.features_column = features_col
+        self.label_column = label_col
+        self.num_epoch = int(num_epoch)
+        self.communication_window = int(communication_window)
+        self.master_port = master_port
+        self.device = device
+        self.seed = seed
+        self.extra = extra
+
+    def _cfg(self):
+        return {"algorithm": self.algorithm, "worker_optimizer": self.worker_optimizer, "loss": self.loss,
+                "batch_size": self.batch_size, "num_epoch": self.num_epoch,
+                "communication_window": self.communication_window, "seed": self.seed, **self.extra}
+
+    def _shards(self, dataframe, shuffle):
+        df = dataframe
+        if shuffle:
+            from .utils import shuffle as _shuffle
+
+            df = _shuffle(df, self.seed)
+        if df.rdd_partitions_count() != self.num_workers:
+            df = df.repartition(self.num_workers)
+        parts = df.partition_arrays([self.features_column, self.label_column], np.float32)
+        return [p[0] for p in parts], [p[1] for p in parts]
+
+    def train(self, dataframe, shuffle=False):
+        self.record_training_start()
+        Xs, Ys = self._shards(dataframe, shuffle)
+        sizes = [x.shape[0] for x in Xs]
+        cfg = self._cfg()
+        args = [(cfg, self.master_model, Xs[r], Ys[r], sizes) for r in range(self.num_workers)]
+        results = run_workers(_train_worker, self.num_workers, args, device=self.device)
+        self.history = [r["history"] for r in results]
+        ps = self.parameter_server
+        ps.num_updates = int(results[0]["num_updates"])
+        ps.center = results[0]["flat"]
+        ps.states = results[0].get("states")
+        self.worker_times = [r["time"] for r in results]
+        self._results = results
+        model = ps.get_model()
+        self.record_training_end()
+        return model
+
+
+class SingleTrainer(_ShardedTrainer):
+    """One worker on the coalesced frame (``ddl_mnist_aztk.py:215``)."""
+
+    algorithm = "single"
+
+    def __init__(self, keras_model, worker_optimizer, loss, metrics=None, features_col="features",
+                 label_col="label", num_epoch=1, batch_size=32, **kw):
+        super().__init__(keras_model, worker_optimizer, loss, metrics, 1, batch_size, features_col, label_col,
+                         num_epoch, 1, **kw)
+
+    def train(self, dataframe, shuffle=False):
+        model = super().train(dataframe.coalesce(1), shuffle)
+        self.parameter_server.num_updates = len(self.history[0]) if self.history else 0
+        return model
+
+
+class AveragingTrainer(_ShardedTrainer):
+    algorithm = "averaging"
+
+    def __init__(self, keras_model, worker_optimizer, loss, metrics=None, features_col="features",
+                 label_col="label", num_epoch=1, batch_size=32, num_workers=2, **kw):
+        super().__init__(keras_model, worker_optimizer, loss, metrics, num_workers, batch_size, features_col,
+                         label_col, num_epoch, 1, **kw)
+
+
+class EnsembleTrainer(_ShardedTrainer):
+    algorithm = "ensemble"
+
+    def __init__(self, keras_model, worker_optimizer, loss, metrics=None, features_col="features",
+                 label_col="label", batch_size=32, num_ensembles=2, num_epoch=1, **kw):
+        super().__init__(keras_model, worker_optimizer, loss, metrics, num_ensembles, batch_size, features_col,
+                         label_col, num_epoch, 1, **kw)
+
+    def train(self, dataframe, shuffle=False):
+        super().train(dataframe, shuffle)
+        models = []
+        for r in self._results:
+            ps = ParameterServer(self.master_model)
+            ps.center, ps.states = r["flat"], r.get("states")
+            models.append(ps.get_model())
+        return models
+
+
+class DistributedTrainer(_ShardedTrainer):
+    pass
+
+
+class AsynchronousDistributedTrainer(DistributedTrainer):
+    def __init__(self, *a, parallelism_factor=1, **kw):
+        super().__init__(*a, **kw)
+        self.parallelism_factor = parallelism_factor
+
+
+class ADAG(AsynchronousDistributedTrainer):
+    """Asynchronous Distributed Adaptive Gradients — window-normalised delta commits."""
+
+    algorithm = "adag"
+
+    def __init__(self, keras_model, worker_optimizer, loss, metrics=None, num_workers=2, batch_size=32,
+                 features_col="features", label_col="label", num_epoch=1, communication_window=12,
+                 master_port=5000, loss_weights=None, **kw):
+        super().__init__(keras_model, worker_optimizer, loss, metrics, num_workers, batch_size, features_col,
+                         label_col, num_epoch, communication_window, master_port, loss_weights, **kw)
+
+
+class DynSGD(AsynchronousDistributedTrainer):
+    """Staleness-aware async SGD (commit scaled by 1/(staleness+1))."""
+
+    algorithm = "dynsgd"
+
+    def __init__(self, keras_model, worker_optimizer, loss, metrics=None, num_workers=2, batch_size=32,
+                 features_col="features", label_col="label", num_epoch=1, communication_window=5,
+                 master_port=5000, loss_weights=None, **kw):
+        super().__init__(keras_model, worker_optimizer, loss, metrics, num_workers, batch_size, features_col,
+                         label_col, num_epoch, communication_window, master_port, loss_weights, **kw)
+
+
+class DOWNPOUR(AsynchronousDistributedTrainer):
+    algorithm = "downpour"
+
+    def __init__(self, keras_model, worker_optimizer, loss, metrics=None, num_workers=2, batch_size=32,
+                 features_col="features", label_col="label", num_epoch=1, communication_window=5,
+                 master_port=5000, loss_weights=None, **kw):
+        super().__init__(keras_model, worker_optimizer, loss, metrics, num_workers, batch_size, features_col,
+                         label_col, num_epoch, communication_window, master_port, loss_weights, **kw)
+
+
+class EASGD(AsynchronousDistributedTrainer):
+    """Elastic averaging SGD (synchronous rounds every ``communication_window`` batches)."""
+
+    algorithm = "easgd"
+
+    def __init__(self, keras_model, worker_optimizer, loss, metrics=None, features_col="features",
+                 label_col="label", num_epoch=1, batch_size=32, num_workers=2, rho=5.0, learning_rate=0.1,
+                 master_port=5000, loss_weights=None, communication_window=1, **kw):
+        super().__init__(keras_model, worker_optimizer, loss, metrics, num_workers, batch_size, features_col,
+                         label_col, num_epoch, communication_window, master_port, loss_weights,
+                         alpha=min(1.0, float(rho) * float(learning_rate) / max(num_workers, 1)), **kw)
+        self.rho, self.learning_rate = rho, learning_rate
+
+
+class AEASGD(EASGD):
+    algorithm = "aeasgd"
+
+    def __init__(self, keras_model, worker_optimizer, loss, metrics=None, num_workers=2, batch_size=32,
+                 features_col="features", label_col="label", num_epoch=1, communication_window=32, rho=5.0,
+                 learning_rate=0.1, master_port=5000, loss_weights=None, **kw):
+        super().__init__(keras_model, worker_optimizer, loss, metrics, features_col, label_col, num_epoch,
+                         batch_size, num_workers, rho, learning_rate, master_port, loss_weights,
+                         communication_window=communication_window, **kw)
+
+
+class EAMSGD(EASGD):
+    algorithm = "eamsgd"
+
+    def __init__(self, keras_model, worker_optimizer, loss, metrics=None, num_workers=2, batch_size=32,
+                 features_col="features", label_col="label", num_epoch=1, communication_window=32, rho=5.0,
+                 learning_rate=0.1, momentum=0.9, master_port=5000, loss_weights=None, **kw):
+        super().__init__(keras_model, worker_optimizer, loss, metrics, features_col, label_col, num_epoch,
+                         batch_size, num_workers, rho, learning_rate, master_port, loss_weights,
+                         communication_window=communication_window, momentum=momentum, **kw)
+
+
+class SynchronousDataParallel(DistributedTrainer):
+    """North-star trainer: per-step gradient all-reduce (RCCL, bucketed, overlapped)."""
+
+    algorithm = "syncdp"
+
+    def __init__(self, keras_model, worker_optimizer, loss, metrics=None, num_workers=2, batch_size=32,
+                 features_col="features", label_col="label", num_epoch=1, bucket_mb=None, **kw):
+        super().__init__(keras_model, worker_optimizer, loss, metrics, num_workers, batch_size, features_col,
+                         label_col, num_epoch, 1, bucket_mb=bucket_mb, **kw)
+
+
+SyncDP = SynchronousDataParallel
+
+__all__ = ["Trainer", "SingleTrainer", "AveragingTrainer", "EnsembleTrainer", "DistributedTrainer",
+           "AsynchronousDistributedTrainer", "ADAG", "DynSGD", "DOWNPOUR", "EASGD", "AEASGD", "EAMSGD",
+           "SynchronousDataParallel", "SyncDP", "ParameterServer"]
+_ = copy
