@@ -204,9 +204,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams
   constexpr int RM = WTM / 16, RN = WTN / 16;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const bool one_stage = p.k_split <= BK;  // must match launch_tile's LDS allocation
   char* lds_a0 = smem;
   char* lds_a1 = smem + A_BYTES;
-  char* lds_b0 = smem + 2 * A_BYTES;
+  char* lds_b0 = smem + (one_stage ? A_BYTES : 2 * A_BYTES);
   char* lds_b1 = smem + 2 * A_BYTES + B_BYTES;
 
   const int tiles_n = (p.N + BN - 1) / BN;
@@ -432,7 +433,9 @@ template <int BM, int BN, int AMODE, int BMODE, int EPI>
 inline int launch_tile(const GemmParams& p, hipStream_t s) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
   const int splits = (p.K + p.k_split - 1) / p.k_split;
-  const size_t lds = 2 * (BM + BN) * BK * 2;
+  // single K-tile (1x1 convs with K <= 64): one LDS stage -> twice the resident blocks per CU
+  const bool one_stage = p.k_split <= BK;
+  const size_t lds = (one_stage ? 1 : 2) * (BM + BN) * BK * 2;
   hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, AMODE, BMODE, EPI>), dim3(tiles, splits > 0 ? splits : 1), dim3(NTHREADS),
                      lds, s, p);
   return (int)hipGetLastError();

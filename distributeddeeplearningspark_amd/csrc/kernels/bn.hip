@@ -96,8 +96,8 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const uint4* __restrict__
 static dim3 col_grid(long M, int C) {
   const int CV = C >> 3, CT = CV < 256 ? CV : 256, RT = 256 / CT;
   const int gy = (CV + CT - 1) / CT;
-  long gx = (M + RT - 1) / RT;
-  const long cap = 2048 / gy > 1 ? 2048 / gy : 1;
+  long gx = (M + 4 * RT - 1) / (4 * RT);
+  const long cap = 4096 / gy > 1 ? 4096 / gy : 1;
   if (gx > cap) gx = cap;
   return dim3((unsigned)gx, (unsigned)gy);
 }
@@ -239,25 +239,26 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint4* __restr
     }
     const long step = (long)gridDim.x * g.RT;
     long r = (long)blockIdx.x * g.RT + g.rt;
-    for (; r + step < M; r += 2 * step) {  // two rows of dy and x in flight per lane
-      const long i0 = r * g.CV + g.cv, i1 = (r + step) * g.CV + g.cv;
-      const uint4 d0 = dy[i0], x0 = x[i0], d1 = dy[i1], x1 = x[i1];
-      float d[8], xv[8];
-      unpack8(d0, d);
-      unpack8(x0, xv);
-      relu_mask(d, xv, y, i0, sc, sh, mode);
+    for (; r + 3 * step < M; r += 4 * step) {  // four rows of dy and x in flight per lane
+      long ix[4];
+      uint4 dd[4], xx[4];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        acc[i] += d[i];
-        acc[8 + i] += d[i] * (xv[i] - mu[i]);
+      for (int q = 0; q < 4; ++q) {
+        ix[q] = (r + q * step) * g.CV + g.cv;
+        dd[q] = dy[ix[q]];
+        xx[q] = x[ix[q]];
       }
-      unpack8(d1, d);
-      unpack8(x1, xv);
-      relu_mask(d, xv, y, i1, sc, sh, mode);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        acc[i] += d[i];
-        acc[8 + i] += d[i] * (xv[i] - mu[i]);
+      for (int q = 0; q < 4; ++q) {
+        float d[8], xv[8];
+        unpack8(dd[q], d);
+        unpack8(xx[q], xv);
+        relu_mask(d, xv, y, ix[q], sc, sh, mode);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          acc[i] += d[i];
+          acc[8 + i] += d[i] * (xv[i] - mu[i]);
+        }
       }
     }
     for (; r < M; r += step) {

@@ -150,7 +150,8 @@ class Layer:
                 if e.master is None:
                     e._initial = arr
                 else:
-                    e.master.copy_(torch.from_numpy(arr))
+                    with torch.no_grad():
+                        e.master.copy_(torch.from_numpy(arr))
             else:
                 self._states[e].copy_(torch.as_tensor(np.asarray(w), dtype=torch.float32))
 

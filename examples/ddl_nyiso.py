@@ -1,0 +1,117 @@
+#!/usr/bin/env python
+"""NYISO hourly-load forecasting with GRU and LSTM regressors trained by ADAG — the
+reference's ``ddl_nyiso_aztk.py`` / ``ddl_nyiso_hdi.ipynb`` workflow on this framework.
+
+Differences from the reference: synthetic NYISO-shaped data instead of
+the Azure-Blob CSV (no network, no storage keys), ``local[N]`` master instead of
+AZTK/YARN, and one worker process per MI355X (or CPU executor) instead of Spark tasks
+talking to a socket parameter server.
+
+    python examples/ddl_nyiso.py [--workers 4] [--epochs 20] [--device auto|cpu]
+"""
+from __future__ import annotations
+
+import argparse
+import datetime as dt
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from distributeddeeplearningspark_amd.context import SparkConf, SparkContext, SparkSession, SQLContext  # noqa: E402
+from distributeddeeplearningspark_amd.data.synthetic import nyiso_like  # noqa: E402
+from distributeddeeplearningspark_amd.evaluators import get_MAPE  # noqa: E402
+from distributeddeeplearningspark_amd.ml.feature import VectorAssembler  # noqa: E402
+from distributeddeeplearningspark_amd.models.zoo import gru_regressor, lstm_regressor  # noqa: E402
+from distributeddeeplearningspark_amd.predictors import ModelPredictor  # noqa: E402
+from distributeddeeplearningspark_amd.sql import functions as F  # noqa: E402
+from distributeddeeplearningspark_amd.sql.types import TimestampType  # noqa: E402
+from distributeddeeplearningspark_amd.sql.window import Window  # noqa: E402
+from distributeddeeplearningspark_amd.trainers import ADAG  # noqa: E402
+from distributeddeeplearningspark_amd.transformers import MinMaxTransformer, ReshapeTransformer  # noqa: E402
+
+LEN_SEQ_IN, LEN_SEQ_OUT, LEN_EXTRA_IN, LEN_TEST_DATA = 24, 1, 1, 120
+N_UNITS, BATCH_SIZE, COM_WINDOW = 128, 32, 5
+
+
+def build_frames(sqlc, csv_path, num_workers):
+    raw_df = sqlc.read.format("com.databricks.spark.csv").options(header="true", inferSchema="true").load(csv_path)
+    func = F.udf(lambda x: dt.datetime.strptime(x[:19], "%m/%d/%Y %H:%M:%S"), TimestampType())
+    raw_df = raw_df.withColumn("TimeStamp", func(F.col("TimeStamp")))
+    df = raw_df.select(["TimeStamp", "Name", "HourAvgLoad", "temperature"])
+    orig_min = df.select(F.min("temperature")).collect()[0][0]
+    orig_max = df.select(F.max("temperature")).collect()[0][0]
+    df = MinMaxTransformer(n_min=0.0, n_max=1.0, o_min=orig_min, o_max=orig_max, input_col="temperature",
+                           output_col="NormTemp", is_vector=False).transform(df)
+    orig_min = df.select(F.min("HourAvgLoad")).collect()[0][0]
+    orig_max = df.select(F.max("HourAvgLoad")).collect()[0][0]
+    df = MinMaxTransformer(n_min=0.0, n_max=1.0, o_min=orig_min, o_max=orig_max, input_col="HourAvgLoad",
+                           output_col="NormLoad", is_vector=False).transform(df)
+    w = Window.partitionBy("Name").orderBy("TimeStamp")
+    for n_lag in range(LEN_SEQ_IN, 0, -1):
+        df = df.withColumn("NormLoad_lag" + str(n_lag), F.lag(F.col("NormLoad"), count=n_lag).over(w))
+    for n_lag in range(1, LEN_SEQ_OUT + 1):
+        df = df.withColumn("NormLoad_next" + str(n_lag), F.lead(F.col("NormLoad"), count=n_lag).over(w))
+        df = df.withColumn("OrigNormLoad_next" + str(n_lag), F.lead(F.col("HourAvgLoad"), count=n_lag).over(w))
+        df = df.withColumn("NormTemp_next" + str(n_lag), F.lead(F.col("NormTemp"), count=n_lag).over(w))
+    df = df.na.drop()
+    features = ["NormLoad_lag" + str(n) for n in range(LEN_SEQ_IN, 0, -1)] + \
+        ["NormTemp_next" + str(n) for n in range(1, LEN_SEQ_OUT + 1)]
+    df = VectorAssembler(inputCols=features, outputCol="features").transform(df)
+    df = ReshapeTransformer("features", "feature_matrix", (LEN_SEQ_IN + LEN_EXTRA_IN, 1)).transform(df)
+    df = VectorAssembler(inputCols=["NormLoad_next1"], outputCol="labels").transform(df)
+    df = VectorAssembler(inputCols=["OrigNormLoad_next1"], outputCol="labels2").transform(df)
+    df = ReshapeTransformer("labels", "label_matrix", (LEN_SEQ_OUT, 1)).transform(df)
+    df_train = df.limit(df.count() - LEN_TEST_DATA)
+    df_test = df.orderBy("TimeStamp", ascending=False).limit(LEN_TEST_DATA).orderBy("TimeStamp", ascending=True)
+    cols = ["features", "feature_matrix", "labels", "labels2", "label_matrix"]
+    df_train = df_train.select(*cols).repartition(num_workers).cache()
+    df_test = df_test.select(*cols).repartition(num_workers).cache()
+    return df_train, df_test, orig_min, orig_max
+
+
+def run(model, optimizer, df_train, df_test, orig_min, orig_max, num_workers, epochs, device):
+    model.summary()
+    trainer = ADAG(keras_model=model, worker_optimizer=optimizer, loss="mean_squared_error", num_workers=num_workers,
+                   batch_size=BATCH_SIZE, communication_window=COM_WINDOW, num_epoch=epochs,
+                   features_col="feature_matrix", label_col="labels", device=device)
+    trained = trainer.train(df_train)
+    print("Number of parameter updates " + str(trainer.parameter_server.num_updates))
+    print("Total training time in seconds " + str(trainer.get_training_time()))
+    df_pred = ModelPredictor(keras_model=trained, features_col="feature_matrix").predict(df_test.limit(24))
+    inv = MinMaxTransformer(n_min=orig_min, n_max=orig_max, o_min=0.0, o_max=1.0, input_col="prediction",
+                            output_col="prediction2", is_vector=True)
+    df_pred = inv.transform(df_pred)
+    df_pred.select("labels2", "prediction2").show(5)
+    actual = df_pred.select("labels2").rdd.map(lambda x: list(x[0])).collect()
+    pred = df_pred.select("prediction2").rdd.map(lambda x: list(x[0])).collect()
+    mape = get_MAPE(actual, pred)
+    print("MAPE", mape)
+    return trainer, mape
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workers", type=int, default=2)
+    ap.add_argument("--epochs", type=int, default=20)
+    ap.add_argument("--device", default="auto")
+    ap.add_argument("--csv", default="/tmp/ddl_nyiso_synthetic.csv")
+    a = ap.parse_args()
+    nyiso_like().to_csv(a.csv, index=False)
+    conf = SparkConf().set("spark.app.name", "ddl_nyiso").set("spark.master", f"local[{a.workers}]")
+    conf.set("spark.executor.cores", 1).set("spark.executor.instances", a.workers)
+    sc = SparkContext(conf=conf)
+    sqlc = SQLContext(sc)
+    SparkSession.builder.getOrCreate().sparkContext.setLogLevel("ERROR")
+    df_train, df_test, omin, omax = build_frames(sqlc, a.csv, a.workers)
+    res = {}
+    for name, model, opt in (("GRU", gru_regressor(N_UNITS), "adagrad"), ("LSTM", lstm_regressor(N_UNITS), "adam")):
+        tr, mape = run(model, opt, df_train, df_test, omin, omax, a.workers, a.epochs, a.device)
+        res[name] = {"updates": tr.parameter_server.num_updates, "time_s": tr.get_training_time(), "mape": mape}
+    print(res)
+
+
+if __name__ == "__main__":
+    main()

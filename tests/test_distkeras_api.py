@@ -1,0 +1,234 @@
+"""dist-keras surface: transformers, model API (param counts / Keras layouts / JSON),
+predictors, evaluators, MAPE, and the trainers on CPU executors (gloo, world size 2)."""
+import json
+
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from distributeddeeplearningspark_amd.context import SparkSession
+from distributeddeeplearningspark_amd.evaluators import AccuracyEvaluator, get_MAPE
+from distributeddeeplearningspark_amd.ml.feature import VectorAssembler
+from distributeddeeplearningspark_amd.models import Dense, Sequential, model_from_json
+from distributeddeeplearningspark_amd.models.zoo import gru_regressor, lenet5, lstm_regressor, mnist_cnn, vgg16
+from distributeddeeplearningspark_amd.predictors import ModelPredictor
+from distributeddeeplearningspark_amd.transformers import (DenseTransformer, LabelIndexTransformer,
+                                                           MinMaxTransformer, OneHotTransformer, ReshapeTransformer)
+from distributeddeeplearningspark_amd.utils import deserialize_keras_model, serialize_keras_model
+
+
+@pytest.fixture(scope="module")
+def spark():
+    return SparkSession.builder.master("local[2]").getOrCreate()
+
+
+# ------------------------------------------------------------------ transformers
+def test_minmax_scalar_vector_inverse(spark):
+    df = spark.createDataFrame(pd.DataFrame({"t": [10.0, 20.0, 30.0]}))
+    df = MinMaxTransformer(n_min=0.0, n_max=1.0, o_min=10.0, o_max=30.0, input_col="t", output_col="n",
+                           is_vector=False).transform(df)
+    assert df.toPandas().n.tolist() == [0.0, 0.5, 1.0]
+    df = VectorAssembler(inputCols=["n"], outputCol="v").transform(df)
+    inv = MinMaxTransformer(n_min=10.0, n_max=30.0, o_min=0.0, o_max=1.0, input_col="v", output_col="back",
+                            is_vector=True).transform(df)
+    assert [r.back.toArray()[0] for r in inv.collect()] == [10.0, 20.0, 30.0]
+
+
+def test_onehot_reshape_dense_labelindex(spark):
+    df = spark.createDataFrame(pd.DataFrame({"label": [3, 0, 9]}))
+    df = OneHotTransformer(10, input_col="label", output_col="enc").transform(df)
+    enc = np.stack([r.enc.toArray() for r in df.collect()])
+    assert enc.argmax(1).tolist() == [3, 0, 9] and enc.sum() == 3
+    df = DenseTransformer(input_col="enc", output_col="dense").transform(df)
+    df = ReshapeTransformer("dense", "mat", (2, 5)).transform(df)
+    assert dict(df.dtypes)["mat"] == "array<array<double>>"
+    assert np.asarray(df.first().mat).shape == (2, 5)
+    df = LabelIndexTransformer(output_dim=10, input_col="enc").transform(df)
+    assert df.toPandas().prediction_index.tolist() == [3.0, 0.0, 9.0]
+    assert AccuracyEvaluator(prediction_col="prediction_index", label_col="label").evaluate(df) == 1.0
+
+
+def test_mape_semantics():
+    assert abs(get_MAPE([[100.0], [200.0]], [[110.0], [180.0]]) - 10.0) < 1e-12
+    assert np.isnan(get_MAPE([[0.0]], [[1.0]]))  # inf -> nan (ddl_nyiso_aztk.py:240-241)
+
+
+# ------------------------------------------------------------------ models
+def test_reference_param_counts():
+    # SURVEY §4 oracles: 1,048,853 / 50,049 / 66,689 (ddl_nyiso_hdi.ipynb:549-554,772-777)
+    assert mnist_cnn().count_params() or True
+    m = mnist_cnn()
+    m.build_model()
+    assert m.count_params() == 1048853
+    g = gru_regressor()
+    g.build_model()
+    assert g.count_params() == 50049
+    assert [l.count_params() for l in g.layers] == [49920, 129]
+    lst = lstm_regressor()
+    lst.build_model()
+    assert lst.count_params() == 66689
+    assert [l.count_params() for l in lst.layers] == [66560, 129]
+    v = vgg16()
+    v.build_model()
+    l5 = lenet5()
+    l5.build_model()
+    assert l5.count_params() == 61706
+
+
+def test_summary_format(capsys):
+    g = gru_regressor()
+    g.summary()
+    out = capsys.readouterr().out
+    assert "(None, 128)" in out and "49920" in out and "Total params: 50,049" in out
+
+
+def test_keras_weight_layouts_and_json_roundtrip():
+    m = mnist_cnn()
+    ws = m.get_weights()
+    assert [w.shape for w in ws] == [(3, 3, 1, 32), (32,), (3, 3, 32, 32), (32,), (4608, 225), (225,), (225, 10), (10,)]
+    g = gru_regressor()
+    assert [w.shape for w in g.get_weights()] == [(1, 384), (128, 384), (384,), (128, 1), (1,)]
+    lst = lstm_regressor()
+    b = lst.get_weights()[2]
+    assert (b[128:256] == 1).all() and (b[:128] == 0).all()  # unit_forget_bias, gate order i,f,c,o
+    m2 = model_from_json(m.to_json())
+    m2.set_weights(ws)
+    for a, c in zip(ws, m2.get_weights()):
+        np.testing.assert_array_equal(a, c)
+    d = serialize_keras_model(m)
+    json.loads(d["model"])
+    m3 = deserialize_keras_model(d)
+    x = np.random.rand(2, 28, 28, 1).astype(np.float32)
+    np.testing.assert_allclose(m.predict(x), m3.predict(x), rtol=1e-5, atol=1e-6)
+
+
+def test_gru_lstm_match_keras_math():
+    """Hand-written Keras-2 GRU (reset_after=False) / LSTM cell, numpy, vs our layers."""
+    rng = np.random.default_rng(0)
+    x = rng.normal(size=(3, 5, 1)).astype(np.float32)
+    hs = lambda z: np.clip(0.2 * z + 0.5, 0, 1)
+    for kind in ("gru", "lstm"):
+        m = gru_regressor(units=4, seq_len=5) if kind == "gru" else lstm_regressor(units=4, seq_len=5)
+        W, U, b, Wd, bd = m.get_weights()
+        H = 4
+        h = np.zeros((3, H))
+        c = np.zeros((3, H))
+        for t in range(5):
+            xt = x[:, t] @ W + b
+            if kind == "gru":
+                z = hs(xt[:, :H] + h @ U[:, :H])
+                r = hs(xt[:, H:2 * H] + h @ U[:, H:2 * H])
+                hh = np.tanh(xt[:, 2 * H:] + (r * h) @ U[:, 2 * H:])
+                h = z * h + (1 - z) * hh
+            else:
+                g = xt + h @ U
+                i, f, cc, o = hs(g[:, :H]), hs(g[:, H:2 * H]), np.tanh(g[:, 2 * H:3 * H]), hs(g[:, 3 * H:])
+                c = f * c + i * cc
+                h = o * np.tanh(c)
+        ref = h @ Wd + bd
+        np.testing.assert_allclose(m.predict(x), ref, rtol=1e-4, atol=1e-5)
+
+
+def test_train_on_batch_learns_regression():
+    torch.manual_seed(0)
+    from distributeddeeplearningspark_amd.models.optimizers import Adam
+
+    m = Sequential([Dense(16, activation="relu", input_shape=(4,)), Dense(1)])
+    m.compile(Adam(lr=0.01), "mean_squared_error")
+    x = np.random.rand(256, 4).astype(np.float32)
+    y = (x @ np.array([1.0, -2.0, 0.5, 3.0], dtype=np.float32))[:, None]
+    first = m.evaluate(x, y)
+    m.fit(x, y, batch_size=32, epochs=30)
+    assert m.evaluate(x, y) < 0.1 * first
+
+
+# ------------------------------------------------------------------ trainers (multi-process gloo)
+def _mnist_frame(spark, n=600):
+    from distributeddeeplearningspark_amd.data.synthetic import mnist_like
+
+    raw = spark.createDataFrame(mnist_like(n, seed=2))
+    feats = [c for c in raw.columns if c != "label"]
+    df = VectorAssembler(inputCols=feats, outputCol="features").transform(raw)
+    df = OneHotTransformer(10, input_col="label", output_col="label_encoded").transform(df)
+    df = MinMaxTransformer(n_min=0.0, n_max=1.0, o_min=0.0, o_max=250.0, input_col="features",
+                           output_col="fn").transform(df)
+    df = ReshapeTransformer("fn", "matrix", (28, 28, 1)).transform(df)
+    return df.select("matrix", "label", "label_encoded")
+
+
+@pytest.mark.parametrize("algo", ["ADAG", "DynSGD", "DOWNPOUR", "AEASGD"])
+def test_trainers_two_workers_update_law(spark, algo):
+    from distributeddeeplearningspark_amd import trainers as T
+
+    df = _mnist_frame(spark, 400).repartition(2)
+    cls = getattr(T, algo)
+    tr = cls(keras_model=mnist_cnn(), worker_optimizer="adam", loss="categorical_crossentropy", num_workers=2,
+             batch_size=16, communication_window=5, num_epoch=2, features_col="matrix", label_col="label_encoded",
+             device="cpu")
+    model = tr.train(df)
+    # num_updates = sum_w floor(E * floor(rows_w / bs) / window): 200 rows -> 12 batches -> 24 steps -> 4 commits
+    assert tr.parameter_server.num_updates == 2 * ((2 * (200 // 16)) // 5)
+    assert tr.get_training_time() > 0
+    assert len(tr.get_history()) == 2 and len(tr.get_history()[0]) == 24
+    pred = ModelPredictor(keras_model=model, features_col="matrix").predict(df)
+    pred = LabelIndexTransformer(output_dim=10).transform(pred)
+    acc = AccuracyEvaluator(prediction_col="prediction_index", label_col="label").evaluate(pred)
+    assert acc > 0.5, acc
+
+
+def test_adag_sync_semantics_match_simulation(spark):
+    """2 workers, window 2: the center after training equals a single-process simulation
+    c += sum_w (W_w - c)/k with worker-local SGD from the same start."""
+    from distributeddeeplearningspark_amd.trainers import ADAG
+
+    rng = np.random.default_rng(0)
+    x = rng.normal(size=(32, 3)).astype(np.float32)
+    y = (x.sum(1, keepdims=True)).astype(np.float32)
+    df = spark.createDataFrame({"f": list(x), "l": list(y)}).repartition(2)
+    base = Sequential([Dense(1, input_shape=(3,))])
+    w0 = base.get_weights()
+    tr = ADAG(keras_model=base, worker_optimizer="sgd", loss="mean_squared_error", num_workers=2, batch_size=4,
+              communication_window=2, num_epoch=1, features_col="f", label_col="l", device="cpu")
+    out = tr.train(df).get_weights()
+    # simulation
+    shards = [x[0::2], x[1::2]], [y[0::2], y[1::2]]
+    center = [w.copy() for w in w0]
+    workers = []
+    for r in range(2):
+        m = Sequential([Dense(1, input_shape=(3,))])
+        m.compile("sgd", "mean_squared_error")
+        m.set_weights(center)
+        workers.append(m)
+    for rnd in range(2):
+        deltas = []
+        for r, m in enumerate(workers):
+            m.set_weights(center)
+            for b in range(2):
+                i = (rnd * 2 + b) * 4
+                m.train_on_batch(shards[0][r][i:i + 4], shards[1][r][i:i + 4])
+            deltas.append([(a - c) / 2 for a, c in zip(m.get_weights(), center)])
+        center = [c + d0 + d1 for c, d0, d1 in zip(center, *deltas)]
+    for a, b in zip(out, center):
+        np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-6)
+    assert tr.parameter_server.num_updates == 4
+
+
+def test_single_averaging_ensemble_syncdp(spark):
+    from distributeddeeplearningspark_amd.trainers import (AveragingTrainer, EnsembleTrainer, SingleTrainer,
+                                                            SynchronousDataParallel)
+
+    df = _mnist_frame(spark, 200)
+    common = dict(worker_optimizer="adam", loss="categorical_crossentropy", features_col="matrix",
+                  label_col="label_encoded", batch_size=20, num_epoch=1, device="cpu")
+    st = SingleTrainer(keras_model=mnist_cnn(), **common)
+    st.train(df)
+    assert st.parameter_server.num_updates == 10
+    av = AveragingTrainer(keras_model=mnist_cnn(), num_workers=2, **common)
+    av.train(df.repartition(2))
+    ens = EnsembleTrainer(keras_model=mnist_cnn(), num_ensembles=2, **{k: v for k, v in common.items()})
+    models = ens.train(df.repartition(2))
+    assert len(models) == 2
+    sd = SynchronousDataParallel(keras_model=mnist_cnn(), num_workers=2, **common)
+    sd.train(df.repartition(2))
+    assert sd.parameter_server.num_updates == 5
