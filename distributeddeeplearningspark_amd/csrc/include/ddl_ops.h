@@ -7,15 +7,19 @@
 
 namespace ddl {
 
-constexpr int kBnShards = 32;  // == kStatShards: sharded atomic accumulation of per-channel sums
+constexpr int kBnShards = 32;     // == kStatShards: sharded atomic sums of the fused GEMM-epilogue statistics
+constexpr int kMaxPartials = 512;  // partial rows of a column-reduction sweep
 
 // ---------------- batch norm (x: [M, C] bf16, C % 8 == 0) ----------------
-// ws: [kBnShards][2][C] fp32, must be zero on entry (accumulates sum / sumsq)
+// Per-channel sums live in a workspace ws[S][2][C] (S partial rows, summed by the finalize):
+//   * fused conv-epilogue statistics: S = kBnShards, zeroed, accumulated with atomics;
+//   * bn_stats / bn_bwd_reduce sweeps: S = bn_partial_rows(M, C), every row written (no zeroing).
+int bn_partial_rows(long M, int C);
 int bn_stats(const void* x, float* ws, long M, int C, hipStream_t s);
 // ws -> mean/invstd (saved for backward), scale/shift for apply, running stats update
-int bn_finalize(const float* ws, long M, int C, const float* gamma, const float* beta, float eps, float momentum,
-                float* running_mean, float* running_var, float* save_mean, float* save_invstd, float* scale,
-                float* shift, hipStream_t s);
+int bn_finalize(const float* ws, int S, long M, int C, const float* gamma, const float* beta, float eps,
+                float momentum, float* running_mean, float* running_var, float* save_mean, float* save_invstd,
+                float* scale, float* shift, hipStream_t s);
 // y = relu?(x*scale[c] + shift[c] + resid)
 int bn_apply(const void* x, const float* scale, const float* shift, const void* resid, void* y, long M, int C,
              int relu, hipStream_t s);
@@ -24,7 +28,7 @@ int bn_apply(const void* x, const float* scale, const float* shift, const void* 
 int bn_bwd_reduce(const void* dy, const void* x, const void* y, const float* scale, const float* shift,
                   const float* mean, float* ws, long M, int C, int mode, hipStream_t s);
 // pass 2: grads of gamma/beta (+=) and per-channel dx = A*dy' + B*x + K coefficients
-int bn_bwd_finalize(const float* ws, long M, int C, const float* gamma, const float* mean, const float* invstd,
+int bn_bwd_finalize(const float* ws, int S, long M, int C, const float* gamma, const float* mean, const float* invstd,
                     float* dgamma, float* dbeta, float* coef, hipStream_t s);
 // pass 3: dx = A*dy' + B*x + K;  optionally dres = dy' (masked gradient of the residual branch)
 int bn_bwd_dx(const void* dy, const void* x, const void* y, const float* scale, const float* shift,

@@ -36,24 +36,35 @@ struct ColGeom {  // thread -> (row-lane, column-vector) mapping for column redu
   }
 };
 
-// Block reduction of 16 per-thread partials over the RT row-lanes, then sharded atomics.
+// Block reduction of 16 per-thread partials over the RT row-lanes (LDS tree), then ONE
+// plain store per value into partial row blockIdx.x of ws[S][2][C] (no atomics: the
+// per-channel finalize sums the S partial rows).
 __device__ __forceinline__ void col_reduce_store(float (&acc)[16], const ColGeom& g, float* ws, int C) {
   __shared__ float red[256 * 17];
+  if (g.RT > 1) {
 #pragma unroll
-  for (int i = 0; i < 16; ++i) red[threadIdx.x * 17 + i] = acc[i];
-  __syncthreads();
+    for (int i = 0; i < 16; ++i) red[threadIdx.x * 17 + i] = acc[i];
+    __syncthreads();
+    for (int n = g.RT; n > 1;) {  // pairwise tree, any RT
+      const int half = (n + 1) >> 1;
+      const bool take = g.rt < n - half;
+      n = half;
+      if (take) {
+        const int t = (g.rt + half) * g.CT + g.ct;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[i] += red[t * 17 + i];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) red[threadIdx.x * 17 + i] = acc[i];
+      }
+      __syncthreads();
+    }
+  }
   if (g.rt == 0 && g.cv < g.CV) {
-    for (int r = 1; r < g.RT; ++r) {
-      const int t = r * g.CT + g.ct;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[i] += red[t * 17 + i];
-    }
-    float* dst = ws + (long)(blockIdx.x % kBnShards) * 2 * C + g.cv * 8;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      atomicAdd(dst + i, acc[i]);
-      atomicAdd(dst + C + i, acc[8 + i]);
-    }
+    float* dst = ws + (long)blockIdx.x * 2 * C + g.cv * 8;
+    *reinterpret_cast<float4*>(dst) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    *reinterpret_cast<float4*>(dst + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+    *reinterpret_cast<float4*>(dst + C) = make_float4(acc[8], acc[9], acc[10], acc[11]);
+    *reinterpret_cast<float4*>(dst + C + 4) = make_float4(acc[12], acc[13], acc[14], acc[15]);
   }
 }
 
@@ -93,30 +104,64 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const uint4* __restrict__
   col_reduce_store(acc, g, ws, C);
 }
 
+// partial rows (= grid.x) of a column reduction: >= 16 rows per lane, <= kMaxPartials rows
 static dim3 col_grid(long M, int C) {
   const int CV = C >> 3, CT = CV < 256 ? CV : 256, RT = 256 / CT;
   const int gy = (CV + CT - 1) / CT;
-  long gx = (M + 4 * RT - 1) / (4 * RT);
-  const long cap = 4096 / gy > 1 ? 4096 / gy : 1;
-  if (gx > cap) gx = cap;
+  long gx = M / (16L * RT);
+  if (gx > kMaxPartials) gx = kMaxPartials;
+  if (gx < 1) gx = 1;
   return dim3((unsigned)gx, (unsigned)gy);
 }
+
+int bn_partial_rows(long M, int C) { return (int)col_grid(M, C).x; }
 
 int bn_stats(const void* x, float* ws, long M, int C, hipStream_t s) {
   hipLaunchKernelGGL(bn_stats_kernel, col_grid(M, C), dim3(256), 0, s, (const uint4*)x, ws, M, C);
   return (int)hipGetLastError();
 }
 
-__global__ void bn_finalize_kernel(const float* ws, long M, int C, const float* gamma, const float* beta, float eps,
-                                   float momentum, float* rmean, float* rvar, float* smean, float* sinv, float* scale,
-                                   float* shift) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s1 = 0.0, s2 = 0.0;
-  for (int k = 0; k < kBnShards; ++k) {
-    s1 += ws[(long)k * 2 * C + c];
-    s2 += ws[(long)k * 2 * C + C + c];
+// Sum of the S partial rows of ws[S][2][C] for 64 channels per 256-thread block:
+// 4 row-lanes per channel, 4 independent accumulators each, then an LDS combine.
+// Returns true in the lane that owns channel c (row-lane 0).
+__device__ __forceinline__ bool sum_partials(const float* ws, int S, int C, int& c, double& s1, double& s2) {
+  const int cl = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  c = blockIdx.x * 64 + cl;
+  double a1 = 0.0, a2 = 0.0;
+  if (c < C) {
+    float p1[4] = {0.f, 0.f, 0.f, 0.f}, p2[4] = {0.f, 0.f, 0.f, 0.f};
+    int k = sl;
+    for (; k + 12 < S; k += 16) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        p1[u] += ws[(long)(k + 4 * u) * 2 * C + c];
+        p2[u] += ws[(long)(k + 4 * u) * 2 * C + C + c];
+      }
+    }
+    for (; k < S; k += 4) {
+      p1[0] += ws[(long)k * 2 * C + c];
+      p2[0] += ws[(long)k * 2 * C + C + c];
+    }
+    a1 = (double)p1[0] + p1[1] + p1[2] + p1[3];
+    a2 = (double)p2[0] + p2[1] + p2[2] + p2[3];
   }
+  __shared__ double red[2][256];
+  red[0][threadIdx.x] = a1;
+  red[1][threadIdx.x] = a2;
+  __syncthreads();
+  if (sl != 0 || c >= C) return false;
+  s1 = red[0][cl] + red[0][cl + 64] + red[0][cl + 128] + red[0][cl + 192];
+  s2 = red[1][cl] + red[1][cl + 64] + red[1][cl + 128] + red[1][cl + 192];
+  return true;
+}
+
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* ws, int S, long M, int C, const float* gamma,
+                                                          const float* beta, float eps, float momentum, float* rmean,
+                                                          float* rvar, float* smean, float* sinv, float* scale,
+                                                          float* shift) {
+  int c;
+  double s1, s2;
+  if (!sum_partials(ws, S, C, c, s1, s2)) return;
   const double mean = s1 / (double)M;
   double var = s2 / (double)M - mean * mean;
   if (var < 0) var = 0;
@@ -134,11 +179,11 @@ __global__ void bn_finalize_kernel(const float* ws, long M, int C, const float* 
   }
 }
 
-int bn_finalize(const float* ws, long M, int C, const float* gamma, const float* beta, float eps, float momentum,
-                float* running_mean, float* running_var, float* save_mean, float* save_invstd, float* scale,
-                float* shift, hipStream_t s) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, M, C, gamma, beta, eps, momentum,
-                     running_mean, running_var, save_mean, save_invstd, scale, shift);
+int bn_finalize(const float* ws, int S, long M, int C, const float* gamma, const float* beta, float eps,
+                float momentum, float* running_mean, float* running_var, float* save_mean, float* save_invstd,
+                float* scale, float* shift, hipStream_t s) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, s, ws, S, M, C, gamma, beta, eps,
+                     momentum, running_mean, running_var, save_mean, save_invstd, scale, shift);
   return (int)hipGetLastError();
 }
 
@@ -286,15 +331,14 @@ int bn_bwd_reduce(const void* dy, const void* x, const void* y, const float* sca
 
 // coef[c] = A, coef[C+c] = B, coef[2C+c] = K with dx = A*dy' + B*x + K
 //   (= gamma*invstd * (dy' - mean(dy') - xhat * mean(dy'*xhat)))
-__global__ void bn_bwd_finalize_kernel(const float* ws, long M, int C, const float* gamma, const float* mean,
-                                       const float* invstd, float* dgamma, float* dbeta, float* coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float s1 = 0.f, s2 = 0.f;
-  for (int k = 0; k < kBnShards; ++k) {
-    s1 += ws[(long)k * 2 * C + c];
-    s2 += ws[(long)k * 2 * C + C + c];
-  }
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* ws, int S, long M, int C,
+                                                              const float* gamma, const float* mean,
+                                                              const float* invstd, float* dgamma, float* dbeta,
+                                                              float* coef) {
+  int c;
+  double d1, d2;
+  if (!sum_partials(ws, S, C, c, d1, d2)) return;
+  float s1 = (float)d1, s2 = (float)d2;
   const float inv = invstd[c];
   s2 *= inv;  // sum dy' * xhat
   if (dbeta) dbeta[c] += s1;
@@ -307,9 +351,9 @@ __global__ void bn_bwd_finalize_kernel(const float* ws, long M, int C, const flo
   coef[2 * C + c] = -A * m1 + A * m2 * inv * mean[c];
 }
 
-int bn_bwd_finalize(const float* ws, long M, int C, const float* gamma, const float* mean, const float* invstd,
+int bn_bwd_finalize(const float* ws, int S, long M, int C, const float* gamma, const float* mean, const float* invstd,
                     float* dgamma, float* dbeta, float* coef, hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, M, C, gamma, mean, invstd,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, s, ws, S, M, C, gamma, mean, invstd,
                      dgamma, dbeta, coef);
   return (int)hipGetLastError();
 }

@@ -32,21 +32,26 @@ T* optr(const c10::optional<at::Tensor>& t) {
 void bn_stats_(const at::Tensor& x, const at::Tensor& ws, int64_t C) {
   GPU(x); BF16(x); F32(ws);
   CK(C % 8 == 0 && x.numel() % C == 0, "bn_stats: C % 8 and numel % C");
-  CK(ws.numel() >= (int64_t)kBnShards * 2 * C, "bn_stats: workspace too small");
+  CK(ws.numel() >= (int64_t)bn_partial_rows(x.numel() / C, (int)C) * 2 * C, "bn_stats: workspace too small");
   at::DeviceGuard g(x.device());
   HIP_OK(bn_stats(x.data_ptr(), ws.data_ptr<float>(), x.numel() / C, (int)C, cur_stream()));
 }
 
+int64_t bn_partial_rows_(int64_t M, int64_t C) { return bn_partial_rows(M, (int)C); }
+
+// S (partial rows) = ws.numel() / (2C)
 void bn_finalize_(const at::Tensor& ws, int64_t M, int64_t C, c10::optional<at::Tensor> gamma,
                   c10::optional<at::Tensor> beta, double eps, double momentum, c10::optional<at::Tensor> rmean,
                   c10::optional<at::Tensor> rvar, const at::Tensor& smean, const at::Tensor& sinv,
                   const at::Tensor& scale, const at::Tensor& shift) {
   GPU(ws); F32(ws); F32(smean); F32(sinv); F32(scale); F32(shift);
   CK(smean.numel() >= C && sinv.numel() >= C && scale.numel() >= C && shift.numel() >= C, "bn_finalize: sizes");
+  CK(ws.numel() % (2 * C) == 0, "bn_finalize: ws must be [S][2][C]");
   at::DeviceGuard g(ws.device());
-  HIP_OK(bn_finalize(ws.data_ptr<float>(), M, (int)C, optr<const float>(gamma), optr<const float>(beta), (float)eps,
-                     (float)momentum, optr<float>(rmean), optr<float>(rvar), smean.data_ptr<float>(),
-                     sinv.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(), cur_stream()));
+  HIP_OK(bn_finalize(ws.data_ptr<float>(), (int)(ws.numel() / (2 * C)), M, (int)C, optr<const float>(gamma),
+                     optr<const float>(beta), (float)eps, (float)momentum, optr<float>(rmean), optr<float>(rvar),
+                     smean.data_ptr<float>(), sinv.data_ptr<float>(), scale.data_ptr<float>(),
+                     shift.data_ptr<float>(), cur_stream()));
 }
 
 void bn_apply_(const at::Tensor& x, const at::Tensor& scale, const at::Tensor& shift, c10::optional<at::Tensor> resid,
@@ -67,7 +72,7 @@ void bn_bwd_reduce_(const at::Tensor& dy, const at::Tensor& x, c10::optional<at:
   CK(dy.numel() == x.numel() && x.numel() % C == 0 && C % 8 == 0, "bn_bwd_reduce: shapes");
   if (mode == 1) { CK(y.has_value(), "mode 1 needs y"); BF16(*y); CK(y->numel() == x.numel(), "bn_bwd_reduce: y shape"); }
   if (mode == 2) { CK(scale.has_value() && shift.has_value(), "mode 2 needs scale/shift"); F32(*scale); F32(*shift); }
-  CK(ws.numel() >= (int64_t)kBnShards * 2 * C, "bn_bwd_reduce: workspace too small");
+  CK(ws.numel() >= (int64_t)bn_partial_rows(x.numel() / C, (int)C) * 2 * C, "bn_bwd_reduce: workspace too small");
   at::DeviceGuard g(x.device());
   HIP_OK(bn_bwd_reduce(dy.data_ptr(), x.data_ptr(), optr<const void>(y), optr<const float>(scale),
                        optr<const float>(shift), mean.data_ptr<float>(), ws.data_ptr<float>(), x.numel() / C, (int)C,
@@ -79,8 +84,9 @@ void bn_bwd_finalize_(const at::Tensor& ws, int64_t M, int64_t C, c10::optional<
                       c10::optional<at::Tensor> dbeta, const at::Tensor& coef) {
   GPU(ws); F32(ws); F32(mean); F32(invstd); F32(coef);
   CK(coef.numel() >= 3 * C, "bn_bwd_finalize: coef size");
+  CK(ws.numel() % (2 * C) == 0, "bn_bwd_finalize: ws must be [S][2][C]");
   at::DeviceGuard g(ws.device());
-  HIP_OK(bn_bwd_finalize(ws.data_ptr<float>(), M, (int)C, optr<const float>(gamma), mean.data_ptr<float>(),
+  HIP_OK(bn_bwd_finalize(ws.data_ptr<float>(), (int)(ws.numel() / (2 * C)), M, (int)C, optr<const float>(gamma), mean.data_ptr<float>(),
                          invstd.data_ptr<float>(), optr<float>(dgamma), optr<float>(dbeta), coef.data_ptr<float>(),
                          cur_stream()));
 }
@@ -275,6 +281,7 @@ void sumsq_(const at::Tensor& x, const at::Tensor& out) {
 void register_ops(py::module& m) {
   m.attr("BN_SHARDS") = (int)kBnShards;
   m.def("bn_stats", &bn_stats_);
+  m.def("bn_partial_rows", &bn_partial_rows_);
   m.def("bn_finalize", &bn_finalize_);
   m.def("bn_apply", &bn_apply_);
   m.def("bn_bwd_reduce", &bn_bwd_reduce_);

@@ -18,6 +18,12 @@ from .layers import BatchNormalization, Conv2D, Dense, Flatten, MaxPooling2D
 from ..ops import pool as pool_ops
 
 
+def _fused() -> bool:
+    import os
+
+    return os.environ.get("DDL_FUSED_BLOCKS", "1") != "0"
+
+
 class ConvBN(Layer):
     """conv(no bias) -> BN (training stats fused into the conv epilogue) -> [+resid] -> [ReLU]."""
 
@@ -85,6 +91,10 @@ class Bottleneck(Layer):
         return ((H - 1) // st + 1, (W - 1) // st + 1, self.width * self.expansion)
 
     def call(self, x, training=False):
+        if training and use_native(x) and _fused():  # whole block as one hand-scheduled node (ops/fused_blocks.py)
+            from ..ops.fused_blocks import bottleneck
+
+            return bottleneck(self, x, self.c1.conv.kernel.data)
         sc = self.down.call(x, training) if self.down else x
         y = self.c1.call(x, training)
         y = self.c2.call(y, training)
@@ -131,7 +141,12 @@ class ResNet(Model):
         return True
 
     def forward(self, x, training=False, logits=False):
-        y = self.stem.call(x, training)
+        if training and use_native(x) and _fused():
+            from ..ops.fused_blocks import convbn_relu
+
+            y = convbn_relu(self.stem, x, self.stem.conv.kernel.data)
+        else:
+            y = self.stem.call(x, training)
         y = pool_ops.max_pool2d(y, 3, 2, 1)
         for b in self.stages:
             y = b.call(y, training)

@@ -1,0 +1,187 @@
+"""Fused ResNet bottleneck (GPU): the whole conv-BN-ReLU x3 + shortcut block is ONE
+autograd node whose backward is scheduled by hand.
+
+What the fusion buys over composing per-op autograd nodes:
+  * the block-input gradient ``dX = dgrad(conv1) + dShortcut`` is produced by the
+    conv1 data-gradient GEMM epilogue (residual add), instead of a separate add kernel;
+  * every BN uses the statistics the producing conv's epilogue accumulated;
+  * the BN backward ReLU masks are recomputed from the conv outputs (mode 2) except
+    where a residual enters (mode 1), so no extra activation tensor is read;
+  * all workspaces come from the per-step statistics pool;
+  * parameter-gradient hooks (for the overlapped RCCL all-reduce) fire per layer in
+    backward order as soon as each layer's gradients are final.
+Reference semantics are unchanged: ``relu(bn3(conv3(relu(bn2(conv2(relu(bn1(conv1 x))))))) + sc(x))``.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import conv as CV
+from . import gemm as G
+from ._native import C
+from .norm import new_stats_workspace, partials_workspace
+
+
+class _ConvBNState:
+    """Per-(conv,BN) forward results needed by the backward."""
+
+    __slots__ = ("g", "yc", "y", "mean", "invstd", "scale", "shift", "mode")
+
+
+def _bn_forward(layer_bn, yc, stats, resid, relu, training):
+    Cc = yc.shape[-1]
+    M = yc.numel() // Cc
+    dev = yc.device
+    bn = layer_bn
+    gamma = None if bn.gamma is None else bn.gamma.master
+    beta = None if bn.beta is None else bn.beta.master
+    rm, rv = bn._states["moving_mean"], bn._states["moving_variance"]
+    scale = torch.empty(Cc, dtype=torch.float32, device=dev)
+    shift = torch.empty(Cc, dtype=torch.float32, device=dev)
+    mean = torch.empty(Cc, dtype=torch.float32, device=dev)
+    invstd = torch.empty(Cc, dtype=torch.float32, device=dev)
+    C().bn_finalize(stats, M, Cc, gamma, beta, bn.epsilon, 1.0 - bn.momentum, rm, rv, mean, invstd, scale, shift)
+    y = torch.empty_like(yc)
+    C().bn_apply(yc, scale, shift, resid, y, Cc, relu)
+    return y, mean, invstd, scale, shift
+
+
+def convbn_forward(unit, x, resid=None, relu=True):
+    """conv (fused statistics) + BN (+resid)(+relu) for a ``models.resnet.ConvBN`` unit."""
+    conv, bn = unit.conv, unit.bn
+    N, H, W, Ci = x.shape
+    kh, kw = conv.kernel_size
+    p = conv.padding if isinstance(conv.padding, tuple) else (kh // 2, kw // 2)
+    g = CV.geometry(N, H, W, Ci, conv.filters, kh, kw, conv.strides, p, conv.dilation_rate)
+    stats = new_stats_workspace(conv.filters, x.device)
+    yc = CV.conv_fwd_native(x, conv.kernel.data, g, stats=stats)
+    st = _ConvBNState()
+    st.g, st.yc = g, yc
+    st.y, st.mean, st.invstd, st.scale, st.shift = _bn_forward(bn, yc, stats, resid, relu, True)
+    st.mode = 0 if not relu else (1 if resid is not None else 2)
+    return st
+
+
+def bn_backward(unit, st, dy, want_dres):
+    bn = unit.bn
+    Cc = st.yc.shape[-1]
+    M = st.yc.numel() // Cc
+    ws = partials_workspace(M, Cc, dy.device)
+    y = st.y if st.mode == 1 else None
+    C().bn_bwd_reduce(dy, st.yc, y, st.scale, st.shift, st.mean, ws, Cc, st.mode)
+    coef = torch.empty(3 * Cc, dtype=torch.float32, device=dy.device)
+    C().bn_bwd_finalize(ws, M, Cc, None if bn.gamma is None else bn.gamma.master, st.mean, st.invstd,
+                        None if bn.gamma is None else bn.gamma.grad, None if bn.beta is None else bn.beta.grad, coef)
+    dyc = torch.empty_like(dy)
+    dres = torch.empty_like(dy) if want_dres else None
+    C().bn_bwd_dx(dy, st.yc, y, st.scale, st.shift, coef, dyc, dres, Cc, st.mode)
+    if bn.grad_hook is not None:
+        bn.grad_hook()
+    return dyc, dres
+
+
+def conv_backward(unit, st, dyc, x, need_dx, resid=None):
+    conv = unit.conv
+    CV.conv_wgrad_native(dyc, x, st.g, conv.kernel.grad)
+    if conv.grad_hook is not None:
+        conv.grad_hook()
+    if not need_dx:
+        return None
+    return CV.conv_dgrad_native(dyc, conv.kernel.data, st.g, resid=resid)
+
+
+class _BottleneckFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, block):
+        x = x.contiguous()
+        s_down = convbn_forward(block.down, x, relu=False) if block.down is not None else None
+        sc = s_down.y if s_down is not None else x
+        s1 = convbn_forward(block.c1, x, relu=True)
+        s2 = convbn_forward(block.c2, s1.y, relu=True)
+        s3 = convbn_forward(block.c3, s2.y, resid=sc, relu=True)
+        ctx.block, ctx.states = block, (s_down, s1, s2, s3)
+        ctx.save_for_backward(x)
+        ctx.needs_dx = ctx.needs_input_grad[0]
+        return s3.y
+
+    @staticmethod
+    def backward(ctx, dout):
+        (x,) = ctx.saved_tensors
+        b = ctx.block
+        s_down, s1, s2, s3 = ctx.states
+        dout = dout.contiguous()
+        d3c, dsc = bn_backward(b.c3, s3, dout, want_dres=True)
+        d2 = conv_backward(b.c3, s3, d3c, s2.y, True)
+        d2c, _ = bn_backward(b.c2, s2, d2, False)
+        d1 = conv_backward(b.c2, s2, d2c, s1.y, True)
+        d1c, _ = bn_backward(b.c1, s1, d1, False)
+        if s_down is not None:
+            ddc, _ = bn_backward(b.down, s_down, dsc, False)
+            dsc = conv_backward(b.down, s_down, ddc, x, ctx.needs_dx)
+        # dX = dgrad(conv1) + dShortcut: the residual add rides in the conv1 dgrad epilogue
+        dx = conv_backward(b.c1, s1, d1c, x, ctx.needs_dx, resid=dsc)
+        ctx.states = None
+        return dx, None, None
+
+
+def bottleneck(block, x, anchor):
+    """``anchor``: any parameter view requiring grad (makes the node part of the graph)."""
+    return _BottleneckFn.apply(x, anchor, block)
+
+
+def convbn_relu(unit, x, anchor, relu=True):
+    """Single fused conv+BN(+ReLU) unit as one autograd node (the ResNet stem)."""
+    return _ConvBNFn.apply(x, anchor, unit, relu)
+
+
+class _ConvBNFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, unit, relu):
+        x = x.contiguous()
+        Ci = x.shape[-1]
+        ctx.ci = Ci
+        if Ci % 8:  # stem: pad 3 -> 8 channels (16-B vectors)
+            cp = -(-Ci // 8) * 8
+            x = torch.nn.functional.pad(x, (0, cp - Ci))
+            w = torch.nn.functional.pad(unit.conv.kernel.data.detach(), (0, cp - Ci))
+        else:
+            w = unit.conv.kernel.data
+        conv = unit.conv
+        N, H, W, Cp = x.shape
+        kh, kw = conv.kernel_size
+        p = conv.padding if isinstance(conv.padding, tuple) else (kh // 2, kw // 2)
+        g = CV.geometry(N, H, W, Cp, conv.filters, kh, kw, conv.strides, p, conv.dilation_rate)
+        stats = new_stats_workspace(conv.filters, x.device)
+        yc = CV.conv_fwd_native(x, w, g, stats=stats)
+        st = _ConvBNState()
+        st.g, st.yc = g, yc
+        st.y, st.mean, st.invstd, st.scale, st.shift = _bn_forward(unit.bn, yc, stats, None, relu, True)
+        st.mode = 2 if relu else 0
+        ctx.unit, ctx.st, ctx.w = unit, st, w
+        ctx.save_for_backward(x)
+        ctx.needs_dx = ctx.needs_input_grad[0]
+        return st.y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        unit, st = ctx.unit, ctx.st
+        dyc, _ = bn_backward(unit, st, dy.contiguous(), False)
+        conv = unit.conv
+        g = st.g
+        if g.Ci != ctx.ci:
+            tmp = torch.zeros((g.Co, g.KH, g.KW, g.Ci), dtype=torch.float32, device=dy.device)
+            CV.conv_wgrad_native(dyc, x, g, tmp)
+            conv.kernel.grad.add_(tmp[..., : ctx.ci])
+        else:
+            CV.conv_wgrad_native(dyc, x, g, conv.kernel.grad)
+        if conv.grad_hook is not None:
+            conv.grad_hook()
+        dx = None
+        if ctx.needs_dx:
+            dx = CV.conv_dgrad_native(dyc, ctx.w, g)[..., : ctx.ci].contiguous()
+        ctx.st = None
+        return dx, None, None, None
+
+
+_ = G

@@ -57,6 +57,11 @@ def new_stats_workspace(C_, device):
     return torch.zeros((SHARDS, 2, C_), dtype=torch.float32, device=device)
 
 
+def partials_workspace(M, C_, device):
+    """[S, 2, C] partial-sum rows written (not accumulated) by a bn_stats / bn_bwd_reduce sweep."""
+    return torch.empty((C().bn_partial_rows(M, C_), 2, C_), dtype=torch.float32, device=device)
+
+
 def reset_workspaces(device):
     """Call once per training step before the forward (zeroes all statistics workspaces)."""
     if torch.device(device).type == "cuda":
@@ -101,7 +106,7 @@ class _BatchNormFn(torch.autograd.Function):
             invstd = torch.empty(Cc, dtype=torch.float32, device=dev)
             if training:
                 if stats is None:
-                    stats = new_stats_workspace(Cc, dev)
+                    stats = partials_workspace(M, Cc, dev)
                     C().bn_stats(x, stats, Cc)
                 C().bn_finalize(stats, M, Cc, gamma, beta, eps, momentum, rmean, rvar, mean, invstd, scale, shift)
             else:
@@ -157,7 +162,7 @@ class _BatchNormFn(torch.autograd.Function):
                 dx = (d * scale).to(x.dtype)
                 dres = d.to(x.dtype) if ctx.has_resid else None
             else:
-                ws = new_stats_workspace(Cc, x.device)
+                ws = partials_workspace(M, Cc, x.device)
                 C().bn_bwd_reduce(dy, x, y, scale, shift, mean, ws, Cc, ctx.mode)
                 coef = torch.empty(3 * Cc, dtype=torch.float32, device=x.device)
                 C().bn_bwd_finalize(ws, M, Cc, gamma, mean, invstd, ggamma, gbeta, coef)

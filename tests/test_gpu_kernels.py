@@ -353,3 +353,28 @@ def test_resnet50_step_matches_reference():
     assert abs(lh - lc) < 0.12 * max(1.0, abs(lc)), res
     assert abs(ll - lc) < 0.12 * max(1.0, abs(lc)), res
     assert abs(gh - gc) < 0.1 * gc, res
+
+
+def test_fused_bottleneck_matches_composed_ops():
+    """ops/fused_blocks.py (one autograd node per block) vs the per-op autograd graph."""
+    import os
+
+    from distributeddeeplearningspark_amd.models import ResNet50
+
+    torch.manual_seed(1)
+    x = torch.randn(8, 64, 64, 3)
+    y = torch.randint(0, 10, (8,))
+    res = {}
+    for fused in ("1", "0"):
+        os.environ["DDL_FUSED_BLOCKS"] = fused
+        try:
+            m = ResNet50(input_shape=(64, 64, 3), num_classes=10)
+            m.compile("sgd", "sparse_categorical_crossentropy")
+            m.place(DEV, seed=5)
+            loss = m.backward_step(m.to_input(x), m.to_target(y))
+            res[fused] = (float(loss), m.arena.grad.clone())
+        finally:
+            os.environ.pop("DDL_FUSED_BLOCKS", None)
+    assert abs(res["1"][0] - res["0"][0]) < 1e-3 * max(1.0, abs(res["0"][0])), (res["1"][0], res["0"][0])
+    g1, g0 = res["1"][1], res["0"][1]
+    assert ((g1 - g0).norm() / g0.norm()).item() < 2e-2

@@ -15,6 +15,8 @@ from distributeddeeplearningspark_amd.sql.types import TimestampType
 
 @pytest.fixture(scope="module")
 def spark():
+    if SparkSession._active is not None:
+        SparkSession._active.stop()
     conf = SparkConf().set("spark.master", "local[2]").set("spark.executor.instances", 2).set("spark.executor.cores", 2)
     sc = SparkContext(conf=conf)
     s = SparkSession.builder.getOrCreate()
