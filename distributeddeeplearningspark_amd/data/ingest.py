@@ -84,3 +84,66 @@ class SyntheticImageStream:
         self.i = (self.i + 1) % len(self.xs)
         self.feeder.submit(self.xs[self.i], self.ys[self.i])  # prefetch the next batch under this step
         return x, y
+
+
+class ShardLoader:
+    """Epoch iterator over a resident host shard, assembled by the native ``BatchLoader``
+    (``csrc/runtime/loader.cpp``): a C++ thread gathers (optionally shuffled) rows into a
+    ring of pinned buffers while the previous batch trains; each batch is copied to the
+    device on a side stream.  Replaces the reference's per-row Python mini-batch assembly
+    (``X = [row[features_col]]``, SURVEY §3.3 hot loop 3).
+
+    Yields ``(x, y)`` device tensors; ``x`` is cast to ``x_dtype`` on the device.
+    """
+
+    def __init__(self, x: np.ndarray, y: np.ndarray | None, batch: int, device="cpu", shuffle=False, seed=0,
+                 drop_last=True, n_buffers=4, threads=4, x_dtype=None):
+        from ..ops._native import C
+
+        self.x = torch.from_numpy(np.ascontiguousarray(x))
+        self.y = None if y is None else torch.from_numpy(np.ascontiguousarray(y))
+        self.batch, self.device = int(batch), torch.device(device)
+        self.x_dtype = x_dtype
+        self._impl = C().BatchLoader(self.x, self.y, self.batch, bool(shuffle), int(seed), bool(drop_last),
+                                     int(threads))
+        pin = self.device.type == "cuda"
+
+        def buf(t):
+            b = torch.empty((self.batch,) + tuple(t.shape[1:]), dtype=t.dtype)
+            return b.pin_memory() if pin else b
+
+        self._xb = [buf(self.x) for _ in range(n_buffers)]
+        self._yb = [buf(self.y) for _ in range(n_buffers)] if self.y is not None else []
+        self._impl.set_buffers(self._xb, self._yb)
+        self._stream = torch.cuda.Stream(self.device) if pin else None
+        self.epoch = 0
+
+    def __len__(self):
+        return self._impl.batches_per_epoch
+
+    def _to_device(self, t, n):
+        t = t[:n]
+        if self._stream is None:
+            return t.clone()
+        with torch.cuda.stream(self._stream):
+            d = t.to(self.device, non_blocking=True)
+        return d
+
+    def __iter__(self):
+        self._impl.start_epoch(self.epoch)
+        self.epoch += 1
+        while True:
+            slot, n = self._impl.next()
+            if slot < 0:
+                return
+            xd = self._to_device(self._xb[slot], n)
+            yd = self._to_device(self._yb[slot], n) if self._yb else None
+            if self._stream is not None:
+                ev = torch.cuda.Event()
+                ev.record(self._stream)
+                torch.cuda.current_stream(self.device).wait_event(ev)
+                ev.synchronize()  # slot may be refilled only after its H2D copy landed
+            self._impl.release(slot)
+            if self.x_dtype is not None and xd.is_floating_point():
+                xd = xd.to(self.x_dtype)
+            yield xd, yd

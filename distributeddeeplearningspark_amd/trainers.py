@@ -30,7 +30,11 @@ Execution (MI355X-native, not a socket parameter server):
       SingleTrainer      one worker on the coalesced frame
       SynchronousDataParallel (new)  per-step bucketed gradient all-reduce, overlapped
     These are the synchronous equivalents of dist-keras' asynchronous commits
-    (documented deviation: no stale updates are applied).
+    (no stale updates are applied in the default ``mode="sync"``).
+  * ``mode="async"`` (constructor kwarg) reproduces the reference's true asynchrony:
+    the driver hosts the native C++ TCP parameter server (``parallel/ps.py``,
+    ``csrc/runtime/param_server.cpp``) and workers pull/commit without barriers; DynSGD's
+    ``1/(staleness+1)`` scaling is then applied server-side from real staleness.
 """
 from __future__ import annotations
 
@@ -139,6 +143,62 @@ class _CommitWorker(_Worker):
             DataParallel.all_reduce_flat_(_FlatReducer(self.pg), t)
 
 
+class _AsyncPSWorker(_Worker):
+    """True asynchronous worker against the native parameter server (``mode="async"``):
+    pull -> train ``communication_window`` batches -> commit residual -> pull, with no
+    barrier between workers (reference ``distkeras/workers.py`` ADAGWorker/DynSGDWorker
+    optimize loop).  Rules:
+      adag      residual = (W - W_anchor) / window
+      dynsgd    residual = (W - W_anchor), the server scales by 1/(staleness+1)
+      downpour  residual = (W - W_anchor)
+      easgd*    E = alpha * (W - center); W -= E; commit E
+    """
+
+    def num_updates(self):
+        return self._n
+
+    def run(self, X, Y):
+        from .parallel.ps import ParameterServerClient
+
+        a, algo, k = self.arena, self.cfg["algorithm"], self.k
+        W = a.master.detach()
+        cli = ParameterServerClient(self.cfg["ps_port"], self.pg.rank, W.numel())
+        self._n = 0
+        try:
+            def pull():
+                with torch.no_grad():
+                    W.copy_(cli.pull().to(W.device))
+                    a.sync_compute()
+                return W.clone()
+
+            anchor = pull()
+            it = 0
+            for xb, yb in self.batches(X, Y):
+                self.history.append(self.model.train_on_batch(xb, yb))
+                it += 1
+                if it % k:
+                    continue
+                with torch.no_grad():
+                    if algo in ("easgd", "aeasgd", "eamsgd"):
+                        e = (W - anchor) * self.cfg["alpha"]
+                        W.sub_(e)
+                        cli.commit(e)
+                    else:
+                        r = W - anchor
+                        if algo == "adag":
+                            r.div_(k)
+                        cli.commit(r)
+                self._n += 1
+                if algo in ("easgd", "aeasgd", "eamsgd"):
+                    anchor = cli.pull().to(W.device).clone()  # elastic: keep local weights, refresh center
+                    a.sync_compute()
+                else:
+                    anchor = pull()
+        finally:
+            cli.close()
+        return W.clone()
+
+
 class _FlatReducer:
     """Minimal object to reuse DataParallel.all_reduce_flat_ without hooks."""
 
@@ -233,7 +293,10 @@ def _train_worker(rank, world, pg, cfg, blob, X, Y, sizes):
     if blob.get("states"):
         set_states(model, blob["states"])
     Xd, Yd = _to_device(X, model), _to_device(Y, model)
-    w = _WORKERS[cfg["algorithm"]](cfg, model, pg, sizes)
+    cls = _WORKERS[cfg["algorithm"]]
+    if cfg.get("mode") == "async" and issubclass(cls, _CommitWorker):
+        cls = _AsyncPSWorker
+    w = cls(cfg, model, pg, sizes)
     final = w.run(Xd, Yd)
     if model.device.type == "cuda":
         torch.cuda.synchronize(model.device)
@@ -351,18 +414,46 @@ class _ShardedTrainer(Trainer):
         Xs, Ys = self._shards(dataframe, shuffle)
         sizes = [x.shape[0] for x in Xs]
         cfg = self._cfg()
-        args = [(cfg, self.master_model, Xs[r], Ys[r], sizes) for r in range(self.num_workers)]
-        results = run_workers(_train_worker, self.num_workers, args, device=self.device)
+        server = None
+        if cfg.get("mode") == "async" and issubclass(_WORKERS[self.algorithm], _CommitWorker):
+            server = self._start_async_server(cfg)
+        try:
+            args = [(cfg, self.master_model, Xs[r], Ys[r], sizes) for r in range(self.num_workers)]
+            results = run_workers(_train_worker, self.num_workers, args, device=self.device)
+        finally:
+            if server is not None:
+                center, n_upd = server.center().numpy().copy(), server.num_updates
+                server.stop()
         self.history = [r["history"] for r in results]
         ps = self.parameter_server
-        ps.num_updates = int(results[0]["num_updates"])
-        ps.center = results[0]["flat"]
+        if server is not None:  # the driver-hosted center is the trained model
+            ps.num_updates, ps.center = int(n_upd), center
+        else:
+            ps.num_updates = int(results[0]["num_updates"])
+            ps.center = results[0]["flat"]
         ps.states = results[0].get("states")
         self.worker_times = [r["time"] for r in results]
         self._results = results
         model = ps.get_model()
         self.record_training_end()
         return model
+
+
+    def _start_async_server(self, cfg):
+        """Host the native parameter server on the driver (single node, 127.0.0.1)."""
+        import os
+
+        from .parallel.ps import RULE_ADD, RULE_DYNSGD, ParameterServerProcess
+
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            raise NotImplementedError("mode='async' runs workers from the driver; under torchrun use mode='sync'")
+        blob = {k: v for k, v in self.master_model.items() if k not in ("optimizer", "loss")}
+        m = deserialize_keras_model(blob, device="cpu")
+        rule = RULE_DYNSGD if self.algorithm == "dynsgd" else RULE_ADD
+        server = ParameterServerProcess(m.arena.master.detach(), rule=rule,
+                                        port=int(self.extra.get("ps_port", 0)))
+        cfg["ps_port"] = server.port
+        return server
 
 
 class SingleTrainer(_ShardedTrainer):

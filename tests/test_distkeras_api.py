@@ -232,3 +232,74 @@ def test_single_averaging_ensemble_syncdp(spark):
     sd = SynchronousDataParallel(keras_model=mnist_cnn(), num_workers=2, **common)
     sd.train(df.repartition(2))
     assert sd.parameter_server.num_updates == 5
+
+
+# ------------------------------------------------------------------ native async parameter server
+def test_native_param_server_protocol():
+    """commit/pull framing, ADD vs DynSGD staleness rule (center += r / (staleness + 1))."""
+    import torch
+
+    from distributeddeeplearningspark_amd.parallel.ps import (RULE_ADD, RULE_DYNSGD, ParameterServerClient,
+                                                              ParameterServerProcess)
+
+    init = torch.arange(6, dtype=torch.float32)
+    with ParameterServerProcess(init, rule=RULE_ADD) as ps:
+        a = ParameterServerClient(ps.port, 0, 6)
+        b = ParameterServerClient(ps.port, 1, 6)
+        assert torch.equal(a.pull(), init) and a.last_update == 0
+        a.commit(torch.ones(6))
+        b.commit(torch.full((6,), 2.0))
+        assert torch.equal(b.pull(), init + 3) and b.last_update == 2
+        a.close(), b.close()
+        assert ps.num_updates == 2 and torch.equal(ps.center(), init + 3)
+    with ParameterServerProcess(torch.zeros(4), rule=RULE_DYNSGD) as ps:
+        a = ParameterServerClient(ps.port, 0, 4)
+        b = ParameterServerClient(ps.port, 1, 4)
+        a.pull(), b.pull()  # both at update 0
+        a.commit(torch.ones(4))  # staleness 0 -> +1
+        b.commit(torch.ones(4))  # staleness 1 -> +1/2
+        np.testing.assert_allclose(ps.center().numpy(), 1.5)
+        a.close(), b.close()
+
+
+def test_async_adag_single_worker_matches_simulation(spark):
+    """One async worker: pull -> k steps -> commit (W - anchor)/k -> pull, exactly."""
+    from distributeddeeplearningspark_amd.trainers import ADAG
+
+    rng = np.random.default_rng(1)
+    x = rng.normal(size=(24, 3)).astype(np.float32)
+    y = x.sum(1, keepdims=True).astype(np.float32)
+    df = spark.createDataFrame({"f": list(x), "l": list(y)}).repartition(1)
+    base = Sequential([Dense(1, input_shape=(3,))])
+    w0 = base.get_weights()
+    tr = ADAG(keras_model=base, worker_optimizer="sgd", loss="mean_squared_error", num_workers=1, batch_size=4,
+              communication_window=3, num_epoch=1, features_col="f", label_col="l", device="cpu", mode="async")
+    out = tr.train(df).get_weights()
+    m = Sequential([Dense(1, input_shape=(3,))])
+    m.compile("sgd", "mean_squared_error")
+    center = [w.copy() for w in w0]
+    for rnd in range(2):
+        m.set_weights(center)
+        for b in range(3):
+            i = (rnd * 3 + b) * 4
+            m.train_on_batch(x[i:i + 4], y[i:i + 4])
+        center = [c + (a - c) / 3 for a, c in zip(m.get_weights(), center)]
+    for a, b in zip(out, center):
+        np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-6)
+    assert tr.parameter_server.num_updates == 2
+
+
+@pytest.mark.parametrize("algo", ["DynSGD", "DOWNPOUR"])
+def test_async_two_workers_train(spark, algo):
+    from distributeddeeplearningspark_amd import trainers as T
+
+    df = _mnist_frame(spark, 400).repartition(2)
+    tr = getattr(T, algo)(keras_model=mnist_cnn(), worker_optimizer="adam", loss="categorical_crossentropy",
+                          num_workers=2, batch_size=16, communication_window=5, num_epoch=2, features_col="matrix",
+                          label_col="label_encoded", device="cpu", mode="async")
+    model = tr.train(df)
+    assert tr.parameter_server.num_updates == 2 * ((2 * (200 // 16)) // 5)
+    pred = ModelPredictor(keras_model=model, features_col="matrix").predict(df)
+    pred = LabelIndexTransformer(output_dim=10).transform(pred)
+    acc = AccuracyEvaluator(prediction_col="prediction_index", label_col="label").evaluate(pred)
+    assert acc > 0.5, acc
