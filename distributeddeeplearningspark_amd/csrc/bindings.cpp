@@ -52,9 +52,9 @@ void fill_geom(ConvGeom& g, const py::dict& d) {
 void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t M, int64_t N, int64_t K,
           int64_t a_mode, int64_t b_mode, int64_t lda, int64_t ldb, int64_t ldc, int64_t epi, int64_t tile,
           int64_t k_split, double alpha, double beta, c10::optional<at::Tensor> bias,
-          c10::optional<at::Tensor> resid, int64_t ldr, bool relu, c10::optional<py::dict> geom,
+          c10::optional<at::Tensor> resid, int64_t ldr, int64_t relu, c10::optional<py::dict> geom,
           c10::optional<py::dict> outmap, int64_t b_kdiv, int64_t b_tap_stride,
-          c10::optional<at::Tensor> stats) {
+          c10::optional<at::Tensor> stats, c10::optional<at::Tensor> aux, double drop_p, int64_t drop_seed) {
   CHECK_CUDA(a);
   CHECK_CUDA(b);
   CHECK_CUDA(c);
@@ -92,7 +92,22 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
   p.b_tap_stride = b_tap_stride;
   p.alpha = (float)alpha;
   p.beta = (float)beta;
-  p.relu = relu ? 1 : 0;
+  TORCH_CHECK(relu >= ACT_NONE && relu <= ACT_GELU_BWD, "gemm: bad activation code");
+  TORCH_CHECK(epi == EPI_BF16 || (relu == 0 && drop_p == 0.0), "gemm: activation/dropout need the bf16 epilogue");
+  p.relu = (int)relu;
+  if (relu >= ACT_GELU) {
+    TORCH_CHECK(aux.has_value(), "gemm: GELU epilogues need the aux (pre-activation) tensor");
+    CHECK_CUDA(*aux);
+    CHECK_BF16(*aux);
+    TORCH_CHECK(aux->numel() >= (M - 1) * ldc + N && ((uintptr_t)aux->data_ptr() % 16) == 0, "gemm: aux size/alignment");
+    p.aux = aux->data_ptr();
+  }
+  TORCH_CHECK(drop_p >= 0.0 && drop_p < 1.0, "gemm: dropout p in [0, 1)");
+  if (drop_p > 0.0) {
+    p.drop_thresh = (uint32_t)std::min(4294967295.0, drop_p * 4294967296.0);
+    p.drop_scale = (float)(1.0 / (1.0 - drop_p));
+    p.drop_seed = (unsigned long long)drop_seed;
+  }
   p.ldr = ldr;
   if (bias) {
     CHECK_CUDA(*bias);
@@ -144,6 +159,7 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
 
 void register_ops(py::module& m);      // ops_bindings.cpp style registrations (elementwise, norms, ...)
 void register_runtime(py::module& m);  // host runtime (parameter server, ingest)
+void register_transformer(py::module& m);  // attention, LayerNorm, embeddings
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "MI355X-native kernels and runtime of distributeddeeplearningspark_amd";
@@ -152,7 +168,12 @@ PYBIND11_MODULE(_C, m) {
         py::arg("ldb"), py::arg("ldc"), py::arg("epi"), py::arg("tile"), py::arg("k_split"), py::arg("alpha") = 1.0,
         py::arg("beta") = 0.0, py::arg("bias") = py::none(), py::arg("resid") = py::none(), py::arg("ldr") = 0,
         py::arg("relu") = false, py::arg("geom") = py::none(), py::arg("outmap") = py::none(),
-        py::arg("b_kdiv") = 0, py::arg("b_tap_stride") = 0, py::arg("stats") = py::none());
+        py::arg("b_kdiv") = 0, py::arg("b_tap_stride") = 0, py::arg("stats") = py::none(),
+        py::arg("aux") = py::none(), py::arg("drop_p") = 0.0, py::arg("drop_seed") = 0);
+  m.attr("ACT_NONE") = (int)ACT_NONE;
+  m.attr("ACT_RELU") = (int)ACT_RELU;
+  m.attr("ACT_GELU") = (int)ACT_GELU;
+  m.attr("ACT_GELU_BWD") = (int)ACT_GELU_BWD;
   m.attr("OP_KC") = (int)OP_KC;
   m.attr("OP_RC") = (int)OP_RC;
   m.attr("OP_KC_GATHER") = (int)OP_KC_GATHER;
@@ -164,5 +185,6 @@ PYBIND11_MODULE(_C, m) {
   m.attr("EPI_F32") = (int)EPI_F32;
   m.attr("EPI_F32_ATOMIC") = (int)EPI_F32_ATOMIC;
   register_ops(m);
+  register_transformer(m);
   register_runtime(m);
 }

@@ -42,6 +42,27 @@ __device__ __forceinline__ float warp_max(float v) {
   return v;
 }
 
+// Counter-based dropout: element `idx` of a call with seed `seed` is kept iff
+// hash(seed + idx) >= thresh (thresh = p * 2^32).  Stateless, so backward passes
+// regenerate the mask instead of storing it.
+__device__ __forceinline__ uint32_t drop_hash(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return (uint32_t)x;
+}
+__device__ __forceinline__ bool drop_keep(uint64_t seed, uint64_t idx, uint32_t thresh) {
+  return drop_hash(seed + idx) >= thresh;
+}
+
+// exact (erf) GELU and its derivative (BERT "gelu")
+__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_grad_f(float x) {
+  return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
+}
+
 // XCD-aware bijective remap of a 1-D block id (MI355X: 8 XCDs, blocks dealt round-robin).
 // Blocks that share an XCD (bid % 8 equal) receive a contiguous range of logical tiles.
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {

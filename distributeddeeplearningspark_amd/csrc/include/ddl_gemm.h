@@ -66,11 +66,22 @@ struct GemmParams {
   const float* bias;
   const void* resid; long ldr;
   float alpha, beta;
+  // bf16 epilogue activation (field name kept from the first version):
+  //   ACT_NONE, ACT_RELU (after the residual add), ACT_GELU (aux <- pre-activation),
+  //   ACT_GELU_BWD (v *= gelu'(aux[m][n]), the data-gradient of a GELU-fused Linear)
   int relu;
   // optional fused per-column batch statistics of the stored bf16 output:
   // stats[shard][0][n] += sum, stats[shard][1][n] += sum of squares (shard = tile % kStatShards)
   float* stats;
+  void* aux;          // bf16 [M][ldc]: pre-activation (ACT_GELU out / ACT_GELU_BWD in)
+  // dropout applied after bias/activation and before the residual add:
+  // keep element (m, n) iff drop_hash(drop_seed + m*N + n) >= drop_thresh, kept values * drop_scale
+  uint32_t drop_thresh;
+  float drop_scale;
+  unsigned long long drop_seed;
 };
+
+enum Activation : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_GELU_BWD = 3 };
 
 constexpr int kStatShards = 32;
 

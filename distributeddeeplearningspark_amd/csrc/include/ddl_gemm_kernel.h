@@ -331,6 +331,32 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] += (n + e < p.N) ? p.bias[n + e] : 0.f;
         }
+        if (p.relu >= ACT_GELU) {  // transformer FFN: GELU fwd (saving the pre-activation) or its gradient
+          bf16_t* ax = reinterpret_cast<bf16_t*>(p.aux) + (long)m * p.ldc + n;
+          if (p.relu == ACT_GELU) {
+            bf16_t pa[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              pa[e] = f2bf(v[e]);
+              v[e] = gelu_f(bf2f(pa[e]));
+            }
+            if (full)
+              *reinterpret_cast<uint2*>(ax) = make_uint2((uint32_t)pa[0] | ((uint32_t)pa[1] << 16),
+                                                         (uint32_t)pa[2] | ((uint32_t)pa[3] << 16));
+            else
+              for (int e = 0; e < 4; ++e)
+                if (n + e < p.N) ax[e] = pa[e];
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] *= (n + e < p.N) ? gelu_grad_f(bf2f(ax[e])) : 0.f;
+          }
+        }
+        if (p.drop_thresh) {
+          const unsigned long long base = (unsigned long long)m * (unsigned long long)p.N + (unsigned long long)n;
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            v[e] = drop_keep(p.drop_seed, base + e, p.drop_thresh) ? v[e] * p.drop_scale : 0.f;
+        }
         if (p.resid) {
           const bf16_t* r = reinterpret_cast<const bf16_t*>(p.resid) + (long)m * p.ldr + n;
           if (full) {
@@ -345,7 +371,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams
               if (n + e < p.N) v[e] += bf2f(r[e]);
           }
         }
-        if (p.relu) {
+        if (p.relu == ACT_RELU) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
         }

@@ -46,7 +46,7 @@ int avgpool_global_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream
 // logits [B, K] (bf16 or fp32), target: class index (int64) OR probability rows (fp32 [B,K]).
 // loss_rows[b] = CE; dlogits = (softmax - target) * grad_scale  (same dtype as logits)
 int softmax_xent(const void* logits, int logits_bf16, const int64_t* labels, const float* target_probs,
-                 float* loss_rows, void* dlogits, int B, int K, float grad_scale, float label_smoothing,
+                 float* loss_rows, void* dlogits, int B, int K, long ld, float grad_scale, float label_smoothing,
                  int ignore_index, hipStream_t s);
 
 // ---------------- elementwise ----------------
@@ -73,5 +73,47 @@ int rmsprop_step(float* w, const float* g, float* acc, void* w16, long n, float 
                  float gscale, hipStream_t s);
 // sum of squares of a flat fp32 buffer into out[0] (for grad-norm clipping / checksums); out must be zeroed
 int sumsq_f32(const float* x, long n, float* out, hipStream_t s);
+
+// ---------------- transformer ops (BERT) ----------------
+// Fused multi-head attention, head dim 64, S % 128 == 0 (kernels/attention.hip).
+struct AttnParams {
+  const uint16_t* qkv; long ld;   // [B*S][ld] bf16, head h of q/k/v at q_off/k_off/v_off + 64h
+  int q_off, k_off, v_off;
+  uint16_t* o; long ldo;          // [B*S][ldo] context, head h at 64h (forward output, backward input)
+  float* lse;                     // [B][H][S] base-2 log-sum-exp of the scaled scores
+  const int* lens;                // [B] valid keys per sequence (nullable)
+  int B, H, S;
+  float scale, scale_log2;        // softmax scale, scale * log2(e)
+  uint32_t drop_thresh;           // attention-probability dropout (0 = off)
+  float drop_scale;
+  unsigned long long drop_seed;
+  // backward only
+  const uint16_t* dout; long lddo;  // dO
+  float* dvec;                      // [B][H][S] scratch: rowsum(dO * O)
+  uint16_t* dqkv; long lddqkv;      // gradient of the qkv buffer (same column layout)
+};
+int attn_fwd(const AttnParams& p, hipStream_t s);
+int attn_bwd(const AttnParams& p, hipStream_t s);
+
+// LayerNorm over rows of x [M][H] bf16 (H % 8 == 0, H <= 4096); gamma/beta fp32; saves mean/rstd.
+// optional output dropout (drop_p > 0; element index row*H + n) — BERT embedding dropout
+int layernorm_fwd(const void* x, const float* gamma, const float* beta, void* y, float* mean, float* rstd, long M,
+                  int H, float eps, float drop_p, unsigned long long seed, hipStream_t s);
+// dx = LN'(dy); dx_drop = dx * dropout-mask(seed, m*H+n) * 1/(1-p) (the gradient entering the
+// dropout of the residual branch, nullable); per-wave partial rows ws[P][2][H] of dgamma/dbeta
+int ln_partial_rows(long M);
+// in_drop_p/in_seed: dy is first masked by the forward's output dropout
+int layernorm_bwd(const void* dy, const void* x, const float* mean, const float* rstd, const float* gamma, void* dx,
+                  void* dx_drop, float drop_p, unsigned long long seed, float* ws, int P, long M, int H,
+                  float in_drop_p, unsigned long long in_seed, hipStream_t s);
+// out[n] (+)= sum_p ws[p][n]
+int colsum_partials(const float* ws, int P, int N, float* out, int accumulate, hipStream_t s);
+// out[t] = word[ids[t]] + pos[t % S] + type[types[t]]  (bf16 tables, types nullable -> row 0)
+int embed_fwd(const int64_t* ids, const int64_t* types, const void* word, const void* pos, const void* type,
+              void* out, long T, int S, int H, hipStream_t s);
+// gword[ids[t]] += ds[t] (fp32 atomics), gpos[t % S] += ds[t]; per-wave partial rows of the
+// token-type gradient wsT[P][ntypes][H] (ntypes <= 2)
+int embed_bwd(const int64_t* ids, const int64_t* types, const void* ds, float* gword, float* gpos, float* wsT, int P,
+              int ntypes, long T, int S, int H, hipStream_t s);
 
 }  // namespace ddl

@@ -1,0 +1,518 @@
+// Fused multi-head attention (forward + backward) for gfx950, head dim 64.
+//
+// Layout: the QKV projection output is consumed in place, [tokens, ld] row-major with
+// head h of Q/K/V at columns q_off/k_off/v_off + 64h (BERT: ld = 3*768); the context
+// output is [tokens, ldo] with head h at columns 64h — i.e. directly the input of the
+// output projection.  No transposes, no materialised score matrix.
+//
+// Every product runs on v_mfma_f32_16x16x32_bf16.  The trick that keeps the softmax
+// in registers: scores are computed TRANSPOSED, S^T = K Q^T, so that one lane owns one
+// query (column lane&15 of the D fragment) across 4 keys per 16x16 tile.  Row
+// statistics (max, sum) are then in-lane + two xor-shuffles, and P^T is already laid out
+// as the B operand of O^T = V^T P^T once the 32 keys of an MFMA k-step are enumerated in
+// the order the lane holds them (keys 4g..4g+3 and 16+4g..16+4g+3 of the step).  The V^T
+// A-operand is produced in that same key order by ds_read_b64_tr_b16 (hardware transpose
+// reads) from a row-major, XOR-swizzled 64x64 LDS tile.  The backward uses the same two
+// fragment readers:
+//   attn_bwd_dkdv : a workgroup owns 128 keys (32 per wave), streams 64-query tiles of
+//                   Q/dO through LDS: S = Q K^T, dP = dO V^T, dV += P^T dO, dK += dS^T Q;
+//   attn_bwd_dq   : a workgroup owns 128 queries, streams K/V tiles: dQ += dS K.
+// (Two kernels instead of atomics on dQ: deterministic, no fp32 scratch.)
+// Softmax uses base-2 exponentials with scale*log2(e) folded in; the forward saves the
+// base-2 log-sum-exp per query.  Dropout on the attention probabilities is a stateless
+// hash of (seed, b, h, i, j), regenerated in the backward.  Key padding: lens[b] valid
+// keys (nullable -> all valid).
+#include "ddl_common.h"
+#include "ddl_ops.h"
+
+namespace ddl {
+namespace {
+
+constexpr int HD = 64;            // head dim
+constexpr int TQ = 64;            // rows of a streamed LDS tile
+constexpr int TILE_BYTES = TQ * HD * 2;
+constexpr int THREADS = 256;      // 4 waves, each owns 32 rows (queries or keys)
+constexpr int BLOCK_ROWS = 128;
+
+__device__ __forceinline__ int tile_byte(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+
+struct TileStage {
+  uint4 reg[2];
+  __device__ __forceinline__ void load(const bf16_t* base, long ld, int r0, int nrows) {
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const int idx = threadIdx.x + v * THREADS;
+      const int row = idx >> 3, ch = idx & 7;
+      reg[v] = (r0 + row < nrows) ? *reinterpret_cast<const uint4*>(base + (long)(r0 + row) * ld + ch * 8)
+                                  : make_uint4(0, 0, 0, 0);
+    }
+  }
+  __device__ __forceinline__ void store(char* lds) const {
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const int idx = threadIdx.x + v * THREADS;
+      *reinterpret_cast<uint4*>(lds + tile_byte(idx >> 3, idx & 7)) = reg[v];
+    }
+  }
+};
+
+// 8 consecutive elements of tile row `row` at columns 32kk + 8g (fragment whose k runs along the row)
+__device__ __forceinline__ bf16x8 frag_row(const char* lds, int row, int kk, int g) {
+  return *reinterpret_cast<const bf16x8*>(lds + tile_byte(row, 4 * kk + g));
+}
+
+// fragment whose k runs DOWN the tile: lane (g, li) gets column cb+li of rows ra..ra+3 (slots 0-3)
+// and rb..rb+3 (slots 4-7); ra/rb are uniform per 16-lane group.
+__device__ __forceinline__ bf16x8 frag_col(const char* lds, int ra, int rb, int cb, int lane) {
+  const int li = lane & 15, q = li >> 2, pp = li & 3;
+  const int col = cb + 4 * pp;
+  const int ch = col >> 3, within = (col & 7) * 2;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DDL_LDS s16x4*)(lds + tile_byte(ra + q, ch) + within));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DDL_LDS s16x4*)(lds + tile_byte(rb + q, ch) + within));
+  const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+__device__ __forceinline__ bf16x8 pack8(const f32x4& a, const f32x4& b) {
+  bf16x8 r;
+  r[0] = (__bf16)a[0]; r[1] = (__bf16)a[1]; r[2] = (__bf16)a[2]; r[3] = (__bf16)a[3];
+  r[4] = (__bf16)b[0]; r[5] = (__bf16)b[1]; r[6] = (__bf16)b[2]; r[7] = (__bf16)b[3];
+  return r;
+}
+
+__device__ __forceinline__ bf16x8 ldg_frag(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
+
+__device__ __forceinline__ unsigned long long drop_index(int bh, int S, int i, int j) {
+  return ((unsigned long long)bh * (unsigned long long)S + (unsigned long long)i) * (unsigned long long)S +
+         (unsigned long long)j;
+}
+
+// ================================================================ forward
+__global__ __launch_bounds__(THREADS, 2) void attn_fwd_kernel(const AttnParams p) {
+  __shared__ __attribute__((aligned(16))) char lds[2][2][TILE_BYTES];
+  const int h = blockIdx.y, b = blockIdx.z, S = p.S;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
+  const long tok0 = (long)b * S;
+  const bf16_t* Q = p.qkv + tok0 * p.ld + p.q_off + h * HD;
+  const bf16_t* K = p.qkv + tok0 * p.ld + p.k_off + h * HD;
+  const bf16_t* V = p.qkv + tok0 * p.ld + p.v_off + h * HD;
+  const int len = p.lens ? min(max(p.lens[b], 0), S) : S;
+  const int q0 = blockIdx.x * BLOCK_ROWS + w * 32;
+  const int bh = b * p.H + h;
+
+  bf16x8 qf[2][2];
+#pragma unroll
+  for (int it = 0; it < 2; ++it)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) qf[it][kk] = ldg_frag(Q + (long)(q0 + 16 * it + li) * p.ld + 32 * kk + 8 * g);
+
+  f32x4 o[4][2];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int it = 0; it < 2; ++it) o[dt][it] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+
+  const int nkt = (len + TQ - 1) / TQ;
+  TileStage sk, sv;
+  if (nkt > 0) {
+    sk.load(K, p.ld, 0, len);
+    sv.load(V, p.ld, 0, len);
+    sk.store(lds[0][0]);
+    sv.store(lds[0][1]);
+  }
+  __syncthreads();
+  for (int t = 0; t < nkt; ++t) {
+    const char* kl = lds[t & 1][0];
+    const char* vl = lds[t & 1][1];
+    const bool more = t + 1 < nkt;
+    if (more) {
+      sk.load(K, p.ld, (t + 1) * TQ, len);
+      sv.load(V, p.ld, (t + 1) * TQ, len);
+    }
+    // S^T[j = 16jt + 4g + e][i = 16it + li]
+    f32x4 s[4][2];
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt) {
+      const bf16x8 k0 = frag_row(kl, 16 * jt + li, 0, g), k1 = frag_row(kl, 16 * jt + li, 1, g);
+#pragma unroll
+      for (int it = 0; it < 2; ++it) {
+        f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
+        a = mfma16x16x32(k0, qf[it][0], a);
+        s[jt][it] = mfma16x16x32(k1, qf[it][1], a);
+      }
+    }
+    const int kb = t * TQ;
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int j = kb + 16 * jt + 4 * g + e;
+          const float v = (j < len) ? s[jt][it][e] * p.scale_log2 : -INFINITY;
+          s[jt][it][e] = v;
+          mx = fmaxf(mx, v);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m[it], mx);  // finite: key kb < len is valid
+      const float alpha = exp2f(m[it] - mn);
+      m[it] = mn;
+      float rs = 0.f;
+#pragma unroll
+      for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float pv = exp2f(s[jt][it][e] - mn);
+          s[jt][it][e] = pv;
+          rs += pv;
+        }
+      l[it] = l[it] * alpha + rs;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) o[dt][it] *= alpha;
+    }
+    if (p.drop_thresh) {
+#pragma unroll
+      for (int it = 0; it < 2; ++it)
+#pragma unroll
+        for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const unsigned long long idx = drop_index(bh, S, q0 + 16 * it + li, kb + 16 * jt + 4 * g + e);
+            s[jt][it][e] = drop_keep(p.drop_seed, idx, p.drop_thresh) ? s[jt][it][e] * p.drop_scale : 0.f;
+          }
+    }
+    // O^T[d][i] += sum_j V^T[d][j] P^T[j][i]
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const bf16x8 pb0 = pack8(s[2 * kk][0], s[2 * kk + 1][0]);
+      const bf16x8 pb1 = pack8(s[2 * kk][1], s[2 * kk + 1][1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x8 va = frag_col(vl, 32 * kk + 4 * g, 32 * kk + 16 + 4 * g, 16 * dt, lane);
+        o[dt][0] = mfma16x16x32(va, pb0, o[dt][0]);
+        o[dt][1] = mfma16x16x32(va, pb1, o[dt][1]);
+      }
+    }
+    if (more) {
+      sk.store(lds[(t + 1) & 1][0]);
+      sv.store(lds[(t + 1) & 1][1]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    float lt = l[it];
+    lt += __shfl_xor(lt, 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    const float inv = lt > 0.f ? 1.f / lt : 0.f;
+    const int i = q0 + 16 * it + li;
+    bf16_t* orow = p.o + (tok0 + i) * p.ldo + h * HD;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const f32x4 v = o[dt][it] * inv;
+      *reinterpret_cast<uint2*>(orow + 16 * dt + 4 * g) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+    }
+    if (g == 0) p.lse[(long)bh * S + i] = lt > 0.f ? m[it] + __log2f(lt) : INFINITY;
+  }
+}
+
+// ================================================================ backward: D = rowsum(dO * O)
+__global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const AttnParams p, long rows) {
+  // one 16-B vector per thread; 8 threads per (token, head) row of 64
+  const long gid = (long)blockIdx.x * 256 + threadIdx.x;
+  const long r = gid >> 3;
+  float acc = 0.f;
+  if (r < rows) {
+    const long tok = r / p.H;
+    const int h = (int)(r - tok * p.H);
+    const int c = (int)(gid & 7) * 8;
+    const uint4 a = *reinterpret_cast<const uint4*>(p.o + tok * p.ldo + h * HD + c);
+    const uint4 d = *reinterpret_cast<const uint4*>(p.dout + tok * p.lddo + h * HD + c);
+    const uint32_t av[4] = {a.x, a.y, a.z, a.w}, dv[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      acc += __uint_as_float(av[e] << 16) * __uint_as_float(dv[e] << 16);
+      acc += __uint_as_float(av[e] & 0xffff0000u) * __uint_as_float(dv[e] & 0xffff0000u);
+    }
+  }
+  acc += __shfl_xor(acc, 1, 64);
+  acc += __shfl_xor(acc, 2, 64);
+  acc += __shfl_xor(acc, 4, 64);
+  if (r < rows && (gid & 7) == 0) {
+    const long tok = r / p.H;
+    const int h = (int)(r - tok * p.H);
+    const long b = tok / p.S, i = tok - b * p.S;
+    p.dvec[(b * p.H + h) * p.S + i] = acc;
+  }
+}
+
+// ================================================================ backward: dK, dV
+__global__ __launch_bounds__(THREADS, 1) void attn_bwd_dkdv_kernel(const AttnParams p) {
+  __shared__ __attribute__((aligned(16))) char lds[2][2][TILE_BYTES];  // [buf][Q, dO]
+  __shared__ float s_lse[2][TQ], s_d[2][TQ];
+  const int h = blockIdx.y, b = blockIdx.z, S = p.S;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
+  const long tok0 = (long)b * S;
+  const int bh = b * p.H + h;
+  const bf16_t* Q = p.qkv + tok0 * p.ld + p.q_off + h * HD;
+  const bf16_t* K = p.qkv + tok0 * p.ld + p.k_off + h * HD;
+  const bf16_t* V = p.qkv + tok0 * p.ld + p.v_off + h * HD;
+  const bf16_t* dO = p.dout + tok0 * p.lddo + h * HD;
+  const float* lse = p.lse + (long)bh * S;
+  const float* dv = p.dvec + (long)bh * S;
+  const int len = p.lens ? min(max(p.lens[b], 0), S) : S;
+  const int k0 = blockIdx.x * BLOCK_ROWS + w * 32;
+  bf16_t* dK = p.dqkv + tok0 * p.lddqkv + p.k_off + h * HD;
+  bf16_t* dV = p.dqkv + tok0 * p.lddqkv + p.v_off + h * HD;
+
+  // K / V fragments as the B operand of S = Q K^T and dP = dO V^T: [d][j = 16jt + li]
+  bf16x8 kf[2][2], vf[2][2];
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      kf[jt][kk] = ldg_frag(K + (long)(k0 + 16 * jt + li) * p.ld + 32 * kk + 8 * g);
+      vf[jt][kk] = ldg_frag(V + (long)(k0 + 16 * jt + li) * p.ld + 32 * kk + 8 * g);
+    }
+  // D layout accumulators: [j = 16jt + 4g + e][d = 16dt + li]
+  f32x4 adv[2][4], adk[2][4];
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) adv[jt][dt] = adk[jt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const bool any_key = blockIdx.x * BLOCK_ROWS < len;  // block-uniform
+  const int nqt = any_key ? S / TQ : 0;
+  TileStage sq, sd;
+  float r_lse = 0.f, r_d = 0.f;
+  if (nqt > 0) {
+    sq.load(Q, p.ld, 0, S);
+    sd.load(dO, p.lddo, 0, S);
+    sq.store(lds[0][0]);
+    sd.store(lds[0][1]);
+    if (threadIdx.x < TQ) {
+      s_lse[0][threadIdx.x] = lse[threadIdx.x];
+      s_d[0][threadIdx.x] = dv[threadIdx.x];
+    }
+  }
+  __syncthreads();
+  for (int t = 0; t < nqt; ++t) {
+    const int buf = t & 1;
+    const char* ql = lds[buf][0];
+    const char* dl = lds[buf][1];
+    const bool more = t + 1 < nqt;
+    if (more) {
+      sq.load(Q, p.ld, (t + 1) * TQ, S);
+      sd.load(dO, p.lddo, (t + 1) * TQ, S);
+      if (threadIdx.x < TQ) {
+        r_lse = lse[(t + 1) * TQ + threadIdx.x];
+        r_d = dv[(t + 1) * TQ + threadIdx.x];
+      }
+    }
+    const int qb = t * TQ;
+    // S, dP: [i = 16it + 4g + e][j = 16jt + li]
+    f32x4 s[4][2], dp[4][2];
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const bf16x8 q0f = frag_row(ql, 16 * it + li, 0, g), q1f = frag_row(ql, 16 * it + li, 1, g);
+      const bf16x8 d0f = frag_row(dl, 16 * it + li, 0, g), d1f = frag_row(dl, 16 * it + li, 1, g);
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt) {
+        f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f}, c = f32x4{0.f, 0.f, 0.f, 0.f};
+        a = mfma16x16x32(q0f, kf[jt][0], a);
+        s[it][jt] = mfma16x16x32(q1f, kf[jt][1], a);
+        c = mfma16x16x32(d0f, vf[jt][0], c);
+        dp[it][jt] = mfma16x16x32(d1f, vf[jt][1], c);
+      }
+    }
+    // P, dS (P kept in s[], dropout-scaled P in pd via s after dS is formed)
+#pragma unroll
+    for (int it = 0; it < 4; ++it)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int il = 16 * it + 4 * g + e;
+        const float lq = s_lse[buf][il], dq = s_d[buf][il];
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt) {
+          const int j = k0 + 16 * jt + li;
+          float pv = (j < len) ? exp2f(s[it][jt][e] * p.scale_log2 - lq) : 0.f;
+          float keep = 1.f;
+          if (p.drop_thresh)
+            keep = drop_keep(p.drop_seed, drop_index(bh, S, qb + il, j), p.drop_thresh) ? p.drop_scale : 0.f;
+          dp[it][jt][e] = pv * (dp[it][jt][e] * keep - dq);  // dS
+          s[it][jt][e] = pv * keep;                          // dropped P (for dV)
+        }
+      }
+    // dV[j][d] += sum_i Pd[i][j] dO[i][d] ; dK[j][d] += sum_i dS[i][j] Q[i][d]
+#pragma unroll
+    for (int kq = 0; kq < 2; ++kq) {
+      bf16x8 pa[2], sa[2];
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt) {
+        pa[jt] = pack8(s[2 * kq][jt], s[2 * kq + 1][jt]);
+        sa[jt] = pack8(dp[2 * kq][jt], dp[2 * kq + 1][jt]);
+      }
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x8 db = frag_col(dl, 32 * kq + 4 * g, 32 * kq + 16 + 4 * g, 16 * dt, lane);
+        const bf16x8 qb2 = frag_col(ql, 32 * kq + 4 * g, 32 * kq + 16 + 4 * g, 16 * dt, lane);
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt) {
+          adv[jt][dt] = mfma16x16x32(pa[jt], db, adv[jt][dt]);
+          adk[jt][dt] = mfma16x16x32(sa[jt], qb2, adk[jt][dt]);
+        }
+      }
+    }
+    if (more) {
+      sq.store(lds[buf ^ 1][0]);
+      sd.store(lds[buf ^ 1][1]);
+      if (threadIdx.x < TQ) {
+        s_lse[buf ^ 1][threadIdx.x] = r_lse;
+        s_d[buf ^ 1][threadIdx.x] = r_d;
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const long j = k0 + 16 * jt + 4 * g + e;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        dK[j * p.lddqkv + 16 * dt + li] = f2bf(adk[jt][dt][e] * p.scale);
+        dV[j * p.lddqkv + 16 * dt + li] = f2bf(adv[jt][dt][e]);
+      }
+    }
+}
+
+// ================================================================ backward: dQ
+__global__ __launch_bounds__(THREADS, 2) void attn_bwd_dq_kernel(const AttnParams p) {
+  __shared__ __attribute__((aligned(16))) char lds[2][2][TILE_BYTES];  // [buf][K, V]
+  const int h = blockIdx.y, b = blockIdx.z, S = p.S;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
+  const long tok0 = (long)b * S;
+  const int bh = b * p.H + h;
+  const bf16_t* Q = p.qkv + tok0 * p.ld + p.q_off + h * HD;
+  const bf16_t* K = p.qkv + tok0 * p.ld + p.k_off + h * HD;
+  const bf16_t* V = p.qkv + tok0 * p.ld + p.v_off + h * HD;
+  const bf16_t* dO = p.dout + tok0 * p.lddo + h * HD;
+  const int len = p.lens ? min(max(p.lens[b], 0), S) : S;
+  const int q0 = blockIdx.x * BLOCK_ROWS + w * 32;
+  bf16_t* dQ = p.dqkv + tok0 * p.lddqkv + p.q_off + h * HD;
+
+  bf16x8 qf[2][2], df[2][2];
+  float lq[2], dq[2];
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int i = q0 + 16 * it + li;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      qf[it][kk] = ldg_frag(Q + (long)i * p.ld + 32 * kk + 8 * g);
+      df[it][kk] = ldg_frag(dO + (long)i * p.lddo + 32 * kk + 8 * g);
+    }
+    lq[it] = p.lse[(long)bh * S + i];
+    dq[it] = p.dvec[(long)bh * S + i];
+  }
+  f32x4 acc[2][4];  // dQ[i = 16it + 4g + e][d = 16dt + li]
+#pragma unroll
+  for (int it = 0; it < 2; ++it)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) acc[it][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nkt = (len + TQ - 1) / TQ;
+  TileStage sk, sv;
+  if (nkt > 0) {
+    sk.load(K, p.ld, 0, len);
+    sv.load(V, p.ld, 0, len);
+    sk.store(lds[0][0]);
+    sv.store(lds[0][1]);
+  }
+  __syncthreads();
+  for (int t = 0; t < nkt; ++t) {
+    const char* kl = lds[t & 1][0];
+    const char* vl = lds[t & 1][1];
+    const bool more = t + 1 < nkt;
+    if (more) {
+      sk.load(K, p.ld, (t + 1) * TQ, len);
+      sv.load(V, p.ld, (t + 1) * TQ, len);
+    }
+    const int kb = t * TQ;
+    // S^T, dP^T: [j = 16jt + 4g + e][i = 16it + li]
+    f32x4 s[4][2], dp[4][2];
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt) {
+      const bf16x8 k0f = frag_row(kl, 16 * jt + li, 0, g), k1f = frag_row(kl, 16 * jt + li, 1, g);
+      const bf16x8 v0f = frag_row(vl, 16 * jt + li, 0, g), v1f = frag_row(vl, 16 * jt + li, 1, g);
+#pragma unroll
+      for (int it = 0; it < 2; ++it) {
+        f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f}, c = f32x4{0.f, 0.f, 0.f, 0.f};
+        a = mfma16x16x32(k0f, qf[it][0], a);
+        s[jt][it] = mfma16x16x32(k1f, qf[it][1], a);
+        c = mfma16x16x32(v0f, df[it][0], c);
+        dp[jt][it] = mfma16x16x32(v1f, df[it][1], c);
+      }
+    }
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+      for (int it = 0; it < 2; ++it)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int j = kb + 16 * jt + 4 * g + e;
+          const float pv = (j < len) ? exp2f(s[jt][it][e] * p.scale_log2 - lq[it]) : 0.f;
+          float keep = 1.f;
+          if (p.drop_thresh)
+            keep = drop_keep(p.drop_seed, drop_index(bh, S, q0 + 16 * it + li, j), p.drop_thresh) ? p.drop_scale
+                                                                                                   : 0.f;
+          s[jt][it][e] = pv * (dp[jt][it][e] * keep - dq[it]);  // dS^T
+        }
+    // dQ[i][d] += sum_j dS[i][j] K[j][d]
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const bf16x8 a0 = pack8(s[2 * kk][0], s[2 * kk + 1][0]);
+      const bf16x8 a1 = pack8(s[2 * kk][1], s[2 * kk + 1][1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x8 kb2 = frag_col(kl, 32 * kk + 4 * g, 32 * kk + 16 + 4 * g, 16 * dt, lane);
+        acc[0][dt] = mfma16x16x32(a0, kb2, acc[0][dt]);
+        acc[1][dt] = mfma16x16x32(a1, kb2, acc[1][dt]);
+      }
+    }
+    if (more) {
+      sk.store(lds[(t + 1) & 1][0]);
+      sv.store(lds[(t + 1) & 1][1]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int it = 0; it < 2; ++it)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const long i = q0 + 16 * it + 4 * g + e;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) dQ[i * p.lddqkv + 16 * dt + li] = f2bf(acc[it][dt][e] * p.scale);
+    }
+}
+
+}  // namespace
+
+int attn_fwd(const AttnParams& p, hipStream_t s) {
+  if (p.B <= 0) return 0;
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3(p.S / BLOCK_ROWS, p.H, p.B), dim3(THREADS), 0, s, p);
+  return (int)hipGetLastError();
+}
+
+int attn_bwd(const AttnParams& p, hipStream_t s) {
+  if (p.B <= 0) return 0;
+  const long rows = (long)p.B * p.S * p.H;
+  hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s, p, rows);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(p.S / BLOCK_ROWS, p.H, p.B), dim3(THREADS), 0, s, p);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(p.S / BLOCK_ROWS, p.H, p.B), dim3(THREADS), 0, s, p);
+  return (int)hipGetLastError();
+}
+
+}  // namespace ddl

@@ -1,0 +1,329 @@
+// LayerNorm forward/backward, BERT embeddings forward/backward, partial-row column sums.
+//
+// Rows are processed one wave per row with 16-B vectors (lane owns vectors lane, lane+64, ...
+// of the row), statistics in fp32 registers, two-pass (mean, then centred variance).
+// Backward: dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * gamma, and the
+// parameter gradients are accumulated per lane across the rows a wave visits, then
+// written as one partial row per wave (no atomics); colsum_partials finishes them.
+// The residual-branch dropout mask (same hash and element index as the producing GEMM's
+// epilogue) is regenerated here so the masked gradient leaves in the same pass.
+#include <algorithm>
+
+#include "ddl_common.h"
+#include "ddl_ops.h"
+
+namespace ddl {
+namespace {
+
+__device__ __forceinline__ void unpack8(const uint4& u, float* f) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    f[2 * e] = __uint_as_float(w[e] << 16);
+    f[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ uint4 pack8f(const float* f) {
+  return make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]),
+                    pack_bf16x2(f[6], f[7]));
+}
+
+template <int VPL>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, bf16_t* __restrict__ y,
+                                                     float* __restrict__ mean, float* __restrict__ rstd, long M, int H,
+                                                     float eps, uint32_t thresh, float dscale,
+                                                     unsigned long long seed) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const int nv = H >> 3;
+  const bf16_t* xr = x + row * H;
+  float v[VPL][8];
+  float s = 0.f;
+#pragma unroll
+  for (int u = 0; u < VPL; ++u) {
+    const int c = lane + 64 * u;
+    if (c < nv) {
+      unpack8(*reinterpret_cast<const uint4*>(xr + c * 8), v[u]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += v[u][e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[u][e] = 0.f;
+    }
+  }
+  const float mu = warp_sum(s) / (float)H;
+  float q = 0.f;
+#pragma unroll
+  for (int u = 0; u < VPL; ++u)
+    if (lane + 64 * u < nv)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = v[u][e] - mu;
+        q += d * d;
+      }
+  const float rs = rsqrtf(warp_sum(q) / (float)H + eps);
+#pragma unroll
+  for (int u = 0; u < VPL; ++u) {
+    const int c = lane + 64 * u;
+    if (c < nv) {
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int n = c * 8 + e;
+        o[e] = (v[u][e] - mu) * rs * (gamma ? gamma[n] : 1.f) + (beta ? beta[n] : 0.f);
+        if (thresh)  // output dropout (BERT embeddings), element index row*H + n
+          o[e] = drop_keep(seed, (unsigned long long)row * (unsigned long long)H + n, thresh) ? o[e] * dscale : 0.f;
+      }
+      *reinterpret_cast<uint4*>(y + row * H + c * 8) = pack8f(o);
+    }
+  }
+  if (lane == 0) {
+    mean[row] = mu;
+    rstd[row] = rs;
+  }
+}
+
+template <int VPL>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                     const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                     const float* __restrict__ gamma, bf16_t* __restrict__ dx,
+                                                     bf16_t* __restrict__ dxd, uint32_t thresh, float dscale,
+                                                     unsigned long long seed, float* __restrict__ ws, long M, int H,
+                                                     uint32_t in_thresh, float in_scale, unsigned long long in_seed) {
+  const int lane = threadIdx.x & 63;
+  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int nwaves = gridDim.x * 4;
+  const int nv = H >> 3;
+  float dg[VPL][8], db[VPL][8];
+#pragma unroll
+  for (int u = 0; u < VPL; ++u)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dg[u][e] = db[u][e] = 0.f;
+  for (long row = wave; row < M; row += nwaves) {
+    const float mu = mean[row], rs = rstd[row];
+    float gy[VPL][8], xh[VPL][8];
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int u = 0; u < VPL; ++u) {
+      const int c = lane + 64 * u;
+      if (c < nv) {
+        float d[8], xv[8];
+        unpack8(*reinterpret_cast<const uint4*>(dy + row * H + c * 8), d);
+        unpack8(*reinterpret_cast<const uint4*>(x + row * H + c * 8), xv);
+        if (in_thresh) {  // dy arrives through the forward's output dropout
+          const unsigned long long base = (unsigned long long)row * (unsigned long long)H + c * 8;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) d[e] = drop_keep(in_seed, base + e, in_thresh) ? d[e] * in_scale : 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float xhat = (xv[e] - mu) * rs;
+          const float gm = gamma ? gamma[c * 8 + e] : 1.f;
+          dg[u][e] += d[e] * xhat;
+          db[u][e] += d[e];
+          xh[u][e] = xhat;
+          gy[u][e] = d[e] * gm;
+          a += gy[u][e];
+          b += gy[u][e] * xhat;
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xh[u][e] = gy[u][e] = 0.f;
+      }
+    }
+    a = warp_sum(a) / (float)H;
+    b = warp_sum(b) / (float)H;
+#pragma unroll
+    for (int u = 0; u < VPL; ++u) {
+      const int c = lane + 64 * u;
+      if (c < nv) {
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = rs * (gy[u][e] - a - xh[u][e] * b);
+        *reinterpret_cast<uint4*>(dx + row * H + c * 8) = pack8f(o);
+        if (dxd) {
+          const unsigned long long base = (unsigned long long)row * (unsigned long long)H + c * 8;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = drop_keep(seed, base + e, thresh) ? o[e] * dscale : 0.f;
+          *reinterpret_cast<uint4*>(dxd + row * H + c * 8) = pack8f(o);
+        }
+      }
+    }
+  }
+  if (ws) {
+    float* w0 = ws + (long)wave * 2 * H;
+#pragma unroll
+    for (int u = 0; u < VPL; ++u) {
+      const int c = lane + 64 * u;
+      if (c < nv) {
+        *reinterpret_cast<float4*>(w0 + c * 8) = make_float4(dg[u][0], dg[u][1], dg[u][2], dg[u][3]);
+        *reinterpret_cast<float4*>(w0 + c * 8 + 4) = make_float4(dg[u][4], dg[u][5], dg[u][6], dg[u][7]);
+        *reinterpret_cast<float4*>(w0 + H + c * 8) = make_float4(db[u][0], db[u][1], db[u][2], db[u][3]);
+        *reinterpret_cast<float4*>(w0 + H + c * 8 + 4) = make_float4(db[u][4], db[u][5], db[u][6], db[u][7]);
+      }
+    }
+  }
+}
+
+// out[n] (+)= sum_p ws[p][n]; block (64 columns x 16 row groups)
+__global__ __launch_bounds__(1024) void colsum_kernel(const float* __restrict__ ws, int P, int N,
+                                                      float* __restrict__ out, int accumulate) {
+  __shared__ float red[16][65];
+  const int n = blockIdx.x * 64 + threadIdx.x;
+  float s = 0.f;
+  if (n < N)
+    for (int p = threadIdx.y; p < P; p += 16) s += ws[(long)p * N + n];
+  red[threadIdx.y][threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.y == 0 && n < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t += red[r][threadIdx.x];
+    out[n] = accumulate ? out[n] + t : t;
+  }
+}
+
+__global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restrict__ ids,
+                                                        const int64_t* __restrict__ types,
+                                                        const bf16_t* __restrict__ word, const bf16_t* __restrict__ pos,
+                                                        const bf16_t* __restrict__ typ, bf16_t* __restrict__ out,
+                                                        long T, int S, int H) {
+  const int nv = H >> 3;
+  const long gid = (long)blockIdx.x * 256 + threadIdx.x;
+  const long t = gid / nv;
+  if (t >= T) return;
+  const int c = (int)(gid - t * nv) * 8;
+  float a[8], b[8], d[8];
+  unpack8(*reinterpret_cast<const uint4*>(word + ids[t] * H + c), a);
+  unpack8(*reinterpret_cast<const uint4*>(pos + (t % S) * H + c), b);
+  unpack8(*reinterpret_cast<const uint4*>(typ + (types ? types[t] : 0) * H + c), d);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a[e] += b[e] + d[e];
+  *reinterpret_cast<uint4*>(out + t * H + c) = pack8f(a);
+}
+
+__global__ __launch_bounds__(256) void embed_bwd_kernel(const int64_t* __restrict__ ids,
+                                                        const int64_t* __restrict__ types,
+                                                        const bf16_t* __restrict__ ds, float* __restrict__ gword,
+                                                        float* __restrict__ gpos, float* __restrict__ wsT, int ntypes,
+                                                        long T, int S, int H) {
+  // one wave per token (strided); lane owns columns 8*(lane + 64u)..+7
+  const int lane = threadIdx.x & 63;
+  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int nwaves = gridDim.x * 4;
+  const int nv = H >> 3;
+  float acc[2][4][8];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[a][u][e] = 0.f;
+  for (long t = wave; t < T; t += nwaves) {
+    const long id = ids[t];
+    const int ty = types ? (int)types[t] : 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = lane + 64 * u;
+      if (c < nv) {
+        float d[8];
+        unpack8(*reinterpret_cast<const uint4*>(ds + t * H + c * 8), d);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          if (gword) atomicAdd(gword + id * H + c * 8 + e, d[e]);
+          if (gpos) atomicAdd(gpos + (t % S) * H + c * 8 + e, d[e]);
+          if (ty == 0) acc[0][u][e] += d[e];
+          else acc[1][u][e] += d[e];
+        }
+      }
+    }
+  }
+  if (wsT) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      if (a >= ntypes) break;
+      float* w0 = wsT + ((long)wave * ntypes + a) * H;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int c = lane + 64 * u;
+        if (c < nv)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) w0[c * 8 + e] = acc[a][u][e];
+      }
+    }
+  }
+}
+
+constexpr int kLnBwdBlocks = 256;
+
+}  // namespace
+
+int layernorm_fwd(const void* x, const float* gamma, const float* beta, void* y, float* mean, float* rstd, long M,
+                  int H, float eps, float drop_p, unsigned long long seed, hipStream_t s) {
+  if (M <= 0) return 0;
+  const uint32_t th = drop_p > 0.f ? (uint32_t)std::min(4294967295.0, (double)drop_p * 4294967296.0) : 0u;
+  const float ds = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  const int nv = H / 8;
+  const dim3 grid((unsigned)((M + 3) / 4));
+  auto X = reinterpret_cast<const bf16_t*>(x);
+  auto Y = reinterpret_cast<bf16_t*>(y);
+  if (nv <= 64) hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed);
+  else if (nv <= 128) hipLaunchKernelGGL(ln_fwd_kernel<2>, grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed);
+  else if (nv <= 256) hipLaunchKernelGGL(ln_fwd_kernel<4>, grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed);
+  else hipLaunchKernelGGL(ln_fwd_kernel<8>, grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed);
+  return (int)hipGetLastError();
+}
+
+int ln_partial_rows(long M) {
+  const long blocks = std::min<long>(kLnBwdBlocks, (M + 3) / 4);
+  return (int)std::max<long>(1, blocks) * 4;
+}
+
+int layernorm_bwd(const void* dy, const void* x, const float* mean, const float* rstd, const float* gamma, void* dx,
+                  void* dx_drop, float drop_p, unsigned long long seed, float* ws, int P, long M, int H,
+                  float in_drop_p, unsigned long long in_seed, hipStream_t s) {
+  if (M <= 0) return 0;
+  const uint32_t ith = in_drop_p > 0.f ? (uint32_t)std::min(4294967295.0, (double)in_drop_p * 4294967296.0) : 0u;
+  const float iscale = in_drop_p > 0.f ? 1.f / (1.f - in_drop_p) : 1.f;
+  const int nv = H / 8;
+  const dim3 grid((unsigned)(P / 4));
+  const uint32_t thresh = drop_p > 0.f ? (uint32_t)std::min(4294967295.0, (double)drop_p * 4294967296.0) : 0u;
+  const float dscale = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  auto DY = reinterpret_cast<const bf16_t*>(dy);
+  auto X = reinterpret_cast<const bf16_t*>(x);
+  auto DX = reinterpret_cast<bf16_t*>(dx);
+  auto DD = reinterpret_cast<bf16_t*>(dx_drop);
+  if (nv <= 64) hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed);
+  else if (nv <= 128) hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed);
+  else if (nv <= 256) hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed);
+  else hipLaunchKernelGGL(ln_bwd_kernel<8>, grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed);
+  return (int)hipGetLastError();
+}
+
+int colsum_partials(const float* ws, int P, int N, float* out, int accumulate, hipStream_t s) {
+  if (N <= 0) return 0;
+  hipLaunchKernelGGL(colsum_kernel, dim3((N + 63) / 64), dim3(64, 16), 0, s, ws, P, N, out, accumulate);
+  return (int)hipGetLastError();
+}
+
+int embed_fwd(const int64_t* ids, const int64_t* types, const void* word, const void* pos, const void* type,
+              void* out, long T, int S, int H, hipStream_t s) {
+  if (T <= 0) return 0;
+  const long n = T * (H / 8);
+  hipLaunchKernelGGL(embed_fwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ids, types,
+                     reinterpret_cast<const bf16_t*>(word), reinterpret_cast<const bf16_t*>(pos),
+                     reinterpret_cast<const bf16_t*>(type), reinterpret_cast<bf16_t*>(out), T, S, H);
+  return (int)hipGetLastError();
+}
+
+int embed_bwd(const int64_t* ids, const int64_t* types, const void* ds, float* gword, float* gpos, float* wsT, int P,
+              int ntypes, long T, int S, int H, hipStream_t s) {
+  if (T <= 0) return 0;
+  hipLaunchKernelGGL(embed_bwd_kernel, dim3((unsigned)(P / 4)), dim3(256), 0, s, ids, types,
+                     reinterpret_cast<const bf16_t*>(ds), gword, gpos, wsT, ntypes, T, S, H);
+  return (int)hipGetLastError();
+}
+
+}  // namespace ddl

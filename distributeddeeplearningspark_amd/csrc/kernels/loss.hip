@@ -18,10 +18,10 @@ template <bool BF16>
 __global__ __launch_bounds__(256) void softmax_xent_kernel(const void* __restrict__ logits,
                                                             const int64_t* __restrict__ labels,
                                                             const float* __restrict__ tprob, float* loss_rows,
-                                                            void* dlogits, int K, float gscale, float smooth,
+                                                            void* dlogits, int K, long ld, float gscale, float smooth,
                                                             int ignore_index) {
   const int b = blockIdx.x;
-  const long base = (long)b * K;
+  const long base = (long)b * ld;  // row stride ld >= K (padded vocabularies); tprob rows are dense [B][K]
   __shared__ float sm[2][4];
   // pass 1: online max / sum-exp
   float m = -INFINITY, s = 0.f;
@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const void* __restric
     const float x = ld_logit<BF16>(logits, base + k);
     const float p = __expf(x - lse);
     float t;
-    if (tprob) t = tprob[base + k];
+    if (tprob) t = tprob[(long)b * K + k];
     else t = (k == lab ? 1.f - smooth : 0.f) + off;
     if (ignored) t = 0.f;
     lpart += t * (lse - x);
@@ -72,6 +72,11 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const void* __restric
       else reinterpret_cast<float*>(dlogits)[base + k] = g;
     }
   }
+  if (dlogits)  // zero the padding columns so padded GEMMs can consume dlogits directly
+    for (long k = K + threadIdx.x; k < ld; k += 256) {
+      if constexpr (BF16) reinterpret_cast<bf16_t*>(dlogits)[base + k] = 0;
+      else reinterpret_cast<float*>(dlogits)[base + k] = 0.f;
+    }
   lpart = warp_sum(lpart);
   __syncthreads();
   if (lane == 0) sm[0][wid] = lpart;
@@ -80,15 +85,15 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const void* __restric
 }
 
 int softmax_xent(const void* logits, int logits_bf16, const int64_t* labels, const float* target_probs,
-                 float* loss_rows, void* dlogits, int B, int K, float grad_scale, float label_smoothing,
+                 float* loss_rows, void* dlogits, int B, int K, long ld, float grad_scale, float label_smoothing,
                  int ignore_index, hipStream_t s) {
   if (B <= 0) return 0;
   if (logits_bf16)
     hipLaunchKernelGGL(softmax_xent_kernel<true>, dim3(B), dim3(256), 0, s, logits, labels, target_probs, loss_rows,
-                       dlogits, K, grad_scale, label_smoothing, ignore_index);
+                       dlogits, K, ld, grad_scale, label_smoothing, ignore_index);
   else
     hipLaunchKernelGGL(softmax_xent_kernel<false>, dim3(B), dim3(256), 0, s, logits, labels, target_probs, loss_rows,
-                       dlogits, K, grad_scale, label_smoothing, ignore_index);
+                       dlogits, K, ld, grad_scale, label_smoothing, ignore_index);
   return (int)hipGetLastError();
 }
 

@@ -152,7 +152,8 @@ void softmax_xent_(const at::Tensor& logits, c10::optional<at::Tensor> labels, c
                    const at::Tensor& loss_rows, c10::optional<at::Tensor> dlogits, double grad_scale, double smoothing,
                    int64_t ignore_index) {
   GPU(logits);
-  CK(logits.dim() == 2 && logits.is_contiguous(), "softmax_xent: logits [B,K] contiguous");
+  CK(logits.dim() == 2 && logits.stride(1) == 1 && logits.stride(0) >= logits.size(1),
+     "softmax_xent: logits [B,K] with unit column stride");
   const bool bf = logits.scalar_type() == at::kBFloat16;
   CK(bf || logits.scalar_type() == at::kFloat, "softmax_xent: logits bf16/fp32");
   const int B = logits.size(0), K = logits.size(1);
@@ -161,10 +162,14 @@ void softmax_xent_(const at::Tensor& logits, c10::optional<at::Tensor> labels, c
   CK((labels.has_value()) != (probs.has_value()), "exactly one of labels/probs");
   if (labels) CK(labels->scalar_type() == at::kLong && labels->numel() == B, "labels int64 [B]");
   if (probs) { F32(*probs); CK(probs->numel() == (int64_t)B * K, "probs [B,K]"); }
-  if (dlogits) CK(dlogits->scalar_type() == logits.scalar_type() && dlogits->numel() == logits.numel(), "dlogits");
+  const long ld = logits.stride(0);
+  if (dlogits)
+    CK(dlogits->scalar_type() == logits.scalar_type() && dlogits->dim() == 2 && dlogits->size(0) == B &&
+           dlogits->stride(0) == ld && dlogits->stride(1) == 1,
+       "dlogits: same layout as logits");
   at::DeviceGuard g(logits.device());
   HIP_OK(softmax_xent(logits.data_ptr(), bf ? 1 : 0, optr<const int64_t>(labels), optr<const float>(probs),
-                      loss_rows.data_ptr<float>(), optr<void>(dlogits), B, K, (float)grad_scale, (float)smoothing,
+                      loss_rows.data_ptr<float>(), optr<void>(dlogits), B, K, ld, (float)grad_scale, (float)smoothing,
                       (int)ignore_index, cur_stream()));
 }
 

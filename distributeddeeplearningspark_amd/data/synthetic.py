@@ -76,3 +76,26 @@ def mlm_tokens(batch: int, seq: int = 512, vocab: int = 30522, mask_prob: float 
     labels = np.where(m, ids, -100)
     inp = np.where(m, mask_id, ids)
     return inp.astype(np.int64), labels.astype(np.int64)
+
+
+def mlm_batch(batch: int, seq: int = 512, vocab: int = 30522, max_predictions: int = 80, mask_prob: float = 0.15,
+              seed: int = 0, mask_id: int = 103):
+    """BERT pretraining-format batch (static shapes, no host sync in the step):
+    ``x = {"input_ids"}``, ``y = {"positions" [B,P], "labels" [B,P] (-100 padding), "num_masked"}``.
+    Each sequence masks ``min(max_predictions, round(mask_prob*seq))`` positions
+    (80/10/10 replacement: [MASK] / random token / unchanged)."""
+    rng = np.random.default_rng(seed)
+    ids = rng.integers(1000, vocab, (batch, seq)).astype(np.int64)
+    n = min(max_predictions, max(1, int(round(mask_prob * seq))))
+    pos = np.zeros((batch, max_predictions), np.int64)
+    labels = np.full((batch, max_predictions), -100, np.int64)
+    inp = ids.copy()
+    for b in range(batch):
+        p = np.sort(rng.choice(seq, n, replace=False))
+        pos[b, :n] = p
+        labels[b, :n] = ids[b, p]
+        r = rng.random(n)
+        inp[b, p[r < 0.8]] = mask_id
+        rnd = (r >= 0.8) & (r < 0.9)
+        inp[b, p[rnd]] = rng.integers(1000, vocab, int(rnd.sum()))
+    return {"input_ids": inp}, {"positions": pos, "labels": labels, "num_masked": batch * n}

@@ -51,7 +51,7 @@ def choose_split(M: int, N: int, K: int, tile: int, allow: bool) -> int:
 
 def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, beta=0.0, bias=None, resid=None,
          ldr=0, relu=False, geom=None, outmap=None, b_kdiv=0, b_tap_stride=0, stats=None, tile=None, k_split=None,
-         bn_cap=128):
+         bn_cap=128, aux=None, drop_p=0.0, drop_seed=0):
     """Raw launcher with automatic tile / split-K choice.
 
     With ``epi == EPI_F32`` and a split-K decomposition the launch switches to the
@@ -68,31 +68,40 @@ def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, bet
             raise ValueError("split-K fp32 gemm supports beta in {0,1} (beta=0 needs a zeroed C)")
         epi = EPI_F32_ATOMIC
     C().gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, tile, k_split, alpha, beta, bias, resid, ldr,
-             relu, geom, outmap, b_kdiv, b_tap_stride, stats)
+             int(relu), geom, outmap, b_kdiv, b_tap_stride, stats, aux, float(drop_p), int(drop_seed))
     return c
 
 
 # ----------------------------------------------------------------------------------------
 # 2-D helpers (row-major tensors)
 # ----------------------------------------------------------------------------------------
-def linear_fwd(x2, w, bias=None, relu=False, out=None, resid=None, stats=None):
-    """y[M,N] = x2[M,K] @ w[N,K]^T (+bias)(+resid)(relu) -> bf16."""
+ACT_NONE, ACT_RELU, ACT_GELU, ACT_GELU_BWD = 0, 1, 2, 3
+
+
+def linear_fwd(x2, w, bias=None, relu=False, out=None, resid=None, stats=None, act=None, aux=None, drop_p=0.0,
+               drop_seed=0):
+    """y[M,N] = x2[M,K] @ w[N,K]^T (+bias) -> act -> dropout (+resid) -> bf16.
+
+    ``act``: ACT_RELU / ACT_GELU (``aux`` receives the bf16 pre-activation)."""
     M, K = x2.shape
     N = w.shape[0]
     if out is None:
         out = torch.empty((M, N), dtype=torch.bfloat16, device=x2.device)
-    return gemm(x2, w, out, M, N, K, KC, KC, x2.stride(0), w.stride(0), out.stride(0), EPI_BF16, bias=bias, relu=relu,
-                resid=resid, ldr=(resid.stride(0) if resid is not None else 0), stats=stats)
+    act = (ACT_RELU if relu else ACT_NONE) if act is None else act
+    return gemm(x2, w, out, M, N, K, KC, KC, x2.stride(0), w.stride(0), out.stride(0), EPI_BF16, bias=bias, relu=act,
+                resid=resid, ldr=(resid.stride(0) if resid is not None else 0), stats=stats, aux=aux, drop_p=drop_p,
+                drop_seed=drop_seed)
 
 
-def linear_dgrad(dy, w, out=None, resid=None):
-    """dx[M,K] = dy[M,N] @ w[N,K] -> bf16 (w read row-contiguous; no transpose copy)."""
+def linear_dgrad(dy, w, out=None, resid=None, gelu_pre=None):
+    """dx[M,K] = dy[M,N] @ w[N,K] (* gelu'(gelu_pre)) (+resid) -> bf16 (w read row-contiguous)."""
     M, N = dy.shape
     K = w.shape[1]
     if out is None:
         out = torch.empty((M, K), dtype=torch.bfloat16, device=dy.device)
     return gemm(dy, w, out, M, K, N, KC, RC, dy.stride(0), w.stride(0), out.stride(0), EPI_BF16, resid=resid,
-                ldr=(resid.stride(0) if resid is not None else 0))
+                ldr=(resid.stride(0) if resid is not None else 0),
+                relu=(ACT_GELU_BWD if gelu_pre is not None else ACT_NONE), aux=gelu_pre)
 
 
 def linear_wgrad(dy, x2, gw):

@@ -14,11 +14,29 @@ if [ "${SKIP_TESTS:-0}" != "1" ]; then
   tail -5 gpurun_out/gpu_tests.log
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest crashed rc=$rc"; exit $rc; fi
 fi
+if [ "${SMOKE:-1}" = "1" ]; then
+  timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1
+  src=$?
+  tail -2 gpurun_out/smoke.log
+  if [ $src -ne 0 ]; then echo "smoke failed rc=$src"; exit $src; fi
+fi
 if [ "${SKIP_BENCH:-0}" != "1" ]; then
   timeout -k 10 ${BENCH_TIMEOUT:-600} python bench.py --steps $STEPS --warmup 3 ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
   brc=$?
   tail -3 gpurun_out/bench.log
   if [ $brc -ne 0 ]; then echo "bench failed rc=$brc"; exit $brc; fi
+fi
+if [ "${VGG:-0}" = "1" ]; then
+  timeout -k 10 600 python bench.py --model vgg16 --steps $STEPS --warmup 3 > gpurun_out/bench_vgg.log 2>&1
+  vrc=$?
+  tail -2 gpurun_out/bench_vgg.log
+  if [ $vrc -ne 0 ]; then echo "vgg bench failed rc=$vrc"; exit $vrc; fi
+fi
+if [ "${BERT:-0}" = "1" ]; then
+  timeout -k 10 600 python bench.py --model bert --steps ${BERT_STEPS:-5} --warmup 2 ${BERT_ARGS:-} > gpurun_out/bench_bert.log 2>&1
+  berc=$?
+  tail -2 gpurun_out/bench_bert.log
+  if [ $berc -ne 0 ]; then echo "bert bench failed rc=$berc"; exit $berc; fi
 fi
 if [ "${PROFILE:-0}" = "1" ]; then
   cd /tmp

@@ -356,27 +356,30 @@ def test_resnet50_step_matches_reference():
 
 
 def test_fused_bottleneck_matches_composed_ops():
-    """ops/fused_blocks.py (one autograd node per block) vs the per-op autograd graph."""
+    """ops/fused_blocks.py (one autograd node per block) vs the per-op autograd graph.
+
+    A one-block ResNet (stem + one bottleneck with projection shortcut): the full-depth
+    random-init ResNet-50 at a tiny batch is chaotic (1-ulp bf16 flips from atomic-order
+    differences in the BN statistics move its loss by percents), so the comparison is made
+    where it is well conditioned."""
     import os
 
-    from distributeddeeplearningspark_amd.models import ResNet50
+    from distributeddeeplearningspark_amd.models.resnet import ResNet
 
     torch.manual_seed(1)
-    x = torch.randn(8, 64, 64, 3)
-    y = torch.randint(0, 10, (8,))
+    x = torch.randn(16, 32, 32, 3)
+    y = torch.randint(0, 10, (16,))
     res = {}
     for fused in ("1", "0"):
         os.environ["DDL_FUSED_BLOCKS"] = fused
         try:
-            m = ResNet50(input_shape=(64, 64, 3), num_classes=10)
+            m = ResNet(blocks=(2,), input_shape=(32, 32, 3), num_classes=10)
             m.compile("sgd", "sparse_categorical_crossentropy")
             m.place(DEV, seed=5)
             loss = m.backward_step(m.to_input(x), m.to_target(y))
             res[fused] = (float(loss), m.arena.grad.clone())
         finally:
             os.environ.pop("DDL_FUSED_BLOCKS", None)
-    # the two paths round bf16 intermediates at different points (fused residual add in the
-    # BN-apply / dgrad epilogues), so they agree to bf16 noise accumulated over 16 blocks
     assert abs(res["1"][0] - res["0"][0]) < 1e-2 * max(1.0, abs(res["0"][0])), (res["1"][0], res["0"][0])
     g1, g0 = res["1"][1], res["0"][1]
-    assert ((g1 - g0).norm() / g0.norm()).item() < 5e-2
+    assert ((g1 - g0).norm() / g0.norm()).item() < 3e-2

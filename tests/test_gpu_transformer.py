@@ -1,0 +1,216 @@
+"""Numerics of the transformer HIP kernels (attention, LayerNorm, embeddings, GELU /
+dropout GEMM epilogues, padded-vocabulary xent) against fp32 PyTorch references of the
+same math, including the stateless dropout masks, plus a tiny BERT GPU-vs-CPU step."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def rnd(*shape, scale=1.0, seed=0, dtype=torch.bfloat16):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(dtype).to(DEV)
+
+
+def close(a, b, rtol=2e-2, atol=2e-2, what=""):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs()
+    bad = (err > atol + rtol * b.abs()).float().mean().item()
+    rel = (err.norm() / (b.norm() + 1e-12)).item()
+    assert bad < 2e-3 and rel < 2e-2, f"{what}: frac_bad={bad:.2e} rel_l2={rel:.2e} max_err={err.max().item():.3e}"
+
+
+@pytest.mark.parametrize("S,lens,drop", [(128, None, 0.0), (256, [256, 131], 0.0), (256, None, 0.1),
+                                         (384, [300, 384], 0.1)])
+def test_attention_fwd_bwd(S, lens, drop):
+    from distributeddeeplearningspark_amd.ops import transformer as T
+
+    B, NH = 2, 4
+    W = 3 * NH * 64
+    qkv = rnd(B * S, W, seed=1)
+    lt = None if lens is None else torch.tensor(lens, dtype=torch.int32, device=DEV)
+    x = qkv.clone().requires_grad_(True)
+    o = T.attention(x, B, S, NH, lens=lt, drop_p=drop, seed=77)
+    do = rnd(B * S, NH * 64, seed=2)
+    o.backward(do)
+    xr = qkv.float().requires_grad_(True)
+    orf = T.attention_ref(xr, B, S, NH, 0, NH * 64, 2 * NH * 64, lt, 0.125, drop, 77)
+    orf.backward(do.float())
+    close(o, orf, what="attn fwd")
+    close(x.grad, xr.grad, what="attn dqkv")
+
+
+def test_attention_head_offsets_strided():
+    """q/k/v blocks at arbitrary column offsets of a wider buffer (ld > 3*H*64)."""
+    from distributeddeeplearningspark_amd.ops import transformer as T
+
+    B, S, NH = 1, 128, 2
+    buf = rnd(B * S, 1024, seed=3)
+    o = T.attention(buf, B, S, NH, q_off=512, k_off=0, v_off=256)
+    ref = T.attention_ref(buf.float(), B, S, NH, 512, 0, 256)
+    close(o, ref, what="attn offsets")
+
+
+@pytest.mark.parametrize("H", [128, 768, 1024, 3072])
+def test_layernorm_fwd_bwd(H):
+    from distributeddeeplearningspark_amd.ops import transformer as T
+
+    M = 300
+    x = (rnd(M, H, seed=4).float() * 3 + 1).to(torch.bfloat16)
+    g = torch.rand(H, device=DEV) + 0.5
+    b = torch.randn(H, device=DEV) * 0.1
+    gg, gb = torch.zeros(H, device=DEV), torch.zeros(H, device=DEV)
+    xg = x.clone().requires_grad_(True)
+    y = T.layer_norm(xg, g, b, 1e-12, grad_gamma=gg, grad_beta=gb, anchor=g.clone().requires_grad_(True))
+    dy = rnd(M, H, seed=5)
+    y.backward(dy)
+    xr = x.float().requires_grad_(True)
+    gr, br = g.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(xr, (H,), gr, br, 1e-12)
+    yr.backward(dy.float())
+    close(y, yr, what="ln fwd")
+    close(xg.grad, xr.grad, what="ln dx")
+    close(gg, gr.grad, rtol=1e-2, atol=1e-2, what="ln dgamma")
+    close(gb, br.grad, rtol=1e-2, atol=1e-2, what="ln dbeta")
+
+
+def test_layernorm_dropout_paths():
+    """Output dropout of the forward, input dropout of the backward and the masked dx_drop
+    output all reproduce dropout_ref's hash mask."""
+    from distributeddeeplearningspark_amd.ops import transformer as T
+    from distributeddeeplearningspark_amd.ops._native import C
+
+    M, H, p, seed = 64, 256, 0.2, 12345
+    x = rnd(M, H, seed=6)
+    y = torch.empty_like(x)
+    mean = torch.empty(M, device=DEV)
+    rstd = torch.empty(M, device=DEV)
+    C().layernorm_fwd(x, None, None, y, mean, rstd, 1e-5, p, seed)
+    ref = T.dropout_ref(torch.nn.functional.layer_norm(x.float(), (H,), eps=1e-5), p, seed)
+    close(y, ref, what="ln output dropout")
+    dy = rnd(M, H, seed=7)
+    dx = torch.empty_like(x)
+    dxd = torch.empty_like(x)
+    C().layernorm_bwd(dy, x, mean, rstd, None, dx, dxd, p, seed + 1, None, p, seed)
+    xr = x.float().requires_grad_(True)
+    yr = T.dropout_ref(torch.nn.functional.layer_norm(xr, (H,), eps=1e-5), p, seed)
+    yr.backward(dy.float())
+    close(dx, xr.grad, what="ln bwd with input dropout")
+    close(dxd, T.dropout_ref(xr.grad, p, seed + 1), what="ln bwd dx_drop")
+
+
+def test_gemm_gelu_dropout_resid_epilogues():
+    from distributeddeeplearningspark_amd.ops import gemm as G
+    from distributeddeeplearningspark_amd.ops import transformer as T
+
+    M, N, K = 384, 512, 256
+    x, w = rnd(M, K, seed=8), rnd(N, K, scale=0.1, seed=9)
+    bias = torch.randn(N, device=DEV) * 0.1
+    pre = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    y = G.linear_fwd(x, w, bias=bias, act=G.ACT_GELU, aux=pre)
+    pre_r = x.float() @ w.float().t() + bias
+    close(pre, pre_r, what="gelu aux")
+    close(y, torch.nn.functional.gelu(pre_r), what="gelu out")
+    # d(pre) = (dy @ W2) * gelu'(pre)  with W2 [N2, N]
+    N2 = 256
+    w2 = rnd(N2, N, scale=0.1, seed=10)
+    dy = rnd(M, N2, seed=11)
+    dpre = G.linear_dgrad(dy, w2, gelu_pre=pre)
+    pr = pre.float().requires_grad_(True)
+    torch.nn.functional.gelu(pr).backward(dy.float() @ w2.float())
+    close(dpre, pr.grad, what="gelu bwd epilogue")
+    # dropout + residual
+    res = rnd(M, N, seed=12)
+    out = G.linear_fwd(x, w, bias=bias, resid=res, drop_p=0.1, drop_seed=99)
+    close(out, res.float() + T.dropout_ref(pre_r, 0.1, 99), what="dropout+resid")
+
+
+def test_embeddings_fwd_bwd():
+    from distributeddeeplearningspark_amd.ops._native import C
+
+    V, P, NT, H, B, S = 1000, 256, 2, 256, 3, 128
+    word, pos, typ = rnd(V, H, seed=13), rnd(P, H, seed=14), rnd(NT, H, seed=15)
+    ids = torch.randint(0, V, (B * S,), device=DEV)
+    tt = torch.randint(0, NT, (B * S,), device=DEV)
+    out = torch.empty(B * S, H, dtype=torch.bfloat16, device=DEV)
+    C().embed_fwd(ids, tt, word, pos, typ, out, S)
+    pidx = torch.arange(B * S, device=DEV) % S
+    ref = word.float()[ids] + pos.float()[pidx] + typ.float()[tt]
+    close(out, ref, what="embed fwd")
+    ds = rnd(B * S, H, seed=16)
+    gw, gp = torch.zeros(V, H, device=DEV), torch.zeros(P, H, device=DEV)
+    Pp = C().embed_partial_rows(B * S)
+    ws = torch.empty(Pp, NT, H, device=DEV)
+    gt = torch.zeros(NT, H, device=DEV)
+    C().embed_bwd(ids, tt, ds, gw, gp, ws, NT, S)
+    C().colsum_partials(ws.view(Pp, NT * H), Pp, NT * H, gt.view(-1), True)
+    d = ds.float()
+    close(gw, torch.zeros(V, H, device=DEV).index_add_(0, ids, d), rtol=1e-3, atol=1e-3, what="gword")
+    close(gp, torch.zeros(P, H, device=DEV).index_add_(0, pidx, d), rtol=1e-3, atol=1e-3, what="gpos")
+    close(gt, torch.zeros(NT, H, device=DEV).index_add_(0, tt, d), rtol=1e-3, atol=1e-3, what="gtype")
+
+
+def test_softmax_xent_padded_rows():
+    from distributeddeeplearningspark_amd.ops._native import C
+
+    M, V, Vp = 50, 1003, 1008
+    buf = rnd(M, Vp, seed=17)
+    labels = torch.randint(0, V, (M,), device=DEV)
+    labels[::7] = -100
+    loss = torch.empty(M, device=DEV)
+    dl = torch.full((M, Vp), 7.0, dtype=torch.bfloat16, device=DEV)
+    C().softmax_xent(buf[:, :V], labels, None, loss, dl[:, :V], 0.5, 0.0, -100)
+    lg = buf[:, :V].float().requires_grad_(True)
+    ref = torch.nn.functional.cross_entropy(lg, labels, ignore_index=-100, reduction="none")
+    (ref.sum() * 0.5).backward()
+    close(loss, ref, rtol=1e-3, atol=1e-3, what="xent loss rows")
+    close(dl[:, :V], lg.grad, what="xent grad")
+    assert torch.all(dl[:, V:] == 0), "padding columns must be zeroed"
+
+
+def test_bert_tiny_gpu_matches_cpu():
+    """One training step of a tiny BERT-MLM (dropout ON, same hash masks) on the HIP path
+    vs the fp32 CPU reference: loss and the whole flat gradient arena."""
+    from distributeddeeplearningspark_amd.models.bert import BertConfig, BertForMaskedLM
+
+    cfg = BertConfig.tiny(hidden_dropout_prob=0.1, attention_probs_dropout_prob=0.1)
+    B, S, Pm = 2, 128, 20
+    g = torch.Generator().manual_seed(0)
+    ids = torch.randint(0, cfg.vocab_size, (B, S), generator=g)
+    pos = torch.stack([torch.randperm(S, generator=g)[:Pm].sort().values for _ in range(B)])
+    labels = torch.gather(ids, 1, pos)
+    labels[0, -3:] = -100
+    res = {}
+    for dev in ("cpu", DEV):
+        m = BertForMaskedLM(cfg)
+        m.compile("adam", "sparse_categorical_crossentropy")
+        m.place(dev, seed=3)
+        x = m.to_input({"input_ids": ids, "lens": torch.tensor([S, 100], dtype=torch.int32)})
+        y = m.to_target({"positions": pos, "labels": labels})
+        loss = m.backward_step(x, y)
+        res[dev] = (float(loss), m.arena.grad.detach().float().cpu().clone())
+    (lc, gc), (lg, gg) = res["cpu"], res[DEV]
+    assert abs(lc - lg) < 2e-2 * abs(lc), (lc, lg)
+    rel = ((gg - gc).norm() / gc.norm()).item()
+    assert rel < 5e-2, rel
+
+
+def test_bert_base_layer_shapes_run():
+    """BERT-base geometry (H=768, 12 heads, I=3072, S=512) forward+backward of 2 layers."""
+    from distributeddeeplearningspark_amd.models.bert import BertConfig, BertForMaskedLM
+
+    cfg = BertConfig(num_hidden_layers=2)
+    m = BertForMaskedLM(cfg)
+    m.compile("adamw", "sparse_categorical_crossentropy")
+    m.place(DEV, seed=0)
+    B, S, Pm = 2, 512, 80
+    ids = torch.randint(0, cfg.vocab_size, (B, S))
+    pos = torch.stack([torch.randperm(S)[:Pm].sort().values for _ in range(B)])
+    loss = m.train_on_batch({"input_ids": ids}, {"positions": pos, "labels": torch.gather(ids, 1, pos),
+                                                  "num_masked": B * Pm})
+    assert math.isfinite(loss) and abs(loss - math.log(cfg.vocab_size)) < 1.5, loss
+    assert torch.isfinite(m.arena.master).all()
