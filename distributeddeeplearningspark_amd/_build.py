@@ -138,6 +138,7 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = True) ->
     link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(OUT),
             f"-L{tlib}", f"-Wl,-rpath,{tlib}",
             "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-lc10", "-lc10_hip", "-ltorch_python",
+            f"-L{ROCM}/lib", f"-Wl,-rpath,{ROCM}/lib", "-lrocprofiler-sdk-roctx",
             "-lpthread"]
     r = subprocess.run(link, capture_output=True, text=True)
     if r.returncode != 0:

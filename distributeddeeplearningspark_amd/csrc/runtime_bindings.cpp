@@ -17,7 +17,10 @@ void check_f32_cpu(const at::Tensor& t, const char* what) {
 
 }  // namespace
 
+void register_trace(py::module& m);  // runtime/trace.cpp
+
 void register_runtime(py::module& m) {
+  register_trace(m);
   py::class_<ParamServer>(m, "ParamServer")
       .def(py::init([](const at::Tensor& init, int rule, int port) {
              check_f32_cpu(init, "init");

@@ -22,6 +22,27 @@ def _load():
         _C = importlib.import_module("distributeddeeplearningspark_amd._C")
     except Exception as e:  # pragma: no cover - depends on build state
         _ERR = e
+        return
+    _warn_if_stale()
+
+
+def _warn_if_stale():
+    """Loud warning when a kernel/binding source is newer than the loaded extension."""
+    import glob
+    import warnings
+
+    so = getattr(_C, "__file__", None)
+    if not so:
+        return
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
+    srcs = [p for pat in ("**/*.hip", "**/*.cpp", "**/*.h") for p in glob.glob(os.path.join(root, pat), recursive=True)]
+    try:
+        newest = max(os.path.getmtime(p) for p in srcs)
+        if newest > os.path.getmtime(so) + 1.0:
+            warnings.warn("distributeddeeplearningspark_amd: _C.so is older than its sources; rebuild with "
+                          "`python -m distributeddeeplearningspark_amd._build`", RuntimeWarning, stacklevel=3)
+    except (ValueError, OSError):
+        pass
 
 
 def has_native() -> bool:

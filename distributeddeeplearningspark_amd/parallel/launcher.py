@@ -72,8 +72,36 @@ def _child_main(payload_path: str, result_path: str):
     os.replace(tmp, result_path)
 
 
-def run_workers(fn, num_workers: int, args_per_rank, device: str | None = None, timeout_s: float = 3600.0):
-    """Run ``fn(rank, world, pg, *args_per_rank[rank])`` on ``num_workers`` workers, return results by rank."""
+def run_workers(fn, num_workers: int, args_per_rank, device: str | None = None, timeout_s: float = 3600.0,
+                max_restarts: int | None = None):
+    """Run ``fn(rank, world, pg, *args_per_rank[rank])`` on ``num_workers`` workers, return results by rank.
+
+    ``max_restarts`` (default ``DDL_MAX_RESTARTS`` or 0): when a spawned worker dies, all
+    workers are torn down and the job is started again (``DDL_RESTART_COUNT`` tells the
+    new workers which attempt they are); workers that checkpoint (``utils/checkpoint.py``)
+    resume from their last checkpoint — the MI355X analog of Spark re-running a failed task.
+    """
+    if max_restarts is None:
+        max_restarts = int(os.environ.get("DDL_MAX_RESTARTS", "0"))
+    attempt = 0
+    while True:
+        try:
+            return _run_once(fn, num_workers, args_per_rank, device, timeout_s, attempt)
+        except WorkerFailure as e:
+            if attempt >= max_restarts:
+                raise
+            attempt += 1
+            print(f"[ddl-launcher] {e.short}; restarting all workers (attempt {attempt}/{max_restarts})",
+                  flush=True)
+
+
+class WorkerFailure(RuntimeError):
+    def __init__(self, msg, short):
+        super().__init__(msg)
+        self.short = short
+
+
+def _run_once(fn, num_workers, args_per_rank, device, timeout_s, attempt):
     from . import comm
 
     env_world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -106,6 +134,7 @@ def run_workers(fn, num_workers: int, args_per_rank, device: str | None = None, 
     env = dict(os.environ)
     root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    env["DDL_RESTART_COUNT"] = str(attempt)
     for r in range(num_workers):
         pp, rp = os.path.join(tmpdir, f"in{r}.pkl"), os.path.join(tmpdir, f"out{r}.pkl")
         with open(pp, "wb") as f:
@@ -150,7 +179,7 @@ def run_workers(fn, num_workers: int, args_per_rank, device: str | None = None, 
         shutil.rmtree(tmpdir, ignore_errors=True)
     if errors:
         r = sorted(errors)[0]
-        raise RuntimeError(f"worker {r} failed:\n{errors[r]}")
+        raise WorkerFailure(f"worker {r} failed:\n{errors[r]}", f"worker {r} failed")
     return [results[r] for r in range(num_workers)]
 
 
