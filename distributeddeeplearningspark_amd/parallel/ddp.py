@@ -133,22 +133,52 @@ class DataParallel:
                 for t in layer._states.values():
                     self.pg.broadcast_(t, src)
 
-    def train_step(self, x, y):
+    def train_step(self, x, y, timer=None):
+        """zero grads -> forward -> backward (bucket all-reduces overlap it) -> wait -> optimizer.
+
+        ``timer``: optional :class:`utils.tracing.StepTimer` collecting per-phase GPU times;
+        every phase is also a roctx range when tracing is on (``DDL_TRACE=1``)."""
         from ..ops.norm import reset_workspaces
+        from ..utils.tracing import trace_range
 
         m = self.model
-        reset_workspaces(m.device)
-        m.arena.zero_grad()
-        if self.overlap:
-            self._begin()
-        loss = m.compute_loss(x, y, training=True)
-        loss.backward()
-        if self.overlap:
-            self._finish()
-        elif self.pg.distributed:
-            self.sync_gradients()
-        m.optimizer.step(grad_scale=1.0 / self.pg.world_size)
+        phase = timer.phase if timer is not None else (lambda name: trace_range(name))
+        with trace_range("train_step"):
+            reset_workspaces(m.device)
+            m.arena.zero_grad()
+            if self.overlap:
+                self._begin()
+            with phase("forward"):
+                loss = m.compute_loss(x, y, training=True)
+            with phase("backward"):
+                loss.backward()
+            with phase("allreduce"):
+                if self.overlap:
+                    self._finish()
+                elif self.pg.distributed:
+                    self.sync_gradients()
+            with phase("optimizer"):
+                m.optimizer.step(grad_scale=1.0 / self.pg.world_size)
         return loss.detach()
+
+    @property
+    def grad_bytes(self) -> int:
+        return self.arena.grad.numel() * self.arena.grad.element_size() if self.pg.distributed else 0
+
+    def check_replicas(self, raise_on_mismatch: bool = True) -> bool:
+        """Divergence detection: after a synchronous update every replica must
+        hold identical weights.  Compares float64 (sum, sum-of-squares) checksums of the
+        flat master buffer across ranks."""
+        from ..utils.fault import replica_checksum
+
+        if not self.pg.distributed:
+            return True
+        mine = replica_checksum(self.arena.master)
+        allc = self.pg.all_gather_object(mine)
+        ok = all(c == allc[0] for c in allc)
+        if not ok and raise_on_mismatch:
+            raise RuntimeError(f"data-parallel replicas diverged: checksums {allc}")
+        return ok
 
     def all_reduce_flat_(self, t: torch.Tensor, average: bool = False):
         """All-reduce an arbitrary flat buffer in bucket-sized chunks (ADAG / DynSGD deltas)."""

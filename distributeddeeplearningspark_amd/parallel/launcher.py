@@ -133,7 +133,14 @@ def _run_once(fn, num_workers, args_per_rank, device, timeout_s, attempt):
     procs, res_paths = [], []
     env = dict(os.environ)
     root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    paths = [root]
+    try:  # the worker function's own directory, so test / script modules unpickle in the child
+        import inspect
+
+        paths.append(os.path.dirname(os.path.abspath(inspect.getfile(fn))))
+    except (TypeError, OSError):
+        pass
+    env["PYTHONPATH"] = os.pathsep.join(paths + ([env["PYTHONPATH"]] if env.get("PYTHONPATH") else []))
     env["DDL_RESTART_COUNT"] = str(attempt)
     for r in range(num_workers):
         pp, rp = os.path.join(tmpdir, f"in{r}.pkl"), os.path.join(tmpdir, f"out{r}.pkl")

@@ -86,6 +86,39 @@ class _Worker:
     def run(self, X, Y):
         raise NotImplementedError
 
+    # ---------------------------------------------------------------- fault tolerance
+    def _tick(self, it):
+        from .utils.fault import maybe_inject
+
+        maybe_inject(self.pg.rank, it)
+        if getattr(self, "watchdog", None) is not None:
+            self.watchdog.beat(it)
+
+    def _resume(self):
+        """(iterations already done, commit rounds already done) from the newest checkpoint."""
+        d = self.cfg.get("checkpoint_dir")
+        if not d:
+            return 0, 0
+        from .utils.checkpoint import latest_checkpoint, load_checkpoint
+
+        path = latest_checkpoint(d)
+        if path is None:
+            return 0, 0
+        _, meta = load_checkpoint(path, self.model)
+        ex = meta.get("extra", {})
+        self.resumed_from = path
+        return int(ex.get("it", 0)), int(ex.get("round", 0))
+
+    def _maybe_checkpoint(self, rnd, it):
+        d, every = self.cfg.get("checkpoint_dir"), int(self.cfg.get("checkpoint_every", 0) or 0)
+        if not d or every <= 0 or rnd % every:
+            return
+        from .utils.checkpoint import save_checkpoint
+
+        save_checkpoint(d, self.model, step=it, extra={"round": rnd, "it": it, "algorithm": self.cfg["algorithm"]},
+                        rank=self.pg.rank)
+        self.pg.barrier()  # nobody runs ahead of a checkpoint it may have to resume from
+
 
 class _CommitWorker(_Worker):
     """Periodic commit rounds (ADAG / DynSGD / DOWNPOUR / EASGD family)."""
@@ -94,14 +127,19 @@ class _CommitWorker(_Worker):
 
     def run(self, X, Y):
         a = self.arena
+        it0, rnd = self._resume()
         center = a.master.detach().clone()
-        it = rnd = 0
+        it = 0
         for xb, yb in self.batches(X, Y):
-            self.history.append(self.model.train_on_batch(xb, yb))
             it += 1
+            if it <= it0:  # resumed: these batches were consumed before the checkpoint
+                continue
+            self._tick(it)
+            self.history.append(self.model.train_on_batch(xb, yb))
             if it % self.k == 0 and rnd < self.rounds:
                 self.commit(center, rnd)
                 rnd += 1
+                self._maybe_checkpoint(rnd, it)
         while rnd < self.rounds:  # my shard is exhausted: join the remaining rounds with a zero delta
             self.commit(center, rnd)
             rnd += 1
@@ -263,14 +301,19 @@ class _SyncDPWorker(_Worker):
         from .parallel.ddp import DataParallel
 
         ddp = DataParallel(self.model, self.pg, bucket_mb=self.cfg.get("bucket_mb"))
+        it0, _ = self._resume()
         ddp.broadcast_parameters()
         it = 0
         for xb, yb in self.batches(X, Y):
             if it >= self.steps:
                 break
+            it += 1
+            if it <= it0:
+                continue
+            self._tick(it)
             xb, yb = self.model.to_input(xb), self.model.to_target(yb)
             self.history.append(float(ddp.train_step(xb, yb)))
-            it += 1
+            self._maybe_checkpoint(it, it)  # every `checkpoint_every` steps (with optimizer state)
         return self.arena.master.detach().clone()
 
 
@@ -297,7 +340,16 @@ def _train_worker(rank, world, pg, cfg, blob, X, Y, sizes):
     if cfg.get("mode") == "async" and issubclass(cls, _CommitWorker):
         cls = _AsyncPSWorker
     w = cls(cfg, model, pg, sizes)
-    final = w.run(Xd, Yd)
+    w.watchdog = None
+    if cfg.get("watchdog_s"):
+        from .utils.fault import Watchdog
+
+        w.watchdog = Watchdog(float(cfg["watchdog_s"])).start()
+    try:
+        final = w.run(Xd, Yd)
+    finally:
+        if w.watchdog is not None:
+            w.watchdog.stop()
     if model.device.type == "cuda":
         torch.cuda.synchronize(model.device)
     out = {"rank": rank, "history": w.history, "num_updates": w.num_updates(), "time": time.time() - t0}
@@ -419,7 +471,8 @@ class _ShardedTrainer(Trainer):
             server = self._start_async_server(cfg)
         try:
             args = [(cfg, self.master_model, Xs[r], Ys[r], sizes) for r in range(self.num_workers)]
-            results = run_workers(_train_worker, self.num_workers, args, device=self.device)
+            results = run_workers(_train_worker, self.num_workers, args, device=self.device,
+                                  max_restarts=self.extra.get("max_restarts"))
         finally:
             if server is not None:
                 center, n_upd = server.center().numpy().copy(), server.num_updates
