@@ -69,7 +69,12 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
   if (b_mode == OP_RC || b_mode == OP_RC_TAPS) TORCH_CHECK(ldb % 8 == 0, "gemm: ldb must be a multiple of 8");
   TORCH_CHECK(((uintptr_t)a.data_ptr() % 16) == 0 && ((uintptr_t)b.data_ptr() % 16) == 0, "gemm: operands must be 16-B aligned");
   TORCH_CHECK(k_split > 0 && k_split % 64 == 0, "gemm: k_split must be a positive multiple of 64");
-  TORCH_CHECK(tile >= 0 && tile <= 3, "gemm: bad tile id");
+  TORCH_CHECK(tile >= 0 && tile <= kTile256, "gemm: bad tile id");
+  if (tile == kTile256) {
+    TORCH_CHECK(a_mode <= OP_RC && b_mode <= OP_RC && !outmap.has_value(), "gemm256: plain KC/RC operands only");
+    TORCH_CHECK(K % 64 == 0 && k_split % 64 == 0, "gemm256: K and k_split must be multiples of 64");
+    TORCH_CHECK(M >= 8 && N >= 8, "gemm256: M, N >= 8");
+  }
   const int bm = (tile == 0 || tile == 1) ? 128 : 64;
   const int bn = (tile == 0 || tile == 2) ? 128 : 64;
   if (a_mode == OP_RC || a_mode == OP_RC_GATHER) TORCH_CHECK(M % 8 == 0, "gemm: row-contiguous A needs M % 8 == 0");
@@ -160,6 +165,7 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
 void register_ops(py::module& m);      // ops_bindings.cpp style registrations (elementwise, norms, ...)
 void register_runtime(py::module& m);  // host runtime (parameter server, ingest)
 void register_transformer(py::module& m);  // attention, LayerNorm, embeddings
+void register_rnn(py::module& m);          // persistent GRU / LSTM
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "MI355X-native kernels and runtime of distributeddeeplearningspark_amd";
@@ -186,5 +192,6 @@ PYBIND11_MODULE(_C, m) {
   m.attr("EPI_F32_ATOMIC") = (int)EPI_F32_ATOMIC;
   register_ops(m);
   register_transformer(m);
+  register_rnn(m);
   register_runtime(m);
 }

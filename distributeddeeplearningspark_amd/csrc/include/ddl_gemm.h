@@ -84,6 +84,7 @@ struct GemmParams {
 enum Activation : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_GELU_BWD = 3 };
 
 constexpr int kStatShards = 32;
+constexpr int kTile256 = 4;  // tile id of the 256x256 ping-pong kernel (ddl_gemm256.h)
 
 // host launcher (defined in gemm_bf16.hip); returns hipError_t as int
 int launch_gemm_bf16(const GemmParams& p, int epi, int tile, void* stream);

@@ -198,94 +198,25 @@ struct Operand {
   }
 };
 
-template <int BM, int BN, int AMODE, int BMODE, int EPI>
-__global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams p) {
-  constexpr int WTM = BM / 2, WTN = BN / 2;
-  constexpr int RM = WTM / 16, RN = WTN / 16;
-  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const bool one_stage = p.k_split <= BK;  // must match launch_tile's LDS allocation
-  char* lds_a0 = smem;
-  char* lds_a1 = smem + A_BYTES;
-  char* lds_b0 = smem + (one_stage ? A_BYTES : 2 * A_BYTES);
-  char* lds_b1 = smem + 2 * A_BYTES + B_BYTES;
-
-  const int tiles_n = (p.N + BN - 1) / BN;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int tm = bid / tiles_n, tn = bid - tm * tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int kbeg = blockIdx.y * p.k_split;
-  const int kend = min(p.K, kbeg + p.k_split);
-  const int nk = (kend - kbeg + BK - 1) / BK;
-
-  const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
-  const int wm0 = (wid >> 1) * WTM, wn0 = (wid & 1) * WTN;
-
-  Operand<BM, AMODE> A;
-  Operand<BN, BMODE> B;
-  A.init(p.a, p.lda, p.M, m0, p.K, p.g);
-  B.init(p.b, p.ldb, p.N, n0, p.K, p.g);
-
-  f32x4 acc[RM][RN];
-#pragma unroll
-  for (int i = 0; i < RM; ++i)
-#pragma unroll
-    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  if (nk > 0) {
-    A.load(kbeg, p.g, p.b_kdiv, p.b_tap_stride);
-    B.load(kbeg, p.g, p.b_kdiv, p.b_tap_stride);
-    A.store(lds_a0);
-    B.store(lds_b0);
-    __syncthreads();
-  }
-  for (int t = 0; t < nk; ++t) {
-    const bool odd = t & 1;
-    const char* la = odd ? lds_a1 : lds_a0;
-    const char* lb = odd ? lds_b1 : lds_b0;
-    const bool more = t + 1 < nk;
-    if (more) {
-      A.load(kbeg + (t + 1) * BK, p.g, p.b_kdiv, p.b_tap_stride);
-      B.load(kbeg + (t + 1) * BK, p.g, p.b_kdiv, p.b_tap_stride);
-    }
-#pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk) {
-      bf16x8 af[RM], bf[RN];
-#pragma unroll
-      for (int i = 0; i < RM; ++i) af[i] = A.frag(la, kk, i, wm0, lane);
-#pragma unroll
-      for (int j = 0; j < RN; ++j) bf[j] = B.frag(lb, kk, j, wn0, lane);
-#pragma unroll
-      for (int i = 0; i < RM; ++i)
-#pragma unroll
-        for (int j = 0; j < RN; ++j) {
-          if constexpr (EPI == EPI_BF16)
-            acc[i][j] = mfma16x16x32(bf[j], af[i], acc[i][j]);  // D^T: 4 consecutive n per lane (vector stores)
-          else
-            acc[i][j] = mfma16x16x32(af[i], bf[j], acc[i][j]);  // D: 16 consecutive n per row (coalesced atomics)
-        }
-    }
-    if (more) {
-      A.store(odd ? lds_a0 : lds_a1);
-      B.store(odd ? lds_b0 : lds_b1);
-    }
-    __syncthreads();
-  }
-
+// Epilogue shared by the GEMM kernels.  mb / nb: first row / column of this wave's
+// RM x RN fragment block.  bf16 epilogue: acc holds D^T fragments (lane owns 4 consecutive
+// columns of one row); fp32 epilogues: D fragments (16 consecutive columns per row).
+template <int RM, int RN, int EPI>
+__device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[RM][RN], const int mb, const int nb,
+                                              const int lane, const int bid) {
   // ---------------------------------- epilogue ----------------------------------
   if constexpr (EPI != EPI_BF16) {
     // fp32 (weight-gradient) epilogue, D orientation: acc[i][j][e] = C[m0+wm0+16i+4(lane>>4)+e][n0+wn0+16j+(lane&15)]
     // -> each atomic wave-instruction covers 4 rows x 64 contiguous bytes.
 #pragma unroll
     for (int j = 0; j < RN; ++j) {
-      const int n = n0 + wn0 + 16 * j + (lane & 15);
+      const int n = nb + 16 * j + (lane & 15);
       if (n >= p.N) continue;
 #pragma unroll
       for (int i = 0; i < RM; ++i) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int m = m0 + wm0 + 16 * i + 4 * (lane >> 4) + e;
+          const int m = mb + 16 * i + 4 * (lane >> 4) + e;
           if (m >= p.M) continue;
           float* c = reinterpret_cast<float*>(p.c) + (long)m * p.ldc + n;
           const float v = acc[i][j][e] * p.alpha;
@@ -308,7 +239,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams
   const bool vec_ok = (p.ldc % 4) == 0 && (!p.resid || (p.ldr % 4) == 0);
 #pragma unroll
   for (int i = 0; i < RM; ++i) {
-    const int m = m0 + wm0 + 16 * i + mrow;
+    const int m = mb + 16 * i + mrow;
     if (m >= p.M) continue;
     long rowoff;
     int nn = 0, ii = 0, jj = 0;
@@ -320,7 +251,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams
     }
 #pragma unroll
     for (int j = 0; j < RN; ++j) {
-      const int n = n0 + wn0 + 16 * j + ncol;
+      const int n = nb + 16 * j + ncol;
       if (n >= p.N) continue;
       const bool full = vec_ok && (n + 3 < p.N);
       float v[4];
@@ -420,7 +351,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams
             bf16_t* z = cb + ((long)(nn * p.om.hy + hy) * p.om.wy + wy) * p.ldc;
 #pragma unroll
             for (int j = 0; j < RN; ++j) {
-              const int n = n0 + wn0 + 16 * j + ncol;
+              const int n = nb + 16 * j + ncol;
               if (n + 3 < p.N && vec_ok) *reinterpret_cast<uint2*>(z + n) = make_uint2(0, 0);
               else
                 for (int e = 0; e < 4; ++e)
@@ -444,7 +375,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams
             a += __shfl_xor(a, o, 64);
             b += __shfl_xor(b, o, 64);
           }
-          const int n = n0 + wn0 + 16 * j + ncol + e;
+          const int n = nb + 16 * j + ncol + e;
           if (mrow == 0 && n < p.N) {
             atomicAdd(st + n, a);
             atomicAdd(st + p.N + n, b);
@@ -453,6 +384,84 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams
       }
     }
   }
+}
+
+template <int BM, int BN, int AMODE, int BMODE, int EPI>
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams p) {
+  constexpr int WTM = BM / 2, WTN = BN / 2;
+  constexpr int RM = WTM / 16, RN = WTN / 16;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const bool one_stage = p.k_split <= BK;  // must match launch_tile's LDS allocation
+  char* lds_a0 = smem;
+  char* lds_a1 = smem + A_BYTES;
+  char* lds_b0 = smem + (one_stage ? A_BYTES : 2 * A_BYTES);
+  char* lds_b1 = smem + 2 * A_BYTES + B_BYTES;
+
+  const int tiles_n = (p.N + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = bid / tiles_n, tn = bid - tm * tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kbeg = blockIdx.y * p.k_split;
+  const int kend = min(p.K, kbeg + p.k_split);
+  const int nk = (kend - kbeg + BK - 1) / BK;
+
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int wm0 = (wid >> 1) * WTM, wn0 = (wid & 1) * WTN;
+
+  Operand<BM, AMODE> A;
+  Operand<BN, BMODE> B;
+  A.init(p.a, p.lda, p.M, m0, p.K, p.g);
+  B.init(p.b, p.ldb, p.N, n0, p.K, p.g);
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+    A.load(kbeg, p.g, p.b_kdiv, p.b_tap_stride);
+    B.load(kbeg, p.g, p.b_kdiv, p.b_tap_stride);
+    A.store(lds_a0);
+    B.store(lds_b0);
+    __syncthreads();
+  }
+  for (int t = 0; t < nk; ++t) {
+    const bool odd = t & 1;
+    const char* la = odd ? lds_a1 : lds_a0;
+    const char* lb = odd ? lds_b1 : lds_b0;
+    const bool more = t + 1 < nk;
+    if (more) {
+      A.load(kbeg + (t + 1) * BK, p.g, p.b_kdiv, p.b_tap_stride);
+      B.load(kbeg + (t + 1) * BK, p.g, p.b_kdiv, p.b_tap_stride);
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8 af[RM], bf[RN];
+#pragma unroll
+      for (int i = 0; i < RM; ++i) af[i] = A.frag(la, kk, i, wm0, lane);
+#pragma unroll
+      for (int j = 0; j < RN; ++j) bf[j] = B.frag(lb, kk, j, wn0, lane);
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j) {
+          if constexpr (EPI == EPI_BF16)
+            acc[i][j] = mfma16x16x32(bf[j], af[i], acc[i][j]);  // D^T: 4 consecutive n per lane (vector stores)
+          else
+            acc[i][j] = mfma16x16x32(af[i], bf[j], acc[i][j]);  // D: 16 consecutive n per row (coalesced atomics)
+        }
+    }
+    if (more) {
+      A.store(odd ? lds_a0 : lds_a1);
+      B.store(odd ? lds_b0 : lds_b1);
+    }
+    __syncthreads();
+  }
+
+  gemm_epilogue<RM, RN, EPI>(p, acc, m0 + wm0, n0 + wn0, lane, bid);
 }
 
 template <int BM, int BN, int AMODE, int BMODE, int EPI>

@@ -116,4 +116,12 @@ int embed_fwd(const int64_t* ids, const int64_t* types, const void* word, const 
 int embed_bwd(const int64_t* ids, const int64_t* types, const void* ds, float* gword, float* gpos, float* wsT, int P,
               int ntypes, long T, int S, int H, hipStream_t s);
 
+// ---------------- persistent recurrent cells (Keras GRU reset_after=False / LSTM, fp32) ----------------
+// xw: [B][T][G*H] input projections (incl. bias); hs/cs: [B][T+1][H]; gates: [B][T][G*H] post-activation
+int rnn_fwd(int cell, const float* xw, const float* U, float* hs, float* cs, float* gates, float* y, int B, int T,
+            int H, int rs, hipStream_t s);
+// UT = U^T [G*H][H]; dgates [B][T][G*H] = gradients of the gate pre-activations
+int rnn_bwd(int cell, const float* dy, const float* UT, const float* hs, const float* cs, const float* gates,
+            float* dgates, int B, int T, int H, int rs, hipStream_t s);
+
 }  // namespace ddl

@@ -5,11 +5,16 @@ namespace ddl {
 int launch_gemm_plain_akc(const GemmParams& p, int epi, int tile, hipStream_t s);
 int launch_gemm_plain_arc(const GemmParams& p, int epi, int tile, hipStream_t s);
 int launch_gemm_conv(const GemmParams& p, int epi, int tile, hipStream_t s);
+int launch_gemm256(const GemmParams& p, int epi, hipStream_t s);
 
 int launch_gemm_bf16(const GemmParams& p, int epi, int tile, void* stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (p.M <= 0 || p.N <= 0) return 0;
   const bool plain = (p.a_mode == OP_KC || p.a_mode == OP_RC) && (p.b_mode == OP_KC || p.b_mode == OP_RC);
+  if (tile == kTile256) {  // 256x256 ping-pong kernel: plain operands, K and k_split multiples of 64
+    if (!plain || p.K % 64 || p.k_split % 64 || p.om.enabled) return (int)hipErrorInvalidValue;
+    return launch_gemm256(p, epi, s);
+  }
   if (plain) return p.a_mode == OP_KC ? launch_gemm_plain_akc(p, epi, tile, s) : launch_gemm_plain_arc(p, epi, tile, s);
   return launch_gemm_conv(p, epi, tile, s);
 }

@@ -1,0 +1,90 @@
+// pybind11 registrations of the persistent GRU / LSTM kernels (kernels/rnn.hip).  The input
+// projection and the parameter-gradient contractions are plain fp32 library GEMMs (ATen);
+// the recurrences run in the hand-written kernels.
+#include <torch/extension.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <ATen/DeviceGuard.h>
+
+#include "ddl_ops.h"
+
+namespace py = pybind11;
+using namespace ddl;
+
+namespace {
+
+inline hipStream_t cur_stream() { return at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+
+int cell_id(const std::string& cell) {
+  TORCH_CHECK(cell == "gru" || cell == "lstm", "rnn: cell must be 'gru' or 'lstm'");
+  return cell == "gru" ? 0 : 1;
+}
+
+py::tuple rnn_fwd_(const std::string& cell, const at::Tensor& x, const at::Tensor& W, const at::Tensor& U,
+                   c10::optional<at::Tensor> b, bool rs) {
+  const int c = cell_id(cell);
+  const int G = c == 0 ? 3 : 4;
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.dim() == 3, "rnn_fwd: x [B,T,I] fp32 on GPU");
+  const int64_t B = x.size(0), T = x.size(1), I = x.size(2), H = U.size(0);
+  TORCH_CHECK(W.size(0) == I && W.size(1) == G * H && U.size(1) == G * H, "rnn_fwd: W [I,GH], U [H,GH]");
+  at::DeviceGuard g(x.device());
+  at::Tensor xw = at::matmul(x.reshape({B * T, I}), W);
+  if (b) xw.add_(*b);
+  xw = xw.contiguous();
+  auto opt = x.options();
+  at::Tensor hs = at::empty({B, T + 1, H}, opt);
+  at::Tensor cs = c == 1 ? at::empty({B, T + 1, H}, opt) : at::empty({0}, opt);
+  at::Tensor gates = at::empty({B, T, G * H}, opt);
+  at::Tensor y = rs ? at::empty({B, T, H}, opt) : at::empty({B, H}, opt);
+  at::Tensor Uc = U.contiguous();
+  int e = rnn_fwd(c, xw.data_ptr<float>(), Uc.data_ptr<float>(), hs.data_ptr<float>(),
+                  c == 1 ? cs.data_ptr<float>() : nullptr, gates.data_ptr<float>(), y.data_ptr<float>(), (int)B,
+                  (int)T, (int)H, rs ? 1 : 0, cur_stream());
+  TORCH_CHECK(e == 0, "rnn_fwd launch failed: ", hipGetErrorString((hipError_t)e));
+  py::list saved;
+  saved.append(hs);
+  saved.append(cs);
+  saved.append(gates);
+  return py::make_tuple(y, saved);
+}
+
+py::tuple rnn_bwd_(const std::string& cell, const at::Tensor& dy, const at::Tensor& x, const at::Tensor& W,
+                   const at::Tensor& U, c10::optional<at::Tensor> b, bool rs, std::vector<at::Tensor> saved) {
+  const int c = cell_id(cell);
+  const int G = c == 0 ? 3 : 4;
+  const int64_t B = x.size(0), T = x.size(1), I = x.size(2), H = U.size(0);
+  TORCH_CHECK(saved.size() == 3, "rnn_bwd: saved = [hs, cs, gates]");
+  const at::Tensor& hs = saved[0];
+  const at::Tensor& cs = saved[1];
+  const at::Tensor& gates = saved[2];
+  at::DeviceGuard g(x.device());
+  at::Tensor dyc = dy.contiguous();
+  at::Tensor UT = U.t().contiguous();
+  at::Tensor dgates = at::empty({B, T, G * H}, x.options());
+  int e = rnn_bwd(c, dyc.data_ptr<float>(), UT.data_ptr<float>(), hs.data_ptr<float>(),
+                  c == 1 ? cs.data_ptr<float>() : nullptr, gates.data_ptr<float>(), dgates.data_ptr<float>(), (int)B,
+                  (int)T, (int)H, rs ? 1 : 0, cur_stream());
+  TORCH_CHECK(e == 0, "rnn_bwd launch failed: ", hipGetErrorString((hipError_t)e));
+  at::Tensor dg = dgates.view({B * T, G * H});
+  at::Tensor x2 = x.reshape({B * T, I});
+  at::Tensor dW = at::matmul(x2.t(), dg);
+  at::Tensor dx = at::matmul(dg, W.t()).view({B, T, I});
+  at::Tensor db = b ? dg.sum(0) : at::Tensor();
+  at::Tensor hp = hs.narrow(1, 0, T).reshape({B * T, H});
+  at::Tensor dU;
+  if (c == 0) {
+    dU = at::empty_like(U);
+    dU.narrow(1, 0, 2 * H).copy_(at::matmul(hp.t(), dg.narrow(1, 0, 2 * H)));
+    at::Tensor rh = gates.view({B * T, G * H}).narrow(1, H, H) * hp;
+    dU.narrow(1, 2 * H, H).copy_(at::matmul(rh.t(), dg.narrow(1, 2 * H, H)));
+  } else {
+    dU = at::matmul(hp.t(), dg);
+  }
+  return py::make_tuple(dx, dW, dU, db.defined() ? py::cast(db) : py::none());
+}
+
+}  // namespace
+
+void register_rnn(py::module& m) {
+  m.def("rnn_fwd", &rnn_fwd_, "persistent GRU/LSTM forward (fp32)");
+  m.def("rnn_bwd", &rnn_bwd_, "persistent GRU/LSTM backward (fp32)");
+}

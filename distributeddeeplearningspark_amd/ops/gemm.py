@@ -18,8 +18,26 @@ from ._native import C
 
 KC, RC, KC_GATHER, RC_GATHER, RC_TAPS, KC_GATHER8, RC_GATHER8 = 0, 1, 2, 3, 4, 5, 6
 EPI_BF16, EPI_F32, EPI_F32_ATOMIC = 0, 1, 2
-_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64)}
+TILE256 = 4  # 256x256 ping-pong kernel (csrc/include/ddl_gemm256.h): plain KC/RC operands, K % 64 == 0
+_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), TILE256: (256, 256)}
 _CU = 256
+import os as _os
+
+# Measured (scripts/bench_gemm.py, random bf16): the 256x256 kernel wins on large-K, large-M/N
+# GEMMs (8192^3: ~1045 vs ~810 TF for the 128-tile kernel) but loses on the BERT / ResNet
+# shapes (K <= 3072 with <= 2.25 workgroup rounds), so it is opt-in (DDL_GEMM256=1) and
+# auto-selected only for GEMMs with many tiles AND a long K loop.
+_USE256 = _os.environ.get("DDL_GEMM256", "auto")
+
+
+def use_tile256(M: int, N: int, K: int, a_mode: int, b_mode: int, epi: int) -> bool:
+    """The 256x256 kernel pays off when its tiles (times split-K for fp32 outputs) fill the chip."""
+    if _USE256 == "0" or a_mode > RC or b_mode > RC or K % 64 or M < 128 or N < 128:
+        return False
+    tiles = math.ceil(M / 256) * math.ceil(N / 256)
+    if _USE256 == "1":
+        return tiles >= _CU // 2
+    return epi == EPI_BF16 and tiles >= 4 * _CU and K >= 4096
 
 
 def choose_tile(M: int, N: int, bn_cap: int = 128) -> int:
@@ -42,9 +60,10 @@ def choose_split(M: int, N: int, K: int, tile: int, allow: bool) -> int:
         return kfull
     bm, bn = _TILES[tile]
     tiles = math.ceil(M / bm) * math.ceil(N / bn)
-    if tiles >= 2 * _CU or K < 1024:
+    per_cu = 1 if tile == TILE256 else 2  # resident workgroups per CU
+    if tiles >= per_cu * _CU or K < 1024:
         return kfull
-    splits = min(math.ceil(4 * _CU / tiles), max(1, K // 512))
+    splits = min(math.ceil(2 * per_cu * _CU / tiles), max(1, K // 512))
     ks = math.ceil(K / splits / 64) * 64
     return max(64, ks)
 
@@ -60,7 +79,7 @@ def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, bet
     ``beta == 1`` semantics.
     """
     if tile is None:
-        tile = choose_tile(M, N, bn_cap)
+        tile = TILE256 if (outmap is None and use_tile256(M, N, K, a_mode, b_mode, epi)) else choose_tile(M, N, bn_cap)
     if k_split is None:
         k_split = choose_split(M, N, K, tile, allow=(epi != EPI_BF16))
     if epi == EPI_F32 and k_split < K:

@@ -1,9 +1,10 @@
 """``DataFrameReader`` / ``DataFrameWriter``: CSV (header + inferSchema, the reference's
 ``com.databricks.spark.csv`` ingest, ``ddl_mnist_aztk.py:100-107``), Parquet, JSON.
 
-Paths are local files or directories (``file://`` accepted).  Cloud URIs
-(``wasb://``, ``abfs://``, ``s3://``) are rejected with a clear error: this
-environment has no network and the framework never ships storage credentials.
+Paths are local files or directories (``file://`` accepted).  ``wasb[s]://`` /
+``abfs[s]://`` URIs of an account attached with ``utils.storage.attach_storage_container``
+resolve to its local mount; other cloud URIs are rejected with a clear error (no network,
+and the framework never ships storage credentials).
 """
 from __future__ import annotations
 
@@ -19,6 +20,9 @@ from .dataframe import DataFrame, from_columns
 
 
 def _local(path: str) -> list[str]:
+    from ..utils.storage import resolve
+
+    path = resolve(path)
     if path.startswith("file://"):
         path = path[len("file://"):]
     if "://" in path:
