@@ -93,7 +93,7 @@ def init_from_env(prefer_gpu: bool = True, timeout_s: float = 600.0, backend: st
         device = torch.device("cpu")
     be = None
     if world > 1:
-        be = backend or ("nccl" if use_gpu else "gloo")
+        be = backend or os.environ.get("DDL_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if not dist.is_initialized():
             kw = dict(backend=be, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
