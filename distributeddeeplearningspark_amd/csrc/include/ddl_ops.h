@@ -103,11 +103,17 @@ int layernorm_fwd(const void* x, const float* gamma, const float* beta, void* y,
 // dropout of the residual branch, nullable); per-wave partial rows ws[P][2][H] of dgamma/dbeta
 int ln_partial_rows(long M);
 // in_drop_p/in_seed: dy is first masked by the forward's output dropout
+// parts = 2: ws[P][2][H] = (dgamma, dbeta); parts = 3: ws[P][3][H] = (dbias, dgamma, dbeta) where
+// dbias = column sums of dx_drop, the bias gradient of the GEMM whose dropped output fed the residual sum
 int layernorm_bwd(const void* dy, const void* x, const float* mean, const float* rstd, const float* gamma, void* dx,
                   void* dx_drop, float drop_p, unsigned long long seed, float* ws, int P, long M, int H,
-                  float in_drop_p, unsigned long long in_seed, hipStream_t s);
+                  float in_drop_p, unsigned long long in_seed, int parts, hipStream_t s);
+// word-embedding gradient from tokens sorted by id (no atomics); position gradient (sum over batch)
+int embed_word_grad(const int64_t* sorted_ids, const int64_t* perm, const void* ds, float* gword, long T, int H,
+                    hipStream_t s);
+int embed_pos_grad(const void* ds, float* gpos, int B, int S, int H, hipStream_t s);
 // out[n] (+)= sum_p ws[p][n]
-int colsum_partials(const float* ws, int P, int N, float* out, int accumulate, hipStream_t s);
+int colsum_partials(const float* ws, int P, int N, float* out, int accumulate, hipStream_t s, long ld = 0);
 // out[t] = word[ids[t]] + pos[t % S] + type[types[t]]  (bf16 tables, types nullable -> row 0)
 int embed_fwd(const int64_t* ids, const int64_t* types, const void* word, const void* pos, const void* type,
               void* out, long T, int S, int H, hipStream_t s);

@@ -82,10 +82,20 @@ __device__ __forceinline__ bf16x8 pack8(const f32x4& a, const f32x4& b) {
 
 __device__ __forceinline__ bf16x8 ldg_frag(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
-__device__ __forceinline__ unsigned long long drop_index(int bh, int S, int i, int j) {
-  return ((unsigned long long)bh * (unsigned long long)S + (unsigned long long)i) * (unsigned long long)S +
-         (unsigned long long)j;
+// Attention-probability dropout: keep (b, h, i, j) iff mix32(row_key(bh, i) + j) >= thresh.
+// The per-(row) key is hashed once, every element costs one 32-bit mix (vs a 64-bit hash).
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
 }
+__device__ __forceinline__ uint32_t row_key(unsigned long long seed, int bh, int S, int i) {
+  return mix32((uint32_t)seed ^ mix32((uint32_t)(bh * S + i) + (uint32_t)(seed >> 32)));
+}
+__device__ __forceinline__ bool keep_elem(uint32_t rk, int j, uint32_t thresh) { return mix32(rk + (uint32_t)j) >= thresh; }
 
 // ================================================================ forward
 __global__ __launch_bounds__(THREADS, 2) void attn_fwd_kernel(const AttnParams p) {
@@ -112,6 +122,9 @@ __global__ __launch_bounds__(THREADS, 2) void attn_fwd_kernel(const AttnParams p
 #pragma unroll
     for (int it = 0; it < 2; ++it) o[dt][it] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+  uint32_t rk[2];
+#pragma unroll
+  for (int it = 0; it < 2; ++it) rk[it] = row_key(p.drop_seed, bh, S, q0 + 16 * it + li);
 
   const int nkt = (len + TQ - 1) / TQ;
   TileStage sk, sv;
@@ -179,10 +192,9 @@ __global__ __launch_bounds__(THREADS, 2) void attn_fwd_kernel(const AttnParams p
 #pragma unroll
         for (int jt = 0; jt < 4; ++jt)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const unsigned long long idx = drop_index(bh, S, q0 + 16 * it + li, kb + 16 * jt + 4 * g + e);
-            s[jt][it][e] = drop_keep(p.drop_seed, idx, p.drop_thresh) ? s[jt][it][e] * p.drop_scale : 0.f;
-          }
+          for (int e = 0; e < 4; ++e)
+            s[jt][it][e] = keep_elem(rk[it], kb + 16 * jt + 4 * g + e, p.drop_thresh) ? s[jt][it][e] * p.drop_scale
+                                                                                    : 0.f;
     }
     // O^T[d][i] += sum_j V^T[d][j] P^T[j][i]
 #pragma unroll
@@ -335,13 +347,13 @@ __global__ __launch_bounds__(THREADS, 1) void attn_bwd_dkdv_kernel(const AttnPar
       for (int e = 0; e < 4; ++e) {
         const int il = 16 * it + 4 * g + e;
         const float lq = s_lse[buf][il], dq = s_d[buf][il];
+        const uint32_t rki = p.drop_thresh ? row_key(p.drop_seed, bh, S, qb + il) : 0u;
 #pragma unroll
         for (int jt = 0; jt < 2; ++jt) {
           const int j = k0 + 16 * jt + li;
           float pv = (j < len) ? exp2f(s[it][jt][e] * p.scale_log2 - lq) : 0.f;
           float keep = 1.f;
-          if (p.drop_thresh)
-            keep = drop_keep(p.drop_seed, drop_index(bh, S, qb + il, j), p.drop_thresh) ? p.drop_scale : 0.f;
+          if (p.drop_thresh) keep = keep_elem(rki, j, p.drop_thresh) ? p.drop_scale : 0.f;
           dp[it][jt][e] = pv * (dp[it][jt][e] * keep - dq);  // dS
           s[it][jt][e] = pv * keep;                          // dropped P (for dV)
         }
@@ -406,6 +418,7 @@ __global__ __launch_bounds__(THREADS, 2) void attn_bwd_dq_kernel(const AttnParam
 
   bf16x8 qf[2][2], df[2][2];
   float lq[2], dq[2];
+  uint32_t rk[2];
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
     const int i = q0 + 16 * it + li;
@@ -416,6 +429,7 @@ __global__ __launch_bounds__(THREADS, 2) void attn_bwd_dq_kernel(const AttnParam
     }
     lq[it] = p.lse[(long)bh * S + i];
     dq[it] = p.dvec[(long)bh * S + i];
+    rk[it] = row_key(p.drop_seed, bh, S, i);
   }
   f32x4 acc[2][4];  // dQ[i = 16it + 4g + e][d = 16dt + li]
 #pragma unroll
@@ -465,9 +479,7 @@ __global__ __launch_bounds__(THREADS, 2) void attn_bwd_dq_kernel(const AttnParam
           const int j = kb + 16 * jt + 4 * g + e;
           const float pv = (j < len) ? exp2f(s[jt][it][e] * p.scale_log2 - lq[it]) : 0.f;
           float keep = 1.f;
-          if (p.drop_thresh)
-            keep = drop_keep(p.drop_seed, drop_index(bh, S, q0 + 16 * it + li, j), p.drop_thresh) ? p.drop_scale
-                                                                                                   : 0.f;
+          if (p.drop_thresh) keep = keep_elem(rk[it], j, p.drop_thresh) ? p.drop_scale : 0.f;
           s[jt][it][e] = pv * (dp[jt][it][e] * keep - dq[it]);  // dS^T
         }
     // dQ[i][d] += sum_j dS[i][j] K[j][d]

@@ -91,16 +91,17 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
                                                      const float* __restrict__ gamma, bf16_t* __restrict__ dx,
                                                      bf16_t* __restrict__ dxd, uint32_t thresh, float dscale,
                                                      unsigned long long seed, float* __restrict__ ws, long M, int H,
-                                                     uint32_t in_thresh, float in_scale, unsigned long long in_seed) {
+                                                     uint32_t in_thresh, float in_scale, unsigned long long in_seed,
+                                                     int parts) {
   const int lane = threadIdx.x & 63;
   const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int nwaves = gridDim.x * 4;
   const int nv = H >> 3;
-  float dg[VPL][8], db[VPL][8];
+  float dg[VPL][8], db[VPL][8], dd[VPL][8];
 #pragma unroll
   for (int u = 0; u < VPL; ++u)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) dg[u][e] = db[u][e] = 0.f;
+    for (int e = 0; e < 8; ++e) dg[u][e] = db[u][e] = dd[u][e] = 0.f;
   for (long row = wave; row < M; row += nwaves) {
     const float mu = mean[row], rs = rstd[row];
     float gy[VPL][8], xh[VPL][8];
@@ -142,18 +143,39 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
         float o[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) o[e] = rs * (gy[u][e] - a - xh[u][e] * b);
-        *reinterpret_cast<uint4*>(dx + row * H + c * 8) = pack8f(o);
+        uint4 packed = pack8f(o);
+        *reinterpret_cast<uint4*>(dx + row * H + c * 8) = packed;
         if (dxd) {
           const unsigned long long base = (unsigned long long)row * (unsigned long long)H + c * 8;
 #pragma unroll
           for (int e = 0; e < 8; ++e) o[e] = drop_keep(seed, base + e, thresh) ? o[e] * dscale : 0.f;
-          *reinterpret_cast<uint4*>(dxd + row * H + c * 8) = pack8f(o);
+          packed = pack8f(o);
+          *reinterpret_cast<uint4*>(dxd + row * H + c * 8) = packed;
+        }
+        if (parts == 3) {  // column sums of the stored gradient (dx_drop, else dx): the sublayer's bias grad
+          float r[8];
+          unpack8(packed, r);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) dd[u][e] += r[e];
         }
       }
     }
   }
   if (ws) {
-    float* w0 = ws + (long)wave * 2 * H;
+    // parts == 2: [dgamma | dbeta]; parts == 3: [dbias | dgamma | dbeta] (the arena order of a
+    // sublayer's output bias followed by the LayerNorm's gamma and beta)
+    float* wb = ws + (long)wave * parts * H;
+    float* w0 = parts == 3 ? wb + H : wb;
+    if (parts == 3) {
+#pragma unroll
+      for (int u = 0; u < VPL; ++u) {
+        const int c = lane + 64 * u;
+        if (c < nv) {
+          *reinterpret_cast<float4*>(wb + c * 8) = make_float4(dd[u][0], dd[u][1], dd[u][2], dd[u][3]);
+          *reinterpret_cast<float4*>(wb + c * 8 + 4) = make_float4(dd[u][4], dd[u][5], dd[u][6], dd[u][7]);
+        }
+      }
+    }
 #pragma unroll
     for (int u = 0; u < VPL; ++u) {
       const int c = lane + 64 * u;
@@ -167,21 +189,25 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
   }
 }
 
-// out[n] (+)= sum_p ws[p][n]; block (64 columns x 16 row groups)
-__global__ __launch_bounds__(1024) void colsum_kernel(const float* __restrict__ ws, int P, int N,
-                                                      float* __restrict__ out, int accumulate) {
+// out[n] += sum_p ws[p][n]; block = 64 columns x 16 row-lanes over a chunk of kColsumRows rows,
+// grid.y = row chunks (one fp32 atomic per column per block; out zeroed by the launcher when
+// not accumulating)
+constexpr int kColsumRows = 128;
+__global__ __launch_bounds__(1024) void colsum_kernel(const float* __restrict__ ws, int P, int N, long ld,
+                                                      float* __restrict__ out) {
   __shared__ float red[16][65];
   const int n = blockIdx.x * 64 + threadIdx.x;
+  const int p0 = blockIdx.y * kColsumRows, p1 = min(P, p0 + kColsumRows);
   float s = 0.f;
   if (n < N)
-    for (int p = threadIdx.y; p < P; p += 16) s += ws[(long)p * N + n];
+    for (int p = p0 + threadIdx.y; p < p1; p += 16) s += ws[(long)p * ld + n];
   red[threadIdx.y][threadIdx.x] = s;
   __syncthreads();
   if (threadIdx.y == 0 && n < N) {
     float t = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) t += red[r][threadIdx.x];
-    out[n] = accumulate ? out[n] + t : t;
+    atomicAdd(out + n, t);
   }
 }
 
@@ -256,6 +282,69 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const int64_t* __restric
   }
 }
 
+// word-embedding gradient from tokens sorted by id: wave w sums the rows of sorted positions
+// [32w, 32w + 32), flushing one partial sum per run of equal ids.  A run that lies entirely
+// inside the chunk has a single writer (plain read-modify-write); a run crossing a chunk edge
+// (a frequent id such as [MASK]) is flushed with fp32 atomics, one per chunk.
+constexpr int kEmbChunk = 32;
+__global__ __launch_bounds__(256) void embed_word_grad_kernel(const int64_t* __restrict__ sorted_ids,
+                                                             const int64_t* __restrict__ perm,
+                                                             const bf16_t* __restrict__ ds, float* __restrict__ gword,
+                                                             long T, int H) {
+  const long c0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * kEmbChunk;
+  const int lane = threadIdx.x & 63;
+  if (c0 >= T) return;
+  const long c1 = min(T, c0 + kEmbChunk);
+  const bool head_shared = c0 > 0 && sorted_ids[c0 - 1] == sorted_ids[c0];
+  const bool tail_shared = c1 < T && sorted_ids[c1] == sorted_ids[c1 - 1];
+  for (int c = lane * 8; c < H; c += 512) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    long run_start = c0;
+    int64_t id = sorted_ids[c0];
+    for (long j = c0; j < c1; ++j) {
+      float d[8];
+      unpack8(*reinterpret_cast<const uint4*>(ds + perm[j] * H + c), d);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += d[e];
+      const bool last = j + 1 == c1 || sorted_ids[j + 1] != id;
+      if (last) {
+        float* g = gword + id * H + c;
+        const bool shared = (run_start == c0 && head_shared) || (j + 1 == c1 && tail_shared);
+        if (shared) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) atomicAdd(g + e, acc[e]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) g[e] += acc[e];
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+        if (j + 1 < c1) {
+          run_start = j + 1;
+          id = sorted_ids[j + 1];
+        }
+      }
+    }
+  }
+}
+
+// position-embedding gradient: gpos[s][h] += sum_b ds[b*S + s][h]  (column sums, no atomics)
+__global__ __launch_bounds__(256) void embed_pos_grad_kernel(const bf16_t* __restrict__ ds, float* __restrict__ gpos,
+                                                            int B, int S, int H) {
+  const long col = (long)blockIdx.x * 256 + threadIdx.x;  // over S*H/2 bf16 pairs
+  if (col * 2 >= (long)S * H) return;
+  float a = 0.f, b = 0.f;
+  const uint32_t* p = reinterpret_cast<const uint32_t*>(ds) + col;
+  const long stride = (long)S * H / 2;
+  for (int r = 0; r < B; ++r) {
+    const uint32_t w = p[r * stride];
+    a += __uint_as_float(w << 16);
+    b += __uint_as_float(w & 0xffff0000u);
+  }
+  gpos[col * 2] += a;
+  gpos[col * 2 + 1] += b;
+}
+
 constexpr int kLnBwdBlocks = 256;
 
 }  // namespace
@@ -283,7 +372,7 @@ int ln_partial_rows(long M) {
 
 int layernorm_bwd(const void* dy, const void* x, const float* mean, const float* rstd, const float* gamma, void* dx,
                   void* dx_drop, float drop_p, unsigned long long seed, float* ws, int P, long M, int H,
-                  float in_drop_p, unsigned long long in_seed, hipStream_t s) {
+                  float in_drop_p, unsigned long long in_seed, int parts, hipStream_t s) {
   if (M <= 0) return 0;
   const uint32_t ith = in_drop_p > 0.f ? (uint32_t)std::min(4294967295.0, (double)in_drop_p * 4294967296.0) : 0u;
   const float iscale = in_drop_p > 0.f ? 1.f / (1.f - in_drop_p) : 1.f;
@@ -295,16 +384,21 @@ int layernorm_bwd(const void* dy, const void* x, const float* mean, const float*
   auto X = reinterpret_cast<const bf16_t*>(x);
   auto DX = reinterpret_cast<bf16_t*>(dx);
   auto DD = reinterpret_cast<bf16_t*>(dx_drop);
-  if (nv <= 64) hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed);
-  else if (nv <= 128) hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed);
-  else if (nv <= 256) hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed);
-  else hipLaunchKernelGGL(ln_bwd_kernel<8>, grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed);
+  if (nv <= 64) hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts);
+  else if (nv <= 128) hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts);
+  else if (nv <= 256) hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts);
+  else hipLaunchKernelGGL(ln_bwd_kernel<8>, grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts);
   return (int)hipGetLastError();
 }
 
-int colsum_partials(const float* ws, int P, int N, float* out, int accumulate, hipStream_t s) {
+int colsum_partials(const float* ws, int P, int N, float* out, int accumulate, hipStream_t s, long ld) {
   if (N <= 0) return 0;
-  hipLaunchKernelGGL(colsum_kernel, dim3((N + 63) / 64), dim3(64, 16), 0, s, ws, P, N, out, accumulate);
+  if (!accumulate) {
+    const hipError_t e = hipMemsetAsync(out, 0, sizeof(float) * (size_t)N, s);
+    if (e != hipSuccess) return (int)e;
+  }
+  hipLaunchKernelGGL(colsum_kernel, dim3((N + 63) / 64, (P + kColsumRows - 1) / kColsumRows), dim3(64, 16), 0, s, ws,
+                     P, N, ld > 0 ? ld : (long)N, out);
   return (int)hipGetLastError();
 }
 
@@ -315,6 +409,22 @@ int embed_fwd(const int64_t* ids, const int64_t* types, const void* word, const 
   hipLaunchKernelGGL(embed_fwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ids, types,
                      reinterpret_cast<const bf16_t*>(word), reinterpret_cast<const bf16_t*>(pos),
                      reinterpret_cast<const bf16_t*>(type), reinterpret_cast<bf16_t*>(out), T, S, H);
+  return (int)hipGetLastError();
+}
+
+int embed_word_grad(const int64_t* sorted_ids, const int64_t* perm, const void* ds, float* gword, long T, int H,
+                    hipStream_t s) {
+  if (T <= 0) return 0;
+  const long waves = (T + kEmbChunk - 1) / kEmbChunk;
+  hipLaunchKernelGGL(embed_word_grad_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, sorted_ids, perm,
+                     reinterpret_cast<const bf16_t*>(ds), gword, T, H);
+  return (int)hipGetLastError();
+}
+
+int embed_pos_grad(const void* ds, float* gpos, int B, int S, int H, hipStream_t s) {
+  const long n = (long)S * H / 2;
+  hipLaunchKernelGGL(embed_pos_grad_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                     reinterpret_cast<const bf16_t*>(ds), gpos, B, S, H);
   return (int)hipGetLastError();
 }
 

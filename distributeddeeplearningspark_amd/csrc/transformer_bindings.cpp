@@ -122,7 +122,8 @@ int64_t ln_partial_rows_(int64_t M) { return ln_partial_rows(M); }
 
 void layernorm_bwd_(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& mean, const at::Tensor& rstd,
                     c10::optional<at::Tensor> gamma, const at::Tensor& dx, c10::optional<at::Tensor> dx_drop,
-                    double drop_p, int64_t seed, c10::optional<at::Tensor> ws, double in_drop_p, int64_t in_seed) {
+                    double drop_p, int64_t seed, c10::optional<at::Tensor> ws, double in_drop_p, int64_t in_seed,
+                    int64_t parts) {
   GPU(dy); BF16(dy); BF16(x); BF16(dx); F32(mean); F32(rstd);
   const int64_t H = x.size(-1), M = x.numel() / H;
   CK(H % 8 == 0 && H <= 4096, "layernorm_bwd: H % 8 == 0 and H <= 4096");
@@ -130,20 +131,41 @@ void layernorm_bwd_(const at::Tensor& dy, const at::Tensor& x, const at::Tensor&
   if (gamma) { F32(*gamma); CK(gamma->numel() == H, "gamma [H]"); }
   if (dx_drop) { BF16(*dx_drop); CK(dx_drop->numel() == x.numel(), "dx_drop shape"); }
   const int P = ln_partial_rows(M);
-  if (ws) { F32(*ws); CK(ws->numel() >= (int64_t)P * 2 * H, "layernorm_bwd: ws must hold [P][2][H]"); }
+  CK(parts == 2 || parts == 3, "layernorm_bwd: parts must be 2 or 3");
+  if (ws) { F32(*ws); CK(ws->numel() >= (int64_t)P * parts * H, "layernorm_bwd: ws must hold [P][parts][H]"); }
   at::DeviceGuard g(x.device());
   HIP_OK(layernorm_bwd(dy.data_ptr(), x.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
                        optr<const float>(gamma), dx.data_ptr(), optr<void>(dx_drop), dx_drop ? (float)drop_p : 0.f,
                        (unsigned long long)seed, optr<float>(ws), P, M, (int)H, (float)in_drop_p,
-                       (unsigned long long)in_seed, cur_stream()));
+                       (unsigned long long)in_seed, (int)parts, cur_stream()));
 }
 
-void colsum_partials_(const at::Tensor& ws, int64_t P, int64_t N, const at::Tensor& out, bool accumulate) {
+void embed_word_grad_(const at::Tensor& sorted_ids, const at::Tensor& perm, const at::Tensor& ds,
+                      const at::Tensor& gword) {
+  GPU(ds); I64(sorted_ids); I64(perm); BF16(ds); F32(gword);
+  const int64_t T = sorted_ids.numel(), H = ds.size(-1);
+  CK(perm.numel() == T && ds.numel() == T * H && gword.size(-1) == H && H % 8 == 0, "embed_word_grad: shapes");
+  at::DeviceGuard g(ds.device());
+  HIP_OK(embed_word_grad(sorted_ids.data_ptr<int64_t>(), perm.data_ptr<int64_t>(), ds.data_ptr(),
+                         gword.data_ptr<float>(), T, (int)H, cur_stream()));
+}
+
+void embed_pos_grad_(const at::Tensor& ds, const at::Tensor& gpos, int64_t B, int64_t S) {
+  GPU(ds); BF16(ds); F32(gpos);
+  const int64_t H = ds.size(-1);
+  CK(ds.numel() == B * S * H && gpos.size(0) >= S && gpos.size(1) == H && H % 2 == 0, "embed_pos_grad: shapes");
+  at::DeviceGuard g(ds.device());
+  HIP_OK(embed_pos_grad(ds.data_ptr(), gpos.data_ptr<float>(), (int)B, (int)S, (int)H, cur_stream()));
+}
+
+void colsum_partials_(const at::Tensor& ws, int64_t P, int64_t N, const at::Tensor& out, bool accumulate,
+                      int64_t ld) {
   GPU(ws); F32(ws); F32(out);
-  CK(ws.numel() >= P * N && out.numel() >= N, "colsum_partials: sizes");
+  if (ld <= 0) ld = N;
+  CK(ld >= N && ws.numel() >= (P - 1) * ld + N && out.numel() >= N, "colsum_partials: sizes");
   at::DeviceGuard g(ws.device());
   HIP_OK(colsum_partials(ws.data_ptr<float>(), (int)P, (int)N, out.data_ptr<float>(), accumulate ? 1 : 0,
-                         cur_stream()));
+                         cur_stream(), (long)ld));
 }
 
 void embed_fwd_(const at::Tensor& ids, c10::optional<at::Tensor> types, const at::Tensor& word, const at::Tensor& pos,
@@ -191,8 +213,11 @@ void register_transformer(py::module& m) {
   m.def("ln_partial_rows", &ln_partial_rows_);
   m.def("layernorm_bwd", &layernorm_bwd_, py::arg("dy"), py::arg("x"), py::arg("mean"), py::arg("rstd"),
         py::arg("gamma"), py::arg("dx"), py::arg("dx_drop"), py::arg("drop_p"), py::arg("seed"), py::arg("ws"),
-        py::arg("in_drop_p") = 0.0, py::arg("in_seed") = 0);
-  m.def("colsum_partials", &colsum_partials_);
+        py::arg("in_drop_p") = 0.0, py::arg("in_seed") = 0, py::arg("parts") = 2);
+  m.def("embed_word_grad", &embed_word_grad_);
+  m.def("embed_pos_grad", &embed_pos_grad_);
+  m.def("colsum_partials", &colsum_partials_, py::arg("ws"), py::arg("P"), py::arg("N"), py::arg("out"),
+        py::arg("accumulate"), py::arg("ld") = 0);
   m.def("embed_fwd", &embed_fwd_);
   m.def("embed_partial_rows", &embed_partial_rows_);
   m.def("embed_bwd", &embed_bwd_);

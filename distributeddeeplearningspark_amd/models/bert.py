@@ -85,6 +85,26 @@ def _seed(*parts) -> int:
     return h & 0x7FFFFFFFFFFFFFFF
 
 
+def _contiguous(*ts) -> bool:
+    """True when the 1-D tensors are back-to-back in memory (consecutive arena parameters)."""
+    for a, b in zip(ts, ts[1:]):
+        if a.data_ptr() + a.numel() * a.element_size() != b.data_ptr():
+            return False
+    return True
+
+
+def _ln_param_grads(ws, H, g_param, b_param):
+    """Column sums of LayerNorm partial rows [P][2][H] into (gamma, beta) gradients."""
+    P_ = ws.shape[0]
+    if _contiguous(g_param.grad, b_param.grad):
+        C().colsum_partials(ws.view(P_, 2 * H), P_, 2 * H, g_param.grad.as_strided((2 * H,), (1,)), True)
+    else:
+        red = torch.empty(2 * H, dtype=torch.float32, device=ws.device)
+        C().colsum_partials(ws.view(P_, 2 * H), P_, 2 * H, red, False)
+        g_param.grad.add_(red[:H])
+        b_param.grad.add_(red[H:])
+
+
 def _bias_grad(d2, gb):
     if gb is not None:
         C().bias_grad(d2, gb, d2.shape[1], True)
@@ -229,19 +249,19 @@ class _EmbeddingsFn(torch.autograd.Function):
             de = torch.empty_like(e)
             ws = torch.empty((C().ln_partial_rows(T_), 2, H), dtype=torch.float32, device=e.device)
             C().layernorm_bwd(dy.contiguous(), e, mean, rstd, layer.ln_g.master, de, None, 0.0, 0, ws, ctx.p, ctx.seed)
-            red = torch.empty(2 * H, dtype=torch.float32, device=e.device)
-            C().colsum_partials(ws.view(-1, 2 * H), ws.shape[0], 2 * H, red, False)
-            layer.ln_g.grad.add_(red[:H])
-            layer.ln_b.grad.add_(red[H:])
+            _ln_param_grads(ws, H, layer.ln_g, layer.ln_b)
+            # word rows: tokens sorted by id, one writer per id (no atomics); positions: sum over batch
+            srt = torch.sort(ids.reshape(-1))
+            C().embed_word_grad(srt.values, srt.indices, de, layer.word.grad)
+            C().embed_pos_grad(de, layer.pos.grad, T_ // S, S)
             nt = c.type_vocab_size
             if nt <= 2:
                 P_ = C().embed_partial_rows(T_)
                 wsT = torch.empty((P_, nt, H), dtype=torch.float32, device=e.device)
-                C().embed_bwd(ids.reshape(-1), None if types is None else types.reshape(-1), de, layer.word.grad,
-                              layer.pos.grad, wsT, nt, S)
+                C().embed_bwd(ids.reshape(-1), None if types is None else types.reshape(-1), de, None, None, wsT, nt,
+                              S)
                 C().colsum_partials(wsT.view(P_, nt * H), P_, nt * H, layer.type.grad.view(-1), True)
             else:
-                C().embed_bwd(ids.reshape(-1), None, de, layer.word.grad, layer.pos.grad, None, 1, S)
                 tt = types.reshape(-1) if types is not None else torch.zeros(T_, dtype=torch.long, device=e.device)
                 layer.type.grad.index_add_(0, tt, de.float())
         else:
@@ -313,30 +333,39 @@ class _BertLayerFn(torch.autograd.Function):
         dev = h.device
         dout = dout.contiguous()
         P_ = C().ln_partial_rows(T_)
-        ws = torch.empty((P_, 2, H), dtype=torch.float32, device=dev)
-        red = torch.empty(2 * H, dtype=torch.float32, device=dev)
+        ws = torch.empty((P_, 3, H), dtype=torch.float32, device=dev)
+        red = torch.empty(3 * H, dtype=torch.float32, device=dev)
 
-        def ln_back(dy, x, m, r, g_param, b_param, dseed):
+        def ln_back(dy, x, m, r, g_param, b_param, dseed, bias_param):
+            """LN backward; the same sweep emits the dropout-masked gradient of the residual
+            branch and its column sums (= the branch GEMM's bias gradient).  Partial rows are
+            [dbias | dgamma | dbeta], the arena order of (bias, gamma, beta), so one column-sum
+            launch accumulates straight into the gradient arena."""
             dx = torch.empty_like(x)
             dxd = torch.empty_like(x) if p_h > 0 else None
-            C().layernorm_bwd(dy, x, m, r, g_param.master, dx, dxd, p_h, dseed, ws)
-            C().colsum_partials(ws.view(-1, 2 * H), P_, 2 * H, red, False)
-            g_param.grad.add_(red[:H])
-            b_param.grad.add_(red[H:])
+            C().layernorm_bwd(dy, x, m, r, g_param.master, dx, dxd, p_h, dseed, ws, 0.0, 0, 3)
+            if _contiguous(bias_param.grad, g_param.grad, b_param.grad):
+                span = bias_param.grad.as_strided((3 * H,), (1,))  # [bias | gamma | beta] of the arena
+                C().colsum_partials(ws.view(-1, 3 * H), P_, 3 * H, span, True)
+            else:
+                C().colsum_partials(ws.view(-1, 3 * H), P_, 3 * H, red, False)
+                bias_param.grad.add_(red[:H])
+                g_param.grad.add_(red[H : 2 * H])
+                b_param.grad.add_(red[2 * H :])
             return dx, (dxd if dxd is not None else dx)
 
         # ---- FFN block
-        ds2, ds2d = ln_back(dout, s2, m2, r2, L.ln2_g, L.ln2_b, seeds[2])
+        ds2, ds2d = ln_back(dout, s2, m2, r2, L.ln2_g, L.ln2_b, seeds[2], L.out_b)
         _wgrad(ds2d, f, L.out_w.grad)
-        _bias_grad(ds2d, L.out_b.grad)
-        dpre = G.linear_dgrad(ds2d, L.out_w.data, gelu_pre=pre)  # d(pre) = (ds2d W2) * gelu'(pre)
+        st = torch.zeros((32, 2, c.intermediate_size), dtype=torch.float32, device=dev)
+        # d(pre) = (ds2d W2) * gelu'(pre); its column sums (bias grad of W1) come from the epilogue statistics
+        dpre = G.linear_dgrad(ds2d, L.out_w.data, gelu_pre=pre, stats=st)
         _wgrad(dpre, a, L.i_w.grad)
-        _bias_grad(dpre, L.i_b.grad)
+        C().colsum_partials(st.view(32, -1), 32, c.intermediate_size, L.i_b.grad, True, 2 * c.intermediate_size)
         da = G.linear_dgrad(dpre, L.i_w.data, resid=ds2)  # + residual gradient
         # ---- attention block
-        ds1, ds1d = ln_back(da, s1, m1, r1, L.ln1_g, L.ln1_b, seeds[1])
+        ds1, ds1d = ln_back(da, s1, m1, r1, L.ln1_g, L.ln1_b, seeds[1], L.o_b)
         _wgrad(ds1d, ctxo, L.o_w.grad)
-        _bias_grad(ds1d, L.o_b.grad)
         dctx = G.linear_dgrad(ds1d, L.o_w.data)
         dqkv = torch.empty_like(qkv)
         dvec = torch.empty((B, NH, S), dtype=torch.float32, device=dev)
@@ -414,10 +443,7 @@ class _MLMHeadFn(torch.autograd.Function):
         P_ = C().ln_partial_rows(M)
         ws = torch.empty((P_, 2, H), dtype=torch.float32, device=hm.device)
         C().layernorm_bwd(dt2, t, mt, rt, head.ln_g.master, dt, None, 0.0, 0, ws)
-        red = torch.empty(2 * H, dtype=torch.float32, device=hm.device)
-        C().colsum_partials(ws.view(-1, 2 * H), P_, 2 * H, red, False)
-        head.ln_g.grad.add_(red[:H])
-        head.ln_b.grad.add_(red[H:])
+        _ln_param_grads(ws, H, head.ln_g, head.ln_b)
         # t = gelu(pre): d(pre) = dt * gelu'(pre) — GEMM-free here, one fused elementwise via the dgrad epilogue
         # of the transform is not available (t is produced by the GELU epilogue), so apply it on the host side:
         dpre = (dt.float() * _gelu_grad(pre.float())).to(torch.bfloat16)

@@ -112,15 +112,17 @@ def linear_fwd(x2, w, bias=None, relu=False, out=None, resid=None, stats=None, a
                 drop_seed=drop_seed)
 
 
-def linear_dgrad(dy, w, out=None, resid=None, gelu_pre=None):
-    """dx[M,K] = dy[M,N] @ w[N,K] (* gelu'(gelu_pre)) (+resid) -> bf16 (w read row-contiguous)."""
+def linear_dgrad(dy, w, out=None, resid=None, gelu_pre=None, stats=None):
+    """dx[M,K] = dy[M,N] @ w[N,K] (* gelu'(gelu_pre)) (+resid) -> bf16 (w read row-contiguous).
+
+    ``stats`` ([32, 2, K] fp32, zeroed): per-column sums / sums of squares of the output."""
     M, N = dy.shape
     K = w.shape[1]
     if out is None:
         out = torch.empty((M, K), dtype=torch.bfloat16, device=dy.device)
     return gemm(dy, w, out, M, K, N, KC, RC, dy.stride(0), w.stride(0), out.stride(0), EPI_BF16, resid=resid,
                 ldr=(resid.stride(0) if resid is not None else 0),
-                relu=(ACT_GELU_BWD if gelu_pre is not None else ACT_NONE), aux=gelu_pre)
+                relu=(ACT_GELU_BWD if gelu_pre is not None else ACT_NONE), aux=gelu_pre, stats=stats)
 
 
 def linear_wgrad(dy, x2, gw):

@@ -55,6 +55,26 @@ def dropout_ref(x: torch.Tensor, p: float, seed: int) -> torch.Tensor:
 
 
 # ============================================================================ attention
+def mix32_ref(x: torch.Tensor) -> torch.Tensor:
+    """``mix32`` of csrc/kernels/attention.hip on int64 tensors holding uint32 values."""
+    m = 0xFFFFFFFF
+    x = x & m
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & m
+    x = x ^ (x >> 15)
+    x = (x * 0x846CA68B) & m
+    return x ^ (x >> 16)
+
+
+def attn_keep_ref(seed: int, row: torch.Tensor, j: torch.Tensor, p: float) -> torch.Tensor:
+    """Attention-probability dropout mask: keep iff mix32(row_key(row) + j) >= p * 2^32, with
+    row_key = mix32(seed_lo ^ mix32(row + seed_hi)) and row = (b*H + h)*S + i."""
+    s = seed & 0xFFFFFFFFFFFFFFFF
+    lo, hi = s & 0xFFFFFFFF, s >> 32
+    rk = mix32_ref(lo ^ mix32_ref(row.to(torch.int64) + hi))
+    return mix32_ref(rk + j.to(torch.int64)) >= drop_thresh(p)
+
+
 def attention_ref(qkv, B, S, H, q_off, k_off, v_off, lens=None, scale=0.125, drop_p=0.0, seed=0):
     """fp32 reference: qkv [B*S, W] -> context [B*S, H*64]."""
     x = qkv.float().view(B, S, -1)
@@ -74,8 +94,8 @@ def attention_ref(qkv, B, S, H, q_off, k_off, v_off, lens=None, scale=0.125, dro
         bh = torch.arange(B * H, device=qkv.device).view(B, H, 1, 1)
         i = torch.arange(S, device=qkv.device).view(1, 1, S, 1)
         j = torch.arange(S, device=qkv.device).view(1, 1, 1, S)
-        idx = (bh * S + i) * S + j
-        p = torch.where(keep_mask_ref(seed, idx, drop_p), p / (1.0 - drop_p), torch.zeros((), device=p.device))
+        keep = attn_keep_ref(seed, bh * S + i, j, drop_p)
+        p = torch.where(keep, p / (1.0 - drop_p), torch.zeros((), device=p.device))
     o = torch.einsum("bhij,bhjd->bhid", p, v)
     return o.permute(0, 2, 1, 3).reshape(B * S, H * 64)
 

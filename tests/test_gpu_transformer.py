@@ -214,3 +214,24 @@ def test_bert_base_layer_shapes_run():
                                                   "num_masked": B * Pm})
     assert math.isfinite(loss) and abs(loss - math.log(cfg.vocab_size)) < 1.5, loss
     assert torch.isfinite(m.arena.master).all()
+
+
+def test_embed_word_grad_sorted_runs_and_pos_grad():
+    """Sorted-run word gradient (plain writes inside a chunk, atomics across chunk edges) with a
+    very frequent id, and the batch-sum position gradient."""
+    from distributeddeeplearningspark_amd.ops._native import C
+
+    V, H, B, S = 500, 768, 4, 256
+    g = torch.Generator().manual_seed(3)
+    ids = torch.randint(0, V, (B * S,), generator=g)
+    ids[torch.rand(B * S, generator=g) < 0.4] = 103  # [MASK]-like hot id: runs span many chunks
+    ids = ids.to(DEV)
+    ds = rnd(B * S, H, seed=21)
+    gw = torch.full((V, H), 0.5, device=DEV)
+    srt = torch.sort(ids)
+    C().embed_word_grad(srt.values, srt.indices, ds, gw)
+    ref = torch.full((V, H), 0.5, device=DEV).index_add_(0, ids, ds.float())
+    close(gw, ref, rtol=1e-3, atol=1e-3, what="sorted word grad")
+    gp = torch.zeros(S, H, device=DEV)
+    C().embed_pos_grad(ds, gp, B, S)
+    close(gp, ds.float().view(B, S, H).sum(0), rtol=1e-3, atol=1e-3, what="pos grad")
