@@ -57,6 +57,8 @@ int add_bf16(const void* a, const void* b, void* y, long n, hipStream_t s);
 int bias_grad(const void* dy, float* db, long M, int N, int accumulate, hipStream_t s);  // db[n] (+)= sum_m dy[m][n]
 int im2col(const void* x, void* col, int n, int hi, int wi, int c, int ho, int wo, int sh, int sw, int ntaps,
            const int* dh, const int* dw, int kpad, hipStream_t s);
+// stem space-to-depth: [N][H][W][C<=4] -> [N][Ho][Wo][16] (block 2, zero padding `pad`)
+int s2d_pad(const void* x, void* y, int N, int H, int W, int C, int Ho, int Wo, int pad, hipStream_t s);
 // ingest: uint8 NHWC images -> bf16 normalised, channel-padded NHWC (cpad >= c)
 int normalize_u8(const uint8_t* x, void* y, long npix, int c, int cpad, const float* mean, const float* invstd,
                  hipStream_t s);

@@ -95,7 +95,13 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
 __device__ __forceinline__ uint32_t row_key(unsigned long long seed, int bh, int S, int i) {
   return mix32((uint32_t)seed ^ mix32((uint32_t)(bh * S + i) + (uint32_t)(seed >> 32)));
 }
-__device__ __forceinline__ bool keep_elem(uint32_t rk, int j, uint32_t thresh) { return mix32(rk + (uint32_t)j) >= thresh; }
+// one 32-bit mix serves two neighbouring keys: key j uses the low (j even) / high (j odd) 16 bits
+// of mix32(rk + j/2), compared against th16 = thresh >> 16
+__device__ __forceinline__ uint32_t pair_hash(uint32_t rk, int j) { return mix32(rk + ((uint32_t)j >> 1)); }
+__device__ __forceinline__ bool keep_bits(uint32_t h, int j, uint32_t th16) {
+  return ((j & 1) ? (h >> 16) : (h & 0xffffu)) >= th16;
+}
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 // ================================================================ forward
 __global__ __launch_bounds__(THREADS, 2) void attn_fwd_kernel(const AttnParams p) {
@@ -156,45 +162,54 @@ __global__ __launch_bounds__(THREADS, 2) void attn_fwd_kernel(const AttnParams p
       }
     }
     const int kb = t * TQ;
+    const bool full = kb + TQ <= len;  // tile fully inside the valid keys (wave-uniform)
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
       float mx = -INFINITY;
+      if (!full) {
+#pragma unroll
+        for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (kb + 16 * jt + 4 * g + e >= len) s[jt][it][e] = -INFINITY;
+      }
 #pragma unroll
       for (int jt = 0; jt < 4; ++jt)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int j = kb + 16 * jt + 4 * g + e;
-          const float v = (j < len) ? s[jt][it][e] * p.scale_log2 : -INFINITY;
-          s[jt][it][e] = v;
-          mx = fmaxf(mx, v);
-        }
+        for (int e = 0; e < 4; ++e) mx = fmaxf(mx, s[jt][it][e]);
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mn = fmaxf(m[it], mx);  // finite: key kb < len is valid
-      const float alpha = exp2f(m[it] - mn);
+      const float mn = fmaxf(m[it], mx * p.scale_log2);  // running max of the scaled (log2) scores
+      const float alpha = fexp2(m[it] - mn);
       m[it] = mn;
       float rs = 0.f;
 #pragma unroll
       for (int jt = 0; jt < 4; ++jt)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float pv = exp2f(s[jt][it][e] - mn);
+          const float pv = fexp2(fmaf(s[jt][it][e], p.scale_log2, -mn));
           s[jt][it][e] = pv;
           rs += pv;
         }
       l[it] = l[it] * alpha + rs;
+      if (!__all(alpha == 1.f)) {  // the running max moved for some query of the wave
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) o[dt][it] *= alpha;
+        for (int dt = 0; dt < 4; ++dt) o[dt][it] *= alpha;
+      }
     }
     if (p.drop_thresh) {
+      const uint32_t th16 = p.drop_thresh >> 16;
 #pragma unroll
       for (int it = 0; it < 2; ++it)
 #pragma unroll
         for (int jt = 0; jt < 4; ++jt)
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            s[jt][it][e] = keep_elem(rk[it], kb + 16 * jt + 4 * g + e, p.drop_thresh) ? s[jt][it][e] * p.drop_scale
-                                                                                    : 0.f;
+          for (int e = 0; e < 4; e += 2) {
+            const int j = kb + 16 * jt + 4 * g + e;
+            const uint32_t h = pair_hash(rk[it], j);
+            s[jt][it][e] = keep_bits(h, j, th16) ? s[jt][it][e] * p.drop_scale : 0.f;
+            s[jt][it][e + 1] = keep_bits(h, j + 1, th16) ? s[jt][it][e + 1] * p.drop_scale : 0.f;
+          }
     }
     // O^T[d][i] += sum_j V^T[d][j] P^T[j][i]
 #pragma unroll
@@ -265,6 +280,7 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const AttnParams p, l
 __global__ __launch_bounds__(THREADS, 1) void attn_bwd_dkdv_kernel(const AttnParams p) {
   __shared__ __attribute__((aligned(16))) char lds[2][2][TILE_BYTES];  // [buf][Q, dO]
   __shared__ float s_lse[2][TQ], s_d[2][TQ];
+  __shared__ uint32_t s_rk[2][TQ];
   const int h = blockIdx.y, b = blockIdx.z, S = p.S;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
   const long tok0 = (long)b * S;
@@ -300,6 +316,7 @@ __global__ __launch_bounds__(THREADS, 1) void attn_bwd_dkdv_kernel(const AttnPar
   const int nqt = any_key ? S / TQ : 0;
   TileStage sq, sd;
   float r_lse = 0.f, r_d = 0.f;
+  uint32_t r_rk = 0u;
   if (nqt > 0) {
     sq.load(Q, p.ld, 0, S);
     sd.load(dO, p.lddo, 0, S);
@@ -308,6 +325,7 @@ __global__ __launch_bounds__(THREADS, 1) void attn_bwd_dkdv_kernel(const AttnPar
     if (threadIdx.x < TQ) {
       s_lse[0][threadIdx.x] = lse[threadIdx.x];
       s_d[0][threadIdx.x] = dv[threadIdx.x];
+      s_rk[0][threadIdx.x] = row_key(p.drop_seed, bh, S, threadIdx.x);
     }
   }
   __syncthreads();
@@ -322,6 +340,7 @@ __global__ __launch_bounds__(THREADS, 1) void attn_bwd_dkdv_kernel(const AttnPar
       if (threadIdx.x < TQ) {
         r_lse = lse[(t + 1) * TQ + threadIdx.x];
         r_d = dv[(t + 1) * TQ + threadIdx.x];
+        r_rk = row_key(p.drop_seed, bh, S, (t + 1) * TQ + threadIdx.x);
       }
     }
     const int qb = t * TQ;
@@ -341,19 +360,22 @@ __global__ __launch_bounds__(THREADS, 1) void attn_bwd_dkdv_kernel(const AttnPar
       }
     }
     // P, dS (P kept in s[], dropout-scaled P in pd via s after dS is formed)
+    const bool kfull = k0 + 32 <= len;  // this wave's 32 keys all valid (wave-uniform)
+    const uint32_t th16 = p.drop_thresh >> 16;
 #pragma unroll
     for (int it = 0; it < 4; ++it)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int il = 16 * it + 4 * g + e;
         const float lq = s_lse[buf][il], dq = s_d[buf][il];
-        const uint32_t rki = p.drop_thresh ? row_key(p.drop_seed, bh, S, qb + il) : 0u;
+        const uint32_t rki = s_rk[buf][il];
 #pragma unroll
         for (int jt = 0; jt < 2; ++jt) {
           const int j = k0 + 16 * jt + li;
-          float pv = (j < len) ? exp2f(s[it][jt][e] * p.scale_log2 - lq) : 0.f;
+          float pv = fexp2(fmaf(s[it][jt][e], p.scale_log2, -lq));
+          if (!kfull && j >= len) pv = 0.f;
           float keep = 1.f;
-          if (p.drop_thresh) keep = keep_elem(rki, j, p.drop_thresh) ? p.drop_scale : 0.f;
+          if (p.drop_thresh) keep = keep_bits(pair_hash(rki, j), j, th16) ? p.drop_scale : 0.f;
           dp[it][jt][e] = pv * (dp[it][jt][e] * keep - dq);  // dS
           s[it][jt][e] = pv * keep;                          // dropped P (for dV)
         }
@@ -384,6 +406,7 @@ __global__ __launch_bounds__(THREADS, 1) void attn_bwd_dkdv_kernel(const AttnPar
       if (threadIdx.x < TQ) {
         s_lse[buf ^ 1][threadIdx.x] = r_lse;
         s_d[buf ^ 1][threadIdx.x] = r_d;
+        s_rk[buf ^ 1][threadIdx.x] = r_rk;
       }
     }
     __syncthreads();
@@ -470,17 +493,29 @@ __global__ __launch_bounds__(THREADS, 2) void attn_bwd_dq_kernel(const AttnParam
         dp[jt][it] = mfma16x16x32(v1f, df[it][1], c);
       }
     }
+    const bool full = kb + TQ <= len;
+    const uint32_t th16 = p.drop_thresh >> 16;
 #pragma unroll
     for (int jt = 0; jt < 4; ++jt)
 #pragma unroll
       for (int it = 0; it < 2; ++it)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
+        for (int e = 0; e < 4; e += 2) {
           const int j = kb + 16 * jt + 4 * g + e;
-          const float pv = (j < len) ? exp2f(s[jt][it][e] * p.scale_log2 - lq[it]) : 0.f;
-          float keep = 1.f;
-          if (p.drop_thresh) keep = keep_elem(rk[it], j, p.drop_thresh) ? p.drop_scale : 0.f;
-          s[jt][it][e] = pv * (dp[jt][it][e] * keep - dq[it]);  // dS^T
+          float p0 = fexp2(fmaf(s[jt][it][e], p.scale_log2, -lq[it]));
+          float p1 = fexp2(fmaf(s[jt][it][e + 1], p.scale_log2, -lq[it]));
+          if (!full) {
+            if (j >= len) p0 = 0.f;
+            if (j + 1 >= len) p1 = 0.f;
+          }
+          float k0v = 1.f, k1v = 1.f;
+          if (p.drop_thresh) {
+            const uint32_t h = pair_hash(rk[it], j);
+            k0v = keep_bits(h, j, th16) ? p.drop_scale : 0.f;
+            k1v = keep_bits(h, j + 1, th16) ? p.drop_scale : 0.f;
+          }
+          s[jt][it][e] = p0 * (dp[jt][it][e] * k0v - dq[it]);  // dS^T
+          s[jt][it][e + 1] = p1 * (dp[jt][it][e + 1] * k1v - dq[it]);
         }
     // dQ[i][d] += sum_j dS[i][j] K[j][d]
 #pragma unroll

@@ -137,4 +137,41 @@ int normalize_u8(const uint8_t* x, void* y, long npix, int c, int cpad, const fl
   return (int)hipGetLastError();
 }
 
+// Space-to-depth (block 2) with zero padding for the ResNet stem: x [N][H][W][C] (C <= 4) ->
+// y [N][Ho][Wo][16], y[n][I][J][(2a + b) * C + ch] = x[n][2I + a - pad][2J + b - pad][ch] (0 outside),
+// channels 4C..15 zero.  A 7x7 stride-2 conv on x equals a 4x4 stride-1 conv on y, with 12 of 16
+// channels used instead of 3 of 8 after the 16-B channel padding (see ops/conv.py stem path).
+__global__ void s2d_pad_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int N, int H, int W, int C,
+                               int Ho, int Wo, int pad) {
+  const long pix = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (pix >= (long)N * Ho * Wo) return;
+  const int J = (int)(pix % Wo);
+  const long t = pix / Wo;
+  const int I = (int)(t % Ho);
+  const int n = (int)(t / Ho);
+  uint16_t v[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = 0;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int r = 2 * I + a - pad, c = 2 * J + b - pad;
+      if ((unsigned)r < (unsigned)H && (unsigned)c < (unsigned)W) {
+        const bf16_t* src = x + (((long)n * H + r) * W + c) * C;
+        for (int ch = 0; ch < C; ++ch) v[(2 * a + b) * C + ch] = src[ch];
+      }
+    }
+  uint4* dst = reinterpret_cast<uint4*>(y + pix * 16);
+  dst[0] = make_uint4(v[0] | (v[1] << 16), v[2] | (v[3] << 16), v[4] | (v[5] << 16), v[6] | (v[7] << 16));
+  dst[1] = make_uint4(v[8] | (v[9] << 16), v[10] | (v[11] << 16), v[12] | (v[13] << 16), v[14] | (v[15] << 16));
+}
+
+int s2d_pad(const void* x, void* y, int N, int H, int W, int C, int Ho, int Wo, int pad, hipStream_t s) {
+  const long n = (long)N * Ho * Wo;
+  hipLaunchKernelGGL(s2d_pad_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                     reinterpret_cast<const bf16_t*>(x), reinterpret_cast<bf16_t*>(y), N, H, W, C, Ho, Wo, pad);
+  return (int)hipGetLastError();
+}
+
 }  // namespace ddl

@@ -216,6 +216,15 @@ void im2col_(const at::Tensor& x, const at::Tensor& col, int64_t ho, int64_t wo,
   HIP_OK(im2col(x.data_ptr(), col.data_ptr(), N, x.size(1), x.size(2), x.size(3), ho, wo, sh, sw, (int)dh.size(),
                 dh.data(), dw.data(), (int)kpad, cur_stream()));
 }
+void s2d_pad_(const at::Tensor& x, const at::Tensor& y, int64_t pad) {
+  GPU(x); BF16(x); BF16(y);
+  CK(x.dim() == 4 && x.size(3) <= 4 && y.dim() == 4 && y.size(3) == 16 && y.size(0) == x.size(0), "s2d_pad: shapes");
+  CK(2 * y.size(1) >= x.size(1) + 2 * pad && 2 * y.size(2) >= x.size(2) + 2 * pad, "s2d_pad: output too small");
+  at::DeviceGuard g(x.device());
+  HIP_OK(s2d_pad(x.data_ptr(), y.data_ptr(), (int)x.size(0), (int)x.size(1), (int)x.size(2), (int)x.size(3),
+                 (int)y.size(1), (int)y.size(2), (int)pad, cur_stream()));
+}
+
 void normalize_u8_(const at::Tensor& x, const at::Tensor& y, const at::Tensor& mean, const at::Tensor& invstd,
                    int64_t C, int64_t CP) {
   GPU(x);
@@ -304,6 +313,7 @@ void register_ops(py::module& m) {
   m.def("bias_grad", &bias_grad_);
   m.def("im2col", &im2col_);
   m.def("normalize_u8", &normalize_u8_);
+  m.def("s2d_pad", &s2d_pad_);
   m.def("sgd_step", &sgd_step_);
   m.def("adam_step", &adam_step_);
   m.def("adagrad_step", &adagrad_step_);

@@ -131,7 +131,73 @@ def bottleneck(block, x, anchor):
 
 def convbn_relu(unit, x, anchor, relu=True):
     """Single fused conv+BN(+ReLU) unit as one autograd node (the ResNet stem)."""
+    if not x.requires_grad and _stem_s2d_ok(unit.conv, x.shape[-1]):
+        return _StemS2DFn.apply(x, anchor, unit, relu)
     return _ConvBNFn.apply(x, anchor, unit, relu)
+
+
+def _stem_s2d_ok(conv, Ci) -> bool:
+    """7x7 / stride 2 / pad 3 stem on <= 4 channels: run as a 4x4 stride-1 conv after a
+    block-2 space-to-depth (12 of 16 channels used instead of 3 of 8, K = 256 instead of 392)."""
+    import os
+
+    return (os.environ.get("DDL_STEM_S2D", "1") != "0" and Ci <= 4 and tuple(conv.kernel_size) == (7, 7)
+            and tuple(conv.strides) == (2, 2) and tuple(conv.dilation_rate) == (1, 1)
+            and (conv.padding == (3, 3) or conv.padding == 3 or conv.padding == "same"))
+
+
+def _s2d_weight(w):
+    """[Co, 7, 7, C] -> [Co, 4, 4, 16]: W'[A][B][(2a+b)C + ch] = W[2A+a][2B+b][ch] (zero past 7)."""
+    Co, _, _, Cc = w.shape
+    w8 = torch.nn.functional.pad(w, (0, 0, 0, 1, 0, 1))  # [Co, 8, 8, C]
+    w4 = w8.view(Co, 4, 2, 4, 2, Cc).permute(0, 1, 3, 2, 4, 5).reshape(Co, 4, 4, 4 * Cc)
+    return torch.nn.functional.pad(w4, (0, 16 - 4 * Cc)).contiguous()
+
+
+def _s2d_weight_grad(g4, Cc):
+    """Inverse of _s2d_weight for gradients: [Co, 4, 4, 16] -> [Co, 7, 7, C]."""
+    Co = g4.shape[0]
+    g = g4[..., : 4 * Cc].reshape(Co, 4, 4, 2, 2, Cc).permute(0, 1, 3, 2, 4, 5).reshape(Co, 8, 8, Cc)
+    return g[:, :7, :7, :]
+
+
+class _StemS2DFn(torch.autograd.Function):
+    """ResNet stem conv (7x7 s2 p3, 3 channels) + BN (+ReLU) through space-to-depth."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, unit, relu):
+        x = x.contiguous()
+        N, H, W, Cc = x.shape
+        conv = unit.conv
+        Ho, Wo = (H + 6 + 1) // 2, (W + 6 + 1) // 2
+        xs = torch.empty((N, Ho, Wo, 16), dtype=x.dtype, device=x.device)
+        C().s2d_pad(x, xs, 3)
+        w4 = _s2d_weight(conv.kernel.data.detach())
+        g = CV.geometry(N, Ho, Wo, 16, conv.filters, 4, 4, (1, 1), (0, 0), (1, 1))
+        stats = new_stats_workspace(conv.filters, x.device)
+        yc = CV.conv_fwd_native(xs, w4, g, stats=stats)
+        st = _ConvBNState()
+        st.g, st.yc = g, yc
+        st.y, st.mean, st.invstd, st.scale, st.shift = _bn_forward(unit.bn, yc, stats, None, relu, True)
+        st.mode = 2 if relu else 0
+        ctx.unit, ctx.st, ctx.cc = unit, st, Cc
+        ctx.save_for_backward(xs)
+        return st.y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (xs,) = ctx.saved_tensors
+        unit, st = ctx.unit, ctx.st
+        dyc, _ = bn_backward(unit, st, dy.contiguous(), False)
+        conv = unit.conv
+        g = st.g
+        tmp = torch.zeros((g.Co, 4, 4, 16), dtype=torch.float32, device=dy.device)
+        CV.conv_wgrad_native(dyc, xs, g, tmp)
+        conv.kernel.grad.add_(_s2d_weight_grad(tmp, ctx.cc))
+        if conv.grad_hook is not None:
+            conv.grad_hook()
+        ctx.st = None
+        return None, None, None, None  # the stem input is data: no gradient
 
 
 class _ConvBNFn(torch.autograd.Function):

@@ -67,12 +67,17 @@ def mix32_ref(x: torch.Tensor) -> torch.Tensor:
 
 
 def attn_keep_ref(seed: int, row: torch.Tensor, j: torch.Tensor, p: float) -> torch.Tensor:
-    """Attention-probability dropout mask: keep iff mix32(row_key(row) + j) >= p * 2^32, with
-    row_key = mix32(seed_lo ^ mix32(row + seed_hi)) and row = (b*H + h)*S + i."""
+    """Attention-probability dropout mask.  One 32-bit hash h = mix32(row_key(row) + j // 2)
+    serves a pair of keys: key j keeps iff its 16-bit half (low for even j, high for odd j)
+    is >= floor(p * 2^32) >> 16, with row_key = mix32(seed_lo ^ mix32(row + seed_hi)) and
+    row = (b*H + h)*S + i."""
     s = seed & 0xFFFFFFFFFFFFFFFF
     lo, hi = s & 0xFFFFFFFF, s >> 32
     rk = mix32_ref(lo ^ mix32_ref(row.to(torch.int64) + hi))
-    return mix32_ref(rk + j.to(torch.int64)) >= drop_thresh(p)
+    j = j.to(torch.int64)
+    h = mix32_ref(rk + (j >> 1))
+    bits = torch.where((j & 1) == 1, h >> 16, h & 0xFFFF)
+    return bits >= (drop_thresh(p) >> 16)
 
 
 def attention_ref(qkv, B, S, H, q_off, k_off, v_off, lens=None, scale=0.125, drop_p=0.0, seed=0):

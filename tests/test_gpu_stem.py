@@ -1,0 +1,34 @@
+"""Space-to-depth ResNet stem (7x7 s2 conv as a 4x4 s1 conv on a block-2 s2d input) vs the
+channel-padded implicit-GEMM stem: same forward and the same parameter gradients."""
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(s2d):
+    from distributeddeeplearningspark_amd.models.resnet import ResNet
+
+    os.environ["DDL_STEM_S2D"] = "1" if s2d else "0"
+    try:
+        torch.manual_seed(0)
+        x = torch.randn(8, 96, 96, 3)
+        y = torch.randint(0, 10, (8,))
+        m = ResNet(blocks=(1,), input_shape=(96, 96, 3), num_classes=10)
+        m.compile("sgd", "sparse_categorical_crossentropy")
+        m.place("cuda", seed=1)
+        loss = float(m.backward_step(m.to_input(x), m.to_target(y)))
+        stem = m.stem.conv.kernel.grad.detach().clone()
+        return loss, stem, m.arena.grad.detach().clone()
+    finally:
+        os.environ.pop("DDL_STEM_S2D", None)
+
+
+def test_stem_s2d_matches_padded_path():
+    l1, s1, g1 = _run(True)
+    l0, s0, g0 = _run(False)
+    assert abs(l1 - l0) < 1e-2 * max(1.0, abs(l0)), (l1, l0)
+    assert ((s1 - s0).norm() / s0.norm()).item() < 3e-2
+    assert ((g1 - g0).norm() / g0.norm()).item() < 3e-2
