@@ -69,7 +69,15 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
   if (b_mode == OP_RC || b_mode == OP_RC_TAPS) TORCH_CHECK(ldb % 8 == 0, "gemm: ldb must be a multiple of 8");
   TORCH_CHECK(((uintptr_t)a.data_ptr() % 16) == 0 && ((uintptr_t)b.data_ptr() % 16) == 0, "gemm: operands must be 16-B aligned");
   TORCH_CHECK(k_split > 0 && k_split % 64 == 0, "gemm: k_split must be a positive multiple of 64");
-  TORCH_CHECK(tile >= 0 && tile <= kTile256, "gemm: bad tile id");
+  TORCH_CHECK(tile >= 0 && tile <= kTileStream, "gemm: bad tile id");
+  if (tile == kTileStream) {
+    TORCH_CHECK(a_mode == OP_KC && (b_mode == OP_KC || b_mode == OP_RC) && epi == EPI_BF16 && !outmap.has_value() &&
+                    relu <= ACT_RELU && drop_p == 0.0 && beta == 0.0 && k_split >= K,
+                "gemm stream: KC x (KC|RC) operands, bf16 epilogue without GELU/dropout/outmap/beta/split-K");
+    TORCH_CHECK(gemm_stream_panel((int)N, (int)K) > 0, "gemm stream: unsupported (N, K) = (", N, ", ", K, ")");
+    TORCH_CHECK(ldc % 8 == 0 && ((uintptr_t)c.data_ptr() % 16) == 0, "gemm stream: 16-B aligned output rows");
+    TORCH_CHECK(!resid || (ldr % 4 == 0 && ((uintptr_t)resid->data_ptr() % 8) == 0), "gemm stream: resid alignment");
+  }
   if (tile == kTile256) {
     TORCH_CHECK(a_mode <= OP_RC && b_mode <= OP_RC && !outmap.has_value(), "gemm256: plain KC/RC operands only");
     TORCH_CHECK(K % 64 == 0 && k_split % 64 == 0, "gemm256: K and k_split must be multiples of 64");

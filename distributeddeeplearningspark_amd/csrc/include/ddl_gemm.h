@@ -84,7 +84,11 @@ struct GemmParams {
 enum Activation : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_GELU_BWD = 3 };
 
 constexpr int kStatShards = 32;
-constexpr int kTile256 = 4;  // tile id of the 256x256 ping-pong kernel (ddl_gemm256.h)
+constexpr int kTile256 = 4;     // tile id of the 256x256 ping-pong kernel (ddl_gemm256.h)
+constexpr int kTileStream = 5;  // tile id of the weight-stationary streaming kernel (gemm_stream.hip)
+
+// panel width of the streaming kernel for (N, K), 0 when it does not apply
+int gemm_stream_panel(int N, int K);
 
 // host launcher (defined in gemm_bf16.hip); returns hipError_t as int
 int launch_gemm_bf16(const GemmParams& p, int epi, int tile, void* stream);

@@ -19,7 +19,8 @@ from ._native import C
 KC, RC, KC_GATHER, RC_GATHER, RC_TAPS, KC_GATHER8, RC_GATHER8 = 0, 1, 2, 3, 4, 5, 6
 EPI_BF16, EPI_F32, EPI_F32_ATOMIC = 0, 1, 2
 TILE256 = 4  # 256x256 ping-pong kernel (csrc/include/ddl_gemm256.h): plain KC/RC operands, K % 64 == 0
-_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), TILE256: (256, 256)}
+TILE_STREAM = 5  # weight-stationary streaming kernel (csrc/kernels/gemm_stream.hip): K in {64, 128, 256}
+_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), TILE256: (256, 256), TILE_STREAM: (64, 256)}
 _CU = 256
 import os as _os
 
@@ -28,6 +29,35 @@ import os as _os
 # shapes (K <= 3072 with <= 2.25 workgroup rounds), so it is opt-in (DDL_GEMM256=1) and
 # auto-selected only for GEMMs with many tiles AND a long K loop.
 _USE256 = _os.environ.get("DDL_GEMM256", "auto")
+
+
+_USE_STREAM = _os.environ.get("DDL_GEMM_STREAM", "1")
+
+
+def stream_panel(N: int, K: int) -> int:
+    """Panel width of the streaming kernel for (N, K) (mirror of ``gemm_stream_panel``), 0 if n/a."""
+    if K not in (64, 128, 256):
+        return 0
+    max_nb = 128 if K == 256 else 256
+    nb = max_nb
+    while nb >= 64:
+        if N % nb == 0 and (N == nb or nb == max_nb):
+            return nb
+        nb //= 2
+    return 0
+
+
+def use_stream(M, N, K, a_mode, b_mode, epi, lda, ldc, *, outmap=None, aux=None, drop_p=0.0, relu=0, beta=0.0,
+               resid=None, ldr=0) -> bool:
+    """Skinny-K streaming kernel: ResNet 1x1 convolutions and their data-gradients at large M
+    (memory-bound; the 128-tile kernel writes 32-B segments and re-stages the weights per tile)."""
+    if _USE_STREAM == "0" or a_mode != KC or b_mode not in (KC, RC) or epi != EPI_BF16:
+        return False
+    if outmap is not None or aux is not None or drop_p or int(relu) > ACT_RELU or beta:
+        return False
+    if M < 16384 or not stream_panel(N, K) or lda % 8 or ldc % 8 or (resid is not None and ldr % 4):
+        return False
+    return True
 
 
 def use_tile256(M: int, N: int, K: int, a_mode: int, b_mode: int, epi: int) -> bool:
@@ -79,7 +109,13 @@ def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, bet
     ``beta == 1`` semantics.
     """
     if tile is None:
-        tile = TILE256 if (outmap is None and use_tile256(M, N, K, a_mode, b_mode, epi)) else choose_tile(M, N, bn_cap)
+        if use_stream(M, N, K, a_mode, b_mode, epi, lda, ldc, outmap=outmap, aux=aux, drop_p=drop_p, relu=relu,
+                      beta=beta, resid=resid, ldr=ldr):
+            tile = TILE_STREAM
+        elif outmap is None and use_tile256(M, N, K, a_mode, b_mode, epi):
+            tile = TILE256
+        else:
+            tile = choose_tile(M, N, bn_cap)
     if k_split is None:
         k_split = choose_split(M, N, K, tile, allow=(epi != EPI_BF16))
     if epi == EPI_F32 and k_split < K:
