@@ -193,12 +193,29 @@ __device__ __forceinline__ void load8f(const float* p, float* f) {
   f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
 }
 
+// ReLU bit mask of a residual BN (bn_apply output, mode-3 backward input).  The 64 lanes of a
+// wave always hold 64 consecutive, 64-aligned vector indices (C a power of two: ColGeom maps
+// lane -> (row, 8-channel vector) in row-major order), so the mask of one wave is 8 ballots:
+// word [idx / 64][i] bit (idx % 64) = element i of vector idx.  Written as 64 B by 8 lanes and
+// read back with scalar loads — byte-per-lane stores cost as much as a 16-B store each.
+__device__ __forceinline__ void store_mask_bits(uint8_t* __restrict__ mask, long idx, uint32_t bits) {
+  const int lane = threadIdx.x & 63;
+  uint64_t w = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint64_t b = __ballot((bits >> i) & 1u);
+    if (lane == i) w = b;
+  }
+  if (lane < 8) reinterpret_cast<uint64_t*>(mask)[(idx >> 6) * 8 + lane] = w;
+}
+
 // Streaming sweeps use the column-fixed mapping of ColGeom: a lane keeps ONE 8-channel
 // vector (per-channel parameters live in registers, no per-element index division) and
 // walks rows; two rows are in flight per lane.
 __global__ __launch_bounds__(256) void bn_apply_kernel(const uint4* __restrict__ x, const float* __restrict__ scale,
                                                         const float* __restrict__ shift, const uint4* __restrict__ res,
-                                                        uint4* __restrict__ y, long M, int C, int relu) {
+                                                        uint4* __restrict__ y, uint8_t* __restrict__ mask, long M,
+                                                        int C, int relu) {
   ColGeom g(C);
   if (!g.active) return;
   float sc[8], sh[8];
@@ -221,14 +238,17 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint4* __restrict__
       if (h == 1 && !two) break;
       unpack8(h ? x1 : x0, f);
       if (res) unpack8(h ? r1 : r0, q);
+      uint32_t bits = 0;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         float o = f[i] * sc[i] + sh[i];
         if (res) o += q[i];
+        bits |= (o > 0.f ? 1u : 0u) << i;
         if (relu) o = fmaxf(o, 0.f);
         f[i] = o;
       }
       y[h ? i1 : i0] = pack8(f);
+      if (mask) store_mask_bits(mask, h ? i1 : i0, bits);
     }
   }
 }
@@ -242,19 +262,27 @@ static dim3 stream_grid(long M, int C) {
   return dim3((unsigned)(gx > 0 ? gx : 1), (unsigned)gy);
 }
 
-int bn_apply(const void* x, const float* scale, const float* shift, const void* resid, void* y, long M, int C, int relu,
-             hipStream_t s) {
+int bn_apply(const void* x, const float* scale, const float* shift, const void* resid, void* y, void* mask, long M,
+             int C, int relu, hipStream_t s) {
   hipLaunchKernelGGL(bn_apply_kernel, stream_grid(M, C), dim3(256), 0, s, (const uint4*)x, scale, shift,
-                     (const uint4*)resid, (uint4*)y, M, C, relu);
+                     (const uint4*)resid, (uint4*)y, (uint8_t*)mask, M, C, relu);
   return (int)hipGetLastError();
 }
 
-// ReLU mask of the backward: mode 1 reads the forward output y (> 0), mode 2 recomputes
+// ReLU mask of the backward: mode 1 reads the forward output y (> 0); mode 2 recomputes
 // x*scale+shift > 0 from the BN input already in registers (no extra tensor read: the
-// forward computed the same fmaf on the same values).
+// forward computed the same fmaf on the same values); mode 3 reads the bit mask the forward
+// apply stored (one byte per 8 channels: 1/16 of the bytes of y) — for BNs with a residual
+// add, whose output cannot be recomputed from x alone.
 __device__ __forceinline__ void relu_mask(float* d, const float* xv, const uint4* __restrict__ y, long idx,
                                           const float* sc, const float* sh, int mode) {
-  if (mode == 1) {
+  if (mode == 3) {
+    const long chunk = __builtin_amdgcn_readfirstlane((int)(idx >> 6));  // wave-uniform: scalar loads
+    const uint64_t* __restrict__ mw = reinterpret_cast<const uint64_t*>(y) + chunk * 8;
+    const int sh6 = (int)(idx & 63);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d[i] = ((mw[i] >> sh6) & 1ull) ? d[i] : 0.f;
+  } else if (mode == 1) {
     float yv[8];
     unpack8(y[idx], yv);
 #pragma unroll

@@ -55,13 +55,18 @@ void bn_finalize_(const at::Tensor& ws, int64_t M, int64_t C, c10::optional<at::
 }
 
 void bn_apply_(const at::Tensor& x, const at::Tensor& scale, const at::Tensor& shift, c10::optional<at::Tensor> resid,
-               const at::Tensor& y, int64_t C, bool relu) {
+               const at::Tensor& y, int64_t C, bool relu, c10::optional<at::Tensor> mask) {
   GPU(x); BF16(x); BF16(y); F32(scale); F32(shift);
   CK(C % 8 == 0 && x.numel() % C == 0 && y.numel() == x.numel(), "bn_apply: shapes");
   if (resid) { BF16(*resid); CK(resid->numel() == x.numel(), "bn_apply: resid shape"); }
+  if (mask) {
+    CK(mask->scalar_type() == at::kByte && mask->is_contiguous() && mask->numel() >= (x.numel() / 8 + 63) / 64 * 64,
+       "bn_apply: mask must be uint8 [ceil(numel / 512) * 64]");
+    CK((C & (C - 1)) == 0, "bn_apply: the bit mask needs a power-of-two channel count");
+  }
   at::DeviceGuard g(x.device());
   HIP_OK(bn_apply(x.data_ptr(), scale.data_ptr<float>(), shift.data_ptr<float>(), optr<const void>(resid), y.data_ptr(),
-                  x.numel() / C, (int)C, relu ? 1 : 0, cur_stream()));
+                  optr<void>(mask), x.numel() / C, (int)C, relu ? 1 : 0, cur_stream()));
 }
 
 // relu mask mode: 0 none; 1 from y (forward output); 2 recomputed from x*scale+shift
@@ -71,6 +76,9 @@ void bn_bwd_reduce_(const at::Tensor& dy, const at::Tensor& x, c10::optional<at:
   GPU(dy); BF16(dy); BF16(x); F32(mean); F32(ws);
   CK(dy.numel() == x.numel() && x.numel() % C == 0 && C % 8 == 0, "bn_bwd_reduce: shapes");
   if (mode == 1) { CK(y.has_value(), "mode 1 needs y"); BF16(*y); CK(y->numel() == x.numel(), "bn_bwd_reduce: y shape"); }
+  if (mode == 3) CK(y.has_value() && y->scalar_type() == at::kByte && y->numel() >= (x.numel() / 8 + 63) / 64 * 64 &&
+                    (C & (C - 1)) == 0, "mode 3 needs the uint8 bit mask of bn_apply");
+  CK(mode >= 0 && mode <= 3, "bn_bwd_reduce: mode");
   if (mode == 2) { CK(scale.has_value() && shift.has_value(), "mode 2 needs scale/shift"); F32(*scale); F32(*shift); }
   CK(ws.numel() >= (int64_t)bn_partial_rows(x.numel() / C, (int)C) * 2 * C, "bn_bwd_reduce: workspace too small");
   at::DeviceGuard g(x.device());
@@ -98,6 +106,9 @@ void bn_bwd_dx_(const at::Tensor& dy, const at::Tensor& x, c10::optional<at::Ten
   CK(dy.numel() == x.numel() && dx.numel() == x.numel() && x.numel() % C == 0 && C % 8 == 0, "bn_bwd_dx: shapes");
   CK(coef.numel() >= 3 * C, "bn_bwd_dx: coef size");
   if (mode == 1) { CK(y.has_value(), "mode 1 needs y"); BF16(*y); CK(y->numel() == x.numel(), "bn_bwd_dx: y shape"); }
+  if (mode == 3) CK(y.has_value() && y->scalar_type() == at::kByte && y->numel() >= (x.numel() / 8 + 63) / 64 * 64 &&
+                    (C & (C - 1)) == 0, "mode 3 needs the uint8 bit mask of bn_apply");
+  CK(mode >= 0 && mode <= 3, "bn_bwd_dx: mode");
   if (mode == 2) { CK(scale.has_value() && shift.has_value(), "mode 2 needs scale/shift"); F32(*scale); F32(*shift); }
   if (dres) { BF16(*dres); CK(dres->numel() == x.numel(), "bn_bwd_dx: dres shape"); }
   at::DeviceGuard g(x.device());

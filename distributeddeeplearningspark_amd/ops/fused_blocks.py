@@ -25,10 +25,10 @@ from .norm import new_stats_workspace, partials_workspace
 class _ConvBNState:
     """Per-(conv,BN) forward results needed by the backward."""
 
-    __slots__ = ("g", "yc", "y", "mean", "invstd", "scale", "shift", "mode")
+    __slots__ = ("g", "yc", "y", "mean", "invstd", "scale", "shift", "mode", "mask")
 
 
-def _bn_forward(layer_bn, yc, stats, resid, relu, training):
+def _bn_forward(layer_bn, yc, stats, resid, relu, training, mask=None):
     Cc = yc.shape[-1]
     M = yc.numel() // Cc
     dev = yc.device
@@ -42,7 +42,7 @@ def _bn_forward(layer_bn, yc, stats, resid, relu, training):
     invstd = torch.empty(Cc, dtype=torch.float32, device=dev)
     C().bn_finalize(stats, M, Cc, gamma, beta, bn.epsilon, 1.0 - bn.momentum, rm, rv, mean, invstd, scale, shift)
     y = torch.empty_like(yc)
-    C().bn_apply(yc, scale, shift, resid, y, Cc, relu)
+    C().bn_apply(yc, scale, shift, resid, y, Cc, relu, mask)
     return y, mean, invstd, scale, shift
 
 
@@ -57,8 +57,13 @@ def convbn_forward(unit, x, resid=None, relu=True):
     yc = CV.conv_fwd_native(x, conv.kernel.data, g, stats=stats)
     st = _ConvBNState()
     st.g, st.yc = g, yc
-    st.y, st.mean, st.invstd, st.scale, st.shift = _bn_forward(bn, yc, stats, resid, relu, True)
-    st.mode = 0 if not relu else (1 if resid is not None else 2)
+    # ReLU after a residual add: the backward mask cannot be recomputed from yc alone, so the
+    # apply pass stores it as bits (mode 3) instead of the backward re-reading the bf16 output
+    Co = yc.shape[-1]
+    bits = relu and resid is not None and Co & (Co - 1) == 0
+    st.mask = torch.empty(-(-yc.numel() // 512) * 64, dtype=torch.uint8, device=yc.device) if bits else None
+    st.y, st.mean, st.invstd, st.scale, st.shift = _bn_forward(bn, yc, stats, resid, relu, True, st.mask)
+    st.mode = 0 if not relu else (2 if resid is None else (3 if bits else 1))
     return st
 
 
@@ -67,7 +72,7 @@ def bn_backward(unit, st, dy, want_dres):
     Cc = st.yc.shape[-1]
     M = st.yc.numel() // Cc
     ws = partials_workspace(M, Cc, dy.device)
-    y = st.y if st.mode == 1 else None
+    y = st.y if st.mode == 1 else (st.mask if st.mode == 3 else None)
     C().bn_bwd_reduce(dy, st.yc, y, st.scale, st.shift, st.mean, ws, Cc, st.mode)
     coef = torch.empty(3 * Cc, dtype=torch.float32, device=dy.device)
     C().bn_bwd_finalize(ws, M, Cc, None if bn.gamma is None else bn.gamma.master, st.mean, st.invstd,

@@ -117,7 +117,7 @@ class _BatchNormFn(torch.autograd.Function):
                 scale = (g * invstd).contiguous()
                 shift = (b - rmean * scale).contiguous()
             y = torch.empty_like(x)
-            C().bn_apply(x, scale, shift, None if resid is None else resid.contiguous(), y, Cc, relu)
+            C().bn_apply(x, scale, shift, None if resid is None else resid.contiguous(), y, Cc, relu, None)
             ctx.gg, ctx.gbt = ggamma, gbeta
             # relu mask for backward: recompute from x*scale+shift (no resid) or read y (resid)
             ctx.mode = 0 if not relu else (1 if resid is not None else 2)
