@@ -65,6 +65,27 @@ __device__ __forceinline__ float gelu_grad_f(float x) {
 
 // XCD-aware bijective remap of a 1-D block id (MI355X: 8 XCDs, blocks dealt round-robin).
 // Blocks that share an XCD (bid % 8 equal) receive a contiguous range of logical tiles.
+// 64 zero bytes: the source of LDS-DMA lanes whose element lies outside the operand
+// (padding taps, rows / k past the end) — the DMA cannot write a constant.
+static __device__ __attribute__((aligned(64))) uint4 ddl_zero_page[4];
+
+// 16-B LDS-DMA (global_load_lds_dwordx4): lane i's 16 bytes land at lds_wave + 16 i, where
+// lds_wave is the wave-uniform LDS byte address.  Issued from inline asm so the compiler does not
+// see a pending LDS write (it would drain vmcnt(0) before every later LDS access); the kernel
+// orders the ring itself with explicit s_waitcnt vmcnt + barriers.
+__device__ __forceinline__ void dma16(const void* src, uint32_t lds_wave) {
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds_wave) : "memory", "m0");
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return __builtin_amdgcn_readfirstlane(
+      (uint32_t) reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) char*)p));
+}
+// s_waitcnt vmcnt(N) (gfx9 encoding), visible to the compiler's wait-insertion pass
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);
+}
+
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int q = nwg / 8, r = nwg % 8;
   const int xcd = bid % 8, idx = bid / 8;

@@ -13,6 +13,7 @@
 #pragma once
 #include "ddl_common.h"
 #include "ddl_gemm.h"
+#include <stdlib.h>
 
 namespace ddl {
 
@@ -75,53 +76,42 @@ struct Operand {
     }
   }
 
-  __device__ __forceinline__ void load(int k0, const ConvGeom& g, int kdiv, long tap_stride) {
-    if constexpr (MODE == OP_KC) {
-#pragma unroll
-      for (int v = 0; v < V; ++v) {
-        const int idx = threadIdx.x + v * NTHREADS;
-        const int row = idx >> 3, kc = idx & 7;
+  // Source of 16-B vector v of the K-tile at k0 (nullptr: zero).  SWZ: vector v is LDS unit
+  // threadIdx.x + 256 v of the SWIZZLED image (the LDS-DMA writes lane-linearly, so the swizzle
+  // moves to the source); !SWZ: vector v is the unswizzled (row, chunk) the register path stores.
+  template <bool SWZ>
+  __device__ __forceinline__ const bf16_t* addr(int v, int k0, const ConvGeom& g, int kdiv, long tap_stride) const {
+    const int idx = threadIdx.x + v * NTHREADS;
+    if constexpr (KC) {
+      const int row = idx >> 3;
+      const int kc = SWZ ? ((idx & 7) ^ ((row >> 1) & 7)) : (idx & 7);
+      if constexpr (MODE == OP_KC) {
         const int r = r0 + row, k = k0 + kc * 8;
-        reg[v] = (r < rows && k < K) ? ldg16(ptr + (long)r * ld + k) : make_uint4(0, 0, 0, 0);
-      }
-    } else if constexpr (MODE == OP_RC) {
-#pragma unroll
-      for (int v = 0; v < V; ++v) {
-        const int idx = threadIdx.x + v * NTHREADS;
-        const int krow = idx / (R / 8), rc = idx % (R / 8);
-        const int r = r0 + rc * 8, k = k0 + krow;
-        reg[v] = (r < rows && k < K) ? ldg16(ptr + (long)k * ld + r) : make_uint4(0, 0, 0, 0);
-      }
-    } else if constexpr (MODE == OP_KC_GATHER) {
-      const int t = k0 / g.tap_c;  // block-uniform: tap_c % 64 == 0
-      const int c0 = k0 - t * g.tap_c;
-      const int dh = g.dh[t], dw = g.dw[t];
-#pragma unroll
-      for (int v = 0; v < V; ++v) {
-        const int idx = threadIdx.x + v * NTHREADS;
-        const int kc = idx & 7;
-        const int ih = hbase[v] + dh, iw = wbase[v] + dw;
+        return (r < rows && k < K) ? ptr + (long)r * ld + k : nullptr;
+      } else if constexpr (MODE == OP_KC_GATHER) {
+        const int t = k0 / g.tap_c;  // block-uniform: tap_c % 64 == 0
+        const int c0 = k0 - t * g.tap_c;
+        const int ih = hbase[v] + g.dh[t], iw = wbase[v] + g.dw[t];
         const bool ok = rvalid[v] && (unsigned)ih < (unsigned)g.hi && (unsigned)iw < (unsigned)g.wi;
-        reg[v] = ok ? ldg16(ptr + ((long)(pixbase[v] + ih * g.wi + iw)) * g.c + c0 + kc * 8) : make_uint4(0, 0, 0, 0);
-      }
-    } else if constexpr (MODE == OP_KC_GATHER8) {
-#pragma unroll
-      for (int v = 0; v < V; ++v) {
-        const int idx = threadIdx.x + v * NTHREADS;
-        const int k = k0 + (idx & 7) * 8;
+        return ok ? ptr + ((long)(pixbase[v] + ih * g.wi + iw)) * g.c + c0 + kc * 8 : nullptr;
+      } else {  // OP_KC_GATHER8
+        const int k = k0 + kc * 8;
         bool ok = rvalid[v] && k < K;
         const int t = ok ? k / g.tap_c : 0;
         const int c = k - t * g.tap_c;
         const int ih = hbase[v] + g.dh[t], iw = wbase[v] + g.dw[t];
         ok = ok && (unsigned)ih < (unsigned)g.hi && (unsigned)iw < (unsigned)g.wi;
-        reg[v] = ok ? ldg16(ptr + ((long)(pixbase[v] + ih * g.wi + iw)) * g.c + c) : make_uint4(0, 0, 0, 0);
+        return ok ? ptr + ((long)(pixbase[v] + ih * g.wi + iw)) * g.c + c : nullptr;
       }
-    } else if constexpr (MODE == OP_RC_GATHER8) {
-#pragma unroll
-      for (int v = 0; v < V; ++v) {
-        const int idx = threadIdx.x + v * NTHREADS;
-        const int krow = idx / (R / 8), rc = idx % (R / 8);
-        const int k = k0 + krow, r = r0 + rc * 8;
+    } else {
+      const int krow = idx / (R / 8);
+      const int rc = SWZ ? ((idx % (R / 8)) ^ (rc_swz<R>(krow) << 1)) : (idx % (R / 8));
+      const int k = k0 + krow;
+      if constexpr (MODE == OP_RC) {
+        const int r = r0 + rc * 8;
+        return (r < rows && k < K) ? ptr + (long)k * ld + r : nullptr;
+      } else if constexpr (MODE == OP_RC_GATHER8) {
+        const int r = r0 + rc * 8;
         bool ok = k < K && r < rows;
         const int t = ok ? r / g.tap_c : 0;
         const int c = r - t * g.tap_c;
@@ -129,34 +119,38 @@ struct Operand {
         pix_decompose((uint32_t)(ok ? k : 0), g.ho, g.wo, n, i, j);
         const int ih = i * g.sh + g.dh[t], iw = j * g.sw + g.dw[t];
         ok = ok && (unsigned)ih < (unsigned)g.hi && (unsigned)iw < (unsigned)g.wi;
-        reg[v] = ok ? ldg16(ptr + ((long)((n * g.hi + ih) * g.wi + iw)) * g.c + c) : make_uint4(0, 0, 0, 0);
-      }
-    } else if constexpr (MODE == OP_RC_GATHER) {
-      const int t = r0 / g.tap_c;  // block-uniform: tap_c % R == 0
-      const int c0 = r0 - t * g.tap_c;
-      const int dh = g.dh[t], dw = g.dw[t];
-#pragma unroll
-      for (int v = 0; v < V; ++v) {
-        const int idx = threadIdx.x + v * NTHREADS;
-        const int krow = idx / (R / 8), rc = idx % (R / 8);
-        const int k = k0 + krow;
+        return ok ? ptr + ((long)((n * g.hi + ih) * g.wi + iw)) * g.c + c : nullptr;
+      } else if constexpr (MODE == OP_RC_GATHER) {
+        const int t = r0 / g.tap_c;  // block-uniform: tap_c % R == 0
+        const int c0 = r0 - t * g.tap_c;
         int n, i, j;
         pix_decompose((uint32_t)(k < K ? k : 0), g.ho, g.wo, n, i, j);
-        const int ih = i * g.sh + dh, iw = j * g.sw + dw;
+        const int ih = i * g.sh + g.dh[t], iw = j * g.sw + g.dw[t];
         const bool ok = k < K && (unsigned)ih < (unsigned)g.hi && (unsigned)iw < (unsigned)g.wi;
-        reg[v] = ok ? ldg16(ptr + ((long)((n * g.hi + ih) * g.wi + iw)) * g.c + c0 + rc * 8) : make_uint4(0, 0, 0, 0);
+        return ok ? ptr + ((long)((n * g.hi + ih) * g.wi + iw)) * g.c + c0 + rc * 8 : nullptr;
+      } else {  // OP_RC_TAPS: k = tap*kdiv + co ; addr = ptr + co*ld + wt[tap]*tap_stride + r
+        const int t = k0 / kdiv;  // block-uniform: kdiv % 64 == 0
+        const int co0 = k0 - t * kdiv;
+        const int r = r0 + rc * 8;
+        return (r < rows && k < K) ? ptr + (long)g.wt[t] * tap_stride + (long)(co0 + krow) * ld + r : nullptr;
       }
-    } else {  // OP_RC_TAPS: k = tap*kdiv + co ; addr = ptr + co*ld + wt[tap]*tap_stride + r
-      const int t = k0 / kdiv;  // block-uniform: kdiv % 64 == 0
-      const int co0 = k0 - t * kdiv;
-      const bf16_t* base = ptr + (long)g.wt[t] * tap_stride;
+    }
+  }
+
+  __device__ __forceinline__ void load(int k0, const ConvGeom& g, int kdiv, long tap_stride) {
 #pragma unroll
-      for (int v = 0; v < V; ++v) {
-        const int idx = threadIdx.x + v * NTHREADS;
-        const int krow = idx / (R / 8), rc = idx % (R / 8);
-        const int r = r0 + rc * 8, k = k0 + krow;
-        reg[v] = (r < rows && k < K) ? ldg16(base + (long)(co0 + krow) * ld + r) : make_uint4(0, 0, 0, 0);
-      }
+    for (int v = 0; v < V; ++v) {
+      const bf16_t* src = addr<false>(v, k0, g, kdiv, tap_stride);
+      reg[v] = src ? ldg16(src) : make_uint4(0, 0, 0, 0);
+    }
+  }
+
+  // LDS-DMA of the K-tile at k0 into a (swizzled) LDS image: V wave-instructions of 1 KB each
+  __device__ __forceinline__ void dma(char* lds, int k0, const ConvGeom& g, int kdiv, long tap_stride, int wid) const {
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const bf16_t* src = addr<true>(v, k0, g, kdiv, tap_stride);
+      dma16(src ? (const void*)src : (const void*)ddl_zero_page, lds_addr(lds + v * (NTHREADS * 16) + wid * 1024));
     }
   }
 
@@ -464,15 +458,121 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams
   gemm_epilogue<RM, RN, EPI>(p, acc, m0 + wm0, n0 + wn0, lane, bid);
 }
 
+// LDS-DMA variant of the same kernel: identical tiles, operand modes, fragments and epilogue,
+// but the K-tiles are staged with global_load_lds (Operand::dma: no VGPR round trip, no VALU
+// pack, the LDS swizzle moved to the source address; padding and out-of-range vectors read
+// ddl_zero_page).  ST = 1: one LDS stage per block (32 KB at 128x128, so 4 blocks share a CU
+// and each block's load latency hides under the others' MFMAs); ST = 2: two stages, the next
+// K-tile's DMA in flight under the current tile's MFMAs (counted vmcnt, raw barriers).
+template <int BM, int BN, int AMODE, int BMODE, int EPI, int ST>
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_dma_kernel(const GemmParams p) {
+  constexpr int WTM = BM / 2, WTN = BN / 2;
+  constexpr int RM = WTM / 16, RN = WTN / 16;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int VA = BM / 32, VB = BN / 32;  // DMA wave-instructions per operand per K-tile
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tiles_n = (p.N + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = bid / tiles_n, tn = bid - tm * tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kbeg = blockIdx.y * p.k_split;
+  const int kend = min(p.K, kbeg + p.k_split);
+  const int nk = (kend - kbeg + BK - 1) / BK;
+
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int wm0 = (wid >> 1) * WTM, wn0 = (wid & 1) * WTN;
+
+  Operand<BM, AMODE> A;
+  Operand<BN, BMODE> B;
+  A.init(p.a, p.lda, p.M, m0, p.K, p.g);
+  B.init(p.b, p.ldb, p.N, n0, p.K, p.g);
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto stage = [&](int buf) { return smem + buf * (A_BYTES + B_BYTES); };
+  if (nk > 0) {
+    A.dma(stage(0), kbeg, p.g, p.b_kdiv, p.b_tap_stride, wid);
+    B.dma(stage(0) + A_BYTES, kbeg, p.g, p.b_kdiv, p.b_tap_stride, wid);
+  }
+  for (int t = 0; t < nk; ++t) {
+    const char* la = stage(ST == 2 ? (t & 1) : 0);
+    const char* lb = la + A_BYTES;
+    if constexpr (ST == 2) {
+      if (t + 1 < nk) {  // refill the stage read in iteration t - 1 (freed by its closing barrier)
+        char* nx = stage((t + 1) & 1);
+        A.dma(nx, kbeg + (t + 1) * BK, p.g, p.b_kdiv, p.b_tap_stride, wid);
+        B.dma(nx + A_BYTES, kbeg + (t + 1) * BK, p.g, p.b_kdiv, p.b_tap_stride, wid);
+        wait_vmcnt<VA + VB>();  // this wave's tile-t DMAs done, tile t+1 still in flight
+      } else {
+        wait_vmcnt<0>();
+      }
+    } else {
+      wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();  // every wave's tile-t DMAs have landed
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8 af[RM], bf[RN];
+#pragma unroll
+      for (int i = 0; i < RM; ++i) af[i] = A.frag(la, kk, i, wm0, lane);
+#pragma unroll
+      for (int j = 0; j < RN; ++j) bf[j] = B.frag(lb, kk, j, wn0, lane);
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j) {
+          if constexpr (EPI == EPI_BF16)
+            acc[i][j] = mfma16x16x32(bf[j], af[i], acc[i][j]);
+          else
+            acc[i][j] = mfma16x16x32(af[i], bf[j], acc[i][j]);
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave is done reading this stage
+    if constexpr (ST == 1) {
+      if (t + 1 < nk) {
+        A.dma(smem, kbeg + (t + 1) * BK, p.g, p.b_kdiv, p.b_tap_stride, wid);
+        B.dma(smem + A_BYTES, kbeg + (t + 1) * BK, p.g, p.b_kdiv, p.b_tap_stride, wid);
+      }
+    }
+  }
+
+  gemm_epilogue<RM, RN, EPI>(p, acc, m0 + wm0, n0 + wn0, lane, bid);
+}
+
+// DDL_GEMM_DMA: 0 = register-staged kernel, 1 = LDS-DMA single stage (default), 2 = LDS-DMA double stage
+inline int gemm_dma_mode() {
+  static int mode = -1;
+  if (mode < 0) {
+    const char* e = getenv("DDL_GEMM_DMA");
+    mode = e ? atoi(e) : 1;
+  }
+  return mode;
+}
+
 template <int BM, int BN, int AMODE, int BMODE, int EPI>
 inline int launch_tile(const GemmParams& p, hipStream_t s) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
   const int splits = (p.K + p.k_split - 1) / p.k_split;
   // single K-tile (1x1 convs with K <= 64): one LDS stage -> twice the resident blocks per CU
   const bool one_stage = p.k_split <= BK;
-  const size_t lds = (one_stage ? 1 : 2) * (BM + BN) * BK * 2;
-  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, AMODE, BMODE, EPI>), dim3(tiles, splits > 0 ? splits : 1), dim3(NTHREADS),
-                     lds, s, p);
+  const dim3 grid(tiles, splits > 0 ? splits : 1);
+  const int dm = gemm_dma_mode();
+  if (dm == 1 || (dm == 2 && one_stage)) {
+    hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, AMODE, BMODE, EPI, 1>), grid, dim3(NTHREADS), (BM + BN) * BK * 2, s, p);
+  } else if (dm == 2) {
+    hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, AMODE, BMODE, EPI, 2>), grid, dim3(NTHREADS), 2 * (BM + BN) * BK * 2, s,
+                       p);
+  } else {
+    const size_t lds = (one_stage ? 1 : 2) * (BM + BN) * BK * 2;
+    hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, AMODE, BMODE, EPI>), grid, dim3(NTHREADS), lds, s, p);
+  }
   return (int)hipGetLastError();
 }
 
