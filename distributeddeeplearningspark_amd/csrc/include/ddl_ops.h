@@ -69,7 +69,9 @@ int normalize_u8(const uint8_t* x, void* y, long npix, int c, int cpad, const fl
 int sgd_step(float* w, const float* g, float* mom, void* w16, long n, float lr, float momentum, float dampening,
              float wd, int nesterov, float gscale, hipStream_t s);
 int adam_step(float* w, const float* g, float* m, float* v, void* w16, long n, float lr, float b1, float b2,
-              float eps, float wd, int adamw, float bc1, float bc2, float gscale, hipStream_t s);
+              float eps, float wd, int adamw, float bc1, float bc2, float gscale, const float* tstep,
+              hipStream_t s);
+int step_tick(float* t, hipStream_t s);
 int adagrad_step(float* w, const float* g, float* acc, void* w16, long n, float lr, float eps, float wd, float gscale,
                  hipStream_t s);
 int rmsprop_step(float* w, const float* g, float* acc, void* w16, long n, float lr, float rho, float eps, float wd,
@@ -130,7 +132,8 @@ int embed_bwd(const int64_t* ids, const int64_t* types, const void* ds, float* g
 int rnn_fwd(int cell, const float* xw, const float* U, float* hs, float* cs, float* gates, float* y, int B, int T,
             int H, int rs, hipStream_t s);
 // UT = U^T [G*H][H]; dgates [B][T][G*H] = gradients of the gate pre-activations
-int rnn_bwd(int cell, const float* dy, const float* UT, const float* hs, const float* cs, const float* gates,
-            float* dgates, int B, int T, int H, int rs, hipStream_t s);
+bool rnn_bwd_uses_ut(int H);
+int rnn_bwd(int cell, const float* dy, const float* U, const float* UT, const float* hs, const float* cs,
+            const float* gates, float* dgates, int B, int T, int H, int rs, hipStream_t s);
 
 }  // namespace ddl

@@ -61,7 +61,12 @@ int sgd_step(float* w, const float* g, float* mom, void* w16, long n, float lr, 
 //   Keras 2: w -= lr * sqrt(bc2)/bc1 * m / (sqrt(v) + eps)
 __global__ __launch_bounds__(256) void adam_kernel(float4* w, const float4* g, float4* m, float4* v, void* w16, long n,
                                                     float lr, float b1, float b2, float eps, float wd, int mode,
-                                                    float bc1, float bc2, float gs) {
+                                                    float bc1, float bc2, float gs, const float* tstep) {
+  if (tstep) {  // graph-replayed step: bias corrections from the device step counter
+    const float t = *tstep;
+    bc1 = 1.f - powf(b1, t);
+    bc2 = 1.f - powf(b2, t);
+  }
   const float sbc2 = sqrtf(bc2);
   DDL_FLAT_FOR(i, n) {
     float4 p = w[i], d = g[i], mm = m[i], vv = v[i];
@@ -84,10 +89,19 @@ __global__ __launch_bounds__(256) void adam_kernel(float4* w, const float4* g, f
 }
 
 int adam_step(float* w, const float* g, float* m, float* v, void* w16, long n, float lr, float b1, float b2, float eps,
-              float wd, int adamw, float bc1, float bc2, float gscale, hipStream_t s) {
+              float wd, int adamw, float bc1, float bc2, float gscale, const float* tstep, hipStream_t s) {
   if (n % 4) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(adam_kernel, dim3(ogrid(n / 4)), dim3(256), 0, s, (float4*)w, (const float4*)g, (float4*)m,
-                     (float4*)v, w16, n, lr, b1, b2, eps, wd, adamw, bc1, bc2, gscale);
+                     (float4*)v, w16, n, lr, b1, b2, eps, wd, adamw, bc1, bc2, gscale, tstep);
+  return (int)hipGetLastError();
+}
+
+// Device-resident optimizer step counter (t += 1), so a captured hipGraph that is
+// replayed every step still sees the right Adam bias corrections.
+__global__ void step_tick_kernel(float* t) { *t += 1.f; }
+
+int step_tick(float* t, hipStream_t s) {
+  hipLaunchKernelGGL(step_tick_kernel, dim3(1), dim3(1), 0, s, t);
   return (int)hipGetLastError();
 }
 

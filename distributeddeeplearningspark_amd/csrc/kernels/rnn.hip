@@ -181,10 +181,266 @@ __global__ __launch_bounds__(512) void rnn_bwd_kernel(const float* __restrict__ 
   }
 }
 
+
+// =============================================================================================
+// Register-resident fast path (H = 64 / 128, the reference's GRU(128) / LSTM(128)).
+//
+// The generic kernels above stream U from L2 on every step (latency-bound: ~3 ms per GRU step
+// at B=32).  Here each workgroup pins the WHOLE recurrent matrix in VGPRs for the sequence:
+//  forward : thread (j, kh) holds U[kh*64 .. kh*64+63][j]  (KS = H/64 lane-adjacent k-splits,
+//            reduced with one xor-shuffle), so NT = G*H*KS threads (768 GRU / 1024 LSTM);
+//  backward: thread (k, js) holds U[k][js*64 .. js*64+63]  (row chunk, contiguous loads),
+//            JSP = pow2(G*H/64) lane-adjacent chunks reduced with xor-shuffles.
+// h / (r*h) / gate-gradient rows live in LDS with 64-float chunks padded to 68 floats, so the
+// lanes of a wave that read different chunks hit different banks.  Per step the only global
+// traffic is the x W + b row (prefetched at the top of the step) and the saved activations.
+// =============================================================================================
+constexpr int CH = 64;       // k / j chunk held in registers
+constexpr int CP = CH + 4;   // padded LDS chunk stride (floats)
+
+__device__ __forceinline__ int cpos(int col) { return (col / CH) * CP + (col % CH); }
+
+template <int CELL, int H>
+constexpr int fwd_threads() { return (CELL == 0 ? 3 : 4) * H * (H / 64); }
+template <int CELL, int H>
+constexpr int bwd_threads() { return H * (((CELL == 0 ? 3 : 4) * H / 64) <= 4 ? 4 : 8); }
+
+template <int CELL, int H, int BB_>
+__global__ __launch_bounds__((fwd_threads<CELL, H>())) void rnn_fwd_reg_kernel(const float* __restrict__ xw, const float* __restrict__ U,
+                                                           float* __restrict__ hs, float* __restrict__ cs,
+                                                           float* __restrict__ gates, float* __restrict__ y, int B,
+                                                           int T, int rs) {
+  constexpr int G = CELL == 0 ? 3 : 4;
+  constexpr int GH = G * H;
+  constexpr int KS = H / CH;
+  constexpr int HC = KS * CP;  // padded row length of h / c
+  __shared__ __attribute__((aligned(16))) float h[BB_][HC];
+  __shared__ __attribute__((aligned(16))) float c[BB_][HC];  // LSTM cell state / GRU r*h
+  __shared__ float gb[BB_][GH];
+  const int tid = threadIdx.x;
+  const int j = tid / KS, kh = tid % KS;
+  const int b0 = blockIdx.x * BB_;
+  const int nb = min(BB_, B - b0);
+  float u[CH];
+#pragma unroll
+  for (int i = 0; i < CH; ++i) u[i] = U[(long)(kh * CH + i) * GH + j];
+  for (int i = tid; i < BB_ * HC; i += blockDim.x) (&h[0][0])[i] = (&c[0][0])[i] = 0.f;
+  for (int i = tid; i < nb * H; i += blockDim.x) {
+    const int r = i / H, k = i - r * H;
+    hs[((long)(b0 + r) * (T + 1)) * H + k] = 0.f;
+    if (CELL == 1) cs[((long)(b0 + r) * (T + 1)) * H + k] = 0.f;
+  }
+  __syncthreads();
+  auto contract = [&](float (*src)[HC], float* acc) {
+#pragma unroll
+    for (int r = 0; r < BB_; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int i = 0; i < CH; i += 4) {
+#pragma unroll
+      for (int r = 0; r < BB_; ++r) {
+        const float4 v = *reinterpret_cast<const float4*>(&src[r][kh * CP + i]);
+        acc[r] += v.x * u[i] + v.y * u[i + 1] + v.z * u[i + 2] + v.w * u[i + 3];
+      }
+    }
+    if (KS == 2) {
+#pragma unroll
+      for (int r = 0; r < BB_; ++r) acc[r] += __shfl_xor(acc[r], 1, 64);
+    }
+  };
+  for (int t = 0; t < T; ++t) {
+    float xv[BB_];
+#pragma unroll
+    for (int r = 0; r < BB_; ++r) xv[r] = (kh == 0 && r < nb) ? xw[((long)(b0 + r) * T + t) * GH + j] : 0.f;
+    float acc[BB_];
+    if (CELL == 1 || j < 2 * H) {  // wave-uniform: 2H columns span whole waves
+      contract(h, acc);
+      if (kh == 0) {
+        const bool is_tanh = CELL == 1 && j >= 2 * H && j < 3 * H;
+#pragma unroll
+        for (int r = 0; r < BB_; ++r) gb[r][j] = is_tanh ? tanhf(acc[r] + xv[r]) : hsig(acc[r] + xv[r]);
+      }
+    }
+    __syncthreads();
+    if (CELL == 0) {
+      for (int i = tid; i < BB_ * H; i += blockDim.x) {
+        const int r = i / H, k = i - r * H;
+        c[r][cpos(k)] = gb[r][H + k] * h[r][cpos(k)];
+      }
+      __syncthreads();
+      if (j >= 2 * H) {
+        contract(c, acc);
+        if (kh == 0) {
+#pragma unroll
+          for (int r = 0; r < BB_; ++r) gb[r][j] = tanhf(acc[r] + xv[r]);
+        }
+      }
+      __syncthreads();
+    }
+    for (int i = tid; i < nb * H; i += blockDim.x) {
+      const int r = i / H, k = i - r * H;
+      const long row = b0 + r;
+      float hn;
+      if (CELL == 0) {
+        const float z = gb[r][k], hh = gb[r][2 * H + k];
+        hn = z * h[r][cpos(k)] + (1.f - z) * hh;
+      } else {
+        const float cn = gb[r][H + k] * c[r][cpos(k)] + gb[r][k] * gb[r][2 * H + k];
+        c[r][cpos(k)] = cn;
+        hn = gb[r][3 * H + k] * tanhf(cn);
+        cs[(row * (T + 1) + t + 1) * H + k] = cn;
+      }
+      h[r][cpos(k)] = hn;
+      hs[(row * (T + 1) + t + 1) * H + k] = hn;
+      if (rs) y[(row * T + t) * H + k] = hn;
+      else if (t == T - 1) y[row * H + k] = hn;
+    }
+    for (int i = tid; i < nb * GH; i += blockDim.x) {
+      const int r = i / GH, jj = i - r * GH;
+      gates[((long)(b0 + r) * T + t) * GH + jj] = gb[r][jj];
+    }
+    __syncthreads();
+  }
+}
+
+template <int CELL, int H, int BB_>
+__global__ __launch_bounds__((bwd_threads<CELL, H>())) void rnn_bwd_reg_kernel(const float* __restrict__ dy, const float* __restrict__ U,
+                                                           const float* __restrict__ hs, const float* __restrict__ cs,
+                                                           const float* __restrict__ gates,
+                                                           float* __restrict__ dgates, int B, int T, int rs) {
+  constexpr int G = CELL == 0 ? 3 : 4;
+  constexpr int GH = G * H;
+  constexpr int JS = GH / CH;                            // column chunks
+  constexpr int JSP = JS <= 4 ? 4 : 8;                   // lanes per k (power of two)
+  constexpr int ZR = CELL == 0 ? 2 * H / CH : JS;        // chunks feeding dh directly
+  __shared__ __attribute__((aligned(16))) float p[BB_][JS * CP];  // pre-activation gradients
+  __shared__ float dh[BB_][H];
+  __shared__ float aux[BB_][H];  // GRU: d*z direct part; LSTM: running dc
+  const int tid = threadIdx.x;
+  const int k = tid / JSP, js = tid % JSP;
+  const bool active = js < JS;
+  const int b0 = blockIdx.x * BB_;
+  const int nb = min(BB_, B - b0);
+  float u[CH];
+#pragma unroll
+  for (int i = 0; i < CH; i += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(&U[(long)k * GH + min(js, JS - 1) * CH + i]);  // idle lanes: never used
+    u[i] = v.x; u[i + 1] = v.y; u[i + 2] = v.z; u[i + 3] = v.w;
+  }
+  for (int i = tid; i < BB_ * H; i += blockDim.x) (&dh[0][0])[i] = (&aux[0][0])[i] = 0.f;
+  for (int i = tid; i < BB_ * JS * CP; i += blockDim.x) (&p[0][0])[i] = 0.f;
+  __syncthreads();
+  auto contract = [&](bool use, float* acc) {
+#pragma unroll
+    for (int r = 0; r < BB_; ++r) acc[r] = 0.f;
+    // every lane computes (no divergence inside the unrolled dot); lanes whose chunk is not
+    // part of this contraction drop their partial before the shuffle reduction
+    const int jc = min(js, JS - 1);
+#pragma unroll
+    for (int i = 0; i < CH; i += 4) {
+#pragma unroll
+      for (int r = 0; r < BB_; ++r) {
+        const float4 v = *reinterpret_cast<const float4*>(&p[r][jc * CP + i]);
+        acc[r] += v.x * u[i] + v.y * u[i + 1] + v.z * u[i + 2] + v.w * u[i + 3];
+      }
+      if ((i & 15) == 12) __builtin_amdgcn_sched_barrier(0);  // bound the LDS loads in flight
+    }
+#pragma unroll
+    for (int r = 0; r < BB_; ++r) {
+      acc[r] = use ? acc[r] : 0.f;
+#pragma unroll
+      for (int o = 1; o < JSP; o <<= 1) acc[r] += __shfl_xor(acc[r], o, 64);
+    }
+  };
+  for (int t = T - 1; t >= 0; --t) {
+    for (int i = tid; i < nb * H; i += blockDim.x) {
+      const int r = i / H, kk = i - r * H;
+      const long row = b0 + r;
+      float d = dh[r][kk];
+      if (rs) d += dy[(row * T + t) * H + kk];
+      else if (t == T - 1) d += dy[row * H + kk];
+      const float* g = gates + (row * T + t) * GH;
+      float* pr = p[r];
+      if (CELL == 0) {
+        const float hp = hs[(row * (T + 1) + t) * H + kk];
+        const float z = g[kk], hh = g[2 * H + kk];
+        pr[cpos(kk)] = d * (hp - hh) * hsig_d(z);
+        pr[cpos(2 * H + kk)] = d * (1.f - z) * (1.f - hh * hh);
+        aux[r][kk] = d * z;
+      } else {
+        const float gi = g[kk], gf = g[H + kk], gg = g[2 * H + kk], go = g[3 * H + kk];
+        const float cn = cs[(row * (T + 1) + t + 1) * H + kk], cp = cs[(row * (T + 1) + t) * H + kk];
+        const float tc = tanhf(cn);
+        const float dc = aux[r][kk] + d * go * (1.f - tc * tc);
+        pr[cpos(kk)] = dc * gg * hsig_d(gi);
+        pr[cpos(H + kk)] = dc * cp * hsig_d(gf);
+        pr[cpos(2 * H + kk)] = dc * gi * (1.f - gg * gg);
+        pr[cpos(3 * H + kk)] = d * tc * hsig_d(go);
+        aux[r][kk] = dc * gf;
+      }
+    }
+    __syncthreads();
+    // GRU: phase 0 = d(r*h) = dp_h Uh^T -> dr and the r-path part of dh_{t-1}; phase 1 = dh_{t-1}.
+    // One call site for the contraction (keeps a single register-resident copy of U).
+#pragma unroll 1
+    for (int ph = CELL == 0 ? 0 : 1; ph < 2; ++ph) {
+      float acc[BB_];
+      contract(active && (ph == 0 ? js >= ZR : js < ZR), acc);
+      if (js == 0) {
+        if (ph == 0) {
+          for (int r = 0; r < nb; ++r) {
+            const long row = b0 + r;
+            const float hp = hs[(row * (T + 1) + t) * H + k];
+            const float rg = gates[(row * T + t) * GH + H + k];
+            p[r][cpos(H + k)] = acc[r] * hp * hsig_d(rg);
+            aux[r][k] += acc[r] * rg;
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < BB_; ++r) dh[r][k] = (CELL == 0 ? aux[r][k] : 0.f) + acc[r];
+        }
+      }
+      if (ph == 0) __syncthreads();
+    }
+    for (int i = tid; i < nb * GH; i += blockDim.x) {
+      const int r = i / GH, jj = i - r * GH;
+      dgates[((long)(b0 + r) * T + t) * GH + jj] = p[r][cpos(jj)];
+    }
+    __syncthreads();
+  }
+}
+
+template <int CELL, int H, int BB_>
+int launch_fwd_reg(const float* xw, const float* U, float* hs, float* cs, float* gates, float* y, int B, int T, int rs,
+                   hipStream_t s) {
+  constexpr int G = CELL == 0 ? 3 : 4;
+  const dim3 grid((B + BB_ - 1) / BB_);
+  hipLaunchKernelGGL((rnn_fwd_reg_kernel<CELL, H, BB_>), grid, dim3(G * H * (H / CH)), 0, s, xw, U, hs, cs, gates, y,
+                     B, T, rs);
+  return (int)hipGetLastError();
+}
+
+template <int CELL, int H, int BB_>
+int launch_bwd_reg(const float* dy, const float* U, const float* hs, const float* cs, const float* gates,
+                   float* dgates, int B, int T, int rs, hipStream_t s) {
+  constexpr int G = CELL == 0 ? 3 : 4;
+  constexpr int JS = G * H / CH;
+  constexpr int JSP = JS <= 4 ? 4 : 8;
+  const dim3 grid((B + BB_ - 1) / BB_);
+  hipLaunchKernelGGL((rnn_bwd_reg_kernel<CELL, H, BB_>), grid, dim3(H * JSP), 0, s, dy, U, hs, cs, gates, dgates, B,
+                     T, rs);
+  return (int)hipGetLastError();
+}
+
 }  // namespace
 
 int rnn_fwd(int cell, const float* xw, const float* U, float* hs, float* cs, float* gates, float* y, int B, int T,
             int H, int rs, hipStream_t s) {
+  if (H == 128)
+    return cell == 0 ? launch_fwd_reg<0, 128, 4>(xw, U, hs, cs, gates, y, B, T, rs, s)
+                     : launch_fwd_reg<1, 128, 4>(xw, U, hs, cs, gates, y, B, T, rs, s);
+  if (H == 64)
+    return cell == 0 ? launch_fwd_reg<0, 64, 2>(xw, U, hs, cs, gates, y, B, T, rs, s)
+                     : launch_fwd_reg<1, 64, 2>(xw, U, hs, cs, gates, y, B, T, rs, s);
   const int G = cell == 0 ? 3 : 4;
   const size_t lds = sizeof(float) * (2 * BB * H + BB * G * H);
   const int threads = std::min(512, ((G * H + 63) / 64) * 64);
@@ -196,8 +452,16 @@ int rnn_fwd(int cell, const float* xw, const float* U, float* hs, float* cs, flo
   return (int)hipGetLastError();
 }
 
-int rnn_bwd(int cell, const float* dy, const float* UT, const float* hs, const float* cs, const float* gates,
-            float* dgates, int B, int T, int H, int rs, hipStream_t s) {
+bool rnn_bwd_uses_ut(int H) { return H != 128 && H != 64; }
+
+int rnn_bwd(int cell, const float* dy, const float* U, const float* UT, const float* hs, const float* cs,
+            const float* gates, float* dgates, int B, int T, int H, int rs, hipStream_t s) {
+  if (H == 128)
+    return cell == 0 ? launch_bwd_reg<0, 128, 2>(dy, U, hs, cs, gates, dgates, B, T, rs, s)
+                     : launch_bwd_reg<1, 128, 4>(dy, U, hs, cs, gates, dgates, B, T, rs, s);
+  if (H == 64)
+    return cell == 0 ? launch_bwd_reg<0, 64, 2>(dy, U, hs, cs, gates, dgates, B, T, rs, s)
+                     : launch_bwd_reg<1, 64, 2>(dy, U, hs, cs, gates, dgates, B, T, rs, s);
   const int G = cell == 0 ? 3 : 4;
   const size_t lds = sizeof(float) * (2 * BB * H + BB * G * H);
   const int threads = std::min(512, ((G * H + 63) / 64) * 64);

@@ -264,15 +264,22 @@ void sgd_step_(const at::Tensor& w, const at::Tensor& g, c10::optional<at::Tenso
 }
 void adam_step_(const at::Tensor& w, const at::Tensor& g, const at::Tensor& m, const at::Tensor& v,
                 c10::optional<at::Tensor> w16, double lr, double b1, double b2, double eps, double wd, int64_t mode,
-                double bc1, double bc2, double gscale) {
+                double bc1, double bc2, double gscale, c10::optional<at::Tensor> tstep) {
   OPT_CHECK(w, g);
   F32(m); F32(v);
+  if (tstep) { F32(*tstep); CK(tstep->numel() == 1 && tstep->device() == w.device(), "adam: step counter"); }
   CK(m.numel() == w.numel() && v.numel() == w.numel(), "adam: state sizes");
   if (w16) { BF16(*w16); CK(w16->numel() == w.numel(), "w16 size"); }
   at::DeviceGuard gd(w.device());
   HIP_OK(adam_step(w.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), optr<void>(w16),
                    w.numel(), (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (int)mode, (float)bc1,
-                   (float)bc2, (float)gscale, cur_stream()));
+                   (float)bc2, (float)gscale, optr<float>(tstep), cur_stream()));
+}
+void step_tick_(const at::Tensor& t) {
+  F32(t);
+  CK(t.is_cuda() && t.numel() == 1, "step counter: one fp32 element on the GPU");
+  at::DeviceGuard gd(t.device());
+  HIP_OK(step_tick(t.data_ptr<float>(), cur_stream()));
 }
 void adagrad_step_(const at::Tensor& w, const at::Tensor& g, const at::Tensor& acc, c10::optional<at::Tensor> w16,
                    double lr, double eps, double wd, double gscale) {
@@ -326,7 +333,10 @@ void register_ops(py::module& m) {
   m.def("normalize_u8", &normalize_u8_);
   m.def("s2d_pad", &s2d_pad_);
   m.def("sgd_step", &sgd_step_);
-  m.def("adam_step", &adam_step_);
+  m.def("adam_step", &adam_step_, "fused Adam/AdamW", py::arg("w"), py::arg("g"), py::arg("m"), py::arg("v"),
+        py::arg("w16"), py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("mode"),
+        py::arg("bc1"), py::arg("bc2"), py::arg("gscale"), py::arg("tstep") = py::none());
+  m.def("step_tick", &step_tick_);
   m.def("adagrad_step", &adagrad_step_);
   m.def("rmsprop_step", &rmsprop_step_);
   m.def("sumsq", &sumsq_);

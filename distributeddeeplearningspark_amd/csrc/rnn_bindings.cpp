@@ -58,9 +58,10 @@ py::tuple rnn_bwd_(const std::string& cell, const at::Tensor& dy, const at::Tens
   const at::Tensor& gates = saved[2];
   at::DeviceGuard g(x.device());
   at::Tensor dyc = dy.contiguous();
-  at::Tensor UT = U.t().contiguous();
+  at::Tensor Uc = U.contiguous();
+  at::Tensor UT = rnn_bwd_uses_ut((int)H) ? U.t().contiguous() : Uc;
   at::Tensor dgates = at::empty({B, T, G * H}, x.options());
-  int e = rnn_bwd(c, dyc.data_ptr<float>(), UT.data_ptr<float>(), hs.data_ptr<float>(),
+  int e = rnn_bwd(c, dyc.data_ptr<float>(), Uc.data_ptr<float>(), UT.data_ptr<float>(), hs.data_ptr<float>(),
                   c == 1 ? cs.data_ptr<float>() : nullptr, gates.data_ptr<float>(), dgates.data_ptr<float>(), (int)B,
                   (int)T, (int)H, rs ? 1 : 0, cur_stream());
   TORCH_CHECK(e == 0, "rnn_bwd launch failed: ", hipGetErrorString((hipError_t)e));

@@ -474,6 +474,7 @@ class BertForMaskedLM(Model):
         self.head = BertMLMHead(c, name=self.name + "/cls/predictions")
         self._step = 0
         self.dropout_seed = 1234
+        self.graph_capturable = False  # dropout hashes are seeded from a host step counter
 
     def sublayers(self):
         return [self.embeddings, *self.encoder, self.head]

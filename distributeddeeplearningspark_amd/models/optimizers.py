@@ -22,10 +22,12 @@ class Optimizer:
         self.iterations = 0
         self.arena = None
         self.state: dict[str, torch.Tensor] = {}
+        self.device_step: torch.Tensor | None = None  # set for graph capture (models/step.py)
 
     def bind(self, arena):
         self.arena = arena
         self.iterations = 0
+        self.device_step = None
         self._alloc()
         return self
 
@@ -46,6 +48,16 @@ class Optimizer:
         for k, v in sd.items():
             if k in self.state:
                 self.state[k].copy_(v.to(self.state[k].device))
+        if self.device_step is not None:
+            self.device_step.fill_(float(self.iterations))
+
+    # ---------------------------------------------------------------- graph capture
+    def enable_device_step(self):
+        """Keep the step counter on the GPU (needed once a step is replayed from a hipGraph:
+        host scalars baked into a captured launch would never change)."""
+        if self.device_step is None and self.arena is not None and self.arena.master.is_cuda:
+            self.device_step = torch.full((1,), float(self.iterations), dtype=torch.float32,
+                                          device=self.arena.master.device)
 
     def _grad_scale(self, grad_scale):
         if self.clipnorm is None:
@@ -101,7 +113,7 @@ class Adam(Optimizer):
     def _apply(self, w, g, w16, gs):
         K.adam_(w, g, self.state["m"], self.state["v"], w16, lr=self.lr, beta1=self.b1, beta2=self.b2, eps=self.eps,
                 weight_decay=self.weight_decay, decoupled=self.decoupled, keras_eps=self.keras_eps,
-                step=self.iterations, grad_scale=gs)
+                step=self.iterations, grad_scale=gs, device_step=self.device_step)
 
     def get_config(self):
         return {**super().get_config(), "beta_1": self.b1, "beta_2": self.b2, "epsilon": self.eps}

@@ -114,6 +114,16 @@ def conv_fwd_native(x, w, g: ConvGeometry, bias=None, relu=False, stats=None):
     return y
 
 
+def _tap_index(cl, device):
+    """Device-resident tap-index tensor of a dgrad class (cached: no host->device copy per
+    step, which also keeps the backward capturable into a hipGraph)."""
+    cache = cl.setdefault("_wt_dev", {})
+    key = str(device)
+    if key not in cache:
+        cache[key] = torch.tensor(cl["wt"], dtype=torch.int64, device=device)
+    return cache[key]
+
+
 def conv_dgrad_native(dy, w, g: ConvGeometry, resid=None):
     """dx = conv^T(dy, w) (+ resid, fused into the epilogue when the layout allows)."""
     dev = dy.device
@@ -143,7 +153,7 @@ def conv_dgrad_native(dy, w, g: ConvGeometry, resid=None):
             kp = math.ceil(nt * g.Co / 8) * 8
             col = _im2col(dy, g, cl["dh"], cl["dw"], cl["Hc"], cl["Wc"], 1, 1, kp)
             # wperm[ci][t][co] = w[co][wt[t]][ci]
-            wsel = w.reshape(g.Co, g.T, g.Ci)[:, cl["wt"], :]
+            wsel = w.reshape(g.Co, g.T, g.Ci).index_select(1, _tap_index(cl, dev))
             wperm = wsel.permute(2, 1, 0).reshape(g.Ci, nt * g.Co)
             if kp != nt * g.Co:
                 wperm = F.pad(wperm, (0, kp - nt * g.Co))

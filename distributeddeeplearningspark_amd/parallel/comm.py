@@ -36,14 +36,30 @@ class ProcessGroup:
             else:
                 dist.barrier(group=self.group)
 
+    @property
+    def host_staged(self) -> bool:
+        """GPU tensors over gloo (replicas co-located on one GPU): collectives go through host memory."""
+        return self.backend == "gloo" and self.device.type == "cuda"
+
     def all_reduce_(self, t: torch.Tensor, op=dist.ReduceOp.SUM, async_op=False):
         if not self.distributed:
             return None
+        if self.host_staged and t.is_cuda:
+            h = t.cpu()
+            dist.all_reduce(h, op=op, group=self.group)
+            t.copy_(h)
+            return _DoneWork() if async_op else None
         return dist.all_reduce(t, op=op, group=self.group, async_op=async_op)
 
     def broadcast_(self, t: torch.Tensor, src: int = 0):
-        if self.distributed:
-            dist.broadcast(t, src, group=self.group)
+        if not self.distributed:
+            return
+        if self.host_staged and t.is_cuda:
+            h = t.cpu()
+            dist.broadcast(h, src, group=self.group)
+            t.copy_(h)
+            return
+        dist.broadcast(t, src, group=self.group)
 
     def all_gather_object(self, obj):
         if not self.distributed:
@@ -72,6 +88,13 @@ class ProcessGroup:
                 dist.destroy_process_group()
             except Exception:
                 pass
+
+
+class _DoneWork:
+    """Completed-work handle for host-staged (synchronous) collectives."""
+
+    def wait(self):
+        return True
 
 
 _DEFAULT: ProcessGroup | None = None

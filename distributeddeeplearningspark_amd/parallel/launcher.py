@@ -36,16 +36,32 @@ def _gpu_count() -> int:
         return 0
 
 
+def workers_per_gpu() -> int:
+    """Replicas allowed on one MI355X (``DDL_WORKERS_PER_GPU``, the analog of
+    ``spark.executor.cores`` per executor).  Default 1: one worker per GPU."""
+    return max(1, int(os.environ.get("DDL_WORKERS_PER_GPU", "1")))
+
+
 def plan_devices(num_workers: int, device: str | None = None) -> list[str]:
     if device is None:
         device = os.environ.get("DDL_DEVICE", "auto")
     n = _gpu_count()
     if device == "cpu" or (device == "auto" and n == 0):
         return ["cpu"] * num_workers
-    if num_workers > n:
-        raise ValueError(f"{num_workers} workers requested but only {n} GPUs: one worker per MI355X "
-                         "(pass device='cpu' to run the workers on CPU executors)")
-    return [f"cuda:{i}" for i in range(num_workers)]
+    wpg = workers_per_gpu()
+    if num_workers > n * wpg:
+        raise ValueError(f"{num_workers} workers requested but only {n} GPUs x {wpg} workers per GPU: one worker "
+                         "per MI355X by default (set DDL_WORKERS_PER_GPU to co-locate small replicas, or pass "
+                         "device='cpu' to run the workers on CPU executors)")
+    # ranks fill GPUs round-robin so co-located replicas are spread as evenly as possible
+    return [f"cuda:{i % n}" for i in range(num_workers)]
+
+
+def backend_for(devices: list[str]) -> str | None:
+    """RCCL needs one rank per GPU; co-located replicas talk over gloo (host-staged)."""
+    if devices[0] == "cpu":
+        return "gloo"
+    return "gloo" if len(set(devices)) < len(devices) else None
 
 
 def _child_main(payload_path: str, result_path: str):
@@ -53,14 +69,14 @@ def _child_main(payload_path: str, result_path: str):
     import pickle
 
     with open(payload_path, "rb") as f:
-        fn, rank, world, port, device, args, threads = pickle.load(f)
+        fn, rank, world, port, device, backend, args, threads = pickle.load(f)
     try:
         import torch
 
         torch.set_num_threads(max(1, threads))
         from .comm import init_process_group
 
-        pg = init_process_group(rank, world, "127.0.0.1", port, device=device, timeout_s=600.0)
+        pg = init_process_group(rank, world, "127.0.0.1", port, device=device, backend=backend, timeout_s=600.0)
         res = fn(rank, world, pg, *args)
         out = ("ok", res)
         pg.shutdown()
@@ -128,6 +144,7 @@ def _run_once(fn, num_workers, args_per_rank, device, timeout_s, attempt):
     import tempfile
 
     port = free_port()
+    backend = backend_for(devices)
     threads = max(1, (os.cpu_count() or 2) // num_workers)
     tmpdir = tempfile.mkdtemp(prefix="ddl_workers_")
     procs, res_paths = [], []
@@ -145,7 +162,7 @@ def _run_once(fn, num_workers, args_per_rank, device, timeout_s, attempt):
     for r in range(num_workers):
         pp, rp = os.path.join(tmpdir, f"in{r}.pkl"), os.path.join(tmpdir, f"out{r}.pkl")
         with open(pp, "wb") as f:
-            pickle.dump((fn, r, num_workers, port, devices[r], args_per_rank[r], threads), f,
+            pickle.dump((fn, r, num_workers, port, devices[r], backend, args_per_rank[r], threads), f,
                         protocol=pickle.HIGHEST_PROTOCOL)
         procs.append(subprocess.Popen([sys.executable, "-m", "distributeddeeplearningspark_amd.parallel.launcher",
                                        pp, rp], env=env))

@@ -68,6 +68,8 @@ class _Worker:
         self.commits_all = [st // self.k for st in self.steps_all]
         self.rounds = max(self.commits_all) if self.commits_all else 0
         self.history: list[float] = []
+        self._step = None
+        self._hist_dev, self._hist_n = None, 0
 
     @property
     def arena(self):
@@ -82,6 +84,38 @@ class _Worker:
 
     def num_updates(self) -> int:
         return int(sum(self.commits_all))
+
+    # ---------------------------------------------------------------- one mini-batch
+    def train_batch(self, xb, yb):
+        """One worker-local optimizer step.  On a GPU the step is a replayed hipGraph
+        (``models/step.py``) and the loss stays on the device until ``losses()``."""
+        if self._step is None:
+            from .models.step import CompiledTrainStep
+
+            self._step = CompiledTrainStep(self.model)
+        m = self.model
+        if m.optimizer.arena is not m.arena:
+            m.optimizer.bind(m.arena)
+        self._record(self._step(m.to_input(xb), m.to_target(yb)))
+
+    def _record(self, loss):
+        if loss.is_cuda:
+            if self._hist_dev is None or self._hist_n == self._hist_dev.numel():
+                grown = torch.empty(max(1024, 2 * self._hist_n), dtype=torch.float32, device=loss.device)
+                if self._hist_dev is not None:
+                    grown[: self._hist_n].copy_(self._hist_dev)
+                self._hist_dev = grown
+            self._hist_dev[self._hist_n].copy_(loss)
+            self._hist_n += 1
+        else:
+            self.history.append(float(loss))
+
+    def losses(self) -> list[float]:
+        """Per-batch loss history (one device->host transfer for the whole run)."""
+        if self._hist_dev is not None and self._hist_n:
+            self.history.extend(self._hist_dev[: self._hist_n].tolist())
+            self._hist_n = 0
+        return self.history
 
     def run(self, X, Y):
         raise NotImplementedError
@@ -135,7 +169,7 @@ class _CommitWorker(_Worker):
             if it <= it0:  # resumed: these batches were consumed before the checkpoint
                 continue
             self._tick(it)
-            self.history.append(self.model.train_on_batch(xb, yb))
+            self.train_batch(xb, yb)
             if it % self.k == 0 and rnd < self.rounds:
                 self.commit(center, rnd)
                 rnd += 1
@@ -212,7 +246,7 @@ class _AsyncPSWorker(_Worker):
             anchor = pull()
             it = 0
             for xb, yb in self.batches(X, Y):
-                self.history.append(self.model.train_on_batch(xb, yb))
+                self.train_batch(xb, yb)
                 it += 1
                 if it % k:
                     continue
@@ -267,7 +301,7 @@ class _AveragingWorker(_Worker):
 
     def run(self, X, Y):
         for xb, yb in self.batches(X, Y):
-            self.history.append(self.model.train_on_batch(xb, yb))
+            self.train_batch(xb, yb)
         W = self.arena.master.detach()
         with torch.no_grad():
             if self.pg.distributed:
@@ -283,7 +317,7 @@ class _EnsembleWorker(_Worker):
 
     def run(self, X, Y):
         for xb, yb in self.batches(X, Y):
-            self.history.append(self.model.train_on_batch(xb, yb))
+            self.train_batch(xb, yb)
         return self.arena.master.detach().clone()
 
 
@@ -312,7 +346,7 @@ class _SyncDPWorker(_Worker):
                 continue
             self._tick(it)
             xb, yb = self.model.to_input(xb), self.model.to_target(yb)
-            self.history.append(float(ddp.train_step(xb, yb)))
+            self._record(ddp.train_step(xb, yb).float())
             self._maybe_checkpoint(it, it)  # every `checkpoint_every` steps (with optimizer state)
         return self.arena.master.detach().clone()
 
@@ -352,7 +386,7 @@ def _train_worker(rank, world, pg, cfg, blob, X, Y, sizes):
             w.watchdog.stop()
     if model.device.type == "cuda":
         torch.cuda.synchronize(model.device)
-    out = {"rank": rank, "history": w.history, "num_updates": w.num_updates(), "time": time.time() - t0}
+    out = {"rank": rank, "history": w.losses(), "num_updates": w.num_updates(), "time": time.time() - t0}
     if rank == 0 or cfg["algorithm"] == "ensemble":
         out["flat"] = final.cpu().numpy().copy()
         out["states"] = get_states(model)

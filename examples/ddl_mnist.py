@@ -65,7 +65,11 @@ def main():
     ap.add_argument("--train-rows", type=int, default=4096)
     ap.add_argument("--test-rows", type=int, default=1024)
     ap.add_argument("--device", default="auto")
+    ap.add_argument("--workers-per-gpu", type=int, default=None,
+                    help="co-locate replicas on one MI355X (the reference's 8 workers on a smaller node)")
     args = ap.parse_args()
+    if args.workers_per_gpu:
+        os.environ["DDL_WORKERS_PER_GPU"] = str(args.workers_per_gpu)
 
     num_workers = args.executors * args.processes  # A4: workers = executors x processes
     print("Number of desired executors: " + str(args.executors))

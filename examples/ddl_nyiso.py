@@ -12,6 +12,7 @@ talking to a socket parameter server.
 from __future__ import annotations
 
 import argparse
+import json
 import datetime as dt
 import os
 import sys
@@ -98,7 +99,11 @@ def main():
     ap.add_argument("--epochs", type=int, default=20)
     ap.add_argument("--device", default="auto")
     ap.add_argument("--csv", default="/tmp/ddl_nyiso_synthetic.csv")
+    ap.add_argument("--workers-per-gpu", type=int, default=None,
+                    help="co-locate replicas on one MI355X (the reference's 4 workers on a 1-GPU box)")
     a = ap.parse_args()
+    if a.workers_per_gpu:
+        os.environ["DDL_WORKERS_PER_GPU"] = str(a.workers_per_gpu)
     nyiso_like().to_csv(a.csv, index=False)
     conf = SparkConf().set("spark.app.name", "ddl_nyiso").set("spark.master", f"local[{a.workers}]")
     conf.set("spark.executor.cores", 1).set("spark.executor.instances", a.workers)
@@ -110,7 +115,7 @@ def main():
     for name, model, opt in (("GRU", gru_regressor(N_UNITS), "adagrad"), ("LSTM", lstm_regressor(N_UNITS), "adam")):
         tr, mape = run(model, opt, df_train, df_test, omin, omax, a.workers, a.epochs, a.device)
         res[name] = {"updates": tr.parameter_server.num_updates, "time_s": tr.get_training_time(), "mape": mape}
-    print(res)
+    print(json.dumps({"workflow": "ddl_nyiso", "workers": a.workers, "epochs": a.epochs, "results": res}))
 
 
 if __name__ == "__main__":
