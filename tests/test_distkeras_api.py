@@ -248,6 +248,7 @@ def test_native_param_server_protocol():
         b = ParameterServerClient(ps.port, 1, 6)
         assert torch.equal(a.pull(), init) and a.last_update == 0
         a.commit(torch.ones(6))
+        a.pull()  # commits are fire-and-forget (as in dist-keras); a pull on the same connection orders them
         b.commit(torch.full((6,), 2.0))
         assert torch.equal(b.pull(), init + 3) and b.last_update == 2
         a.close(), b.close()
@@ -258,6 +259,7 @@ def test_native_param_server_protocol():
         a.pull(), b.pull()  # both at update 0
         a.commit(torch.ones(4))  # staleness 0 -> +1
         b.commit(torch.ones(4))  # staleness 1 -> +1/2
+        a.pull(), b.pull()  # both commits applied (whichever order the server saw them in, the sum is 1.5)
         np.testing.assert_allclose(ps.center().numpy(), 1.5)
         a.close(), b.close()
 
