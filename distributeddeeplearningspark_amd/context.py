@@ -99,6 +99,23 @@ class SparkContext:
         self._stopped = False
         with SparkContext._lock:
             SparkContext._active = self
+        if str(self._conf.get("spark.ddl.prestartExecutors", "false")).lower() == "true":
+            self.start_executors()
+
+    def start_executors(self, device: str | None = None):
+        """Start the executor processes now (``num_executors x num_processes`` of them, one
+        per MI355X or co-located per ``DDL_WORKERS_PER_GPU``); they import torch, initialise
+        HIP and join the process group in the background while the driver runs the ETL, as
+        Spark executors are up before a job is submitted.  Trainers pick the pool up."""
+        from .parallel.executors import get_pool
+        from .parallel.launcher import backend_for, plan_devices
+
+        n = self.num_workers()
+        if n <= 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            return None
+        device = device or self._conf.get("spark.ddl.device") or os.environ.get("DDL_DEVICE", "auto")
+        devices = plan_devices(n, device)
+        return get_pool(devices, backend_for(devices))
 
     @classmethod
     def getOrCreate(cls, conf=None):
@@ -144,7 +161,10 @@ class SparkContext:
         return RDD([data[(i * len(data)) // n:((i + 1) * len(data)) // n] for i in range(n)], self)
 
     def stop(self):
+        from .parallel.executors import shutdown_all
+
         self._stopped = True
+        shutdown_all()  # stopping the context stops its executors (as in Spark)
         with SparkContext._lock:
             if SparkContext._active is self:
                 SparkContext._active = None

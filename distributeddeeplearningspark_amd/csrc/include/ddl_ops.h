@@ -49,6 +49,8 @@ int avgpool_global_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream
 int softmax_xent(const void* logits, int logits_bf16, const int64_t* labels, const float* target_probs,
                  float* loss_rows, void* dlogits, int B, int K, long ld, float grad_scale, float label_smoothing,
                  int ignore_index, hipStream_t s);
+// loss[0] = mean((pred - target)^2); grad = 2 (pred - target) / n  (fp32, one launch)
+int mse_fwd_bwd(const float* pred, const float* target, long n, float* loss, float* grad, hipStream_t s);
 
 // ---------------- elementwise ----------------
 int cast_f32_bf16(const float* x, void* y, long n, hipStream_t s);
@@ -128,10 +130,17 @@ int embed_bwd(const int64_t* ids, const int64_t* types, const void* ds, float* g
               int ntypes, long T, int S, int H, hipStream_t s);
 
 // ---------------- persistent recurrent cells (Keras GRU reset_after=False / LSTM, fp32) ----------------
-// xw: [B][T][G*H] input projections (incl. bias); hs/cs: [B][T+1][H]; gates: [B][T][G*H] post-activation
-int rnn_fwd(int cell, const float* xw, const float* U, float* hs, float* cs, float* gates, float* y, int B, int T,
-            int H, int rs, hipStream_t s);
-// UT = U^T [G*H][H]; dgates [B][T][G*H] = gradients of the gate pre-activations
+// xw: [B][T][G*H] input projections (incl. bias) or nullptr: then the fast path (H = 64/128,
+// I <= 8) computes x W + b in-kernel from x [B][T][I], W [I][G*H], b (nullable);
+// hs/cs: [B][T+1][H]; gates: [B][T][G*H] post-activation
+bool rnn_fast_path(int H);
+bool rnn_fuses_input(int H, int I);
+int rnn_fwd(int cell, const float* xw, const float* x, const float* W, const float* b, int I, const float* U,
+            float* hs, float* cs, float* gates, float* y, int B, int T, int H, int rs, hipStream_t s);
+// gU/gW/gb (fp32, nullable gb) += parameter gradients from dgates (one launch, atomics)
+int rnn_param_grad(int cell, const float* dg, const float* hs, const float* gates, const float* x, float* gU,
+                   float* gW, float* gb, int B, int T, int H, int I, hipStream_t s);
+// UT = U^T [G*H][H] (generic path only); dgates [B][T][G*H] = gradients of the gate pre-activations
 bool rnn_bwd_uses_ut(int H);
 int rnn_bwd(int cell, const float* dy, const float* U, const float* UT, const float* hs, const float* cs,
             const float* gates, float* dgates, int B, int T, int H, int rs, hipStream_t s);

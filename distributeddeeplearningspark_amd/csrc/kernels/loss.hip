@@ -97,4 +97,32 @@ int softmax_xent(const void* logits, int logits_bf16, const int64_t* labels, con
   return (int)hipGetLastError();
 }
 
+// Mean squared error (Keras 'mean_squared_error') forward AND backward in one sweep:
+// loss[0] = mean((p - t)^2), grad = 2 (p - t) / n.  One 1024-thread workgroup (regression
+// heads are small: the reference's Dense(1) over a batch of 32).
+__global__ __launch_bounds__(1024) void mse_kernel(const float* __restrict__ p, const float* __restrict__ t, long n,
+                                                   float* __restrict__ loss, float* __restrict__ grad) {
+  __shared__ float part[16];
+  const float inv = 1.f / (float)n;
+  float acc = 0.f;
+  for (long i = threadIdx.x; i < n; i += 1024) {
+    const float d = p[i] - t[i];
+    acc += d * d;
+    grad[i] = 2.f * d * inv;
+  }
+  acc = warp_sum(acc);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int w = 0; w < 16; ++w) s += part[w];
+    loss[0] = s * inv;
+  }
+}
+
+int mse_fwd_bwd(const float* pred, const float* target, long n, float* loss, float* grad, hipStream_t s) {
+  hipLaunchKernelGGL(mse_kernel, dim3(1), dim3(1024), 0, s, pred, target, n, loss, grad);
+  return (int)hipGetLastError();
+}
+
 }  // namespace ddl

@@ -192,11 +192,16 @@ __global__ __launch_bounds__(512) void rnn_bwd_kernel(const float* __restrict__ 
 //  backward: thread (k, js) holds U[k][js*64 .. js*64+63]  (row chunk, contiguous loads),
 //            JSP = pow2(G*H/64) lane-adjacent chunks reduced with xor-shuffles.
 // h / (r*h) / gate-gradient rows live in LDS with 64-float chunks padded to 68 floats, so the
-// lanes of a wave that read different chunks hit different banks.  Per step the only global
-// traffic is the x W + b row (prefetched at the top of the step) and the saved activations.
+// lanes of a wave that read different chunks hit different banks.
+// Every per-step global input is prefetched one step ahead into registers (its latency hides
+// behind the current step's contractions); the input projection x W + b is computed in-kernel
+// for narrow inputs (I <= 8: the reference's 25x1 load series), so a step is a pure chain of
+// LDS contractions and barriers.  Element-wise phases map one (row, unit) element per thread.
 // =============================================================================================
 constexpr int CH = 64;       // k / j chunk held in registers
 constexpr int CP = CH + 4;   // padded LDS chunk stride (floats)
+constexpr int IMAX = 8;      // widest input fused into the kernels
+constexpr int RNN_BB_FWD = 1, RNN_BB_BWD = 1;  // default rows per workgroup (H = 128), measured
 
 __device__ __forceinline__ int cpos(int col) { return (col / CH) * CP + (col % CH); }
 
@@ -206,10 +211,10 @@ template <int CELL, int H>
 constexpr int bwd_threads() { return H * (((CELL == 0 ? 3 : 4) * H / 64) <= 4 ? 4 : 8); }
 
 template <int CELL, int H, int BB_>
-__global__ __launch_bounds__((fwd_threads<CELL, H>())) void rnn_fwd_reg_kernel(const float* __restrict__ xw, const float* __restrict__ U,
-                                                           float* __restrict__ hs, float* __restrict__ cs,
-                                                           float* __restrict__ gates, float* __restrict__ y, int B,
-                                                           int T, int rs) {
+__global__ __launch_bounds__((fwd_threads<CELL, H>())) void rnn_fwd_reg_kernel(
+    const float* __restrict__ xw, const float* __restrict__ x, const float* __restrict__ W,
+    const float* __restrict__ bias, int I, const float* __restrict__ U, float* __restrict__ hs,
+    float* __restrict__ cs, float* __restrict__ gates, float* __restrict__ y, int B, int T, int rs) {
   constexpr int G = CELL == 0 ? 3 : 4;
   constexpr int GH = G * H;
   constexpr int KS = H / CH;
@@ -224,12 +229,39 @@ __global__ __launch_bounds__((fwd_threads<CELL, H>())) void rnn_fwd_reg_kernel(c
   float u[CH];
 #pragma unroll
   for (int i = 0; i < CH; ++i) u[i] = U[(long)(kh * CH + i) * GH + j];
+  float wv[IMAX], bv = 0.f;  // input-projection column j (fused path)
+#pragma unroll
+  for (int i = 0; i < IMAX; ++i) wv[i] = (!xw && i < I) ? W[(long)i * GH + j] : 0.f;
+  if (!xw && bias) bv = bias[j];
+  // x W + b of step t for my column and rows (only kh == 0 lanes consume it)
+  auto load_x = [&](int t, float* xv) {
+#pragma unroll
+    for (int r = 0; r < BB_; ++r) {
+      xv[r] = 0.f;
+      if (kh != 0 || r >= nb || t < 0) continue;
+      const long bt = (long)(b0 + r) * T + t;
+      if (xw) {
+        xv[r] = xw[bt * GH + j];
+      } else {
+        float a = bv;
+#pragma unroll
+        for (int i = 0; i < IMAX; ++i)
+          if (i < I) a += x[bt * I + i] * wv[i];
+        xv[r] = a;
+      }
+    }
+  };
   for (int i = tid; i < BB_ * HC; i += blockDim.x) (&h[0][0])[i] = (&c[0][0])[i] = 0.f;
-  for (int i = tid; i < nb * H; i += blockDim.x) {
-    const int r = i / H, k = i - r * H;
-    hs[((long)(b0 + r) * (T + 1)) * H + k] = 0.f;
-    if (CELL == 1) cs[((long)(b0 + r) * (T + 1)) * H + k] = 0.f;
+  // element owned in the state-update phase
+  const int er = tid / H, ek = tid - er * H;
+  const bool eown = er < nb;
+  const long erow = b0 + er;
+  if (eown) {
+    hs[(erow * (T + 1)) * H + ek] = 0.f;
+    if (CELL == 1) cs[(erow * (T + 1)) * H + ek] = 0.f;
   }
+  float xv[BB_];
+  load_x(0, xv);
   __syncthreads();
   auto contract = [&](float (*src)[HC], float* acc) {
 #pragma unroll
@@ -248,9 +280,8 @@ __global__ __launch_bounds__((fwd_threads<CELL, H>())) void rnn_fwd_reg_kernel(c
     }
   };
   for (int t = 0; t < T; ++t) {
-    float xv[BB_];
-#pragma unroll
-    for (int r = 0; r < BB_; ++r) xv[r] = (kh == 0 && r < nb) ? xw[((long)(b0 + r) * T + t) * GH + j] : 0.f;
+    float xn[BB_];
+    load_x(t + 1 < T ? t + 1 : -1, xn);  // prefetch the next step's projection
     float acc[BB_];
     if (CELL == 1 || j < 2 * H) {  // wave-uniform: 2H columns span whole waves
       contract(h, acc);
@@ -276,37 +307,36 @@ __global__ __launch_bounds__((fwd_threads<CELL, H>())) void rnn_fwd_reg_kernel(c
       }
       __syncthreads();
     }
-    for (int i = tid; i < nb * H; i += blockDim.x) {
-      const int r = i / H, k = i - r * H;
-      const long row = b0 + r;
+    if (eown) {
       float hn;
       if (CELL == 0) {
-        const float z = gb[r][k], hh = gb[r][2 * H + k];
-        hn = z * h[r][cpos(k)] + (1.f - z) * hh;
+        const float z = gb[er][ek], hh = gb[er][2 * H + ek];
+        hn = z * h[er][cpos(ek)] + (1.f - z) * hh;
       } else {
-        const float cn = gb[r][H + k] * c[r][cpos(k)] + gb[r][k] * gb[r][2 * H + k];
-        c[r][cpos(k)] = cn;
-        hn = gb[r][3 * H + k] * tanhf(cn);
-        cs[(row * (T + 1) + t + 1) * H + k] = cn;
+        const float cn = gb[er][H + ek] * c[er][cpos(ek)] + gb[er][ek] * gb[er][2 * H + ek];
+        c[er][cpos(ek)] = cn;
+        hn = gb[er][3 * H + ek] * tanhf(cn);
+        cs[(erow * (T + 1) + t + 1) * H + ek] = cn;
       }
-      h[r][cpos(k)] = hn;
-      hs[(row * (T + 1) + t + 1) * H + k] = hn;
-      if (rs) y[(row * T + t) * H + k] = hn;
-      else if (t == T - 1) y[row * H + k] = hn;
+      h[er][cpos(ek)] = hn;
+      hs[(erow * (T + 1) + t + 1) * H + ek] = hn;
+      if (rs) y[(erow * T + t) * H + ek] = hn;
+      else if (t == T - 1) y[erow * H + ek] = hn;
     }
     for (int i = tid; i < nb * GH; i += blockDim.x) {
       const int r = i / GH, jj = i - r * GH;
       gates[((long)(b0 + r) * T + t) * GH + jj] = gb[r][jj];
     }
+#pragma unroll
+    for (int r = 0; r < BB_; ++r) xv[r] = xn[r];
     __syncthreads();
   }
 }
 
 template <int CELL, int H, int BB_>
-__global__ __launch_bounds__((bwd_threads<CELL, H>())) void rnn_bwd_reg_kernel(const float* __restrict__ dy, const float* __restrict__ U,
-                                                           const float* __restrict__ hs, const float* __restrict__ cs,
-                                                           const float* __restrict__ gates,
-                                                           float* __restrict__ dgates, int B, int T, int rs) {
+__global__ __launch_bounds__((bwd_threads<CELL, H>())) void rnn_bwd_reg_kernel(
+    const float* __restrict__ dy, const float* __restrict__ U, const float* __restrict__ hs,
+    const float* __restrict__ cs, const float* __restrict__ gates, float* __restrict__ dgates, int B, int T, int rs) {
   constexpr int G = CELL == 0 ? 3 : 4;
   constexpr int GH = G * H;
   constexpr int JS = GH / CH;                            // column chunks
@@ -315,6 +345,8 @@ __global__ __launch_bounds__((bwd_threads<CELL, H>())) void rnn_bwd_reg_kernel(c
   __shared__ __attribute__((aligned(16))) float p[BB_][JS * CP];  // pre-activation gradients
   __shared__ float dh[BB_][H];
   __shared__ float aux[BB_][H];  // GRU: d*z direct part; LSTM: running dc
+  __shared__ float hpl[BB_][H];  // GRU: h_{t-1} and r of the step, staged for the dr phase
+  __shared__ float rgl[BB_][H];
   const int tid = threadIdx.x;
   const int k = tid / JSP, js = tid % JSP;
   const bool active = js < JS;
@@ -323,11 +355,31 @@ __global__ __launch_bounds__((bwd_threads<CELL, H>())) void rnn_bwd_reg_kernel(c
   float u[CH];
 #pragma unroll
   for (int i = 0; i < CH; i += 4) {
-    const float4 v = *reinterpret_cast<const float4*>(&U[(long)k * GH + min(js, JS - 1) * CH + i]);  // idle lanes: never used
+    const float4 v = *reinterpret_cast<const float4*>(&U[(long)k * GH + min(js, JS - 1) * CH + i]);  // idle: unused
     u[i] = v.x; u[i + 1] = v.y; u[i + 2] = v.z; u[i + 3] = v.w;
   }
   for (int i = tid; i < BB_ * H; i += blockDim.x) (&dh[0][0])[i] = (&aux[0][0])[i] = 0.f;
   for (int i = tid; i < BB_ * JS * CP; i += blockDim.x) (&p[0][0])[i] = 0.f;
+  // element owned in the element-wise phase, and its prefetched inputs
+  const int er = tid / H, ek = tid - er * H;
+  const bool eown = er < nb;
+  const long erow = b0 + er;
+  struct In { float d, g0, g1, g2, g3, hp, cn, cp; };
+  auto load_in = [&](int t, In& v) {
+    if (!eown || t < 0) return;
+    v.d = rs ? dy[(erow * T + t) * H + ek] : (t == T - 1 ? dy[erow * H + ek] : 0.f);
+    const float* g = gates + (erow * T + t) * GH;
+    v.g0 = g[ek]; v.g1 = g[H + ek]; v.g2 = g[2 * H + ek];
+    if (CELL == 1) {
+      v.g3 = g[3 * H + ek];
+      v.cn = cs[(erow * (T + 1) + t + 1) * H + ek];
+      v.cp = cs[(erow * (T + 1) + t) * H + ek];
+    } else {
+      v.hp = hs[(erow * (T + 1) + t) * H + ek];
+    }
+  };
+  In cur{}, nxt{};
+  load_in(T - 1, cur);
   __syncthreads();
   auto contract = [&](bool use, float* acc) {
 #pragma unroll
@@ -352,30 +404,26 @@ __global__ __launch_bounds__((bwd_threads<CELL, H>())) void rnn_bwd_reg_kernel(c
     }
   };
   for (int t = T - 1; t >= 0; --t) {
-    for (int i = tid; i < nb * H; i += blockDim.x) {
-      const int r = i / H, kk = i - r * H;
-      const long row = b0 + r;
-      float d = dh[r][kk];
-      if (rs) d += dy[(row * T + t) * H + kk];
-      else if (t == T - 1) d += dy[row * H + kk];
-      const float* g = gates + (row * T + t) * GH;
-      float* pr = p[r];
+    load_in(t - 1, nxt);  // prefetch the previous step's saved activations
+    if (eown) {
+      const float d = dh[er][ek] + cur.d;
+      float* pr = p[er];
       if (CELL == 0) {
-        const float hp = hs[(row * (T + 1) + t) * H + kk];
-        const float z = g[kk], hh = g[2 * H + kk];
-        pr[cpos(kk)] = d * (hp - hh) * hsig_d(z);
-        pr[cpos(2 * H + kk)] = d * (1.f - z) * (1.f - hh * hh);
-        aux[r][kk] = d * z;
+        const float z = cur.g0, hh = cur.g2;
+        pr[cpos(ek)] = d * (cur.hp - hh) * hsig_d(z);
+        pr[cpos(2 * H + ek)] = d * (1.f - z) * (1.f - hh * hh);
+        aux[er][ek] = d * z;
+        hpl[er][ek] = cur.hp;
+        rgl[er][ek] = cur.g1;
       } else {
-        const float gi = g[kk], gf = g[H + kk], gg = g[2 * H + kk], go = g[3 * H + kk];
-        const float cn = cs[(row * (T + 1) + t + 1) * H + kk], cp = cs[(row * (T + 1) + t) * H + kk];
-        const float tc = tanhf(cn);
-        const float dc = aux[r][kk] + d * go * (1.f - tc * tc);
-        pr[cpos(kk)] = dc * gg * hsig_d(gi);
-        pr[cpos(H + kk)] = dc * cp * hsig_d(gf);
-        pr[cpos(2 * H + kk)] = dc * gi * (1.f - gg * gg);
-        pr[cpos(3 * H + kk)] = d * tc * hsig_d(go);
-        aux[r][kk] = dc * gf;
+        const float gi = cur.g0, gf = cur.g1, gg = cur.g2, go = cur.g3;
+        const float tc = tanhf(cur.cn);
+        const float dc = aux[er][ek] + d * go * (1.f - tc * tc);
+        pr[cpos(ek)] = dc * gg * hsig_d(gi);
+        pr[cpos(H + ek)] = dc * cur.cp * hsig_d(gf);
+        pr[cpos(2 * H + ek)] = dc * gi * (1.f - gg * gg);
+        pr[cpos(3 * H + ek)] = d * tc * hsig_d(go);
+        aux[er][ek] = dc * gf;
       }
     }
     __syncthreads();
@@ -387,11 +435,10 @@ __global__ __launch_bounds__((bwd_threads<CELL, H>())) void rnn_bwd_reg_kernel(c
       contract(active && (ph == 0 ? js >= ZR : js < ZR), acc);
       if (js == 0) {
         if (ph == 0) {
-          for (int r = 0; r < nb; ++r) {
-            const long row = b0 + r;
-            const float hp = hs[(row * (T + 1) + t) * H + k];
-            const float rg = gates[(row * T + t) * GH + H + k];
-            p[r][cpos(H + k)] = acc[r] * hp * hsig_d(rg);
+#pragma unroll
+          for (int r = 0; r < BB_; ++r) {
+            const float rg = rgl[r][k];
+            p[r][cpos(H + k)] = acc[r] * hpl[r][k] * hsig_d(rg);
             aux[r][k] += acc[r] * rg;
           }
         } else {
@@ -405,42 +452,135 @@ __global__ __launch_bounds__((bwd_threads<CELL, H>())) void rnn_bwd_reg_kernel(c
       const int r = i / GH, jj = i - r * GH;
       dgates[((long)(b0 + r) * T + t) * GH + jj] = p[r][cpos(jj)];
     }
+    cur = nxt;
     __syncthreads();
   }
 }
 
-template <int CELL, int H, int BB_>
-int launch_fwd_reg(const float* xw, const float* U, float* hs, float* cs, float* gates, float* y, int B, int T, int rs,
-                   hipStream_t s) {
+// Parameter gradients of a recurrent layer in ONE launch, accumulated (fp32 atomics) straight
+// into the gradient arena:  rows m < H      : gU[m][j] += sum_bt A(bt,m,j) dg[bt][j]
+//                           rows H <= m < H+I: gW[m-H][j] += sum_bt x[bt][m-H] dg[bt][j]
+//                           row m = H+I      : gb[j] += sum_bt dg[bt][j]
+// with A = h_{t-1}[m] (GRU candidate columns: r[m] * h_{t-1}[m]).  Tile 64(m) x 64(j) over a
+// chunk of PG_BT (b,t) rows staged in LDS; 256 threads x 4x4 outputs.
+constexpr int PG_BT = 128;
+
+template <int CELL>
+__global__ __launch_bounds__(256) void rnn_param_grad_kernel(const float* __restrict__ dg, const float* __restrict__ hs,
+                                                             const float* __restrict__ gates,
+                                                             const float* __restrict__ x, float* __restrict__ gU,
+                                                             float* __restrict__ gW, float* __restrict__ gb, int B,
+                                                             int T, int H, int I) {
   constexpr int G = CELL == 0 ? 3 : 4;
+  const int GH = G * H;
+  const int M = H + I + (gb ? 1 : 0);
+  const long BT = (long)B * T;
+  const int m0 = blockIdx.x * 64, j0 = blockIdx.y * 64;
+  const long bt0 = (long)blockIdx.z * PG_BT;
+  const int nbt = (int)min((long)PG_BT, BT - bt0);
+  __shared__ float As[PG_BT][64 + 1];
+  __shared__ float Ds[PG_BT][64 + 1];
+  const bool cand = CELL == 0 && j0 >= 2 * H;  // 2H is a multiple of 64
+  // fill: thread owns column c and rows q = q0, q0+4, ...; (b, t) advance incrementally
+  // (a runtime-T division per element would dominate the kernel)
+  const int c = threadIdx.x & 63, q0 = threadIdx.x >> 6;
+  long b = (bt0 + q0) / T, t = (bt0 + q0) - b * T;
+  for (int q = q0; q < nbt; q += 4, t += 4) {
+    while (t >= T) { t -= T; ++b; }
+    const long bt = bt0 + q;
+    const int m = m0 + c;
+    float a = 0.f;
+    if (m < H) {
+      a = hs[(b * (T + 1) + t) * H + m];
+      if (cand) a *= gates[bt * GH + H + m];
+    } else if (m < H + I) {
+      a = x[bt * I + (m - H)];
+    } else if (m < M) {
+      a = 1.f;
+    }
+    As[q][c] = a;
+    const int jj = j0 + c;
+    Ds[q][c] = jj < GH ? dg[bt * GH + jj] : 0.f;
+  }
+  __syncthreads();
+  const int tm = (threadIdx.x / 16) * 4, tj = (threadIdx.x % 16) * 4;
+  float acc[4][4] = {};
+  for (int q = 0; q < nbt; ++q) {
+    float a[4], d[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { a[i] = As[q][tm + i]; d[i] = Ds[q][tj + i]; }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int l = 0; l < 4; ++l) acc[i][l] += a[i] * d[l];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + tm + i;
+    if (m >= M) continue;
+    float* dst = m < H ? gU + (long)m * GH : (m < H + I ? gW + (long)(m - H) * GH : gb);
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      const int jj = j0 + tj + l;
+      if (jj < GH) atomicAdd(dst + jj, acc[i][l]);
+    }
+  }
+}
+
+template <int CELL, int H, int BB_>
+int launch_fwd_reg(const float* xw, const float* x, const float* W, const float* b, int I, const float* U, float* hs,
+                   float* cs, float* gates, float* y, int B, int T, int rs, hipStream_t s) {
+  constexpr int G = CELL == 0 ? 3 : 4;
+  static_assert(BB_ * H <= fwd_threads<CELL, H>(), "one state element per thread");
   const dim3 grid((B + BB_ - 1) / BB_);
-  hipLaunchKernelGGL((rnn_fwd_reg_kernel<CELL, H, BB_>), grid, dim3(G * H * (H / CH)), 0, s, xw, U, hs, cs, gates, y,
-                     B, T, rs);
+  hipLaunchKernelGGL((rnn_fwd_reg_kernel<CELL, H, BB_>), grid, dim3(G * H * (H / CH)), 0, s, xw, x, W, b, I, U, hs,
+                     cs, gates, y, B, T, rs);
   return (int)hipGetLastError();
 }
 
 template <int CELL, int H, int BB_>
 int launch_bwd_reg(const float* dy, const float* U, const float* hs, const float* cs, const float* gates,
                    float* dgates, int B, int T, int rs, hipStream_t s) {
-  constexpr int G = CELL == 0 ? 3 : 4;
-  constexpr int JS = G * H / CH;
-  constexpr int JSP = JS <= 4 ? 4 : 8;
+  static_assert(BB_ * H <= bwd_threads<CELL, H>(), "one state element per thread");
   const dim3 grid((B + BB_ - 1) / BB_);
-  hipLaunchKernelGGL((rnn_bwd_reg_kernel<CELL, H, BB_>), grid, dim3(H * JSP), 0, s, dy, U, hs, cs, gates, dgates, B,
-                     T, rs);
+  hipLaunchKernelGGL((rnn_bwd_reg_kernel<CELL, H, BB_>), grid, dim3(bwd_threads<CELL, H>()), 0, s, dy, U, hs, cs,
+                     gates, dgates, B, T, rs);
   return (int)hipGetLastError();
 }
 
 }  // namespace
 
-int rnn_fwd(int cell, const float* xw, const float* U, float* hs, float* cs, float* gates, float* y, int B, int T,
-            int H, int rs, hipStream_t s) {
-  if (H == 128)
-    return cell == 0 ? launch_fwd_reg<0, 128, 4>(xw, U, hs, cs, gates, y, B, T, rs, s)
-                     : launch_fwd_reg<1, 128, 4>(xw, U, hs, cs, gates, y, B, T, rs, s);
+bool rnn_fast_path(int H) { return H == 128 || H == 64; }
+bool rnn_fuses_input(int H, int I) { return rnn_fast_path(H) && I <= IMAX; }
+
+// batch rows per workgroup of the register-resident kernels: fewer rows = more CUs busy and
+// less VALU work per step (the recurrence is latency-bound); DDL_RNN_BB overrides (1/2/4)
+static int rnn_rows_per_wg(int dflt) {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DDL_RNN_BB");
+    v = e ? atoi(e) : 0;
+    if (v != 1 && v != 2 && v != 4) v = 0;
+  }
+  return v ? v : dflt;
+}
+
+int rnn_fwd(int cell, const float* xw, const float* x, const float* W, const float* b, int I, const float* U,
+            float* hs, float* cs, float* gates, float* y, int B, int T, int H, int rs, hipStream_t s) {
+  if (H == 128) {
+    const int bb = rnn_rows_per_wg(RNN_BB_FWD);
+#define DDL_RNN_FWD(BBV)                                                                                    \
+  return cell == 0 ? launch_fwd_reg<0, 128, BBV>(xw, x, W, b, I, U, hs, cs, gates, y, B, T, rs, s)           \
+                   : launch_fwd_reg<1, 128, BBV>(xw, x, W, b, I, U, hs, cs, gates, y, B, T, rs, s)
+    if (bb == 1) DDL_RNN_FWD(1);
+    if (bb == 2) DDL_RNN_FWD(2);
+    DDL_RNN_FWD(4);
+#undef DDL_RNN_FWD
+  }
   if (H == 64)
-    return cell == 0 ? launch_fwd_reg<0, 64, 2>(xw, U, hs, cs, gates, y, B, T, rs, s)
-                     : launch_fwd_reg<1, 64, 2>(xw, U, hs, cs, gates, y, B, T, rs, s);
+    return cell == 0 ? launch_fwd_reg<0, 64, 2>(xw, x, W, b, I, U, hs, cs, gates, y, B, T, rs, s)
+                     : launch_fwd_reg<1, 64, 2>(xw, x, W, b, I, U, hs, cs, gates, y, B, T, rs, s);
+  if (!xw) return (int)hipErrorInvalidValue;  // generic kernels need the projection precomputed
   const int G = cell == 0 ? 3 : 4;
   const size_t lds = sizeof(float) * (2 * BB * H + BB * G * H);
   const int threads = std::min(512, ((G * H + 63) / 64) * 64);
@@ -452,13 +592,33 @@ int rnn_fwd(int cell, const float* xw, const float* U, float* hs, float* cs, flo
   return (int)hipGetLastError();
 }
 
-bool rnn_bwd_uses_ut(int H) { return H != 128 && H != 64; }
+bool rnn_bwd_uses_ut(int H) { return !rnn_fast_path(H); }
+
+int rnn_param_grad(int cell, const float* dg, const float* hs, const float* gates, const float* x, float* gU,
+                   float* gW, float* gb, int B, int T, int H, int I, hipStream_t s) {
+  const int G = cell == 0 ? 3 : 4;
+  const int M = H + I + (gb ? 1 : 0);
+  const long BT = (long)B * T;
+  const dim3 grid((M + 63) / 64, (G * H + 63) / 64, (unsigned)((BT + PG_BT - 1) / PG_BT));
+  if (cell == 0)
+    hipLaunchKernelGGL(rnn_param_grad_kernel<0>, grid, dim3(256), 0, s, dg, hs, gates, x, gU, gW, gb, B, T, H, I);
+  else
+    hipLaunchKernelGGL(rnn_param_grad_kernel<1>, grid, dim3(256), 0, s, dg, hs, gates, x, gU, gW, gb, B, T, H, I);
+  return (int)hipGetLastError();
+}
 
 int rnn_bwd(int cell, const float* dy, const float* U, const float* UT, const float* hs, const float* cs,
             const float* gates, float* dgates, int B, int T, int H, int rs, hipStream_t s) {
-  if (H == 128)
-    return cell == 0 ? launch_bwd_reg<0, 128, 2>(dy, U, hs, cs, gates, dgates, B, T, rs, s)
-                     : launch_bwd_reg<1, 128, 4>(dy, U, hs, cs, gates, dgates, B, T, rs, s);
+  if (H == 128) {
+    const int bb = rnn_rows_per_wg(RNN_BB_BWD);
+#define DDL_RNN_BWD(BBV)                                                                                    \
+  return cell == 0 ? launch_bwd_reg<0, 128, BBV>(dy, U, hs, cs, gates, dgates, B, T, rs, s)                   \
+                   : launch_bwd_reg<1, 128, BBV>(dy, U, hs, cs, gates, dgates, B, T, rs, s)
+    if (bb == 1) DDL_RNN_BWD(1);
+    if (bb == 4) DDL_RNN_BWD(4);
+    DDL_RNN_BWD(2);
+#undef DDL_RNN_BWD
+  }
   if (H == 64)
     return cell == 0 ? launch_bwd_reg<0, 64, 2>(dy, U, hs, cs, gates, dgates, B, T, rs, s)
                      : launch_bwd_reg<1, 64, 2>(dy, U, hs, cs, gates, dgates, B, T, rs, s);

@@ -275,6 +275,14 @@ void adam_step_(const at::Tensor& w, const at::Tensor& g, const at::Tensor& m, c
                    w.numel(), (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (int)mode, (float)bc1,
                    (float)bc2, (float)gscale, optr<float>(tstep), cur_stream()));
 }
+void mse_fwd_bwd_(const at::Tensor& pred, const at::Tensor& target, const at::Tensor& loss, const at::Tensor& grad) {
+  F32(pred); F32(target); F32(loss); F32(grad);
+  CK(pred.is_cuda() && pred.numel() == target.numel() && grad.numel() == pred.numel() && loss.numel() == 1,
+     "mse: pred / target / grad sizes");
+  at::DeviceGuard gd(pred.device());
+  HIP_OK(mse_fwd_bwd(pred.data_ptr<float>(), target.data_ptr<float>(), pred.numel(), loss.data_ptr<float>(),
+                     grad.data_ptr<float>(), cur_stream()));
+}
 void step_tick_(const at::Tensor& t) {
   F32(t);
   CK(t.is_cuda() && t.numel() == 1, "step counter: one fp32 element on the GPU");
@@ -337,6 +345,7 @@ void register_ops(py::module& m) {
         py::arg("w16"), py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("mode"),
         py::arg("bc1"), py::arg("bc2"), py::arg("gscale"), py::arg("tstep") = py::none());
   m.def("step_tick", &step_tick_);
+  m.def("mse_fwd_bwd", &mse_fwd_bwd_);
   m.def("adagrad_step", &adagrad_step_);
   m.def("rmsprop_step", &rmsprop_step_);
   m.def("sumsq", &sumsq_);

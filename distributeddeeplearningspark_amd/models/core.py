@@ -215,9 +215,9 @@ class Model(Layer):
         if device is None:
             device = "cuda" if torch.cuda.is_available() else "cpu"
         device = torch.device(device)
-        if dtype is None:
-            dtype = torch.bfloat16 if device.type == "cuda" else torch.float32
         self.build_model()
+        if dtype is None:
+            dtype = torch.bfloat16 if device.type == "cuda" and not self._keeps_fp32() else torch.float32
         old = None
         if self.arena is not None:
             old = self.arena.master.detach().cpu()
@@ -230,6 +230,14 @@ class Model(Layer):
         if self.optimizer is not None:
             self.optimizer.bind(self.arena)
         return self
+
+    def _keeps_fp32(self) -> bool:
+        """Recurrent models train in fp32 on the GPU too: they are the reference's Keras
+        regressors (fp32 GRU/LSTM, ``ddl_nyiso_aztk.py:201-203``), tiny and latency-bound, so
+        bf16 would cost accuracy (MAPE) without buying any speed."""
+        from .layers import _Recurrent
+
+        return any(isinstance(l, _Recurrent) for l in self.all_layers())
 
     def _ensure_placed(self):
         if self.arena is None:

@@ -27,6 +27,15 @@ class _LinearFn(torch.autograd.Function):
         ctx.native = use_native(x)
         ctx.xshape = x.shape
         ctx.needs_dx = ctx.needs_input_grad[0]
+        ctx.fp32 = ctx.native and x.dtype == torch.float32
+        if ctx.fp32:  # fp32 models (the reference's Keras regressors): a plain library GEMM
+            x2 = x.reshape(-1, x.shape[-1])
+            y = torch.addmm(b, x2, w.t()) if b is not None else x2 @ w.t()
+            if relu:
+                y = torch.relu_(y)
+            ctx.gw, ctx.gb = gw, gb
+            ctx.save_for_backward(x2, w, y if relu else None)
+            return y.view(*x.shape[:-1], w.shape[0])
         if ctx.native:
             x2 = x.reshape(-1, x.shape[-1]).contiguous()
             K, N = x2.shape[1], w.shape[0]
@@ -51,7 +60,18 @@ class _LinearFn(torch.autograd.Function):
     def backward(ctx, dy):
         relu, hook = ctx.cfg
         dx = None
-        if ctx.native:
+        if ctx.fp32:
+            x2, w, y = ctx.saved_tensors
+            d2 = dy.reshape(-1, w.shape[0])
+            if relu:
+                d2 = d2 * (y > 0)
+            if ctx.gb is not None:
+                ctx.gb.add_(d2.sum(0))
+            if ctx.gw is not None:
+                ctx.gw.addmm_(d2.t(), x2)
+            if ctx.needs_dx:
+                dx = (d2 @ w).view(ctx.xshape)
+        elif ctx.native:
             x2, w, y = ctx.saved_tensors
             gw, gb = ctx.gw, ctx.gb
             K, N, Kp, Np = ctx.pad

@@ -56,7 +56,28 @@ def softmax_cross_entropy(logits, labels=None, probs=None, label_smoothing=0.0, 
     return _SoftmaxXentFn.apply(logits, labels, probs, float(label_smoothing), int(ignore_index))
 
 
+class _MSEFn(torch.autograd.Function):
+    """One HIP launch computes the loss and stores d loss / d pred (backward = one scale)."""
+
+    @staticmethod
+    def forward(ctx, pred, target):
+        p = pred.contiguous()
+        loss = torch.empty((), dtype=torch.float32, device=p.device)
+        grad = torch.empty_like(p)
+        C().mse_fwd_bwd(p, target.contiguous(), loss, grad)
+        ctx.save_for_backward(grad)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (grad,) = ctx.saved_tensors
+        return grad * g, None
+
+
 def mean_squared_error(pred, target):
+    if use_native(pred) and pred.dtype == torch.float32 and target.dtype == torch.float32 \
+            and pred.shape == target.shape:
+        return _MSEFn.apply(pred, target)
     return ((pred.float() - target.float()) ** 2).mean()
 
 

@@ -78,6 +78,7 @@ class _RecurrentFn(torch.autograd.Function):
             y, saved = C().rnn_fwd(cell, xf.contiguous(), Wf.contiguous(), Uf.contiguous(), bf, rs)
             ctx.native = True
             ctx.grads = (gW, gU, gb)
+            ctx.needs_dx = ctx.needs_input_grad[0]
             ctx.save_for_backward(xf, Wf, Uf, bf, *saved)
             return y.to(dt)
         ctx.native = False
@@ -94,7 +95,10 @@ class _RecurrentFn(torch.autograd.Function):
         xf, Wf, Uf, bf = saved[:4]
         gW, gU, gb = ctx.grads
         if ctx.native:
-            dx, dW, dU, db = C().rnn_bwd(cell, dy.float().contiguous(), xf, Wf, Uf, bf, rs, list(saved[4:]))
+            # fast path: dW/dU/db are accumulated into the fp32 arena slices in-kernel (None here)
+            fp32 = lambda t: t if t is not None and t.dtype == torch.float32 and t.is_contiguous() else None
+            dx, dW, dU, db = C().rnn_bwd(cell, dy.float().contiguous(), xf, Wf, Uf, bf, rs, list(saved[4:]),
+                                         fp32(gW), fp32(gU), fp32(gb), ctx.needs_dx)
         else:
             fn = lambda xx, ww, uu, bb: recurrent_ref(cell, xx, ww, uu, bb, rs, act, ract)
             dx, dW, dU, db = ref_grads(fn, [xf, Wf, Uf, bf], dy.float())

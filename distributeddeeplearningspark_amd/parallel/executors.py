@@ -1,0 +1,291 @@
+"""Long-lived executor processes — the Spark executor analog.
+
+In the reference, executors are JVM processes that YARN/AZTK start with the session
+(``ddl_nyiso_hdi.ipynb:102-125``: 2 executors x 2 cores) and every ``trainer.train(df)``
+ships tasks to those already-running processes (``mapPartitionsWithIndex``).
+Here an :class:`ExecutorPool` is N worker interpreters (one per data-parallel replica,
+bound to one MI355X each, or co-located per ``DDL_WORKERS_PER_GPU``) that import torch,
+initialise HIP and join ONE process group (RCCL over xGMI, or gloo) once, then run any
+number of tasks.  The driver talks to them over an authenticated local socket
+(``multiprocessing.connection``); results come back pickled.
+
+* Pools are cached by (world size, devices, backend) and reused by every trainer call, so
+  ``get_training_time()`` measures training, not interpreter start-up — as in Spark, where
+  the executors are up before the job is submitted.  ``SparkContext`` can pre-start the
+  pool (``spark.ddl.prestartExecutors=true``) so it warms up while the driver runs the ETL.
+* ``DDL_*`` environment variables of the driver are forwarded with every task (fault
+  injection, restart counters and knobs set after the pool started still apply).
+* Any task failure, worker death or timeout tears the whole pool down (a collective of
+  the surviving ranks may be stuck); the launcher's restart logic then starts a new one.
+* ``DDL_EXECUTOR_POOL=0`` disables caching (a fresh pool per call, stopped afterwards).
+"""
+from __future__ import annotations
+
+import atexit
+import os
+import pickle
+import secrets
+import subprocess
+import sys
+import threading
+import time
+import traceback
+from multiprocessing.connection import Client, Listener
+
+_POOLS: dict = {}
+_LOCK = threading.Lock()
+
+
+class PoolFailure(RuntimeError):
+    def __init__(self, msg, short):
+        super().__init__(msg)
+        self.short = short
+
+
+def _ddl_env() -> dict:
+    return {k: v for k, v in os.environ.items() if k.startswith("DDL_")}
+
+
+class ExecutorPool:
+    def __init__(self, devices: list[str], backend: str | None, start_timeout_s: float = 600.0):
+        from .launcher import free_port
+
+        self.devices = list(devices)
+        self.world = len(devices)
+        self.backend = backend
+        self.key = pool_key(devices, backend)
+        self._authkey = secrets.token_bytes(16)
+        self._listener = Listener(("127.0.0.1", 0), authkey=self._authkey)
+        self._conns: dict[int, object] = {}
+        self._accept_err = None
+        self.closed = False
+        self.tasks_run = 0
+        threads = max(1, (os.cpu_count() or 2) // self.world)
+        pg_port = free_port()
+        env = dict(os.environ)
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        env["PYTHONPATH"] = os.pathsep.join([root] + ([env["PYTHONPATH"]] if env.get("PYTHONPATH") else []))
+        host, port = self._listener.address
+        self.procs = []
+        for r, dev in enumerate(self.devices):
+            cmd = [sys.executable, "-m", "distributeddeeplearningspark_amd.parallel.executors", str(port),
+                   self._authkey.hex(), str(r), str(self.world), str(pg_port), dev, backend or "", str(threads)]
+            self.procs.append(subprocess.Popen(cmd, env=env))
+        self._acceptor = threading.Thread(target=self._accept_all, daemon=True)
+        self._acceptor.start()
+        self._start_deadline = time.time() + start_timeout_s
+
+    # ------------------------------------------------------------------ start-up
+    def _accept_all(self):
+        try:
+            while len(self._conns) < self.world:
+                c = self._listener.accept()
+                kind, rank = c.recv()
+                assert kind == "hello"
+                self._conns[int(rank)] = c
+        except BaseException as e:  # listener closed during shutdown, or a bad peer
+            self._accept_err = e
+
+    def wait_ready(self):
+        while True:
+            conns = list(self._conns.values())  # filled by the acceptor thread
+            ready = sum(1 for c in conns if c.poll(0)) if len(conns) == self.world else 0
+            if ready == self.world:
+                for r in range(self.world):
+                    kind, payload = self._conns[r].recv()
+                    if kind != "ready":
+                        self.shutdown(force=True)
+                        raise PoolFailure(f"executor {r} failed to start:\n{payload}", f"executor {r} start failed")
+                return self
+            for r, p in enumerate(self.procs):
+                if p.poll() is not None:
+                    self.shutdown(force=True)
+                    raise PoolFailure(f"executor {r} exited with code {p.returncode} during start-up",
+                                      f"executor {r} died")
+            if time.time() > self._start_deadline:
+                self.shutdown(force=True)
+                raise PoolFailure("executors did not start in time", "executor start timeout")
+            time.sleep(0.02)
+
+    # ------------------------------------------------------------------ tasks
+    def run(self, fn, args_per_rank, timeout_s: float = 3600.0, attempt: int = 0):
+        if getattr(self, "_ready", False) is False:
+            self.wait_ready()
+            self._ready = True
+        env = _ddl_env()
+        env["DDL_RESTART_COUNT"] = str(attempt)
+        paths = []
+        try:  # the task function's own directory, so test / script modules unpickle in the executor
+            import inspect
+
+            paths.append(os.path.dirname(os.path.abspath(inspect.getfile(fn))))
+        except (TypeError, OSError):
+            pass
+        for r in range(self.world):
+            payload = pickle.dumps((fn, args_per_rank[r]), protocol=pickle.HIGHEST_PROTOCOL)
+            self._conns[r].send(("task", paths, payload, env))
+        results, errors = {}, {}
+        deadline = time.time() + timeout_s
+        while len(results) + len(errors) < self.world:
+            progressed = False
+            for r in range(self.world):
+                if r in results or r in errors:
+                    continue
+                c = self._conns[r]
+                try:
+                    has = c.poll(0)
+                except (EOFError, OSError):
+                    has = False
+                if has:
+                    try:
+                        status, payload = c.recv()
+                    except (EOFError, OSError):
+                        status, payload = "error", f"executor {r} connection lost"
+                    (results if status == "ok" else errors)[r] = payload
+                    progressed = True
+                elif self.procs[r].poll() is not None:
+                    errors[r] = f"worker {r} exited with code {self.procs[r].returncode} without a result"
+                    progressed = True
+            if errors:
+                break
+            if time.time() > deadline:
+                self.shutdown(force=True)
+                raise TimeoutError(f"workers did not finish within {timeout_s}s")
+            if not progressed:
+                time.sleep(0.002)
+        if errors:
+            self.shutdown(force=True)
+            r = sorted(errors)[0]
+            raise PoolFailure(f"worker {r} failed:\n{errors[r]}", f"worker {r} failed")
+        self.tasks_run += 1
+        return [results[r] for r in range(self.world)]
+
+    # ------------------------------------------------------------------ teardown
+    def shutdown(self, force: bool = False):
+        if self.closed:
+            return
+        self.closed = True
+        with _LOCK:
+            if _POOLS.get(self.key) is self:
+                del _POOLS[self.key]
+        if not force:
+            for c in self._conns.values():
+                try:
+                    c.send(("stop",))
+                except Exception:
+                    pass
+        deadline = time.time() + (10.0 if not force else 0.0)
+        for p in self.procs:
+            try:
+                p.wait(timeout=max(0.0, deadline - time.time()))
+            except subprocess.TimeoutExpired:
+                pass
+        for p in self.procs:
+            if p.poll() is None:
+                p.kill()
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    pass
+        for c in self._conns.values():
+            try:
+                c.close()
+            except Exception:
+                pass
+        try:
+            self._listener.close()
+        except Exception:
+            pass
+
+
+def pool_key(devices, backend):
+    return (len(devices), tuple(devices), backend)
+
+
+def get_pool(devices: list[str], backend: str | None) -> ExecutorPool:
+    """The cached pool for this topology (started if needed)."""
+    key = pool_key(devices, backend)
+    with _LOCK:
+        pool = _POOLS.get(key)
+        if pool is not None and not pool.closed and all(p.poll() is None for p in pool.procs):
+            return pool
+        if pool is not None:
+            del _POOLS[key]
+    if pool is not None:
+        pool.shutdown(force=True)
+    # one topology at a time: other cached pools hold GPUs / ports that this one may need
+    shutdown_all()
+    pool = ExecutorPool(devices, backend)
+    with _LOCK:
+        _POOLS[key] = pool
+    return pool
+
+
+def pooling_enabled() -> bool:
+    return os.environ.get("DDL_EXECUTOR_POOL", "1") != "0"
+
+
+def shutdown_all():
+    with _LOCK:
+        pools = list(_POOLS.values())
+    for p in pools:
+        p.shutdown()
+
+
+atexit.register(shutdown_all)
+
+
+# ============================================================================ executor side
+def _executor_main(port, authkey_hex, rank, world, pg_port, device, backend, threads):
+    conn = Client(("127.0.0.1", int(port)), authkey=bytes.fromhex(authkey_hex))
+    conn.send(("hello", int(rank)))
+    pg = None
+    try:
+        import torch
+
+        torch.set_num_threads(max(1, int(threads)))
+        from .comm import init_process_group
+
+        pg = init_process_group(int(rank), int(world), "127.0.0.1", int(pg_port), device=device,
+                                backend=backend or None, timeout_s=600.0)
+        conn.send(("ready", None))
+    except BaseException:
+        conn.send(("error", traceback.format_exc()))
+        return 1
+    base_env = {k: v for k, v in os.environ.items() if not k.startswith("DDL_")}
+    while True:
+        try:
+            msg = conn.recv()
+        except (EOFError, OSError):
+            break  # driver went away
+        if msg[0] == "stop":
+            break
+        _, paths, payload, env = msg
+        for k in [k for k in os.environ if k.startswith("DDL_")]:
+            del os.environ[k]
+        os.environ.update(env)
+        os.environ.update({k: v for k, v in base_env.items() if k not in os.environ})
+        for pth in paths:
+            if pth not in sys.path:
+                sys.path.append(pth)
+        try:
+            fn, args = pickle.loads(payload)
+            out = ("ok", fn(int(rank), int(world), pg, *args))
+        except BaseException:  # report every failure to the driver
+            out = ("error", traceback.format_exc())
+        try:
+            conn.send(out)
+        except Exception:
+            conn.send(("error", "result could not be pickled:\n" + traceback.format_exc()))
+        if out[0] == "error":
+            break  # the driver tears the pool down after a failure
+    try:
+        if pg is not None:
+            pg.shutdown()
+    finally:
+        conn.close()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(_executor_main(*sys.argv[1:9]))

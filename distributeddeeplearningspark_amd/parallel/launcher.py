@@ -5,10 +5,10 @@ Three modes, chosen automatically:
   * SPMD  — the job was started by ``torchrun`` (WORLD_SIZE > 1 in the env): every rank
             already runs the driver program; each trains its own partition in-process.
   * local — ``num_workers == 1``: run in the calling process (SingleTrainer, tests).
-  * spawn — the driver spawns ``num_workers`` fresh interpreters (multiprocessing
-            "spawn": a child process started with fork+exec, never an exec of the
-            driver itself), each binding GPU ``rank % n_gpus`` (RCCL) or the CPU (gloo),
-            rendezvousing on a TCP store at 127.0.0.1:<free port>.
+  * pool  — ``num_workers`` long-lived executor processes (``executors.py``: fresh
+            interpreters started as child processes, never an exec of the driver), each
+            binding GPU ``rank % n_gpus`` (RCCL) or the CPU (gloo), rendezvousing on a TCP
+            store at 127.0.0.1:<free port> once and then serving every training call.
 Failures in any worker abort the others and re-raise the worker traceback in the driver
 (Spark would retry the task; here a training job is all-or-nothing — see utils/fault.py
 for checkpoint-based restart).
@@ -64,30 +64,6 @@ def backend_for(devices: list[str]) -> str | None:
     return "gloo" if len(set(devices)) < len(devices) else None
 
 
-def _child_main(payload_path: str, result_path: str):
-    """Entry point of a worker process (``python -m ...parallel.launcher payload result``)."""
-    import pickle
-
-    with open(payload_path, "rb") as f:
-        fn, rank, world, port, device, backend, args, threads = pickle.load(f)
-    try:
-        import torch
-
-        torch.set_num_threads(max(1, threads))
-        from .comm import init_process_group
-
-        pg = init_process_group(rank, world, "127.0.0.1", port, device=device, backend=backend, timeout_s=600.0)
-        res = fn(rank, world, pg, *args)
-        out = ("ok", res)
-        pg.shutdown()
-    except BaseException:  # report every failure to the driver
-        out = ("error", traceback.format_exc())
-    tmp = result_path + ".tmp"
-    with open(tmp, "wb") as f:
-        pickle.dump(out, f, protocol=pickle.HIGHEST_PROTOCOL)
-    os.replace(tmp, result_path)
-
-
 def run_workers(fn, num_workers: int, args_per_rank, device: str | None = None, timeout_s: float = 3600.0,
                 max_restarts: int | None = None):
     """Run ``fn(rank, world, pg, *args_per_rank[rank])`` on ``num_workers`` workers, return results by rank.
@@ -136,78 +112,19 @@ def _run_once(fn, num_workers, args_per_rank, device, timeout_s, attempt):
             torch.cuda.set_device(dev)
         pg = comm.ProcessGroup(0, 1, 0, dev, None)
         return [fn(0, 1, pg, *args_per_rank[0])]
-    # Fresh interpreters started as child processes (no re-import of the driver's __main__,
-    # so reference-style scripts without an ``if __name__ == "__main__"`` guard work).
-    import pickle
-    import subprocess
-    import sys
-    import tempfile
+    # Long-lived executor processes (fresh interpreters started as child processes, never an
+    # exec of the driver; reference-style scripts without a __main__ guard work), cached and
+    # reused across trainer calls — see executors.py.
+    from .executors import ExecutorPool, PoolFailure, get_pool, pooling_enabled
 
-    port = free_port()
     backend = backend_for(devices)
-    threads = max(1, (os.cpu_count() or 2) // num_workers)
-    tmpdir = tempfile.mkdtemp(prefix="ddl_workers_")
-    procs, res_paths = [], []
-    env = dict(os.environ)
-    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    paths = [root]
-    try:  # the worker function's own directory, so test / script modules unpickle in the child
-        import inspect
-
-        paths.append(os.path.dirname(os.path.abspath(inspect.getfile(fn))))
-    except (TypeError, OSError):
-        pass
-    env["PYTHONPATH"] = os.pathsep.join(paths + ([env["PYTHONPATH"]] if env.get("PYTHONPATH") else []))
-    env["DDL_RESTART_COUNT"] = str(attempt)
-    for r in range(num_workers):
-        pp, rp = os.path.join(tmpdir, f"in{r}.pkl"), os.path.join(tmpdir, f"out{r}.pkl")
-        with open(pp, "wb") as f:
-            pickle.dump((fn, r, num_workers, port, devices[r], backend, args_per_rank[r], threads), f,
-                        protocol=pickle.HIGHEST_PROTOCOL)
-        procs.append(subprocess.Popen([sys.executable, "-m", "distributeddeeplearningspark_amd.parallel.launcher",
-                                       pp, rp], env=env))
-        res_paths.append(rp)
-    results, errors = {}, {}
-    deadline = time.time() + timeout_s
+    pool = get_pool(devices, backend) if pooling_enabled() else ExecutorPool(devices, backend)
     try:
-        while len(results) + len(errors) < num_workers:
-            progressed = False
-            for r, (p, rp) in enumerate(zip(procs, res_paths)):
-                if r in results or r in errors:
-                    continue
-                if os.path.exists(rp):
-                    with open(rp, "rb") as f:
-                        status, payload = pickle.load(f)
-                    (results if status == "ok" else errors)[r] = payload
-                    progressed = True
-                elif p.poll() is not None:
-                    errors[r] = f"worker {r} exited with code {p.returncode} without a result"
-                    progressed = True
-            if errors:
-                break
-            if time.time() > deadline:
-                raise TimeoutError(f"workers did not finish within {timeout_s}s")
-            if not progressed:
-                time.sleep(0.05)
+        return pool.run(fn, args_per_rank, timeout_s=timeout_s, attempt=attempt)
+    except PoolFailure as e:
+        raise WorkerFailure(str(e), e.short) from None
     finally:
-        for p in procs:
-            if errors and p.poll() is None:
-                p.terminate()
-        for p in procs:
-            try:
-                p.wait(timeout=60)
-            except subprocess.TimeoutExpired:
-                p.kill()
-        import shutil
-
-        shutil.rmtree(tmpdir, ignore_errors=True)
-    if errors:
-        r = sorted(errors)[0]
-        raise WorkerFailure(f"worker {r} failed:\n{errors[r]}", f"worker {r} failed")
-    return [results[r] for r in range(num_workers)]
+        if not pooling_enabled():
+            pool.shutdown()
 
 
-if __name__ == "__main__":
-    import sys as _sys
-
-    _child_main(_sys.argv[1], _sys.argv[2])

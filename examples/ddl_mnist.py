@@ -84,6 +84,8 @@ def main():
     conf.set("spark.locality.wait", "0")
     conf.set("spark.serializer", "org.apache.spark.serializer.KryoSerializer")
     conf.set("spark.local.dir", "/tmp/" + get_os_username() + "/spark/")
+    # executors come up (torch import, HIP init, process group) while the driver runs the ETL
+    conf.set("spark.ddl.prestartExecutors", "true").set("spark.ddl.device", args.device)
     sc = SparkContext(conf=conf)
     sqlc = SQLContext(sc)
     spark = SparkSession.builder.getOrCreate()

@@ -107,6 +107,8 @@ def main():
     nyiso_like().to_csv(a.csv, index=False)
     conf = SparkConf().set("spark.app.name", "ddl_nyiso").set("spark.master", f"local[{a.workers}]")
     conf.set("spark.executor.cores", 1).set("spark.executor.instances", a.workers)
+    # executors come up (torch import, HIP init, process group) while the driver runs the ETL
+    conf.set("spark.ddl.prestartExecutors", "true").set("spark.ddl.device", a.device)
     sc = SparkContext(conf=conf)
     sqlc = SQLContext(sc)
     SparkSession.builder.getOrCreate().sparkContext.setLogLevel("ERROR")

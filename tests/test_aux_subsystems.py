@@ -150,3 +150,52 @@ def test_ddp_replica_checksums_gloo():
 
     res = run_workers(_replica_worker, 2, [()] * 2, device="cpu")
     assert res == [(True, False), (True, False)]
+
+
+def _pid_env_worker(rank, world, pg):
+    import os
+
+    return os.getpid(), os.environ.get("DDL_TEST_KNOB")
+
+
+def _fail_once_worker(rank, world, pg):
+    import os
+
+    if rank == 1 and os.environ.get("DDL_RESTART_COUNT") == "0":
+        raise RuntimeError("boom")
+    return os.getpid()
+
+
+def test_executor_pool_is_reused_and_forwards_env(monkeypatch):
+    """Executors are long-lived (Spark executor analog): the second job runs in the same
+    processes, sees DDL_* variables set after the pool started, and a failed task tears the
+    pool down so the restart runs on fresh executors."""
+    from distributeddeeplearningspark_amd.parallel.executors import shutdown_all
+    from distributeddeeplearningspark_amd.parallel.launcher import run_workers
+
+    shutdown_all()
+    a = run_workers(_pid_env_worker, 2, [()] * 2, device="cpu")
+    monkeypatch.setenv("DDL_TEST_KNOB", "42")
+    b = run_workers(_pid_env_worker, 2, [()] * 2, device="cpu")
+    assert [p for p, _ in a] == [p for p, _ in b]
+    assert [k for _, k in a] == [None, None] and [k for _, k in b] == ["42", "42"]
+    pids = run_workers(_fail_once_worker, 2, [()] * 2, device="cpu", max_restarts=1)
+    assert set(pids).isdisjoint(p for p, _ in a)
+
+
+def test_spark_context_prestarts_executors():
+    from distributeddeeplearningspark_amd.context import SparkConf, SparkContext
+    from distributeddeeplearningspark_amd.parallel import executors as E
+
+    E.shutdown_all()
+    conf = SparkConf().set("spark.master", "local[2]").set("spark.executor.instances", 2) \
+        .set("spark.executor.cores", 1).set("spark.ddl.prestartExecutors", "true").set("spark.ddl.device", "cpu")
+    sc = SparkContext(conf=conf)
+    try:
+        assert len(E._POOLS) == 1
+        pool = next(iter(E._POOLS.values()))
+        pool.wait_ready()
+        assert pool.world == 2 and all(p.poll() is None for p in pool.procs)
+    finally:
+        sc.stop()
+    assert not E._POOLS

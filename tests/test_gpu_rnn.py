@@ -7,7 +7,7 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("cell", ["gru", "lstm"])
 @pytest.mark.parametrize("rs", [False, True])
-@pytest.mark.parametrize("B,T,I,H", [(32, 25, 1, 128), (5, 7, 3, 64)])
+@pytest.mark.parametrize("B,T,I,H", [(32, 25, 1, 128), (5, 7, 3, 64), (6, 4, 12, 128), (3, 5, 2, 32)])
 def test_rnn_native_matches_reference(cell, rs, B, T, I, H):
     from distributeddeeplearningspark_amd.ops import rnn as R
     from distributeddeeplearningspark_amd.ops._native import C
@@ -31,3 +31,34 @@ def test_rnn_native_matches_reference(cell, rs, B, T, I, H):
                        (gb, br.grad, "db")]:
         err = ((a.detach().cpu().float() - r.detach()).norm() / (r.norm() + 1e-12)).item()
         assert err < 1e-4, (what, err)
+
+
+def test_mse_kernel_matches_reference():
+    from distributeddeeplearningspark_amd.ops import loss as L
+
+    g = torch.Generator().manual_seed(1)
+    p = torch.randn(37, 3, generator=g)
+    t = torch.randn(37, 3, generator=g)
+    pg = p.cuda().requires_grad_(True)
+    out = L.mean_squared_error(pg, t.cuda())
+    (out * 3.0).backward()
+    pr = p.clone().requires_grad_(True)
+    ref = ((pr - t) ** 2).mean()
+    (ref * 3.0).backward()
+    assert abs(out.item() - ref.item()) < 1e-5
+    assert torch.allclose(pg.grad.cpu(), pr.grad, atol=1e-6)
+
+
+def test_recurrent_model_trains_in_fp32_on_gpu():
+    from distributeddeeplearningspark_amd.models import zoo
+
+    m = zoo.gru_regressor()
+    m.compile("adagrad", "mean_squared_error")
+    m.place("cuda:0")
+    assert m.compute_dtype == torch.float32
+    x = torch.rand(32, 25, 1)
+    y = torch.rand(32, 1)
+    l0 = m.train_on_batch(x, y)
+    for _ in range(20):
+        l1 = m.train_on_batch(x, y)
+    assert l1 < l0
