@@ -115,7 +115,17 @@ class SparkContext:
             return None
         device = device or self._conf.get("spark.ddl.device") or os.environ.get("DDL_DEVICE", "auto")
         devices = plan_devices(n, device)
-        return get_pool(devices, backend_for(devices))
+        self._executors = get_pool(devices, backend_for(devices))
+        return self._executors
+
+    def awaitExecutors(self):
+        """Block until the pre-started executors have joined their process group (the
+        session-startup phase of a Spark application, before any job is submitted)."""
+        pool = getattr(self, "_executors", None)
+        if pool is not None and not pool.closed:
+            pool.wait_ready()
+            pool._ready = True
+        return self
 
     @classmethod
     def getOrCreate(cls, conf=None):

@@ -70,6 +70,7 @@ class _Worker:
         self.history: list[float] = []
         self._step = None
         self._hist_dev, self._hist_n = None, 0
+        self.commit_s = 0.0  # wall time inside commit rounds (host-side view)
 
     @property
     def arena(self):
@@ -183,6 +184,13 @@ class _CommitWorker(_Worker):
         return [r for r, c in enumerate(self.commits_all) if rnd < c]
 
     def commit(self, center, rnd):
+        t0 = time.perf_counter()
+        try:
+            self._commit(center, rnd)
+        finally:
+            self.commit_s += time.perf_counter() - t0
+
+    def _commit(self, center, rnd):
         a, pg = self.arena, self.pg
         contrib = self._contributors(rnd)
         mine = pg.rank in contrib
@@ -386,7 +394,8 @@ def _train_worker(rank, world, pg, cfg, blob, X, Y, sizes):
             w.watchdog.stop()
     if model.device.type == "cuda":
         torch.cuda.synchronize(model.device)
-    out = {"rank": rank, "history": w.losses(), "num_updates": w.num_updates(), "time": time.time() - t0}
+    out = {"rank": rank, "history": w.losses(), "num_updates": w.num_updates(), "time": time.time() - t0,
+           "commit_s": w.commit_s, "graph": bool(w._step is not None and w._step.captured)}
     if rank == 0 or cfg["algorithm"] == "ensemble":
         out["flat"] = final.cpu().numpy().copy()
         out["states"] = get_states(model)
@@ -520,6 +529,7 @@ class _ShardedTrainer(Trainer):
             ps.center = results[0]["flat"]
         ps.states = results[0].get("states")
         self.worker_times = [r["time"] for r in results]
+        self.worker_commit_times = [r.get("commit_s", 0.0) for r in results]
         self._results = results
         model = ps.get_model()
         self.record_training_end()

@@ -141,6 +141,7 @@ def main():
     optimizer_mnist = "adam"
     loss_mnist = "categorical_crossentropy"
     device = None if args.device == "auto" else args.device
+    sc.awaitExecutors()  # session start-up ends here (the reference's executors were up before training)
     trainer = ADAG(keras_model=mnist, worker_optimizer=optimizer_mnist, loss=loss_mnist, num_workers=num_workers,
                    batch_size=16, communication_window=5, num_epoch=args.epochs, features_col="matrix",
                    label_col="label_encoded", device=device)

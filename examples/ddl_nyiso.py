@@ -113,10 +113,13 @@ def main():
     sqlc = SQLContext(sc)
     SparkSession.builder.getOrCreate().sparkContext.setLogLevel("ERROR")
     df_train, df_test, omin, omax = build_frames(sqlc, a.csv, a.workers)
+    sc.awaitExecutors()  # session start-up ends here (the reference's executors were up before training)
     res = {}
     for name, model, opt in (("GRU", gru_regressor(N_UNITS), "adagrad"), ("LSTM", lstm_regressor(N_UNITS), "adam")):
         tr, mape = run(model, opt, df_train, df_test, omin, omax, a.workers, a.epochs, a.device)
-        res[name] = {"updates": tr.parameter_server.num_updates, "time_s": tr.get_training_time(), "mape": mape}
+        res[name] = {"updates": tr.parameter_server.num_updates, "time_s": tr.get_training_time(), "mape": mape,
+                     "worker_s": [round(t, 3) for t in tr.worker_times],
+                     "commit_s": [round(t, 3) for t in tr.worker_commit_times]}
     print(json.dumps({"workflow": "ddl_nyiso", "workers": a.workers, "epochs": a.epochs, "results": res}))
 
 

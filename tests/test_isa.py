@@ -1,0 +1,45 @@
+"""Static checks on the gfx950 machine code of the built extension (CPU-only: llvm-objdump).
+
+The hot kernels must issue MFMA instructions (GEMM / implicit-GEMM conv / attention), the
+GEMM families must stage operands with direct-to-LDS loads or LDS transpose reads, and the
+element-wise / normalisation / recurrent kernels must not spill to scratch."""
+import os
+
+import pytest
+
+SO = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "distributeddeeplearningspark_amd",
+                  "_C.so")
+pytestmark = pytest.mark.skipif(not os.path.exists(SO), reason="extension not built")
+
+
+@pytest.fixture(scope="module")
+def rows():
+    from distributeddeeplearningspark_amd.utils.isa import summary
+
+    return summary(SO)
+
+
+def _pick(rows, needle):
+    sel = [r for r in rows if needle in r["kernel"]]
+    assert sel, f"no kernel matching {needle!r} in the code object"
+    return sel
+
+
+@pytest.mark.parametrize("family", ["gemm_dma_kernel", "gemm256_kernel", "gemm_stream_kernel", "attn_fwd_kernel",
+                                    "attn_bwd_dkdv_kernel", "attn_bwd_dq_kernel"])
+def test_matrix_kernels_issue_mfma(rows, family):
+    for r in _pick(rows, family):
+        assert r["mfma"] > 0, r
+
+
+def test_gemm_operands_staged_through_lds(rows):
+    for r in _pick(rows, "gemm_dma_kernel") + _pick(rows, "gemm256_kernel"):
+        assert r["lds_dma"] > 0, r
+
+
+@pytest.mark.parametrize("family", ["bn_apply_kernel", "bn_bwd_dx_kernel", "bn_bwd_reduce_kernel", "ln_fwd_kernel",
+                                    "ln_bwd_kernel", "rnn_fwd_reg_kernel", "rnn_bwd_reg_kernel", "adam_kernel",
+                                    "softmax_xent_kernel", "attn_fwd_kernel"])
+def test_hot_kernels_do_not_spill(rows, family):
+    for r in _pick(rows, family):
+        assert r["scratch"] == 0, r
