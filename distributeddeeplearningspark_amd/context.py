@@ -124,7 +124,6 @@ class SparkContext:
         pool = getattr(self, "_executors", None)
         if pool is not None and not pool.closed:
             pool.wait_ready()
-            pool._ready = True
         return self
 
     @classmethod

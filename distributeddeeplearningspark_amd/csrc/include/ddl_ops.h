@@ -145,4 +145,9 @@ bool rnn_bwd_uses_ut(int H);
 int rnn_bwd(int cell, const float* dy, const float* U, const float* UT, const float* hs, const float* cs,
             const float* gates, float* dgates, int B, int T, int H, int rs, hipStream_t s);
 
+// ---------------- device ETL (dist-keras column transformers, fp64) ----------------
+int etl_minmax(const double* x, double* y, long n, double o_min, double scale, double n_min, hipStream_t s);
+int etl_one_hot(const int64_t* labels, double* y, long n, int K, int* bad, hipStream_t s);
+int etl_argmax(const double* x, long rows, int K, long ld, int64_t* out, hipStream_t s);
+
 }  // namespace ddl

@@ -283,6 +283,28 @@ void mse_fwd_bwd_(const at::Tensor& pred, const at::Tensor& target, const at::Te
   HIP_OK(mse_fwd_bwd(pred.data_ptr<float>(), target.data_ptr<float>(), pred.numel(), loss.data_ptr<float>(),
                      grad.data_ptr<float>(), cur_stream()));
 }
+void etl_minmax_(const at::Tensor& x, const at::Tensor& y, double o_min, double scale, double n_min) {
+  CK(x.is_cuda() && x.scalar_type() == at::kDouble && y.scalar_type() == at::kDouble && x.is_contiguous() &&
+         y.is_contiguous() && x.numel() == y.numel(), "etl_minmax: contiguous fp64 x / y of equal size");
+  at::DeviceGuard gd(x.device());
+  HIP_OK(etl_minmax(x.data_ptr<double>(), y.data_ptr<double>(), x.numel(), o_min, scale, n_min, cur_stream()));
+}
+void etl_one_hot_(const at::Tensor& labels, const at::Tensor& y, const at::Tensor& bad) {
+  CK(labels.is_cuda() && labels.scalar_type() == at::kLong && labels.is_contiguous(), "etl_one_hot: int64 labels");
+  CK(y.scalar_type() == at::kDouble && y.dim() == 2 && y.size(0) == labels.numel() && y.is_contiguous(),
+     "etl_one_hot: y [n, K] fp64");
+  CK(bad.scalar_type() == at::kInt && bad.numel() == 1, "etl_one_hot: int32 flag");
+  at::DeviceGuard gd(y.device());
+  HIP_OK(etl_one_hot(labels.data_ptr<int64_t>(), y.data_ptr<double>(), labels.numel(), (int)y.size(1),
+                     bad.data_ptr<int>(), cur_stream()));
+}
+void etl_argmax_(const at::Tensor& x, const at::Tensor& out) {
+  CK(x.is_cuda() && x.scalar_type() == at::kDouble && x.dim() == 2 && x.stride(1) == 1, "etl_argmax: x [rows, K] fp64");
+  CK(out.scalar_type() == at::kLong && out.numel() == x.size(0), "etl_argmax: out int64 [rows]");
+  at::DeviceGuard gd(x.device());
+  HIP_OK(etl_argmax(x.data_ptr<double>(), x.size(0), (int)x.size(1), x.stride(0), out.data_ptr<int64_t>(),
+                    cur_stream()));
+}
 void step_tick_(const at::Tensor& t) {
   F32(t);
   CK(t.is_cuda() && t.numel() == 1, "step counter: one fp32 element on the GPU");
@@ -346,6 +368,9 @@ void register_ops(py::module& m) {
         py::arg("bc1"), py::arg("bc2"), py::arg("gscale"), py::arg("tstep") = py::none());
   m.def("step_tick", &step_tick_);
   m.def("mse_fwd_bwd", &mse_fwd_bwd_);
+  m.def("etl_minmax", &etl_minmax_);
+  m.def("etl_one_hot", &etl_one_hot_);
+  m.def("etl_argmax", &etl_argmax_);
   m.def("adagrad_step", &adagrad_step_);
   m.def("rmsprop_step", &rmsprop_step_);
   m.def("sumsq", &sumsq_);

@@ -59,6 +59,7 @@ class ExecutorPool:
         self._conns: dict[int, object] = {}
         self._accept_err = None
         self.closed = False
+        self._ready = False
         self.tasks_run = 0
         threads = max(1, (os.cpu_count() or 2) // self.world)
         pg_port = free_port()
@@ -87,6 +88,8 @@ class ExecutorPool:
             self._accept_err = e
 
     def wait_ready(self):
+        if self._ready:
+            return self
         while True:
             conns = list(self._conns.values())  # filled by the acceptor thread
             ready = sum(1 for c in conns if c.poll(0)) if len(conns) == self.world else 0
@@ -96,6 +99,7 @@ class ExecutorPool:
                     if kind != "ready":
                         self.shutdown(force=True)
                         raise PoolFailure(f"executor {r} failed to start:\n{payload}", f"executor {r} start failed")
+                self._ready = True
                 return self
             for r, p in enumerate(self.procs):
                 if p.poll() is not None:
@@ -109,9 +113,7 @@ class ExecutorPool:
 
     # ------------------------------------------------------------------ tasks
     def run(self, fn, args_per_rank, timeout_s: float = 3600.0, attempt: int = 0):
-        if getattr(self, "_ready", False) is False:
-            self.wait_ready()
-            self._ready = True
+        self.wait_ready()
         env = _ddl_env()
         env["DDL_RESTART_COUNT"] = str(attempt)
         paths = []

@@ -8,7 +8,9 @@ Reference usage (constructor kwargs kept verbatim):
   ``ReshapeTransformer(input_col, output_col, shape)``       ``ddl_mnist_aztk.py:142``
   ``DenseTransformer(input_col, output_col)``               ``ddl_mnist_aztk.py:150``
   ``LabelIndexTransformer(output_dim)``                     ``ddl_mnist_aztk.py:205``
-Every transform is one vectorised numpy pass over the column (no per-row Python).
+Every transform is one vectorised numpy pass over the column (no per-row Python), or —
+with ``device="cuda"`` / ``DDL_ETL_DEVICE=cuda`` — one fp64 HIP kernel on the GPU
+(``ops/etl.py``, ``csrc/kernels/ingest.hip``) with identical results.
 """
 from __future__ import annotations
 
@@ -16,6 +18,7 @@ from collections import OrderedDict
 
 import numpy as np
 
+from .ops import etl as E
 from .sql import types as T
 from .sql.column import ColumnData
 from .sql.dataframe import DataFrame
@@ -44,7 +47,8 @@ class MinMaxTransformer(Transformer):
     """Affine rescale [o_min, o_max] -> [n_min, n_max]; ``is_vector`` selects a vector
     (DenseVector) or scalar (double) output column."""
 
-    def __init__(self, o_min, o_max, n_min, n_max, input_col, output_col, is_vector=True):
+    def __init__(self, o_min, o_max, n_min, n_max, input_col, output_col, is_vector=True, device=None):
+        self.device = device
         self.o_min, self.o_max = float(o_min), float(o_max)
         self.n_min, self.n_max = float(n_min), float(n_max)
         self.input_col, self.output_col, self.is_vector = input_col, output_col, is_vector
@@ -53,7 +57,11 @@ class MinMaxTransformer(Transformer):
 
     def transform(self, dataframe):
         v, cd = _block(dataframe, self.input_col)
-        out = (v.astype(np.float64) - self.o_min) * self.scale + self.n_min
+        dev = E.etl_device(self.device)
+        if dev is not None:
+            out = E.minmax(v, self.o_min, self.scale, self.n_min, dev)
+        else:
+            out = (v.astype(np.float64) - self.o_min) * self.scale + self.n_min
         if self.is_vector:
             out = out.reshape(out.shape[0], -1)
             return _with(dataframe, self.output_col, ColumnData(out, cd.mask, T.VectorUDT()))
@@ -61,12 +69,17 @@ class MinMaxTransformer(Transformer):
 
 
 class OneHotTransformer(Transformer):
-    def __init__(self, output_dim, input_col, output_col):
+    def __init__(self, output_dim, input_col, output_col, device=None):
         self.output_dim, self.input_col, self.output_col = int(output_dim), input_col, output_col
+        self.device = device
 
     def transform(self, dataframe):
         v, cd = _block(dataframe, self.input_col)
         idx = v.reshape(-1).astype(np.int64)
+        dev = E.etl_device(self.device)
+        if dev is not None:
+            return _with(dataframe, self.output_col, ColumnData(E.one_hot(idx, self.output_dim, dev), cd.mask,
+                                                                T.VectorUDT()))
         if len(idx) and (idx.min() < 0 or idx.max() >= self.output_dim):
             raise ValueError(f"OneHotTransformer: label outside [0, {self.output_dim})")
         out = np.zeros((len(idx), self.output_dim), dtype=np.float64)
@@ -105,14 +118,19 @@ class LabelIndexTransformer(Transformer):
     rows whose maximum activation is below it get ``default_index``."""
 
     def __init__(self, output_dim, input_col="prediction", output_col="prediction_index", default_index=0,
-                 activation_threshold=None):
+                 activation_threshold=None, device=None):
+        self.device = device
         self.output_dim, self.input_col, self.output_col = int(output_dim), input_col, output_col
         self.default_index, self.activation_threshold = default_index, activation_threshold
 
     def transform(self, dataframe):
         v, cd = _block(dataframe, self.input_col)
         v = v.reshape(v.shape[0], -1)[:, : self.output_dim]
-        idx = np.argmax(v, axis=1).astype(np.float64) if len(v) else np.zeros(0)
+        dev = E.etl_device(self.device)
+        if dev is not None and len(v):
+            idx = E.argmax(v, dev).astype(np.float64)
+        else:
+            idx = np.argmax(v, axis=1).astype(np.float64) if len(v) else np.zeros(0)
         if self.activation_threshold is not None and len(v):
             idx = np.where(v.max(1) >= self.activation_threshold, idx, float(self.default_index))
         return _with(dataframe, self.output_col, ColumnData(idx, cd.mask, T.DoubleType()))

@@ -148,3 +148,28 @@ def test_write_read_roundtrip(tmp_path, spark):
     assert spark.read.parquet(str(tmp_path / "p")).count() == 3
     with pytest.raises(IOError):
         spark.read.csv("wasb://container@acct.blob.core.windows.net/x.csv")
+
+
+from hypothesis import HealthCheck, given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+
+@settings(max_examples=30, deadline=None, derandomize=True, suppress_health_check=[HealthCheck.function_scoped_fixture])
+@given(n=st.integers(1, 60), groups=st.integers(1, 4), lag=st.integers(1, 5), lead=st.integers(1, 3),
+       seed=st.integers(0, 10_000))
+def test_window_lag_lead_na_drop_match_pandas(spark, n, groups, lag, lead, seed):
+    """Random partitions / orders / offsets: lag & lead over a window, then na.drop, vs pandas."""
+    rng = np.random.default_rng(seed)
+    pdf = pd.DataFrame({"g": rng.integers(0, groups, n).astype(str), "t": rng.permutation(n),
+                        "v": rng.normal(size=n).round(3)})
+    df = spark.createDataFrame(pdf)
+    w = Window.partitionBy("g").orderBy("t")
+    out = df.withColumn("lg", F.lag(F.col("v"), count=lag).over(w)) \
+            .withColumn("ld", F.lead(F.col("v"), count=lead).over(w)).na.drop().orderBy("t").toPandas()
+    ref = pdf.sort_values("t").copy()
+    grp = ref.groupby("g")["v"]
+    ref["lg"], ref["ld"] = grp.shift(lag), grp.shift(-lead)
+    ref = ref.dropna().sort_values("t")
+    assert out["t"].tolist() == ref["t"].tolist()
+    np.testing.assert_allclose(out["lg"].to_numpy(), ref["lg"].to_numpy())
+    np.testing.assert_allclose(out["ld"].to_numpy(), ref["ld"].to_numpy())
