@@ -37,8 +37,8 @@ struct ColGeom {  // thread -> (row-lane, column-vector) mapping for column redu
 };
 
 // Block reduction of 16 per-thread partials over the RT row-lanes (LDS tree), then ONE
-// plain store per value into partial row blockIdx.x of ws[S][2][C] (no atomics: the
-// per-channel finalize sums the S partial rows).
+// atomic add per value into shard row blockIdx.x % kBnShards of the zeroed ws[kBnShards][2][C]
+// (<= kMaxPartials / kBnShards = 16 workgroups share a row; the finalize sums 32 rows).
 __device__ __forceinline__ void col_reduce_store(float (&acc)[16], const ColGeom& g, float* ws, int C) {
   __shared__ float red[256 * 17];
   if (g.RT > 1) {
@@ -60,11 +60,12 @@ __device__ __forceinline__ void col_reduce_store(float (&acc)[16], const ColGeom
     }
   }
   if (g.rt == 0 && g.cv < g.CV) {
-    float* dst = ws + (long)blockIdx.x * 2 * C + g.cv * 8;
-    *reinterpret_cast<float4*>(dst) = make_float4(acc[0], acc[1], acc[2], acc[3]);
-    *reinterpret_cast<float4*>(dst + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
-    *reinterpret_cast<float4*>(dst + C) = make_float4(acc[8], acc[9], acc[10], acc[11]);
-    *reinterpret_cast<float4*>(dst + C + 4) = make_float4(acc[12], acc[13], acc[14], acc[15]);
+    float* dst = ws + (long)(blockIdx.x % kBnShards) * 2 * C + g.cv * 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      atomicAdd(dst + i, acc[i]);
+      atomicAdd(dst + C + i, acc[8 + i]);
+    }
   }
 }
 
@@ -114,7 +115,7 @@ static dim3 col_grid(long M, int C) {
   return dim3((unsigned)gx, (unsigned)gy);
 }
 
-int bn_partial_rows(long M, int C) { return (int)col_grid(M, C).x; }
+int bn_partial_rows(long M, int C) { return kBnShards; }
 
 int bn_stats(const void* x, float* ws, long M, int C, hipStream_t s) {
   hipLaunchKernelGGL(bn_stats_kernel, col_grid(M, C), dim3(256), 0, s, (const uint4*)x, ws, M, C);

@@ -79,8 +79,11 @@ class ConvGeometry:
         nonempty = [c for c in self.classes if c["wt"]]
         # a single class with taps (1x1 / stride-s downsample): its epilogue zero-fills the
         # other s*s-1 positions, so dX needs no separate memset
+        # (its s x s cells must cover the whole input: with padding the class with taps can be an
+        # odd-offset one whose grid stops one row / column short)
         self.dgrad_zero_siblings = (len(nonempty) == 1 and (self.sh > 1 or self.sw > 1) and self.sh == self.sw
-                                    and len(self.classes) == self.sh * self.sw)
+                                    and len(self.classes) == self.sh * self.sw
+                                    and nonempty[0]["Hc"] * self.sh >= H and nonempty[0]["Wc"] * self.sw >= W)
         self.dgrad_needs_zero = (not self.dgrad_zero_siblings) and (
             any(len(c["wt"]) == 0 for c in self.classes) or len(self.classes) < self.sh * self.sw)
 
@@ -204,6 +207,7 @@ class _Conv2dFn(torch.autograd.Function):
         ctx.cfg = cfg
         ctx.native = use_native(x)
         ctx.ci = Ci
+        ctx.co = Co
         if ctx.native:
             x = x.contiguous()
             if Ci % 8:  # 16-B vector granularity: pad channels (stem: 3 -> 8) with zeros
@@ -211,14 +215,26 @@ class _Conv2dFn(torch.autograd.Function):
                 x = F.pad(x, (0, cp - Ci))
                 w = F.pad(w.detach(), (0, cp - Ci))
                 Ci = cp
+            if Co % 8:  # same for the output channels (extra filters are zero, sliced off below)
+                cop = -(-Co // 8) * 8
+                w = F.pad(w.detach(), (0, 0, 0, 0, 0, 0, 0, cop - Co))
+                b = None if b is None else F.pad(b.detach(), (0, cop - Co))
+                Co = cop
             g = geometry(N, H, W, Ci, Co, KH, KW, stride, pad, dil)
-            y = conv_fwd_native(x, w, g, bias=b, relu=relu, stats=stats)
+            st = stats
+            if stats is not None and Co != ctx.co:  # statistics of the padded filters land in a wider workspace
+                st = torch.zeros((stats.shape[0], 2, Co), dtype=torch.float32, device=x.device)
+            y = conv_fwd_native(x, w, g, bias=b, relu=relu, stats=st)
+            if st is not stats:
+                stats.copy_(st[:, :, : ctx.co])
             ctx.g = g
         else:
             y = conv_ref(x, w.to(x.dtype), None if b is None else b.to(x.dtype), stride, pad, dil, relu)
         ctx.gw, ctx.gb = gw, gb
         ctx.save_for_backward(x, w, b, y if relu else None)
         ctx.needs_dx = ctx.needs_input_grad[0]
+        if y.shape[-1] != ctx.co:
+            y = y[..., : ctx.co].contiguous()
         return y
 
     @staticmethod
@@ -230,23 +246,31 @@ class _Conv2dFn(torch.autograd.Function):
         dx = None
         if ctx.native:
             g = ctx.g
+            pad_co = g.Co != ctx.co
+            if pad_co:
+                dy = F.pad(dy, (0, g.Co - ctx.co))
             if relu:
                 d2 = torch.empty_like(dy)
                 C().relu_bwd(dy, y, d2)
                 dy = d2
             if gb is not None:
-                C().bias_grad(dy, gb, g.Co, True)
-            padded = g.Ci != ctx.ci
+                if pad_co:
+                    tb = torch.zeros(g.Co, dtype=torch.float32, device=dy.device)
+                    C().bias_grad(dy, tb, g.Co, True)
+                    gb.add_(tb[: ctx.co])
+                else:
+                    C().bias_grad(dy, gb, g.Co, True)
+            padded = g.Ci != ctx.ci or pad_co
             if gw is not None:
                 if padded:
                     tmp = torch.zeros((g.Co, g.KH, g.KW, g.Ci), dtype=torch.float32, device=dy.device)
                     conv_wgrad_native(dy, x, g, tmp)
-                    gw.add_(tmp[..., : ctx.ci])
+                    gw.add_(tmp[: ctx.co, ..., : ctx.ci])
                 else:
                     conv_wgrad_native(dy, x, g, gw)
             if ctx.needs_dx:
                 dx = conv_dgrad_native(dy, w, g)
-                if padded:
+                if g.Ci != ctx.ci:
                     dx = dx[..., : ctx.ci].contiguous()
         else:
             fn = lambda xx, ww, bb: conv_ref(xx, ww, bb, stride, pad, dil, relu)
