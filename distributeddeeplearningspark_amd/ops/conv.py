@@ -18,6 +18,7 @@ Decomposition (``ConvGeometry``):
 from __future__ import annotations
 
 import math
+import os as _os
 from functools import lru_cache
 
 import torch
@@ -127,9 +128,37 @@ def _tap_index(cl, device):
     return cache[key]
 
 
+def _dgrad_as_forward(g: ConvGeometry):
+    """Stride-1 convolutions: dx is a forward convolution of dy with the flipped, transposed
+    filter (padding d*(k-1) - p), which runs on the forward implicit-GEMM path (K-contiguous
+    weights, no transposed LDS reads) — measured 1.3-1.7x faster than the RC_TAPS data-gradient
+    on the ResNet-50 3x3 layers.  Returns the forward geometry, or None when not applicable."""
+    if g.sh != 1 or g.sw != 1 or g.is_pointwise or _os.environ.get("DDL_DGRAD_AS_FWD", "1") == "0":
+        return None
+    ph, pw = g.dh * (g.KH - 1) - g.ph, g.dw * (g.KW - 1) - g.pw
+    if ph < 0 or pw < 0 or g.Co % 64 or g.T > 64:
+        return None
+    g2 = geometry(g.N, g.Ho, g.Wo, g.Co, g.Ci, g.KH, g.KW, (1, 1), (ph, pw), (g.dh, g.dw))
+    if (g2.Ho, g2.Wo) != (g.H, g.W) or not g2.implicit_fwd:
+        return None
+    return g2
+
+
+_KC_DGRAD = _os.environ.get("DDL_DGRAD_KC", "1") != "0"
+
+
+def flip_filter(w):
+    """[Co, KH, KW, Ci] -> [Ci, KH, KW, Co] with the taps reversed (the transposed conv's filter)."""
+    return w.flip(1, 2).permute(3, 1, 2, 0).contiguous()
+
+
 def conv_dgrad_native(dy, w, g: ConvGeometry, resid=None):
     """dx = conv^T(dy, w) (+ resid, fused into the epilogue when the layout allows)."""
     dev = dy.device
+    if resid is None:
+        g2 = _dgrad_as_forward(g)
+        if g2 is not None:
+            return conv_fwd_native(dy.contiguous(), flip_filter(w), g2)
     if g.is_pointwise:
         dx = torch.empty((g.N, g.H, g.W, g.Ci), dtype=torch.bfloat16, device=dev)
         G.linear_dgrad(dy.view(g.M, g.Co), w.view(g.Co, g.Ci), out=dx.view(-1, g.Ci),
@@ -147,7 +176,15 @@ def conv_dgrad_native(dy, w, g: ConvGeometry, resid=None):
             om = dict(gh=cl["Hc"], gw=cl["Wc"], hy=g.H, wy=g.W, so=g.sh, oh=cl["ph"], ow=cl["pw"],
                       zero=int(g.dgrad_zero_siblings))
         r = None if (resid is None or strided) else resid.view(-1, g.Ci)
-        if g.implicit_dgrad:
+        if g.implicit_dgrad and _KC_DGRAD:
+            # the class's taps of the filter, transposed once to K-contiguous [Ci][taps][Co]: the GEMM
+            # then reads B with ds_read_b128 like a forward conv (faster than the RC_TAPS layout)
+            wkc = w.reshape(g.Co, g.T, g.Ci).index_select(1, _tap_index(cl, dev)).permute(2, 1, 0).contiguous()
+            geom = dict(n=g.N, hi=g.Ho, wi=g.Wo, c=g.Co, ho=cl["Hc"], wo=cl["Wc"], sh=1, sw=1, tap_c=g.Co,
+                        dh=cl["dh"], dw=cl["dw"])
+            G.gemm(dy, wkc, dx, Mc, g.Ci, nt * g.Co, G.KC_GATHER, G.KC, 0, nt * g.Co, g.Ci, G.EPI_BF16,
+                   geom=geom, outmap=om, resid=r, ldr=g.Ci if r is not None else 0)
+        elif g.implicit_dgrad:
             geom = dict(n=g.N, hi=g.Ho, wi=g.Wo, c=g.Co, ho=cl["Hc"], wo=cl["Wc"], sh=1, sw=1, tap_c=g.Co,
                         dh=cl["dh"], dw=cl["dw"], wt=cl["wt"])
             G.gemm(dy, w, dx, Mc, g.Ci, nt * g.Co, G.KC_GATHER, G.RC_TAPS, 0, g.T * g.Ci, g.Ci, G.EPI_BF16,
