@@ -11,11 +11,10 @@ constexpr int kBnShards = 32;     // == kStatShards: sharded atomic sums of the 
 constexpr int kMaxPartials = 512;  // partial rows of a column-reduction sweep
 
 // ---------------- batch norm (x: [M, C] bf16, C % 8 == 0) ----------------
-// Per-channel sums live in a ZEROED workspace ws[kBnShards][2][C], accumulated with sharded
-// atomics (row = producing workgroup % kBnShards) by the fused conv-epilogue statistics and by
-// the bn_stats / bn_bwd_reduce sweeps alike; the finalize sums the 32 rows (a few microseconds,
-// where summing one partial row per sweep workgroup took ~13 us per BN layer).
-int bn_partial_rows(long M, int C);  // == kBnShards
+// Per-channel sums live in a workspace ws[S][2][C] (S partial rows, summed by the finalize):
+//   * fused conv-epilogue statistics: S = kBnShards, zeroed, accumulated with atomics;
+//   * bn_stats / bn_bwd_reduce sweeps: S = bn_partial_rows(M, C), every row written (no zeroing).
+int bn_partial_rows(long M, int C);
 int bn_stats(const void* x, float* ws, long M, int C, hipStream_t s);
 // ws -> mean/invstd (saved for backward), scale/shift for apply, running stats update
 int bn_finalize(const float* ws, int S, long M, int C, const float* gamma, const float* beta, float eps,

@@ -37,8 +37,8 @@ struct ColGeom {  // thread -> (row-lane, column-vector) mapping for column redu
 };
 
 // Block reduction of 16 per-thread partials over the RT row-lanes (LDS tree), then ONE
-// atomic add per value into shard row blockIdx.x % kBnShards of the zeroed ws[kBnShards][2][C]
-// (<= kMaxPartials / kBnShards = 16 workgroups share a row; the finalize sums 32 rows).
+// plain store per value into partial row blockIdx.x of ws[S][2][C] (no atomics: the
+// per-channel finalize sums the S partial rows).
 __device__ __forceinline__ void col_reduce_store(float (&acc)[16], const ColGeom& g, float* ws, int C) {
   __shared__ float red[256 * 17];
   if (g.RT > 1) {
@@ -60,12 +60,11 @@ __device__ __forceinline__ void col_reduce_store(float (&acc)[16], const ColGeom
     }
   }
   if (g.rt == 0 && g.cv < g.CV) {
-    float* dst = ws + (long)(blockIdx.x % kBnShards) * 2 * C + g.cv * 8;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      atomicAdd(dst + i, acc[i]);
-      atomicAdd(dst + C + i, acc[8 + i]);
-    }
+    float* dst = ws + (long)blockIdx.x * 2 * C + g.cv * 8;
+    *reinterpret_cast<float4*>(dst) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    *reinterpret_cast<float4*>(dst + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+    *reinterpret_cast<float4*>(dst + C) = make_float4(acc[8], acc[9], acc[10], acc[11]);
+    *reinterpret_cast<float4*>(dst + C + 4) = make_float4(acc[12], acc[13], acc[14], acc[15]);
   }
 }
 
@@ -115,48 +114,58 @@ static dim3 col_grid(long M, int C) {
   return dim3((unsigned)gx, (unsigned)gy);
 }
 
-int bn_partial_rows(long M, int C) { return kBnShards; }
+int bn_partial_rows(long M, int C) { return (int)col_grid(M, C).x; }
 
 int bn_stats(const void* x, float* ws, long M, int C, hipStream_t s) {
   hipLaunchKernelGGL(bn_stats_kernel, col_grid(M, C), dim3(256), 0, s, (const uint4*)x, ws, M, C);
   return (int)hipGetLastError();
 }
 
-// Sum of the S partial rows of ws[S][2][C] for 64 channels per 256-thread block:
-// 4 row-lanes per channel, 4 independent accumulators each, then an LDS combine.
+// Sum of the S partial rows of ws[S][2][C] for 64 channels per block: NL = blockDim / 64
+// row-lanes per channel (4 for the 32 shard rows of the fused statistics, 16 for the up to 512
+// partial rows of a reduce sweep — one lane per 32 rows instead of 128 keeps the per-layer
+// finalize near the launch floor), 4 independent accumulators each, then an LDS combine.
 // Returns true in the lane that owns channel c (row-lane 0).
 __device__ __forceinline__ bool sum_partials(const float* ws, int S, int C, int& c, double& s1, double& s2) {
+  const int NL = blockDim.x >> 6;
   const int cl = threadIdx.x & 63, sl = threadIdx.x >> 6;
   c = blockIdx.x * 64 + cl;
   double a1 = 0.0, a2 = 0.0;
   if (c < C) {
     float p1[4] = {0.f, 0.f, 0.f, 0.f}, p2[4] = {0.f, 0.f, 0.f, 0.f};
     int k = sl;
-    for (; k + 12 < S; k += 16) {
+    for (; k + 3 * NL < S; k += 4 * NL) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        p1[u] += ws[(long)(k + 4 * u) * 2 * C + c];
-        p2[u] += ws[(long)(k + 4 * u) * 2 * C + C + c];
+        p1[u] += ws[(long)(k + NL * u) * 2 * C + c];
+        p2[u] += ws[(long)(k + NL * u) * 2 * C + C + c];
       }
     }
-    for (; k < S; k += 4) {
+    for (; k < S; k += NL) {
       p1[0] += ws[(long)k * 2 * C + c];
       p2[0] += ws[(long)k * 2 * C + C + c];
     }
     a1 = (double)p1[0] + p1[1] + p1[2] + p1[3];
     a2 = (double)p2[0] + p2[1] + p2[2] + p2[3];
   }
-  __shared__ double red[2][256];
+  __shared__ double red[2][1024];
   red[0][threadIdx.x] = a1;
   red[1][threadIdx.x] = a2;
   __syncthreads();
   if (sl != 0 || c >= C) return false;
-  s1 = red[0][cl] + red[0][cl + 64] + red[0][cl + 128] + red[0][cl + 192];
-  s2 = red[1][cl] + red[1][cl + 64] + red[1][cl + 128] + red[1][cl + 192];
+  s1 = 0.0;
+  s2 = 0.0;
+  for (int l = 0; l < NL; ++l) {
+    s1 += red[0][cl + 64 * l];
+    s2 += red[1][cl + 64 * l];
+  }
   return true;
 }
 
-__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* ws, int S, long M, int C, const float* gamma,
+// threads of a finalize block: 16 row-lanes for long partial-row lists, 4 for the shard rows
+static int finalize_threads(int S) { return S > 64 ? 1024 : 256; }
+
+__global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* ws, int S, long M, int C, const float* gamma,
                                                           const float* beta, float eps, float momentum, float* rmean,
                                                           float* rvar, float* smean, float* sinv, float* scale,
                                                           float* shift) {
@@ -183,7 +192,7 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* ws, int S
 int bn_finalize(const float* ws, int S, long M, int C, const float* gamma, const float* beta, float eps,
                 float momentum, float* running_mean, float* running_var, float* save_mean, float* save_invstd,
                 float* scale, float* shift, hipStream_t s) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, s, ws, S, M, C, gamma, beta, eps,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(finalize_threads(S)), 0, s, ws, S, M, C, gamma, beta, eps,
                      momentum, running_mean, running_var, save_mean, save_invstd, scale, shift);
   return (int)hipGetLastError();
 }
@@ -360,7 +369,7 @@ int bn_bwd_reduce(const void* dy, const void* x, const void* y, const float* sca
 
 // coef[c] = A, coef[C+c] = B, coef[2C+c] = K with dx = A*dy' + B*x + K
 //   (= gamma*invstd * (dy' - mean(dy') - xhat * mean(dy'*xhat)))
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* ws, int S, long M, int C,
+__global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const float* ws, int S, long M, int C,
                                                               const float* gamma, const float* mean,
                                                               const float* invstd, float* dgamma, float* dbeta,
                                                               float* coef) {
@@ -382,7 +391,8 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* ws, i
 
 int bn_bwd_finalize(const float* ws, int S, long M, int C, const float* gamma, const float* mean, const float* invstd,
                     float* dgamma, float* dbeta, float* coef, hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, s, ws, S, M, C, gamma, mean, invstd,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(finalize_threads(S)), 0, s, ws, S, M, C, gamma,
+                     mean, invstd,
                      dgamma, dbeta, coef);
   return (int)hipGetLastError();
 }

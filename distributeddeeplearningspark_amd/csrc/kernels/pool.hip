@@ -21,14 +21,13 @@ __device__ __forceinline__ uint4 pack8p(const float* f) {
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint4* __restrict__ x, uint4* __restrict__ y,
                                                            uint2* __restrict__ am, int N, int H, int W, int CV, int Ho,
                                                            int Wo, int kh, int kw, int sh, int sw, int ph, int pw) {
-  const long total = (long)N * Ho * Wo * CV;
-  for (long v = (long)blockIdx.x * 256 + threadIdx.x; v < total; v += (long)gridDim.x * 256) {
-    const int cv = (int)(v % CV);
-    long p = v / CV;
-    const int ow = (int)(p % Wo);
-    p /= Wo;
-    const int oh = (int)(p % Ho);
-    const int n = (int)(p / Ho);
+  // 32-bit index math (the launcher guarantees total < 2^31): 64-bit divisions cost ~10x more
+  const uint32_t total = (uint32_t)N * Ho * Wo * CV;
+  for (uint32_t v = blockIdx.x * 256u + threadIdx.x; v < total; v += gridDim.x * 256u) {
+    const uint32_t q = v / (uint32_t)CV, cv = v - q * (uint32_t)CV;
+    const uint32_t q2 = q / (uint32_t)Wo, ow = q - q2 * (uint32_t)Wo;
+    const int oh = (int)(q2 % (uint32_t)Ho);
+    const int n = (int)(q2 / (uint32_t)Ho);
     float best[8];
     uint8_t arg[8];
 #pragma unroll
@@ -70,6 +69,7 @@ static unsigned pgrid(long n) {
 int maxpool_fwd(const void* x, void* y, uint8_t* argmax, int N, int H, int W, int C, int Ho, int Wo, int kh, int kw,
                 int sh, int sw, int ph, int pw, hipStream_t s) {
   const long total = (long)N * Ho * Wo * (C / 8);
+  if (total >= (1L << 31) || (long)N * H * W * (C / 8) >= (1L << 31)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(pgrid(total)), dim3(256), 0, s, (const uint4*)x, (uint4*)y,
                      (uint2*)argmax, N, H, W, C / 8, Ho, Wo, kh, kw, sh, sw, ph, pw);
   return (int)hipGetLastError();
@@ -78,14 +78,13 @@ int maxpool_fwd(const void* x, void* y, uint8_t* argmax, int N, int H, int W, in
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const uint4* __restrict__ dy, const uint2* __restrict__ am,
                                                            uint4* __restrict__ dx, int N, int H, int W, int CV, int Ho,
                                                            int Wo, int kh, int kw, int sh, int sw, int ph, int pw) {
-  const long total = (long)N * H * W * CV;
-  for (long v = (long)blockIdx.x * 256 + threadIdx.x; v < total; v += (long)gridDim.x * 256) {
-    const int cv = (int)(v % CV);
-    long p = v / CV;
-    const int w = (int)(p % W);
-    p /= W;
-    const int h = (int)(p % H);
-    const int n = (int)(p / H);
+  const uint32_t total = (uint32_t)N * H * W * CV;  // < 2^31 (launcher): 32-bit index math
+  for (uint32_t v = blockIdx.x * 256u + threadIdx.x; v < total; v += gridDim.x * 256u) {
+    const uint32_t q = v / (uint32_t)CV, cv = v - q * (uint32_t)CV;
+    const uint32_t q2 = q / (uint32_t)W;
+    const int w = (int)(q - q2 * (uint32_t)W);
+    const int h = (int)(q2 % (uint32_t)H);
+    const int n = (int)(q2 / (uint32_t)H);
     float acc[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[i] = 0.f;
@@ -118,6 +117,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const uint4* __restric
 int maxpool_bwd(const void* dy, const uint8_t* argmax, void* dx, int N, int H, int W, int C, int Ho, int Wo, int kh,
                 int kw, int sh, int sw, int ph, int pw, hipStream_t s) {
   const long total = (long)N * H * W * (C / 8);
+  if (total >= (1L << 31)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(pgrid(total)), dim3(256), 0, s, (const uint4*)dy, (const uint2*)argmax,
                      (uint4*)dx, N, H, W, C / 8, Ho, Wo, kh, kw, sh, sw, ph, pw);
   return (int)hipGetLastError();

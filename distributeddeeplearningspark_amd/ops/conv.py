@@ -145,6 +145,7 @@ def _dgrad_as_forward(g: ConvGeometry):
 
 
 _KC_DGRAD = _os.environ.get("DDL_DGRAD_KC", "1") != "0"
+_WIDE_WGRAD = _os.environ.get("DDL_WGRAD_WIDE", "1") != "0"
 
 
 def flip_filter(w):
@@ -210,6 +211,11 @@ def conv_wgrad_native(dy, x, g: ConvGeometry, gw):
     gw2 = gw.view(g.Co, g.T * g.Ci)
     if g.is_pointwise:
         G.linear_wgrad(dy.view(g.M, g.Co), x.view(g.M, g.Ci), gw2)
+    elif g.implicit_wgrad and g.Ci < 128 and _WIDE_WGRAD:
+        # narrow inputs (64 channels): a 128-wide tile spans two taps, so the tap is resolved per
+        # 16-B vector (GATHER8) instead of per tile — twice the MFMA work per LDS fragment read
+        G.gemm(dy, x, gw2, g.Co, g.T * g.Ci, g.M, G.RC, G.RC_GATHER8, g.Co, 0, g.T * g.Ci, G.EPI_F32, beta=1.0,
+               geom=g.fwd_geom, bn_cap=128)
     elif g.implicit_wgrad:
         G.gemm(dy, x, gw2, g.Co, g.T * g.Ci, g.M, G.RC, G.RC_GATHER, g.Co, 0, g.T * g.Ci, G.EPI_F32, beta=1.0,
                geom=g.fwd_geom, bn_cap=min(128, g.Ci))

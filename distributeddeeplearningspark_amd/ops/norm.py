@@ -58,8 +58,8 @@ def new_stats_workspace(C_, device):
 
 
 def partials_workspace(M, C_, device):
-    """Zeroed [32, 2, C] shard rows a bn_stats / bn_bwd_reduce sweep accumulates into (atomics)."""
-    return new_stats_workspace(C_, device)
+    """[S, 2, C] partial-sum rows written (not accumulated) by a bn_stats / bn_bwd_reduce sweep."""
+    return torch.empty((C().bn_partial_rows(M, C_), 2, C_), dtype=torch.float32, device=device)
 
 
 def reset_workspaces(device):
