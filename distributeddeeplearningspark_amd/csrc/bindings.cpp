@@ -54,8 +54,7 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
           int64_t k_split, double alpha, double beta, c10::optional<at::Tensor> bias,
           c10::optional<at::Tensor> resid, int64_t ldr, int64_t relu, c10::optional<py::dict> geom,
           c10::optional<py::dict> outmap, int64_t b_kdiv, int64_t b_tap_stride,
-          c10::optional<at::Tensor> stats, c10::optional<at::Tensor> aux, double drop_p, int64_t drop_seed,
-          c10::optional<at::Tensor> bnb) {
+          c10::optional<at::Tensor> stats, c10::optional<at::Tensor> aux, double drop_p, int64_t drop_seed) {
   CHECK_CUDA(a);
   CHECK_CUDA(b);
   CHECK_CUDA(c);
@@ -73,7 +72,7 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
   TORCH_CHECK(tile >= 0 && tile <= kTileStream, "gemm: bad tile id");
   if (tile == kTileStream) {
     TORCH_CHECK(a_mode == OP_KC && (b_mode == OP_KC || b_mode == OP_RC) && epi == EPI_BF16 && !outmap.has_value() &&
-                    (relu <= ACT_RELU || relu == ACT_BN_BWD) && drop_p == 0.0 && beta == 0.0 && k_split >= K,
+                    relu <= ACT_RELU && drop_p == 0.0 && beta == 0.0 && k_split >= K,
                 "gemm stream: KC x (KC|RC) operands, bf16 epilogue without GELU/dropout/outmap/beta/split-K");
     TORCH_CHECK(gemm_stream_panel((int)N, (int)K) > 0, "gemm stream: unsupported (N, K) = (", N, ", ", K, ")");
     TORCH_CHECK(ldc % 8 == 0 && ((uintptr_t)c.data_ptr() % 16) == 0, "gemm stream: 16-B aligned output rows");
@@ -106,19 +105,11 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
   p.b_tap_stride = b_tap_stride;
   p.alpha = (float)alpha;
   p.beta = (float)beta;
-  TORCH_CHECK(relu >= ACT_NONE && relu <= ACT_BN_BWD, "gemm: bad activation code");
+  TORCH_CHECK(relu >= ACT_NONE && relu <= ACT_GELU_BWD, "gemm: bad activation code");
   TORCH_CHECK(epi == EPI_BF16 || (relu == 0 && drop_p == 0.0), "gemm: activation/dropout need the bf16 epilogue");
   p.relu = (int)relu;
-  if (relu == ACT_BN_BWD) {
-    TORCH_CHECK(bnb.has_value() && stats.has_value() && !outmap.has_value() && !resid.has_value(),
-                "gemm BN-backward epilogue: needs bnb [3][N] and stats, no outmap / residual");
-    CHECK_CUDA(*bnb);
-    CHECK_F32(*bnb);
-    TORCH_CHECK(bnb->numel() >= 3 * N, "gemm: bnb must hold scale, shift, mean ([3][N])");
-    p.bnb = bnb->data_ptr<float>();
-  }
   if (relu >= ACT_GELU) {
-    TORCH_CHECK(aux.has_value(), "gemm: GELU / BN-backward epilogues need the aux tensor");
+    TORCH_CHECK(aux.has_value(), "gemm: GELU epilogues need the aux (pre-activation) tensor");
     CHECK_CUDA(*aux);
     CHECK_BF16(*aux);
     TORCH_CHECK(aux->numel() >= (M - 1) * ldc + N && ((uintptr_t)aux->data_ptr() % 16) == 0, "gemm: aux size/alignment");
@@ -192,12 +183,11 @@ PYBIND11_MODULE(_C, m) {
         py::arg("beta") = 0.0, py::arg("bias") = py::none(), py::arg("resid") = py::none(), py::arg("ldr") = 0,
         py::arg("relu") = false, py::arg("geom") = py::none(), py::arg("outmap") = py::none(),
         py::arg("b_kdiv") = 0, py::arg("b_tap_stride") = 0, py::arg("stats") = py::none(),
-        py::arg("aux") = py::none(), py::arg("drop_p") = 0.0, py::arg("drop_seed") = 0, py::arg("bnb") = py::none());
+        py::arg("aux") = py::none(), py::arg("drop_p") = 0.0, py::arg("drop_seed") = 0);
   m.attr("ACT_NONE") = (int)ACT_NONE;
   m.attr("ACT_RELU") = (int)ACT_RELU;
   m.attr("ACT_GELU") = (int)ACT_GELU;
   m.attr("ACT_GELU_BWD") = (int)ACT_GELU_BWD;
-  m.attr("ACT_BN_BWD") = (int)ACT_BN_BWD;
   m.attr("OP_KC") = (int)OP_KC;
   m.attr("OP_RC") = (int)OP_RC;
   m.attr("OP_KC_GATHER") = (int)OP_KC_GATHER;

@@ -79,14 +79,9 @@ struct GemmParams {
   uint32_t drop_thresh;
   float drop_scale;
   unsigned long long drop_seed;
-  // ACT_BN_BWD (data-gradient GEMM feeding a BatchNorm backward): aux = the BN input x (bf16,
-  // [M][ldc]), bnb = [3][N] fp32 (scale, shift, mean).  The stored output is the ReLU-masked
-  // gradient d' = d * (x*scale + shift > 0) and `stats` accumulates (sum d', sum d' * (x - mean)),
-  // i.e. the BN backward reduction rides in the epilogue instead of a separate sweep over d and x.
-  const float* bnb;
 };
 
-enum Activation : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_GELU_BWD = 3, ACT_BN_BWD = 4 };
+enum Activation : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_GELU_BWD = 3 };
 
 constexpr int kStatShards = 32;
 constexpr int kTile256 = 4;     // tile id of the 256x256 ping-pong kernel (ddl_gemm256.h)

@@ -256,29 +256,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] += (n + e < p.N) ? p.bias[n + e] : 0.f;
         }
-        float bnx[4] = {0.f, 0.f, 0.f, 0.f}, bnmu[4] = {0.f, 0.f, 0.f, 0.f};
-        if (p.relu == ACT_BN_BWD) {  // BN backward: ReLU mask recomputed from the BN input x (= aux)
-          const bf16_t* ax = reinterpret_cast<const bf16_t*>(p.aux) + rowoff + n;
-          if (full) {
-            const uint2 u = *reinterpret_cast<const uint2*>(ax);
-            bnx[0] = __uint_as_float(u.x << 16);
-            bnx[1] = __uint_as_float(u.x & 0xffff0000u);
-            bnx[2] = __uint_as_float(u.y << 16);
-            bnx[3] = __uint_as_float(u.y & 0xffff0000u);
-          } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              if (n + e < p.N) bnx[e] = bf2f(ax[e]);
-          }
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            if (n + e >= p.N) continue;
-            const float sc = p.bnb[n + e], sh = p.bnb[p.N + n + e];
-            bnmu[e] = p.bnb[2 * p.N + n + e];
-            if (!(bnx[e] * sc + sh > 0.f)) v[e] = 0.f;
-          }
-        }
-        if (p.relu == ACT_GELU || p.relu == ACT_GELU_BWD) {  // transformer FFN: GELU fwd (saving the pre-activation) or its gradient
+        if (p.relu >= ACT_GELU) {  // transformer FFN: GELU fwd (saving the pre-activation) or its gradient
           bf16_t* ax = reinterpret_cast<bf16_t*>(p.aux) + (long)m * p.ldc + n;
           if (p.relu == ACT_GELU) {
             bf16_t pa[4];
@@ -328,7 +306,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
           o[e] = f2bf(v[e]);
           const float rr = (n + e < p.N) ? bf2f(o[e]) : 0.f;
           s1[j][e] += rr;
-          s2[j][e] += p.relu == ACT_BN_BWD ? rr * (bnx[e] - bnmu[e]) : rr * rr;
+          s2[j][e] += rr * rr;
         }
         bf16_t* c = reinterpret_cast<bf16_t*>(p.c) + rowoff + n;
         if (full) {

@@ -152,16 +152,6 @@ __global__ __launch_bounds__(gst::THREADS, 2) void gemm_stream_kernel(const Gemm
 #pragma unroll
   for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
   const int oc = threadIdx.x % CF::OCPR, orow = threadIdx.x / CF::OCPR;
-  // ACT_BN_BWD: per-column BN parameters of the 8 columns this thread always reads out
-  const bool bnbwd = p.relu == ACT_BN_BWD;
-  float bsc[8], bsh[8], bmu[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int col = n0 + oc * 8 + e;
-    bsc[e] = bnbwd ? p.bnb[col] : 0.f;
-    bsh[e] = bnbwd ? p.bnb[p.N + col] : 0.f;
-    bmu[e] = bnbwd ? p.bnb[2 * p.N + col] : 0.f;
-  }
   bf16_t* __restrict__ Cout = reinterpret_cast<bf16_t*>(p.c);
 
   for (int i = 0; i < nloc; ++i) {
@@ -235,30 +225,10 @@ __global__ __launch_bounds__(gst::THREADS, 2) void gemm_stream_kernel(const Gemm
     for (int ps = 0; ps < CF::S; ++ps) {
       const int r = orow + ps * CF::RPP;
       const int m = m0 + r;
-      uint4 v = *reinterpret_cast<const uint4*>(stg + r * (CF::NB * 2) + ((oc ^ sw<CF::OCPR>(r)) << 4));
+      const uint4 v = *reinterpret_cast<const uint4*>(stg + r * (CF::NB * 2) + ((oc ^ sw<CF::OCPR>(r)) << 4));
       if (m < p.M) {
-        if (bnbwd) {  // d' = d * (x*scale + shift > 0); stats (sum d', sum d'(x - mean)) of the stored d'
-          const uint4 xv = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(p.aux) + (long)m * p.ldc +
-                                                           n0 + oc * 8);
-          const uint32_t xw[4] = {xv.x, xv.y, xv.z, xv.w};
-          uint32_t dw[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float x0 = __uint_as_float(xw[q] << 16), x1 = __uint_as_float(xw[q] & 0xffff0000u);
-            const bool k0 = x0 * bsc[2 * q] + bsh[2 * q] > 0.f, k1 = x1 * bsc[2 * q + 1] + bsh[2 * q + 1] > 0.f;
-            dw[q] = (k0 ? (dw[q] & 0xffffu) : 0u) | (k1 ? (dw[q] & 0xffff0000u) : 0u);
-            const float d0 = __uint_as_float(dw[q] << 16), d1 = __uint_as_float(dw[q] & 0xffff0000u);
-            s1[2 * q] += d0;
-            s2[2 * q] += d0 * (x0 - bmu[2 * q]);
-            s1[2 * q + 1] += d1;
-            s2[2 * q + 1] += d1 * (x1 - bmu[2 * q + 1]);
-          }
-          v = make_uint4(dw[0], dw[1], dw[2], dw[3]);
-          *reinterpret_cast<uint4*>(Cout + (long)m * p.ldc + n0 + oc * 8) = v;
-        } else {
-          *reinterpret_cast<uint4*>(Cout + (long)m * p.ldc + n0 + oc * 8) = v;
-        }
-        if (p.stats && !bnbwd) {
+        *reinterpret_cast<uint4*>(Cout + (long)m * p.ldc + n0 + oc * 8) = v;
+        if (p.stats) {
           const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
@@ -368,9 +338,7 @@ int launch_gemm_stream(const GemmParams& p, int epi, hipStream_t s) {
   int nb = gemm_stream_panel(p.N, p.K);
   if (p.resid && p.K == 128 && nb == 256) nb = 128;  // 256-wide panel + residual prefetch would spill
   const bool ok = nb && epi == EPI_BF16 && p.a_mode == OP_KC && (p.b_mode == OP_KC || p.b_mode == OP_RC) &&
-                  !p.om.enabled && !p.drop_thresh &&
-                  (((p.relu == ACT_NONE || p.relu == ACT_RELU) && !p.aux) ||
-                   (p.relu == ACT_BN_BWD && p.aux && p.bnb && !p.resid && (uintptr_t)p.aux % 16 == 0)) &&
+                  !p.om.enabled && !p.aux && !p.drop_thresh && (p.relu == ACT_NONE || p.relu == ACT_RELU) &&
                   p.beta == 0.f && p.k_split >= p.K && p.lda % 8 == 0 && p.ldc % 8 == 0 &&
                   (p.b_mode == OP_RC || p.ldb % 8 == 0) && (!p.resid || p.ldr % 4 == 0) &&
                   ((uintptr_t)p.a % 16 == 0) && ((uintptr_t)p.c % 16 == 0) &&

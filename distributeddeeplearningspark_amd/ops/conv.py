@@ -101,16 +101,10 @@ def _im2col(x, g: ConvGeometry, taps_h, taps_w, ho, wo, sh, sw, kpad):
     return col
 
 
-def conv_fwd_native(x, w, g: ConvGeometry, bias=None, relu=False, stats=None, bn_bwd=None):
-    """``bn_bwd = (bn_input, [scale; shift; mean])``: implicit-GEMM path only (see dgrad_fuses_bn)."""
+def conv_fwd_native(x, w, g: ConvGeometry, bias=None, relu=False, stats=None):
     y = torch.empty((g.N, g.Ho, g.Wo, g.Co), dtype=torch.bfloat16, device=x.device)
     y2 = y.view(g.M, g.Co)
-    if bn_bwd is not None:
-        if not (g.implicit_fwd and not g.is_pointwise):
-            raise ValueError("BN-backward epilogue fusion needs the implicit-GEMM forward path")
-        G.gemm(x, w, y2, g.M, g.Co, g.T * g.Ci, G.KC_GATHER, G.KC, 0, g.T * g.Ci, g.Co, G.EPI_BF16,
-               relu=G.ACT_BN_BWD, aux=bn_bwd[0], bnb=bn_bwd[1], geom=g.fwd_geom, stats=stats)
-    elif g.is_pointwise:
+    if g.is_pointwise:
         G.linear_fwd(x.view(g.M, g.Ci), w.view(g.Co, g.Ci), bias=bias, relu=relu, out=y2, stats=stats)
     elif g.implicit_fwd or g.gather8_fwd:
         G.gemm(x, w, y2, g.M, g.Co, g.T * g.Ci, G.KC_GATHER if g.implicit_fwd else G.KC_GATHER8, G.KC, 0,
@@ -152,10 +146,6 @@ def _dgrad_as_forward(g: ConvGeometry):
 
 _KC_DGRAD = _os.environ.get("DDL_DGRAD_KC", "1") != "0"
 _WIDE_WGRAD = _os.environ.get("DDL_WGRAD_WIDE", "1") != "0"
-# BN-backward reduction in the dgrad epilogue (ACT_BN_BWD): numerically verified, but measured
-# SLOWER on ResNet-50 (8,658 vs 9,045 img/s: +2 ms of epilogue loads / atomics in the GEMMs against
-# -0.7 ms of bn_bwd_reduce sweeps), so opt-in (DDL_BN_BWD_EPILOGUE=1) until the epilogue is cheaper.
-_BN_EPI = _os.environ.get("DDL_BN_BWD_EPILOGUE", "0") == "1"
 
 
 def flip_filter(w):
@@ -163,28 +153,9 @@ def flip_filter(w):
     return w.flip(1, 2).permute(3, 1, 2, 0).contiguous()
 
 
-def dgrad_fuses_bn(g: ConvGeometry) -> bool:
-    """Whether conv_dgrad_native can fold a following BatchNorm+ReLU backward reduction into its
-    epilogue (single GEMM writing dx in natural layout: 1x1 convs and stride-1 dgrad-as-forward)."""
-    return _BN_EPI and (g.is_pointwise or _dgrad_as_forward(g) is not None)
-
-
-def conv_dgrad_native(dy, w, g: ConvGeometry, resid=None, bn_bwd=None, stats=None):
-    """dx = conv^T(dy, w) (+ resid, fused into the epilogue when the layout allows).
-
-    ``bn_bwd = (x_bn, bnb)`` with ``stats`` (zeroed [32, 2, Ci]): dx is the input gradient of a
-    ReLU-BatchNorm whose input was ``x_bn``; the epilogue stores the ReLU-masked gradient and
-    accumulates the BN backward sums (only where ``dgrad_fuses_bn(g)``)."""
+def conv_dgrad_native(dy, w, g: ConvGeometry, resid=None):
+    """dx = conv^T(dy, w) (+ resid, fused into the epilogue when the layout allows)."""
     dev = dy.device
-    if bn_bwd is not None:
-        if not dgrad_fuses_bn(g) or resid is not None:
-            raise ValueError("BN-backward fusion not available for this data-gradient")
-        if g.is_pointwise:
-            dx = torch.empty((g.N, g.H, g.W, g.Ci), dtype=torch.bfloat16, device=dev)
-            G.linear_dgrad(dy.view(g.M, g.Co), w.view(g.Co, g.Ci), out=dx.view(-1, g.Ci),
-                           bn_bwd=(bn_bwd[0].view(-1, g.Ci), bn_bwd[1]), stats=stats)
-            return dx
-        return conv_fwd_native(dy.contiguous(), flip_filter(w), _dgrad_as_forward(g), bn_bwd=bn_bwd, stats=stats)
     if resid is None:
         g2 = _dgrad_as_forward(g)
         if g2 is not None:

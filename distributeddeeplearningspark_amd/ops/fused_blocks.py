@@ -25,7 +25,7 @@ from .norm import new_stats_workspace, partials_workspace
 class _ConvBNState:
     """Per-(conv,BN) forward results needed by the backward."""
 
-    __slots__ = ("g", "yc", "y", "mean", "invstd", "scale", "shift", "ssm", "mode", "mask")
+    __slots__ = ("g", "yc", "y", "mean", "invstd", "scale", "shift", "mode", "mask")
 
 
 def _bn_forward(layer_bn, yc, stats, resid, relu, training, mask=None):
@@ -36,14 +36,14 @@ def _bn_forward(layer_bn, yc, stats, resid, relu, training, mask=None):
     gamma = None if bn.gamma is None else bn.gamma.master
     beta = None if bn.beta is None else bn.beta.master
     rm, rv = bn._states["moving_mean"], bn._states["moving_variance"]
-    # scale / shift / mean as rows of ONE [3, C] buffer: the BN-backward GEMM epilogue takes it whole
-    ssm = torch.empty((3, Cc), dtype=torch.float32, device=dev)
-    scale, shift, mean = ssm[0], ssm[1], ssm[2]
+    scale = torch.empty(Cc, dtype=torch.float32, device=dev)
+    shift = torch.empty(Cc, dtype=torch.float32, device=dev)
+    mean = torch.empty(Cc, dtype=torch.float32, device=dev)
     invstd = torch.empty(Cc, dtype=torch.float32, device=dev)
     C().bn_finalize(stats, M, Cc, gamma, beta, bn.epsilon, 1.0 - bn.momentum, rm, rv, mean, invstd, scale, shift)
     y = torch.empty_like(yc)
     C().bn_apply(yc, scale, shift, resid, y, Cc, relu, mask)
-    return y, mean, invstd, scale, shift, ssm
+    return y, mean, invstd, scale, shift
 
 
 def convbn_forward(unit, x, resid=None, relu=True):
@@ -62,25 +62,9 @@ def convbn_forward(unit, x, resid=None, relu=True):
     Co = yc.shape[-1]
     bits = relu and resid is not None and Co & (Co - 1) == 0
     st.mask = torch.empty(-(-yc.numel() // 512) * 64, dtype=torch.uint8, device=yc.device) if bits else None
-    st.y, st.mean, st.invstd, st.scale, st.shift, st.ssm = _bn_forward(bn, yc, stats, resid, relu, True, st.mask)
+    st.y, st.mean, st.invstd, st.scale, st.shift = _bn_forward(bn, yc, stats, resid, relu, True, st.mask)
     st.mode = 0 if not relu else (2 if resid is None else (3 if bits else 1))
     return st
-
-
-def bn_backward_from_stats(unit, st, dprime, stats):
-    """BN backward when the producing data-gradient GEMM already applied the ReLU mask and
-    accumulated (sum d', sum d'(x - mean)) in its epilogue (ACT_BN_BWD): finalize + dx sweep."""
-    bn = unit.bn
-    Cc = st.yc.shape[-1]
-    M = st.yc.numel() // Cc
-    coef = torch.empty(3 * Cc, dtype=torch.float32, device=dprime.device)
-    C().bn_bwd_finalize(stats, M, Cc, None if bn.gamma is None else bn.gamma.master, st.mean, st.invstd,
-                        None if bn.gamma is None else bn.gamma.grad, None if bn.beta is None else bn.beta.grad, coef)
-    dyc = torch.empty_like(dprime)
-    C().bn_bwd_dx(dprime, st.yc, None, st.scale, st.shift, coef, dyc, None, Cc, 0)
-    if bn.grad_hook is not None:
-        bn.grad_hook()
-    return dyc
 
 
 def bn_backward(unit, st, dy, want_dres):
@@ -111,23 +95,6 @@ def conv_backward(unit, st, dyc, x, need_dx, resid=None):
     return CV.conv_dgrad_native(dyc, conv.kernel.data, st.g, resid=resid)
 
 
-def conv_bn_backward(unit, st, dyc, x, prev, prev_st):
-    """conv backward whose data-gradient is the input gradient of the ReLU-BN unit ``prev``:
-    when the dgrad GEMM can carry it, the BN backward reduction runs in that GEMM's epilogue
-    (no separate sweep over dy and the BN input); returns the gradient entering prev's conv."""
-    if prev_st.mode == 2 and CV.dgrad_fuses_bn(st.g):
-        conv = unit.conv
-        CV.conv_wgrad_native(dyc, x, st.g, conv.kernel.grad)
-        if conv.grad_hook is not None:
-            conv.grad_hook()
-        stats = new_stats_workspace(prev_st.yc.shape[-1], dyc.device)
-        dprime = CV.conv_dgrad_native(dyc, conv.kernel.data, st.g, bn_bwd=(prev_st.yc, prev_st.ssm), stats=stats)
-        return bn_backward_from_stats(prev, prev_st, dprime, stats)
-    d = conv_backward(unit, st, dyc, x, True)
-    out, _ = bn_backward(prev, prev_st, d, False)
-    return out
-
-
 class _BottleneckFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, anchor, block):
@@ -149,8 +116,10 @@ class _BottleneckFn(torch.autograd.Function):
         s_down, s1, s2, s3 = ctx.states
         dout = dout.contiguous()
         d3c, dsc = bn_backward(b.c3, s3, dout, want_dres=True)
-        d2c = conv_bn_backward(b.c3, s3, d3c, s2.y, b.c2, s2)
-        d1c = conv_bn_backward(b.c2, s2, d2c, s1.y, b.c1, s1)
+        d2 = conv_backward(b.c3, s3, d3c, s2.y, True)
+        d2c, _ = bn_backward(b.c2, s2, d2, False)
+        d1 = conv_backward(b.c2, s2, d2c, s1.y, True)
+        d1c, _ = bn_backward(b.c1, s1, d1, False)
         if s_down is not None:
             ddc, _ = bn_backward(b.down, s_down, dsc, False)
             dsc = conv_backward(b.down, s_down, ddc, x, ctx.needs_dx)
@@ -214,7 +183,7 @@ class _StemS2DFn(torch.autograd.Function):
         yc = CV.conv_fwd_native(xs, w4, g, stats=stats)
         st = _ConvBNState()
         st.g, st.yc = g, yc
-        st.y, st.mean, st.invstd, st.scale, st.shift, st.ssm = _bn_forward(unit.bn, yc, stats, None, relu, True)
+        st.y, st.mean, st.invstd, st.scale, st.shift = _bn_forward(unit.bn, yc, stats, None, relu, True)
         st.mode = 2 if relu else 0
         ctx.unit, ctx.st, ctx.cc = unit, st, Cc
         ctx.save_for_backward(xs)
@@ -257,7 +226,7 @@ class _ConvBNFn(torch.autograd.Function):
         yc = CV.conv_fwd_native(x, w, g, stats=stats)
         st = _ConvBNState()
         st.g, st.yc = g, yc
-        st.y, st.mean, st.invstd, st.scale, st.shift, st.ssm = _bn_forward(unit.bn, yc, stats, None, relu, True)
+        st.y, st.mean, st.invstd, st.scale, st.shift = _bn_forward(unit.bn, yc, stats, None, relu, True)
         st.mode = 2 if relu else 0
         ctx.unit, ctx.st, ctx.w = unit, st, w
         ctx.save_for_backward(x)

@@ -53,9 +53,7 @@ def use_stream(M, N, K, a_mode, b_mode, epi, lda, ldc, *, outmap=None, aux=None,
     (memory-bound; the 128-tile kernel writes 32-B segments and re-stages the weights per tile)."""
     if _USE_STREAM == "0" or a_mode != KC or b_mode not in (KC, RC) or epi != EPI_BF16:
         return False
-    bn_bwd = int(relu) == ACT_BN_BWD and aux is not None and resid is None
-    if outmap is not None or (aux is not None and not bn_bwd) or drop_p or (int(relu) > ACT_RELU and not bn_bwd) \
-            or beta:
+    if outmap is not None or aux is not None or drop_p or int(relu) > ACT_RELU or beta:
         return False
     if M < 16384 or not stream_panel(N, K) or lda % 8 or ldc % 8 or (resid is not None and ldr % 4):
         return False
@@ -102,7 +100,7 @@ def choose_split(M: int, N: int, K: int, tile: int, allow: bool) -> int:
 
 def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, beta=0.0, bias=None, resid=None,
          ldr=0, relu=False, geom=None, outmap=None, b_kdiv=0, b_tap_stride=0, stats=None, tile=None, k_split=None,
-         bn_cap=128, aux=None, drop_p=0.0, drop_seed=0, bnb=None):
+         bn_cap=128, aux=None, drop_p=0.0, drop_seed=0):
     """Raw launcher with automatic tile / split-K choice.
 
     With ``epi == EPI_F32`` and a split-K decomposition the launch switches to the
@@ -125,14 +123,14 @@ def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, bet
             raise ValueError("split-K fp32 gemm supports beta in {0,1} (beta=0 needs a zeroed C)")
         epi = EPI_F32_ATOMIC
     C().gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, tile, k_split, alpha, beta, bias, resid, ldr,
-             int(relu), geom, outmap, b_kdiv, b_tap_stride, stats, aux, float(drop_p), int(drop_seed), bnb)
+             int(relu), geom, outmap, b_kdiv, b_tap_stride, stats, aux, float(drop_p), int(drop_seed))
     return c
 
 
 # ----------------------------------------------------------------------------------------
 # 2-D helpers (row-major tensors)
 # ----------------------------------------------------------------------------------------
-ACT_NONE, ACT_RELU, ACT_GELU, ACT_GELU_BWD, ACT_BN_BWD = 0, 1, 2, 3, 4
+ACT_NONE, ACT_RELU, ACT_GELU, ACT_GELU_BWD = 0, 1, 2, 3
 
 
 def linear_fwd(x2, w, bias=None, relu=False, out=None, resid=None, stats=None, act=None, aux=None, drop_p=0.0,
@@ -150,22 +148,17 @@ def linear_fwd(x2, w, bias=None, relu=False, out=None, resid=None, stats=None, a
                 drop_seed=drop_seed)
 
 
-def linear_dgrad(dy, w, out=None, resid=None, gelu_pre=None, stats=None, bn_bwd=None):
+def linear_dgrad(dy, w, out=None, resid=None, gelu_pre=None, stats=None):
     """dx[M,K] = dy[M,N] @ w[N,K] (* gelu'(gelu_pre)) (+resid) -> bf16 (w read row-contiguous).
 
-    ``stats`` ([32, 2, K] fp32, zeroed): per-column sums / sums of squares of the output.
-    ``bn_bwd = (x, bnb)``: the output feeds a BatchNorm+ReLU backward whose input was ``x``
-    ([M, K] bf16) and ``bnb = [scale; shift; mean]`` ([3, K] fp32): the ReLU mask is applied
-    in the epilogue and ``stats`` receives (sum d', sum d'(x - mean)) instead."""
+    ``stats`` ([32, 2, K] fp32, zeroed): per-column sums / sums of squares of the output."""
     M, N = dy.shape
     K = w.shape[1]
     if out is None:
         out = torch.empty((M, K), dtype=torch.bfloat16, device=dy.device)
-    act, aux, bnb = (ACT_GELU_BWD if gelu_pre is not None else ACT_NONE), gelu_pre, None
-    if bn_bwd is not None:
-        act, aux, bnb = ACT_BN_BWD, bn_bwd[0], bn_bwd[1]
     return gemm(dy, w, out, M, K, N, KC, RC, dy.stride(0), w.stride(0), out.stride(0), EPI_BF16, resid=resid,
-                ldr=(resid.stride(0) if resid is not None else 0), relu=act, aux=aux, stats=stats, bnb=bnb)
+                ldr=(resid.stride(0) if resid is not None else 0),
+                relu=(ACT_GELU_BWD if gelu_pre is not None else ACT_NONE), aux=gelu_pre, stats=stats)
 
 
 def linear_wgrad(dy, x2, gw):
