@@ -53,6 +53,7 @@ def _common_flags():
         "-I", str(CSRC / "include"),
         "-Wno-unused-result",
         "-Wno-unused-command-line-argument",
+        *os.environ.get("DDL_HIPCC_FLAGS", "").split(),  # experiments, e.g. -DDDL_DMA_MIN_BLOCKS=4
     ]
 
 

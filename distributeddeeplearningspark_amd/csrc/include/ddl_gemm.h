@@ -28,6 +28,11 @@ enum EpilogueMode : int {
   EPI_BF16 = 0,        // bf16 store of alpha*acc (+bias)(+resid)(relu)
   EPI_F32 = 1,         // fp32 store of alpha*acc + beta*C
   EPI_F32_ATOMIC = 2,  // fp32 atomicAdd of alpha*acc (split-K)
+  // EPI_BF16 restricted to alpha / bias / ReLU / BN statistics (no residual, output map, GELU
+  // or dropout).  A separate instantiation because the full epilogue's live state raises the
+  // kernel's VGPR allocation (134 -> occupancy 3 blocks/CU for the 128x128 conv kernel); the
+  // launcher picks it whenever the call does not use the extra features.
+  EPI_BF16_LITE = 3,
 };
 
 constexpr int kMaxTaps = 64;

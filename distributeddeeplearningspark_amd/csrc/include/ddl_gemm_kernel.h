@@ -19,6 +19,12 @@ namespace ddl {
 
 constexpr int BK = 64;
 constexpr int NTHREADS = 256;
+// Minimum resident blocks per CU the LDS-DMA kernel is compiled for.  4 caps the bf16-output
+// kernels at 128 VGPRs (the 128x128 conv kernel otherwise takes 134 -> 3 blocks/CU): one more
+// block per CU to hide the single-stage DMA latency is worth +6 % on ResNet-50.  The fp32
+// weight-gradient kernels keep 2 (at 128 VGPRs their RC fragments spill).
+template <int EPI>
+constexpr int dma_min_blocks() { return (EPI == EPI_F32 || EPI == EPI_F32_ATOMIC) ? 2 : 4; }
 
 // Simple, exact division helper (used where the divisor is a power of two or tiny loops are fine)
 __device__ __forceinline__ void pix_decompose(uint32_t p, uint32_t ho, uint32_t wo, int& n, int& i, int& j) {
@@ -199,7 +205,9 @@ template <int RM, int RN, int EPI>
 __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[RM][RN], const int mb, const int nb,
                                               const int lane, const int bid) {
   // ---------------------------------- epilogue ----------------------------------
-  if constexpr (EPI != EPI_BF16) {
+  constexpr bool BF = EPI == EPI_BF16 || EPI == EPI_BF16_LITE;
+  constexpr bool LITE = EPI == EPI_BF16_LITE;
+  if constexpr (!BF) {
     // fp32 (weight-gradient) epilogue, D orientation: acc[i][j][e] = C[m0+wm0+16i+4(lane>>4)+e][n0+wn0+16j+(lane&15)]
     // -> each atomic wave-instruction covers 4 rows x 64 contiguous bytes.
 #pragma unroll
@@ -230,14 +238,14 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
   for (int j = 0; j < RN; ++j)
 #pragma unroll
     for (int e = 0; e < 4; ++e) s1[j][e] = s2[j][e] = 0.f;
-  const bool vec_ok = (p.ldc % 4) == 0 && (!p.resid || (p.ldr % 4) == 0);
+  const bool vec_ok = (p.ldc % 4) == 0 && (LITE || !p.resid || (p.ldr % 4) == 0);
 #pragma unroll
   for (int i = 0; i < RM; ++i) {
     const int m = mb + 16 * i + mrow;
     if (m >= p.M) continue;
     long rowoff;
     int nn = 0, ii = 0, jj = 0;
-    if (p.om.enabled) {
+    if (!LITE && p.om.enabled) {
       pix_decompose((uint32_t)m, p.om.gh, p.om.gw, nn, ii, jj);
       rowoff = ((long)(nn * p.om.hy + ii * p.om.so + p.om.oh) * p.om.wy + jj * p.om.so + p.om.ow) * p.ldc;
     } else {
@@ -251,12 +259,12 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
       float v[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * p.alpha;
-      if constexpr (EPI == EPI_BF16) {
+      if constexpr (BF) {
         if (p.bias) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] += (n + e < p.N) ? p.bias[n + e] : 0.f;
         }
-        if (p.relu >= ACT_GELU) {  // transformer FFN: GELU fwd (saving the pre-activation) or its gradient
+        if (!LITE && p.relu >= ACT_GELU) {  // transformer FFN: GELU fwd (saving the pre-activation) or its gradient
           bf16_t* ax = reinterpret_cast<bf16_t*>(p.aux) + (long)m * p.ldc + n;
           if (p.relu == ACT_GELU) {
             bf16_t pa[4];
@@ -276,13 +284,13 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
             for (int e = 0; e < 4; ++e) v[e] *= (n + e < p.N) ? gelu_grad_f(bf2f(ax[e])) : 0.f;
           }
         }
-        if (p.drop_thresh) {
+        if (!LITE && p.drop_thresh) {
           const unsigned long long base = (unsigned long long)m * (unsigned long long)p.N + (unsigned long long)n;
 #pragma unroll
           for (int e = 0; e < 4; ++e)
             v[e] = drop_keep(p.drop_seed, base + e, p.drop_thresh) ? v[e] * p.drop_scale : 0.f;
         }
-        if (p.resid) {
+        if (!LITE && p.resid) {
           const bf16_t* r = reinterpret_cast<const bf16_t*>(p.resid) + (long)m * p.ldr + n;
           if (full) {
             const uint2 rv = *reinterpret_cast<const uint2*>(r);
@@ -333,7 +341,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
           if (n + e < p.N) atomicAdd(c + e, v[e]);
       }
     }
-    if constexpr (EPI == EPI_BF16) {
+    if constexpr (EPI == EPI_BF16) {  // (LITE: no output map)
       if (p.om.enabled && p.om.zero_siblings) {  // this class is the only one with taps: zero the rest
         bf16_t* cb = reinterpret_cast<bf16_t*>(p.c);
         for (int a = 0; a < p.om.so; ++a) {
@@ -356,7 +364,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
       }
     }
   }
-  if constexpr (EPI == EPI_BF16) {
+  if constexpr (BF) {
     if (p.stats) {  // reduce over the 16 rows held by lanes sharing (lane>>4), then one atomic per column
       float* st = p.stats + (long)(bid % kStatShards) * 2 * p.N;
 #pragma unroll
@@ -442,7 +450,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams
       for (int i = 0; i < RM; ++i)
 #pragma unroll
         for (int j = 0; j < RN; ++j) {
-          if constexpr (EPI == EPI_BF16)
+          if constexpr (EPI == EPI_BF16 || EPI == EPI_BF16_LITE)
             acc[i][j] = mfma16x16x32(bf[j], af[i], acc[i][j]);  // D^T: 4 consecutive n per lane (vector stores)
           else
             acc[i][j] = mfma16x16x32(af[i], bf[j], acc[i][j]);  // D: 16 consecutive n per row (coalesced atomics)
@@ -465,7 +473,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams
 // and each block's load latency hides under the others' MFMAs); ST = 2: two stages, the next
 // K-tile's DMA in flight under the current tile's MFMAs (counted vmcnt, raw barriers).
 template <int BM, int BN, int AMODE, int BMODE, int EPI, int ST>
-__global__ __launch_bounds__(NTHREADS, 2) void gemm_dma_kernel(const GemmParams p) {
+__global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_kernel(const GemmParams p) {
   constexpr int WTM = BM / 2, WTN = BN / 2;
   constexpr int RM = WTM / 16, RN = WTN / 16;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
@@ -527,7 +535,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_dma_kernel(const GemmParams 
       for (int i = 0; i < RM; ++i)
 #pragma unroll
         for (int j = 0; j < RN; ++j) {
-          if constexpr (EPI == EPI_BF16)
+          if constexpr (EPI == EPI_BF16 || EPI == EPI_BF16_LITE)
             acc[i][j] = mfma16x16x32(bf[j], af[i], acc[i][j]);
           else
             acc[i][j] = mfma16x16x32(af[i], bf[j], acc[i][j]);
@@ -574,6 +582,11 @@ inline int launch_tile(const GemmParams& p, hipStream_t s) {
     hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, AMODE, BMODE, EPI>), grid, dim3(NTHREADS), lds, s, p);
   }
   return (int)hipGetLastError();
+}
+
+// The bf16 epilogue features a call uses beyond bias / ReLU / statistics.
+inline bool needs_full_epilogue(const GemmParams& p) {
+  return p.om.enabled || p.resid || p.aux || p.drop_thresh || p.relu > ACT_RELU;
 }
 
 template <int AMODE, int BMODE, int EPI>

@@ -2,7 +2,9 @@
 #include "ddl_gemm_kernel.h"
 namespace ddl {
 int launch_gemm_conv(const GemmParams& p, int epi, int tile, hipStream_t s) {
-  if (p.a_mode == OP_KC_GATHER && p.b_mode == OP_KC) return launch_modes<OP_KC_GATHER, OP_KC, EPI_BF16>(p, tile, s);
+  if (p.a_mode == OP_KC_GATHER && p.b_mode == OP_KC)
+    return needs_full_epilogue(p) ? launch_modes<OP_KC_GATHER, OP_KC, EPI_BF16>(p, tile, s)
+                                  : launch_modes<OP_KC_GATHER, OP_KC, EPI_BF16_LITE>(p, tile, s);
   if (p.a_mode == OP_KC_GATHER && p.b_mode == OP_RC_TAPS) return launch_modes<OP_KC_GATHER, OP_RC_TAPS, EPI_BF16>(p, tile, s);
   if (p.a_mode == OP_RC && p.b_mode == OP_RC_GATHER) {
     if (epi == EPI_F32) return launch_modes<OP_RC, OP_RC_GATHER, EPI_F32>(p, tile, s);
