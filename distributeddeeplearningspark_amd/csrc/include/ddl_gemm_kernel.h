@@ -23,8 +23,11 @@ constexpr int NTHREADS = 256;
 // kernels at 128 VGPRs (the 128x128 conv kernel otherwise takes 134 -> 3 blocks/CU): one more
 // block per CU to hide the single-stage DMA latency is worth +6 % on ResNet-50.  The fp32
 // weight-gradient kernels keep 2 (at 128 VGPRs their RC fragments spill).
+#ifndef DDL_WGRAD_MIN_BLOCKS
+#define DDL_WGRAD_MIN_BLOCKS 2
+#endif
 template <int EPI>
-constexpr int dma_min_blocks() { return (EPI == EPI_F32 || EPI == EPI_F32_ATOMIC) ? 2 : 4; }
+constexpr int dma_min_blocks() { return (EPI == EPI_F32 || EPI == EPI_F32_ATOMIC) ? DDL_WGRAD_MIN_BLOCKS : 4; }
 
 // Simple, exact division helper (used where the divisor is a power of two or tiny loops are fine)
 __device__ __forceinline__ void pix_decompose(uint32_t p, uint32_t ho, uint32_t wo, int& n, int& i, int& j) {

@@ -215,10 +215,12 @@ def conv_wgrad_native(dy, x, g: ConvGeometry, gw):
         # narrow inputs (64 channels): a 128-wide tile spans two taps, so the tap is resolved per
         # 16-B vector (GATHER8) instead of per tile — twice the MFMA work per LDS fragment read
         G.gemm(dy, x, gw2, g.Co, g.T * g.Ci, g.M, G.RC, G.RC_GATHER8, g.Co, 0, g.T * g.Ci, G.EPI_F32, beta=1.0,
-               geom=g.fwd_geom, bn_cap=128)
+               geom=g.fwd_geom, bn_cap=128, split_rounds=4)
     elif g.implicit_wgrad:
+        # gathered weight gradients are latency-bound per workgroup: 4 rounds of split-K workgroups
+        # (measured: 3-16 % faster than 2 on the ResNet-50 3x3 / strided layers)
         G.gemm(dy, x, gw2, g.Co, g.T * g.Ci, g.M, G.RC, G.RC_GATHER, g.Co, 0, g.T * g.Ci, G.EPI_F32, beta=1.0,
-               geom=g.fwd_geom, bn_cap=min(128, g.Ci))
+               geom=g.fwd_geom, bn_cap=min(128, g.Ci), split_rounds=4)
     elif g.gather8_wgrad:
         G.gemm(dy, x, gw2, g.Co, g.T * g.Ci, g.M, G.RC, G.RC_GATHER8, g.Co, 0, g.T * g.Ci, G.EPI_F32, beta=1.0,
                geom=g.fwd_geom)

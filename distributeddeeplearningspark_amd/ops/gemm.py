@@ -32,6 +32,9 @@ _USE256 = _os.environ.get("DDL_GEMM256", "auto")
 
 
 _USE_STREAM = _os.environ.get("DDL_GEMM_STREAM", "1")
+# split-K fp32 GEMMs (weight gradients): workgroup rounds to aim for; every split adds one fp32
+# atomic per output element, so more rounds trade atomics for parallelism
+_SPLIT_ROUNDS = float(_os.environ.get("DDL_SPLIT_ROUNDS", "2"))
 
 
 def stream_panel(N: int, K: int) -> int:
@@ -83,8 +86,8 @@ def choose_tile(M: int, N: int, bn_cap: int = 128) -> int:
     return 3
 
 
-def choose_split(M: int, N: int, K: int, tile: int, allow: bool) -> int:
-    """Return k_split (elements, multiple of 64)."""
+def choose_split(M: int, N: int, K: int, tile: int, allow: bool, rounds: float | None = None) -> int:
+    """Return k_split (elements, multiple of 64).  ``rounds``: workgroup rounds to aim for."""
     kfull = max(64, math.ceil(K / 64) * 64)
     if not allow:
         return kfull
@@ -93,14 +96,14 @@ def choose_split(M: int, N: int, K: int, tile: int, allow: bool) -> int:
     per_cu = 1 if tile == TILE256 else 2  # resident workgroups per CU
     if tiles >= per_cu * _CU or K < 1024:
         return kfull
-    splits = min(math.ceil(2 * per_cu * _CU / tiles), max(1, K // 512))
+    splits = min(math.ceil((rounds or _SPLIT_ROUNDS) * per_cu * _CU / tiles), max(1, K // 512))
     ks = math.ceil(K / splits / 64) * 64
     return max(64, ks)
 
 
 def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, beta=0.0, bias=None, resid=None,
          ldr=0, relu=False, geom=None, outmap=None, b_kdiv=0, b_tap_stride=0, stats=None, tile=None, k_split=None,
-         bn_cap=128, aux=None, drop_p=0.0, drop_seed=0):
+         bn_cap=128, aux=None, drop_p=0.0, drop_seed=0, split_rounds=None):
     """Raw launcher with automatic tile / split-K choice.
 
     With ``epi == EPI_F32`` and a split-K decomposition the launch switches to the
@@ -117,7 +120,7 @@ def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, bet
         else:
             tile = choose_tile(M, N, bn_cap)
     if k_split is None:
-        k_split = choose_split(M, N, K, tile, allow=(epi != EPI_BF16))
+        k_split = choose_split(M, N, K, tile, allow=(epi != EPI_BF16), rounds=split_rounds)
     if epi == EPI_F32 and k_split < K:
         if beta not in (0.0, 1.0):
             raise ValueError("split-K fp32 gemm supports beta in {0,1} (beta=0 needs a zeroed C)")
@@ -165,7 +168,10 @@ def linear_wgrad(dy, x2, gw):
     """gw[N,K] += dy[M,N]^T @ x2[M,K]  (fp32 accumulation into the gradient arena)."""
     M, N = dy.shape
     K = x2.shape[1]
-    return gemm(dy, x2, gw, N, K, M, RC, RC, dy.stride(0), x2.stride(0), gw.stride(0), EPI_F32, beta=1.0)
+    # measured on the ResNet-50 1x1 weight gradients: one workgroup round (half the fp32 atomics
+    # of two rounds) is 5-15 % faster — these GEMMs are bound by the split-K atomics, not MFMA
+    return gemm(dy, x2, gw, N, K, M, RC, RC, dy.stride(0), x2.stride(0), gw.stride(0), EPI_F32, beta=1.0,
+                split_rounds=1)
 
 
 def matmul(a, b, trans_a=False, trans_b=False, out=None, alpha=1.0):
