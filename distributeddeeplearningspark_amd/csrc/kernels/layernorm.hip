@@ -28,60 +28,72 @@ __device__ __forceinline__ uint4 pack8f(const float* f) {
                     pack_bf16x2(f[6], f[7]));
 }
 
+// One wave per row, grid-stride over rows; gamma / beta of the lane's columns live in registers
+// (loading them per element per row cost 4x the bytes of the row itself through L1).
 template <int VPL>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, bf16_t* __restrict__ y,
                                                      float* __restrict__ mean, float* __restrict__ rstd, long M, int H,
                                                      float eps, uint32_t thresh, float dscale,
                                                      unsigned long long seed) {
-  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (row >= M) return;
   const int nv = H >> 3;
-  const bf16_t* xr = x + row * H;
-  float v[VPL][8];
-  float s = 0.f;
+  float gm[VPL][8], bt[VPL][8];
 #pragma unroll
   for (int u = 0; u < VPL; ++u) {
     const int c = lane + 64 * u;
-    if (c < nv) {
-      unpack8(*reinterpret_cast<const uint4*>(xr + c * 8), v[u]);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) s += v[u][e];
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[u][e] = 0.f;
+    for (int e = 0; e < 8; ++e) {
+      gm[u][e] = (gamma && c < nv) ? gamma[c * 8 + e] : 1.f;
+      bt[u][e] = (beta && c < nv) ? beta[c * 8 + e] : 0.f;
     }
   }
-  const float mu = warp_sum(s) / (float)H;
-  float q = 0.f;
+  for (long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6); row < M; row += (long)gridDim.x * 4) {
+    const bf16_t* xr = x + row * H;
+    float v[VPL][8];
+    float s = 0.f;
 #pragma unroll
-  for (int u = 0; u < VPL; ++u)
-    if (lane + 64 * u < nv)
+    for (int u = 0; u < VPL; ++u) {
+      const int c = lane + 64 * u;
+      if (c < nv) {
+        unpack8(*reinterpret_cast<const uint4*>(xr + c * 8), v[u]);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float d = v[u][e] - mu;
-        q += d * d;
+        for (int e = 0; e < 8; ++e) s += v[u][e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[u][e] = 0.f;
       }
-  const float rs = rsqrtf(warp_sum(q) / (float)H + eps);
-#pragma unroll
-  for (int u = 0; u < VPL; ++u) {
-    const int c = lane + 64 * u;
-    if (c < nv) {
-      float o[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int n = c * 8 + e;
-        o[e] = (v[u][e] - mu) * rs * (gamma ? gamma[n] : 1.f) + (beta ? beta[n] : 0.f);
-        if (thresh)  // output dropout (BERT embeddings), element index row*H + n
-          o[e] = drop_keep(seed, (unsigned long long)row * (unsigned long long)H + n, thresh) ? o[e] * dscale : 0.f;
-      }
-      *reinterpret_cast<uint4*>(y + row * H + c * 8) = pack8f(o);
     }
-  }
-  if (lane == 0) {
-    mean[row] = mu;
-    rstd[row] = rs;
+    const float mu = warp_sum(s) / (float)H;
+    float q = 0.f;
+#pragma unroll
+    for (int u = 0; u < VPL; ++u)
+      if (lane + 64 * u < nv)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = v[u][e] - mu;
+          q += d * d;
+        }
+    const float rs = rsqrtf(warp_sum(q) / (float)H + eps);
+#pragma unroll
+    for (int u = 0; u < VPL; ++u) {
+      const int c = lane + 64 * u;
+      if (c < nv) {
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          o[e] = (v[u][e] - mu) * rs * gm[u][e] + bt[u][e];
+          if (thresh)  // output dropout (BERT embeddings), element index row*H + n
+            o[e] = drop_keep(seed, (unsigned long long)row * (unsigned long long)H + c * 8 + e, thresh) ? o[e] * dscale
+                                                                                                     : 0.f;
+        }
+        *reinterpret_cast<uint4*>(y + row * H + c * 8) = pack8f(o);
+      }
+    }
+    if (lane == 0) {
+      mean[row] = mu;
+      rstd[row] = rs;
+    }
   }
 }
 
@@ -97,11 +109,14 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
   const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int nwaves = gridDim.x * 4;
   const int nv = H >> 3;
-  float dg[VPL][8], db[VPL][8], dd[VPL][8];
+  float dg[VPL][8], db[VPL][8], dd[VPL][8], gmv[VPL][8];
 #pragma unroll
   for (int u = 0; u < VPL; ++u)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) dg[u][e] = db[u][e] = dd[u][e] = 0.f;
+    for (int e = 0; e < 8; ++e) {
+      dg[u][e] = db[u][e] = dd[u][e] = 0.f;
+      gmv[u][e] = (gamma && lane + 64 * u < nv) ? gamma[(lane + 64 * u) * 8 + e] : 1.f;  // hoisted out of the rows
+    }
   for (long row = wave; row < M; row += nwaves) {
     const float mu = mean[row], rs = rstd[row];
     float gy[VPL][8], xh[VPL][8];
@@ -121,7 +136,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float xhat = (xv[e] - mu) * rs;
-          const float gm = gamma ? gamma[c * 8 + e] : 1.f;
+          const float gm = gmv[u][e];
           dg[u][e] += d[e] * xhat;
           db[u][e] += d[e];
           xh[u][e] = xhat;
@@ -355,7 +370,7 @@ int layernorm_fwd(const void* x, const float* gamma, const float* beta, void* y,
   const uint32_t th = drop_p > 0.f ? (uint32_t)std::min(4294967295.0, (double)drop_p * 4294967296.0) : 0u;
   const float ds = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
   const int nv = H / 8;
-  const dim3 grid((unsigned)((M + 3) / 4));
+  const dim3 grid((unsigned)std::min<long>((M + 3) / 4, 2048));  // grid-stride: gamma / beta loaded once per wave
   auto X = reinterpret_cast<const bf16_t*>(x);
   auto Y = reinterpret_cast<bf16_t*>(y);
   if (nv <= 64) hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed);
