@@ -58,6 +58,8 @@ int cast_bf16_f32(const void* x, float* y, long n, hipStream_t s);
 int relu_bwd(const void* dy, const void* y, void* dx, long n, hipStream_t s);
 int add_bf16(const void* a, const void* b, void* y, long n, hipStream_t s);
 int bias_grad(const void* dy, float* db, long M, int N, int accumulate, hipStream_t s);  // db[n] (+)= sum_m dy[m][n]
+// y[C][R] = x[R][C]^T (bf16; R, C, ldx multiples of 8)
+int transpose_bf16(const void* x, void* y, int R, int C, long ldx, hipStream_t s);
 int im2col(const void* x, void* col, int n, int hi, int wi, int c, int ho, int wo, int sh, int sw, int ntaps,
            const int* dh, const int* dw, int kpad, hipStream_t s);
 // stem space-to-depth: [N][H][W][C<=4] -> [N][Ho][Wo][16] (block 2, zero padding `pad`)

@@ -175,3 +175,44 @@ int s2d_pad(const void* x, void* y, int N, int H, int W, int C, int Ho, int Wo, 
 }
 
 }  // namespace ddl
+
+namespace ddl {
+
+// y[c][r] = x[r][c] for a bf16 [R][C] matrix (row stride ldx), y contiguous [C][R].  One 64x64
+// tile per 256-thread block, staged through LDS: 16-B global reads along x's rows, 16-B global
+// writes along y's rows (the transposed weight copy read by the BERT-size Linear data-gradients).
+// Requires R % 8 == 0, C % 8 == 0, ldx % 8 == 0 (checked by the launcher).
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                             int R, int C, long ldx) {
+  __shared__ bf16_t t[64][64 + 2];  // +2: odd 32-bit word stride, column reads spread over banks
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+#pragma unroll
+  for (int v = 0; v < 2; ++v) {  // 64 rows x 8 vectors of 8
+    const int idx = threadIdx.x + v * 256, rr = idx >> 3, cv = (idx & 7) * 8;
+    uint4 d = make_uint4(0, 0, 0, 0);
+    if (r0 + rr < R && c0 + cv < C) d = *reinterpret_cast<const uint4*>(x + (long)(r0 + rr) * ldx + c0 + cv);
+    const bf16_t* e = reinterpret_cast<const bf16_t*>(&d);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t[rr][cv + i] = e[i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int v = 0; v < 2; ++v) {  // 64 output rows (x columns) x 8 vectors of 8
+    const int idx = threadIdx.x + v * 256, cc = idx >> 3, rv = (idx & 7) * 8;
+    if (c0 + cc >= C || r0 + rv >= R) continue;
+    uint4 d;
+    bf16_t* e = reinterpret_cast<bf16_t*>(&d);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) e[i] = t[rv + i][cc];
+    *reinterpret_cast<uint4*>(y + (long)(c0 + cc) * R + r0 + rv) = d;
+  }
+}
+
+int transpose_bf16(const void* x, void* y, int R, int C, long ldx, hipStream_t s) {
+  if (R % 8 || C % 8 || ldx % 8) return (int)hipErrorInvalidValue;
+  const dim3 grid((C + 63) / 64, (R + 63) / 64);
+  hipLaunchKernelGGL(transpose_bf16_kernel, grid, dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y, R, C, ldx);
+  return (int)hipGetLastError();
+}
+
+}  // namespace ddl

@@ -209,6 +209,14 @@ void add_bf16_(const at::Tensor& a, const at::Tensor& b, const at::Tensor& y) {
   at::DeviceGuard g(a.device());
   HIP_OK(add_bf16(a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(), cur_stream()));
 }
+void transpose_bf16_(const at::Tensor& x, const at::Tensor& y) {
+  GPU(x); BF16(y);
+  CK(x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.stride(1) == 1, "transpose: x must be 2-D bf16, unit column stride");
+  CK(y.dim() == 2 && y.size(0) == x.size(1) && y.size(1) == x.size(0), "transpose: y must be [C][R]");
+  CK(x.size(0) % 8 == 0 && x.size(1) % 8 == 0 && x.stride(0) % 8 == 0, "transpose: R, C, ld must be multiples of 8");
+  at::DeviceGuard g(x.device());
+  HIP_OK(transpose_bf16(x.data_ptr(), y.data_ptr(), (int)x.size(0), (int)x.size(1), x.stride(0), cur_stream()));
+}
 void bias_grad_(const at::Tensor& dy, const at::Tensor& db, int64_t N, bool accumulate) {
   GPU(dy); BF16(dy); F32(db);
   CK(dy.numel() % N == 0 && db.numel() >= N, "bias_grad: shapes");
@@ -359,6 +367,7 @@ void register_ops(py::module& m) {
   m.def("relu_bwd", &relu_bwd_);
   m.def("add_bf16", &add_bf16_);
   m.def("bias_grad", &bias_grad_);
+  m.def("transpose_bf16", &transpose_bf16_);
   m.def("im2col", &im2col_);
   m.def("normalize_u8", &normalize_u8_);
   m.def("s2d_pad", &s2d_pad_);

@@ -235,3 +235,25 @@ def test_embed_word_grad_sorted_runs_and_pos_grad():
     gp = torch.zeros(S, H, device=DEV)
     C().embed_pos_grad(ds, gp, B, S)
     close(gp, ds.float().view(B, S, H).sum(0), rtol=1e-3, atol=1e-3, what="pos grad")
+
+
+@pytest.mark.parametrize("R,Cc", [(768, 3072), (3072, 768), (200, 96), (8, 8)])
+def test_transpose_bf16_kernel(R, Cc):
+    from distributeddeeplearningspark_amd.ops import gemm as G
+
+    w = rnd(R, Cc, seed=5)
+    t = G.transpose(w)
+    assert t.shape == (Cc, R) and t.is_contiguous()
+    assert torch.equal(t.cpu(), w.t().contiguous().cpu())
+    ws = rnd(R, Cc + 8, seed=6)[:, :Cc]  # strided rows
+    assert torch.equal(G.transpose(ws).cpu(), ws.t().contiguous().cpu())
+
+
+def test_linear_dgrad_transposed_weight_path():
+    """M >= 4096 rows: the data-gradient reads a HIP-transposed weight copy (KC x KC GEMM)."""
+    from distributeddeeplearningspark_amd.ops import gemm as G
+
+    M, N, K = 4096, 384, 256
+    dy, w = rnd(M, N, seed=7), rnd(N, K, seed=8, scale=0.05)
+    dx = G.linear_dgrad(dy, w)
+    close(dx, dy.float() @ w.float(), what="dgrad KCxKC")
