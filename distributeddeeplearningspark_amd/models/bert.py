@@ -30,6 +30,7 @@ used by the tests as the numerics reference of the GPU path.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import asdict, dataclass
 
 import numpy as np
@@ -110,8 +111,22 @@ def _bias_grad(d2, gb):
         C().bias_grad(d2, gb, d2.shape[1], True)
 
 
+# Epilogue-free weight/data gradients go to hipBLASLt ("plain library GEMMs"); the GEMMs with
+# fused bias/GELU/dropout/residual/LN-stat epilogues stay on the hand-written MFMA kernels.
+_LIB_GEMM = os.environ.get("DDL_BERT_LIB_GEMM", "0") == "1"  # measured slower end-to-end: off
+
+
 def _wgrad(d2, x2, gw):
-    G.linear_wgrad(d2, x2, gw)
+    if _LIB_GEMM and d2.is_cuda:
+        G.lib_wgrad(d2, x2, gw)
+    else:
+        G.linear_wgrad(d2, x2, gw)
+
+
+def _dgrad(dy, w):
+    if _LIB_GEMM and dy.is_cuda:
+        return G.lib_dgrad(dy, w)
+    return G.linear_dgrad(dy, w)
 
 
 # ====================================================================================== layers
@@ -366,7 +381,7 @@ class _BertLayerFn(torch.autograd.Function):
         # ---- attention block
         ds1, ds1d = ln_back(da, s1, m1, r1, L.ln1_g, L.ln1_b, seeds[1], L.o_b)
         _wgrad(ds1d, ctxo, L.o_w.grad)
-        dctx = G.linear_dgrad(ds1d, L.o_w.data)
+        dctx = _dgrad(ds1d, L.o_w.data)
         dqkv = torch.empty_like(qkv)
         dvec = torch.empty((B, NH, S), dtype=torch.float32, device=dev)
         C().attn_bwd(qkv, B, S, NH, 0, H, 2 * H, ctxo, lse, lens, 1.0 / math.sqrt(64), p_a, seeds[0], dctx, dvec,
@@ -438,7 +453,7 @@ class _MLMHeadFn(torch.autograd.Function):
         M = hm.shape[0]
         _wgrad(dlogits, t2, emb.word.grad)  # tied decoder: dE += dlogits^T t2
         _bias_grad(dlogits, head.dec_b.grad)
-        dt2 = G.linear_dgrad(dlogits, emb.word.data)
+        dt2 = _dgrad(dlogits, emb.word.data)
         dt = torch.empty_like(t)
         P_ = C().ln_partial_rows(M)
         ws = torch.empty((P_, 2, H), dtype=torch.float32, device=hm.device)
@@ -449,7 +464,7 @@ class _MLMHeadFn(torch.autograd.Function):
         dpre = (dt.float() * _gelu_grad(pre.float())).to(torch.bfloat16)
         _wgrad(dpre, hm, head.t_w.grad)
         _bias_grad(dpre, head.t_b.grad)
-        dhm = G.linear_dgrad(dpre, head.t_w.data)
+        dhm = _dgrad(dpre, head.t_w.data)
         if head.grad_hook is not None:
             head.grad_hook()
         return dhm, None, None, None, None, None
