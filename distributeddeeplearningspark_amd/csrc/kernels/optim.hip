@@ -68,9 +68,9 @@ __global__ __launch_bounds__(256) void adam_kernel(float4* w, const float4* g, f
     bc2 = 1.f - powf(b2, t);
   }
   const float sbc2 = sqrtf(bc2);
-  DDL_FLAT_FOR(i, n) {
-    float4 p = w[i], d = g[i], mm = m[i], vv = v[i];
-    float *pp = &p.x, *dd = &d.x, *m_ = &mm.x, *v_ = &vv.x;
+  auto upd = [&](float4& p, const float4& d, float4& mm, float4& vv) {
+    float *pp = &p.x, *m_ = &mm.x, *v_ = &vv.x;
+    const float* dd = &d.x;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       float gg = dd[k] * gs;
@@ -81,10 +81,26 @@ __global__ __launch_bounds__(256) void adam_kernel(float4* w, const float4* g, f
       if (mode & 2) pp[k] -= lr * (sbc2 / bc1) * m_[k] / (sqrtf(v_[k]) + eps);
       else pp[k] -= lr * (m_[k] / bc1) / (sqrtf(v_[k]) / sbc2 + eps);
     }
-    w[i] = p;
-    m[i] = mm;
-    v[i] = vv;
-    if (w16) store_bf16x4(w16, i, p);
+  };
+  // two float4 slots per lane per trip, all eight loads issued before any store: twice the
+  // bytes in flight per wave for this 30-byte/parameter stream (HBM-bound)
+  const long n4 = n >> 2, stride = (long)gridDim.x * 256;
+  long i = (long)blockIdx.x * 256 + threadIdx.x;
+  for (; i + stride < n4; i += 2 * stride) {
+    const long j = i + stride;
+    float4 p0 = w[i], d0 = g[i], m0 = m[i], v0 = v[i];
+    float4 p1 = w[j], d1 = g[j], m1 = m[j], v1 = v[j];
+    upd(p0, d0, m0, v0);
+    upd(p1, d1, m1, v1);
+    w[i] = p0; m[i] = m0; v[i] = v0;
+    w[j] = p1; m[j] = m1; v[j] = v1;
+    if (w16) { store_bf16x4(w16, i, p0); store_bf16x4(w16, j, p1); }
+  }
+  if (i < n4) {
+    float4 p0 = w[i], d0 = g[i], m0 = m[i], v0 = v[i];
+    upd(p0, d0, m0, v0);
+    w[i] = p0; m[i] = m0; v[i] = v0;
+    if (w16) store_bf16x4(w16, i, p0);
   }
 }
 
