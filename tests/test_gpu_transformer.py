@@ -257,3 +257,20 @@ def test_linear_dgrad_transposed_weight_path():
     dy, w = rnd(M, N, seed=7), rnd(N, K, seed=8, scale=0.05)
     dx = G.linear_dgrad(dy, w)
     close(dx, dy.float() @ w.float(), what="dgrad KCxKC")
+
+
+@pytest.mark.parametrize("M,N,off", [(16384, 768, 0), (4096, 3072, 0), (333, 2304, 0), (257, 100, 0), (64, 768, 3)])
+def test_bias_grad_vector_and_scalar_paths(M, N, off):
+    """Column sums of a bf16 [M, N] gradient (vector kernel for N % 8 == 0 on 16-byte aligned rows,
+    scalar kernel otherwise) accumulated into fp32, vs an fp32 PyTorch reference."""
+    from distributeddeeplearningspark_amd.ops._native import C
+
+    flat = rnd(M * N + off, seed=5)
+    dy = flat[off:].view(M, N)
+    db = torch.randn(N, device=DEV)
+    ref = db + dy.float().sum(0)
+    C().bias_grad(dy, db, N, True)
+    torch.cuda.synchronize()
+    close(db, ref, rtol=1e-4, atol=1e-2, what="bias_grad")
+    C().bias_grad(dy, db, N, False)
+    close(db, dy.float().sum(0), rtol=1e-4, atol=1e-2, what="bias_grad overwrite")
