@@ -34,6 +34,12 @@ def main():
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--model", default="resnet50", choices=["resnet50", "vgg16", "bert"],
                     help="resnet50 = the BASELINE headline; vgg16 / bert = the other BASELINE.json DP configs")
+    ap.add_argument("--reduce-dtype", default=None, choices=["fp32", "bf16"],
+                    help="gradient all-reduce wire dtype (default DDL_REDUCE_DTYPE or fp32)")
+    ap.add_argument("--graph", type=int, default=None,
+                    help="1 = replay the whole step from a hipGraph (1-GPU runs without a process group "
+                         "only).  Default off: measured neutral on ResNet-50 (9,532 vs 9,562 img/s) and "
+                         "VGG-16 (74.3K vs 75.1K img/s) — both steps are GPU-bound, not launch-bound")
     ap.add_argument("--seq", type=int, default=512)
     ap.add_argument("--layers", type=int, default=12)
     args = ap.parse_args()
@@ -68,19 +74,21 @@ def main():
     model.compile(SGD(lr=0.1 if args.model == "resnet50" else 0.01, momentum=0.9, weight_decay=5e-5),
                   "sparse_categorical_crossentropy")
     model.place(dev, seed=0)
-    ddp = DataParallel(model, pg, bucket_mb=args.bucket_mb, overlap=not args.no_overlap)
+    ddp = make_ddp(model, pg, args)
     ddp.broadcast_parameters()
 
     stream = SyntheticImageStream(args.batch, args.image, n_cls, device=dev, seed=rank, n_buffers=4)
+    step_fn = make_step(ddp, args)
 
     def step():
         x, y = stream.next()
-        return ddp.train_step(x, y)
+        return step_fn(x, y)
 
     for _ in range(args.warmup):
         step()
     pg.barrier()
     torch.cuda.synchronize(dev) if dev.type == "cuda" else None
+    ddp.exposed_comm_ms(reset=True)  # exposed-comm statistics cover the timed steps only
     t0 = time.perf_counter()
     loss = None
     for _ in range(args.steps):
@@ -89,6 +97,7 @@ def main():
     pg.barrier()
     dt = time.perf_counter() - t0
     dt_max = pg.max_scalar(dt)
+    comm = comm_stats(ddp, pg)
     ms = dt_max * 1000.0 / args.steps
     gb = args.batch * world
     ips = gb * args.steps / dt_max
@@ -110,10 +119,48 @@ def main():
             "data": "synthetic",
             "config": {"model": args.model, "global_batch": gb, "seq_len": None, "image": args.image,
                        "per_gpu_batch": args.batch, "parallelism": f"dp{world}", "optimizer": "sgd-momentum",
-                       "final_loss": round(lossv, 4)},
+                       "final_loss": round(lossv, 4), **comm},
         }
         print(json.dumps(out), flush=True)
     pg.shutdown()
+
+
+def make_ddp(model, pg, args):
+    import torch as _t
+
+    from distributeddeeplearningspark_amd.parallel.ddp import DataParallel
+
+    rd = None if args.reduce_dtype is None else (_t.bfloat16 if args.reduce_dtype == "bf16" else _t.float32)
+    return DataParallel(model, pg, bucket_mb=args.bucket_mb, overlap=not args.no_overlap, reduce_dtype=rd,
+                        timing=pg.distributed)
+
+
+def make_step(ddp, args):
+    """The timed step: ``ddp.train_step`` (eager launches + bucket hooks) or, on a 1-GPU run
+    without a process group, the same step replayed from a hipGraph (``models/step.py``)."""
+    use_graph = args.graph if args.graph is not None else 0
+    if not use_graph or ddp.pg.distributed or ddp.model.device.type != "cuda":
+        return ddp.train_step
+    from distributeddeeplearningspark_amd.models.step import CompiledTrainStep
+
+    m = ddp.model
+    if m.optimizer.arena is not m.arena:
+        m.optimizer.bind(m.arena)
+    return CompiledTrainStep(m, warmup=2)
+
+
+def comm_stats(ddp, pg):
+    """Communication evidence for the JSON line: exposed (un-overlapped) all-reduce time per
+    timed step, and the stand-alone full-gradient all-reduce time (max over ranks)."""
+    if not pg.distributed:
+        return {"comm_ms": None, "exposed_comm_ms": None, "bucket_mb": ddp.bucket_mb, "buckets": len(ddp.buckets)}
+    exposed = ddp.exposed_comm_ms()
+    full = ddp.measure_allreduce(iters=5)
+    exposed = pg.max_scalar(exposed if exposed is not None else 0.0)
+    full = pg.max_scalar(full if full is not None else 0.0)
+    return {"comm_ms": round(full, 3), "exposed_comm_ms": round(exposed, 3), "bucket_mb": ddp.bucket_mb,
+            "buckets": len(ddp.buckets), "reduce_dtype": "bf16" if ddp._red is not None else "fp32",
+            "grad_mb": round(ddp.grad_bytes / 2**20, 1), "backend": pg.backend, "forced_pg": pg.forced}
 
 
 def bench_bert(args, pg):
@@ -128,8 +175,9 @@ def bench_bert(args, pg):
     model = BertForMaskedLM(cfg)
     model.compile(AdamW(lr=1e-4, weight_decay=0.01), "sparse_categorical_crossentropy")
     model.place(dev, seed=0)
-    ddp = DataParallel(model, pg, bucket_mb=args.bucket_mb, overlap=not args.no_overlap)
+    ddp = make_ddp(model, pg, args)
     ddp.broadcast_parameters()
+    step_fn = make_step(ddp, args)
     batches = [mlm_batch(args.batch, args.seq, cfg.vocab_size, seed=rank * 100 + i) for i in range(4)]
     batches = [(model.to_input(x), model.to_target(y)) for x, y in batches]
     it = [0]
@@ -137,12 +185,13 @@ def bench_bert(args, pg):
     def step():
         x, y = batches[it[0] % len(batches)]
         it[0] += 1
-        return ddp.train_step(x, y)
+        return step_fn(x, y)
 
     for _ in range(args.warmup):
         step()
     pg.barrier()
     torch.cuda.synchronize(dev) if dev.type == "cuda" else None
+    ddp.exposed_comm_ms(reset=True)  # exposed-comm statistics cover the timed steps only
     t0 = time.perf_counter()
     loss = None
     for _ in range(args.steps):
@@ -150,6 +199,7 @@ def bench_bert(args, pg):
     torch.cuda.synchronize(dev) if dev.type == "cuda" else None
     pg.barrier()
     dt_max = pg.max_scalar(time.perf_counter() - t0)
+    comm = comm_stats(ddp, pg)
     gb = args.batch * world
     tps = gb * args.seq * args.steps / dt_max
     if rank == 0:
@@ -162,7 +212,7 @@ def bench_bert(args, pg):
                        "global_batch": gb, "seq_len": args.seq, "per_gpu_batch": args.batch,
                        "parallelism": f"dp{world}", "optimizer": "adamw", "max_predictions": 80,
                        "sequences_per_sec": round(gb * args.steps / dt_max, 2),
-                       "final_loss": round(float(loss), 4)},
+                       "final_loss": round(float(loss), 4), **comm},
         }), flush=True)
     pg.shutdown()
 

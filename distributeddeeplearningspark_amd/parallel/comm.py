@@ -24,10 +24,11 @@ class ProcessGroup:
     device: torch.device
     backend: str | None
     group: object = None
+    forced: bool = False  # world-1 group created on purpose (DDL_FORCE_DIST=1): collectives still run
 
     @property
     def distributed(self) -> bool:
-        return self.world_size > 1
+        return self.world_size > 1 or self.forced
 
     def barrier(self):
         if self.distributed:
@@ -100,9 +101,22 @@ class _DoneWork:
 _DEFAULT: ProcessGroup | None = None
 
 
-def init_from_env(prefer_gpu: bool = True, timeout_s: float = 600.0, backend: str | None = None) -> ProcessGroup:
-    """Initialise from torchrun-style env (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT)."""
+def force_dist_requested() -> bool:
+    """``DDL_FORCE_DIST=1``: build a real process group even at world size 1, so the whole
+    data-parallel machinery (bucket hooks, RCCL all-reduce / broadcast launches, the
+    comm-stream overlap) runs and can be profiled on a single MI355X."""
+    return os.environ.get("DDL_FORCE_DIST", "0") == "1"
+
+
+def init_from_env(prefer_gpu: bool = True, timeout_s: float = 600.0, backend: str | None = None,
+                  force: bool | None = None) -> ProcessGroup:
+    """Initialise from torchrun-style env (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT).
+
+    ``force`` (default: ``DDL_FORCE_DIST``) creates the "nccl" (RCCL) group — gloo on CPU —
+    even when WORLD_SIZE is 1; the single-rank store is an in-process ``HashStore``."""
     global _DEFAULT
+    if force is None:
+        force = force_dist_requested()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -115,15 +129,18 @@ def init_from_env(prefer_gpu: bool = True, timeout_s: float = 600.0, backend: st
     else:
         device = torch.device("cpu")
     be = None
-    if world > 1:
+    forced = bool(force) and world == 1
+    if world > 1 or forced:
         be = backend or os.environ.get("DDL_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if not dist.is_initialized():
             kw = dict(backend=be, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
+            if forced:
+                kw["store"] = dist.HashStore()
             if be == "nccl":
                 kw["device_id"] = device
             dist.init_process_group(**kw)
-    _DEFAULT = ProcessGroup(rank, world, local, device, be)
+    _DEFAULT = ProcessGroup(rank, world, local, device, be, forced=forced)
     return _DEFAULT
 
 

@@ -1,7 +1,8 @@
 """Synchronous data parallelism: bucketed gradient all-reduce over RCCL, overlapped with backward.
 
 This replaces the reference's parameter-server gradient path (dist-keras commit/pull
-over TCP) with RCCL collectives over xGMI:
+over TCP; call sites ``ddl_mnist_aztk.py:216-219``) with RCCL
+collectives over xGMI:
 
 * Gradients live in ONE flat fp32 buffer (``models/params.py``).  Buckets are
   contiguous slices of it taken from the END (backward produces the last layers'
@@ -14,42 +15,97 @@ over TCP) with RCCL collectives over xGMI:
   no deadlock even if hooks arrive in a slightly different order).
 * Bucket size: xGMI is point-to-point (7 links x ~153 GB/s per MI355X); a ring
   all-reduce is bound by one link, so per-bucket latency alpha must be amortised by
-  tens of MB.  Default 32 MB (override with ``bucket_mb`` / ``DDL_BUCKET_MB``).
+  tens of MB.  Default 32 MB (``bucket_mb`` / ``DDL_BUCKET_MB``); the sweep that picks
+  it is ``scripts/bench_allreduce.py``.
+* ``reduce_dtype=torch.bfloat16`` (``DDL_REDUCE_DTYPE=bf16``): each ready bucket is cast
+  to a bf16 mirror slice by a HIP kernel on the compute stream, the bf16 slice is
+  all-reduced (half the xGMI bytes), and after the last wait ONE HIP cast writes the
+  reduced values back into the fp32 gradient arena.  Accumulation across ranks is then
+  bf16 (RCCL sums in the wire dtype); the default stays fp32 for parity.
 * The 1/world averaging is folded into the optimizer kernel (``grad_scale``), so there
   is no separate scaling pass over the gradients.
+* Timing (``timing=True``): HIP events on the compute stream bracket the part of the
+  step that waits for communication (end of backward -> all buckets reduced), giving the
+  *exposed* communication time; :meth:`measure_allreduce` times the full-gradient
+  all-reduce on its own (``comm_ms`` in ``bench.py``'s JSON).
 """
 from __future__ import annotations
 
 import os
 
 import torch
-import torch.distributed as dist
 
 from .comm import ProcessGroup
 
 
+def _reduce_dtype_from_env():
+    v = os.environ.get("DDL_REDUCE_DTYPE", "fp32").lower()
+    if v in ("bf16", "bfloat16"):
+        return torch.bfloat16
+    if v in ("fp32", "float32", "f32", ""):
+        return torch.float32
+    raise ValueError(f"DDL_REDUCE_DTYPE={v!r}: expected fp32 or bf16")
+
+
+def all_reduce_flat(pg: ProcessGroup, t: torch.Tensor, bucket_bytes: int = 64 << 20, average: bool = False):
+    """All-reduce an arbitrary flat buffer in bucket-sized chunks (ADAG / DynSGD deltas,
+    model averaging).  Chunks are issued back to back (async) and waited together."""
+    if not pg.distributed:
+        return t
+    step = max(int(bucket_bytes) // t.element_size(), 1)
+    works = [pg.all_reduce_(t[i : i + step], async_op=True) for i in range(0, t.numel(), step)]
+    for w in works:
+        if w is not None:
+            w.wait()
+    if average:
+        t.div_(pg.world_size)
+    return t
+
+
+def _cast(src: torch.Tensor, dst: torch.Tensor):
+    """fp32 <-> bf16 over flat slices: HIP kernels on the GPU, torch on the CPU."""
+    from ..ops._native import C, use_native
+
+    if use_native(src):
+        if src.dtype == torch.float32:
+            C().cast_f32_bf16(src, dst)
+        else:
+            C().cast_bf16_f32(src, dst)
+    else:
+        dst.copy_(src)
+
+
 class DataParallel:
     def __init__(self, model, pg: ProcessGroup, bucket_mb: float | None = None, overlap: bool = True,
-                 reduce_dtype: torch.dtype | None = None):
+                 reduce_dtype: torch.dtype | None = None, timing: bool = False):
         self.model = model
         self.pg = pg
         self.overlap = overlap and pg.distributed
         if bucket_mb is None:
             bucket_mb = float(os.environ.get("DDL_BUCKET_MB", "32"))
+        self.bucket_mb = float(bucket_mb)
         self.bucket_bytes = int(bucket_mb * (1 << 20))
-        self.reduce_dtype = reduce_dtype
+        self.reduce_dtype = reduce_dtype if reduce_dtype is not None else _reduce_dtype_from_env()
+        if self.reduce_dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError(f"reduce_dtype {self.reduce_dtype}: expected torch.float32 or torch.bfloat16")
         model._ensure_placed()
         self.arena = model.arena
+        self._red = None  # bf16 mirror of the gradient arena (allocated once)
+        if self.reduce_dtype == torch.bfloat16 and pg.distributed:
+            self._red = torch.zeros(self.arena.numel, dtype=torch.bfloat16, device=self.arena.grad.device)
         self._build_buckets()
         self._works = []
-        self.comm_time_hint = 0.0
+        self.timing = bool(timing) and self.arena.grad.is_cuda
+        self._events = []  # (backward done, comm done) per timed step
         if self.overlap:
             self._install_hooks()
 
     # ---------------------------------------------------------------- buckets
     def _build_buckets(self):
         params = [p for p in self.arena.params if p.trainable]
-        elems_per_bucket = max(self.bucket_bytes // 4, 1 << 14)
+        # bucket size is counted in WIRE bytes, so a bf16 reduce packs twice the elements
+        wire = 2 if self._red is not None else 4
+        elems_per_bucket = max(self.bucket_bytes // wire, 256)
         buckets = []  # list of dict(start, end, params)
         cur = None
         for p in reversed(params):
@@ -105,6 +161,10 @@ class DataParallel:
     def _launch(self, i):
         b = self.buckets[i]
         view = self.arena.grad[b["start"] : b["end"]]
+        if self._red is not None:
+            red = self._red[b["start"] : b["end"]]
+            _cast(view, red)  # on the compute stream: ordered after the bucket's last grad kernel
+            view = red
         self._works.append(self.pg.all_reduce_(view, async_op=True))
 
     def _finish(self):
@@ -113,8 +173,10 @@ class DataParallel:
         self._next = len(self.buckets)
         for w in self._works:
             if w is not None:
-                w.wait()
+                w.wait()  # compute stream waits for the RCCL stream (no host block)
         self._works = []
+        if self._red is not None:
+            _cast(self._red, self.arena.grad)
 
     def sync_gradients(self, arena=None) -> float:
         """All-reduce every bucket (no overlap) — returns the averaging grad scale."""
@@ -152,18 +214,56 @@ class DataParallel:
                 loss = m.compute_loss(x, y, training=True)
             with phase("backward"):
                 loss.backward()
+            ev = None
+            if self.timing and self.pg.distributed:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
             with phase("allreduce"):
                 if self.overlap:
                     self._finish()
                 elif self.pg.distributed:
                     self.sync_gradients()
+            if ev is not None:
+                ev[1].record()
+                self._events.append(ev)
             with phase("optimizer"):
                 m.optimizer.step(grad_scale=1.0 / self.pg.world_size)
         return loss.detach()
 
+    def exposed_comm_ms(self, reset: bool = True) -> float | None:
+        """Mean GPU time per timed step between the end of backward and the moment every
+        bucket is reduced (the communication NOT hidden behind backward).  Call after a
+        device synchronize."""
+        if not self._events:
+            return None
+        v = sum(a.elapsed_time(b) for a, b in self._events) / len(self._events)
+        if reset:
+            self._events = []
+        return v
+
+    def measure_allreduce(self, iters: int = 10, warmup: int = 2) -> float | None:
+        """Milliseconds for one full-gradient all-reduce (every bucket, same dtype / bucket
+        plan as the step), measured alone on the compute stream.  Leaves the gradient
+        arena scaled by world**(iters+warmup): call it outside training, then zero grads."""
+        if not self.pg.distributed or not self.arena.grad.is_cuda:
+            return None
+        for _ in range(warmup):
+            self.sync_gradients()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(iters):
+            self.sync_gradients()
+        b.record()
+        b.synchronize()
+        self.arena.zero_grad()
+        return a.elapsed_time(b) / iters
+
     @property
     def grad_bytes(self) -> int:
-        return self.arena.grad.numel() * self.arena.grad.element_size() if self.pg.distributed else 0
+        """Bytes each rank puts through the all-reduce per step."""
+        if not self.pg.distributed:
+            return 0
+        return self.arena.grad.numel() * (2 if self._red is not None else 4)
 
     def check_replicas(self, raise_on_mismatch: bool = True) -> bool:
         """Divergence detection: after a synchronous update every replica must
@@ -181,13 +281,5 @@ class DataParallel:
         return ok
 
     def all_reduce_flat_(self, t: torch.Tensor, average: bool = False):
-        """All-reduce an arbitrary flat buffer in bucket-sized chunks (ADAG / DynSGD deltas)."""
-        if not self.pg.distributed:
-            return t
-        step = max(self.bucket_bytes // t.element_size(), 1)
-        works = [self.pg.all_reduce_(t[i : i + step], async_op=True) for i in range(0, t.numel(), step)]
-        for w in works:
-            w.wait()
-        if average:
-            t.div_(self.pg.world_size)
-        return t
+        """All-reduce an arbitrary flat buffer in this engine's bucket size."""
+        return all_reduce_flat(self.pg, t, self.bucket_bytes, average)

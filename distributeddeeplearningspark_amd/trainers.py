@@ -218,9 +218,9 @@ class _CommitWorker(_Worker):
 
     def _allreduce(self, t):
         if self.pg.distributed:
-            from .parallel.ddp import DataParallel
+            from .parallel.ddp import all_reduce_flat
 
-            DataParallel.all_reduce_flat_(_FlatReducer(self.pg), t)
+            all_reduce_flat(self.pg, t, 64 << 20)
 
 
 class _AsyncPSWorker(_Worker):
@@ -277,14 +277,6 @@ class _AsyncPSWorker(_Worker):
         finally:
             cli.close()
         return W.clone()
-
-
-class _FlatReducer:
-    """Minimal object to reuse DataParallel.all_reduce_flat_ without hooks."""
-
-    def __init__(self, pg):
-        self.pg = pg
-        self.bucket_bytes = 64 << 20
 
 
 class _AdagWorker(_CommitWorker):

@@ -1,0 +1,134 @@
+"""Synchronous data parallelism (parallel/ddp.py) on CPU gloo: the overlapped per-layer
+bucket hooks at N=4 must equal a single-process emulation of the same schedule (per-replica
+gradients summed, then one optimizer step with grad_scale 1/N), in fp32 and with the bf16
+wire dtype; a forced world-1 process group (DDL_FORCE_DIST=1) must run the collective path
+and give the non-distributed result."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+N = 4
+STEPS = 2
+
+
+def _model():
+    from distributeddeeplearningspark_amd.models import Conv2D, Dense, Flatten, MaxPooling2D, Sequential
+
+    m = Sequential([Conv2D(8, (3, 3), activation="relu", input_shape=(10, 10, 2)), MaxPooling2D((2, 2)),
+                    Conv2D(8, (3, 3), activation="relu"), Flatten(), Dense(16, activation="relu"),
+                    Dense(5, activation="softmax")])
+    m.compile("adam", "categorical_crossentropy")
+    m.place("cpu", seed=7)
+    return m
+
+
+def _data():
+    g = torch.Generator().manual_seed(11)
+    x = torch.rand(STEPS, N, 6, 10, 10, 2, generator=g)
+    y = torch.nn.functional.one_hot(torch.randint(0, 5, (STEPS, N, 6), generator=g), 5).float()
+    return x, y
+
+
+def _ddp_worker(rank, world, pg, reduce_dtype):
+    from distributeddeeplearningspark_amd.parallel.ddp import DataParallel
+
+    m = _model()
+    rd = torch.bfloat16 if reduce_dtype == "bf16" else torch.float32
+    ddp = DataParallel(m, pg, bucket_mb=0.001, overlap=True, reduce_dtype=rd)
+    assert len(ddp.buckets) >= 3, len(ddp.buckets)
+    launched = []
+    orig = ddp._launch
+    ddp._launch = lambda i: (launched.append(i), orig(i))[1]
+    ddp.broadcast_parameters()
+    x, y = _data()
+    losses = [float(ddp.train_step(x[s, rank], y[s, rank])) for s in range(STEPS)]
+    ddp.check_replicas()
+    # buckets go out strictly in index order, every step, every rank
+    assert launched == list(range(len(ddp.buckets))) * STEPS, launched
+    return m.arena.master.detach().clone().numpy(), losses
+
+
+def _emulate():
+    m = _model()
+    x, y = _data()
+    for s in range(STEPS):
+        g = torch.zeros_like(m.arena.grad)
+        for r in range(N):
+            m.backward_step(x[s, r], y[s, r])
+            g += m.arena.grad
+        m.arena.grad.copy_(g)
+        m.optimizer.step(grad_scale=1.0 / N)
+    return m.arena.master.detach().numpy()
+
+
+@pytest.mark.parametrize("reduce_dtype", ["fp32", "bf16"])
+def test_ddp_overlap_hooks_n4_match_emulation(reduce_dtype):
+    from distributeddeeplearningspark_amd.parallel.launcher import run_workers
+
+    res = run_workers(_ddp_worker, N, [(reduce_dtype,)] * N, device="cpu")
+    ref = _emulate()
+    for w, _ in res:  # identical replicas
+        np.testing.assert_array_equal(w, res[0][0])
+    rel = np.linalg.norm(res[0][0] - ref) / np.linalg.norm(ref)
+    assert rel < (1e-5 if reduce_dtype == "fp32" else 2e-3), rel
+
+
+def test_all_reduce_flat_chunks_and_average():
+    from distributeddeeplearningspark_amd.parallel.launcher import run_workers
+
+    res = run_workers(_flat_worker, N, [()] * N, device="cpu")
+    for r in res:
+        np.testing.assert_allclose(r, np.arange(1000, dtype=np.float32) * (N + 1) / 2)
+
+
+def _flat_worker(rank, world, pg):
+    from distributeddeeplearningspark_amd.parallel.ddp import all_reduce_flat
+
+    t = torch.arange(1000, dtype=torch.float32) * (rank + 1)
+    all_reduce_flat(pg, t, bucket_bytes=256, average=True)  # 64-element chunks
+    return t.numpy()
+
+
+_FORCED = r"""
+import json, sys, torch
+sys.path.insert(0, {root!r})
+from distributeddeeplearningspark_amd.parallel import comm
+from distributeddeeplearningspark_amd.parallel.ddp import DataParallel
+sys.path.insert(0, {tests!r})
+from test_ddp_cpu import _model, _data
+pg = comm.init_from_env(prefer_gpu=False)
+assert pg.distributed and pg.forced and pg.world_size == 1 and pg.backend == "gloo", pg
+m = _model()
+ddp = DataParallel(m, pg, bucket_mb=0.001, reduce_dtype={rd})
+n = [0]
+orig = ddp._launch
+ddp._launch = lambda i: (n.__setitem__(0, n[0] + 1), orig(i))[1]
+x, y = _data()
+for s in range(2):
+    ddp.train_step(x[s, 0], y[s, 0])
+assert n[0] == 2 * len(ddp.buckets), (n, len(ddp.buckets))
+torch.save(m.arena.master.detach().clone(), {out!r})
+pg.shutdown()
+"""
+
+
+@pytest.mark.parametrize("rd", ["torch.float32", "torch.bfloat16"])
+def test_forced_world1_process_group_runs_collectives(tmp_path, rd):
+    out = str(tmp_path / "w.pt")
+    code = _FORCED.format(root=ROOT, tests=os.path.join(ROOT, "tests"), out=out, rd=rd)
+    env = dict(os.environ, DDL_FORCE_DIST="1", WORLD_SIZE="1", RANK="0")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    got = torch.load(out, weights_only=True)
+    m = _model()
+    x, y = _data()
+    for s in range(2):
+        m.train_on_batch(x[s, 0], y[s, 0])
+    ref = m.arena.master.detach()
+    rel = ((got - ref).norm() / ref.norm()).item()
+    assert rel < (1e-6 if rd == "torch.float32" else 2e-3), rel
