@@ -80,10 +80,11 @@ __global__ __launch_bounds__(g256::THREADS, 1) void gemm256_kernel(const GemmPar
   __shared__ __attribute__((aligned(16))) char smem[8 * HALF];  // ring: [tile parity][A0, A1, B0, B1]
 
   const int tiles_n = (p.N + 255) >> 8;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  int bid, split;
+  grid_tile(bid, split);
   const int tm = bid / tiles_n, tn = bid - tm * tiles_n;
   const int m0 = tm * 256, n0 = tn * 256;
-  const int kbeg = blockIdx.y * p.k_split;
+  const int kbeg = split * p.k_split;
   const int nk = (min(p.K, kbeg + p.k_split) - kbeg) >> 6;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wr = wid >> 2, wc = wid & 3;

@@ -46,6 +46,7 @@ __device__ __forceinline__ int rc_swz(int k) {
 
 __device__ __forceinline__ uint4 ldg16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
 
+
 // ----------------------------------------------------------------------------------------
 // Operand loaders. R = tile extent along the operand's row dimension (BM for A, BN for B).
 // ----------------------------------------------------------------------------------------
@@ -404,10 +405,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams
   char* lds_b1 = smem + 2 * A_BYTES + B_BYTES;
 
   const int tiles_n = (p.N + BN - 1) / BN;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  int bid, split;
+  grid_tile(bid, split);
   const int tm = bid / tiles_n, tn = bid - tm * tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int kbeg = blockIdx.y * p.k_split;
+  const int kbeg = split * p.k_split;
   const int kend = min(p.K, kbeg + p.k_split);
   const int nk = (kend - kbeg + BK - 1) / BK;
 
@@ -484,10 +486,11 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tiles_n = (p.N + BN - 1) / BN;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  int bid, split;
+  grid_tile(bid, split);
   const int tm = bid / tiles_n, tn = bid - tm * tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int kbeg = blockIdx.y * p.k_split;
+  const int kbeg = split * p.k_split;
   const int kend = min(p.K, kbeg + p.k_split);
   const int nk = (kend - kbeg + BK - 1) / BK;
 
