@@ -173,7 +173,8 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
 void register_ops(py::module& m);      // ops_bindings.cpp style registrations (elementwise, norms, ...)
 void register_runtime(py::module& m);  // host runtime (parameter server, ingest)
 void register_transformer(py::module& m);  // attention, LayerNorm, embeddings
-void register_rnn(py::module& m);          // persistent GRU / LSTM
+void register_rnn(py::module& m);          // persistent GRU / LSTM / SimpleRNN
+void register_layer_ops(py::module& m);    // Keras layer element-wise ops, fp32 GEMM
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "MI355X-native kernels and runtime of distributeddeeplearningspark_amd";
@@ -201,5 +202,6 @@ PYBIND11_MODULE(_C, m) {
   register_ops(m);
   register_transformer(m);
   register_rnn(m);
+  register_layer_ops(m);
   register_runtime(m);
 }

@@ -137,15 +137,54 @@ int embed_bwd(const int64_t* ids, const int64_t* types, const void* ds, float* g
 // hs/cs: [B][T+1][H]; gates: [B][T][G*H] post-activation
 bool rnn_fast_path(int H);
 bool rnn_fuses_input(int H, int I);
+// the register-resident kernels apply for this (cell, H, activations)
+bool rnn_reg_path(int cell, int H, int act, int ract);
+// cell 0 = GRU, 1 = LSTM, 2 = SimpleRNN; act / ract = ActCode of the activation / recurrent activation
+// (the register-resident fast path serves tanh + hard_sigmoid GRU/LSTM, the generic kernels the rest)
 int rnn_fwd(int cell, const float* xw, const float* x, const float* W, const float* b, int I, const float* U,
-            float* hs, float* cs, float* gates, float* y, int B, int T, int H, int rs, hipStream_t s);
+            float* hs, float* cs, float* gates, float* y, int B, int T, int H, int rs, int act, int ract,
+            hipStream_t s);
 // gU/gW/gb (fp32, nullable gb) += parameter gradients from dgates (one launch, atomics)
 int rnn_param_grad(int cell, const float* dg, const float* hs, const float* gates, const float* x, float* gU,
                    float* gW, float* gb, int B, int T, int H, int I, hipStream_t s);
 // UT = U^T [G*H][H] (generic path only); dgates [B][T][G*H] = gradients of the gate pre-activations
 bool rnn_bwd_uses_ut(int H);
 int rnn_bwd(int cell, const float* dy, const float* U, const float* UT, const float* hs, const float* cs,
-            const float* gates, float* dgates, int B, int T, int H, int rs, hipStream_t s);
+            const float* gates, float* dgates, int B, int T, int H, int rs, int act, int ract, hipStream_t s);
+
+// ---------------- Keras layer element-wise ops (kernels/layer_ops.hip) ----------------
+// activation codes shared by the standalone Activation layer and the recurrent cells
+enum ActCode : int {
+  ACT_C_LINEAR = 0, ACT_C_RELU = 1, ACT_C_TANH = 2, ACT_C_SIGMOID = 3, ACT_C_HARD_SIGMOID = 4,
+  ACT_C_ELU = 5, ACT_C_SELU = 6, ACT_C_SOFTPLUS = 7, ACT_C_GELU = 8,
+};
+// y = f(x); dx = dy * f'(.) from ref = y (ref = x for GELU).  bf16 != 0: bf16 storage, else fp32
+int act_fwd(const void* x, void* y, long n, int code, int bf16, hipStream_t s);
+int act_bwd(const void* dy, const void* ref, void* dx, long n, int code, int bf16, hipStream_t s);
+// softmax over the last axis of [R][N]; dx = y * (dy - <dy, y>)
+int softmax_rows_fwd(const void* x, void* y, long R, int N, int bf16, hipStream_t s);
+int softmax_rows_bwd(const void* dy, const void* y, void* dx, long R, int N, int bf16, hipStream_t s);
+// y = keep(i) ? x * scale : 0 with keep(i) = drop_hash(seed + i) >= thresh (also the backward)
+int dropout_apply(const void* x, void* y, long n, unsigned long long seed, uint32_t thresh, float scale, int bf16,
+                  hipStream_t s);
+// NHWC average pooling, padding excluded from the divisor
+int avgpool2d_fwd(const void* x, void* y, int N, int H, int W, int C, int Ho, int Wo, int kh, int kw, int sh, int sw,
+                  int ph, int pw, int bf16, hipStream_t s);
+int avgpool2d_bwd(const void* dy, void* dx, int N, int H, int W, int C, int Ho, int Wo, int kh, int kw, int sh, int sw,
+                  int ph, int pw, int bf16, hipStream_t s);
+// Keras Embedding: out[t] = table[ids[t]] (bad[0] |= 1 on an out-of-range id, row zeroed);
+// backward gw[ids[t]] += dy[t] (fp32 atomics)
+int embedding_gather(const int64_t* ids, const void* table, void* out, long n, int D, long V, int* bad, int bf16,
+                     hipStream_t s);
+int embedding_scatter(const int64_t* ids, const void* dy, float* gw, long n, int D, long V, int bf16, hipStream_t s);
+// y[C][R] = x[R][C] (fp32)
+int transpose_f32(const float* x, float* y, int R, int C, hipStream_t s);
+// db[n] += sum_m dy[m][n] (fp32, dense rows of N)
+int colsum_f32(const float* dy, float* db, long M, int N, hipStream_t s);
+// fp32 MFMA GEMM (kernels/gemm_f32.hip): C = alpha * A B + beta * C (+ bias[n]) (relu);
+// A(m,k) = a[m*sam + k*sak], B(k,n) = b[k*sbk + n*sbn]
+int gemm_f32(const float* a, long sam, long sak, const float* b, long sbk, long sbn, float* c, long ldc, int M, int N,
+             int K, float alpha, float beta, const float* bias, int relu, hipStream_t s);
 
 // ---------------- device ETL (dist-keras column transformers, fp64) ----------------
 int etl_minmax(const double* x, double* y, long n, double o_min, double scale, double n_min, hipStream_t s);

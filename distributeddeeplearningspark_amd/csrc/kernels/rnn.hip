@@ -1,5 +1,7 @@
-// Persistent recurrent kernels (Keras-2 GRU reset_after=False and LSTM; tanh + hard_sigmoid),
-// fp32 like the reference's Keras models (GRU(128) / LSTM(128) over 25 steps).
+// Persistent recurrent kernels (Keras-2 GRU reset_after=False, LSTM and SimpleRNN), fp32 like the
+// reference's Keras models (GRU(128) / LSTM(128) over 25 steps).  The generic
+// kernels take the activation / recurrent activation as ActCodes (ddl_act.h); the
+// register-resident fast path below serves the Keras defaults (tanh + hard_sigmoid).
 //
 // The input projection x W + b of ALL time steps is one GEMM done before the kernel; the
 // kernel then owns BB batch rows for the whole sequence: h (and c) stay in LDS across the
@@ -9,8 +11,7 @@
 // Backward (BPTT) runs the same persistent structure in reverse time, propagating dh (and dc)
 // with U^T columns per thread; it emits the pre-activation gate gradients of every step so
 // that dW, dU, db and dx are plain GEMMs / reductions afterwards.
-#include "ddl_common.h"
-#include "ddl_ops.h"
+#include "ddl_act.h"
 
 namespace ddl {
 namespace {
@@ -21,12 +22,12 @@ __device__ __forceinline__ float hsig(float x) { return fminf(fmaxf(0.2f * x + 0
 __device__ __forceinline__ float hsig_d(float y) { return (y > 0.f && y < 1.f) ? 0.2f : 0.f; }
 
 // ----------------------------------------------------------------------------- forward
-template <int CELL>  // 0 = GRU (gates z, r, h), 1 = LSTM (gates i, f, c, o)
+template <int CELL>  // 0 = GRU (gates z, r, h), 1 = LSTM (gates i, f, c, o), 2 = SimpleRNN (h)
 __global__ __launch_bounds__(512) void rnn_fwd_kernel(const float* __restrict__ xw, const float* __restrict__ U,
                                                       float* __restrict__ hs, float* __restrict__ cs,
                                                       float* __restrict__ gates, float* __restrict__ y, int B, int T,
-                                                      int H, int rs) {
-  constexpr int G = CELL == 0 ? 3 : 4;
+                                                      int H, int rs, int act, int ract) {
+  constexpr int G = CELL == 0 ? 3 : (CELL == 1 ? 4 : 1);
   extern __shared__ float sm[];
   const int GH = G * H;
   float* h = sm;              // [BB][H]
@@ -53,9 +54,10 @@ __global__ __launch_bounds__(512) void rnn_fwd_kernel(const float* __restrict__ 
 #pragma unroll
         for (int r = 0; r < BB; ++r) acc[r] += h[r * H + k] * u;
       }
-      const bool is_tanh = CELL == 1 && j >= 2 * H && j < 3 * H;
+      // LSTM candidate and SimpleRNN use the activation, every other gate the recurrent one
+      const bool main_act = CELL == 2 || (CELL == 1 && j >= 2 * H && j < 3 * H);
 #pragma unroll
-      for (int r = 0; r < BB; ++r) gb[r * GH + j] = is_tanh ? tanhf(acc[r]) : hsig(acc[r]);
+      for (int r = 0; r < BB; ++r) gb[r * GH + j] = act_f(main_act ? act : ract, acc[r]);
     }
     __syncthreads();
     if (CELL == 0) {
@@ -74,7 +76,7 @@ __global__ __launch_bounds__(512) void rnn_fwd_kernel(const float* __restrict__ 
           for (int r = 0; r < BB; ++r) acc[r] += c[r * H + k] * u;
         }
 #pragma unroll
-        for (int r = 0; r < BB; ++r) gb[r * GH + j] = tanhf(acc[r]);
+        for (int r = 0; r < BB; ++r) gb[r * GH + j] = act_f(act, acc[r]);
       }
       __syncthreads();
     }
@@ -82,13 +84,15 @@ __global__ __launch_bounds__(512) void rnn_fwd_kernel(const float* __restrict__ 
       const int r = i / H, k = i - r * H;
       const float* g = gb + r * GH;
       float hn;
-      if (CELL == 0) {
+      if (CELL == 2) {
+        hn = g[k];
+      } else if (CELL == 0) {
         const float z = g[k], hh = g[2 * H + k];
         hn = z * h[i] + (1.f - z) * hh;
       } else {
         const float cn = g[H + k] * c[i] + g[k] * g[2 * H + k];
         c[i] = cn;
-        hn = g[3 * H + k] * tanhf(cn);
+        hn = g[3 * H + k] * act_f(act, cn);
         cs[((long)(b0 + r) * (T + 1) + t + 1) * H + k] = cn;
       }
       h[i] = hn;
@@ -110,8 +114,8 @@ template <int CELL>
 __global__ __launch_bounds__(512) void rnn_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ UT,
                                                       const float* __restrict__ hs, const float* __restrict__ cs,
                                                       const float* __restrict__ gates, float* __restrict__ dgates,
-                                                      int B, int T, int H, int rs) {
-  constexpr int G = CELL == 0 ? 3 : 4;
+                                                      int B, int T, int H, int rs, int act, int ract) {
+  constexpr int G = CELL == 0 ? 3 : (CELL == 1 ? 4 : 1);
   extern __shared__ float sm[];
   const int GH = G * H;
   float* dh = sm;            // [BB][H] running dh (into h_t)
@@ -132,20 +136,22 @@ __global__ __launch_bounds__(512) void rnn_bwd_kernel(const float* __restrict__ 
       const float* g = gates + (row * T + t) * GH;
       const float hp = hs[(row * (T + 1) + t) * H + k];
       float* p = dp + r * GH;
-      if (CELL == 0) {
+      if (CELL == 2) {
+        p[k] = d * act_d(act, g[k]);
+      } else if (CELL == 0) {
         const float z = g[k], hh = g[2 * H + k];
-        p[k] = d * (hp - hh) * hsig_d(z);
-        p[2 * H + k] = d * (1.f - z) * (1.f - hh * hh);
+        p[k] = d * (hp - hh) * act_d(ract, z);
+        p[2 * H + k] = d * (1.f - z) * act_d(act, hh);
         aux[i] = d * z;
       } else {
         const float gi = g[k], gf = g[H + k], gg = g[2 * H + k], go = g[3 * H + k];
         const float cn = cs[(row * (T + 1) + t + 1) * H + k], cp = cs[(row * (T + 1) + t) * H + k];
-        const float tc = tanhf(cn);
-        const float dc = aux[i] + d * go * (1.f - tc * tc);
-        p[k] = dc * gg * hsig_d(gi);
-        p[H + k] = dc * cp * hsig_d(gf);
-        p[2 * H + k] = dc * gi * (1.f - gg * gg);
-        p[3 * H + k] = d * tc * hsig_d(go);
+        const float tc = act_f(act, cn);
+        const float dc = aux[i] + d * go * act_d(act, tc);
+        p[k] = dc * gg * act_d(ract, gi);
+        p[H + k] = dc * cp * act_d(ract, gf);
+        p[2 * H + k] = dc * gi * act_d(act, gg);
+        p[3 * H + k] = d * tc * act_d(ract, go);
         aux[i] = dc * gf;
       }
     }
@@ -159,7 +165,7 @@ __global__ __launch_bounds__(512) void rnn_bwd_kernel(const float* __restrict__ 
         for (int j = 0; j < H; ++j) drh += p[2 * H + j] * UT[(long)(2 * H + j) * H + k];
         const float hp = hs[(row * (T + 1) + t) * H + k];
         const float rg = gates[(row * T + t) * GH + H + k];
-        dp[r * GH + H + k] = drh * hp * hsig_d(rg);
+        dp[r * GH + H + k] = drh * hp * act_d(ract, rg);
         aux[i] += drh * rg;
       }
       __syncthreads();
@@ -471,7 +477,7 @@ __global__ __launch_bounds__(256) void rnn_param_grad_kernel(const float* __rest
                                                              const float* __restrict__ x, float* __restrict__ gU,
                                                              float* __restrict__ gW, float* __restrict__ gb, int B,
                                                              int T, int H, int I) {
-  constexpr int G = CELL == 0 ? 3 : 4;
+  constexpr int G = CELL == 0 ? 3 : (CELL == 1 ? 4 : 1);
   const int GH = G * H;
   const int M = H + I + (gb ? 1 : 0);
   const long BT = (long)B * T;
@@ -552,6 +558,9 @@ int launch_bwd_reg(const float* dy, const float* U, const float* hs, const float
 
 bool rnn_fast_path(int H) { return H == 128 || H == 64; }
 bool rnn_fuses_input(int H, int I) { return rnn_fast_path(H) && I <= IMAX; }
+bool rnn_reg_path(int cell, int H, int act, int ract) {
+  return (cell == 0 || cell == 1) && rnn_fast_path(H) && act == ACT_C_TANH && ract == ACT_C_HARD_SIGMOID;
+}
 
 // batch rows per workgroup of the register-resident kernels: fewer rows = more CUs busy and
 // less VALU work per step (the recurrence is latency-bound); DDL_RNN_BB overrides (1/2/4)
@@ -566,8 +575,10 @@ static int rnn_rows_per_wg(int dflt) {
 }
 
 int rnn_fwd(int cell, const float* xw, const float* x, const float* W, const float* b, int I, const float* U,
-            float* hs, float* cs, float* gates, float* y, int B, int T, int H, int rs, hipStream_t s) {
-  if (H == 128) {
+            float* hs, float* cs, float* gates, float* y, int B, int T, int H, int rs, int act, int ract,
+            hipStream_t s) {
+  const bool reg = rnn_reg_path(cell, H, act, ract);
+  if (reg && H == 128) {
     const int bb = rnn_rows_per_wg(RNN_BB_FWD);
 #define DDL_RNN_FWD(BBV)                                                                                    \
   return cell == 0 ? launch_fwd_reg<0, 128, BBV>(xw, x, W, b, I, U, hs, cs, gates, y, B, T, rs, s)           \
@@ -577,18 +588,20 @@ int rnn_fwd(int cell, const float* xw, const float* x, const float* W, const flo
     DDL_RNN_FWD(4);
 #undef DDL_RNN_FWD
   }
-  if (H == 64)
+  if (reg && H == 64)
     return cell == 0 ? launch_fwd_reg<0, 64, 2>(xw, x, W, b, I, U, hs, cs, gates, y, B, T, rs, s)
                      : launch_fwd_reg<1, 64, 2>(xw, x, W, b, I, U, hs, cs, gates, y, B, T, rs, s);
   if (!xw) return (int)hipErrorInvalidValue;  // generic kernels need the projection precomputed
-  const int G = cell == 0 ? 3 : 4;
+  const int G = cell == 0 ? 3 : (cell == 1 ? 4 : 1);
   const size_t lds = sizeof(float) * (2 * BB * H + BB * G * H);
   const int threads = std::min(512, ((G * H + 63) / 64) * 64);
   const dim3 grid((B + BB - 1) / BB);
   if (cell == 0)
-    hipLaunchKernelGGL(rnn_fwd_kernel<0>, grid, dim3(threads), lds, s, xw, U, hs, cs, gates, y, B, T, H, rs);
+    hipLaunchKernelGGL(rnn_fwd_kernel<0>, grid, dim3(threads), lds, s, xw, U, hs, cs, gates, y, B, T, H, rs, act, ract);
+  else if (cell == 1)
+    hipLaunchKernelGGL(rnn_fwd_kernel<1>, grid, dim3(threads), lds, s, xw, U, hs, cs, gates, y, B, T, H, rs, act, ract);
   else
-    hipLaunchKernelGGL(rnn_fwd_kernel<1>, grid, dim3(threads), lds, s, xw, U, hs, cs, gates, y, B, T, H, rs);
+    hipLaunchKernelGGL(rnn_fwd_kernel<2>, grid, dim3(threads), lds, s, xw, U, hs, cs, gates, y, B, T, H, rs, act, ract);
   return (int)hipGetLastError();
 }
 
@@ -596,20 +609,24 @@ bool rnn_bwd_uses_ut(int H) { return !rnn_fast_path(H); }
 
 int rnn_param_grad(int cell, const float* dg, const float* hs, const float* gates, const float* x, float* gU,
                    float* gW, float* gb, int B, int T, int H, int I, hipStream_t s) {
-  const int G = cell == 0 ? 3 : 4;
+  const int G = cell == 0 ? 3 : (cell == 1 ? 4 : 1);
+  if (cell == 0 && (2 * H) % 64) return (int)hipErrorInvalidValue;  // candidate columns start on a tile
   const int M = H + I + (gb ? 1 : 0);
   const long BT = (long)B * T;
   const dim3 grid((M + 63) / 64, (G * H + 63) / 64, (unsigned)((BT + PG_BT - 1) / PG_BT));
   if (cell == 0)
     hipLaunchKernelGGL(rnn_param_grad_kernel<0>, grid, dim3(256), 0, s, dg, hs, gates, x, gU, gW, gb, B, T, H, I);
-  else
+  else if (cell == 1)
     hipLaunchKernelGGL(rnn_param_grad_kernel<1>, grid, dim3(256), 0, s, dg, hs, gates, x, gU, gW, gb, B, T, H, I);
+  else
+    hipLaunchKernelGGL(rnn_param_grad_kernel<2>, grid, dim3(256), 0, s, dg, hs, gates, x, gU, gW, gb, B, T, H, I);
   return (int)hipGetLastError();
 }
 
 int rnn_bwd(int cell, const float* dy, const float* U, const float* UT, const float* hs, const float* cs,
-            const float* gates, float* dgates, int B, int T, int H, int rs, hipStream_t s) {
-  if (H == 128) {
+            const float* gates, float* dgates, int B, int T, int H, int rs, int act, int ract, hipStream_t s) {
+  const bool reg = rnn_reg_path(cell, H, act, ract);
+  if (reg && H == 128) {
     const int bb = rnn_rows_per_wg(RNN_BB_BWD);
 #define DDL_RNN_BWD(BBV)                                                                                    \
   return cell == 0 ? launch_bwd_reg<0, 128, BBV>(dy, U, hs, cs, gates, dgates, B, T, rs, s)                   \
@@ -619,17 +636,22 @@ int rnn_bwd(int cell, const float* dy, const float* U, const float* UT, const fl
     DDL_RNN_BWD(2);
 #undef DDL_RNN_BWD
   }
-  if (H == 64)
+  if (reg && H == 64)
     return cell == 0 ? launch_bwd_reg<0, 64, 2>(dy, U, hs, cs, gates, dgates, B, T, rs, s)
                      : launch_bwd_reg<1, 64, 2>(dy, U, hs, cs, gates, dgates, B, T, rs, s);
-  const int G = cell == 0 ? 3 : 4;
+  const int G = cell == 0 ? 3 : (cell == 1 ? 4 : 1);
   const size_t lds = sizeof(float) * (2 * BB * H + BB * G * H);
   const int threads = std::min(512, ((G * H + 63) / 64) * 64);
   const dim3 grid((B + BB - 1) / BB);
   if (cell == 0)
-    hipLaunchKernelGGL(rnn_bwd_kernel<0>, grid, dim3(threads), lds, s, dy, UT, hs, cs, gates, dgates, B, T, H, rs);
+    hipLaunchKernelGGL(rnn_bwd_kernel<0>, grid, dim3(threads), lds, s, dy, UT, hs, cs, gates, dgates, B, T, H, rs, act,
+                       ract);
+  else if (cell == 1)
+    hipLaunchKernelGGL(rnn_bwd_kernel<1>, grid, dim3(threads), lds, s, dy, UT, hs, cs, gates, dgates, B, T, H, rs, act,
+                       ract);
   else
-    hipLaunchKernelGGL(rnn_bwd_kernel<1>, grid, dim3(threads), lds, s, dy, UT, hs, cs, gates, dgates, B, T, H, rs);
+    hipLaunchKernelGGL(rnn_bwd_kernel<2>, grid, dim3(threads), lds, s, dy, UT, hs, cs, gates, dgates, B, T, H, rs, act,
+                       ract);
   return (int)hipGetLastError();
 }
 

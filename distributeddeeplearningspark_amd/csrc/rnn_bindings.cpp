@@ -1,6 +1,6 @@
-// pybind11 registrations of the persistent GRU / LSTM kernels (kernels/rnn.hip).  The input
-// projection and the parameter-gradient contractions are plain fp32 library GEMMs (ATen);
-// the recurrences run in the hand-written kernels.
+// pybind11 registrations of the persistent GRU / LSTM / SimpleRNN kernels (kernels/rnn.hip).
+// The input projection, the input gradient and (off the fused path) the parameter-gradient
+// contractions run on the fp32 MFMA GEMM (kernels/gemm_f32.hip); no library GEMM is called.
 #include <torch/extension.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <ATen/DeviceGuard.h>
@@ -15,14 +15,23 @@ namespace {
 inline hipStream_t cur_stream() { return at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
 
 int cell_id(const std::string& cell) {
-  TORCH_CHECK(cell == "gru" || cell == "lstm", "rnn: cell must be 'gru' or 'lstm'");
-  return cell == "gru" ? 0 : 1;
+  TORCH_CHECK(cell == "gru" || cell == "lstm" || cell == "rnn", "rnn: cell must be 'gru', 'lstm' or 'rnn'");
+  return cell == "gru" ? 0 : (cell == "lstm" ? 1 : 2);
+}
+int gates_of(int c) { return c == 0 ? 3 : (c == 1 ? 4 : 1); }
+
+// C[M][N] (fp32, row-major ldc) = alpha * A B + beta * C with element strides (gemm_f32)
+void f32mm(const at::Tensor& a, long sam, long sak, const at::Tensor& b, long sbk, long sbn, at::Tensor& c, long ldc,
+           int64_t M, int64_t N, int64_t K, float beta = 0.f, const float* bias = nullptr) {
+  const int e = gemm_f32(a.data_ptr<float>(), sam, sak, b.data_ptr<float>(), sbk, sbn, c.data_ptr<float>(), ldc, (int)M,
+                         (int)N, (int)K, 1.f, beta, bias, 0, cur_stream());
+  TORCH_CHECK(e == 0, "gemm_f32 launch failed: ", hipGetErrorString((hipError_t)e));
 }
 
 py::tuple rnn_fwd_(const std::string& cell, const at::Tensor& x, const at::Tensor& W, const at::Tensor& U,
-                   c10::optional<at::Tensor> b, bool rs) {
+                   c10::optional<at::Tensor> b, bool rs, int64_t act, int64_t ract) {
   const int c = cell_id(cell);
-  const int G = c == 0 ? 3 : 4;
+  const int G = gates_of(c);
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.dim() == 3, "rnn_fwd: x [B,T,I] fp32 on GPU");
   const int64_t B = x.size(0), T = x.size(1), I = x.size(2), H = U.size(0);
   TORCH_CHECK(W.size(0) == I && W.size(1) == G * H && U.size(1) == G * H, "rnn_fwd: W [I,GH], U [H,GH]");
@@ -31,10 +40,10 @@ py::tuple rnn_fwd_(const std::string& cell, const at::Tensor& x, const at::Tenso
   at::Tensor xc = x.contiguous(), Wc = W.contiguous();
   at::Tensor bc = b ? b->contiguous() : at::Tensor();
   at::Tensor xw;
-  if (!rnn_fuses_input((int)H, (int)I)) {  // wide inputs / generic kernels: one projection GEMM first
-    xw = at::matmul(xc.reshape({B * T, I}), Wc);
-    if (b) xw.add_(bc);
-    xw = xw.contiguous();
+  const bool reg = rnn_reg_path(c, (int)H, (int)act, (int)ract);
+  if (!(reg && rnn_fuses_input((int)H, (int)I))) {  // wide inputs / generic kernels: one projection GEMM first
+    xw = at::empty({B * T, G * H}, x.options());
+    f32mm(xc, I, 1, Wc, G * H, 1, xw, G * H, B * T, G * H, I, 0.f, bc.defined() ? bc.data_ptr<float>() : nullptr);
   }
   auto opt = x.options();
   at::Tensor hs = at::empty({B, T + 1, H}, opt);
@@ -45,7 +54,7 @@ py::tuple rnn_fwd_(const std::string& cell, const at::Tensor& x, const at::Tenso
   int e = rnn_fwd(c, xw.defined() ? xw.data_ptr<float>() : nullptr, xc.data_ptr<float>(), Wc.data_ptr<float>(),
                   bc.defined() ? bc.data_ptr<float>() : nullptr, (int)I, Uc.data_ptr<float>(), hs.data_ptr<float>(),
                   c == 1 ? cs.data_ptr<float>() : nullptr, gates.data_ptr<float>(), y.data_ptr<float>(), (int)B,
-                  (int)T, (int)H, rs ? 1 : 0, cur_stream());
+                  (int)T, (int)H, rs ? 1 : 0, (int)act, (int)ract, cur_stream());
   TORCH_CHECK(e == 0, "rnn_fwd launch failed: ", hipGetErrorString((hipError_t)e));
   py::list saved;
   saved.append(hs);
@@ -60,9 +69,10 @@ py::tuple rnn_fwd_(const std::string& cell, const at::Tensor& x, const at::Tenso
 py::tuple rnn_bwd_(const std::string& cell, const at::Tensor& dy, const at::Tensor& x, const at::Tensor& W,
                    const at::Tensor& U, c10::optional<at::Tensor> b, bool rs, std::vector<at::Tensor> saved,
                    c10::optional<at::Tensor> gW, c10::optional<at::Tensor> gU, c10::optional<at::Tensor> gb,
-                   bool need_dx) {
+                   bool need_dx, int64_t act, int64_t ract) {
   const int c = cell_id(cell);
-  const int G = c == 0 ? 3 : 4;
+  const int G = gates_of(c);
+  const bool reg = rnn_reg_path(c, (int)U.size(0), (int)act, (int)ract);
   const int64_t B = x.size(0), T = x.size(1), I = x.size(2), H = U.size(0);
   TORCH_CHECK(saved.size() == 3, "rnn_bwd: saved = [hs, cs, gates]");
   const at::Tensor& hs = saved[0];
@@ -71,17 +81,27 @@ py::tuple rnn_bwd_(const std::string& cell, const at::Tensor& dy, const at::Tens
   at::DeviceGuard g(x.device());
   at::Tensor dyc = dy.contiguous();
   at::Tensor Uc = U.contiguous();
-  at::Tensor UT = rnn_bwd_uses_ut((int)H) ? U.t().contiguous() : Uc;
+  at::Tensor UT = Uc;
+  if (!reg) {  // the generic kernels read U^T [GH][H]
+    UT = at::empty({G * H, H}, U.options());
+    const int et = transpose_f32(Uc.data_ptr<float>(), UT.data_ptr<float>(), (int)H, (int)(G * H), cur_stream());
+    TORCH_CHECK(et == 0, "transpose_f32 launch failed");
+  }
   at::Tensor dgates = at::empty({B, T, G * H}, x.options());
   int e = rnn_bwd(c, dyc.data_ptr<float>(), Uc.data_ptr<float>(), UT.data_ptr<float>(), hs.data_ptr<float>(),
                   c == 1 ? cs.data_ptr<float>() : nullptr, gates.data_ptr<float>(), dgates.data_ptr<float>(), (int)B,
-                  (int)T, (int)H, rs ? 1 : 0, cur_stream());
+                  (int)T, (int)H, rs ? 1 : 0, (int)act, (int)ract, cur_stream());
   TORCH_CHECK(e == 0, "rnn_bwd launch failed: ", hipGetErrorString((hipError_t)e));
   at::Tensor dg = dgates.view({B * T, G * H});
   at::Tensor xc = x.contiguous();
   py::object dx = py::none();
-  if (need_dx) dx = py::cast(at::matmul(dg, W.t()).view({B, T, I}));
-  const bool fused = rnn_fast_path((int)H) && gU && gW && (gb.has_value() == b.has_value());
+  at::Tensor Wc = W.contiguous();
+  if (need_dx) {  // dx[bt][i] = sum_j dg[bt][j] W[i][j]
+    at::Tensor dxt = at::empty({B * T, I}, x.options());
+    f32mm(dg, G * H, 1, Wc, 1, G * H, dxt, I, B * T, I, G * H);
+    dx = py::cast(dxt.view({B, T, I}));
+  }
+  const bool fused = (c != 0 || (2 * H) % 64 == 0) && gU && gW && (gb.has_value() == b.has_value());
   if (fused) {
     for (const auto* t : {&*gU, &*gW})
       TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous(), "rnn_bwd: fp32 contiguous grad buffers");
@@ -93,18 +113,31 @@ py::tuple rnn_bwd_(const std::string& cell, const at::Tensor& dy, const at::Tens
     TORCH_CHECK(e == 0, "rnn_param_grad launch failed: ", hipGetErrorString((hipError_t)e));
     return py::make_tuple(dx, py::none(), py::none(), py::none());
   }
-  at::Tensor x2 = xc.reshape({B * T, I});
-  at::Tensor dW = at::matmul(x2.t(), dg);
-  at::Tensor db = b ? dg.sum(0) : at::Tensor();
-  at::Tensor hp = hs.narrow(1, 0, T).reshape({B * T, H});
-  at::Tensor dU;
-  if (c == 0) {
-    dU = at::empty_like(U);
-    dU.narrow(1, 0, 2 * H).copy_(at::matmul(hp.t(), dg.narrow(1, 0, 2 * H)));
-    at::Tensor rh = gates.view({B * T, G * H}).narrow(1, H, H) * hp;
-    dU.narrow(1, 2 * H, H).copy_(at::matmul(rh.t(), dg.narrow(1, 2 * H, H)));
+  // unfused parameter gradients (no arena buffers given, or a GRU whose H does not tile): the
+  // same one-launch kernel into fresh zeroed buffers
+  at::Tensor dW = at::zeros({I, G * H}, x.options());
+  at::Tensor dU = at::zeros({H, G * H}, x.options());
+  at::Tensor db = b ? at::zeros({G * H}, x.options()) : at::Tensor();
+  if (c != 0 || (2 * H) % 64 == 0) {
+    e = rnn_param_grad(c, dg.data_ptr<float>(), hs.data_ptr<float>(), gates.data_ptr<float>(), xc.data_ptr<float>(),
+                       dU.data_ptr<float>(), dW.data_ptr<float>(), b ? db.data_ptr<float>() : nullptr, (int)B, (int)T,
+                       (int)H, (int)I, cur_stream());
+    TORCH_CHECK(e == 0, "rnn_param_grad launch failed: ", hipGetErrorString((hipError_t)e));
   } else {
-    dU = at::matmul(hp.t(), dg);
+    // GRU with 2H not a multiple of 64: dU = [h_{t-1}]^T dg for z,r and [r*h_{t-1}]^T dg for h
+    at::Tensor hp = hs.narrow(1, 0, T).contiguous().view({B * T, H});
+    at::Tensor rh = gates.view({B * T, G * H}).narrow(1, H, H).mul(hp).contiguous();
+    f32mm(xc, 1, I, dg, G * H, 1, dW, G * H, I, G * H, B * T);
+    f32mm(hp, 1, H, dg, G * H, 1, dU, G * H, H, 2 * H, B * T);
+    at::Tensor dUh = dU.narrow(1, 2 * H, H);
+    at::Tensor dgh = dg.narrow(1, 2 * H, H);
+    const int e2 = gemm_f32(rh.data_ptr<float>(), 1, H, dgh.data_ptr<float>(), G * H, 1, dUh.data_ptr<float>(), G * H,
+                            (int)H, (int)H, (int)(B * T), 1.f, 0.f, nullptr, 0, cur_stream());
+    TORCH_CHECK(e2 == 0, "gemm_f32 launch failed");
+    if (b) {
+      const int e3 = colsum_f32(dg.data_ptr<float>(), db.data_ptr<float>(), B * T, (int)(G * H), cur_stream());
+      TORCH_CHECK(e3 == 0, "colsum_f32 launch failed");
+    }
   }
   return py::make_tuple(dx, dW, dU, db.defined() ? py::cast(db) : py::none());
 }
@@ -112,8 +145,11 @@ py::tuple rnn_bwd_(const std::string& cell, const at::Tensor& dy, const at::Tens
 }  // namespace
 
 void register_rnn(py::module& m) {
-  m.def("rnn_fwd", &rnn_fwd_, "persistent GRU/LSTM forward (fp32)");
+  m.def("rnn_fwd", &rnn_fwd_, "persistent GRU/LSTM/SimpleRNN forward (fp32)", py::arg("cell"), py::arg("x"),
+        py::arg("W"), py::arg("U"), py::arg("b"), py::arg("rs"), py::arg("act") = (int64_t)ACT_C_TANH,
+        py::arg("ract") = (int64_t)ACT_C_HARD_SIGMOID);
   m.def("rnn_bwd", &rnn_bwd_, "persistent GRU/LSTM backward (fp32)", py::arg("cell"), py::arg("dy"), py::arg("x"),
         py::arg("W"), py::arg("U"), py::arg("b"), py::arg("rs"), py::arg("saved"), py::arg("gW") = py::none(),
-        py::arg("gU") = py::none(), py::arg("gb") = py::none(), py::arg("need_dx") = true);
+        py::arg("gU") = py::none(), py::arg("gb") = py::none(), py::arg("need_dx") = true,
+        py::arg("act") = (int64_t)ACT_C_TANH, py::arg("ract") = (int64_t)ACT_C_HARD_SIGMOID);
 }

@@ -231,6 +231,20 @@ class Model(Layer):
             self.optimizer.bind(self.arena)
         return self
 
+    @property
+    def graph_capturable(self) -> bool:
+        """False when a layer draws host-seeded per-step state (an active Dropout): a replayed
+        hipGraph would freeze its mask, so ``models/step.py`` trains such a model eagerly."""
+        if "_graph_capturable" in self.__dict__:
+            return self.__dict__["_graph_capturable"]
+        from .layers import Dropout
+
+        return not any(isinstance(l, Dropout) and l.rate > 0 for l in self.all_layers())
+
+    @graph_capturable.setter
+    def graph_capturable(self, v: bool):
+        self.__dict__["_graph_capturable"] = bool(v)
+
     def _keeps_fp32(self) -> bool:
         """Recurrent models train in fp32 on the GPU too: they are the reference's Keras
         regressors (fp32 GRU/LSTM, ``ddl_nyiso_aztk.py:201-203``), tiny and latency-bound, so

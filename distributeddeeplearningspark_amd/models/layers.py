@@ -15,6 +15,7 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
+from ..ops import act as act_ops
 from ..ops import conv as conv_ops
 from ..ops import linear as linear_ops
 from ..ops import norm as norm_ops
@@ -23,19 +24,8 @@ from ..ops import rnn as rnn_ops
 from . import params as P
 from .core import Layer
 
-_ACTS = {
-    None: None,
-    "linear": None,
-    "relu": torch.relu,
-    "tanh": torch.tanh,
-    "sigmoid": torch.sigmoid,
-    "hard_sigmoid": lambda x: torch.clamp(0.2 * x + 0.5, 0.0, 1.0),
-    "softmax": lambda x: torch.softmax(x.float(), dim=-1).to(x.dtype),
-    "elu": F.elu,
-    "selu": F.selu,
-    "softplus": F.softplus,
-    "gelu": F.gelu,
-}
+# activation names of the Keras layer set: HIP kernels on the GPU (ops/act.py), torch on the CPU
+_ACTS = (None, "linear") + act_ops.ACT_NAMES + ("softmax",)
 
 
 def _act_name(a):
@@ -49,8 +39,7 @@ def _act_name(a):
 
 
 def apply_activation(name, x):
-    f = _ACTS.get(name)
-    return x if f is None else f(x)
+    return act_ops.activation(x, name)
 
 
 def _pair(v):
@@ -215,8 +204,7 @@ class MaxPooling2D(Layer):
 
 class AveragePooling2D(MaxPooling2D):
     def call(self, x, training=False):
-        y = F.avg_pool2d(x.permute(0, 3, 1, 2), self.pool_size, self.strides, self._pad())
-        return y.permute(0, 2, 3, 1).contiguous()
+        return act_ops.avg_pool2d(x, self.pool_size, self.strides, self._pad())
 
 
 class GlobalAveragePooling2D(Layer):
@@ -256,7 +244,9 @@ class Dropout(Layer):
         self.rate = float(rate)
 
     def call(self, x, training=False):
-        return F.dropout(x, self.rate, training=training) if self.rate > 0 else x
+        # counter-hash mask seeded per call from a host counter (the backward regenerates it), so
+        # a model containing an active Dropout trains eagerly, not from a replayed hipGraph
+        return act_ops.dropout(x, self.rate, training)
 
     def get_config(self):
         return {**super().get_config(), "rate": self.rate}

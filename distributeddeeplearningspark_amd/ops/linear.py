@@ -2,7 +2,9 @@
 
 Weights are stored ``[out, in]`` (K-contiguous for the forward); the data gradient
 reads W row-contiguous (``ds_read_b64_tr_b16``) and the weight gradient accumulates
-fp32 into the gradient arena.
+fp32 into the gradient arena.  fp32 models (the reference's Keras regressors) run the same
+three contractions on the fp32 MFMA GEMM (``csrc/kernels/gemm_f32.hip``: exact fp32,
+element strides instead of transposed copies) with the bias / ReLU in its epilogue.
 """
 from __future__ import annotations
 
@@ -28,11 +30,13 @@ class _LinearFn(torch.autograd.Function):
         ctx.xshape = x.shape
         ctx.needs_dx = ctx.needs_input_grad[0]
         ctx.fp32 = ctx.native and x.dtype == torch.float32
-        if ctx.fp32:  # fp32 models (the reference's Keras regressors): a plain library GEMM
-            x2 = x.reshape(-1, x.shape[-1])
-            y = torch.addmm(b, x2, w.t()) if b is not None else x2 @ w.t()
-            if relu:
-                y = torch.relu_(y)
+        if ctx.fp32:  # fp32 models (the reference's Keras regressors): the fp32 MFMA GEMM
+            x2 = x.reshape(-1, x.shape[-1]).contiguous()
+            w = w.contiguous()
+            M, K, N = x2.shape[0], x2.shape[1], w.shape[0]
+            y = torch.empty((M, N), dtype=torch.float32, device=x.device)
+            C().gemm_f32(x2, K, 1, w, 1, K, y, N, M, N, K, 1.0, 0.0,
+                         None if b is None else b.float().contiguous(), bool(relu))
             ctx.gw, ctx.gb = gw, gb
             ctx.save_for_backward(x2, w, y if relu else None)
             return y.view(*x.shape[:-1], w.shape[0])
@@ -62,15 +66,20 @@ class _LinearFn(torch.autograd.Function):
         dx = None
         if ctx.fp32:
             x2, w, y = ctx.saved_tensors
-            d2 = dy.reshape(-1, w.shape[0])
+            M, K, N = x2.shape[0], x2.shape[1], w.shape[0]
+            d2 = dy.reshape(-1, N).float().contiguous()
             if relu:
-                d2 = d2 * (y > 0)
+                t = torch.empty_like(d2)
+                C().act_bwd(d2, y, t, C().ACT_CODES["relu"])
+                d2 = t
             if ctx.gb is not None:
-                ctx.gb.add_(d2.sum(0))
-            if ctx.gw is not None:
-                ctx.gw.addmm_(d2.t(), x2)
-            if ctx.needs_dx:
-                dx = (d2 @ w).view(ctx.xshape)
+                C().colsum_f32(d2, ctx.gb)
+            if ctx.gw is not None:  # gw[n][k] += sum_m d2[m][n] x2[m][k]
+                C().gemm_f32(d2, 1, N, x2, K, 1, ctx.gw, K, N, K, M, 1.0, 1.0, None, False)
+            if ctx.needs_dx:  # dx[m][k] = sum_n d2[m][n] w[n][k]
+                dxt = torch.empty((M, K), dtype=torch.float32, device=d2.device)
+                C().gemm_f32(d2, N, 1, w, K, 1, dxt, K, M, K, N, 1.0, 0.0, None, False)
+                dx = dxt.view(ctx.xshape)
         elif ctx.native:
             x2, w, y = ctx.saved_tensors
             gw, gb = ctx.gw, ctx.gb

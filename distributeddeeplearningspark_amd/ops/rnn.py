@@ -6,30 +6,27 @@ Math (Keras 2, the reference's GRU/LSTM, ``ddl_nyiso_aztk.py:201-203,249-251``):
   LSTM: i,f,o = hs(x W + h U + b) (gate order i,f,c,o); c = f*c + i*tanh(...); h = o*tanh(c)
 with hs = hard_sigmoid = clip(0.2x+0.5, 0, 1).
 
-The whole input projection x@W for all T steps is ONE GEMM; the recurrence runs in
-the persistent HIP kernel (``csrc/kernels/rnn.hip``) when available, else on the
-reference path below (fp32).  Parameter gradients accumulate into the arena.
+The whole input projection x@W for all T steps is ONE fp32 MFMA GEMM (or fused into the
+register-resident kernel for narrow inputs); the recurrence runs in the persistent HIP kernels
+(``csrc/kernels/rnn.hip``): the register-resident fast path for the Keras defaults (tanh +
+hard_sigmoid, H = 64/128), the generic kernels for every other activation pair, SimpleRNN and
+other widths.  CPU tensors use the reference path below.  Parameter gradients accumulate
+into the arena in one launch.
 """
 from __future__ import annotations
 
 import torch
 
-from ._native import C, has_native, use_native
+from ._native import C, use_native
 from ._ref import accumulate, ref_grads
 
 
 def _act(name):
-    if name in (None, "linear"):
-        return lambda x: x
-    if name == "tanh":
-        return torch.tanh
-    if name == "sigmoid":
-        return torch.sigmoid
-    if name == "relu":
-        return torch.relu
-    if name == "hard_sigmoid":
-        return lambda x: torch.clamp(0.2 * x + 0.5, 0.0, 1.0)
-    raise ValueError(f"unsupported activation {name!r}")
+    from .act import activation_ref
+
+    if name == "softmax" or name == "gelu":
+        raise ValueError(f"unsupported recurrent activation {name!r}")
+    return lambda x: activation_ref(name, x)
 
 
 def recurrent_ref(cell, x, W, U, b, return_sequences, activation="tanh", recurrent_activation="hard_sigmoid"):
@@ -73,9 +70,14 @@ class _RecurrentFn(torch.autograd.Function):
         dt = x.dtype
         xf, Wf, Uf = x.float(), W.float(), U.float()
         bf = None if b is None else b.float()
-        if use_native(x) and has_native() and hasattr(C(), "rnn_fwd") and act == "tanh" and ract == "hard_sigmoid" \
-                and cell in ("gru", "lstm"):
-            y, saved = C().rnn_fwd(cell, xf.contiguous(), Wf.contiguous(), Uf.contiguous(), bf, rs)
+        if use_native(x):
+            codes = C().ACT_CODES
+            for a in (act, ract):
+                if a not in codes or a == "gelu":
+                    raise ValueError(f"recurrent activation {a!r} has no HIP kernel (supported: "
+                                     f"{sorted(k for k in codes if k != 'gelu')})")
+            ctx.codes = (codes[act], codes[ract])
+            y, saved = C().rnn_fwd(cell, xf.contiguous(), Wf.contiguous(), Uf.contiguous(), bf, rs, *ctx.codes)
             ctx.native = True
             ctx.grads = (gW, gU, gb)
             ctx.needs_dx = ctx.needs_input_grad[0]
@@ -98,7 +100,7 @@ class _RecurrentFn(torch.autograd.Function):
             # fast path: dW/dU/db are accumulated into the fp32 arena slices in-kernel (None here)
             fp32 = lambda t: t if t is not None and t.dtype == torch.float32 and t.is_contiguous() else None
             dx, dW, dU, db = C().rnn_bwd(cell, dy.float().contiguous(), xf, Wf, Uf, bf, rs, list(saved[4:]),
-                                         fp32(gW), fp32(gU), fp32(gb), ctx.needs_dx)
+                                         fp32(gW), fp32(gU), fp32(gb), ctx.needs_dx, *ctx.codes)
         else:
             fn = lambda xx, ww, uu, bb: recurrent_ref(cell, xx, ww, uu, bb, rs, act, ract)
             dx, dW, dU, db = ref_grads(fn, [xf, Wf, Uf, bf], dy.float())

@@ -1,0 +1,216 @@
+"""GPU numerics of the Keras layer kernels (csrc/kernels/layer_ops.hip, gemm_f32.hip, the generic
+recurrent cells of rnn.hip) against plain PyTorch fp32 references of the same op, and a check
+that a GPU model built from these layers launches only the framework's HIP kernels."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _C():
+    from distributeddeeplearningspark_amd.ops._native import C
+
+    return C()
+
+
+# ------------------------------------------------------------------------------- fp32 GEMM
+@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (800, 384, 25), (77, 130, 513), (128, 64, 16), (5, 300, 1)])
+@pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (False, True), (True, True)])
+def test_gemm_f32_strides(M, N, K, ta, tb):
+    g = torch.Generator(device=DEV).manual_seed(M * 7 + N)
+    A = torch.randn(M, K, device=DEV, generator=g)
+    B = torch.randn(K, N, device=DEV, generator=g)
+    a = A.t().contiguous() if ta else A  # stored transposed: A(m,k) = a[k*M + m]
+    b = B.t().contiguous() if tb else B
+    sam, sak = (1, M) if ta else (K, 1)
+    sbk, sbn = (1, K) if tb else (N, 1)
+    bias = torch.randn(N, device=DEV, generator=g)
+    C0 = torch.randn(M, N, device=DEV, generator=g)
+    c = C0.clone()
+    _C().gemm_f32(a, sam, sak, b, sbk, sbn, c, N, M, N, K, 0.5, 1.0, bias, True)
+    ref = torch.relu(0.5 * (A.double() @ B.double()) + C0.double() + bias.double())
+    torch.testing.assert_close(c.double(), ref, rtol=1e-5, atol=1e-4)
+
+
+# ------------------------------------------------------------------------------- activations
+ACTS = ["relu", "tanh", "sigmoid", "hard_sigmoid", "elu", "selu", "softplus", "gelu"]
+
+
+@pytest.mark.parametrize("name", ACTS + ["softmax"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_activation_kernels(name, dtype):
+    from distributeddeeplearningspark_amd.ops import act as A
+
+    g = torch.Generator(device=DEV).manual_seed(3)
+    x0 = (torch.randn(37, 70, device=DEV, generator=g) * 3).to(dtype)
+    dy = torch.randn(37, 70, device=DEV, generator=g).to(dtype)
+    x = x0.clone().requires_grad_(True)
+    y = A.activation(x, name)
+    y.backward(dy)
+    xr = x0.float().clone().requires_grad_(True)
+    yr = A.activation_ref(name, xr)
+    yr.backward(dy.float())
+    tol = dict(rtol=2e-2, atol=2e-2) if dtype == torch.bfloat16 else dict(rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(y.float(), yr, **tol)
+    gx, gr = x.grad.float(), xr.grad
+    if name == "hard_sigmoid":  # derivative from the (rounded) output: compare away from the clip kinks
+        keep = (x0.float().abs() - 2.5).abs() > 0.1
+        gx, gr = gx[keep], gr[keep]
+    torch.testing.assert_close(gx, gr, **tol)
+
+
+def test_dropout_kernel_mask_and_backward():
+    from distributeddeeplearningspark_amd.ops import act as A
+
+    x = torch.ones(1 << 20, device=DEV).requires_grad_(True)
+    y = A.dropout(x, 0.25, True, seed=1234)
+    kept = (y != 0).float()
+    frac = float(kept.mean())
+    assert abs(frac - 0.75) < 0.005, frac
+    torch.testing.assert_close(y[y != 0], torch.full_like(y[y != 0], 1 / 0.75))
+    y.backward(torch.ones_like(y))
+    torch.testing.assert_close(x.grad, kept / 0.75)  # same mask regenerated in backward
+    y2 = A.dropout(x.detach(), 0.25, True, seed=1234)
+    assert torch.equal(y2, y.detach())
+    assert A.dropout(x, 0.25, False) is x
+
+
+@pytest.mark.parametrize("k,s,p", [((2, 2), (2, 2), (0, 0)), ((3, 3), (1, 1), (1, 1)), ((3, 3), (2, 2), (1, 1)),
+                                   ((2, 3), (1, 2), (0, 1))])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_avgpool2d_kernel(k, s, p, dtype):
+    from distributeddeeplearningspark_amd.ops import act as A
+
+    g = torch.Generator(device=DEV).manual_seed(5)
+    x0 = torch.randn(3, 11, 9, 20, device=DEV, generator=g).to(dtype)
+    x = x0.clone().requires_grad_(True)
+    y = A.avg_pool2d(x, k, s, p)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr = x0.double().cpu().requires_grad_(True)  # CPU fp64 reference
+    yr = A.avgpool_ref(xr, k, s, p)
+    yr.backward(dy.double().cpu())
+    tol = dict(rtol=2e-2, atol=2e-2) if dtype == torch.bfloat16 else dict(rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(y.double().cpu(), yr.detach(), **tol)
+    torch.testing.assert_close(x.grad.double().cpu(), xr.grad, **tol)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_embedding_kernel(dtype):
+    from distributeddeeplearningspark_amd.ops.embedding import embedding
+
+    g = torch.Generator(device=DEV).manual_seed(9)
+    W = torch.randn(50, 24, device=DEV, generator=g).to(dtype)
+    ids = torch.randint(0, 50, (6, 13), device=DEV, generator=g)
+    gw = torch.zeros(50, 24, device=DEV)
+    w = W.clone().requires_grad_(True)  # as in the arena: compute weights anchor the autograd graph
+    out = embedding(ids, w, grad_w=gw)
+    torch.testing.assert_close(out.float(), W.float()[ids])
+    dy = torch.randn_like(out)
+    out.backward(dy)
+    ref = torch.zeros(50, 24, device=DEV).index_add_(0, ids.reshape(-1), dy.float().reshape(-1, 24))
+    torch.testing.assert_close(gw, ref, rtol=1e-5, atol=1e-5)
+
+
+# ------------------------------------------------------------------------------- recurrent cells
+@pytest.mark.parametrize("cell,H,act,ract", [("rnn", 32, "tanh", "hard_sigmoid"), ("rnn", 100, "relu", "sigmoid"),
+                                             ("gru", 32, "tanh", "sigmoid"), ("lstm", 96, "tanh", "sigmoid"),
+                                             ("gru", 128, "relu", "hard_sigmoid"), ("lstm", 48, "elu", "hard_sigmoid"),
+                                             ("gru", 24, "tanh", "hard_sigmoid")])
+@pytest.mark.parametrize("rs", [False, True])
+def test_generic_recurrent_kernels(cell, H, act, ract, rs):
+    from distributeddeeplearningspark_amd.ops import rnn as R
+
+    G = {"rnn": 1, "gru": 3, "lstm": 4}[cell]
+    B, T, I = 5, 7, 3
+    g = torch.Generator(device=DEV).manual_seed(H + G)
+    x0 = torch.randn(B, T, I, device=DEV, generator=g)
+    W = torch.randn(I, G * H, device=DEV, generator=g) * 0.3
+    U = torch.randn(H, G * H, device=DEV, generator=g) * (0.5 / H ** 0.5)
+    b = torch.randn(G * H, device=DEV, generator=g) * 0.1
+    gW, gU, gb = torch.zeros_like(W), torch.zeros_like(U), torch.zeros_like(b)
+    x = x0.clone().requires_grad_(True)
+    y = R.recurrent(cell, x, W, U, b, grads=(gW, gU, gb), return_sequences=rs, activation=act,
+                    recurrent_activation=ract)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr, Wr, Ur, br = (t.detach().double().requires_grad_(True) for t in (x0, W, U, b))
+    yr = R.recurrent_ref(cell, xr, Wr, Ur, br, rs, act, ract)
+    yr.backward(dy.double())
+    torch.testing.assert_close(y.double(), yr, rtol=1e-4, atol=1e-5)
+    for got, ref in ((x.grad, xr.grad), (gW, Wr.grad), (gU, Ur.grad), (gb, br.grad)):
+        torch.testing.assert_close(got.double(), ref, rtol=1e-3, atol=1e-4)
+
+
+# ------------------------------------------------------------------------------- fp32 Dense
+def test_fp32_dense_on_gemm_f32():
+    from distributeddeeplearningspark_amd.ops.linear import linear
+
+    g = torch.Generator(device=DEV).manual_seed(11)
+    x0 = torch.randn(33, 17, device=DEV, generator=g)
+    w = torch.randn(9, 17, device=DEV, generator=g)
+    b = torch.randn(9, device=DEV, generator=g)
+    gw, gb = torch.zeros_like(w), torch.zeros_like(b)
+    x = x0.clone().requires_grad_(True)
+    y = linear(x, w, b, relu=True, grad_w=gw, grad_b=gb)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr, wr, br = (t.clone().double().requires_grad_(True) for t in (x0, w, b))
+    yr = torch.relu(xr @ wr.t() + br)
+    yr.backward(dy.double())
+    torch.testing.assert_close(y.double(), yr, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(x.grad.double(), xr.grad, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(gw.double(), wr.grad, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(gb.double(), br.grad, rtol=1e-5, atol=1e-5)
+
+
+# ------------------------------------------------------------------------------- no torch kernels
+def _kernel_names(fn):
+    from torch.profiler import ProfilerActivity, profile
+
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        fn()
+        torch.cuda.synchronize()
+    return {e.name for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA}
+
+
+# torch kernels that would mean a layer's COMPUTE fell back to ATen / MIOpen / hipBLASLt.  Glue
+# that stays in ATen (copies into static buffers, memsets, the scalar loss mean) is not listed.
+_DENY = ("tanh", "sigmoid", "elu", "gelu", "softplus", "softmax", "dropout", "bernoulli", "avg_pool", "AvgPool",
+         "avgpool", "embedding", "index_add", "indexing_backward", "Cijk", "gemm", "Gemm", "addmm", "nll", "max_pool",
+         "MaxPool", "miopen", "rnn", "lstm", "gru", "relu", "threshold")
+
+
+@pytest.mark.parametrize("which", ["dense_dropout", "embed_rnn", "avgpool_cnn"])
+def test_layer_models_run_only_hip_kernels(which):
+    from distributeddeeplearningspark_amd.models import layers as L
+    from distributeddeeplearningspark_amd.models.core import Sequential
+
+    torch.manual_seed(0)
+    if which == "dense_dropout":
+        m = Sequential([L.Dense(64, input_shape=(20,), activation="tanh"), L.Dropout(0.3), L.Activation("sigmoid"),
+                        L.Dense(32, activation="elu"), L.Dense(10), L.Activation("softmax")])
+        x, y = torch.randn(16, 20), torch.randint(0, 10, (16,))
+        loss = "sparse_categorical_crossentropy"
+    elif which == "embed_rnn":
+        m = Sequential([L.Embedding(100, 16, input_shape=(12,)), L.SimpleRNN(32, activation="relu"),
+                        L.Dense(1, activation="sigmoid")])
+        x, y = torch.randint(0, 100, (8, 12)), torch.rand(8, 1)
+        loss = "mean_squared_error"
+    else:
+        m = Sequential([L.Conv2D(16, (3, 3), input_shape=(12, 12, 8), padding="same"), L.Activation("relu"),
+                        L.AveragePooling2D((2, 2)), L.Flatten(), L.Dense(10, activation="softmax")])
+        x, y = torch.randn(4, 12, 12, 8), torch.randint(0, 10, (4,))
+        loss = "sparse_categorical_crossentropy"
+    m.compile("adam", loss)
+    m.place(DEV, seed=0)
+    xd, yd = m.to_input(x), m.to_target(y)
+    m.train_on_batch(xd, yd)  # warm-up (lazy workspaces)
+    names = _kernel_names(lambda: m.train_on_batch(xd, yd))
+    fallen = sorted(n for n in names if "ddl::" not in n and any(d in n for d in _DENY))
+    assert not fallen, f"layer compute ran on torch kernels: {fallen}"
+    assert any("ddl::" in n for n in names)
