@@ -383,7 +383,10 @@ int layernorm_fwd(const void* x, const float* gamma, const float* beta, void* y,
 }
 
 int ln_partial_rows(long M) {
-  // workgroups of the row-per-wave backward sweeps (4 waves each); DDL_LN_BWD_BLOCKS overrides
+  // workgroups of the row-per-wave backward sweeps (4 waves each); DDL_LN_BWD_BLOCKS overrides.
+  // The override is read ONCE per process (function-local static: setting it after the first
+  // LayerNorm / embedding backward has no effect) and also sizes embed_bwd's grid and its
+  // token-type partial-row workspace, which share this partial-row count.
   static const long cap = [] {
     const char* e = std::getenv("DDL_LN_BWD_BLOCKS");
     const long v = e ? std::atol(e) : 0;

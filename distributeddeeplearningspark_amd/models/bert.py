@@ -30,7 +30,6 @@ used by the tests as the numerics reference of the GPU path.
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import asdict, dataclass
 
 import numpy as np
@@ -111,21 +110,13 @@ def _bias_grad(d2, gb):
         C().bias_grad(d2, gb, d2.shape[1], True)
 
 
-# Epilogue-free weight/data gradients go to hipBLASLt ("plain library GEMMs"); the GEMMs with
-# fused bias/GELU/dropout/residual/LN-stat epilogues stay on the hand-written MFMA kernels.
-_LIB_GEMM = os.environ.get("DDL_BERT_LIB_GEMM", "0") == "1"  # measured slower end-to-end: off
-
-
+# Every BERT GEMM (fused-epilogue or plain) runs on the hand-written MFMA kernels; the
+# hipBLASLt route tried in round 1 measured slower end-to-end and was removed (PERFORMANCE.md).
 def _wgrad(d2, x2, gw):
-    if _LIB_GEMM and d2.is_cuda:
-        G.lib_wgrad(d2, x2, gw)
-    else:
-        G.linear_wgrad(d2, x2, gw)
+    G.linear_wgrad(d2, x2, gw)
 
 
 def _dgrad(dy, w):
-    if _LIB_GEMM and dy.is_cuda:
-        return G.lib_dgrad(dy, w)
     return G.linear_dgrad(dy, w)
 
 

@@ -198,18 +198,6 @@ def linear_wgrad(dy, x2, gw):
                 split_rounds=_LINEAR_WGRAD_ROUNDS)
 
 
-def lib_wgrad(dy, x2, gw):
-    """gw[N,K] += dy[M,N]^T @ x2[M,K] on hipBLASLt (bf16 in, fp32 out): for epilogue-free weight
-    gradients with a long reduction (BERT's M = B*S = 16384 rows), where the library GEMM is
-    1.3-1.6x faster than the 128-tile kernel's split-K RC x RC path (scripts/bench_gemm.py)."""
-    gw.add_(torch.mm(dy.t(), x2, out_dtype=torch.float32))
-
-
-def lib_dgrad(dy, w):
-    """dx[M,K] = dy[M,N] @ w[N,K] -> bf16 on hipBLASLt: data-gradients with no fused epilogue."""
-    return torch.mm(dy, w)
-
-
 def matmul(a, b, trans_a=False, trans_b=False, out=None, alpha=1.0):
     """General bf16 matmul op(a) @ op(b) -> bf16 using the KC/RC operand modes."""
     M = a.shape[1] if trans_a else a.shape[0]

@@ -383,3 +383,35 @@ def test_fused_bottleneck_matches_composed_ops():
     assert abs(res["1"][0] - res["0"][0]) < 1e-2 * max(1.0, abs(res["0"][0])), (res["1"][0], res["0"][0])
     g1, g0 = res["1"][1], res["0"][1]
     assert ((g1 - g0).norm() / g0.norm()).item() < 3e-2
+
+
+@pytest.mark.parametrize("kind", ["adam", "adamw", "adam_keras"])
+def test_adam_paired_slot_loop(kind):
+    """n = 2 x (4096 x 256 grid) x 4 plus an odd number of float4 slots (flat arenas are
+    multiples of 4): the two-float4-per-lane loop of the Adam kernel and its single-slot tail
+    both run (the small test above only reaches the tail); master weights, moments and the bf16
+    compute copy against the CPU reference."""
+    from distributeddeeplearningspark_amd.ops import optim as O
+
+    n = 2 * 4096 * 256 * 4 + 4 * 5
+    gen = torch.Generator().manual_seed(21)
+    w0, g = torch.randn(n, generator=gen), torch.randn(n, generator=gen)
+    outs = {}
+    for dev in ("cpu", DEV):
+        w, gd = w0.clone().to(dev), g.to(dev)
+        m, v = torch.zeros(n, device=dev), torch.zeros(n, device=dev)
+        w16 = torch.empty(n, dtype=torch.bfloat16, device=dev) if dev != "cpu" else None
+        for step in range(1, 3):
+            if kind == "adam":
+                O.adam_(w, gd, m, v, w16, lr=1e-3, weight_decay=1e-2, step=step)
+            elif kind == "adamw":
+                O.adam_(w, gd, m, v, w16, lr=1e-3, weight_decay=1e-2, decoupled=True, step=step)
+            else:
+                O.adam_(w, gd, m, v, w16, lr=1e-3, eps=1e-7, keras_eps=True, step=step)
+        outs[dev] = (w.cpu(), m.cpu(), v.cpu(), None if w16 is None else w16.float().cpu())
+    close(outs[DEV][0], outs["cpu"][0], rtol=1e-5, atol=1e-6, what=f"{kind} master")
+    close(outs[DEV][1], outs["cpu"][1], rtol=1e-5, atol=1e-6, what=f"{kind} m")
+    close(outs[DEV][2], outs["cpu"][2], rtol=1e-5, atol=1e-6, what=f"{kind} v")
+    close(outs[DEV][3], outs["cpu"][0], rtol=1e-2, atol=1e-2, what=f"{kind} bf16 copy")
+    # every index of the tail was written (a skipped element would keep w0)
+    assert not torch.equal(outs[DEV][0][-20:], w0[-20:])

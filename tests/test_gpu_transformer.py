@@ -274,3 +274,54 @@ def test_bias_grad_vector_and_scalar_paths(M, N, off):
     close(db, ref, rtol=1e-4, atol=1e-2, what="bias_grad")
     C().bias_grad(dy, db, N, False)
     close(db, dy.float().sum(0), rtol=1e-4, atol=1e-2, what="bias_grad overwrite")
+
+
+def _ln_bwd_case(M, H, parts, seed=0):
+    """layernorm_bwd at M rows straight through the binding: dx and the per-wave partial rows
+    of (dbias,) dgamma, dbeta reduced on the host, against fp32 autograd."""
+    from distributeddeeplearningspark_amd.ops._native import C
+
+    x = (rnd(M, H, seed=seed).float() * 2 + 0.5).to(torch.bfloat16)
+    dy = rnd(M, H, seed=seed + 1)
+    g = torch.rand(H, device=DEV) + 0.5
+    y = torch.empty_like(x)
+    mean, rstd = torch.empty(M, device=DEV), torch.empty(M, device=DEV)
+    C().layernorm_fwd(x, g, None, y, mean, rstd, 1e-12, 0.0, 0)
+    P = C().ln_partial_rows(M)
+    ws = torch.full((P, parts, H), float("nan"), device=DEV)
+    dx = torch.empty_like(x)
+    dxd = torch.empty_like(x) if parts == 3 else None
+    C().layernorm_bwd(dy, x, mean, rstd, g, dx, dxd, 0.0, 0, ws, 0.0, 0, parts)
+    red = ws.sum(0)
+    xr, gr = x.float().requires_grad_(True), g.clone().requires_grad_(True)
+    br = torch.zeros(H, device=DEV, requires_grad=True)
+    yr = torch.nn.functional.layer_norm(xr, (H,), gr, br, 1e-12)
+    yr.backward(dy.float())
+    close(dx, xr.grad, what=f"ln dx M={M}")
+    close(red[parts - 2], gr.grad, rtol=1e-2, atol=2e-2, what=f"ln dgamma M={M} parts={parts}")
+    close(red[parts - 1], br.grad, rtol=1e-2, atol=2e-2, what=f"ln dbeta M={M} parts={parts}")
+    if parts == 3:  # dbias = column sums of the (bf16) dx_drop the kernel stored
+        close(dxd, dx, rtol=0, atol=0, what="dx_drop at p = 0")
+        close(red[0], dxd.float().sum(0), rtol=1e-3, atol=1e-3, what=f"ln dbias M={M}")
+
+
+@pytest.mark.parametrize("parts", [2, 3])
+def test_layernorm_bwd_many_rows_per_wave(parts):
+    """M = 9001 (> 4 x the 512-workgroup cap, not a multiple of 4): every wave accumulates its
+    dgamma / dbeta (/ dbias) partial row over several LayerNorm rows."""
+    _ln_bwd_case(9001, 768, parts)
+
+
+def test_layernorm_bwd_blocks_override_child():
+    """DDL_LN_BWD_BLOCKS is read once per process (function-local static): check a small
+    override (3 workgroups) in a fresh child process."""
+    import os
+    import subprocess
+    import sys
+
+    code = ("import sys; sys.path.insert(0, 'tests'); import test_gpu_transformer as t; "
+            "t._ln_bwd_case(9001, 256, 2); t._ln_bwd_case(1000, 768, 3); print('ok')")
+    env = dict(os.environ, DDL_LN_BWD_BLOCKS="3")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
