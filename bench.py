@@ -40,6 +40,12 @@ def main():
                     help="1 = replay the whole step from a hipGraph (1-GPU runs without a process group "
                          "only).  Default off: measured neutral on ResNet-50 (9,532 vs 9,562 img/s) and "
                          "VGG-16 (74.3K vs 75.1K img/s) — both steps are GPU-bound, not launch-bound")
+    ap.add_argument("--via-dataframe", action="store_true",
+                    help="ResNet-50 through the DataFrame/trainer API: an ImageNet-shape uint8 frame, one partition "
+                         "per rank, SynchronousDataParallel(...).train(df); the timed window is the trainer's own "
+                         "steps after --warmup (barrier + synchronize on both sides)")
+    ap.add_argument("--ingest", default="auto", choices=["auto", "resident", "stream"],
+                    help="--via-dataframe: shard residency in HBM or the pinned-ring stream (ShardLoader)")
     ap.add_argument("--seq", type=int, default=512)
     ap.add_argument("--layers", type=int, default=12)
     args = ap.parse_args()
@@ -63,6 +69,8 @@ def main():
     torch.manual_seed(1234 + rank)
     if args.model == "bert":
         return bench_bert(args, pg)
+    if args.via_dataframe:
+        return bench_via_dataframe(args, pg)
     if args.model == "vgg16":
         from distributeddeeplearningspark_amd.models.zoo import vgg16
 
@@ -161,6 +169,51 @@ def comm_stats(ddp, pg):
     return {"comm_ms": round(full, 3), "exposed_comm_ms": round(exposed, 3), "bucket_mb": ddp.bucket_mb,
             "buckets": len(ddp.buckets), "reduce_dtype": "bf16" if ddp._red is not None else "fp32",
             "grad_mb": round(ddp.grad_bytes / 2**20, 1), "backend": pg.backend, "forced_pg": pg.forced}
+
+
+def bench_via_dataframe(args, pg):
+    """ResNet-50 trained by ``SynchronousDataParallel(...).train(df)`` on an ImageNet-shape
+    uint8 frame (the reference's path: DataFrame -> repartition -> one worker per partition,
+    ``ddl_mnist_aztk.py:155-161,216-219``).  Each rank holds the frame (SPMD driver program),
+    trains its partition: uint8 shard -> HBM (resident copy or the pinned-ring stream) ->
+    normalize_u8 -> forward/backward/all-reduce/SGD; timed by the trainer's worker."""
+    from distributeddeeplearningspark_amd.models import ResNet50
+    from distributeddeeplearningspark_amd.models.optimizers import SGD
+    from distributeddeeplearningspark_amd.sql.dataframe import from_columns
+    from distributeddeeplearningspark_amd.trainers import SynchronousDataParallel
+
+    rank, world = pg.rank, pg.world_size
+    per_rank = args.batch * (args.warmup + args.steps)
+    rng = np.random.default_rng(7)
+    n = per_rank * world
+    images = rng.integers(0, 256, (n, args.image, args.image, 3), dtype=np.uint8)
+    labels = rng.integers(0, 1000, n)
+    df = from_columns({"features": images, "label": labels}, num_partitions=world)
+    model = ResNet50(input_shape=(args.image, args.image, 3), num_classes=1000)
+    opt = SGD(lr=0.1, momentum=0.9, weight_decay=5e-5)
+    model.compile(opt, "sparse_categorical_crossentropy")
+    trainer = SynchronousDataParallel(model, worker_optimizer=opt, loss="sparse_categorical_crossentropy",
+                                      num_workers=world, batch_size=args.batch, num_epoch=1,
+                                      features_col="features", label_col="label", bucket_mb=args.bucket_mb,
+                                      ingest=args.ingest, timing_warmup=args.warmup)
+    trainer.train(df)
+    res = trainer._results
+    dt_max = max(r["timed_s"] for r in res)
+    steps = res[0]["timed_steps"]
+    gb = args.batch * world
+    if rank == 0:
+        print(json.dumps({
+            "metric": "images/sec (whole node) ResNet-50 ImageNet-shape at 1/2/4/8 MI355X",
+            "value": round(gb * steps / dt_max, 2), "unit": "images/sec", "n_gpus": world, "steps": steps,
+            "warmup": args.warmup, "ms_per_step": round(dt_max * 1000.0 / steps, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic uint8 ImageNet-shape DataFrame via SynchronousDataParallel.train",
+            "config": {"model": "resnet50", "global_batch": gb, "seq_len": None, "image": args.image,
+                       "per_gpu_batch": args.batch, "parallelism": f"dp{world}", "optimizer": "sgd-momentum",
+                       "path": "dataframe", "ingest": res[0]["ingest"],
+                       "final_loss": round(float(res[0]["history"][-1]), 4)},
+        }), flush=True)
+    pg.shutdown()
 
 
 def bench_bert(args, pg):

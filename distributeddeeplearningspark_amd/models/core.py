@@ -205,6 +205,10 @@ class Model(Layer):
         self.metrics: list = []
         self.history: list[float] = []
         self.seed = 0
+        # uint8 NHWC image inputs are normalised on the device by to_input:
+        # (x - mean[c]) / std[c]; default mean 0 / std 255 (Keras' rescale=1/255)
+        self.input_mean: tuple | None = None
+        self.input_std: tuple | None = None
 
     # ---------------------------------------------------------------- placement
     def build_model(self):
@@ -278,7 +282,28 @@ class Model(Layer):
             x = x.to(self.device, self.compute_dtype, non_blocking=True)
         else:
             x = x.to(self.device, non_blocking=True)
+            if x.dtype == torch.uint8 and x.dim() == 4:
+                x = self.normalize_images(x)
         return x
+
+    def normalize_images(self, x_u8: torch.Tensor) -> torch.Tensor:
+        """uint8 NHWC -> compute dtype, (x - mean) / std per channel: one HIP pass on the GPU
+        (``normalize_u8``, the kernel the ingest feeder uses), torch on the CPU."""
+        from ..ops._native import C, use_native
+
+        c = x_u8.shape[-1]
+        key = (str(x_u8.device), c, self.input_mean, self.input_std)
+        cache = self.__dict__.setdefault("_norm_cache", {})
+        if key not in cache:  # device-resident constants: no host->device copy per batch
+            mean = torch.tensor((self.input_mean or (0.0,) * c)[:c], dtype=torch.float32, device=x_u8.device)
+            std = torch.tensor((self.input_std or (255.0,) * c)[:c], dtype=torch.float32, device=x_u8.device)
+            cache[key] = (mean, std, (1.0 / std).contiguous())
+        mean, std, invstd = cache[key]
+        if use_native(x_u8):
+            out = torch.empty(x_u8.shape, dtype=self.compute_dtype, device=x_u8.device)
+            C().normalize_u8(x_u8.contiguous(), out, mean, invstd, c, c)
+            return out
+        return ((x_u8.to(torch.float32) - mean) / std).to(self.compute_dtype)
 
     def to_target(self, y) -> torch.Tensor:
         if isinstance(y, np.ndarray):
@@ -420,8 +445,11 @@ class Model(Layer):
         return self.arena.master
 
     def to_json(self) -> str:
-        return json.dumps({"class_name": type(self).__name__, "config": self.get_config(),
-                           "backend": "distributeddeeplearningspark_amd", "keras_version": "2.1.6"})
+        d = {"class_name": type(self).__name__, "config": self.get_config(),
+             "backend": "distributeddeeplearningspark_amd", "keras_version": "2.1.6"}
+        if self.input_mean is not None or self.input_std is not None:
+            d["input_normalization"] = {"mean": self.input_mean, "std": self.input_std}
+        return json.dumps(d)
 
     def summary(self, print_fn=print):
         self.build_model()
@@ -542,4 +570,9 @@ def model_from_json(s: str) -> Model:
     cls = _LAYER_TYPES.get(d["class_name"])
     if cls is None:
         raise ValueError(f"unknown model class {d['class_name']!r}")
-    return cls.from_config(d["config"])
+    m = cls.from_config(d["config"])
+    norm = d.get("input_normalization")
+    if norm:
+        m.input_mean = None if norm.get("mean") is None else tuple(norm["mean"])
+        m.input_std = None if norm.get("std") is None else tuple(norm["std"])
+    return m

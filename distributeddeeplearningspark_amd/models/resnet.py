@@ -120,6 +120,8 @@ class ResNet(Model):
                                               name=f"{self.name}/s{si + 1}b{bi + 1}"))
         self.fc = Dense(self.num_classes, name=self.name + "/fc")
         self.zero_init_residual = zero_init_residual
+        # uint8 ImageNet pixels fed through to_input (DataFrame path) get the standard normalisation
+        self.input_mean, self.input_std = (123.675, 116.28, 103.53), (58.395, 57.12, 57.375)
 
     def sublayers(self):
         return [self.stem, *self.stages, self.fc]
@@ -154,7 +156,9 @@ class ResNet(Model):
         y = self.fc.call(y, training)
         if logits:
             return y
-        return torch.softmax(y.float(), dim=-1)
+        from ..ops.act import activation
+
+        return activation(y, "softmax")
 
     def summary_rows(self):
         rows = [(f"{l.name} ({type(l).__name__})", "", l.count_params()) for l in self.sublayers()]

@@ -533,15 +533,22 @@ class DataFrame:
         return RDD([rows[s] for s in self.partition_slices()], self._ctx)
 
     def column_array(self, name: str, dtype=np.float32) -> np.ndarray:
-        """Dense numpy view of a (vector / array / scalar) column for the trainers."""
+        """Dense numpy view of a (vector / array / scalar) column for the trainers.
+
+        ``dtype=None`` keeps the column's own element type (uint8 image tensors stay uint8,
+        integer labels stay integers) and only narrows float64 to float32 — what the
+        trainers ship to the workers, so an ImageNet-shape frame is not inflated 4x."""
         cd = self._table().column(name)
         v = cd.values
         if v.dtype == object:
             v = np.stack([np.asarray(x.toArray() if hasattr(x, "toArray") else x, dtype=np.float64) for x in v])
+        if dtype is None:
+            dtype = np.float32 if v.dtype.kind == "f" else (np.int64 if v.dtype.kind == "b" else v.dtype)
         return np.ascontiguousarray(v.astype(dtype, copy=False))
 
     def partition_arrays(self, cols, dtype=np.float32):
-        """[(array per col) per partition] — how a trainer ships each shard to its worker."""
+        """[(array per col) per partition] — how a trainer ships each shard to its worker
+        (zero-copy slices of one array per column; ``dtype=None``: see :meth:`column_array`)."""
         full = [self.column_array(c, dtype) for c in cols]
         return [[a[s] for a in full] for s in self.partition_slices()]
 

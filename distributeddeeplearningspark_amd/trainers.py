@@ -39,7 +39,9 @@ Execution (MI355X-native, not a socket parameter server):
 from __future__ import annotations
 
 import copy
+import os
 import time
+import warnings
 
 import numpy as np
 import torch
@@ -52,11 +54,61 @@ from .utils import deserialize_keras_model, get_states, serialize_keras_model, s
 # =============================================================================================
 #                                    worker side
 # =============================================================================================
-def _to_device(a: np.ndarray, model):
+def _resident(a: np.ndarray, device):
+    """Copy a host shard into HBM once, in its own dtype, from pinned memory on a side stream:
+    the compute stream waits on an event (the host does not block on the transfer)."""
     t = torch.from_numpy(np.ascontiguousarray(a))
-    if t.is_floating_point():
-        return t.to(model.device, model.compute_dtype)
-    return t.to(model.device)
+    if device.type != "cuda":
+        return t
+    pinned = t.pin_memory()
+    side = torch.cuda.Stream(device)
+    with torch.cuda.stream(side):
+        d = pinned.to(device, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(side)
+    cur = torch.cuda.current_stream(device)
+    cur.wait_event(ev)
+    d.record_stream(cur)
+    return d
+
+
+class _ShardFeed:
+    """How a worker's partition reaches HBM (SURVEY north star: driver-side DataFrame ingest
+    streamed from pinned host buffers with hipMemcpyAsync on a side stream, overlapped with
+    compute).  Shards keep their column dtype (uint8 pixels stay uint8 on the wire and in HBM)
+    and uint8 NHWC images are normalised on the device by ``Model.to_input``.
+
+    * resident — shards up to ``DDL_RESIDENT_MB`` (default 4096 MB; 288 GB of HBM makes this
+      the common case): copied once (``_resident``), batches are device slices;
+    * stream — ``ingest="stream"`` or larger shards: the native ``BatchLoader``
+      (``csrc/runtime/loader.cpp``) fills a ring of pinned buffers on a C++ thread while the
+      previous batch trains and ``ShardLoader`` issues each H2D copy on a side stream.
+
+    Trailing partial batches are dropped (dist-keras worker behaviour)."""
+
+    def __init__(self, X, Y, model, cfg):
+        self.batch, self.epochs, self.n = int(cfg["batch_size"]), int(cfg["num_epoch"]), int(X.shape[0])
+        mode = cfg.get("ingest", "auto")
+        if mode not in ("auto", "resident", "stream"):
+            raise ValueError(f"ingest={mode!r}: expected 'auto', 'resident' or 'stream'")
+        dev = model.device
+        limit = float(os.environ.get("DDL_RESIDENT_MB", "4096")) * (1 << 20)
+        self.streaming = dev.type == "cuda" and (mode == "stream" or (mode == "auto" and X.nbytes + Y.nbytes > limit))
+        if self.streaming:
+            from .data.ingest import ShardLoader
+
+            self.loader = ShardLoader(X, Y, self.batch, device=dev, shuffle=False, drop_last=True)
+        else:
+            self.X, self.Y = _resident(X, dev), _resident(Y, dev)
+
+    def batches(self):
+        bs, nb = self.batch, self.n // self.batch
+        for _ in range(self.epochs):
+            if self.streaming:
+                yield from self.loader  # one epoch per pass over the loader
+            else:
+                for b in range(nb):
+                    yield self.X[b * bs:(b + 1) * bs], self.Y[b * bs:(b + 1) * bs]
 
 
 class _Worker:
@@ -76,12 +128,8 @@ class _Worker:
     def arena(self):
         return self.model.arena
 
-    def batches(self, X, Y):
-        bs = self.cfg["batch_size"]
-        n = X.shape[0] // bs  # trailing partial batch dropped (dist-keras worker behaviour)
-        for _ in range(self.cfg["num_epoch"]):
-            for b in range(n):
-                yield X[b * bs:(b + 1) * bs], Y[b * bs:(b + 1) * bs]
+    def batches(self, feed):
+        return feed.batches()
 
     def num_updates(self) -> int:
         return int(sum(self.commits_all))
@@ -118,7 +166,7 @@ class _Worker:
             self._hist_n = 0
         return self.history
 
-    def run(self, X, Y):
+    def run(self, feed):
         raise NotImplementedError
 
     # ---------------------------------------------------------------- fault tolerance
@@ -160,12 +208,12 @@ class _CommitWorker(_Worker):
 
     rule = "adag"
 
-    def run(self, X, Y):
+    def run(self, feed):
         a = self.arena
         it0, rnd = self._resume()
         center = a.master.detach().clone()
         it = 0
-        for xb, yb in self.batches(X, Y):
+        for xb, yb in self.batches(feed):
             it += 1
             if it <= it0:  # resumed: these batches were consumed before the checkpoint
                 continue
@@ -237,7 +285,7 @@ class _AsyncPSWorker(_Worker):
     def num_updates(self):
         return self._n
 
-    def run(self, X, Y):
+    def run(self, feed):
         from .parallel.ps import ParameterServerClient
 
         a, algo, k = self.arena, self.cfg["algorithm"], self.k
@@ -253,7 +301,7 @@ class _AsyncPSWorker(_Worker):
 
             anchor = pull()
             it = 0
-            for xb, yb in self.batches(X, Y):
+            for xb, yb in self.batches(feed):
                 self.train_batch(xb, yb)
                 it += 1
                 if it % k:
@@ -299,8 +347,8 @@ class _AveragingWorker(_Worker):
     def num_updates(self):
         return 1
 
-    def run(self, X, Y):
-        for xb, yb in self.batches(X, Y):
+    def run(self, feed):
+        for xb, yb in self.batches(feed):
             self.train_batch(xb, yb)
         W = self.arena.master.detach()
         with torch.no_grad():
@@ -315,8 +363,8 @@ class _EnsembleWorker(_Worker):
     def num_updates(self):
         return 0
 
-    def run(self, X, Y):
-        for xb, yb in self.batches(X, Y):
+    def run(self, feed):
+        for xb, yb in self.batches(feed):
             self.train_batch(xb, yb)
         return self.arena.master.detach().clone()
 
@@ -326,21 +374,35 @@ class _SyncDPWorker(_Worker):
 
     def __init__(self, cfg, model, pg, sizes):
         super().__init__(cfg, model, pg, sizes)
+        # every replica must take the same number of synchronous steps: shards of unequal size
+        # (repartition splits rows to within one) train min(steps) and drop the rest
         self.steps = min(self.steps_all) if self.steps_all else 0
+        dropped = max(self.steps_all) - self.steps if self.steps_all else 0
+        if dropped and pg.rank == 0:
+            warnings.warn(f"SynchronousDataParallel: shards of {sizes} rows give {self.steps_all} steps; every "
+                          f"worker trains {self.steps} (up to {dropped} trailing batches dropped on the larger "
+                          "shards)", RuntimeWarning, stacklevel=2)
+        self.timed_s, self.timed_steps = None, 0
 
     def num_updates(self):
         return self.steps
 
-    def run(self, X, Y):
+    def run(self, feed):
         from .parallel.ddp import DataParallel
 
         ddp = DataParallel(self.model, self.pg, bucket_mb=self.cfg.get("bucket_mb"))
         it0, _ = self._resume()
         ddp.broadcast_parameters()
+        # optional measurement window (bench.py --via-dataframe): steps after `timing_warmup`,
+        # bracketed by a barrier + device synchronize on both sides
+        tw = self.cfg.get("timing_warmup")
+        t0 = None
         it = 0
-        for xb, yb in self.batches(X, Y):
+        for xb, yb in self.batches(feed):
             if it >= self.steps:
                 break
+            if tw is not None and it == int(tw):
+                t0 = self._sync_clock()
             it += 1
             if it <= it0:
                 continue
@@ -348,7 +410,15 @@ class _SyncDPWorker(_Worker):
             xb, yb = self.model.to_input(xb), self.model.to_target(yb)
             self._record(ddp.train_step(xb, yb).float())
             self._maybe_checkpoint(it, it)  # every `checkpoint_every` steps (with optimizer state)
+        if t0 is not None:
+            self.timed_s, self.timed_steps = self._sync_clock() - t0, it - int(tw)
         return self.arena.master.detach().clone()
+
+    def _sync_clock(self):
+        if self.model.device.type == "cuda":
+            torch.cuda.synchronize(self.model.device)
+        self.pg.barrier()
+        return time.perf_counter()
 
 
 _WORKERS = {"adag": _AdagWorker, "dynsgd": _DynSGDWorker, "downpour": _DownpourWorker, "easgd": _EASGDWorker,
@@ -369,7 +439,7 @@ def _train_worker(rank, world, pg, cfg, blob, X, Y, sizes):
         model.arena.set_flat(torch.from_numpy(blob["flat"]))
     if blob.get("states"):
         set_states(model, blob["states"])
-    Xd, Yd = _to_device(X, model), _to_device(Y, model)
+    feed = _ShardFeed(X, Y, model, cfg)
     cls = _WORKERS[cfg["algorithm"]]
     if cfg.get("mode") == "async" and issubclass(cls, _CommitWorker):
         cls = _AsyncPSWorker
@@ -380,14 +450,16 @@ def _train_worker(rank, world, pg, cfg, blob, X, Y, sizes):
 
         w.watchdog = Watchdog(float(cfg["watchdog_s"])).start()
     try:
-        final = w.run(Xd, Yd)
+        final = w.run(feed)
     finally:
         if w.watchdog is not None:
             w.watchdog.stop()
     if model.device.type == "cuda":
         torch.cuda.synchronize(model.device)
     out = {"rank": rank, "history": w.losses(), "num_updates": w.num_updates(), "time": time.time() - t0,
-           "commit_s": w.commit_s, "graph": bool(w._step is not None and w._step.captured)}
+           "commit_s": w.commit_s, "graph": bool(w._step is not None and w._step.captured),
+           "ingest": "stream" if feed.streaming else "resident", "timed_s": getattr(w, "timed_s", None),
+           "timed_steps": getattr(w, "timed_steps", 0)}
     if rank == 0 or cfg["algorithm"] == "ensemble":
         out["flat"] = final.cpu().numpy().copy()
         out["states"] = get_states(model)
@@ -493,7 +565,8 @@ class _ShardedTrainer(Trainer):
             df = _shuffle(df, self.seed)
         if df.rdd_partitions_count() != self.num_workers:
             df = df.repartition(self.num_workers)
-        parts = df.partition_arrays([self.features_column, self.label_column], np.float32)
+        # column dtypes are kept (uint8 pixels stay uint8; float64 narrows to float32)
+        parts = df.partition_arrays([self.features_column, self.label_column], None)
         return [p[0] for p in parts], [p[1] for p in parts]
 
     def train(self, dataframe, shuffle=False):

@@ -7,7 +7,10 @@ the Azure-Blob CSV (no network, no storage keys), ``local[N]`` master instead of
 AZTK/YARN, and one worker process per MI355X (or CPU executor) instead of Spark tasks
 talking to a socket parameter server.
 
-    python examples/ddl_nyiso.py [--workers 4] [--epochs 20] [--device auto|cpu]
+    python examples/ddl_nyiso.py [--workers 4] [--epochs 20] [--device auto|cpu] [--hours 11712]
+
+``main()`` returns the per-model results (updates, training time, MAPE, the prediction
+frame) so the workflow is testable end to end (tests/test_workflows.py).
 """
 from __future__ import annotations
 
@@ -90,21 +93,24 @@ def run(model, optimizer, df_train, df_test, orig_min, orig_max, num_workers, ep
     pred = df_pred.select("prediction2").rdd.map(lambda x: list(x[0])).collect()
     mape = get_MAPE(actual, pred)
     print("MAPE", mape)
+    trainer.prediction_frame = df_pred
     return trainer, mape
 
 
-def main():
+def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--workers", type=int, default=2)
     ap.add_argument("--epochs", type=int, default=20)
     ap.add_argument("--device", default="auto")
     ap.add_argument("--csv", default="/tmp/ddl_nyiso_synthetic.csv")
+    ap.add_argument("--hours", type=int, default=11712, help="length of the synthetic hourly series")
+    ap.add_argument("--models", default="GRU,LSTM")
     ap.add_argument("--workers-per-gpu", type=int, default=None,
                     help="co-locate replicas on one MI355X (the reference's 4 workers on a 1-GPU box)")
-    a = ap.parse_args()
+    a = ap.parse_args(argv)
     if a.workers_per_gpu:
         os.environ["DDL_WORKERS_PER_GPU"] = str(a.workers_per_gpu)
-    nyiso_like().to_csv(a.csv, index=False)
+    nyiso_like(hours=a.hours).to_csv(a.csv, index=False)
     conf = SparkConf().set("spark.app.name", "ddl_nyiso").set("spark.master", f"local[{a.workers}]")
     conf.set("spark.executor.cores", 1).set("spark.executor.instances", a.workers)
     # executors come up (torch import, HIP init, process group) while the driver runs the ETL
@@ -114,13 +120,17 @@ def main():
     SparkSession.builder.getOrCreate().sparkContext.setLogLevel("ERROR")
     df_train, df_test, omin, omax = build_frames(sqlc, a.csv, a.workers)
     sc.awaitExecutors()  # session start-up ends here (the reference's executors were up before training)
-    res = {}
+    res, extra = {}, {}
     for name, model, opt in (("GRU", gru_regressor(N_UNITS), "adagrad"), ("LSTM", lstm_regressor(N_UNITS), "adam")):
+        if name not in a.models.split(","):
+            continue
         tr, mape = run(model, opt, df_train, df_test, omin, omax, a.workers, a.epochs, a.device)
         res[name] = {"updates": tr.parameter_server.num_updates, "time_s": tr.get_training_time(), "mape": mape,
                      "worker_s": [round(t, 3) for t in tr.worker_times],
                      "commit_s": [round(t, 3) for t in tr.worker_commit_times]}
+        extra[name] = tr
     print(json.dumps({"workflow": "ddl_nyiso", "workers": a.workers, "epochs": a.epochs, "results": res}))
+    return {"results": res, "trainers": extra, "train_rows": [s.stop - s.start for s in df_train.partition_slices()]}
 
 
 if __name__ == "__main__":

@@ -1,0 +1,160 @@
+"""End-to-end workflows on CPU executors: the NYISO GRU/LSTM chain of the reference
+(lag/lead -> VectorAssembler -> Reshape(25,1) -> ADAG -> inverse MinMax -> MAPE,
+``ddl_nyiso_aztk.py:109-274``), BASELINE.json config #1 (LeNet-5 on MNIST-shape data through
+ADAG on ``local[2]`` CPU executors), the HDInsight notebook's session flow
+(``ddl_nyiso_hdi.ipynb`` cell 2: yarn-client conf, ``sc.stop()``, re-created context), the
+partition-parallel ``ModelPredictor`` and the dtype-preserving DataFrame -> worker shards."""
+import math
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "examples"))
+
+
+@pytest.fixture(autouse=True)
+def _fresh_session():
+    from distributeddeeplearningspark_amd.context import SparkContext, SparkSession
+
+    yield
+    if SparkSession._active is not None:
+        SparkSession._active.stop()
+    if SparkContext._active is not None:
+        SparkContext._active.stop()
+
+
+def _update_law(rows, batch, epochs, window):
+    return sum((epochs * (r // batch)) // window for r in rows)
+
+
+def test_ddl_nyiso_workflow_end_to_end(tmp_path, capsys):
+    import ddl_nyiso
+
+    out = ddl_nyiso.main(["--workers", "2", "--epochs", "2", "--device", "cpu", "--hours", "1500",
+                          "--csv", str(tmp_path / "nyiso.csv")])
+    rows = out["train_rows"]
+    assert len(rows) == 2 and sum(rows) == 1500 - 25 - 120  # 24 lags + 1 lead dropped, 120 test rows
+    for name in ("GRU", "LSTM"):
+        r = out["results"][name]
+        assert r["updates"] == _update_law(rows, 32, 2, 5), (name, r["updates"], rows)
+        assert math.isfinite(r["mape"]) and 0.0 < r["mape"] < 100.0
+        pf = out["trainers"][name].prediction_frame
+        assert {"prediction", "prediction2", "labels2"} <= set(pf.columns)
+        pred = np.array([row["prediction2"].toArray()[0] for row in pf.collect()])
+        assert pred.shape == (24,) and np.isfinite(pred).all()
+    text = capsys.readouterr().out
+    assert "Number of parameter updates" in text and "Total params: 50,049" in text  # GRU(128) summary
+
+
+def test_lenet5_adag_local2_cpu_executors():
+    """BASELINE.json config #1: LeNet-5 on MNIST-shape synthetic data, Spark local[2] CPU executors."""
+    from distributeddeeplearningspark_amd.context import SparkConf, SparkContext, SQLContext
+    from distributeddeeplearningspark_amd.data.synthetic import mnist_like
+    from distributeddeeplearningspark_amd.models.zoo import lenet5
+    from distributeddeeplearningspark_amd.sql.dataframe import from_columns
+    from distributeddeeplearningspark_amd.trainers import ADAG
+
+    sc = SparkContext(conf=SparkConf().setMaster("local[2]").setAppName("lenet5"))
+    SQLContext(sc)
+    pdf = mnist_like(512, seed=1)
+    y = pdf["label"].to_numpy()
+    x = pdf.drop(columns=["label"]).to_numpy().reshape(-1, 28, 28, 1).astype(np.float32) / 255.0
+    onehot = np.eye(10, dtype=np.float64)[y]
+    df = from_columns({"features": x, "label": onehot}, num_partitions=2)
+    model = lenet5()
+    model.build_model()
+    n_params = model.count_params()
+    trainer = ADAG(keras_model=model, worker_optimizer="adam", loss="categorical_crossentropy",
+                   num_workers=sc.num_workers(), batch_size=32, communication_window=4, num_epoch=3, device="cpu")
+    trained = trainer.train(df)
+    assert trained.count_params() == n_params
+    assert trainer.parameter_server.num_updates == _update_law([256, 256], 32, 3, 4)
+    hist = trainer.get_averaged_history()
+    assert np.mean(hist[-4:]) < np.mean(hist[:4])
+    acc = (trained.predict(x).argmax(1) == y).mean()
+    assert acc > 0.3
+
+
+def test_hdinsight_session_flow(tmp_path):
+    """Notebook flow: a pre-existing shell context is stopped and re-created from a yarn-client
+    conf; SQLContext / SparkSession / storage attach and num_workers follow the new conf."""
+    import distributeddeeplearningspark_amd as ddl
+    from distributeddeeplearningspark_amd.context import SparkConf, SparkContext, SparkSession, SQLContext
+    from distributeddeeplearningspark_amd.utils import get_os_username
+    from distributeddeeplearningspark_amd.utils.storage import attach_storage_container
+
+    sc = SparkContext.getOrCreate()  # what the pyspark kernel provides before the notebook runs
+    num_processes, num_executors = 2, 2
+    conf = SparkConf()
+    conf.set("spark.app.name", "Distributed Keras NYISO")
+    conf.set("spark.master", "yarn-client")
+    conf.set("spark.executor.cores", num_processes)
+    conf.set("spark.executor.instances", num_executors)
+    conf.set("spark.executor.memory", "2g")
+    conf.set("spark.locality.wait", "0")
+    conf.set("spark.serializer", "org.apache.spark.serializer.KryoSerializer")
+    conf.set("spark.local.dir", "/tmp/" + get_os_username() + "/dist-keras")
+    sc.stop()
+    assert sc._stopped and SparkContext._active is None
+    sc = SparkContext(conf=conf)
+    sqlc = SQLContext(sc)
+    spark = SparkSession.builder.getOrCreate()
+    assert spark.sparkContext is sc and sc.master == "yarn-client"
+    assert sc.num_workers() == num_executors * num_processes
+    attach_storage_container(spark, "publicdat", key="not-kept", root=str(tmp_path))
+    from distributeddeeplearningspark_amd.utils.storage import resolve
+
+    assert resolve("wasb://nyiso@publicdat.blob.core.windows.net/x.csv").startswith(str(tmp_path))
+    df = sqlc.createDataFrame([(1, 2.0), (2, 3.0)], ["a", "b"])
+    assert df.count() == 2
+    _ = ddl
+
+
+def test_partition_parallel_predictor_matches_local():
+    from distributeddeeplearningspark_amd.models import Dense, Sequential
+    from distributeddeeplearningspark_amd.predictors import ModelPredictor
+    from distributeddeeplearningspark_amd.sql.dataframe import from_columns
+
+    rng = np.random.default_rng(0)
+    x = rng.normal(size=(301, 7))
+    df = from_columns({"features": x, "id": np.arange(301)}, num_partitions=3)
+    m = Sequential([Dense(16, input_shape=(7,), activation="tanh"), Dense(3, activation="softmax")])
+    m.compile("adam", "categorical_crossentropy")
+    m.place("cpu", seed=3)
+    local = ModelPredictor(m, device="cpu", num_workers=1).predict(df)
+    par = ModelPredictor(m, device="cpu", num_workers=2).predict(df)
+    a = np.stack([r["prediction"].toArray() for r in local.collect()])
+    b = np.stack([r["prediction"].toArray() for r in par.collect()])
+    assert a.shape == (301, 3)
+    np.testing.assert_array_equal(a, b)
+    assert [r["id"] for r in par.collect()] == list(range(301))
+    assert par.rdd_partitions_count() == 3
+
+
+def test_partition_arrays_keep_uint8_pixels():
+    from distributeddeeplearningspark_amd.sql.dataframe import from_columns
+
+    imgs = np.random.default_rng(1).integers(0, 256, (10, 8, 8, 3), dtype=np.uint8)
+    df = from_columns({"image": imgs, "label": np.arange(10), "w": np.linspace(0, 1, 10)}, num_partitions=2)
+    parts = df.partition_arrays(["image", "label", "w"], None)
+    assert [p[0].dtype for p in parts] == [np.uint8, np.uint8]
+    assert parts[0][1].dtype == np.int64 and parts[0][2].dtype == np.float32
+    np.testing.assert_array_equal(np.concatenate([p[0] for p in parts]), imgs)
+    assert parts[0][0].base is not None  # zero-copy slices of one array
+
+
+def test_uint8_images_normalised_by_to_input():
+    import torch
+
+    from distributeddeeplearningspark_amd.models import ResNet50
+
+    m = ResNet50(input_shape=(32, 32, 3), num_classes=10)
+    x = np.full((2, 32, 32, 3), 200, dtype=np.uint8)
+    m.place("cpu")
+    t = m.to_input(x)
+    assert t.dtype == torch.float32
+    torch.testing.assert_close(t[0, 0, 0], torch.tensor([(200 - 123.675) / 58.395, (200 - 116.28) / 57.12,
+                                                         (200 - 103.53) / 57.375]))
