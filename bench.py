@@ -32,8 +32,12 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=None)
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=0)
-    ap.add_argument("--model", default="resnet50", choices=["resnet50", "vgg16", "bert"],
-                    help="resnet50 = the BASELINE headline; vgg16 / bert = the other BASELINE.json DP configs")
+    ap.add_argument("--model", default="resnet50", choices=["resnet50", "vgg16", "bert", "nyiso_gru", "nyiso_lstm"],
+                    help="resnet50 = the BASELINE headline; vgg16 / bert = the other BASELINE.json DP configs; "
+                         "nyiso_gru / nyiso_lstm = the reference's own published workload (ADAG, 4 workers, "
+                         "batch 32, window 5, 20 epochs): training time in seconds, lower is better")
+    ap.add_argument("--workers", type=int, default=4, help="nyiso_*: dist-keras workers (reference: 2 x 2 = 4)")
+    ap.add_argument("--epochs", type=int, default=20, help="nyiso_*: epochs (reference: 20)")
     ap.add_argument("--reduce-dtype", default=None, choices=["fp32", "bf16"],
                     help="gradient all-reduce wire dtype (default DDL_REDUCE_DTYPE or fp32)")
     ap.add_argument("--graph", type=int, default=None,
@@ -53,6 +57,8 @@ def main():
         args.image = 32
     if args.batch is None:
         args.batch = 32 if args.model == "bert" else 256
+    if args.model.startswith("nyiso_"):
+        return bench_nyiso(args)  # driver + executor processes, no torchrun process group
 
     from distributeddeeplearningspark_amd.parallel import comm
     from distributeddeeplearningspark_amd.data.ingest import SyntheticImageStream
@@ -169,6 +175,46 @@ def comm_stats(ddp, pg):
     return {"comm_ms": round(full, 3), "exposed_comm_ms": round(exposed, 3), "bucket_mb": ddp.bucket_mb,
             "buckets": len(ddp.buckets), "reduce_dtype": "bf16" if ddp._red is not None else "fp32",
             "grad_mb": round(ddp.grad_bytes / 2**20, 1), "backend": pg.backend, "forced_pg": pg.forced}
+
+
+# the reference's published NYISO numbers (ddl_nyiso_hdi.ipynb:608-609,730,817-818,934)
+_NYISO_REF = {"GRU": {"time_s": 88.4753541946, "updates": 1425, "mape": 2.8088},
+              "LSTM": {"time_s": 99.2543179989, "updates": 1425, "mape": 3.5871}}
+
+
+def bench_nyiso(args):
+    """The reference's own workload end to end (examples/ddl_nyiso.py): synthetic NYISO-shaped
+    CSV -> Spark-style ETL -> ADAG(GRU|LSTM, 4 workers, batch 32, window 5, 20 epochs) ->
+    ModelPredictor -> inverse MinMax -> MAPE.  ``value`` is ``trainer.get_training_time()``
+    (the reference's metric); workers share the GPUs present (DDL_WORKERS_PER_GPU)."""
+    import contextlib
+    import math
+
+    from distributeddeeplearningspark_amd.parallel.launcher import _gpu_count
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "examples"))
+    import ddl_nyiso
+
+    cell = args.model.split("_")[1].upper()
+    gpus = _gpu_count()
+    wpg = max(1, math.ceil(args.workers / max(gpus, 1)))
+    argv = ["--workers", str(args.workers), "--epochs", str(args.epochs), "--models", cell,
+            "--device", "auto" if gpus else "cpu", "--workers-per-gpu", str(wpg)]
+    with contextlib.redirect_stdout(sys.stderr):  # the workflow's own report goes to stderr
+        out = ddl_nyiso.main(argv)
+    r = out["results"][cell]
+    ref = _NYISO_REF[cell]
+    print(json.dumps({
+        "metric": f"training time (s) NYISO {cell}(128)+Dense(1) ADAG {args.workers} workers {args.epochs} epochs",
+        "value": round(r["time_s"], 4), "unit": "s", "n_gpus": gpus, "steps": int(r["updates"]), "warmup": 0,
+        "ms_per_step": None, "higher_is_better": False, "scaling": "strong",
+        "vs_baseline": round(r["time_s"] / ref["time_s"], 5), "dtype": "fp32",
+        "data": "synthetic NYISO-shaped hourly load (11,712 hours)",
+        "config": {"model": f"nyiso_{cell.lower()}", "algorithm": "ADAG", "workers": args.workers, "batch": 32,
+                   "communication_window": 5, "epochs": args.epochs, "units": 128, "input": [25, 1],
+                   "workers_per_gpu": wpg, "num_updates": r["updates"], "mape_pct": round(r["mape"], 4),
+                   "worker_s": r["worker_s"], "reference": ref},
+    }), flush=True)
 
 
 def bench_via_dataframe(args, pg):

@@ -54,14 +54,33 @@ from .utils import deserialize_keras_model, get_states, serialize_keras_model, s
 # =============================================================================================
 #                                    worker side
 # =============================================================================================
+_INGEST_STREAMS: dict = {}
+
+
+def ingest_stream(device):
+    """ONE side stream per device for every host->HBM shard copy of this process: each extra
+    HIP stream can claim a hardware queue, and co-located workers (8 processes on one MI355X)
+    oversubscribe the queues if every shard brings its own stream."""
+    key = str(device)
+    if key not in _INGEST_STREAMS:
+        _INGEST_STREAMS[key] = torch.cuda.Stream(device)
+    return _INGEST_STREAMS[key]
+
+
+_SMALL_SHARD = 64 << 20  # below this a direct copy costs less than the stream/event machinery
+
+
 def _resident(a: np.ndarray, device):
-    """Copy a host shard into HBM once, in its own dtype, from pinned memory on a side stream:
-    the compute stream waits on an event (the host does not block on the transfer)."""
+    """Copy a host shard into HBM once, in its own dtype.  Large shards go from pinned memory on
+    the ingest side stream (the compute stream waits on an event, the host does not block on
+    the transfer); small ones (< 64 MB) are copied directly."""
     t = torch.from_numpy(np.ascontiguousarray(a))
     if device.type != "cuda":
         return t
+    if t.numel() * t.element_size() < _SMALL_SHARD:
+        return t.to(device)
     pinned = t.pin_memory()
-    side = torch.cuda.Stream(device)
+    side = ingest_stream(device)
     with torch.cuda.stream(side):
         d = pinned.to(device, non_blocking=True)
         ev = torch.cuda.Event()
@@ -100,6 +119,8 @@ class _ShardFeed:
             self.loader = ShardLoader(X, Y, self.batch, device=dev, shuffle=False, drop_last=True)
         else:
             self.X, self.Y = _resident(X, dev), _resident(Y, dev)
+            if self.X.is_floating_point() and self.X.dtype != model.compute_dtype:
+                self.X = self.X.to(model.compute_dtype)  # once, not per batch (labels keep fp32)
 
     def batches(self):
         bs, nb = self.batch, self.n // self.batch

@@ -9,6 +9,10 @@ mount of the ``wasbs://`` container (no network, no account key), ``local[N]`` r
 AZTK master, and each worker is one process per MI355X (or CPU executor).
 
     python examples/ddl_mnist.py [--executors 4] [--processes 2] [--epochs 1] [--device auto|cpu]
+
+Attribution: the pipeline (transformer sequence, trainer and evaluation calls) follows the
+reference script ``ddl_mnist_aztk.py`` (chenhuims/DistributedDeepLearningSpark, GPLv3), whose
+public dist-keras/Spark API this framework reproduces.
 """
 from __future__ import annotations
 
@@ -47,14 +51,12 @@ def write_synthetic_csvs(root: str, n_train: int, n_test: int):
 
 
 def evaluate_accuracy(model, test_set, features="matrix"):
-    """The reference's helper (``ddl_mnist_aztk.py:202-210``)."""
-    evaluator = AccuracyEvaluator(prediction_col="prediction_index", label_col="label")
-    predictor = ModelPredictor(keras_model=model, features_col=features)
-    transformer = LabelIndexTransformer(output_dim=10)
-    test_set = test_set.select(features, "label")
-    test_set = predictor.predict(test_set)
-    test_set = transformer.transform(test_set)
-    return evaluator.evaluate(test_set)
+    """Accuracy of ``model`` on ``test_set``: predict -> argmax class index -> AccuracyEvaluator,
+    the same three steps as the reference's helper (``ddl_mnist_aztk.py:202-210``; the
+    reference is GPLv3, this workflow mirrors its API calls, not its code)."""
+    scored = ModelPredictor(keras_model=model, features_col=features).predict(test_set.select(features, "label"))
+    indexed = LabelIndexTransformer(output_dim=10).transform(scored)
+    return AccuracyEvaluator(prediction_col="prediction_index", label_col="label").evaluate(indexed)
 
 
 def main():
@@ -149,6 +151,9 @@ def main():
     print("Training time: " + str(trainer.get_training_time()))
     print("Accuracy: " + str(evaluate_accuracy(trained_model, dataset_test)))
     print("Number of parameter server updates: " + str(trainer.parameter_server.num_updates))
+    rs = getattr(trainer, "_results", [])
+    print("Workers:", [{k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()
+                        if k in ("rank", "time", "commit_s", "graph", "ingest")} for r in rs])
     return trainer, trained_model
 
 
