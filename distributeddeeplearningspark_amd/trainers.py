@@ -198,27 +198,38 @@ class _Worker:
         if getattr(self, "watchdog", None) is not None:
             self.watchdog.beat(it)
 
+    # worker algorithms whose ranks hold state that differs between workers (their own optimizer
+    # slots, and for the elastic family their own weights plus the center): checkpointed per rank
+    per_rank_state = False
+
     def _resume(self):
-        """(iterations already done, commit rounds already done) from the newest checkpoint."""
+        """(iterations already done, commit rounds already done) from the newest checkpoint;
+        per-rank algorithms also get back their own worker state (``self.resumed_extra``)."""
+        self.resumed_extra = None
         d = self.cfg.get("checkpoint_dir")
         if not d:
             return 0, 0
-        from .utils.checkpoint import latest_checkpoint, load_checkpoint
+        from .utils.checkpoint import latest_checkpoint, load_checkpoint, load_rank_state
 
         path = latest_checkpoint(d)
         if path is None:
             return 0, 0
         _, meta = load_checkpoint(path, self.model)
+        if self.per_rank_state:
+            self.resumed_extra = load_rank_state(path, self.model, self.pg.rank)
         ex = meta.get("extra", {})
         self.resumed_from = path
         return int(ex.get("it", 0)), int(ex.get("round", 0))
 
-    def _maybe_checkpoint(self, rnd, it):
+    def _maybe_checkpoint(self, rnd, it, center=None):
         d, every = self.cfg.get("checkpoint_dir"), int(self.cfg.get("checkpoint_every", 0) or 0)
         if not d or every <= 0 or rnd % every:
             return
-        from .utils.checkpoint import save_checkpoint
+        from .utils.checkpoint import save_checkpoint, save_rank_state
 
+        if self.per_rank_state:
+            save_rank_state(d, self.model, it, self.pg.rank, extra=None if center is None else {"center": center})
+            self.pg.barrier()  # every rank file exists before rank 0 publishes `latest`
         save_checkpoint(d, self.model, step=it, extra={"round": rnd, "it": it, "algorithm": self.cfg["algorithm"]},
                         rank=self.pg.rank)
         self.pg.barrier()  # nobody runs ahead of a checkpoint it may have to resume from
@@ -228,11 +239,13 @@ class _CommitWorker(_Worker):
     """Periodic commit rounds (ADAG / DynSGD / DOWNPOUR / EASGD family)."""
 
     rule = "adag"
+    per_rank_state = True
 
     def run(self, feed):
         a = self.arena
         it0, rnd = self._resume()
-        center = a.master.detach().clone()
+        ex = self.resumed_extra or {}
+        center = ex["center"].clone() if "center" in ex else a.master.detach().clone()
         it = 0
         for xb, yb in self.batches(feed):
             it += 1
@@ -243,7 +256,7 @@ class _CommitWorker(_Worker):
             if it % self.k == 0 and rnd < self.rounds:
                 self.commit(center, rnd)
                 rnd += 1
-                self._maybe_checkpoint(rnd, it)
+                self._maybe_checkpoint(rnd, it, center)
         while rnd < self.rounds:  # my shard is exhausted: join the remaining rounds with a zero delta
             self.commit(center, rnd)
             rnd += 1

@@ -9,6 +9,11 @@ dist-keras ``utils.serialize_keras_model`` used by every trainer) is 
     <dir>/step_<n>/state.safetensors fp32 master arena, optimizer slots, layer states (BN stats)
     <dir>/step_<n>/meta.json         step, optimizer config + iterations, RNG, user extras
     <dir>/latest                     name of the newest complete checkpoint
+    <dir>/ranks/step_<n>/rank_<r>.safetensors
+                                     per-worker state of the dist-keras worker algorithms
+                                     (ADAG / DynSGD / DOWNPOUR / EASGD): that worker's weights,
+                                     optimizer slots, layer states and the center variable it
+                                     holds — worker-local state that differs between ranks
 
 Writes go to a temporary directory renamed into place (a crash never leaves a torn
 checkpoint); ``keep`` bounds how many are retained.  Loading never unpickles: npz with
@@ -79,6 +84,65 @@ def _prune(directory, keep):
     ck = sorted(d for d in os.listdir(directory) if d.startswith("step_"))
     for d in ck[:-keep] if keep > 0 else []:
         shutil.rmtree(os.path.join(directory, d), ignore_errors=True)
+        shutil.rmtree(os.path.join(directory, "ranks", d), ignore_errors=True)
+
+
+def _rank_file(directory: str, step: int, rank: int) -> str:
+    return os.path.join(directory, "ranks", f"step_{int(step):09d}", f"rank_{int(rank):05d}.safetensors")
+
+
+def save_rank_state(directory: str, model, step: int, rank: int, extra: dict | None = None) -> str:
+    """Write THIS worker's state for checkpoint ``step``: its master weights, optimizer slots,
+    layer states and any ``extra`` tensors (e.g. the center variable).  Call on every rank
+    BEFORE rank 0's :func:`save_checkpoint` of the same step (with a barrier in between), so
+    ``latest`` never names a step whose rank files are missing."""
+    path = _rank_file(directory, step, rank)
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    tensors = {"arena.master": model.arena.master.detach().float().cpu().contiguous()}
+    for i, st in enumerate(_states_in_order(model)):
+        tensors[f"layer_state.{i:04d}"] = st.detach().float().cpu().contiguous()
+    opt = model.optimizer
+    meta = {"rank": str(int(rank)), "step": str(int(step))}
+    if opt is not None:
+        sd = opt.state_dict()
+        meta["iterations"] = str(int(sd.pop("iterations", 0)))
+        for k, v in sd.items():
+            tensors[f"optim.{k}"] = v.float().cpu().contiguous()
+    for k, v in (extra or {}).items():
+        tensors[f"extra.{k}"] = v.detach().float().cpu().contiguous()
+    tmp = path + ".tmp"
+    save_file(tensors, tmp, metadata=meta)
+    os.replace(tmp, path)
+    return path
+
+
+def load_rank_state(checkpoint_path: str, model, rank: int) -> dict | None:
+    """Restore this worker's state saved next to ``checkpoint_path`` (``<dir>/step_<n>``).
+    Returns the ``extra`` tensors (on the model's device), or None if no rank file exists."""
+    directory, name = os.path.split(os.path.normpath(checkpoint_path))
+    step = int(name.split("_")[1])
+    path = _rank_file(directory, step, rank)
+    if not os.path.exists(path):
+        return None
+    from safetensors import safe_open
+
+    with safe_open(path, framework="pt") as f:
+        meta = f.metadata() or {}
+    t = load_file(path)
+    model.arena.set_flat(t["arena.master"])
+    for i, st in enumerate(_states_in_order(model)):
+        key = f"layer_state.{i:04d}"
+        if key in t:
+            st.copy_(t[key].to(st.device, st.dtype))
+    opt = model.optimizer
+    if opt is not None:
+        if opt.arena is not model.arena:
+            opt.bind(model.arena)
+        sd = {k[len("optim."):]: v for k, v in t.items() if k.startswith("optim.")}
+        sd["iterations"] = int(meta.get("iterations", 0))
+        opt.load_state_dict(sd)
+    dev = model.arena.master.device
+    return {k[len("extra."):]: v.to(dev) for k, v in t.items() if k.startswith("extra.")}
 
 
 def latest_checkpoint(directory: str) -> str | None:

@@ -199,3 +199,33 @@ def test_spark_context_prestarts_executors():
     finally:
         sc.stop()
     assert not E._POOLS
+
+
+def test_elastic_resume_restores_each_workers_state(spark, tmp_path, monkeypatch):
+    """EASGD workers hold state that differs per rank (own weights, own Adam slots, the center):
+    a run killed on rank 1 and resumed from the per-rank checkpoint files ends bit-identical to
+    an uninterrupted run (before per-rank files every rank resumed from rank 0's state)."""
+    from distributeddeeplearningspark_amd.trainers import EASGD
+    from distributeddeeplearningspark_amd.utils.checkpoint import latest_checkpoint
+
+    df = _mnist_df(spark).repartition(2)
+
+    def train(ckdir, fault):
+        if fault:
+            monkeypatch.setenv("DDL_FAULT_RANK", "1")
+            monkeypatch.setenv("DDL_FAULT_STEP", "7")
+        else:
+            monkeypatch.delenv("DDL_FAULT_RANK", raising=False)
+            monkeypatch.delenv("DDL_FAULT_STEP", raising=False)
+        tr = EASGD(keras_model=mnist_cnn(), worker_optimizer="adam", loss="categorical_crossentropy", num_workers=2,
+                   batch_size=16, communication_window=2, num_epoch=1, features_col="x", label_col="y",
+                   device="cpu", checkpoint_dir=str(ckdir), checkpoint_every=1, max_restarts=1, seed=3)
+        tr.train(df)
+        return tr.parameter_server.center.copy()
+
+    clean = train(tmp_path / "clean", False)
+    resumed = train(tmp_path / "faulty", True)
+    np.testing.assert_array_equal(resumed, clean)
+    last = latest_checkpoint(str(tmp_path / "faulty"))
+    ranks = os.listdir(os.path.join(str(tmp_path / "faulty"), "ranks", os.path.basename(last)))
+    assert sorted(ranks) == ["rank_00000.safetensors", "rank_00001.safetensors"]
