@@ -177,6 +177,11 @@ int avgpool2d_bwd(const void* dy, void* dx, int N, int H, int W, int C, int Ho, 
 int embedding_gather(const int64_t* ids, const void* table, void* out, long n, int D, long V, int* bad, int bf16,
                      hipStream_t s);
 int embedding_scatter(const int64_t* ids, const void* dy, float* gw, long n, int D, long V, int bf16, hipStream_t s);
+// conv data-gradient filter layouts: out[ci][t][co] = w[co][taps.t[t]][ci] (bf16, nt <= 64 taps)
+constexpr int kMaxFilterTaps = 64;
+struct FilterTaps { int16_t t[kMaxFilterTaps]; };
+int filter_taps_transpose(const void* w, void* out, int Co, int T, int Ci, const FilterTaps& taps, int nt,
+                          hipStream_t s);
 // y[C][R] = x[R][C] (fp32)
 int transpose_f32(const float* x, float* y, int R, int C, hipStream_t s);
 // db[n] += sum_m dy[m][n] (fp32, dense rows of N)

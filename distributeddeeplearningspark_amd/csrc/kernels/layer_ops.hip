@@ -163,6 +163,29 @@ __global__ __launch_bounds__(256) void embedding_scatter_kernel(const int64_t* _
   for (int d = lane; d < D; d += 64) atomicAdd(gw + id * D + d, ldf(dy, t * D + d));
 }
 
+// Conv data-gradient filters: out[ci][t][co] = w[co][taps[t]][ci] (bf16) — the flipped filter
+// of a stride-1 dgrad (taps reversed) and the K-contiguous per-class filters of a strided dgrad,
+// in ONE pass (replaces flip + permute-copy / index_select + permute-copy: 2-3 ATen launches per
+// conv per step).  32x32 (co, ci) tiles through LDS so both the read (ci) and the write (co) are
+// contiguous; blockIdx.z = output tap.
+__global__ __launch_bounds__(256) void filter_taps_transpose_kernel(const bf16_t* __restrict__ w,
+                                                                    bf16_t* __restrict__ out, int Co, int T,
+                                                                    int Ci, int nt, FilterTaps taps) {
+  __shared__ bf16_t tile[32][33];
+  const int t = blockIdx.z, src_t = taps.t[t];
+  const int co0 = blockIdx.y * 32, ci0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int i = ty; i < 32; i += 8) {
+    const int co = co0 + i, ci = ci0 + tx;
+    tile[i][tx] = (co < Co && ci < Ci) ? w[((long)co * T + src_t) * Ci + ci] : (bf16_t)0;
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    const int ci = ci0 + i, co = co0 + tx;
+    if (ci < Ci && co < Co) out[((long)ci * nt + t) * Co + co] = tile[tx][i];
+  }
+}
+
 // y[C][R] = x[R][C] (fp32) through a padded 32x32 LDS tile
 __global__ __launch_bounds__(256) void transpose_f32_kernel(const float* __restrict__ x, float* __restrict__ y, int R,
                                                             int C) {
@@ -258,6 +281,15 @@ int avgpool2d_bwd(const void* dy, void* dx, int N, int H, int W, int C, int Ho, 
   else
     hipLaunchKernelGGL(avgpool2d_bwd_kernel<float>, dim3(blocks_for(n)), dim3(256), 0, s, (const float*)dy,
                        (float*)dx, N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw);
+  return (int)hipGetLastError();
+}
+
+int filter_taps_transpose(const void* w, void* out, int Co, int T, int Ci, const FilterTaps& taps, int nt,
+                          hipStream_t s) {
+  if (nt <= 0 || nt > kMaxFilterTaps || Co <= 0 || Ci <= 0) return (int)hipErrorInvalidValue;
+  const dim3 grid((Ci + 31) / 32, (Co + 31) / 32, nt);
+  hipLaunchKernelGGL(filter_taps_transpose_kernel, grid, dim3(256), 0, s, (const bf16_t*)w, (bf16_t*)out, Co, T, Ci,
+                     nt, taps);
   return (int)hipGetLastError();
 }
 

@@ -163,6 +163,23 @@ void embedding_bwd_(const at::Tensor& ids, const at::Tensor& dy, const at::Tenso
                            (int)gw.size(1), gw.size(0), bf, cur_stream()));
 }
 
+// out [Ci][nt][Co] = w [Co][T][Ci] gathered at the given taps
+void filter_taps_transpose_(const at::Tensor& w, const at::Tensor& out, std::vector<int64_t> taps) {
+  CK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.dim() == 4,
+     "filter_taps_transpose: w [Co][KH][KW][Ci] contiguous bf16");
+  const int64_t Co = w.size(0), T = w.size(1) * w.size(2), Ci = w.size(3), nt = (int64_t)taps.size();
+  CK(nt >= 1 && nt <= kMaxFilterTaps, "filter_taps_transpose: 1..64 taps");
+  CK(out.is_cuda() && out.scalar_type() == at::kBFloat16 && out.is_contiguous() && out.numel() == Ci * nt * Co,
+     "filter_taps_transpose: out [Ci][nt][Co] contiguous bf16");
+  FilterTaps ft{};
+  for (int64_t i = 0; i < nt; ++i) {
+    CK(taps[i] >= 0 && taps[i] < T, "filter_taps_transpose: tap out of range");
+    ft.t[i] = (int16_t)taps[i];
+  }
+  at::DeviceGuard g(w.device());
+  HIP_OK(filter_taps_transpose(w.data_ptr(), out.data_ptr(), (int)Co, (int)T, (int)Ci, ft, (int)nt, cur_stream()));
+}
+
 }  // namespace
 
 void register_layer_ops(py::module& m) {
@@ -179,6 +196,7 @@ void register_layer_ops(py::module& m) {
         py::arg("K"), py::arg("alpha") = 1.0, py::arg("beta") = 0.0, py::arg("bias") = py::none(),
         py::arg("relu") = false);
   m.def("transpose_f32", &transpose_f32_, "y = x^T (fp32)");
+  m.def("filter_taps_transpose", &filter_taps_transpose_, "conv dgrad filter: out[ci][t][co] = w[co][taps[t]][ci]");
   m.def("embedding_fwd", &embedding_fwd_, "Keras Embedding gather (bf16/fp32 table)");
   m.def("embedding_bwd", &embedding_bwd_, "Keras Embedding gradient scatter-add into fp32");
   m.attr("ACT_CODES") = py::dict(py::arg("linear") = (int)ACT_C_LINEAR, py::arg("relu") = (int)ACT_C_RELU,

@@ -149,8 +149,23 @@ _WIDE_WGRAD = _os.environ.get("DDL_WGRAD_WIDE", "1") != "0"
 
 
 def flip_filter(w):
-    """[Co, KH, KW, Ci] -> [Ci, KH, KW, Co] with the taps reversed (the transposed conv's filter)."""
+    """[Co, KH, KW, Ci] -> [Ci, KH, KW, Co] with the taps reversed (the transposed conv's filter):
+    one HIP pass on the GPU (``filter_taps_transpose``), flip + permute on the CPU."""
+    Co, KH, KW, Ci = w.shape
+    if use_native(w) and w.dtype == torch.bfloat16:
+        out = torch.empty((Ci, KH, KW, Co), dtype=w.dtype, device=w.device)
+        C().filter_taps_transpose(w.contiguous(), out, list(range(KH * KW - 1, -1, -1)))
+        return out
     return w.flip(1, 2).permute(3, 1, 2, 0).contiguous()
+
+
+def class_filter(w, g: ConvGeometry, cl):
+    """K-contiguous filter of one strided data-gradient class: [Ci][taps of the class][Co]."""
+    if use_native(w) and w.dtype == torch.bfloat16:
+        out = torch.empty((g.Ci, len(cl["wt"]), g.Co), dtype=w.dtype, device=w.device)
+        C().filter_taps_transpose(w.contiguous(), out, list(cl["wt"]))
+        return out
+    return w.reshape(g.Co, g.T, g.Ci).index_select(1, _tap_index(cl, w.device)).permute(2, 1, 0).contiguous()
 
 
 def conv_dgrad_native(dy, w, g: ConvGeometry, resid=None):
@@ -180,7 +195,7 @@ def conv_dgrad_native(dy, w, g: ConvGeometry, resid=None):
         if g.implicit_dgrad and _KC_DGRAD:
             # the class's taps of the filter, transposed once to K-contiguous [Ci][taps][Co]: the GEMM
             # then reads B with ds_read_b128 like a forward conv (faster than the RC_TAPS layout)
-            wkc = w.reshape(g.Co, g.T, g.Ci).index_select(1, _tap_index(cl, dev)).permute(2, 1, 0).contiguous()
+            wkc = class_filter(w, g, cl)
             geom = dict(n=g.N, hi=g.Ho, wi=g.Wo, c=g.Co, ho=cl["Hc"], wo=cl["Wc"], sh=1, sw=1, tap_c=g.Co,
                         dh=cl["dh"], dw=cl["dw"])
             G.gemm(dy, wkc, dx, Mc, g.Ci, nt * g.Co, G.KC_GATHER, G.KC, 0, nt * g.Co, g.Ci, G.EPI_BF16,
