@@ -69,7 +69,7 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
   if (b_mode == OP_RC || b_mode == OP_RC_TAPS) TORCH_CHECK(ldb % 8 == 0, "gemm: ldb must be a multiple of 8");
   TORCH_CHECK(((uintptr_t)a.data_ptr() % 16) == 0 && ((uintptr_t)b.data_ptr() % 16) == 0, "gemm: operands must be 16-B aligned");
   TORCH_CHECK(k_split > 0 && k_split % 64 == 0, "gemm: k_split must be a positive multiple of 64");
-  TORCH_CHECK(tile >= 0 && tile <= kTileStream, "gemm: bad tile id");
+  TORCH_CHECK(tile >= 0 && tile <= kTileConv3, "gemm: bad tile id");
   if (tile == kTileStream) {
     TORCH_CHECK(a_mode == OP_KC && (b_mode == OP_KC || b_mode == OP_RC) && epi == EPI_BF16 && !outmap.has_value() &&
                     relu <= ACT_RELU && drop_p == 0.0 && beta == 0.0 && k_split >= K,
@@ -164,6 +164,9 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
     p.stats = stats->data_ptr<float>();
   }
   (void)bm;
+  if (tile == kTileConv3)
+    TORCH_CHECK(conv3x3_halo_ok(p) && epi == EPI_BF16, "gemm conv3x3: needs a 3x3 / stride-1 / pad-1 KC_GATHER x KC "
+                "conv with C % 64 == 0, N % 64 == 0, no split-K and at most bias/ReLU/statistics in the epilogue");
   at::DeviceGuard guard(a.device());
   HIP_OK(launch_gemm_bf16(p, (int)epi, (int)tile, cur_stream()));
 }

@@ -91,6 +91,10 @@ enum Activation : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_GELU_BWD =
 constexpr int kStatShards = 32;
 constexpr int kTile256 = 4;     // tile id of the 256x256 ping-pong kernel (ddl_gemm256.h)
 constexpr int kTileStream = 5;  // tile id of the weight-stationary streaming kernel (gemm_stream.hip)
+constexpr int kTileConv3 = 6;   // tile id of the 3x3 stride-1 halo convolution kernel (conv3x3.hip)
+
+// the halo kernel applies to this (KC_GATHER x KC, 3x3 / stride 1 / pad 1) GEMM
+bool conv3x3_halo_ok(const GemmParams& p);
 
 // panel width of the streaming kernel for (N, K), 0 when it does not apply
 int gemm_stream_panel(int N, int K);

@@ -203,11 +203,13 @@ struct Operand {
 };
 
 // Epilogue shared by the GEMM kernels.  mb / nb: first row / column of this wave's
-// RM x RN fragment block.  bf16 epilogue: acc holds D^T fragments (lane owns 4 consecutive
+// RM x RN fragment block; rows >= mend (default p.M) are not stored (tile-local row limits of
+// the halo conv kernel).  bf16 epilogue: acc holds D^T fragments (lane owns 4 consecutive
 // columns of one row); fp32 epilogues: D fragments (16 consecutive columns per row).
 template <int RM, int RN, int EPI>
 __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[RM][RN], const int mb, const int nb,
-                                              const int lane, const int bid) {
+                                              const int lane, const int bid, int mend = -1) {
+  const int mlim = mend < 0 ? p.M : mend;
   // ---------------------------------- epilogue ----------------------------------
   constexpr bool BF = EPI == EPI_BF16 || EPI == EPI_BF16_LITE;
   constexpr bool LITE = EPI == EPI_BF16_LITE;
@@ -223,7 +225,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int m = mb + 16 * i + 4 * (lane >> 4) + e;
-          if (m >= p.M) continue;
+          if (m >= mlim) continue;
           float* c = reinterpret_cast<float*>(p.c) + (long)m * p.ldc + n;
           const float v = acc[i][j][e] * p.alpha;
           if constexpr (EPI == EPI_F32) *c = (p.beta != 0.f) ? v + p.beta * *c : v;
@@ -246,7 +248,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
 #pragma unroll
   for (int i = 0; i < RM; ++i) {
     const int m = mb + 16 * i + mrow;
-    if (m >= p.M) continue;
+    if (m >= mlim) continue;
     long rowoff;
     int nn = 0, ii = 0, jj = 0;
     if (!LITE && p.om.enabled) {

@@ -7,6 +7,7 @@ int launch_gemm_plain_arc(const GemmParams& p, int epi, int tile, hipStream_t s)
 int launch_gemm_conv(const GemmParams& p, int epi, int tile, hipStream_t s);
 int launch_gemm256(const GemmParams& p, int epi, hipStream_t s);
 int launch_gemm_stream(const GemmParams& p, int epi, hipStream_t s);
+int launch_conv3x3(const GemmParams& p, int epi, hipStream_t s);
 
 int launch_gemm_bf16(const GemmParams& p, int epi, int tile, void* stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -17,6 +18,7 @@ int launch_gemm_bf16(const GemmParams& p, int epi, int tile, void* stream) {
     return launch_gemm256(p, epi, s);
   }
   if (tile == kTileStream) return launch_gemm_stream(p, epi, s);  // validates its own preconditions
+  if (tile == kTileConv3) return launch_conv3x3(p, epi, s);       // validates its own preconditions
   if (plain) return p.a_mode == OP_KC ? launch_gemm_plain_akc(p, epi, tile, s) : launch_gemm_plain_arc(p, epi, tile, s);
   return launch_gemm_conv(p, epi, tile, s);
 }

@@ -101,10 +101,36 @@ def _im2col(x, g: ConvGeometry, taps_h, taps_w, ho, wo, sh, sw, kpad):
     return col
 
 
+_HALO3 = _os.environ.get("DDL_CONV3X3", "1") != "0"
+
+
+def halo3_ok(g: ConvGeometry) -> bool:
+    """The 3x3 / stride-1 / pad-1 halo kernel applies (mirror of ``conv3x3_halo_ok`` in
+    csrc/kernels/conv3x3.hip: C and Co multiples of 64, a row tiling of <= 256 output pixels
+    whose halo fits 384 LDS rows)."""
+    if not (_HALO3 and g.KH == 3 and g.KW == 3 and (g.sh, g.sw) == (1, 1) and (g.ph, g.pw) == (1, 1)
+            and (g.dh, g.dw) == (1, 1) and g.Ci % 64 == 0 and g.Co % 64 == 0 and g.implicit_fwd):
+        return False
+    if g.Ci == 64 and g.Co == 64 and _os.environ.get("DDL_CONV3X3_C64", "0") != "1":
+        # one 64-channel chunk: the halo prologue is not amortised; measured 0.128 vs 0.120 ms at
+        # 56x56 (ResNet stage 1) — the implicit GEMM keeps these
+        return False
+    H, W = g.H, g.W
+    if H * W <= 256:
+        return H * W * max(1, min(256 // (H * W), 384 // ((H + 2) * (W + 2)))) >= 64
+    for r in range(min(H, 256 // W), 0, -1):
+        if H % r == 0 and (r + 2) * (W + 2) <= 384:
+            return r * W >= 64
+    return False
+
+
 def conv_fwd_native(x, w, g: ConvGeometry, bias=None, relu=False, stats=None):
     y = torch.empty((g.N, g.Ho, g.Wo, g.Co), dtype=torch.bfloat16, device=x.device)
     y2 = y.view(g.M, g.Co)
-    if g.is_pointwise:
+    if halo3_ok(g):
+        G.gemm(x, w, y2, g.M, g.Co, g.T * g.Ci, G.KC_GATHER, G.KC, 0, g.T * g.Ci, g.Co, G.EPI_BF16, bias=bias,
+               relu=relu, geom=g.fwd_geom, stats=stats, tile=G.TILE_CONV3)
+    elif g.is_pointwise:
         G.linear_fwd(x.view(g.M, g.Ci), w.view(g.Co, g.Ci), bias=bias, relu=relu, out=y2, stats=stats)
     elif g.implicit_fwd or g.gather8_fwd:
         G.gemm(x, w, y2, g.M, g.Co, g.T * g.Ci, G.KC_GATHER if g.implicit_fwd else G.KC_GATHER8, G.KC, 0,

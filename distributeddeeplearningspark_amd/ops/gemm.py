@@ -20,7 +20,9 @@ KC, RC, KC_GATHER, RC_GATHER, RC_TAPS, KC_GATHER8, RC_GATHER8 = 0, 1, 2, 3, 4, 5
 EPI_BF16, EPI_F32, EPI_F32_ATOMIC = 0, 1, 2
 TILE256 = 4  # 256x256 ping-pong kernel (csrc/include/ddl_gemm256.h): plain KC/RC operands, K % 64 == 0
 TILE_STREAM = 5  # weight-stationary streaming kernel (csrc/kernels/gemm_stream.hip): K in {64, 128, 256}
-_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), TILE256: (256, 256), TILE_STREAM: (64, 256)}
+TILE_CONV3 = 6  # 3x3 stride-1 halo convolution (csrc/kernels/conv3x3.hip): KC_GATHER x KC, no split-K
+_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), TILE256: (256, 256), TILE_STREAM: (64, 256),
+          TILE_CONV3: (224, 128)}
 _CU = 256
 import os as _os
 

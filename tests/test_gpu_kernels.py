@@ -465,3 +465,33 @@ def test_resnet_per_layer_gradients_match_fp32_cpu():
         if cos["hip"] < min(cos["lib"] - 0.03, 0.995) or cos["hip"] < 0.85 or rel["hip"] > max(0.08, rel["lib"] + 0.03):
             bad.append((pname, round(cos["hip"], 4), round(cos["lib"], 4), round(rel["hip"], 4), round(rel["lib"], 4)))
     assert not bad, f"(layer, cos hip, cos lib, norm err hip, norm err lib): {bad}"
+
+
+@pytest.mark.parametrize("N,H,W,Ci,Co", [(3, 56, 56, 64, 64), (2, 28, 28, 128, 128), (5, 14, 14, 256, 256),
+                                         (9, 7, 7, 512, 512), (2, 20, 12, 64, 192), (4, 9, 9, 128, 64)])
+@pytest.mark.parametrize("bias_relu", [False, True])
+def test_conv3x3_halo_kernel(N, H, W, Ci, Co, bias_relu, monkeypatch):
+    """3x3 stride-1 halo kernel (csrc/kernels/conv3x3.hip) vs fp32 PyTorch: whole-row tiles of
+    one image (56/28/20 wide), whole images per tile with a partial last group of images (N=9 at
+    7x7, N=5 at 14x14), 64- and 128-channel output tiles, bias+ReLU and the fused BN statistics."""
+    from distributeddeeplearningspark_amd.ops import conv as CV
+    from distributeddeeplearningspark_amd.ops import gemm as G
+
+    monkeypatch.setenv("DDL_CONV3X3_C64", "1")  # also the 64 -> 64 channel case (off by default)
+    g = CV.geometry(N, H, W, Ci, Co, 3, 3, (1, 1), (1, 1), (1, 1))
+    assert CV.halo3_ok(g)
+    x = rnd(N, H, W, Ci, seed=1)
+    w = rnd(Co, 3, 3, Ci, scale=0.05, seed=2)
+    b = torch.randn(Co, device=DEV) * 0.1 if bias_relu else None
+    st = torch.zeros((32, 2, Co), dtype=torch.float32, device=DEV)
+    y = CV.conv_fwd_native(x, w, g, bias=b, relu=bias_relu, stats=st)
+    ref = CV.conv_ref(x.float(), w.float(), b, (1, 1), (1, 1), (1, 1), relu=bias_relu)
+    close(y, ref, what="halo conv")
+    yf = y.float().reshape(-1, Co)
+    close(st.sum(0)[0], yf.sum(0), rtol=1e-3, atol=1e-1, what="halo stats sum")
+    close(st.sum(0)[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-1, what="halo stats sumsq")
+    # the implicit-GEMM kernel on the same problem agrees too (same bf16 rounding of the output)
+    y2 = torch.empty_like(y)
+    G.gemm(x, w, y2.view(g.M, Co), g.M, Co, 9 * Ci, G.KC_GATHER, G.KC, 0, 9 * Ci, Co, G.EPI_BF16, bias=b,
+           relu=bias_relu, geom=g.fwd_geom)
+    close(y, y2, rtol=1e-2, atol=1e-2, what="halo vs implicit GEMM")
