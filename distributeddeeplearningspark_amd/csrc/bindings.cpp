@@ -35,6 +35,7 @@ void fill_geom(ConvGeom& g, const py::dict& d) {
   g.sh = d["sh"].cast<int>();
   g.sw = d["sw"].cast<int>();
   g.tap_c = d["tap_c"].cast<int>();
+  g.tap_shift = (g.tap_c > 0 && (g.tap_c & (g.tap_c - 1)) == 0) ? __builtin_ctz((unsigned)g.tap_c) : -1;
   auto dh = d["dh"].cast<std::vector<int>>();
   auto dw = d["dw"].cast<std::vector<int>>();
   std::vector<int> wt = d.contains("wt") ? d["wt"].cast<std::vector<int>>() : std::vector<int>(dh.size(), 0);

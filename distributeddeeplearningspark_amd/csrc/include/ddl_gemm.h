@@ -43,6 +43,7 @@ struct ConvGeom {
   int sh, sw;         // stride on that grid
   int ntaps;
   int tap_c;          // channels per tap inside the gathered dimension
+  int tap_shift;      // log2(tap_c) when tap_c is a power of two, else -1 (per-vector tap lookups)
   int8_t dh[kMaxTaps];
   int8_t dw[kMaxTaps];
   int16_t wt[kMaxTaps];  // weight tap index (OP_RC_TAPS)

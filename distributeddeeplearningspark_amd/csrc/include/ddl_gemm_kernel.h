@@ -63,13 +63,41 @@ struct Operand {
   int pixbase[V];  // n*hi*wi
   int hbase[V], wbase[V];
   bool rvalid[V];
+  // gather state (RC_GATHER / RC_GATHER8): the output pixel k = k0 + krow of vector v, kept as
+  // (n, i, j) and advanced by BK per staged K-tile (the K-tiles are staged strictly in order), so
+  // the main loop does no integer division (two runtime divisions per vector per K-tile made the
+  // gathered weight-gradient kernels VALU-bound on address arithmetic)
+  static constexpr bool RCG = (MODE == OP_RC_GATHER || MODE == OP_RC_GATHER8);
+  int qn[RCG ? V : 1], qi[RCG ? V : 1], qj[RCG ? V : 1];
+  int tap8[MODE == OP_RC_GATHER8 ? V : 1], ch8[MODE == OP_RC_GATHER8 ? V : 1];
+  int di, dj;
 
-  __device__ __forceinline__ void init(const void* p, long ld_, int rows_, int r0_, int K_, const ConvGeom& g) {
+  __device__ __forceinline__ void init(const void* p, long ld_, int rows_, int r0_, int K_, const ConvGeom& g,
+                                       int k0 = 0) {
     ptr = reinterpret_cast<const bf16_t*>(p);
     ld = ld_;
     rows = rows_;
     r0 = r0_;
     K = K_;
+    if constexpr (RCG) {
+      di = BK / g.wo;
+      dj = BK - di * g.wo;
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const int idx = threadIdx.x + v * NTHREADS;
+        const int krow = idx / (R / 8);
+        const int k = k0 + krow;
+        pix_decompose((uint32_t)(k < K ? k : 0), g.ho, g.wo, qn[v], qi[v], qj[v]);
+        if constexpr (MODE == OP_RC_GATHER8) {
+          // the (tap, channel) of this thread's 8 columns does not depend on k (SWZ or not: both
+          // column permutations are functions of krow only, fixed per thread)
+          const int rc = (idx % (R / 8)) ^ (rc_swz<R>(krow) << 1);
+          const int r = r0 + rc * 8;
+          tap8[v] = r < rows ? r / g.tap_c : 0;
+          ch8[v] = r - tap8[v] * g.tap_c;
+        }
+      }
+    }
     if constexpr (MODE == OP_KC_GATHER || MODE == OP_KC_GATHER8) {
 #pragma unroll
       for (int v = 0; v < V; ++v) {
@@ -107,7 +135,7 @@ struct Operand {
       } else {  // OP_KC_GATHER8
         const int k = k0 + kc * 8;
         bool ok = rvalid[v] && k < K;
-        const int t = ok ? k / g.tap_c : 0;
+        const int t = ok ? (g.tap_shift >= 0 ? k >> g.tap_shift : k / g.tap_c) : 0;
         const int c = k - t * g.tap_c;
         const int ih = hbase[v] + g.dh[t], iw = wbase[v] + g.dw[t];
         ok = ok && (unsigned)ih < (unsigned)g.hi && (unsigned)iw < (unsigned)g.wi;
@@ -121,28 +149,51 @@ struct Operand {
         const int r = r0 + rc * 8;
         return (r < rows && k < K) ? ptr + (long)k * ld + r : nullptr;
       } else if constexpr (MODE == OP_RC_GATHER8) {
-        const int r = r0 + rc * 8;
-        bool ok = k < K && r < rows;
-        const int t = ok ? r / g.tap_c : 0;
-        const int c = r - t * g.tap_c;
-        int n, i, j;
-        pix_decompose((uint32_t)(ok ? k : 0), g.ho, g.wo, n, i, j);
-        const int ih = i * g.sh + g.dh[t], iw = j * g.sw + g.dw[t];
+        // (rc is the SWZ-permuted column chunk; the (tap, channel) of it was fixed in init for the
+        // swizzled order; the register path (SWZ = false) recomputes it)
+        int t = tap8[v], c = ch8[v];
+        bool ok = k < K;
+        if constexpr (!SWZ) {
+          const int r = r0 + rc * 8;
+          ok = ok && r < rows;
+          t = r < rows ? r / g.tap_c : 0;
+          c = r - t * g.tap_c;
+        } else {
+          ok = ok && r0 + rc * 8 < rows;
+        }
+        const int ih = qi[v] * g.sh + g.dh[t], iw = qj[v] * g.sw + g.dw[t];
         ok = ok && (unsigned)ih < (unsigned)g.hi && (unsigned)iw < (unsigned)g.wi;
-        return ok ? ptr + ((long)((n * g.hi + ih) * g.wi + iw)) * g.c + c : nullptr;
+        return ok ? ptr + ((long)((qn[v] * g.hi + ih) * g.wi + iw)) * g.c + c : nullptr;
       } else if constexpr (MODE == OP_RC_GATHER) {
         const int t = r0 / g.tap_c;  // block-uniform: tap_c % R == 0
         const int c0 = r0 - t * g.tap_c;
-        int n, i, j;
-        pix_decompose((uint32_t)(k < K ? k : 0), g.ho, g.wo, n, i, j);
-        const int ih = i * g.sh + g.dh[t], iw = j * g.sw + g.dw[t];
+        const int ih = qi[v] * g.sh + g.dh[t], iw = qj[v] * g.sw + g.dw[t];
         const bool ok = k < K && (unsigned)ih < (unsigned)g.hi && (unsigned)iw < (unsigned)g.wi;
-        return ok ? ptr + ((long)((n * g.hi + ih) * g.wi + iw)) * g.c + c0 + rc * 8 : nullptr;
+        return ok ? ptr + ((long)((qn[v] * g.hi + ih) * g.wi + iw)) * g.c + c0 + rc * 8 : nullptr;
       } else {  // OP_RC_TAPS: k = tap*kdiv + co ; addr = ptr + co*ld + wt[tap]*tap_stride + r
         const int t = k0 / kdiv;  // block-uniform: kdiv % 64 == 0
         const int co0 = k0 - t * kdiv;
         const int r = r0 + rc * 8;
         return (r < rows && k < K) ? ptr + (long)g.wt[t] * tap_stride + (long)(co0 + krow) * ld + r : nullptr;
+      }
+    }
+  }
+
+  // RC gather modes: move the per-vector pixel state to the next K-tile (k += BK)
+  __device__ __forceinline__ void advance(const ConvGeom& g) {
+    if constexpr (RCG) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        qj[v] += dj;
+        qi[v] += di;
+        if (qj[v] >= g.wo) {
+          qj[v] -= g.wo;
+          qi[v] += 1;
+        }
+        while (qi[v] >= g.ho) {
+          qi[v] -= g.ho;
+          qn[v] += 1;
+        }
       }
     }
   }
@@ -153,15 +204,17 @@ struct Operand {
       const bf16_t* src = addr<false>(v, k0, g, kdiv, tap_stride);
       reg[v] = src ? ldg16(src) : make_uint4(0, 0, 0, 0);
     }
+    advance(g);
   }
 
   // LDS-DMA of the K-tile at k0 into a (swizzled) LDS image: V wave-instructions of 1 KB each
-  __device__ __forceinline__ void dma(char* lds, int k0, const ConvGeom& g, int kdiv, long tap_stride, int wid) const {
+  __device__ __forceinline__ void dma(char* lds, int k0, const ConvGeom& g, int kdiv, long tap_stride, int wid) {
 #pragma unroll
     for (int v = 0; v < V; ++v) {
       const bf16_t* src = addr<true>(v, k0, g, kdiv, tap_stride);
       dma16(src ? (const void*)src : (const void*)ddl_zero_page, lds_addr(lds + v * (NTHREADS * 16) + wid * 1024));
     }
+    advance(g);
   }
 
   __device__ __forceinline__ void store(char* lds) const {
@@ -421,8 +474,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams
 
   Operand<BM, AMODE> A;
   Operand<BN, BMODE> B;
-  A.init(p.a, p.lda, p.M, m0, p.K, p.g);
-  B.init(p.b, p.ldb, p.N, n0, p.K, p.g);
+  A.init(p.a, p.lda, p.M, m0, p.K, p.g, kbeg);
+  B.init(p.b, p.ldb, p.N, n0, p.K, p.g, kbeg);
 
   f32x4 acc[RM][RN];
 #pragma unroll
@@ -502,8 +555,8 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
 
   Operand<BM, AMODE> A;
   Operand<BN, BMODE> B;
-  A.init(p.a, p.lda, p.M, m0, p.K, p.g);
-  B.init(p.b, p.ldb, p.N, n0, p.K, p.g);
+  A.init(p.a, p.lda, p.M, m0, p.K, p.g, kbeg);
+  B.init(p.b, p.ldb, p.N, n0, p.K, p.g, kbeg);
 
   f32x4 acc[RM][RN];
 #pragma unroll
@@ -512,6 +565,56 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
     for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto stage = [&](int buf) { return smem + buf * (A_BYTES + B_BYTES); };
+  if constexpr (ST >= 3) {
+    // ST-slot ring, ONE barrier per K-tile: ST-1 tiles are issued ahead.  At iteration t the wave
+    // waits (counted vmcnt) for its tile-t DMAs only, the barrier then publishes tile t to every
+    // wave AND proves every wave has finished reading slot (t-1) % ST (its tile t-1 fragments
+    // were consumed by iteration t-1's MFMAs), so that slot is refilled with tile t+ST-1 right
+    // after the barrier and loads stay in flight across ST-2 barriers.
+    constexpr int PER = VA + VB;
+#pragma unroll
+    for (int s = 0; s < ST - 1; ++s)
+      if (s < nk) {
+        A.dma(stage(s), kbeg + s * BK, p.g, p.b_kdiv, p.b_tap_stride, wid);
+        B.dma(stage(s) + A_BYTES, kbeg + s * BK, p.g, p.b_kdiv, p.b_tap_stride, wid);
+      }
+    int slot = 0;
+    for (int t = 0; t < nk; ++t) {
+      const int ahead = min(ST - 2, nk - 1 - t);  // tiles issued after tile t still allowed in flight
+      if (ahead >= 2) wait_vmcnt<2 * PER>();
+      else if (ahead == 1) wait_vmcnt<PER>();
+      else wait_vmcnt<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (t + ST - 1 < nk) {
+        char* nx = stage(slot == 0 ? ST - 1 : slot - 1);
+        A.dma(nx, kbeg + (t + ST - 1) * BK, p.g, p.b_kdiv, p.b_tap_stride, wid);
+        B.dma(nx + A_BYTES, kbeg + (t + ST - 1) * BK, p.g, p.b_kdiv, p.b_tap_stride, wid);
+      }
+      const char* la = stage(slot);
+      const char* lb = la + A_BYTES;
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk) {
+        bf16x8 af[RM], bf[RN];
+#pragma unroll
+        for (int i = 0; i < RM; ++i) af[i] = A.frag(la, kk, i, wm0, lane);
+#pragma unroll
+        for (int j = 0; j < RN; ++j) bf[j] = B.frag(lb, kk, j, wn0, lane);
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j) {
+            if constexpr (EPI == EPI_BF16 || EPI == EPI_BF16_LITE)
+              acc[i][j] = mfma16x16x32(bf[j], af[i], acc[i][j]);
+            else
+              acc[i][j] = mfma16x16x32(af[i], bf[j], acc[i][j]);
+          }
+      }
+      slot = slot + 1 == ST ? 0 : slot + 1;
+    }
+    gemm_epilogue<RM, RN, EPI>(p, acc, m0 + wm0, n0 + wn0, lane, bid);
+    return;
+  }
   if (nk > 0) {
     A.dma(stage(0), kbeg, p.g, p.b_kdiv, p.b_tap_stride, wid);
     B.dma(stage(0) + A_BYTES, kbeg, p.g, p.b_kdiv, p.b_tap_stride, wid);
@@ -572,6 +675,31 @@ inline int gemm_dma_mode() {
   return mode;
 }
 
+// LDS ring depth of the fp32-output (weight-gradient) kernels, forced by DDL_WGRAD_STAGES: 1 = the
+// single-stage kernel, 3 / 4 = the one-barrier ring with 2 / 3 K-tiles in flight; unset = default.  These kernels run at 2
+// blocks per CU, too few for co-resident blocks alone to hide the LDS-DMA latency.
+inline int wgrad_stages() {
+  static int st = -1;
+  if (st < 0) {
+    const char* e = getenv("DDL_WGRAD_STAGES");
+    st = e ? atoi(e) : 0;  // 0: per-operand-mode default (launch_tile)
+    if (st != 0 && st != 1 && st != 3 && st != 4) st = 0;
+  }
+  return st;
+}
+
+template <int BM, int BN, int AMODE, int BMODE, int EPI, int ST>
+inline int launch_ring(const dim3 grid, const GemmParams& p, hipStream_t s) {
+  constexpr int lds = ST * (BM + BN) * BK * 2;
+  static bool attr = [] {  // dynamic LDS above 64 KB must be allowed explicitly
+    return lds <= 65536 || hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_dma_kernel<BM, BN, AMODE, BMODE, EPI, ST>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, AMODE, BMODE, EPI, ST>), grid, dim3(NTHREADS), lds, s, p);
+  return (int)hipGetLastError();
+}
+
 template <int BM, int BN, int AMODE, int BMODE, int EPI>
 inline int launch_tile(const GemmParams& p, hipStream_t s) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
@@ -580,6 +708,14 @@ inline int launch_tile(const GemmParams& p, hipStream_t s) {
   const bool one_stage = p.k_split <= BK;
   const dim3 grid(tiles, splits > 0 ? splits : 1);
   const int dm = gemm_dma_mode();
+  if constexpr (EPI == EPI_F32 || EPI == EPI_F32_ATOMIC) {
+    // default: the 3-slot ring for plain (1x1 / Linear) weight gradients, measured 10-25 % faster on
+    // the ResNet-50 1x1 layers; the gathered (3x3 / strided) ones stay single-stage (ring 30 % slower)
+    constexpr bool plain = AMODE == OP_RC && BMODE == OP_RC;
+    const int st = one_stage ? 1 : (wgrad_stages() ? wgrad_stages() : (plain ? 3 : 1));
+    if (dm == 1 && st == 3) return launch_ring<BM, BN, AMODE, BMODE, EPI, 3>(grid, p, s);
+    if (dm == 1 && st == 4) return launch_ring<BM, BN, AMODE, BMODE, EPI, 4>(grid, p, s);
+  }
   if (dm == 1 || (dm == 2 && one_stage)) {
     hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, AMODE, BMODE, EPI, 1>), grid, dim3(NTHREADS), (BM + BN) * BK * 2, s, p);
   } else if (dm == 2) {
