@@ -23,7 +23,7 @@ int bn_finalize(const float* ws, int S, long M, int C, const float* gamma, const
 // y = relu?(x*scale[c] + shift[c] + resid)
 // mask (optional): one byte per 8 channels, bit i = (pre-ReLU output > 0), the mode-3 backward mask
 int bn_apply(const void* x, const float* scale, const float* shift, const void* resid, void* y, void* mask, long M,
-             int C, int relu, hipStream_t s);
+             int C, int relu, hipStream_t s, const float* res_scale = nullptr, const float* res_shift = nullptr);
 // backward pass 1: dy' = dy * relu-mask ; ws[shard][0][c] += sum dy', ws[shard][1][c] += sum dy'*(x-mean)
 // mask mode: 0 none, 1 (y > 0) from the forward output, 2 (x*scale+shift > 0) recomputed from x
 int bn_bwd_reduce(const void* dy, const void* x, const void* y, const float* scale, const float* shift,

@@ -225,12 +225,20 @@ __device__ __forceinline__ void store_mask_bits(uint8_t* __restrict__ mask, long
 __global__ __launch_bounds__(256) void bn_apply_kernel(const uint4* __restrict__ x, const float* __restrict__ scale,
                                                         const float* __restrict__ shift, const uint4* __restrict__ res,
                                                         uint4* __restrict__ y, uint8_t* __restrict__ mask, long M,
-                                                        int C, int relu) {
+                                                        int C, int relu, const float* __restrict__ res_scale,
+                                                        const float* __restrict__ res_shift) {
   ColGeom g(C);
   if (!g.active) return;
-  float sc[8], sh[8];
+  float sc[8], sh[8], rsc[8], rsh[8];
   load8f(scale + g.cv * 8, sc);
   load8f(shift + g.cv * 8, sh);
+  // dual apply: the residual is itself a pre-BN tensor (ResNet downsample shortcut), normalised
+  // here instead of in a separate apply sweep that would write and re-read it
+  const bool rbn = res_scale != nullptr;
+  if (rbn) {
+    load8f(res_scale + g.cv * 8, rsc);
+    load8f(res_shift + g.cv * 8, rsh);
+  }
   const long step = (long)gridDim.x * g.RT;
   for (long r = (long)blockIdx.x * g.RT + g.rt; r < M; r += 2 * step) {
     const bool two = r + step < M;
@@ -252,7 +260,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint4* __restrict__
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         float o = f[i] * sc[i] + sh[i];
-        if (res) o += q[i];
+        if (res) o += rbn ? q[i] * rsc[i] + rsh[i] : q[i];
         bits |= (o > 0.f ? 1u : 0u) << i;
         if (relu) o = fmaxf(o, 0.f);
         f[i] = o;
@@ -273,9 +281,9 @@ static dim3 stream_grid(long M, int C) {
 }
 
 int bn_apply(const void* x, const float* scale, const float* shift, const void* resid, void* y, void* mask, long M,
-             int C, int relu, hipStream_t s) {
+             int C, int relu, hipStream_t s, const float* res_scale, const float* res_shift) {
   hipLaunchKernelGGL(bn_apply_kernel, stream_grid(M, C), dim3(256), 0, s, (const uint4*)x, scale, shift,
-                     (const uint4*)resid, (uint4*)y, (uint8_t*)mask, M, C, relu);
+                     (const uint4*)resid, (uint4*)y, (uint8_t*)mask, M, C, relu, res_scale, res_shift);
   return (int)hipGetLastError();
 }
 

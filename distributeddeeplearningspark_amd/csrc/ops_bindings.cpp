@@ -55,10 +55,17 @@ void bn_finalize_(const at::Tensor& ws, int64_t M, int64_t C, c10::optional<at::
 }
 
 void bn_apply_(const at::Tensor& x, const at::Tensor& scale, const at::Tensor& shift, c10::optional<at::Tensor> resid,
-               const at::Tensor& y, int64_t C, bool relu, c10::optional<at::Tensor> mask) {
+               const at::Tensor& y, int64_t C, bool relu, c10::optional<at::Tensor> mask,
+               c10::optional<at::Tensor> res_scale, c10::optional<at::Tensor> res_shift) {
   GPU(x); BF16(x); BF16(y); F32(scale); F32(shift);
   CK(C % 8 == 0 && x.numel() % C == 0 && y.numel() == x.numel(), "bn_apply: shapes");
   if (resid) { BF16(*resid); CK(resid->numel() == x.numel(), "bn_apply: resid shape"); }
+  CK(res_scale.has_value() == res_shift.has_value() && (!res_scale || resid), "bn_apply: res_scale/res_shift pair needs resid");
+  if (res_scale) {
+    F32(*res_scale); F32(*res_shift);
+    CK(res_scale->numel() == C && res_shift->numel() == C && res_scale->is_contiguous() && res_shift->is_contiguous(),
+       "bn_apply: res_scale/res_shift [C]");
+  }
   if (mask) {
     CK(mask->scalar_type() == at::kByte && mask->is_contiguous() && mask->numel() >= (x.numel() / 8 + 63) / 64 * 64,
        "bn_apply: mask must be uint8 [ceil(numel / 512) * 64]");
@@ -66,7 +73,8 @@ void bn_apply_(const at::Tensor& x, const at::Tensor& scale, const at::Tensor& s
   }
   at::DeviceGuard g(x.device());
   HIP_OK(bn_apply(x.data_ptr(), scale.data_ptr<float>(), shift.data_ptr<float>(), optr<const void>(resid), y.data_ptr(),
-                  optr<void>(mask), x.numel() / C, (int)C, relu ? 1 : 0, cur_stream()));
+                  optr<void>(mask), x.numel() / C, (int)C, relu ? 1 : 0, cur_stream(), optr<const float>(res_scale),
+                  optr<const float>(res_shift)));
 }
 
 // relu mask mode: 0 none; 1 from y (forward output); 2 recomputed from x*scale+shift
@@ -353,7 +361,9 @@ void register_ops(py::module& m) {
   m.def("bn_stats", &bn_stats_);
   m.def("bn_partial_rows", &bn_partial_rows_);
   m.def("bn_finalize", &bn_finalize_);
-  m.def("bn_apply", &bn_apply_);
+  m.def("bn_apply", &bn_apply_, py::arg("x"), py::arg("scale"), py::arg("shift"), py::arg("resid"), py::arg("y"),
+        py::arg("C"), py::arg("relu"), py::arg("mask") = py::none(), py::arg("res_scale") = py::none(),
+        py::arg("res_shift") = py::none());
   m.def("bn_bwd_reduce", &bn_bwd_reduce_);
   m.def("bn_bwd_finalize", &bn_bwd_finalize_);
   m.def("bn_bwd_dx", &bn_bwd_dx_);

@@ -28,7 +28,10 @@ class _ConvBNState:
     __slots__ = ("g", "yc", "y", "mean", "invstd", "scale", "shift", "mode", "mask")
 
 
-def _bn_forward(layer_bn, yc, stats, resid, relu, training, mask=None):
+def _bn_forward(layer_bn, yc, stats, resid, relu, training, mask=None, apply=True, res_affine=None):
+    """Finalize the fused statistics into scale/shift (+ running stats) and, with ``apply``, write
+    ``relu(yc * scale + shift + resid)``; ``res_affine = (scale_r, shift_r)`` normalises a pre-BN
+    residual on the fly (the downsample shortcut's BN rides in its consumer's apply sweep)."""
     Cc = yc.shape[-1]
     M = yc.numel() // Cc
     dev = yc.device
@@ -41,13 +44,17 @@ def _bn_forward(layer_bn, yc, stats, resid, relu, training, mask=None):
     mean = torch.empty(Cc, dtype=torch.float32, device=dev)
     invstd = torch.empty(Cc, dtype=torch.float32, device=dev)
     C().bn_finalize(stats, M, Cc, gamma, beta, bn.epsilon, 1.0 - bn.momentum, rm, rv, mean, invstd, scale, shift)
+    if not apply:
+        return None, mean, invstd, scale, shift
     y = torch.empty_like(yc)
-    C().bn_apply(yc, scale, shift, resid, y, Cc, relu, mask)
+    rs, rt = res_affine if res_affine is not None else (None, None)
+    C().bn_apply(yc, scale, shift, resid, y, Cc, relu, mask, rs, rt)
     return y, mean, invstd, scale, shift
 
 
-def convbn_forward(unit, x, resid=None, relu=True):
-    """conv (fused statistics) + BN (+resid)(+relu) for a ``models.resnet.ConvBN`` unit."""
+def convbn_forward(unit, x, resid=None, relu=True, apply=True, res_affine=None):
+    """conv (fused statistics) + BN (+resid)(+relu) for a ``models.resnet.ConvBN`` unit.
+    ``apply=False``: statistics and scale/shift only (``st.y`` is None: the consumer applies them)."""
     conv, bn = unit.conv, unit.bn
     N, H, W, Ci = x.shape
     kh, kw = conv.kernel_size
@@ -62,7 +69,8 @@ def convbn_forward(unit, x, resid=None, relu=True):
     Co = yc.shape[-1]
     bits = relu and resid is not None and Co & (Co - 1) == 0
     st.mask = torch.empty(-(-yc.numel() // 512) * 64, dtype=torch.uint8, device=yc.device) if bits else None
-    st.y, st.mean, st.invstd, st.scale, st.shift = _bn_forward(bn, yc, stats, resid, relu, True, st.mask)
+    st.y, st.mean, st.invstd, st.scale, st.shift = _bn_forward(bn, yc, stats, resid, relu, True, st.mask, apply,
+                                                               res_affine)
     st.mode = 0 if not relu else (2 if resid is None else (3 if bits else 1))
     return st
 
@@ -99,11 +107,14 @@ class _BottleneckFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, anchor, block):
         x = x.contiguous()
-        s_down = convbn_forward(block.down, x, relu=False) if block.down is not None else None
-        sc = s_down.y if s_down is not None else x
+        # the downsample BN is not applied on its own: its scale/shift normalise the shortcut inside
+        # the block-output apply sweep (one write + one read of the shortcut tensor saved)
+        s_down = convbn_forward(block.down, x, relu=False, apply=False) if block.down is not None else None
+        sc = s_down.yc if s_down is not None else x
         s1 = convbn_forward(block.c1, x, relu=True)
         s2 = convbn_forward(block.c2, s1.y, relu=True)
-        s3 = convbn_forward(block.c3, s2.y, resid=sc, relu=True)
+        s3 = convbn_forward(block.c3, s2.y, resid=sc, relu=True,
+                            res_affine=None if s_down is None else (s_down.scale, s_down.shift))
         ctx.block, ctx.states = block, (s_down, s1, s2, s3)
         ctx.save_for_backward(x)
         ctx.needs_dx = ctx.needs_input_grad[0]

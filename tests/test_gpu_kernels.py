@@ -200,6 +200,30 @@ def test_batchnorm(resid, relu):
     close(rv, 0.9 + 0.1 * var.detach() * n / (n - 1), rtol=1e-3, atol=1e-3, what="running var")
 
 
+@pytest.mark.parametrize("Cc", [64, 256, 2048])
+def test_bn_apply_dual(Cc):
+    """bn_apply with a pre-BN residual normalised in the same sweep (ResNet downsample shortcut):
+    relu(x*s + t + r*rs + rt) and its bit mask, vs fp32 torch on the same bf16 inputs."""
+    M = 3 * 49 + 5
+    x = rnd(M, Cc, seed=21)
+    r = rnd(M, Cc, seed=22)
+    s, t = torch.rand(Cc, device=DEV) + 0.5, torch.randn(Cc, device=DEV) * 0.1
+    rs, rt = torch.rand(Cc, device=DEV) + 0.5, torch.randn(Cc, device=DEV) * 0.1
+    y = torch.empty_like(x)
+    mask = torch.zeros(-(-x.numel() // 512) * 64, dtype=torch.uint8, device=DEV)
+    _C().bn_apply(x, s, t, r, y, Cc, True, mask, rs, rt)
+    pre = x.float() * s + t + (r.float() * rs + rt)
+    close(y, torch.relu(pre), rtol=1e-2, atol=1e-2, what="dual apply")
+    # the bit mask (bn.hip relu_mask mode 3): element e = 8 v + i of 16-B vector v is bit (v & 63) of
+    # 64-bit word 8 (v >> 6) + i
+    words = mask.view(torch.int64).cpu()
+    e = torch.arange(x.numel())
+    v, i = e >> 3, e & 7
+    bits = (words[8 * (v >> 6) + i] >> (v & 63)) & 1
+    ref = (pre.flatten().cpu() > 0).long()
+    assert (bits != ref).float().mean().item() < 1e-3
+
+
 # ----------------------------------------------------------------------------- pooling
 @pytest.mark.parametrize("k,s,p,H", [(3, 2, 1, 16), (2, 2, 0, 24), (3, 2, 1, 15)])
 def test_maxpool(k, s, p, H):
@@ -370,19 +394,25 @@ def test_fused_bottleneck_matches_composed_ops():
     x = torch.randn(16, 32, 32, 3)
     y = torch.randint(0, 10, (16,))
     res = {}
-    for fused in ("1", "0"):
+    for fused, dev in (("1", DEV), ("0", DEV), ("0", "cpu")):
         os.environ["DDL_FUSED_BLOCKS"] = fused
         try:
             m = ResNet(blocks=(2,), input_shape=(32, 32, 3), num_classes=10)
             m.compile("sgd", "sparse_categorical_crossentropy")
-            m.place(DEV, seed=5)
+            m.place(dev, seed=5)
             loss = m.backward_step(m.to_input(x), m.to_target(y))
-            res[fused] = (float(loss), m.arena.grad.clone())
+            res[fused + dev] = (float(loss.detach()), m.arena.grad.float().cpu().clone())
         finally:
             os.environ.pop("DDL_FUSED_BLOCKS", None)
-    assert abs(res["1"][0] - res["0"][0]) < 1e-2 * max(1.0, abs(res["0"][0])), (res["1"][0], res["0"][0])
-    g1, g0 = res["1"][1], res["0"][1]
-    assert ((g1 - g0).norm() / g0.norm()).item() < 3e-2
+    l1, l0, lc = res["1" + DEV][0], res["0" + DEV][0], res["0cpu"][0]
+    assert abs(l1 - l0) < 1e-2 * max(1.0, abs(l0)), (l1, l0)
+    # the fused node applies the downsample BN inside the block-output sweep (the shortcut is never
+    # rounded to bf16), so it differs from the composed bf16 graph by that rounding; both must sit
+    # as close to the fp32 CPU gradients (bf16 noise through the BN backward: ~5-8 % per layer)
+    g1, g0, gc = res["1" + DEV][1], res["0" + DEV][1], res["0cpu"][1]
+    e1, e0 = ((g1 - gc).norm() / gc.norm()).item(), ((g0 - gc).norm() / gc.norm()).item()
+    assert e1 < 1.25 * e0 + 1e-2 and e1 < 0.1, (e1, e0)
+    assert ((g1 - g0).norm() / g0.norm()).item() < 6e-2
 
 
 @pytest.mark.parametrize("kind", ["adam", "adamw", "adam_keras"])
