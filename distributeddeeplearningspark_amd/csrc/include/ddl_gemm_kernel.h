@@ -678,13 +678,18 @@ inline int gemm_dma_mode() {
 // LDS ring depth of the fp32-output (weight-gradient) kernels, forced by DDL_WGRAD_STAGES: 1 = the
 // single-stage kernel, 3 / 4 = the one-barrier ring with 2 / 3 K-tiles in flight; unset = default.  These kernels run at 2
 // blocks per CU, too few for co-resident blocks alone to hide the LDS-DMA latency.
+inline int stages_env(const char* name) {
+  const char* e = getenv(name);
+  int st = e ? atoi(e) : 0;  // 0: per-operand-mode default (launch_tile)
+  return (st == 1 || st == 3 || st == 4) ? st : 0;
+}
 inline int wgrad_stages() {
-  static int st = -1;
-  if (st < 0) {
-    const char* e = getenv("DDL_WGRAD_STAGES");
-    st = e ? atoi(e) : 0;  // 0: per-operand-mode default (launch_tile)
-    if (st != 0 && st != 1 && st != 3 && st != 4) st = 0;
-  }
+  static const int st = stages_env("DDL_WGRAD_STAGES");
+  return st;
+}
+// the same for the gathered fp32 kernels only (conv weight gradients, split-K small-grid forward)
+inline int gather_stages() {
+  static const int st = stages_env("DDL_GATHER_STAGES");
   return st;
 }
 
@@ -709,10 +714,14 @@ inline int launch_tile(const GemmParams& p, hipStream_t s) {
   const dim3 grid(tiles, splits > 0 ? splits : 1);
   const int dm = gemm_dma_mode();
   if constexpr (EPI == EPI_F32 || EPI == EPI_F32_ATOMIC) {
-    // default: the 3-slot ring for plain (1x1 / Linear) weight gradients, measured 10-25 % faster on
-    // the ResNet-50 1x1 layers; the gathered (3x3 / strided) ones stay single-stage (ring 30 % slower)
-    constexpr bool plain = AMODE == OP_RC && BMODE == OP_RC;
-    const int st = one_stage ? 1 : (wgrad_stages() ? wgrad_stages() : (plain ? 3 : 1));
+    // default: the 3-slot ring for plain (1x1 / Linear) weight gradients on 64x128 / 128x64 tiles
+    // (72 KB: still 2 workgroups per CU), measured 10-25 % faster on the ResNet-50 1x1 layers; not on
+    // 128x128 tiles (96 KB -> 1 workgroup per CU: BERT-base 664K -> 630K tokens/s) nor on the
+    // gathered (3x3 / strided) weight gradients (ring 30 % slower there)
+    constexpr bool plain = AMODE == OP_RC && BMODE == OP_RC && BM * BN < 128 * 128;
+    const int st = one_stage ? 1
+                             : (wgrad_stages() ? wgrad_stages()
+                                               : (plain ? 3 : (gather_stages() ? gather_stages() : 1)));
     if (dm == 1 && st == 3) return launch_ring<BM, BN, AMODE, BMODE, EPI, 3>(grid, p, s);
     if (dm == 1 && st == 4) return launch_ring<BM, BN, AMODE, BMODE, EPI, 4>(grid, p, s);
   }

@@ -104,6 +104,76 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const uint4* __restrict__
   col_reduce_store(acc, g, ws, C);
 }
 
+// Split-K bf16 finalize: y = bf16(ws + bias) (ReLU), plus per-column statistics of the ROUNDED
+// output accumulated into the [kStatShards][2][C] workspace of the GEMM epilogue (shard =
+// block % kStatShards).  Convolutions whose output tiles cannot fill the chip (VGG / ResNet layers
+// at 2x2-4x4 spatial) run their K loop split over workgroups into an fp32 workspace; this pass
+// completes them with the epilogue the un-split GEMM would have applied.
+__global__ __launch_bounds__(256) void splitk_finalize_kernel(const float4* __restrict__ ws, uint4* __restrict__ y,
+                                                              const float* __restrict__ bias, float* stats, long M,
+                                                              int C, int relu) {
+  ColGeom g(C);
+  float acc[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  if (g.active) {
+    float b[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) b[i] = bias ? bias[g.cv * 8 + i] : 0.f;
+    const long step = (long)gridDim.x * g.RT;
+    for (long r = (long)blockIdx.x * g.RT + g.rt; r < M; r += step) {
+      const long idx = r * g.CV + g.cv;
+      const float4 u = ws[2 * idx], v = ws[2 * idx + 1];
+      float f[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        f[i] += b[i];
+        if (relu) f[i] = fmaxf(f[i], 0.f);
+      }
+      const uint4 o = pack8(f);
+      y[idx] = o;
+      if (stats) {
+        float q[8];
+        unpack8(o, q);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          acc[i] += q[i];
+          acc[8 + i] += q[i] * q[i];
+        }
+      }
+    }
+  }
+  if (!stats) return;
+  __shared__ float red[256 * 17];
+  if (g.RT > 1) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) red[threadIdx.x * 17 + i] = acc[i];
+    __syncthreads();
+    if (g.rt == 0 && g.active)
+      for (int t = 1; t < g.RT; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[i] += red[(t * g.CT + g.ct) * 17 + i];
+  }
+  if (g.rt == 0 && g.active) {
+    float* st = stats + (long)(blockIdx.x % kBnShards) * 2 * C + g.cv * 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      atomicAdd(st + i, acc[i]);
+      atomicAdd(st + C + i, acc[8 + i]);
+    }
+  }
+}
+
+int splitk_finalize(const float* ws, void* y, const float* bias, float* stats, long M, int C, int relu, hipStream_t s) {
+  const int CV = C >> 3, CT = CV < 256 ? CV : 256, RT = 256 / CT;
+  const int gy = (CV + CT - 1) / CT;
+  long gx = (M + 4 * RT - 1) / (4 * RT);  // >= 4 rows per lane
+  if (gx > 1024) gx = 1024;
+  hipLaunchKernelGGL(splitk_finalize_kernel, dim3((unsigned)(gx > 0 ? gx : 1), (unsigned)gy), dim3(256), 0, s,
+                     (const float4*)ws, (uint4*)y, bias, stats, M, C, relu);
+  return (int)hipGetLastError();
+}
+
 // partial rows (= grid.x) of a column reduction: >= 16 rows per lane, <= kMaxPartials rows
 static dim3 col_grid(long M, int C) {
   const int CV = C >> 3, CT = CV < 256 ? CV : 256, RT = 256 / CT;

@@ -37,6 +37,17 @@ void bn_stats_(const at::Tensor& x, const at::Tensor& ws, int64_t C) {
   HIP_OK(bn_stats(x.data_ptr(), ws.data_ptr<float>(), x.numel() / C, (int)C, cur_stream()));
 }
 
+void splitk_finalize_(const at::Tensor& ws, const at::Tensor& y, int64_t C, c10::optional<at::Tensor> bias, bool relu,
+                      c10::optional<at::Tensor> stats) {
+  GPU(ws); F32(ws); BF16(y);
+  CK(C % 8 == 0 && ws.numel() % C == 0 && y.numel() == ws.numel() && y.is_contiguous(), "splitk_finalize: shapes");
+  if (bias) { F32(*bias); CK(bias->numel() == C, "splitk_finalize: bias [C]"); }
+  if (stats) { F32(*stats); CK(stats->numel() == (int64_t)kBnShards * 2 * C, "splitk_finalize: stats [32, 2, C]"); }
+  at::DeviceGuard g(ws.device());
+  HIP_OK(splitk_finalize(ws.data_ptr<float>(), y.data_ptr(), optr<const float>(bias), optr<float>(stats), ws.numel() / C,
+                         (int)C, relu ? 1 : 0, cur_stream()));
+}
+
 int64_t bn_partial_rows_(int64_t M, int64_t C) { return bn_partial_rows(M, (int)C); }
 
 // S (partial rows) = ws.numel() / (2C)
@@ -359,6 +370,7 @@ void sumsq_(const at::Tensor& x, const at::Tensor& out) {
 void register_ops(py::module& m) {
   m.attr("BN_SHARDS") = (int)kBnShards;
   m.def("bn_stats", &bn_stats_);
+  m.def("splitk_finalize", &splitk_finalize_);
   m.def("bn_partial_rows", &bn_partial_rows_);
   m.def("bn_finalize", &bn_finalize_);
   m.def("bn_apply", &bn_apply_, py::arg("x"), py::arg("scale"), py::arg("shift"), py::arg("resid"), py::arg("y"),

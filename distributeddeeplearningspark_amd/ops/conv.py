@@ -124,9 +124,33 @@ def halo3_ok(g: ConvGeometry) -> bool:
     return False
 
 
+_SPLITK_FWD = _os.environ.get("DDL_CONV_SPLITK", "1") != "0"
+_SPLITK_MAX_TILES = int(_os.environ.get("DDL_CONV_SPLITK_TILES", "512"))
+
+
+def splitk_fwd_ok(g: ConvGeometry) -> bool:
+    """Gathered convolutions with few output tiles (<= 512 64x64 tiles: VGG's 2x2 / 4x4 layers,
+    ResNet-50 at 7x7 with small batches) and a long K loop: one workgroup per output tile would
+    walk taps x channels alone (measured 77 us for VGG-16's 512-channel 2x2 layers on 88
+    workgroups), so the K loop is split over workgroups into an fp32 workspace and a finalize pass
+    adds bias / ReLU / statistics."""
+    if not (_SPLITK_FWD and g.implicit_fwd and g.T * g.Ci >= 1024 and g.Co % 8 == 0):
+        return False
+    return math.ceil(g.M / 64) * math.ceil(g.Co / 64) <= _SPLITK_MAX_TILES
+
+
 def conv_fwd_native(x, w, g: ConvGeometry, bias=None, relu=False, stats=None):
     y = torch.empty((g.N, g.Ho, g.Wo, g.Co), dtype=torch.bfloat16, device=x.device)
     y2 = y.view(g.M, g.Co)
+    if splitk_fwd_ok(g):
+        ws = torch.zeros((g.M, g.Co), dtype=torch.float32, device=x.device)
+        K = g.T * g.Ci
+        tiles = math.ceil(g.M / 64) * math.ceil(g.Co / 64)
+        splits = max(2, min(math.ceil(4 * 256 / tiles), K // 512))  # ~4 workgroups per CU, >= 8 K-tiles each
+        G.gemm(x, w, ws, g.M, g.Co, K, G.KC_GATHER, G.KC, 0, K, g.Co, G.EPI_F32, geom=g.fwd_geom, tile=3,
+               k_split=math.ceil(K / splits / 64) * 64)
+        C().splitk_finalize(ws, y2, g.Co, bias, bool(relu), stats)
+        return y
     if halo3_ok(g):
         G.gemm(x, w, y2, g.M, g.Co, g.T * g.Ci, G.KC_GATHER, G.KC, 0, g.T * g.Ci, g.Co, G.EPI_BF16, bias=bias,
                relu=relu, geom=g.fwd_geom, stats=stats, tile=G.TILE_CONV3)

@@ -114,6 +114,8 @@ CONV_CASES = [
     (4, 28, 28, 1, 32, 3, 1, 0),   # MNIST conv1
     (4, 26, 26, 32, 32, 3, 1, 0),  # MNIST conv2 (im2col fwd / implicit-less dgrad)
     (2, 9, 9, 128, 128, 3, 1, 1),
+    (4, 4, 4, 256, 128, 3, 1, 1),  # few output tiles: split-K forward (fp32 workspace + finalize)
+    (8, 2, 2, 512, 512, 3, 1, 1),  # VGG-16's 2x2 layers
 ]
 
 
@@ -142,6 +144,29 @@ def test_conv_fwd_bwd(case):
     close(xg.grad, xr.grad.permute(0, 2, 3, 1), what=f"conv dgrad {case}")
     close(gw, wr.grad.permute(0, 2, 3, 1), rtol=1e-2, atol=1e-2, what=f"conv wgrad {case}")
     close(gb, br.grad, rtol=1e-2, atol=1e-2, what=f"conv bgrad {case}")
+
+
+@pytest.mark.parametrize("relu", [False, True])
+def test_conv_splitk_forward_stats(relu):
+    """Split-K forward of a small-grid conv: bias, ReLU and the fused per-channel statistics of the
+    rounded bf16 output ([32, 2, C] sharded sums, as the GEMM epilogue writes them)."""
+    from distributeddeeplearningspark_amd.ops import conv as CV
+
+    N, H, Ci, Co = 16, 4, 512, 256
+    g = CV.geometry(N, H, H, Ci, Co, 3, 3, (1, 1), (1, 1), (1, 1))
+    assert CV.splitk_fwd_ok(g)
+    x = rnd(N, H, H, Ci, seed=30)
+    w = rnd(Co, 3, 3, Ci, scale=1.0 / math.sqrt(9 * Ci), seed=31)
+    b = torch.randn(Co, device=DEV) * 0.1
+    st = torch.zeros(32, 2, Co, device=DEV)
+    y = CV.conv_fwd_native(x, w, g, bias=b, relu=relu, stats=st)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b, 1, 1).permute(0, 2, 3, 1)
+    if relu:
+        ref = torch.relu(ref)
+    close(y, ref, what="split-K conv fwd")
+    o = y.float().reshape(-1, Co)
+    close(st.sum(0)[0], o.sum(0), rtol=1e-3, atol=1e-2, what="split-K stats sum")
+    close(st.sum(0)[1], (o * o).sum(0), rtol=1e-3, atol=1e-2, what="split-K stats sumsq")
 
 
 def test_conv_relu_fused():
