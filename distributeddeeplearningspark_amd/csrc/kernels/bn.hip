@@ -7,6 +7,7 @@
 // All sweeps move 16 B per lane (8 bf16) — these kernels are HBM-bound by design.
 #include "ddl_common.h"
 #include "ddl_ops.h"
+#include <stdlib.h>
 
 namespace ddl {
 
@@ -179,7 +180,12 @@ static dim3 col_grid(long M, int C) {
   const int CV = C >> 3, CT = CV < 256 ? CV : 256, RT = 256 / CT;
   const int gy = (CV + CT - 1) / CT;
   long gx = M / (16L * RT);
-  if (gx > kMaxPartials) gx = kMaxPartials;
+  static const int cap = [] {  // DDL_BN_PARTIALS: experiments (<= kMaxPartials * 8)
+    const char* e = getenv("DDL_BN_PARTIALS");
+    const int v = e ? atoi(e) : kMaxPartials;
+    return v >= 16 && v <= 8 * kMaxPartials ? v : kMaxPartials;
+  }();
+  if (gx > cap) gx = cap;
   if (gx < 1) gx = 1;
   return dim3((unsigned)gx, (unsigned)gy);
 }
@@ -273,20 +279,22 @@ __device__ __forceinline__ void load8f(const float* p, float* f) {
   f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
 }
 
-// ReLU bit mask of a residual BN (bn_apply output, mode-3 backward input).  The 64 lanes of a
-// wave always hold 64 consecutive, 64-aligned vector indices (C a power of two: ColGeom maps
-// lane -> (row, 8-channel vector) in row-major order), so the mask of one wave is 8 ballots:
-// word [idx / 64][i] bit (idx % 64) = element i of vector idx.  Written as 64 B by 8 lanes and
-// read back with scalar loads — byte-per-lane stores cost as much as a 16-B store each.
-__device__ __forceinline__ void store_mask_bits(uint8_t* __restrict__ mask, long idx, uint32_t bits) {
-  const int lane = threadIdx.x & 63;
-  uint64_t w = 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const uint64_t b = __ballot((bits >> i) & 1u);
-    if (lane == i) w = b;
+// ReLU bit mask of a BN with a residual add: one byte per 16-B vector, bit i = channel 8 v + i
+// positive, so the backward sweeps load each lane's byte with its data vectors (a byte load in flight
+// with them, instead of the dependent scalar loads of a ballot-word layout: bn_bwd_reduce mode 3
+// ran at 4.3 TB/s vs 5.5 for mode 2).  The store packs 4 lanes' bytes into one dword (the lanes
+// of a wave hold consecutive vectors when CT * RT == 256); otherwise one byte per lane.
+__device__ __forceinline__ void store_mask_bits(uint8_t* __restrict__ mask, long idx, uint32_t bits, bool packed) {
+  if (packed) {
+    // DPP row_shl:n (lane i reads lane i + n inside its 16-lane row): VALU moves, no LDS crossbar
+    const int b = (int)(bits & 0xffu);
+    const uint32_t w = (uint32_t)b | ((uint32_t)__builtin_amdgcn_update_dpp(0, b, 0x101, 0xf, 0xf, false) << 8) |
+                       ((uint32_t)__builtin_amdgcn_update_dpp(0, b, 0x102, 0xf, 0xf, false) << 16) |
+                       ((uint32_t)__builtin_amdgcn_update_dpp(0, b, 0x103, 0xf, 0xf, false) << 24);
+    if ((threadIdx.x & 3) == 0) *reinterpret_cast<uint32_t*>(mask + idx) = w;
+  } else {
+    mask[idx] = (uint8_t)bits;
   }
-  if (lane < 8) reinterpret_cast<uint64_t*>(mask)[(idx >> 6) * 8 + lane] = w;
 }
 
 // Streaming sweeps use the column-fixed mapping of ColGeom: a lane keeps ONE 8-channel
@@ -336,7 +344,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint4* __restrict__
         f[i] = o;
       }
       y[h ? i1 : i0] = pack8(f);
-      if (mask) store_mask_bits(mask, h ? i1 : i0, bits);
+      if (mask) store_mask_bits(mask, h ? i1 : i0, bits, g.CT * g.RT == 256);
     }
   }
 }
@@ -362,14 +370,15 @@ int bn_apply(const void* x, const float* scale, const float* shift, const void* 
 // forward computed the same fmaf on the same values); mode 3 reads the bit mask the forward
 // apply stored (one byte per 8 channels: 1/16 of the bytes of y) — for BNs with a residual
 // add, whose output cannot be recomputed from x alone.
+// mode 3's mask byte of vector idx (loaded by the caller with its data vectors)
+__device__ __forceinline__ uint32_t mask_byte(const uint4* __restrict__ y, long idx, int mode) {
+  return mode == 3 ? (uint32_t)reinterpret_cast<const uint8_t*>(y)[idx] : 0u;
+}
 __device__ __forceinline__ void relu_mask(float* d, const float* xv, const uint4* __restrict__ y, long idx,
-                                          const float* sc, const float* sh, int mode) {
+                                          const float* sc, const float* sh, int mode, uint32_t mb = 0) {
   if (mode == 3) {
-    const long chunk = __builtin_amdgcn_readfirstlane((int)(idx >> 6));  // wave-uniform: scalar loads
-    const uint64_t* __restrict__ mw = reinterpret_cast<const uint64_t*>(y) + chunk * 8;
-    const int sh6 = (int)(idx & 63);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) d[i] = ((mw[i] >> sh6) & 1ull) ? d[i] : 0.f;
+    for (int i = 0; i < 8; ++i) d[i] = ((mb >> i) & 1u) ? d[i] : 0.f;
   } else if (mode == 1) {
     float yv[8];
     unpack8(y[idx], yv);
@@ -403,18 +412,20 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint4* __restr
     for (; r + 3 * step < M; r += 4 * step) {  // four rows of dy and x in flight per lane
       long ix[4];
       uint4 dd[4], xx[4];
+      uint32_t mb[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         ix[q] = (r + q * step) * g.CV + g.cv;
         dd[q] = dy[ix[q]];
         xx[q] = x[ix[q]];
+        mb[q] = mask_byte(y, ix[q], mode);
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         float d[8], xv[8];
         unpack8(dd[q], d);
         unpack8(xx[q], xv);
-        relu_mask(d, xv, y, ix[q], sc, sh, mode);
+        relu_mask(d, xv, y, ix[q], sc, sh, mode, mb[q]);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           acc[i] += d[i];
@@ -427,7 +438,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint4* __restr
       float d[8], xv[8];
       unpack8(dy[idx], d);
       unpack8(x[idx], xv);
-      relu_mask(d, xv, y, idx, sc, sh, mode);
+      relu_mask(d, xv, y, idx, sc, sh, mode, mask_byte(y, idx, mode));
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         acc[i] += d[i];
@@ -500,6 +511,7 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const uint4* __restrict_
     const long i0 = r * g.CV + g.cv, i1 = (r + step) * g.CV + g.cv;
     const uint4 d0 = dy[i0], x0 = x[i0];
     const uint4 d1 = two ? dy[i1] : d0, x1 = two ? x[i1] : x0;
+    const uint32_t m0 = mask_byte(y, i0, mode), m1 = two ? mask_byte(y, i1, mode) : m0;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       if (h == 1 && !two) break;
@@ -507,7 +519,7 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const uint4* __restrict_
       float d[8], xv[8], o[8];
       unpack8(h ? d1 : d0, d);
       unpack8(h ? x1 : x0, xv);
-      relu_mask(d, xv, y, idx, sc, sh, mode);
+      relu_mask(d, xv, y, idx, sc, sh, mode, h ? m1 : m0);
       if (dres) dres[idx] = pack8(d);
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] = A[i] * d[i] + B[i] * xv[i] + K[i];

@@ -78,9 +78,8 @@ void bn_apply_(const at::Tensor& x, const at::Tensor& scale, const at::Tensor& s
        "bn_apply: res_scale/res_shift [C]");
   }
   if (mask) {
-    CK(mask->scalar_type() == at::kByte && mask->is_contiguous() && mask->numel() >= (x.numel() / 8 + 63) / 64 * 64,
-       "bn_apply: mask must be uint8 [ceil(numel / 512) * 64]");
-    CK((C & (C - 1)) == 0, "bn_apply: the bit mask needs a power-of-two channel count");
+    CK(mask->scalar_type() == at::kByte && mask->is_contiguous() && mask->numel() >= (x.numel() / 8 + 3) / 4 * 4,
+       "bn_apply: mask must be uint8 [numel / 8 rounded up to 4] (one byte per 8 channels)");
   }
   at::DeviceGuard g(x.device());
   HIP_OK(bn_apply(x.data_ptr(), scale.data_ptr<float>(), shift.data_ptr<float>(), optr<const void>(resid), y.data_ptr(),
@@ -95,8 +94,8 @@ void bn_bwd_reduce_(const at::Tensor& dy, const at::Tensor& x, c10::optional<at:
   GPU(dy); BF16(dy); BF16(x); F32(mean); F32(ws);
   CK(dy.numel() == x.numel() && x.numel() % C == 0 && C % 8 == 0, "bn_bwd_reduce: shapes");
   if (mode == 1) { CK(y.has_value(), "mode 1 needs y"); BF16(*y); CK(y->numel() == x.numel(), "bn_bwd_reduce: y shape"); }
-  if (mode == 3) CK(y.has_value() && y->scalar_type() == at::kByte && y->numel() >= (x.numel() / 8 + 63) / 64 * 64 &&
-                    (C & (C - 1)) == 0, "mode 3 needs the uint8 bit mask of bn_apply");
+  if (mode == 3) CK(y.has_value() && y->scalar_type() == at::kByte && y->numel() >= x.numel() / 8,
+                    "mode 3 needs the uint8 bit mask of bn_apply");
   CK(mode >= 0 && mode <= 3, "bn_bwd_reduce: mode");
   if (mode == 2) { CK(scale.has_value() && shift.has_value(), "mode 2 needs scale/shift"); F32(*scale); F32(*shift); }
   CK(ws.numel() >= (int64_t)bn_partial_rows(x.numel() / C, (int)C) * 2 * C, "bn_bwd_reduce: workspace too small");
@@ -125,8 +124,8 @@ void bn_bwd_dx_(const at::Tensor& dy, const at::Tensor& x, c10::optional<at::Ten
   CK(dy.numel() == x.numel() && dx.numel() == x.numel() && x.numel() % C == 0 && C % 8 == 0, "bn_bwd_dx: shapes");
   CK(coef.numel() >= 3 * C, "bn_bwd_dx: coef size");
   if (mode == 1) { CK(y.has_value(), "mode 1 needs y"); BF16(*y); CK(y->numel() == x.numel(), "bn_bwd_dx: y shape"); }
-  if (mode == 3) CK(y.has_value() && y->scalar_type() == at::kByte && y->numel() >= (x.numel() / 8 + 63) / 64 * 64 &&
-                    (C & (C - 1)) == 0, "mode 3 needs the uint8 bit mask of bn_apply");
+  if (mode == 3) CK(y.has_value() && y->scalar_type() == at::kByte && y->numel() >= x.numel() / 8,
+                    "mode 3 needs the uint8 bit mask of bn_apply");
   CK(mode >= 0 && mode <= 3, "bn_bwd_dx: mode");
   if (mode == 2) { CK(scale.has_value() && shift.has_value(), "mode 2 needs scale/shift"); F32(*scale); F32(*shift); }
   if (dres) { BF16(*dres); CK(dres->numel() == x.numel(), "bn_bwd_dx: dres shape"); }

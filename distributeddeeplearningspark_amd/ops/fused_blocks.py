@@ -66,9 +66,8 @@ def convbn_forward(unit, x, resid=None, relu=True, apply=True, res_affine=None):
     st.g, st.yc = g, yc
     # ReLU after a residual add: the backward mask cannot be recomputed from yc alone, so the
     # apply pass stores it as bits (mode 3) instead of the backward re-reading the bf16 output
-    Co = yc.shape[-1]
-    bits = relu and resid is not None and Co & (Co - 1) == 0
-    st.mask = torch.empty(-(-yc.numel() // 512) * 64, dtype=torch.uint8, device=yc.device) if bits else None
+    bits = relu and resid is not None
+    st.mask = torch.empty(-(-yc.numel() // 32) * 4, dtype=torch.uint8, device=yc.device) if bits else None
     st.y, st.mean, st.invstd, st.scale, st.shift = _bn_forward(bn, yc, stats, resid, relu, True, st.mask, apply,
                                                                res_affine)
     st.mode = 0 if not relu else (2 if resid is None else (3 if bits else 1))
