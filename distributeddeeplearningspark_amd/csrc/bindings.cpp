@@ -55,7 +55,8 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
           int64_t k_split, double alpha, double beta, c10::optional<at::Tensor> bias,
           c10::optional<at::Tensor> resid, int64_t ldr, int64_t relu, c10::optional<py::dict> geom,
           c10::optional<py::dict> outmap, int64_t b_kdiv, int64_t b_tap_stride,
-          c10::optional<at::Tensor> stats, c10::optional<at::Tensor> aux, double drop_p, int64_t drop_seed) {
+          c10::optional<at::Tensor> stats, c10::optional<at::Tensor> aux, double drop_p, int64_t drop_seed,
+          c10::optional<at::Tensor> resid_mask) {
   CHECK_CUDA(a);
   CHECK_CUDA(b);
   CHECK_CUDA(c);
@@ -134,6 +135,13 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
     CHECK_BF16(*resid);
     p.resid = resid->data_ptr();
   }
+  if (resid_mask) {
+    TORCH_CHECK(resid.has_value() && epi == EPI_BF16 && !outmap.has_value(), "gemm: resid_mask needs a residual (bf16, no outmap)");
+    TORCH_CHECK(resid_mask->scalar_type() == at::kByte && resid_mask->is_contiguous() && ldr % 8 == 0 &&
+                    resid_mask->numel() >= ((M - 1) * ldr + N + 7) / 8,
+                "gemm: resid_mask must be uint8 [M * ldr / 8] with ldr % 8 == 0");
+    p.resid_mask = resid_mask->data_ptr<uint8_t>();
+  }
   if (geom) {
     fill_geom(p.g, *geom);
     if (a_mode == OP_KC_GATHER) TORCH_CHECK(p.g.tap_c % 64 == 0 && K == (int64_t)p.g.ntaps * p.g.tap_c, "conv A gather: tap_c % 64 and K = taps*C");
@@ -188,7 +196,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("beta") = 0.0, py::arg("bias") = py::none(), py::arg("resid") = py::none(), py::arg("ldr") = 0,
         py::arg("relu") = false, py::arg("geom") = py::none(), py::arg("outmap") = py::none(),
         py::arg("b_kdiv") = 0, py::arg("b_tap_stride") = 0, py::arg("stats") = py::none(),
-        py::arg("aux") = py::none(), py::arg("drop_p") = 0.0, py::arg("drop_seed") = 0);
+        py::arg("aux") = py::none(), py::arg("drop_p") = 0.0, py::arg("drop_seed") = 0,
+        py::arg("resid_mask") = py::none());
   m.attr("ACT_NONE") = (int)ACT_NONE;
   m.attr("ACT_RELU") = (int)ACT_RELU;
   m.attr("ACT_GELU") = (int)ACT_GELU;

@@ -71,6 +71,10 @@ struct GemmParams {
   OutMap om;
   const float* bias;
   const void* resid; long ldr;
+  // optional ReLU bit mask of the residual (bn.hip mode-3 layout: byte (m*ldr + n) / 8, bit n % 8):
+  // resid is added only where the bit is set — the masked gradient of a residual BN is formed in
+  // the consumer's epilogue instead of being written out by the BN backward sweep
+  const uint8_t* resid_mask;
   float alpha, beta;
   // bf16 epilogue activation (field name kept from the first version):
   //   ACT_NONE, ACT_RELU (after the residual add), ACT_GELU (aux <- pre-activation),

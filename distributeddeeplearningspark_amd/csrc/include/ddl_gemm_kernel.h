@@ -46,6 +46,19 @@ __device__ __forceinline__ int rc_swz(int k) {
 
 __device__ __forceinline__ uint4 ldg16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
 
+// KC_GATHER8 looks a tap up per 16-B vector and K-tile with a per-LANE tap index; indexing the
+// kernel-argument tap table that way compiles to two dependent byte loads from the kernarg segment
+// plus an s_waitcnt vmcnt(0) per vector — which also drains every LDS-DMA in flight (the ResNet stem
+// ran at 0.38 ms).  Such kernels copy the table once into the first bytes of their LDS:
+// entry t = (dw[t] << 16) | (dh[t] & 0xffff).
+template <int AMODE>
+constexpr int tap_table_bytes() { return AMODE == OP_KC_GATHER8 ? 4 * kMaxTaps : 0; }
+
+__device__ __forceinline__ void load_tap_table(int* tab, const ConvGeom& g) {
+  if ((int)threadIdx.x < g.ntaps) tab[threadIdx.x] = ((int)g.dw[threadIdx.x] << 16) | ((int)g.dh[threadIdx.x] & 0xffff);
+  __syncthreads();
+}
+
 
 // ----------------------------------------------------------------------------------------
 // Operand loaders. R = tile extent along the operand's row dimension (BM for A, BN for B).
@@ -70,7 +83,9 @@ struct Operand {
   static constexpr bool RCG = (MODE == OP_RC_GATHER || MODE == OP_RC_GATHER8);
   int qn[RCG ? V : 1], qi[RCG ? V : 1], qj[RCG ? V : 1];
   int tap8[MODE == OP_RC_GATHER8 ? V : 1], ch8[MODE == OP_RC_GATHER8 ? V : 1];
+  int dh8[MODE == OP_RC_GATHER8 ? V : 1], dw8[MODE == OP_RC_GATHER8 ? V : 1];  // that tap's offsets
   int di, dj;
+  const DDL_LDS int* tt = nullptr;  // KC_GATHER8: the LDS copy of the tap table (load_tap_table)
 
   __device__ __forceinline__ void init(const void* p, long ld_, int rows_, int r0_, int K_, const ConvGeom& g,
                                        int k0 = 0) {
@@ -95,6 +110,8 @@ struct Operand {
           const int r = r0 + rc * 8;
           tap8[v] = r < rows ? r / g.tap_c : 0;
           ch8[v] = r - tap8[v] * g.tap_c;
+          dh8[v] = g.dh[tap8[v]];
+          dw8[v] = g.dw[tap8[v]];
         }
       }
     }
@@ -137,7 +154,8 @@ struct Operand {
         bool ok = rvalid[v] && k < K;
         const int t = ok ? (g.tap_shift >= 0 ? k >> g.tap_shift : k / g.tap_c) : 0;
         const int c = k - t * g.tap_c;
-        const int ih = hbase[v] + g.dh[t], iw = wbase[v] + g.dw[t];
+        const int e = tt[t];
+        const int ih = hbase[v] + (int)(short)(e & 0xffff), iw = wbase[v] + (e >> 16);
         ok = ok && (unsigned)ih < (unsigned)g.hi && (unsigned)iw < (unsigned)g.wi;
         return ok ? ptr + ((long)(pixbase[v] + ih * g.wi + iw)) * g.c + c : nullptr;
       }
@@ -151,17 +169,19 @@ struct Operand {
       } else if constexpr (MODE == OP_RC_GATHER8) {
         // (rc is the SWZ-permuted column chunk; the (tap, channel) of it was fixed in init for the
         // swizzled order; the register path (SWZ = false) recomputes it)
-        int t = tap8[v], c = ch8[v];
+        int c = ch8[v], dhv = dh8[v], dwv = dw8[v];
         bool ok = k < K;
         if constexpr (!SWZ) {
           const int r = r0 + rc * 8;
           ok = ok && r < rows;
-          t = r < rows ? r / g.tap_c : 0;
+          const int t = r < rows ? r / g.tap_c : 0;
           c = r - t * g.tap_c;
+          dhv = g.dh[t];
+          dwv = g.dw[t];
         } else {
           ok = ok && r0 + rc * 8 < rows;
         }
-        const int ih = qi[v] * g.sh + g.dh[t], iw = qj[v] * g.sw + g.dw[t];
+        const int ih = qi[v] * g.sh + dhv, iw = qj[v] * g.sw + dwv;
         ok = ok && (unsigned)ih < (unsigned)g.hi && (unsigned)iw < (unsigned)g.wi;
         return ok ? ptr + ((long)((qn[v] * g.hi + ih) * g.wi + iw)) * g.c + c : nullptr;
       } else if constexpr (MODE == OP_RC_GATHER) {
@@ -351,17 +371,25 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
         }
         if (!LITE && p.resid) {
           const bf16_t* r = reinterpret_cast<const bf16_t*>(p.resid) + (long)m * p.ldr + n;
+          float rv4[4];
           if (full) {
             const uint2 rv = *reinterpret_cast<const uint2*>(r);
-            v[0] += __uint_as_float(rv.x << 16);
-            v[1] += __uint_as_float(rv.x & 0xffff0000u);
-            v[2] += __uint_as_float(rv.y << 16);
-            v[3] += __uint_as_float(rv.y & 0xffff0000u);
+            rv4[0] = __uint_as_float(rv.x << 16);
+            rv4[1] = __uint_as_float(rv.x & 0xffff0000u);
+            rv4[2] = __uint_as_float(rv.y << 16);
+            rv4[3] = __uint_as_float(rv.y & 0xffff0000u);
           } else {
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-              if (n + e < p.N) v[e] += bf2f(r[e]);
+            for (int e = 0; e < 4; ++e) rv4[e] = (n + e < p.N) ? bf2f(r[e]) : 0.f;
           }
+          if (p.resid_mask) {  // bits n .. n+3 of the row's mask (n % 4 == 0: one byte)
+            const long bit = (long)m * p.ldr + n;
+            const uint32_t mb = (uint32_t)p.resid_mask[bit >> 3] >> (bit & 7);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) rv4[e] = ((mb >> e) & 1u) ? rv4[e] : 0.f;
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += rv4[e];
         }
         if (p.relu == ACT_RELU) {
 #pragma unroll
@@ -452,7 +480,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams
   constexpr int WTM = BM / 2, WTN = BN / 2;
   constexpr int RM = WTM / 16, RN = WTN / 16;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  constexpr int TAPB = tap_table_bytes<AMODE>();
+  char* smem = smem_raw + TAPB;
   const bool one_stage = p.k_split <= BK;  // must match launch_tile's LDS allocation
   char* lds_a0 = smem;
   char* lds_a1 = smem + A_BYTES;
@@ -474,6 +504,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams
 
   Operand<BM, AMODE> A;
   Operand<BN, BMODE> B;
+  if constexpr (TAPB > 0) {
+    load_tap_table(reinterpret_cast<int*>(smem_raw), p.g);
+    A.tt = (const DDL_LDS int*)(smem_raw);
+  }
   A.init(p.a, p.lda, p.M, m0, p.K, p.g, kbeg);
   B.init(p.b, p.ldb, p.N, n0, p.K, p.g, kbeg);
 
@@ -538,7 +572,9 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
   constexpr int RM = WTM / 16, RN = WTN / 16;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int VA = BM / 32, VB = BN / 32;  // DMA wave-instructions per operand per K-tile
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  constexpr int TAPB = tap_table_bytes<AMODE>();
+  char* smem = smem_raw + TAPB;
 
   const int tiles_n = (p.N + BN - 1) / BN;
   int bid, split;
@@ -555,6 +591,10 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
 
   Operand<BM, AMODE> A;
   Operand<BN, BMODE> B;
+  if constexpr (TAPB > 0) {
+    load_tap_table(reinterpret_cast<int*>(smem_raw), p.g);
+    A.tt = (const DDL_LDS int*)(smem_raw);
+  }
   A.init(p.a, p.lda, p.M, m0, p.K, p.g, kbeg);
   B.init(p.b, p.ldb, p.N, n0, p.K, p.g, kbeg);
 
@@ -695,7 +735,7 @@ inline int gather_stages() {
 
 template <int BM, int BN, int AMODE, int BMODE, int EPI, int ST>
 inline int launch_ring(const dim3 grid, const GemmParams& p, hipStream_t s) {
-  constexpr int lds = ST * (BM + BN) * BK * 2;
+  constexpr int lds = ST * (BM + BN) * BK * 2 + tap_table_bytes<AMODE>();
   static bool attr = [] {  // dynamic LDS above 64 KB must be allowed explicitly
     return lds <= 65536 || hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_dma_kernel<BM, BN, AMODE, BMODE, EPI, ST>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
@@ -725,13 +765,15 @@ inline int launch_tile(const GemmParams& p, hipStream_t s) {
     if (dm == 1 && st == 3) return launch_ring<BM, BN, AMODE, BMODE, EPI, 3>(grid, p, s);
     if (dm == 1 && st == 4) return launch_ring<BM, BN, AMODE, BMODE, EPI, 4>(grid, p, s);
   }
+  constexpr int TAPB = tap_table_bytes<AMODE>();
   if (dm == 1 || (dm == 2 && one_stage)) {
-    hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, AMODE, BMODE, EPI, 1>), grid, dim3(NTHREADS), (BM + BN) * BK * 2, s, p);
+    hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, AMODE, BMODE, EPI, 1>), grid, dim3(NTHREADS), (BM + BN) * BK * 2 + TAPB,
+                       s, p);
   } else if (dm == 2) {
-    hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, AMODE, BMODE, EPI, 2>), grid, dim3(NTHREADS), 2 * (BM + BN) * BK * 2, s,
-                       p);
+    hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, AMODE, BMODE, EPI, 2>), grid, dim3(NTHREADS),
+                       2 * (BM + BN) * BK * 2 + TAPB, s, p);
   } else {
-    const size_t lds = (one_stage ? 1 : 2) * (BM + BN) * BK * 2;
+    const size_t lds = (one_stage ? 1 : 2) * (BM + BN) * BK * 2 + TAPB;
     hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, AMODE, BMODE, EPI>), grid, dim3(NTHREADS), lds, s, p);
   }
   return (int)hipGetLastError();

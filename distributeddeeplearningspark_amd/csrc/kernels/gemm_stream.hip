@@ -160,14 +160,26 @@ __global__ __launch_bounds__(gst::THREADS, 2) void gemm_stream_kernel(const Gemm
     const int m0 = tile_m0(i);
     // residual rows of this tile, issued ahead of the refill so their wait can be counted past it
     uint2 rres[BM / 16][CF::RN];
+    // residual ReLU mask (p.resid_mask): the 16 * RN columns this lane's row touches are 2 * RN
+    // consecutive mask bytes — one 2/4/8-byte load per row block; all ones when there is no mask
+    uint64_t rmsk[BM / 16];
     if constexpr (RES) {
+      const bool has_mask = p.resid_mask != nullptr;
 #pragma unroll
       for (int mb = 0; mb < BM / 16; ++mb) {
         const int m = min(m0 + 16 * mb + (lane & 15), p.M - 1);
+        const long row = (long)m * p.ldr + n0 + WN * w;
 #pragma unroll
         for (int rn = 0; rn < CF::RN; ++rn)
-          rres[mb][rn] = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(p.resid) + (long)m * p.ldr +
-                                                         n0 + WN * w + 16 * rn + 4 * (lane >> 4));
+          rres[mb][rn] = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(p.resid) + row + 16 * rn +
+                                                         4 * (lane >> 4));
+        rmsk[mb] = ~0ull;
+        if (has_mask) {
+          const uint8_t* mp = p.resid_mask + (row >> 3);
+          if constexpr (CF::RN == 1) rmsk[mb] = *reinterpret_cast<const uint16_t*>(mp);
+          else if constexpr (CF::RN == 2) rmsk[mb] = *reinterpret_cast<const uint32_t*>(mp);
+          else rmsk[mb] = *reinterpret_cast<const uint64_t*>(mp);
+        }
       }
     }
     const int ahead = i + CF::NBUF - 1;
@@ -204,10 +216,11 @@ __global__ __launch_bounds__(gst::THREADS, 2) void gemm_stream_kernel(const Gemm
         for (int e = 0; e < 4; ++e) v[e] = fmaf(acc[mb][rn][e], p.alpha, bias_r[rn][e]);
         if constexpr (RES) {
           const uint2 rv = rres[mb][rn];
-          v[0] += __uint_as_float(rv.x << 16);
-          v[1] += __uint_as_float(rv.x & 0xffff0000u);
-          v[2] += __uint_as_float(rv.y << 16);
-          v[3] += __uint_as_float(rv.y & 0xffff0000u);
+          const uint32_t mk = (uint32_t)(rmsk[mb] >> (16 * rn + 4 * (lane >> 4)));
+          v[0] += (mk & 1u) ? __uint_as_float(rv.x << 16) : 0.f;
+          v[1] += (mk & 2u) ? __uint_as_float(rv.x & 0xffff0000u) : 0.f;
+          v[2] += (mk & 4u) ? __uint_as_float(rv.y << 16) : 0.f;
+          v[3] += (mk & 8u) ? __uint_as_float(rv.y & 0xffff0000u) : 0.f;
         }
         if (p.relu == ACT_RELU) {
 #pragma unroll

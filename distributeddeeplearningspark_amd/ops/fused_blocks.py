@@ -92,14 +92,14 @@ def bn_backward(unit, st, dy, want_dres):
     return dyc, dres
 
 
-def conv_backward(unit, st, dyc, x, need_dx, resid=None):
+def conv_backward(unit, st, dyc, x, need_dx, resid=None, resid_mask=None):
     conv = unit.conv
     CV.conv_wgrad_native(dyc, x, st.g, conv.kernel.grad)
     if conv.grad_hook is not None:
         conv.grad_hook()
     if not need_dx:
         return None
-    return CV.conv_dgrad_native(dyc, conv.kernel.data, st.g, resid=resid)
+    return CV.conv_dgrad_native(dyc, conv.kernel.data, st.g, resid=resid, resid_mask=resid_mask)
 
 
 class _BottleneckFn(torch.autograd.Function):
@@ -125,7 +125,10 @@ class _BottleneckFn(torch.autograd.Function):
         b = ctx.block
         s_down, s1, s2, s3 = ctx.states
         dout = dout.contiguous()
-        d3c, dsc = bn_backward(b.c3, s3, dout, want_dres=True)
+        # identity shortcut: its gradient is dout masked by the block-output ReLU; instead of the BN
+        # backward writing it out, conv1's data-gradient epilogue adds dout under the bit mask
+        masked_sc = s_down is None and s3.mode == 3 and s1.g.is_pointwise
+        d3c, dsc = bn_backward(b.c3, s3, dout, want_dres=not masked_sc)
         d2 = conv_backward(b.c3, s3, d3c, s2.y, True)
         d2c, _ = bn_backward(b.c2, s2, d2, False)
         d1 = conv_backward(b.c2, s2, d2c, s1.y, True)
@@ -134,7 +137,10 @@ class _BottleneckFn(torch.autograd.Function):
             ddc, _ = bn_backward(b.down, s_down, dsc, False)
             dsc = conv_backward(b.down, s_down, ddc, x, ctx.needs_dx)
         # dX = dgrad(conv1) + dShortcut: the residual add rides in the conv1 dgrad epilogue
-        dx = conv_backward(b.c1, s1, d1c, x, ctx.needs_dx, resid=dsc)
+        if masked_sc:
+            dx = conv_backward(b.c1, s1, d1c, x, ctx.needs_dx, resid=dout, resid_mask=s3.mask)
+        else:
+            dx = conv_backward(b.c1, s1, d1c, x, ctx.needs_dx, resid=dsc)
         ctx.states = None
         return dx, None, None
 

@@ -110,7 +110,7 @@ def choose_split(M: int, N: int, K: int, tile: int, allow: bool, rounds: float |
 
 def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, beta=0.0, bias=None, resid=None,
          ldr=0, relu=False, geom=None, outmap=None, b_kdiv=0, b_tap_stride=0, stats=None, tile=None, k_split=None,
-         bn_cap=128, aux=None, drop_p=0.0, drop_seed=0, split_rounds=None):
+         bn_cap=128, aux=None, drop_p=0.0, drop_seed=0, split_rounds=None, resid_mask=None):
     """Raw launcher with automatic tile / split-K choice.
 
     With ``epi == EPI_F32`` and a split-K decomposition the launch switches to the
@@ -133,7 +133,7 @@ def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, bet
             raise ValueError("split-K fp32 gemm supports beta in {0,1} (beta=0 needs a zeroed C)")
         epi = EPI_F32_ATOMIC
     C().gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, tile, k_split, alpha, beta, bias, resid, ldr,
-             int(relu), geom, outmap, b_kdiv, b_tap_stride, stats, aux, float(drop_p), int(drop_seed))
+             int(relu), geom, outmap, b_kdiv, b_tap_stride, stats, aux, float(drop_p), int(drop_seed), resid_mask)
     return c
 
 
@@ -158,10 +158,12 @@ def linear_fwd(x2, w, bias=None, relu=False, out=None, resid=None, stats=None, a
                 drop_seed=drop_seed)
 
 
-def linear_dgrad(dy, w, out=None, resid=None, gelu_pre=None, stats=None):
+def linear_dgrad(dy, w, out=None, resid=None, gelu_pre=None, stats=None, resid_mask=None):
     """dx[M,K] = dy[M,N] @ w[N,K] (* gelu'(gelu_pre)) (+resid) -> bf16 (w read row-contiguous).
 
-    ``stats`` ([32, 2, K] fp32, zeroed): per-column sums / sums of squares of the output."""
+    ``stats`` ([32, 2, K] fp32, zeroed): per-column sums / sums of squares of the output;
+    ``resid_mask``: uint8 ReLU bit mask of ``resid`` (bn.hip mode-3 layout) — only the masked
+    residual is added."""
     M, N = dy.shape
     K = w.shape[1]
     if out is None:
@@ -174,9 +176,9 @@ def linear_dgrad(dy, w, out=None, resid=None, gelu_pre=None, stats=None):
         # of paired transposed LDS reads: the BERT-size data-gradients run ~1.4x faster this way
         wt = transpose(w)
         return gemm(dy, wt, out, M, K, N, KC, KC, dy.stride(0), wt.stride(0), out.stride(0), EPI_BF16, resid=resid,
-                    ldr=ldr, relu=act, aux=gelu_pre, stats=stats)
+                    ldr=ldr, relu=act, aux=gelu_pre, stats=stats, resid_mask=resid_mask)
     return gemm(dy, w, out, M, K, N, KC, RC, dy.stride(0), w.stride(0), out.stride(0), EPI_BF16, resid=resid,
-                ldr=ldr, relu=act, aux=gelu_pre, stats=stats)
+                ldr=ldr, relu=act, aux=gelu_pre, stats=stats, resid_mask=resid_mask)
 
 
 def transpose(w):

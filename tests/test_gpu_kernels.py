@@ -146,6 +146,23 @@ def test_conv_fwd_bwd(case):
     close(gb, br.grad, rtol=1e-2, atol=1e-2, what=f"conv bgrad {case}")
 
 
+@pytest.mark.parametrize("M,N,K", [(20000, 256, 64), (600, 512, 128), (4096, 2048, 512)])
+def test_dgrad_masked_residual(M, N, K):
+    """dx = dy @ w + resid * bit(mask): the identity-shortcut gradient of a ResNet block added
+    under the block-output ReLU mask in the data-gradient epilogue (streaming kernel at large M,
+    the tile kernels otherwise)."""
+    from distributeddeeplearningspark_amd.ops import gemm as G
+
+    dy, w, r = rnd(M, K, seed=40), rnd(K, N, scale=0.1, seed=41), rnd(M, N, seed=42)
+    keep = torch.rand(M, N, device=DEV) > 0.5
+    # bn.hip mode-3 layout: byte e // 8 holds bit e % 8 of flat element e
+    bits = keep.reshape(-1, 8).to(torch.uint8) << torch.arange(8, device=DEV, dtype=torch.uint8)
+    mask = bits.sum(1, dtype=torch.uint8)
+    out = G.linear_dgrad(dy, w, resid=r, resid_mask=mask)
+    ref = dy.float() @ w.float() + r.float() * keep
+    close(out, ref, what=f"masked residual dgrad {M}x{N}x{K}")
+
+
 @pytest.mark.parametrize("relu", [False, True])
 def test_conv_splitk_forward_stats(relu):
     """Split-K forward of a small-grid conv: bias, ReLU and the fused per-channel statistics of the
