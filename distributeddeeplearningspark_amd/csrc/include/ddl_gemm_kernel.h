@@ -46,13 +46,21 @@ __device__ __forceinline__ int rc_swz(int k) {
 
 __device__ __forceinline__ uint4 ldg16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
 
-// KC_GATHER8 looks a tap up per 16-B vector and K-tile with a per-LANE tap index; indexing the
-// kernel-argument tap table that way compiles to two dependent byte loads from the kernarg segment
-// plus an s_waitcnt vmcnt(0) per vector — which also drains every LDS-DMA in flight (the ResNet stem
-// ran at 0.38 ms).  Such kernels copy the table once into the first bytes of their LDS:
+// The gathering operand modes look tap offsets up in the kernel-argument tap table.  gfx950 has no
+// scalar byte loads, so g.dh[t] / g.dw[t] compile to dependent VECTOR byte loads from the kernarg
+// segment (per lane for KC_GATHER8, per K-tile even for a block-uniform t) whose s_waitcnt vmcnt
+// also drains every LDS-DMA in flight: each K-tile paid a kernarg round trip before its DMAs could
+// issue, and a deeper LDS-DMA ring was drained at every refill.  Gathering kernels therefore copy the
+// table once into the first bytes of their LDS (ds_read: counted by lgkmcnt, not vmcnt):
 // entry t = (dw[t] << 16) | (dh[t] & 0xffff).
-template <int AMODE>
-constexpr int tap_table_bytes() { return AMODE == OP_KC_GATHER8 ? 4 * kMaxTaps : 0; }
+template <int AMODE, int BMODE = OP_KC>
+constexpr int tap_table_bytes() {
+  return (AMODE == OP_KC_GATHER8 || AMODE == OP_KC_GATHER || BMODE == OP_RC_GATHER || BMODE == OP_RC_GATHER8)
+             ? 4 * kMaxTaps
+             : 0;
+}
+__device__ __forceinline__ int tap_dh(int e) { return (int)(short)(e & 0xffff); }
+__device__ __forceinline__ int tap_dw(int e) { return e >> 16; }
 
 __device__ __forceinline__ void load_tap_table(int* tab, const ConvGeom& g) {
   if ((int)threadIdx.x < g.ntaps) tab[threadIdx.x] = ((int)g.dw[threadIdx.x] << 16) | ((int)g.dh[threadIdx.x] & 0xffff);
@@ -84,8 +92,9 @@ struct Operand {
   int qn[RCG ? V : 1], qi[RCG ? V : 1], qj[RCG ? V : 1];
   int tap8[MODE == OP_RC_GATHER8 ? V : 1], ch8[MODE == OP_RC_GATHER8 ? V : 1];
   int dh8[MODE == OP_RC_GATHER8 ? V : 1], dw8[MODE == OP_RC_GATHER8 ? V : 1];  // that tap's offsets
+  int dhb, dwb;  // RC_GATHER: the block's tap offsets (t = r0 / tap_c is fixed per block)
   int di, dj;
-  const DDL_LDS int* tt = nullptr;  // KC_GATHER8: the LDS copy of the tap table (load_tap_table)
+  const DDL_LDS int* tt = nullptr;  // gather modes: the LDS copy of the tap table (load_tap_table)
 
   __device__ __forceinline__ void init(const void* p, long ld_, int rows_, int r0_, int K_, const ConvGeom& g,
                                        int k0 = 0) {
@@ -97,6 +106,11 @@ struct Operand {
     if constexpr (RCG) {
       di = BK / g.wo;
       dj = BK - di * g.wo;
+      if constexpr (MODE == OP_RC_GATHER) {
+        const int e = tt[r0 / g.tap_c];
+        dhb = tap_dh(e);
+        dwb = tap_dw(e);
+      }
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         const int idx = threadIdx.x + v * NTHREADS;
@@ -110,8 +124,8 @@ struct Operand {
           const int r = r0 + rc * 8;
           tap8[v] = r < rows ? r / g.tap_c : 0;
           ch8[v] = r - tap8[v] * g.tap_c;
-          dh8[v] = g.dh[tap8[v]];
-          dw8[v] = g.dw[tap8[v]];
+          dh8[v] = tap_dh(tt[tap8[v]]);
+          dw8[v] = tap_dw(tt[tap8[v]]);
         }
       }
     }
@@ -146,7 +160,8 @@ struct Operand {
       } else if constexpr (MODE == OP_KC_GATHER) {
         const int t = k0 / g.tap_c;  // block-uniform: tap_c % 64 == 0
         const int c0 = k0 - t * g.tap_c;
-        const int ih = hbase[v] + g.dh[t], iw = wbase[v] + g.dw[t];
+        const int e = tt[t];
+        const int ih = hbase[v] + tap_dh(e), iw = wbase[v] + tap_dw(e);
         const bool ok = rvalid[v] && (unsigned)ih < (unsigned)g.hi && (unsigned)iw < (unsigned)g.wi;
         return ok ? ptr + ((long)(pixbase[v] + ih * g.wi + iw)) * g.c + c0 + kc * 8 : nullptr;
       } else {  // OP_KC_GATHER8
@@ -155,7 +170,7 @@ struct Operand {
         const int t = ok ? (g.tap_shift >= 0 ? k >> g.tap_shift : k / g.tap_c) : 0;
         const int c = k - t * g.tap_c;
         const int e = tt[t];
-        const int ih = hbase[v] + (int)(short)(e & 0xffff), iw = wbase[v] + (e >> 16);
+        const int ih = hbase[v] + tap_dh(e), iw = wbase[v] + tap_dw(e);
         ok = ok && (unsigned)ih < (unsigned)g.hi && (unsigned)iw < (unsigned)g.wi;
         return ok ? ptr + ((long)(pixbase[v] + ih * g.wi + iw)) * g.c + c : nullptr;
       }
@@ -176,8 +191,8 @@ struct Operand {
           ok = ok && r < rows;
           const int t = r < rows ? r / g.tap_c : 0;
           c = r - t * g.tap_c;
-          dhv = g.dh[t];
-          dwv = g.dw[t];
+          dhv = tap_dh(tt[t]);
+          dwv = tap_dw(tt[t]);
         } else {
           ok = ok && r0 + rc * 8 < rows;
         }
@@ -187,7 +202,7 @@ struct Operand {
       } else if constexpr (MODE == OP_RC_GATHER) {
         const int t = r0 / g.tap_c;  // block-uniform: tap_c % R == 0
         const int c0 = r0 - t * g.tap_c;
-        const int ih = qi[v] * g.sh + g.dh[t], iw = qj[v] * g.sw + g.dw[t];
+        const int ih = qi[v] * g.sh + dhb, iw = qj[v] * g.sw + dwb;
         const bool ok = k < K && (unsigned)ih < (unsigned)g.hi && (unsigned)iw < (unsigned)g.wi;
         return ok ? ptr + ((long)((qn[v] * g.hi + ih) * g.wi + iw)) * g.c + c0 + rc * 8 : nullptr;
       } else {  // OP_RC_TAPS: k = tap*kdiv + co ; addr = ptr + co*ld + wt[tap]*tap_stride + r
@@ -481,7 +496,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams
   constexpr int RM = WTM / 16, RN = WTN / 16;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  constexpr int TAPB = tap_table_bytes<AMODE>();
+  constexpr int TAPB = tap_table_bytes<AMODE, BMODE>();
   char* smem = smem_raw + TAPB;
   const bool one_stage = p.k_split <= BK;  // must match launch_tile's LDS allocation
   char* lds_a0 = smem;
@@ -507,6 +522,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams
   if constexpr (TAPB > 0) {
     load_tap_table(reinterpret_cast<int*>(smem_raw), p.g);
     A.tt = (const DDL_LDS int*)(smem_raw);
+    B.tt = (const DDL_LDS int*)(smem_raw);
   }
   A.init(p.a, p.lda, p.M, m0, p.K, p.g, kbeg);
   B.init(p.b, p.ldb, p.N, n0, p.K, p.g, kbeg);
@@ -573,7 +589,7 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int VA = BM / 32, VB = BN / 32;  // DMA wave-instructions per operand per K-tile
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  constexpr int TAPB = tap_table_bytes<AMODE>();
+  constexpr int TAPB = tap_table_bytes<AMODE, BMODE>();
   char* smem = smem_raw + TAPB;
 
   const int tiles_n = (p.N + BN - 1) / BN;
@@ -594,6 +610,7 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
   if constexpr (TAPB > 0) {
     load_tap_table(reinterpret_cast<int*>(smem_raw), p.g);
     A.tt = (const DDL_LDS int*)(smem_raw);
+    B.tt = (const DDL_LDS int*)(smem_raw);
   }
   A.init(p.a, p.lda, p.M, m0, p.K, p.g, kbeg);
   B.init(p.b, p.ldb, p.N, n0, p.K, p.g, kbeg);
@@ -735,7 +752,7 @@ inline int gather_stages() {
 
 template <int BM, int BN, int AMODE, int BMODE, int EPI, int ST>
 inline int launch_ring(const dim3 grid, const GemmParams& p, hipStream_t s) {
-  constexpr int lds = ST * (BM + BN) * BK * 2 + tap_table_bytes<AMODE>();
+  constexpr int lds = ST * (BM + BN) * BK * 2 + tap_table_bytes<AMODE, BMODE>();
   static bool attr = [] {  // dynamic LDS above 64 KB must be allowed explicitly
     return lds <= 65536 || hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_dma_kernel<BM, BN, AMODE, BMODE, EPI, ST>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
@@ -765,7 +782,7 @@ inline int launch_tile(const GemmParams& p, hipStream_t s) {
     if (dm == 1 && st == 3) return launch_ring<BM, BN, AMODE, BMODE, EPI, 3>(grid, p, s);
     if (dm == 1 && st == 4) return launch_ring<BM, BN, AMODE, BMODE, EPI, 4>(grid, p, s);
   }
-  constexpr int TAPB = tap_table_bytes<AMODE>();
+  constexpr int TAPB = tap_table_bytes<AMODE, BMODE>();
   if (dm == 1 || (dm == 2 && one_stage)) {
     hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, AMODE, BMODE, EPI, 1>), grid, dim3(NTHREADS), (BM + BN) * BK * 2 + TAPB,
                        s, p);
