@@ -750,6 +750,16 @@ inline int gather_stages() {
   return st;
 }
 
+inline int device_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  return cus;
+}
+
 template <int BM, int BN, int AMODE, int BMODE, int EPI, int ST>
 inline int launch_ring(const dim3 grid, const GemmParams& p, hipStream_t s) {
   constexpr int lds = ST * (BM + BN) * BK * 2 + tap_table_bytes<AMODE, BMODE>();
@@ -775,7 +785,10 @@ inline int launch_tile(const GemmParams& p, hipStream_t s) {
     // (72 KB: still 2 workgroups per CU), measured 10-25 % faster on the ResNet-50 1x1 layers; not on
     // 128x128 tiles (96 KB -> 1 workgroup per CU: BERT-base 664K -> 630K tokens/s) nor on the
     // gathered (3x3 / strided) weight gradients (ring 30 % slower there)
-    constexpr bool plain = AMODE == OP_RC && BMODE == OP_RC && BM * BN < 128 * 128;
+    constexpr bool plain_tile = AMODE == OP_RC && BMODE == OP_RC && BM * BN < 128 * 128;
+    // ... and only when the grid is one round at 2 workgroups per CU (the ring's 72 KB of LDS): a
+    // longer grid (BERT's weight gradients: 576 workgroups) runs 4 single-stage workgroups per CU
+    const bool plain = plain_tile && (long)grid.x * grid.y <= 2L * device_cus();
     const int st = one_stage ? 1
                              : (wgrad_stages() ? wgrad_stages()
                                                : (plain ? 3 : (gather_stages() ? gather_stages() : 1)));
