@@ -57,10 +57,28 @@ __device__ __forceinline__ bool drop_keep(uint64_t seed, uint64_t idx, uint32_t 
   return drop_hash(seed + idx) >= thresh;
 }
 
-// exact (erf) GELU and its derivative (BERT "gelu")
-__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+// erf-form GELU and its derivative (BERT "gelu"; not the tanh approximation)
+// erf without exp or branches (Abramowitz & Stegun 7.1.28, |error| <= 3e-7, far below bf16's
+// 2^-9): 1 - (1 + a1 x + ... + a6 x^6)^-16 — 6 FMAs, 4 squarings and one v_rcp_f32.  In the GELU
+// GEMM epilogues it replaced the library erff: BERT FFN1 forward 0.145 -> 0.131 ms, its GELU
+// data-gradient 0.189 -> 0.144 ms (with the 8-B pre-activation load), BERT-base 671K -> 696K tok/s
+__device__ __forceinline__ float erf_fast(float x) {
+  const float a = fabsf(x);
+  float p = fmaf(4.30638e-5f, a, 2.765672e-4f);
+  p = fmaf(p, a, 1.520143e-4f);
+  p = fmaf(p, a, 9.2705272e-3f);
+  p = fmaf(p, a, 4.22820123e-2f);
+  p = fmaf(p, a, 7.05230784e-2f);
+  p = fmaf(p, a, 1.f);
+  p *= p;
+  p *= p;
+  p *= p;
+  p *= p;
+  return copysignf(1.f - __builtin_amdgcn_rcpf(p), x);
+}
+__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erf_fast(x * 0.70710678118654752f)); }
 __device__ __forceinline__ float gelu_grad_f(float x) {
-  return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
+  return 0.5f * (1.f + erf_fast(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
 }
 
 // XCD-aware bijective remap of a 1-D block id (MI355X: 8 XCDs, blocks dealt round-robin).

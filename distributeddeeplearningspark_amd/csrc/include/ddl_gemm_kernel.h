@@ -333,6 +333,16 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
 #pragma unroll
     for (int e = 0; e < 4; ++e) s1[j][e] = s2[j][e] = 0.f;
   const bool vec_ok = (p.ldc % 4) == 0 && (LITE || !p.resid || (p.ldr % 4) == 0);
+  // bias of this lane's columns, loaded once: inside the row loop the compiler must re-load it
+  // after every output store (p.bias may alias p.c), 4 * RM * RN dependent loads per lane
+  float bias_r[RN][4];
+#pragma unroll
+  for (int j = 0; j < RN; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int n = nb + 16 * j + ncol + e;
+      bias_r[j][e] = (p.bias && n < p.N) ? p.bias[n] : 0.f;
+    }
 #pragma unroll
   for (int i = 0; i < RM; ++i) {
     const int m = mb + 16 * i + mrow;
@@ -354,10 +364,8 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * p.alpha;
       if constexpr (BF) {
-        if (p.bias) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] += (n + e < p.N) ? p.bias[n + e] : 0.f;
-        }
+        for (int e = 0; e < 4; ++e) v[e] += bias_r[j][e];
         if (!LITE && p.relu >= ACT_GELU) {  // transformer FFN: GELU fwd (saving the pre-activation) or its gradient
           bf16_t* ax = reinterpret_cast<bf16_t*>(p.aux) + (long)m * p.ldc + n;
           if (p.relu == ACT_GELU) {
@@ -373,9 +381,20 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
             else
               for (int e = 0; e < 4; ++e)
                 if (n + e < p.N) ax[e] = pa[e];
-          } else {
+          } else {  // one 8-B load of the 4 pre-activations (not four 2-B loads)
+            float pre[4];
+            if (full) {
+              const uint2 av = *reinterpret_cast<const uint2*>(ax);
+              pre[0] = __uint_as_float(av.x << 16);
+              pre[1] = __uint_as_float(av.x & 0xffff0000u);
+              pre[2] = __uint_as_float(av.y << 16);
+              pre[3] = __uint_as_float(av.y & 0xffff0000u);
+            } else {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] *= (n + e < p.N) ? gelu_grad_f(bf2f(ax[e])) : 0.f;
+              for (int e = 0; e < 4; ++e) pre[e] = (n + e < p.N) ? bf2f(ax[e]) : 0.f;
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] *= (n + e < p.N) ? gelu_grad_f(pre[e]) : 0.f;
           }
         }
         if (!LITE && p.drop_thresh) {
