@@ -139,24 +139,11 @@ def splitk_fwd_ok(g: ConvGeometry) -> bool:
     return math.ceil(g.M / 64) * math.ceil(g.Co / 64) <= _SPLITK_MAX_TILES
 
 
-_SPLITK_WS = {}
-
-
-def _splitk_workspace(M, N, device):
-    """Persistent zeroed fp32 [M, N] accumulator of the split-K forward: ``splitk_finalize`` zeroes
-    it again as it reads it, so consecutive calls (one stream) need no fill launch."""
-    key = (M, N, str(device))
-    ws = _SPLITK_WS.get(key)
-    if ws is None:
-        ws = _SPLITK_WS[key] = torch.zeros((M, N), dtype=torch.float32, device=device)
-    return ws
-
-
 def conv_fwd_native(x, w, g: ConvGeometry, bias=None, relu=False, stats=None):
     y = torch.empty((g.N, g.Ho, g.Wo, g.Co), dtype=torch.bfloat16, device=x.device)
     y2 = y.view(g.M, g.Co)
     if splitk_fwd_ok(g):
-        ws = _splitk_workspace(g.M, g.Co, x.device)
+        ws = G.splitk_workspace(g.M, g.Co, x.device)
         K = g.T * g.Ci
         tiles = math.ceil(g.M / 64) * math.ceil(g.Co / 64)
         splits = max(2, min(math.ceil(4 * 256 / tiles), K // 512))  # ~4 workgroups per CU, >= 8 K-tiles each

@@ -158,6 +158,22 @@ def linear_fwd(x2, w, bias=None, relu=False, out=None, resid=None, stats=None, a
                 drop_seed=drop_seed)
 
 
+_SPLITK_WS = {}
+
+
+def splitk_workspace(M, N, device):
+    """Persistent zeroed fp32 [M, N] accumulator of a split-K bf16 GEMM: ``splitk_finalize`` zeroes
+    it again as it reads it, so consecutive calls (one stream) need no fill launch."""
+    key = (M, N, str(device))
+    ws = _SPLITK_WS.get(key)
+    if ws is None:
+        ws = _SPLITK_WS[key] = torch.zeros((M, N), dtype=torch.float32, device=device)
+    return ws
+
+
+_SPLITK_DGRAD = _os.environ.get("DDL_DGRAD_SPLITK", "1") != "0"
+
+
 def linear_dgrad(dy, w, out=None, resid=None, gelu_pre=None, stats=None, resid_mask=None):
     """dx[M,K] = dy[M,N] @ w[N,K] (* gelu'(gelu_pre)) (+resid) -> bf16 (w read row-contiguous).
 
@@ -170,6 +186,18 @@ def linear_dgrad(dy, w, out=None, resid=None, gelu_pre=None, stats=None, resid_m
         out = torch.empty((M, K), dtype=torch.bfloat16, device=dy.device)
     act = ACT_GELU_BWD if gelu_pre is not None else ACT_NONE
     ldr = resid.stride(0) if resid is not None else 0
+    tiles = math.ceil(M / 64) * math.ceil(K / 64)
+    if (_SPLITK_DGRAD and gelu_pre is None and resid is None and N >= 4096 and tiles <= 1024 and K % 8 == 0
+            and out.is_contiguous() and out.dtype == torch.bfloat16 and dy.device.type == "cuda"):
+        # few output tiles over a long reduction (BERT's MLM decoder: [masked tokens, 768] over the
+        # 30,522-word vocabulary ran on 240 workgroups of ~480 K-steps): split the reduction over
+        # workgroups into an fp32 workspace, then round (+ statistics) in one finalize pass
+        ws = splitk_workspace(M, K, dy.device)
+        splits = max(2, min(math.ceil(2048 / tiles), N // 512))
+        gemm(dy, w, ws, M, K, N, KC, RC, dy.stride(0), w.stride(0), K, EPI_F32, tile=3,
+             k_split=math.ceil(N / splits / 64) * 64)
+        C().splitk_finalize(ws, out, K, None, False, stats)
+        return out
     if M >= _WT_MIN_M and not use_stream(M, K, N, KC, RC, EPI_BF16, dy.stride(0), out.stride(0), aux=gelu_pre,
                                           relu=act, resid=resid, ldr=ldr):
         # transpose the (small) weight once so the GEMM reads B K-contiguous with ds_read_b128 instead

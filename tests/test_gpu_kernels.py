@@ -163,6 +163,25 @@ def test_dgrad_masked_residual(M, N, K):
     close(out, ref, what=f"masked residual dgrad {M}x{N}x{K}")
 
 
+@pytest.mark.parametrize("M", [300, 2458])
+def test_linear_dgrad_splitk(M):
+    """Long-reduction data-gradient on few output tiles (BERT's MLM decoder: masked tokens x 768
+    over the vocabulary) runs split-K into the fp32 workspace: values, statistics, and the
+    workspace left zeroed for the next call (two calls, same shape)."""
+    from distributeddeeplearningspark_amd.ops import gemm as G
+
+    V, H = 8200, 768
+    for seed in (50, 52):
+        dy, w = rnd(M, V, seed=seed), rnd(V, H, scale=0.02, seed=seed + 1)
+        st = torch.zeros(32, 2, H, device=DEV)
+        out = G.linear_dgrad(dy, w, stats=st)
+        ref = dy.float() @ w.float()
+        close(out, ref, what=f"split-K dgrad M={M} seed={seed}")
+        o = out.float()
+        close(st.sum(0)[0], o.sum(0), rtol=1e-3, atol=1e-2, what="split-K dgrad stats")
+    assert G.splitk_workspace(M, H, dy.device).abs().max().item() == 0.0
+
+
 @pytest.mark.parametrize("relu", [False, True])
 def test_conv_splitk_forward_stats(relu):
     """Split-K forward of a small-grid conv: bias, ReLU and the fused per-channel statistics of the
