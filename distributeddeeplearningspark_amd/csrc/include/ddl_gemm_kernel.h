@@ -93,6 +93,14 @@ struct Operand {
   int tap8[MODE == OP_RC_GATHER8 ? V : 1], ch8[MODE == OP_RC_GATHER8 ? V : 1];
   int dh8[MODE == OP_RC_GATHER8 ? V : 1], dw8[MODE == OP_RC_GATHER8 ? V : 1];  // that tap's offsets
   int dhb, dwb;  // RC_GATHER: the block's tap offsets (t = r0 / tap_c is fixed per block)
+  // plain KC / RC modes, LDS-DMA (swizzled) order: each staged vector's element offset without the
+  // K-tile term, its k offset inside the tile, and whether its row is in range — precomputed so a
+  // K-tile's DMA addresses cost an add and a compare per vector instead of a 64-bit multiply, the
+  // swizzle and a branch (the BERT weight-gradient loop issued 7 VALU per MFMA on address math)
+  static constexpr bool PLAIN = (MODE == OP_KC || MODE == OP_RC);
+  long boff[PLAIN ? V : 1];
+  int kofs[PLAIN ? V : 1];
+  bool rok[PLAIN ? V : 1];
   int di, dj;
   const DDL_LDS int* tt = nullptr;  // gather modes: the LDS copy of the tap table (load_tap_table)
 
@@ -103,6 +111,27 @@ struct Operand {
     rows = rows_;
     r0 = r0_;
     K = K_;
+    if constexpr (PLAIN) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const int idx = threadIdx.x + v * NTHREADS;
+        if constexpr (MODE == OP_KC) {
+          const int row = idx >> 3;
+          const int kc = (idx & 7) ^ ((row >> 1) & 7);
+          const int r = r0 + row;
+          kofs[v] = kc * 8;
+          boff[v] = (long)r * ld + kc * 8;
+          rok[v] = r < rows;
+        } else {
+          const int krow = idx / (R / 8);
+          const int rc = (idx % (R / 8)) ^ (rc_swz<R>(krow) << 1);
+          const int r = r0 + rc * 8;
+          kofs[v] = krow;
+          boff[v] = (long)krow * ld + r;
+          rok[v] = r < rows;
+        }
+      }
+    }
     if constexpr (RCG) {
       di = BK / g.wo;
       dj = BK - di * g.wo;
@@ -155,8 +184,12 @@ struct Operand {
       const int row = idx >> 3;
       const int kc = SWZ ? ((idx & 7) ^ ((row >> 1) & 7)) : (idx & 7);
       if constexpr (MODE == OP_KC) {
-        const int r = r0 + row, k = k0 + kc * 8;
-        return (r < rows && k < K) ? ptr + (long)r * ld + k : nullptr;
+        if constexpr (SWZ) {
+          return (rok[v] && k0 + kofs[v] < K) ? ptr + boff[v] + k0 : nullptr;
+        } else {
+          const int r = r0 + row, k = k0 + kc * 8;
+          return (r < rows && k < K) ? ptr + (long)r * ld + k : nullptr;
+        }
       } else if constexpr (MODE == OP_KC_GATHER) {
         const int t = k0 / g.tap_c;  // block-uniform: tap_c % 64 == 0
         const int c0 = k0 - t * g.tap_c;
@@ -179,8 +212,12 @@ struct Operand {
       const int rc = SWZ ? ((idx % (R / 8)) ^ (rc_swz<R>(krow) << 1)) : (idx % (R / 8));
       const int k = k0 + krow;
       if constexpr (MODE == OP_RC) {
-        const int r = r0 + rc * 8;
-        return (r < rows && k < K) ? ptr + (long)k * ld + r : nullptr;
+        if constexpr (SWZ) {
+          return (rok[v] && k0 + kofs[v] < K) ? ptr + boff[v] + (long)k0 * ld : nullptr;
+        } else {
+          const int r = r0 + rc * 8;
+          return (r < rows && k < K) ? ptr + (long)k * ld + r : nullptr;
+        }
       } else if constexpr (MODE == OP_RC_GATHER8) {
         // (rc is the SWZ-permuted column chunk; the (tap, channel) of it was fixed in init for the
         // swizzled order; the register path (SWZ = false) recomputes it)
@@ -244,10 +281,13 @@ struct Operand {
 
   // LDS-DMA of the K-tile at k0 into a (swizzled) LDS image: V wave-instructions of 1 KB each
   __device__ __forceinline__ void dma(char* lds, int k0, const ConvGeom& g, int kdiv, long tap_stride, int wid) {
+    // the wave-uniform LDS destination once per call (the generic -> LDS cast carries a null check
+    // and two readfirstlanes), then scalar offsets per vector
+    const uint32_t base = lds_addr(lds) + (uint32_t)__builtin_amdgcn_readfirstlane(wid) * 1024u;
 #pragma unroll
     for (int v = 0; v < V; ++v) {
       const bf16_t* src = addr<true>(v, k0, g, kdiv, tap_stride);
-      dma16(src ? (const void*)src : (const void*)ddl_zero_page, lds_addr(lds + v * (NTHREADS * 16) + wid * 1024));
+      dma16(src ? (const void*)src : (const void*)ddl_zero_page, base + (uint32_t)(v * NTHREADS * 16));
     }
     advance(g);
   }
