@@ -68,6 +68,15 @@ __device__ __forceinline__ void load_tap_table(int* tab, const ConvGeom& g) {
 }
 
 
+// Source selection of a staged vector: the LDS-DMA path (SWZ) substitutes the zero page for an
+// out-of-range vector right here (a select, no branch around the address arithmetic and no second
+// null test in dma()); the register path keeps nullptr (= load zeros).
+template <bool SWZ>
+__device__ __forceinline__ const bf16_t* vsrc(bool ok, const bf16_t* p) {
+  if constexpr (SWZ) return ok ? p : reinterpret_cast<const bf16_t*>(ddl_zero_page);
+  else return ok ? p : nullptr;
+}
+
 // ----------------------------------------------------------------------------------------
 // Operand loaders. R = tile extent along the operand's row dimension (BM for A, BN for B).
 // ----------------------------------------------------------------------------------------
@@ -174,7 +183,7 @@ struct Operand {
     }
   }
 
-  // Source of 16-B vector v of the K-tile at k0 (nullptr: zero).  SWZ: vector v is LDS unit
+  // Source of 16-B vector v of the K-tile at k0 (vsrc: zero page / nullptr).  SWZ: vector v is LDS unit
   // threadIdx.x + 256 v of the SWIZZLED image (the LDS-DMA writes lane-linearly, so the swizzle
   // moves to the source); !SWZ: vector v is the unswizzled (row, chunk) the register path stores.
   template <bool SWZ>
@@ -185,7 +194,7 @@ struct Operand {
       const int kc = SWZ ? ((idx & 7) ^ ((row >> 1) & 7)) : (idx & 7);
       if constexpr (MODE == OP_KC) {
         if constexpr (SWZ) {
-          return (rok[v] && k0 + kofs[v] < K) ? ptr + boff[v] + k0 : nullptr;
+          return vsrc<true>(rok[v] && k0 + kofs[v] < K, ptr + boff[v] + k0);
         } else {
           const int r = r0 + row, k = k0 + kc * 8;
           return (r < rows && k < K) ? ptr + (long)r * ld + k : nullptr;
@@ -196,7 +205,7 @@ struct Operand {
         const int e = tt[t];
         const int ih = hbase[v] + tap_dh(e), iw = wbase[v] + tap_dw(e);
         const bool ok = rvalid[v] && (unsigned)ih < (unsigned)g.hi && (unsigned)iw < (unsigned)g.wi;
-        return ok ? ptr + ((long)(pixbase[v] + ih * g.wi + iw)) * g.c + c0 + kc * 8 : nullptr;
+        return vsrc<SWZ>(ok, ptr + ((long)(pixbase[v] + ih * g.wi + iw)) * g.c + c0 + kc * 8);
       } else {  // OP_KC_GATHER8
         const int k = k0 + kc * 8;
         bool ok = rvalid[v] && k < K;
@@ -205,7 +214,7 @@ struct Operand {
         const int e = tt[t];
         const int ih = hbase[v] + tap_dh(e), iw = wbase[v] + tap_dw(e);
         ok = ok && (unsigned)ih < (unsigned)g.hi && (unsigned)iw < (unsigned)g.wi;
-        return ok ? ptr + ((long)(pixbase[v] + ih * g.wi + iw)) * g.c + c : nullptr;
+        return vsrc<SWZ>(ok, ptr + ((long)(pixbase[v] + ih * g.wi + iw)) * g.c + c);
       }
     } else {
       const int krow = idx / (R / 8);
@@ -213,7 +222,7 @@ struct Operand {
       const int k = k0 + krow;
       if constexpr (MODE == OP_RC) {
         if constexpr (SWZ) {
-          return (rok[v] && k0 + kofs[v] < K) ? ptr + boff[v] + (long)k0 * ld : nullptr;
+          return vsrc<true>(rok[v] && k0 + kofs[v] < K, ptr + boff[v] + (long)k0 * ld);
         } else {
           const int r = r0 + rc * 8;
           return (r < rows && k < K) ? ptr + (long)k * ld + r : nullptr;
@@ -235,18 +244,18 @@ struct Operand {
         }
         const int ih = qi[v] * g.sh + dhv, iw = qj[v] * g.sw + dwv;
         ok = ok && (unsigned)ih < (unsigned)g.hi && (unsigned)iw < (unsigned)g.wi;
-        return ok ? ptr + ((long)((qn[v] * g.hi + ih) * g.wi + iw)) * g.c + c : nullptr;
+        return vsrc<SWZ>(ok, ptr + ((long)((qn[v] * g.hi + ih) * g.wi + iw)) * g.c + c);
       } else if constexpr (MODE == OP_RC_GATHER) {
         const int t = r0 / g.tap_c;  // block-uniform: tap_c % R == 0
         const int c0 = r0 - t * g.tap_c;
         const int ih = qi[v] * g.sh + dhb, iw = qj[v] * g.sw + dwb;
         const bool ok = k < K && (unsigned)ih < (unsigned)g.hi && (unsigned)iw < (unsigned)g.wi;
-        return ok ? ptr + ((long)((qn[v] * g.hi + ih) * g.wi + iw)) * g.c + c0 + rc * 8 : nullptr;
+        return vsrc<SWZ>(ok, ptr + ((long)((qn[v] * g.hi + ih) * g.wi + iw)) * g.c + c0 + rc * 8);
       } else {  // OP_RC_TAPS: k = tap*kdiv + co ; addr = ptr + co*ld + wt[tap]*tap_stride + r
         const int t = k0 / kdiv;  // block-uniform: kdiv % 64 == 0
         const int co0 = k0 - t * kdiv;
         const int r = r0 + rc * 8;
-        return (r < rows && k < K) ? ptr + (long)g.wt[t] * tap_stride + (long)(co0 + krow) * ld + r : nullptr;
+        return vsrc<SWZ>(r < rows && k < K, ptr + (long)g.wt[t] * tap_stride + (long)(co0 + krow) * ld + r);
       }
     }
   }
@@ -286,8 +295,7 @@ struct Operand {
     const uint32_t base = lds_addr(lds) + (uint32_t)__builtin_amdgcn_readfirstlane(wid) * 1024u;
 #pragma unroll
     for (int v = 0; v < V; ++v) {
-      const bf16_t* src = addr<true>(v, k0, g, kdiv, tap_stride);
-      dma16(src ? (const void*)src : (const void*)ddl_zero_page, base + (uint32_t)(v * NTHREADS * 16));
+      dma16(addr<true>(v, k0, g, kdiv, tap_stride), base + (uint32_t)(v * NTHREADS * 16));
     }
     advance(g);
   }
