@@ -144,6 +144,9 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
   }
   if (geom) {
     fill_geom(p.g, *geom);
+    // the gathering operand modes compute element offsets in 32 bits (ddl_gemm_kernel.h)
+    TORCH_CHECK((int64_t)p.g.n * p.g.hi * p.g.wi * p.g.c < (int64_t(1) << 31),
+                "gemm: a gathered tensor must have fewer than 2^31 elements");
     if (a_mode == OP_KC_GATHER) TORCH_CHECK(p.g.tap_c % 64 == 0 && K == (int64_t)p.g.ntaps * p.g.tap_c, "conv A gather: tap_c % 64 and K = taps*C");
     if (b_mode == OP_RC_GATHER) TORCH_CHECK(p.g.tap_c % bn == 0 && N == (int64_t)p.g.ntaps * p.g.tap_c, "conv B gather: tap_c % BN and N = taps*C");
     if (b_mode == OP_RC_TAPS) TORCH_CHECK(b_kdiv % 64 == 0 && K == (int64_t)p.g.ntaps * b_kdiv, "conv B taps: kdiv % 64 and K = taps*kdiv");

@@ -93,6 +93,10 @@ struct Operand {
   int pixbase[V];  // n*hi*wi
   int hbase[V], wbase[V];
   bool rvalid[V];
+  // KC gathers, LDS-DMA order: the element offset of the vector's output pixel at tap (0, 0),
+  // channel chunk included — a K-tile adds the block-uniform tap offset (dh*wi + dw)*c + c0.
+  // Gathered tensors hold < 2^31 elements (host check), so the offsets are 32-bit.
+  int pofs[(MODE == OP_KC_GATHER || MODE == OP_KC_GATHER8) ? V : 1];
   // gather state (RC_GATHER / RC_GATHER8): the output pixel k = k0 + krow of vector v, kept as
   // (n, i, j) and advanced by BK per staged K-tile (the K-tiles are staged strictly in order), so
   // the main loop does no integer division (two runtime divisions per vector per K-tile made the
@@ -179,6 +183,8 @@ struct Operand {
         pixbase[v] = n * g.hi * g.wi;
         hbase[v] = i * g.sh;
         wbase[v] = j * g.sw;
+        const int kc = (idx & 7) ^ ((row >> 1) & 7);  // the swizzled chunk the DMA path stages
+        pofs[v] = (pixbase[v] + hbase[v] * g.wi + wbase[v]) * g.c + (MODE == OP_KC_GATHER ? kc * 8 : 0);
       }
     }
   }
@@ -203,18 +209,22 @@ struct Operand {
         const int t = k0 / g.tap_c;  // block-uniform: tap_c % 64 == 0
         const int c0 = k0 - t * g.tap_c;
         const int e = tt[t];
-        const int ih = hbase[v] + tap_dh(e), iw = wbase[v] + tap_dw(e);
+        const int dh = tap_dh(e), dw = tap_dw(e);
+        const int ih = hbase[v] + dh, iw = wbase[v] + dw;
         const bool ok = rvalid[v] && (unsigned)ih < (unsigned)g.hi && (unsigned)iw < (unsigned)g.wi;
-        return vsrc<SWZ>(ok, ptr + ((long)(pixbase[v] + ih * g.wi + iw)) * g.c + c0 + kc * 8);
+        if constexpr (SWZ) return vsrc<true>(ok, ptr + (pofs[v] + (dh * g.wi + dw) * g.c + c0));
+        else return vsrc<false>(ok, ptr + ((long)(pixbase[v] + ih * g.wi + iw)) * g.c + c0 + kc * 8);
       } else {  // OP_KC_GATHER8
         const int k = k0 + kc * 8;
         bool ok = rvalid[v] && k < K;
         const int t = ok ? (g.tap_shift >= 0 ? k >> g.tap_shift : k / g.tap_c) : 0;
         const int c = k - t * g.tap_c;
         const int e = tt[t];
-        const int ih = hbase[v] + tap_dh(e), iw = wbase[v] + tap_dw(e);
+        const int dh = tap_dh(e), dw = tap_dw(e);
+        const int ih = hbase[v] + dh, iw = wbase[v] + dw;
         ok = ok && (unsigned)ih < (unsigned)g.hi && (unsigned)iw < (unsigned)g.wi;
-        return vsrc<SWZ>(ok, ptr + ((long)(pixbase[v] + ih * g.wi + iw)) * g.c + c);
+        if constexpr (SWZ) return vsrc<true>(ok, ptr + (pofs[v] + (dh * g.wi + dw) * g.c + c));
+        else return vsrc<false>(ok, ptr + ((long)(pixbase[v] + ih * g.wi + iw)) * g.c + c);
       }
     } else {
       const int krow = idx / (R / 8);
@@ -244,13 +254,13 @@ struct Operand {
         }
         const int ih = qi[v] * g.sh + dhv, iw = qj[v] * g.sw + dwv;
         ok = ok && (unsigned)ih < (unsigned)g.hi && (unsigned)iw < (unsigned)g.wi;
-        return vsrc<SWZ>(ok, ptr + ((long)((qn[v] * g.hi + ih) * g.wi + iw)) * g.c + c);
+        return vsrc<SWZ>(ok, ptr + (((qn[v] * g.hi + ih) * g.wi + iw) * g.c + c));  // < 2^31: 32-bit
       } else if constexpr (MODE == OP_RC_GATHER) {
         const int t = r0 / g.tap_c;  // block-uniform: tap_c % R == 0
         const int c0 = r0 - t * g.tap_c;
         const int ih = qi[v] * g.sh + dhb, iw = qj[v] * g.sw + dwb;
         const bool ok = k < K && (unsigned)ih < (unsigned)g.hi && (unsigned)iw < (unsigned)g.wi;
-        return vsrc<SWZ>(ok, ptr + ((long)((qn[v] * g.hi + ih) * g.wi + iw)) * g.c + c0 + rc * 8);
+        return vsrc<SWZ>(ok, ptr + (((qn[v] * g.hi + ih) * g.wi + iw) * g.c + c0 + rc * 8));  // 32-bit
       } else {  // OP_RC_TAPS: k = tap*kdiv + co ; addr = ptr + co*ld + wt[tap]*tap_stride + r
         const int t = k0 / kdiv;  // block-uniform: kdiv % 64 == 0
         const int co0 = k0 - t * kdiv;
