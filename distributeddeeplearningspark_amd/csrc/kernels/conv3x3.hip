@@ -87,21 +87,34 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv3x3_halo_kernel(const GemmPar
 
   const bf16_t* x = reinterpret_cast<const bf16_t*>(p.a);
   const int halo_instr = t.hr_pad / 32;  // 1-KB DMA pieces per wave
-  auto stage_halo = [&](int kc) {
-    for (int j = 0; j < halo_instr; ++j) {
-      const int piece = wid + 4 * j;
-      const int h = piece * 8 + (lane >> 3);
+  // Source of each of this lane's halo pieces for channel chunk 0 (element offset, -1 = padding):
+  // resolved once — the (image, row, column) of a halo row costs two integer divisions, which the
+  // per-chunk staging paid again for every 64-channel chunk.  The halo image is < 2^31 elements.
+  constexpr int kMaxHaloInstr = C3_MAX_HALO_ROWS / 32;
+  int hofs[kMaxHaloInstr];
+#pragma unroll
+  for (int j = 0; j < kMaxHaloInstr; ++j) {
+    hofs[j] = -1;
+    const int piece = wid + 4 * j;
+    const int h = piece * 8 + (lane >> 3);
+    if (j < halo_instr && h < t.hr) {
       const int chunk = (lane & 7) ^ (h & 6);  // source-side swizzle (LDS-DMA writes lane-linearly)
-      const void* src = ddl_zero_page;
-      if (h < t.hr) {
-        const int im = h / (t.hh * t.ww);
-        const int rem = h - im * t.hh * t.ww;
-        const int hy = rem / t.ww, hx = rem - hy * t.ww;
-        const int n = img0 + im, iy = oy0 + hy - 1, ix = hx - 1;
-        if (n < N && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
-          src = x + (((long)n * H + iy) * W + ix) * C + kc * 64 + chunk * 8;
+      const int im = h / (t.hh * t.ww);
+      const int rem = h - im * t.hh * t.ww;
+      const int hy = rem / t.ww, hx = rem - hy * t.ww;
+      const int n = img0 + im, iy = oy0 + hy - 1, ix = hx - 1;
+      if (n < N && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+        hofs[j] = ((n * H + iy) * W + ix) * C + chunk * 8;
+    }
+  }
+  const uint32_t halo_lds = lds_addr(halo) + (uint32_t)__builtin_amdgcn_readfirstlane(wid) * 1024u;
+  auto stage_halo = [&](int kc) {
+#pragma unroll
+    for (int j = 0; j < kMaxHaloInstr; ++j) {
+      if (j < halo_instr) {
+        const void* src = hofs[j] >= 0 ? (const void*)(x + hofs[j] + kc * 64) : (const void*)ddl_zero_page;
+        dma16(src, halo_lds + (uint32_t)(j * 4096));
       }
-      dma16(src, lds_addr(halo + piece * 1024));
     }
   };
   auto stage_b = [&](int s, char* buf) {
