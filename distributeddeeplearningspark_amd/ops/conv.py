@@ -126,6 +126,7 @@ def halo3_ok(g: ConvGeometry) -> bool:
 
 _SPLITK_FWD = _os.environ.get("DDL_CONV_SPLITK", "1") != "0"
 _SPLITK_MAX_TILES = int(_os.environ.get("DDL_CONV_SPLITK_TILES", "512"))
+_SPLITK_WG = int(_os.environ.get("DDL_CONV_SPLITK_WG", "1024"))  # workgroups the split aims for
 
 
 def splitk_fwd_ok(g: ConvGeometry) -> bool:
@@ -146,7 +147,7 @@ def conv_fwd_native(x, w, g: ConvGeometry, bias=None, relu=False, stats=None):
         ws = G.splitk_workspace(g.M, g.Co, x.device)
         K = g.T * g.Ci
         tiles = math.ceil(g.M / 64) * math.ceil(g.Co / 64)
-        splits = max(2, min(math.ceil(4 * 256 / tiles), K // 512))  # ~4 workgroups per CU, >= 8 K-tiles each
+        splits = max(2, min(math.ceil(_SPLITK_WG / tiles), K // 512))  # ~4 workgroups per CU, >= 8 K-tiles each
         G.gemm(x, w, ws, g.M, g.Co, K, G.KC_GATHER, G.KC, 0, K, g.Co, G.EPI_F32, geom=g.fwd_geom, tile=3,
                k_split=math.ceil(K / splits / 64) * 64)
         C().splitk_finalize(ws, y2, g.Co, bias, bool(relu), stats)
