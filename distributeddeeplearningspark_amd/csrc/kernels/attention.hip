@@ -286,8 +286,9 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const AttnParams p, l
 template <int MINB>
 __global__ __launch_bounds__(THREADS, MINB) void attn_bwd_dkdv_kernel(const AttnParams p) {
   __shared__ __attribute__((aligned(16))) char lds[2][2][TILE_BYTES];  // [buf][Q, dO]
-  __shared__ float s_lse[2][TQ], s_d[2][TQ];
-  __shared__ uint32_t s_rk[2][TQ];
+  __shared__ __attribute__((aligned(16))) float s_lse[2][TQ];
+  __shared__ __attribute__((aligned(16))) float s_d[2][TQ];
+  __shared__ __attribute__((aligned(16))) uint32_t s_rk[2][TQ];
   const int h = blockIdx.y, b = blockIdx.z, S = p.S;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
   const long tok0 = (long)b * S;
@@ -350,51 +351,58 @@ __global__ __launch_bounds__(THREADS, MINB) void attn_bwd_dkdv_kernel(const Attn
         r_rk = row_key(p.drop_seed, bh, S, (t + 1) * TQ + threadIdx.x);
       }
     }
-    const int qb = t * TQ;
-    // S, dP: [i = 16it + 4g + e][j = 16jt + li]
-    f32x4 s[4][2], dp[4][2];
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const bf16x8 q0f = frag_row(ql, 16 * it + li, 0, g), q1f = frag_row(ql, 16 * it + li, 1, g);
-      const bf16x8 d0f = frag_row(dl, 16 * it + li, 0, g), d1f = frag_row(dl, 16 * it + li, 1, g);
-#pragma unroll
-      for (int jt = 0; jt < 2; ++jt) {
-        f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f}, c = f32x4{0.f, 0.f, 0.f, 0.f};
-        a = mfma16x16x32(q0f, kf[jt][0], a);
-        s[it][jt] = mfma16x16x32(q1f, kf[jt][1], a);
-        c = mfma16x16x32(d0f, vf[jt][0], c);
-        dp[it][jt] = mfma16x16x32(d1f, vf[jt][1], c);
-      }
-    }
-    // P, dS (P kept in s[], dropout-scaled P in pd via s after dS is formed)
+    // The 64-query tile is processed as two 32-query halves: S / dP of one half (16 fp32 per
+    // lane each) are consumed by the dV / dK MFMAs before the next half is formed, which keeps
+    // the kernel inside 256 registers at 2 workgroups/CU without scratch spills.
     const bool kfull = k0 + 32 <= len;  // this wave's 32 keys all valid (wave-uniform)
     const uint32_t th16 = p.drop_thresh >> 16;
 #pragma unroll
-    for (int it = 0; it < 4; ++it)
+    for (int kq = 0; kq < 2; ++kq) {
+      // S, dP: [i = 32kq + 16i2 + 4g + e][j = 16jt + li]
+      f32x4 s[2][2], dp[2][2];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int il = 16 * it + 4 * g + e;
-        const float lq = s_lse[buf][il], dq = s_d[buf][il];
-        const uint32_t rki = s_rk[buf][il];
+      for (int i2 = 0; i2 < 2; ++i2) {
+        const int it = 2 * kq + i2;
+        const bf16x8 q0f = frag_row(ql, 16 * it + li, 0, g), q1f = frag_row(ql, 16 * it + li, 1, g);
+        const bf16x8 d0f = frag_row(dl, 16 * it + li, 0, g), d1f = frag_row(dl, 16 * it + li, 1, g);
 #pragma unroll
         for (int jt = 0; jt < 2; ++jt) {
-          const int j = k0 + 16 * jt + li;
-          float pv = fexp2(fmaf(s[it][jt][e], p.scale_log2, -lq));
-          if (!kfull && j >= len) pv = 0.f;
-          float keep = 1.f;
-          if (p.drop_thresh) keep = keep_bits(pair_hash(rki, j), j, th16) ? p.drop_scale : 0.f;
-          dp[it][jt][e] = pv * (dp[it][jt][e] * keep - dq);  // dS
-          s[it][jt][e] = pv * keep;                          // dropped P (for dV)
+          f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f}, c = f32x4{0.f, 0.f, 0.f, 0.f};
+          a = mfma16x16x32(q0f, kf[jt][0], a);
+          s[i2][jt] = mfma16x16x32(q1f, kf[jt][1], a);
+          c = mfma16x16x32(d0f, vf[jt][0], c);
+          dp[i2][jt] = mfma16x16x32(d1f, vf[jt][1], c);
         }
       }
-    // dV[j][d] += sum_i Pd[i][j] dO[i][d] ; dK[j][d] += sum_i dS[i][j] Q[i][d]
+      // P, dS (dropout-scaled P kept in s[] for dV); the lane's 4 query rows of a 16-row group
+      // are consecutive, so their lse / D / dropout keys are one 16-B LDS read each
 #pragma unroll
-    for (int kq = 0; kq < 2; ++kq) {
+      for (int i2 = 0; i2 < 2; ++i2) {
+        const int il0 = 16 * (2 * kq + i2) + 4 * g;
+        const f32x4 lq4 = *reinterpret_cast<const f32x4*>(&s_lse[buf][il0]);
+        const f32x4 dq4 = *reinterpret_cast<const f32x4*>(&s_d[buf][il0]);
+        const uint4 rk4 = *reinterpret_cast<const uint4*>(&s_rk[buf][il0]);
+        const uint32_t rkv[4] = {rk4.x, rk4.y, rk4.z, rk4.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+#pragma unroll
+          for (int jt = 0; jt < 2; ++jt) {
+            const int j = k0 + 16 * jt + li;
+            float pv = fexp2(fmaf(s[i2][jt][e], p.scale_log2, -lq4[e]));
+            if (!kfull && j >= len) pv = 0.f;
+            float keep = 1.f;
+            if (p.drop_thresh) keep = keep_bits(pair_hash(rkv[e], j), j, th16) ? p.drop_scale : 0.f;
+            dp[i2][jt][e] = pv * (dp[i2][jt][e] * keep - dq4[e]);  // dS
+            s[i2][jt][e] = pv * keep;                              // dropped P (for dV)
+          }
+        }
+      }
+      // dV[j][d] += sum_i Pd[i][j] dO[i][d] ; dK[j][d] += sum_i dS[i][j] Q[i][d]
       bf16x8 pa[2], sa[2];
 #pragma unroll
       for (int jt = 0; jt < 2; ++jt) {
-        pa[jt] = pack8(s[2 * kq][jt], s[2 * kq + 1][jt]);
-        sa[jt] = pack8(dp[2 * kq][jt], dp[2 * kq + 1][jt]);
+        pa[jt] = pack8(s[0][jt], s[1][jt]);
+        sa[jt] = pack8(dp[0][jt], dp[1][jt]);
       }
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
