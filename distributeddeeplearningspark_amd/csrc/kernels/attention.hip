@@ -38,25 +38,23 @@ constexpr int BLOCK_ROWS = 128;
 
 __device__ __forceinline__ int tile_byte(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
 
-struct TileStage {
-  uint4 reg[2];
-  __device__ __forceinline__ void load(const bf16_t* base, long ld, int r0, int nrows) {
+// LDS-DMA of a 64x64 bf16 tile (rows r0.. of `base`, row stride ld) into the swizzled image:
+// wave w's two 1-KB instructions fill linear 16-B slots v*256 + 64w + lane, i.e. tile row
+// slot>>3, physical chunk slot&7 -> the lane fetches logical chunk (slot&7) ^ ((row>>1)&7).
+// Rows at or past nrows read the zero page.  No staging registers; the caller waits
+// vmcnt(0) + barrier before the tile is read.
+__device__ __forceinline__ void dma_tile(const bf16_t* base, long ld, int r0, int nrows, char* lds) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t lb = lds_addr(lds) + (uint32_t)__builtin_amdgcn_readfirstlane(w) * 1024u;
 #pragma unroll
-    for (int v = 0; v < 2; ++v) {
-      const int idx = threadIdx.x + v * THREADS;
-      const int row = idx >> 3, ch = idx & 7;
-      reg[v] = (r0 + row < nrows) ? *reinterpret_cast<const uint4*>(base + (long)(r0 + row) * ld + ch * 8)
-                                  : make_uint4(0, 0, 0, 0);
-    }
+  for (int v = 0; v < 2; ++v) {
+    const int idx = v * THREADS + w * 64 + lane;
+    const int row = idx >> 3, ch = (idx & 7) ^ ((row >> 1) & 7);
+    const void* src = (r0 + row < nrows) ? (const void*)(base + (long)(r0 + row) * ld + ch * 8)
+                                         : (const void*)ddl_zero_page;
+    dma16(src, lb + (uint32_t)(v * THREADS * 16));
   }
-  __device__ __forceinline__ void store(char* lds) const {
-#pragma unroll
-    for (int v = 0; v < 2; ++v) {
-      const int idx = threadIdx.x + v * THREADS;
-      *reinterpret_cast<uint4*>(lds + tile_byte(idx >> 3, idx & 7)) = reg[v];
-    }
-  }
-};
+}
 
 // 8 consecutive elements of tile row `row` at columns 32kk + 8g (fragment whose k runs along the row)
 __device__ __forceinline__ bf16x8 frag_row(const char* lds, int row, int kk, int g) {
@@ -106,7 +104,8 @@ __device__ __forceinline__ bool keep_bits(uint32_t h, int j, uint32_t th16) {
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 // ================================================================ forward
-__global__ __launch_bounds__(THREADS, 2) void attn_fwd_kernel(const AttnParams p) {
+template <int MINB>
+__global__ __launch_bounds__(THREADS, MINB) void attn_fwd_kernel(const AttnParams p) {
   __shared__ __attribute__((aligned(16))) char lds[2][2][TILE_BYTES];
   const int h = blockIdx.y, b = blockIdx.z, S = p.S;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
@@ -135,89 +134,89 @@ __global__ __launch_bounds__(THREADS, 2) void attn_fwd_kernel(const AttnParams p
   for (int it = 0; it < 2; ++it) rk[it] = row_key(p.drop_seed, bh, S, q0 + 16 * it + li);
 
   const int nkt = (len + TQ - 1) / TQ;
-  TileStage sk, sv;
   if (nkt > 0) {
-    sk.load(K, p.ld, 0, len);
-    sv.load(V, p.ld, 0, len);
-    sk.store(lds[0][0]);
-    sv.store(lds[0][1]);
+    dma_tile(K, p.ld, 0, len, lds[0][0]);
+    dma_tile(V, p.ld, 0, len, lds[0][1]);
   }
+  wait_vmcnt<0>();
   __syncthreads();
   for (int t = 0; t < nkt; ++t) {
     const char* kl = lds[t & 1][0];
     const char* vl = lds[t & 1][1];
     const bool more = t + 1 < nkt;
     if (more) {
-      sk.load(K, p.ld, (t + 1) * TQ, len);
-      sv.load(V, p.ld, (t + 1) * TQ, len);
+      dma_tile(K, p.ld, (t + 1) * TQ, len, lds[(t + 1) & 1][0]);
+      dma_tile(V, p.ld, (t + 1) * TQ, len, lds[(t + 1) & 1][1]);
     }
-    // S^T[j = 16jt + 4g + e][i = 16it + li]
-    f32x4 s[4][2];
-#pragma unroll
-    for (int jt = 0; jt < 4; ++jt) {
-      const bf16x8 k0 = frag_row(kl, 16 * jt + li, 0, g), k1 = frag_row(kl, 16 * jt + li, 1, g);
-#pragma unroll
-      for (int it = 0; it < 2; ++it) {
-        f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
-        a = mfma16x16x32(k0, qf[it][0], a);
-        s[jt][it] = mfma16x16x32(k1, qf[it][1], a);
-      }
-    }
-    const int kb = t * TQ;
-    const bool full = kb + TQ <= len;  // tile fully inside the valid keys (wave-uniform)
-#pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      float mx = -INFINITY;
-      if (!full) {
-#pragma unroll
-        for (int jt = 0; jt < 4; ++jt)
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (kb + 16 * jt + 4 * g + e >= len) s[jt][it][e] = -INFINITY;
-      }
-#pragma unroll
-      for (int jt = 0; jt < 4; ++jt)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) mx = fmaxf(mx, s[jt][it][e]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mn = fmaxf(m[it], mx * p.scale_log2);  // running max of the scaled (log2) scores
-      const float alpha = fexp2(m[it] - mn);
-      m[it] = mn;
-      float rs = 0.f;
-#pragma unroll
-      for (int jt = 0; jt < 4; ++jt)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float pv = fexp2(fmaf(s[jt][it][e], p.scale_log2, -mn));
-          s[jt][it][e] = pv;
-          rs += pv;
-        }
-      l[it] = l[it] * alpha + rs;
-      if (!__all(alpha == 1.f)) {  // the running max moved for some query of the wave
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) o[dt][it] *= alpha;
-      }
-    }
-    if (p.drop_thresh) {
-      const uint32_t th16 = p.drop_thresh >> 16;
-#pragma unroll
-      for (int it = 0; it < 2; ++it)
-#pragma unroll
-        for (int jt = 0; jt < 4; ++jt)
-#pragma unroll
-          for (int e = 0; e < 4; e += 2) {
-            const int j = kb + 16 * jt + 4 * g + e;
-            const uint32_t h = pair_hash(rk[it], j);
-            s[jt][it][e] = keep_bits(h, j, th16) ? s[jt][it][e] * p.drop_scale : 0.f;
-            s[jt][it][e + 1] = keep_bits(h, j + 1, th16) ? s[jt][it][e + 1] * p.drop_scale : 0.f;
-          }
-    }
-    // O^T[d][i] += sum_j V^T[d][j] P^T[j][i]
+    // the 64-key tile as two 32-key online-softmax steps (one half's scores live at a time)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      const bf16x8 pb0 = pack8(s[2 * kk][0], s[2 * kk + 1][0]);
-      const bf16x8 pb1 = pack8(s[2 * kk][1], s[2 * kk + 1][1]);
+      // S^T[j = 32kk + 16j2 + 4g + e][i = 16it + li]
+      f32x4 s[2][2];
+#pragma unroll
+      for (int j2 = 0; j2 < 2; ++j2) {
+        const int jt = 2 * kk + j2;
+        const bf16x8 k0 = frag_row(kl, 16 * jt + li, 0, g), k1 = frag_row(kl, 16 * jt + li, 1, g);
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+          f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
+          a = mfma16x16x32(k0, qf[it][0], a);
+          s[j2][it] = mfma16x16x32(k1, qf[it][1], a);
+        }
+      }
+      const int kb = t * TQ + 32 * kk;
+      const bool full = kb + 32 <= len;  // half fully inside the valid keys (wave-uniform)
+#pragma unroll
+      for (int it = 0; it < 2; ++it) {
+        float mx = -INFINITY;
+        if (!full) {
+#pragma unroll
+          for (int j2 = 0; j2 < 2; ++j2)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (kb + 16 * j2 + 4 * g + e >= len) s[j2][it][e] = -INFINITY;
+        }
+#pragma unroll
+        for (int j2 = 0; j2 < 2; ++j2)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) mx = fmaxf(mx, s[j2][it][e]);
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float mn = fmaxf(m[it], mx * p.scale_log2);  // running max of the scaled (log2) scores
+        const float alpha = fexp2(m[it] - mn);
+        m[it] = mn;
+        float rs = 0.f;
+#pragma unroll
+        for (int j2 = 0; j2 < 2; ++j2)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float pv = fexp2(fmaf(s[j2][it][e], p.scale_log2, -mn));
+            s[j2][it][e] = pv;
+            rs += pv;
+          }
+        l[it] = l[it] * alpha + rs;
+        if (!__all(alpha == 1.f)) {  // the running max moved for some query of the wave
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) o[dt][it] *= alpha;
+        }
+      }
+      if (p.drop_thresh) {
+        const uint32_t th16 = p.drop_thresh >> 16;
+#pragma unroll
+        for (int it = 0; it < 2; ++it)
+#pragma unroll
+          for (int j2 = 0; j2 < 2; ++j2)
+#pragma unroll
+            for (int e = 0; e < 4; e += 2) {
+              const int j = kb + 16 * j2 + 4 * g + e;
+              const uint32_t h = pair_hash(rk[it], j);
+              s[j2][it][e] = keep_bits(h, j, th16) ? s[j2][it][e] * p.drop_scale : 0.f;
+              s[j2][it][e + 1] = keep_bits(h, j + 1, th16) ? s[j2][it][e + 1] * p.drop_scale : 0.f;
+            }
+      }
+      // O^T[d][i] += sum_j V^T[d][j] P^T[j][i]
+      const bf16x8 pb0 = pack8(s[0][0], s[1][0]);
+      const bf16x8 pb1 = pack8(s[0][1], s[1][1]);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const bf16x8 va = frag_col(vl, 32 * kk + 4 * g, 32 * kk + 16 + 4 * g, 16 * dt, lane);
@@ -225,10 +224,7 @@ __global__ __launch_bounds__(THREADS, 2) void attn_fwd_kernel(const AttnParams p
         o[dt][1] = mfma16x16x32(va, pb1, o[dt][1]);
       }
     }
-    if (more) {
-      sk.store(lds[(t + 1) & 1][0]);
-      sv.store(lds[(t + 1) & 1][1]);
-    }
+    wait_vmcnt<0>();
     __syncthreads();
   }
 #pragma unroll
@@ -322,20 +318,18 @@ __global__ __launch_bounds__(THREADS, MINB) void attn_bwd_dkdv_kernel(const Attn
 
   const bool any_key = blockIdx.x * BLOCK_ROWS < len;  // block-uniform
   const int nqt = any_key ? S / TQ : 0;
-  TileStage sq, sd;
   float r_lse = 0.f, r_d = 0.f;
   uint32_t r_rk = 0u;
   if (nqt > 0) {
-    sq.load(Q, p.ld, 0, S);
-    sd.load(dO, p.lddo, 0, S);
-    sq.store(lds[0][0]);
-    sd.store(lds[0][1]);
+    dma_tile(Q, p.ld, 0, S, lds[0][0]);
+    dma_tile(dO, p.lddo, 0, S, lds[0][1]);
     if (threadIdx.x < TQ) {
       s_lse[0][threadIdx.x] = lse[threadIdx.x];
       s_d[0][threadIdx.x] = dv[threadIdx.x];
       s_rk[0][threadIdx.x] = row_key(p.drop_seed, bh, S, threadIdx.x);
     }
   }
+  wait_vmcnt<0>();
   __syncthreads();
   for (int t = 0; t < nqt; ++t) {
     const int buf = t & 1;
@@ -343,8 +337,8 @@ __global__ __launch_bounds__(THREADS, MINB) void attn_bwd_dkdv_kernel(const Attn
     const char* dl = lds[buf][1];
     const bool more = t + 1 < nqt;
     if (more) {
-      sq.load(Q, p.ld, (t + 1) * TQ, S);
-      sd.load(dO, p.lddo, (t + 1) * TQ, S);
+      dma_tile(Q, p.ld, (t + 1) * TQ, S, lds[buf ^ 1][0]);
+      dma_tile(dO, p.lddo, (t + 1) * TQ, S, lds[buf ^ 1][1]);
       if (threadIdx.x < TQ) {
         r_lse = lse[(t + 1) * TQ + threadIdx.x];
         r_d = dv[(t + 1) * TQ + threadIdx.x];
@@ -416,14 +410,13 @@ __global__ __launch_bounds__(THREADS, MINB) void attn_bwd_dkdv_kernel(const Attn
       }
     }
     if (more) {
-      sq.store(lds[buf ^ 1][0]);
-      sd.store(lds[buf ^ 1][1]);
       if (threadIdx.x < TQ) {
         s_lse[buf ^ 1][threadIdx.x] = r_lse;
         s_d[buf ^ 1][threadIdx.x] = r_d;
         s_rk[buf ^ 1][threadIdx.x] = r_rk;
       }
     }
+    wait_vmcnt<0>();
     __syncthreads();
   }
 #pragma unroll
@@ -440,7 +433,8 @@ __global__ __launch_bounds__(THREADS, MINB) void attn_bwd_dkdv_kernel(const Attn
 }
 
 // ================================================================ backward: dQ
-__global__ __launch_bounds__(THREADS, 2) void attn_bwd_dq_kernel(const AttnParams p) {
+template <int MINB>
+__global__ __launch_bounds__(THREADS, MINB) void attn_bwd_dq_kernel(const AttnParams p) {
   __shared__ __attribute__((aligned(16))) char lds[2][2][TILE_BYTES];  // [buf][K, V]
   const int h = blockIdx.y, b = blockIdx.z, S = p.S;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
@@ -476,67 +470,67 @@ __global__ __launch_bounds__(THREADS, 2) void attn_bwd_dq_kernel(const AttnParam
     for (int dt = 0; dt < 4; ++dt) acc[it][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nkt = (len + TQ - 1) / TQ;
-  TileStage sk, sv;
   if (nkt > 0) {
-    sk.load(K, p.ld, 0, len);
-    sv.load(V, p.ld, 0, len);
-    sk.store(lds[0][0]);
-    sv.store(lds[0][1]);
+    dma_tile(K, p.ld, 0, len, lds[0][0]);
+    dma_tile(V, p.ld, 0, len, lds[0][1]);
   }
+  wait_vmcnt<0>();
   __syncthreads();
   for (int t = 0; t < nkt; ++t) {
     const char* kl = lds[t & 1][0];
     const char* vl = lds[t & 1][1];
     const bool more = t + 1 < nkt;
     if (more) {
-      sk.load(K, p.ld, (t + 1) * TQ, len);
-      sv.load(V, p.ld, (t + 1) * TQ, len);
+      dma_tile(K, p.ld, (t + 1) * TQ, len, lds[(t + 1) & 1][0]);
+      dma_tile(V, p.ld, (t + 1) * TQ, len, lds[(t + 1) & 1][1]);
     }
     const int kb = t * TQ;
-    // S^T, dP^T: [j = 16jt + 4g + e][i = 16it + li]
-    f32x4 s[4][2], dp[4][2];
-#pragma unroll
-    for (int jt = 0; jt < 4; ++jt) {
-      const bf16x8 k0f = frag_row(kl, 16 * jt + li, 0, g), k1f = frag_row(kl, 16 * jt + li, 1, g);
-      const bf16x8 v0f = frag_row(vl, 16 * jt + li, 0, g), v1f = frag_row(vl, 16 * jt + li, 1, g);
-#pragma unroll
-      for (int it = 0; it < 2; ++it) {
-        f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f}, c = f32x4{0.f, 0.f, 0.f, 0.f};
-        a = mfma16x16x32(k0f, qf[it][0], a);
-        s[jt][it] = mfma16x16x32(k1f, qf[it][1], a);
-        c = mfma16x16x32(v0f, df[it][0], c);
-        dp[jt][it] = mfma16x16x32(v1f, df[it][1], c);
-      }
-    }
     const bool full = kb + TQ <= len;
     const uint32_t th16 = p.drop_thresh >> 16;
-#pragma unroll
-    for (int jt = 0; jt < 4; ++jt)
-#pragma unroll
-      for (int it = 0; it < 2; ++it)
-#pragma unroll
-        for (int e = 0; e < 4; e += 2) {
-          const int j = kb + 16 * jt + 4 * g + e;
-          float p0 = fexp2(fmaf(s[jt][it][e], p.scale_log2, -lq[it]));
-          float p1 = fexp2(fmaf(s[jt][it][e + 1], p.scale_log2, -lq[it]));
-          if (!full) {
-            if (j >= len) p0 = 0.f;
-            if (j + 1 >= len) p1 = 0.f;
-          }
-          float k0v = 1.f, k1v = 1.f;
-          if (p.drop_thresh) {
-            const uint32_t h = pair_hash(rk[it], j);
-            k0v = keep_bits(h, j, th16) ? p.drop_scale : 0.f;
-            k1v = keep_bits(h, j + 1, th16) ? p.drop_scale : 0.f;
-          }
-          s[jt][it][e] = p0 * (dp[jt][it][e] * k0v - dq[it]);  // dS^T
-          s[jt][it][e + 1] = p1 * (dp[jt][it][e + 1] * k1v - dq[it]);
-        }
-    // dQ[i][d] += sum_j dS[i][j] K[j][d]
+    // the 64-key tile as two 32-key halves (S^T / dP^T of one half live at a time)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      const bf16x8 a0 = pack8(s[2 * kk][0], s[2 * kk + 1][0]);
-      const bf16x8 a1 = pack8(s[2 * kk][1], s[2 * kk + 1][1]);
+      // S^T, dP^T: [j = 32kk + 16j2 + 4g + e][i = 16it + li]
+      f32x4 s[2][2], dp[2][2];
+#pragma unroll
+      for (int j2 = 0; j2 < 2; ++j2) {
+        const int jt = 2 * kk + j2;
+        const bf16x8 k0f = frag_row(kl, 16 * jt + li, 0, g), k1f = frag_row(kl, 16 * jt + li, 1, g);
+        const bf16x8 v0f = frag_row(vl, 16 * jt + li, 0, g), v1f = frag_row(vl, 16 * jt + li, 1, g);
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+          f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f}, c = f32x4{0.f, 0.f, 0.f, 0.f};
+          a = mfma16x16x32(k0f, qf[it][0], a);
+          s[j2][it] = mfma16x16x32(k1f, qf[it][1], a);
+          c = mfma16x16x32(v0f, df[it][0], c);
+          dp[j2][it] = mfma16x16x32(v1f, df[it][1], c);
+        }
+      }
+#pragma unroll
+      for (int j2 = 0; j2 < 2; ++j2)
+#pragma unroll
+        for (int it = 0; it < 2; ++it)
+#pragma unroll
+          for (int e = 0; e < 4; e += 2) {
+            const int j = kb + 16 * (2 * kk + j2) + 4 * g + e;
+            float p0 = fexp2(fmaf(s[j2][it][e], p.scale_log2, -lq[it]));
+            float p1 = fexp2(fmaf(s[j2][it][e + 1], p.scale_log2, -lq[it]));
+            if (!full) {
+              if (j >= len) p0 = 0.f;
+              if (j + 1 >= len) p1 = 0.f;
+            }
+            float k0v = 1.f, k1v = 1.f;
+            if (p.drop_thresh) {
+              const uint32_t h = pair_hash(rk[it], j);
+              k0v = keep_bits(h, j, th16) ? p.drop_scale : 0.f;
+              k1v = keep_bits(h, j + 1, th16) ? p.drop_scale : 0.f;
+            }
+            s[j2][it][e] = p0 * (dp[j2][it][e] * k0v - dq[it]);  // dS^T
+            s[j2][it][e + 1] = p1 * (dp[j2][it][e + 1] * k1v - dq[it]);
+          }
+      // dQ[i][d] += sum_j dS[i][j] K[j][d]
+      const bf16x8 a0 = pack8(s[0][0], s[1][0]);
+      const bf16x8 a1 = pack8(s[0][1], s[1][1]);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const bf16x8 kb2 = frag_col(kl, 32 * kk + 4 * g, 32 * kk + 16 + 4 * g, 16 * dt, lane);
@@ -544,10 +538,7 @@ __global__ __launch_bounds__(THREADS, 2) void attn_bwd_dq_kernel(const AttnParam
         acc[1][dt] = mfma16x16x32(a1, kb2, acc[1][dt]);
       }
     }
-    if (more) {
-      sk.store(lds[(t + 1) & 1][0]);
-      sv.store(lds[(t + 1) & 1][1]);
-    }
+    wait_vmcnt<0>();
     __syncthreads();
   }
 #pragma unroll
@@ -564,7 +555,11 @@ __global__ __launch_bounds__(THREADS, 2) void attn_bwd_dq_kernel(const AttnParam
 
 int attn_fwd(const AttnParams& p, hipStream_t s) {
   if (p.B <= 0) return 0;
-  hipLaunchKernelGGL(attn_fwd_kernel, dim3(p.S / BLOCK_ROWS, p.H, p.B), dim3(THREADS), 0, s, p);
+  static const int occ = getenv("DDL_ATTN_FWD_OCC") ? atoi(getenv("DDL_ATTN_FWD_OCC")) : 2;
+  if (occ == 3)
+    hipLaunchKernelGGL(attn_fwd_kernel<3>, dim3(p.S / BLOCK_ROWS, p.H, p.B), dim3(THREADS), 0, s, p);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel<2>, dim3(p.S / BLOCK_ROWS, p.H, p.B), dim3(THREADS), 0, s, p);
   return (int)hipGetLastError();
 }
 
@@ -573,11 +568,17 @@ int attn_bwd(const AttnParams& p, hipStream_t s) {
   const long rows = (long)p.B * p.S * p.H;
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s, p, rows);
   static const int dkdv_occ = getenv("DDL_ATTN_DKDV_OCC") ? atoi(getenv("DDL_ATTN_DKDV_OCC")) : 2;
-  if (dkdv_occ != 1)
+  if (dkdv_occ == 3)
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<3>, dim3(p.S / BLOCK_ROWS, p.H, p.B), dim3(THREADS), 0, s, p);
+  else if (dkdv_occ != 1)
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel<2>, dim3(p.S / BLOCK_ROWS, p.H, p.B), dim3(THREADS), 0, s, p);
   else
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel<1>, dim3(p.S / BLOCK_ROWS, p.H, p.B), dim3(THREADS), 0, s, p);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(p.S / BLOCK_ROWS, p.H, p.B), dim3(THREADS), 0, s, p);
+  static const int dq_occ = getenv("DDL_ATTN_DQ_OCC") ? atoi(getenv("DDL_ATTN_DQ_OCC")) : 2;
+  if (dq_occ == 3)
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<3>, dim3(p.S / BLOCK_ROWS, p.H, p.B), dim3(THREADS), 0, s, p);
+  else
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<2>, dim3(p.S / BLOCK_ROWS, p.H, p.B), dim3(THREADS), 0, s, p);
   return (int)hipGetLastError();
 }
 
