@@ -238,6 +238,8 @@ void transpose_bf16_(const at::Tensor& x, const at::Tensor& y) {
 void bias_grad_(const at::Tensor& dy, const at::Tensor& db, int64_t N, bool accumulate) {
   GPU(dy); BF16(dy); F32(db);
   CK(dy.numel() % N == 0 && db.numel() >= N, "bias_grad: shapes");
+  // the kernels read dy as a dense [M][N] array (row stride N, 16-B vectors): no strided views
+  CK(dy.is_contiguous() && db.is_contiguous(), "bias_grad: dy and db must be contiguous");
   at::DeviceGuard g(dy.device());
   HIP_OK(bias_grad(dy.data_ptr(), db.data_ptr<float>(), dy.numel() / N, (int)N, accumulate ? 1 : 0, cur_stream()));
 }

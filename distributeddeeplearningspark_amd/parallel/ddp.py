@@ -16,7 +16,8 @@ collectives over xGMI:
 * Bucket size: xGMI is point-to-point (7 links x ~153 GB/s per MI355X); a ring
   all-reduce is bound by one link, so per-bucket latency alpha must be amortised by
   tens of MB.  Default 32 MB (``bucket_mb`` / ``DDL_BUCKET_MB``); the sweep that picks
-  it is ``scripts/bench_allreduce.py``.
+  it is ``scripts/bench_allreduce.py``.  The bucket of the first layers is cut small
+  (``DDL_TAIL_BUCKET_MB``, 4 MB): it is the one reduction that cannot overlap backward.
 * ``reduce_dtype=torch.bfloat16`` (``DDL_REDUCE_DTYPE=bf16``): each ready bucket is cast
   to a bf16 mirror slice by a HIP kernel on the compute stream, the bf16 slice is
   all-reduced (half the xGMI bytes), and after the last wait ONE HIP cast writes the
@@ -106,20 +107,31 @@ class DataParallel:
         # bucket size is counted in WIRE bytes, so a bf16 reduce packs twice the elements
         wire = 2 if self._red is not None else 4
         elems_per_bucket = max(self.bucket_bytes // wire, 256)
-        buckets = []  # list of dict(start, end, params)
+        # The bucket holding the FIRST layers launches only after the whole backward is done, so
+        # its all-reduce is never hidden: it is cut from the front of the arena at a small size
+        # (DDL_TAIL_BUCKET_MB, default min(4 MB, bucket)), the rest in full-size buckets.  With
+        # buckets cut from the end instead, ResNet-50's last 32 MB bucket spanned stage 3 down to
+        # the stem and its whole reduction waited for the stem's gradients.
+        tail_mb = float(os.environ.get("DDL_TAIL_BUCKET_MB", min(4.0, self.bucket_mb)))
+        cap = max(int(tail_mb * (1 << 20)) // wire, 256)
+        buckets = []  # built front -> back, reversed below: index 0 = end of the arena
         cur = None
-        for p in reversed(params):
+        for p in params:
             end = p.offset + (-(-p.numel // 64) * 64)
             if cur is None:
                 cur = {"start": p.offset, "end": end, "params": [p]}
             else:
-                cur["start"] = p.offset
+                cur["end"] = end
                 cur["params"].append(p)
-            if cur["end"] - cur["start"] >= elems_per_bucket:
+            if cur["end"] - cur["start"] >= cap:
                 buckets.append(cur)
                 cur = None
+                cap = elems_per_bucket
         if cur is not None:
             buckets.append(cur)
+        buckets.reverse()
+        for b in buckets:
+            b["params"].reverse()
         if buckets:
             buckets[0]["end"] = self.arena.numel  # include the alignment tail
             buckets[-1]["start"] = 0

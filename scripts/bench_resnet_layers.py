@@ -25,6 +25,13 @@ SHAPES = [
     (14, 1024, 512, 1, 1, 1), (14, 512, 512, 3, 2, 1), (7, 512, 2048, 1, 1, 3), (14, 1024, 2048, 1, 2, 1),
     (7, 2048, 512, 1, 1, 2), (7, 512, 512, 3, 1, 2),
 ]
+# SHAPES=vgg16: the CIFAR VGG-16 convolutions (32x32 input; the 3-channel stem is left out)
+VGG16_SHAPES = [
+    (32, 64, 64, 3, 1, 1), (16, 64, 128, 3, 1, 1), (16, 128, 128, 3, 1, 1), (8, 128, 256, 3, 1, 1),
+    (8, 256, 256, 3, 1, 2), (4, 256, 512, 3, 1, 1), (4, 512, 512, 3, 1, 2), (2, 512, 512, 3, 1, 3),
+]
+if os.environ.get("SHAPES") == "vgg16":
+    SHAPES = VGG16_SHAPES
 
 
 def timeit(fn, reps=10):

@@ -78,6 +78,28 @@ def test_ddp_overlap_hooks_n4_match_emulation(reduce_dtype):
     assert rel < (1e-5 if reduce_dtype == "fp32" else 2e-3), rel
 
 
+def test_bucket_layout_small_tail_contiguous():
+    """Buckets tile the gradient arena back to front without gaps; the last-launched bucket
+    (first layers, never overlapped) is cut at the tail size, the others at the bucket size."""
+    from distributeddeeplearningspark_amd.models import ResNet50
+    from distributeddeeplearningspark_amd.parallel.comm import ProcessGroup
+    from distributeddeeplearningspark_amd.parallel.ddp import DataParallel
+
+    m = ResNet50(input_shape=(32, 32, 3), num_classes=10)
+    m.compile("sgd", "sparse_categorical_crossentropy")
+    m.place("cpu", seed=0)
+    ddp = DataParallel(m, ProcessGroup(0, 1, 0, torch.device("cpu"), None), bucket_mb=4, overlap=False)
+    bs = ddp.buckets
+    assert len(bs) >= 4
+    assert bs[0]["end"] == m.arena.numel and bs[-1]["start"] == 0
+    for a, b in zip(bs, bs[1:]):  # index order = launch order = back to front, no gaps
+        assert b["end"] == a["start"]
+    tail = bs[-1]["end"] - bs[-1]["start"]
+    assert tail * 4 <= 4 * 2**20 + 4 * max(p.numel for p in bs[-1]["params"])
+    owners = [ddp.bucket_of[id(p)] for p in m.arena.params if p.trainable]
+    assert owners == sorted(owners, reverse=True)  # later parameters -> earlier buckets
+
+
 def test_all_reduce_flat_chunks_and_average():
     from distributeddeeplearningspark_amd.parallel.launcher import run_workers
 
