@@ -45,6 +45,9 @@ def main():
                "apply_us": round(t_apply * 1e6, 1), "apply_TBs": round((3 if resid else 2) * S / t_apply / 1e12, 2),
                "reduce_us": round(t_red * 1e6, 1), "reduce_TBs": round(2 * S / t_red / 1e12, 2),
                "dx_us": round(t_dx * 1e6, 1), "dx_TBs": round((4 if resid else 3) * S / t_dx / 1e12, 2)}
+        t_copy = timeit(lambda: y.copy_(x))  # read + write yardstick at the same size
+        row["copy_us"] = round(t_copy * 1e6, 1)
+        row["copy_TBs"] = round(2 * S / t_copy / 1e12, 2)
         out.append(row)
         print(json.dumps(row), flush=True)
 
