@@ -404,11 +404,13 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint4* __restr
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
   if (g.active) {
     float mu[8], sc[8], sh[8];
+    load8f(mean + g.cv * 8, mu);  // 16-B loads: 24 dependent 4-B loads per lane before the sweep otherwise
+    if (mode == 2) {
+      load8f(scale + g.cv * 8, sc);
+      load8f(shift + g.cv * 8, sh);
+    } else {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      mu[i] = mean[g.cv * 8 + i];
-      sc[i] = mode == 2 ? scale[g.cv * 8 + i] : 0.f;
-      sh[i] = mode == 2 ? shift[g.cv * 8 + i] : 0.f;
+      for (int i = 0; i < 8; ++i) sc[i] = sh[i] = 0.f;
     }
     const long step = (long)gridDim.x * g.RT;
     long r = (long)blockIdx.x * g.RT + g.rt;

@@ -32,7 +32,9 @@ __device__ __forceinline__ uint4 pack8f(const float* f) {
 
 // One wave per row, grid-stride over rows; gamma / beta of the lane's columns live in registers
 // (loading them per element per row cost 4x the bytes of the row itself through L1).
-template <int VPL>
+// PF: the next row's vectors are loaded before this row's two reductions (one row in flight under
+// the math of the current one; without it each row paid the full load latency serially).
+template <int VPL, bool PF>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, bf16_t* __restrict__ y,
                                                      float* __restrict__ mean, float* __restrict__ rstd, long M, int H,
@@ -42,23 +44,45 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
   const int nv = H >> 3;
   float gm[VPL][8], bt[VPL][8];
 #pragma unroll
-  for (int u = 0; u < VPL; ++u) {
+  for (int u = 0; u < VPL; ++u) {  // 16-B loads (gamma / beta rows are 32-B aligned: H % 8 == 0)
     const int c = lane + 64 * u;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      gm[u][e] = (gamma && c < nv) ? gamma[c * 8 + e] : 1.f;
-      bt[u][e] = (beta && c < nv) ? beta[c * 8 + e] : 0.f;
-    }
+    const bool ok = c < nv;
+    const float4 g0 = (gamma && ok) ? reinterpret_cast<const float4*>(gamma)[2 * c] : make_float4(1.f, 1.f, 1.f, 1.f);
+    const float4 g1 = (gamma && ok) ? reinterpret_cast<const float4*>(gamma)[2 * c + 1] : make_float4(1.f, 1.f, 1.f, 1.f);
+    const float4 b0 = (beta && ok) ? reinterpret_cast<const float4*>(beta)[2 * c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 b1 = (beta && ok) ? reinterpret_cast<const float4*>(beta)[2 * c + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
+    gm[u][0] = g0.x; gm[u][1] = g0.y; gm[u][2] = g0.z; gm[u][3] = g0.w;
+    gm[u][4] = g1.x; gm[u][5] = g1.y; gm[u][6] = g1.z; gm[u][7] = g1.w;
+    bt[u][0] = b0.x; bt[u][1] = b0.y; bt[u][2] = b0.z; bt[u][3] = b0.w;
+    bt[u][4] = b1.x; bt[u][5] = b1.y; bt[u][6] = b1.z; bt[u][7] = b1.w;
   }
-  for (long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6); row < M; row += (long)gridDim.x * 4) {
-    const bf16_t* xr = x + row * H;
+  const long rstep = (long)gridDim.x * 4;
+  long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  uint4 nx[VPL];
+  auto fetch = [&](long r) {
+#pragma unroll
+    for (int u = 0; u < VPL; ++u)
+      if (lane + 64 * u < nv) nx[u] = *reinterpret_cast<const uint4*>(x + r * H + (lane + 64 * u) * 8);
+  };
+  if (PF && row < M) fetch(row);
+  for (; row < M; row += rstep) {
+    uint4 cur[VPL];
+    if (PF) {
+#pragma unroll
+      for (int u = 0; u < VPL; ++u) cur[u] = nx[u];
+      if (row + rstep < M) fetch(row + rstep);
+    } else {
+      fetch(row);
+#pragma unroll
+      for (int u = 0; u < VPL; ++u) cur[u] = nx[u];
+    }
     float v[VPL][8];
     float s = 0.f;
 #pragma unroll
     for (int u = 0; u < VPL; ++u) {
       const int c = lane + 64 * u;
       if (c < nv) {
-        unpack8(*reinterpret_cast<const uint4*>(xr + c * 8), v[u]);
+        unpack8(cur[u], v[u]);
 #pragma unroll
         for (int e = 0; e < 8; ++e) s += v[u][e];
       } else {
@@ -99,7 +123,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
   }
 }
 
-template <int VPL>
+template <int VPL, bool PF>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const float* __restrict__ gamma, bf16_t* __restrict__ dx,
@@ -117,10 +141,48 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       dg[u][e] = db[u][e] = dd[u][e] = 0.f;
-      gmv[u][e] = (gamma && lane + 64 * u < nv) ? gamma[(lane + 64 * u) * 8 + e] : 1.f;  // hoisted out of the rows
     }
+#pragma unroll
+  for (int u = 0; u < VPL; ++u) {  // hoisted out of the rows; 16-B loads (gamma is 16-B aligned: host check)
+    const int c = lane + 64 * u;
+    const bool ok = gamma && c < nv;
+    const float4 g0 = ok ? reinterpret_cast<const float4*>(gamma)[2 * c] : make_float4(1.f, 1.f, 1.f, 1.f);
+    const float4 g1 = ok ? reinterpret_cast<const float4*>(gamma)[2 * c + 1] : make_float4(1.f, 1.f, 1.f, 1.f);
+    gmv[u][0] = g0.x; gmv[u][1] = g0.y; gmv[u][2] = g0.z; gmv[u][3] = g0.w;
+    gmv[u][4] = g1.x; gmv[u][5] = g1.y; gmv[u][6] = g1.z; gmv[u][7] = g1.w;
+  }
+  // PF: the next row's dy / x vectors and statistics are loaded before this row's math
+  uint4 ndy[VPL], nx[VPL];
+  float nmu = 0.f, nrs = 0.f;
+  auto fetch = [&](long r) {
+#pragma unroll
+    for (int u = 0; u < VPL; ++u)
+      if (lane + 64 * u < nv) {
+        ndy[u] = *reinterpret_cast<const uint4*>(dy + r * H + (lane + 64 * u) * 8);
+        nx[u] = *reinterpret_cast<const uint4*>(x + r * H + (lane + 64 * u) * 8);
+      }
+    nmu = mean[r];
+    nrs = rstd[r];
+  };
+  if (PF && wave < M) fetch(wave);
   for (long row = wave; row < M; row += nwaves) {
-    const float mu = mean[row], rs = rstd[row];
+    uint4 cdy[VPL], cx[VPL];
+    if (PF) {
+#pragma unroll
+      for (int u = 0; u < VPL; ++u) {
+        cdy[u] = ndy[u];
+        cx[u] = nx[u];
+      }
+    } else {
+      fetch(row);
+#pragma unroll
+      for (int u = 0; u < VPL; ++u) {
+        cdy[u] = ndy[u];
+        cx[u] = nx[u];
+      }
+    }
+    const float mu = nmu, rs = nrs;
+    if (PF && row + nwaves < M) fetch(row + nwaves);
     float gy[VPL][8], xh[VPL][8];
     float a = 0.f, b = 0.f;
 #pragma unroll
@@ -128,8 +190,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
       const int c = lane + 64 * u;
       if (c < nv) {
         float d[8], xv[8];
-        unpack8(*reinterpret_cast<const uint4*>(dy + row * H + c * 8), d);
-        unpack8(*reinterpret_cast<const uint4*>(x + row * H + c * 8), xv);
+        unpack8(cdy[u], d);
+        unpack8(cx[u], xv);
         if (in_thresh) {  // dy arrives through the forward's output dropout
           const unsigned long long base = (unsigned long long)row * (unsigned long long)H + c * 8;
 #pragma unroll
@@ -366,19 +428,35 @@ constexpr int kLnBwdBlocks = 512;  // 2 waves/SIMD: LN bwd 48 -> 37 us per BERT 
 
 }  // namespace
 
+// DDL_LN_PREFETCH=0 selects the row-serial LayerNorm sweeps (A/B knob; read once per process)
+static bool ln_prefetch() {
+  static const bool on = [] {
+    const char* e = std::getenv("DDL_LN_PREFETCH");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int layernorm_fwd(const void* x, const float* gamma, const float* beta, void* y, float* mean, float* rstd, long M,
                   int H, float eps, float drop_p, unsigned long long seed, hipStream_t s) {
   if (M <= 0) return 0;
   const uint32_t th = drop_p > 0.f ? (uint32_t)std::min(4294967295.0, (double)drop_p * 4294967296.0) : 0u;
   const float ds = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
   const int nv = H / 8;
-  const dim3 grid((unsigned)std::min<long>((M + 3) / 4, 2048));  // grid-stride: gamma / beta loaded once per wave
+  const bool PF = ln_prefetch();
+  // grid-stride: gamma / beta loaded once per wave (DDL_LN_FWD_BLOCKS: experiment knob, read once)
+  static const long cap = [] {
+    const char* e = std::getenv("DDL_LN_FWD_BLOCKS");
+    const long v = e ? std::atol(e) : 0;
+    return v > 0 ? v : 2048L;
+  }();
+  const dim3 grid((unsigned)std::min<long>((M + 3) / 4, cap));
   auto X = reinterpret_cast<const bf16_t*>(x);
   auto Y = reinterpret_cast<bf16_t*>(y);
-  if (nv <= 64) hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed);
-  else if (nv <= 128) hipLaunchKernelGGL(ln_fwd_kernel<2>, grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed);
-  else if (nv <= 256) hipLaunchKernelGGL(ln_fwd_kernel<4>, grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed);
-  else hipLaunchKernelGGL(ln_fwd_kernel<8>, grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed);
+  if (nv <= 64) { if (PF) hipLaunchKernelGGL((ln_fwd_kernel<1, true>), grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed); else hipLaunchKernelGGL((ln_fwd_kernel<1, false>), grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed); }
+  else if (nv <= 128) { if (PF) hipLaunchKernelGGL((ln_fwd_kernel<2, true>), grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed); else hipLaunchKernelGGL((ln_fwd_kernel<2, false>), grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed); }
+  else if (nv <= 256) { if (PF) hipLaunchKernelGGL((ln_fwd_kernel<4, true>), grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed); else hipLaunchKernelGGL((ln_fwd_kernel<4, false>), grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed); }
+  else { if (PF) hipLaunchKernelGGL((ln_fwd_kernel<8, true>), grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed); else hipLaunchKernelGGL((ln_fwd_kernel<8, false>), grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed); }
   return (int)hipGetLastError();
 }
 
@@ -403,6 +481,7 @@ int layernorm_bwd(const void* dy, const void* x, const float* mean, const float*
   const uint32_t ith = in_drop_p > 0.f ? (uint32_t)std::min(4294967295.0, (double)in_drop_p * 4294967296.0) : 0u;
   const float iscale = in_drop_p > 0.f ? 1.f / (1.f - in_drop_p) : 1.f;
   const int nv = H / 8;
+  const bool PF = ln_prefetch();
   const dim3 grid((unsigned)(P / 4));
   const uint32_t thresh = drop_p > 0.f ? (uint32_t)std::min(4294967295.0, (double)drop_p * 4294967296.0) : 0u;
   const float dscale = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
@@ -410,10 +489,10 @@ int layernorm_bwd(const void* dy, const void* x, const float* mean, const float*
   auto X = reinterpret_cast<const bf16_t*>(x);
   auto DX = reinterpret_cast<bf16_t*>(dx);
   auto DD = reinterpret_cast<bf16_t*>(dx_drop);
-  if (nv <= 64) hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts);
-  else if (nv <= 128) hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts);
-  else if (nv <= 256) hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts);
-  else hipLaunchKernelGGL(ln_bwd_kernel<8>, grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts);
+  if (nv <= 64) { if (PF) hipLaunchKernelGGL((ln_bwd_kernel<1, true>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts); else hipLaunchKernelGGL((ln_bwd_kernel<1, false>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts); }
+  else if (nv <= 128) { if (PF) hipLaunchKernelGGL((ln_bwd_kernel<2, true>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts); else hipLaunchKernelGGL((ln_bwd_kernel<2, false>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts); }
+  else if (nv <= 256) { if (PF) hipLaunchKernelGGL((ln_bwd_kernel<4, true>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts); else hipLaunchKernelGGL((ln_bwd_kernel<4, false>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts); }
+  else { if (PF) hipLaunchKernelGGL((ln_bwd_kernel<8, true>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts); else hipLaunchKernelGGL((ln_bwd_kernel<8, false>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts); }
   return (int)hipGetLastError();
 }
 

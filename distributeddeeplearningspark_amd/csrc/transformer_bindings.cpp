@@ -110,8 +110,8 @@ void layernorm_fwd_(const at::Tensor& x, c10::optional<at::Tensor> gamma, c10::o
   const int64_t H = x.size(-1), M = x.numel() / H;
   CK(H % 8 == 0 && H <= 4096, "layernorm: H % 8 == 0 and H <= 4096");
   CK(y.numel() == x.numel() && mean.numel() == M && rstd.numel() == M, "layernorm: shapes");
-  if (gamma) { F32(*gamma); CK(gamma->numel() == H, "gamma [H]"); }
-  if (beta) { F32(*beta); CK(beta->numel() == H, "beta [H]"); }
+  if (gamma) { F32(*gamma); CK(gamma->numel() == H && (uintptr_t)gamma->data_ptr() % 16 == 0, "gamma [H], 16-B aligned"); }
+  if (beta) { F32(*beta); CK(beta->numel() == H && (uintptr_t)beta->data_ptr() % 16 == 0, "beta [H], 16-B aligned"); }
   at::DeviceGuard g(x.device());
   HIP_OK(layernorm_fwd(x.data_ptr(), optr<const float>(gamma), optr<const float>(beta), y.data_ptr(),
                        mean.data_ptr<float>(), rstd.data_ptr<float>(), M, (int)H, (float)eps, (float)drop_p,
@@ -128,7 +128,7 @@ void layernorm_bwd_(const at::Tensor& dy, const at::Tensor& x, const at::Tensor&
   const int64_t H = x.size(-1), M = x.numel() / H;
   CK(H % 8 == 0 && H <= 4096, "layernorm_bwd: H % 8 == 0 and H <= 4096");
   CK(dy.numel() == x.numel() && dx.numel() == x.numel() && mean.numel() == M && rstd.numel() == M, "shapes");
-  if (gamma) { F32(*gamma); CK(gamma->numel() == H, "gamma [H]"); }
+  if (gamma) { F32(*gamma); CK(gamma->numel() == H && (uintptr_t)gamma->data_ptr() % 16 == 0, "gamma [H], 16-B aligned"); }
   if (dx_drop) { BF16(*dx_drop); CK(dx_drop->numel() == x.numel(), "dx_drop shape"); }
   const int P = ln_partial_rows(M);
   CK(parts == 2 || parts == 3, "layernorm_bwd: parts must be 2 or 3");
