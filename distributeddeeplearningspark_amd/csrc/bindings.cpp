@@ -128,6 +128,7 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
     CHECK_CUDA(*bias);
     CHECK_F32(*bias);
     TORCH_CHECK(bias->numel() >= N, "bias too short");
+    TORCH_CHECK((uintptr_t)bias->data_ptr() % 16 == 0, "gemm: bias must be 16-B aligned (vector loads)");
     p.bias = bias->data_ptr<float>();
   }
   if (resid) {

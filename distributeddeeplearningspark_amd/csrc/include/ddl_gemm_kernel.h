@@ -393,14 +393,23 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
   const bool vec_ok = (p.ldc % 4) == 0 && (LITE || !p.resid || (p.ldr % 4) == 0);
   // bias of this lane's columns, loaded once: inside the row loop the compiler must re-load it
   // after every output store (p.bias may alias p.c), 4 * RM * RN dependent loads per lane
+  // (one 16-B load per fragment column group where the 4 columns are in range: n % 4 == 0 and the
+  // bias is a 16-B aligned fp32 vector — host check)
   float bias_r[RN][4];
 #pragma unroll
-  for (int j = 0; j < RN; ++j)
+  for (int j = 0; j < RN; ++j) {
+    const int n = nb + 16 * j + ncol;
+    if (p.bias && n + 3 < p.N) {
+      const float4 bv = *reinterpret_cast<const float4*>(p.bias + n);
+      bias_r[j][0] = bv.x;
+      bias_r[j][1] = bv.y;
+      bias_r[j][2] = bv.z;
+      bias_r[j][3] = bv.w;
+    } else {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int n = nb + 16 * j + ncol + e;
-      bias_r[j][e] = (p.bias && n < p.N) ? p.bias[n] : 0.f;
+      for (int e = 0; e < 4; ++e) bias_r[j][e] = (p.bias && n + e < p.N) ? p.bias[n + e] : 0.f;
     }
+  }
 #pragma unroll
   for (int i = 0; i < RM; ++i) {
     const int m = mb + 16 * i + mrow;

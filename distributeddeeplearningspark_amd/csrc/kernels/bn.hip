@@ -119,8 +119,10 @@ __global__ __launch_bounds__(256) void splitk_finalize_kernel(float4* __restrict
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
   if (g.active) {
     float b[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) b[i] = bias ? bias[g.cv * 8 + i] : 0.f;
+    const float4 b0 = bias ? reinterpret_cast<const float4*>(bias)[2 * g.cv] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 b1 = bias ? reinterpret_cast<const float4*>(bias)[2 * g.cv + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
+    b[0] = b0.x; b[1] = b0.y; b[2] = b0.z; b[3] = b0.w;
+    b[4] = b1.x; b[5] = b1.y; b[6] = b1.z; b[7] = b1.w;
     const long step = (long)gridDim.x * g.RT;
     for (long r = (long)blockIdx.x * g.RT + g.rt; r < M; r += step) {
       const long idx = r * g.CV + g.cv;

@@ -138,10 +138,14 @@ __global__ __launch_bounds__(gst::THREADS, 2) void gemm_stream_kernel(const Gemm
   }
   float bias_r[CF::RN][4];
 #pragma unroll
-  for (int rn = 0; rn < CF::RN; ++rn)
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      bias_r[rn][e] = p.bias ? p.bias[n0 + WN * w + 16 * rn + 4 * (lane >> 4) + e] : 0.f;
+  for (int rn = 0; rn < CF::RN; ++rn) {  // one 16-B load per 4 columns (N % panel == 0: always in range)
+    const float4 bv = p.bias ? *reinterpret_cast<const float4*>(p.bias + n0 + WN * w + 16 * rn + 4 * (lane >> 4))
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+    bias_r[rn][0] = bv.x;
+    bias_r[rn][1] = bv.y;
+    bias_r[rn][2] = bv.z;
+    bias_r[rn][3] = bv.w;
+  }
   wait_vm<0>();  // B fragments and bias in registers before the LDS-DMA ring starts
   auto tile_m0 = [&](int i) { return min((int)blockIdx.x + i * (int)gridDim.x, mt - 1) * BM; };
 
