@@ -45,13 +45,19 @@ __device__ __forceinline__ float warp_max(float v) {
 // Counter-based dropout: element `idx` of a call with seed `seed` is kept iff
 // hash(seed + idx) >= thresh (thresh = p * 2^32).  Stateless, so backward passes
 // regenerate the mask instead of storing it.
+// Counter hash of the dropout masks (x = seed + element index): the 64-bit counter is folded to
+// 32 bits (high word times the golden-ratio constant) and mixed by a 32-bit finaliser (xor-shift /
+// multiply, 'lowbias32').  Three 32-bit multiplies instead of the two 64-bit ones (~4 v_mul each)
+// of murmur's fmix64, which made the dropout-carrying LayerNorm / GEMM epilogues VALU-heavy.
+// Mirrored bit for bit by ops/transformer.py:drop_hash_ref.
 __device__ __forceinline__ uint32_t drop_hash(uint64_t x) {
-  x ^= x >> 33;
-  x *= 0xff51afd7ed558ccdULL;
-  x ^= x >> 33;
-  x *= 0xc4ceb9fe1a85ec53ULL;
-  x ^= x >> 33;
-  return (uint32_t)x;
+  uint32_t h = (uint32_t)x ^ ((uint32_t)(x >> 32) * 0x9E3779B9u);
+  h ^= h >> 16;
+  h *= 0x7FEB352Du;
+  h ^= h >> 15;
+  h *= 0x846CA68Bu;
+  h ^= h >> 16;
+  return h;
 }
 __device__ __forceinline__ bool drop_keep(uint64_t seed, uint64_t idx, uint32_t thresh) {
   return drop_hash(seed + idx) >= thresh;

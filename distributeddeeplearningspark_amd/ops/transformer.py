@@ -16,26 +16,19 @@ import torch
 from ._native import C, use_native
 from ._ref import accumulate, ref_grads
 
-_M1 = 0xFF51AFD7ED558CCD - (1 << 64)  # the mixing constants as signed int64 (wrap-around multiply)
-_M2 = 0xC4CEB9FE1A85EC53 - (1 << 64)
-
-
-def _srl33(x: torch.Tensor) -> torch.Tensor:
-    return (x >> 33) & 0x7FFFFFFF  # logical shift right by 33 of a 64-bit pattern
-
-
 def drop_hash_ref(seed: int, idx: torch.Tensor) -> torch.Tensor:
-    """``drop_hash`` of ddl_common.h on int64 tensors (returns the low 32 bits, int64)."""
+    """``drop_hash`` of ddl_common.h on int64 tensors (returns the 32-bit hash as int64)."""
     s = seed & 0xFFFFFFFFFFFFFFFF
     if s >= 1 << 63:
         s -= 1 << 64
-    x = idx.to(torch.int64) + s
-    x = x ^ _srl33(x)
-    x = x * _M1
-    x = x ^ _srl33(x)
-    x = x * _M2
-    x = x ^ _srl33(x)
-    return x & 0xFFFFFFFF
+    x = idx.to(torch.int64) + s  # wraps mod 2^64 like the device's uint64 add
+    m = 0xFFFFFFFF
+    h = (x & m) ^ ((((x >> 32) & m) * 0x9E3779B9) & m)
+    h = h ^ (h >> 16)
+    h = (h * 0x7FEB352D) & m
+    h = h ^ (h >> 15)
+    h = (h * 0x846CA68B) & m
+    return h ^ (h >> 16)
 
 
 def drop_thresh(p: float) -> int:
