@@ -151,7 +151,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
     gmv[u][0] = g0.x; gmv[u][1] = g0.y; gmv[u][2] = g0.z; gmv[u][3] = g0.w;
     gmv[u][4] = g1.x; gmv[u][5] = g1.y; gmv[u][6] = g1.z; gmv[u][7] = g1.w;
   }
-  // PF: the next row's dy / x vectors and statistics are loaded before this row's math
+  // PF: the next row's dy / x vectors and statistics are loaded before this row's math (VPL <= 2 only:
+  // the prefetched row costs 16 VGPRs per VPL and the VPL = 8 instantiation spilled)
   uint4 ndy[VPL], nx[VPL];
   float nmu = 0.f, nrs = 0.f;
   auto fetch = [&](long r) {
@@ -173,13 +174,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
         cdy[u] = ndy[u];
         cx[u] = nx[u];
       }
-    } else {
-      fetch(row);
-#pragma unroll
-      for (int u = 0; u < VPL; ++u) {
-        cdy[u] = ndy[u];
-        cx[u] = nx[u];
-      }
+    } else {  // loads stay inside the vector loop below (the VPL = 8 instantiation is at the VGPR limit)
+      nmu = mean[row];
+      nrs = rstd[row];
     }
     const float mu = nmu, rs = nrs;
     if (PF && row + nwaves < M) fetch(row + nwaves);
@@ -190,8 +187,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
       const int c = lane + 64 * u;
       if (c < nv) {
         float d[8], xv[8];
-        unpack8(cdy[u], d);
-        unpack8(cx[u], xv);
+        unpack8(PF ? cdy[u] : *reinterpret_cast<const uint4*>(dy + row * H + c * 8), d);
+        unpack8(PF ? cx[u] : *reinterpret_cast<const uint4*>(x + row * H + c * 8), xv);
         if (in_thresh) {  // dy arrives through the forward's output dropout
           const unsigned long long base = (unsigned long long)row * (unsigned long long)H + c * 8;
 #pragma unroll
@@ -456,7 +453,7 @@ int layernorm_fwd(const void* x, const float* gamma, const float* beta, void* y,
   if (nv <= 64) { if (PF) hipLaunchKernelGGL((ln_fwd_kernel<1, true>), grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed); else hipLaunchKernelGGL((ln_fwd_kernel<1, false>), grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed); }
   else if (nv <= 128) { if (PF) hipLaunchKernelGGL((ln_fwd_kernel<2, true>), grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed); else hipLaunchKernelGGL((ln_fwd_kernel<2, false>), grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed); }
   else if (nv <= 256) { if (PF) hipLaunchKernelGGL((ln_fwd_kernel<4, true>), grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed); else hipLaunchKernelGGL((ln_fwd_kernel<4, false>), grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed); }
-  else { if (PF) hipLaunchKernelGGL((ln_fwd_kernel<8, true>), grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed); else hipLaunchKernelGGL((ln_fwd_kernel<8, false>), grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed); }
+  else hipLaunchKernelGGL((ln_fwd_kernel<8, false>), grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed);
   return (int)hipGetLastError();
 }
 
@@ -491,8 +488,8 @@ int layernorm_bwd(const void* dy, const void* x, const float* mean, const float*
   auto DD = reinterpret_cast<bf16_t*>(dx_drop);
   if (nv <= 64) { if (PF) hipLaunchKernelGGL((ln_bwd_kernel<1, true>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts); else hipLaunchKernelGGL((ln_bwd_kernel<1, false>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts); }
   else if (nv <= 128) { if (PF) hipLaunchKernelGGL((ln_bwd_kernel<2, true>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts); else hipLaunchKernelGGL((ln_bwd_kernel<2, false>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts); }
-  else if (nv <= 256) { if (PF) hipLaunchKernelGGL((ln_bwd_kernel<4, true>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts); else hipLaunchKernelGGL((ln_bwd_kernel<4, false>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts); }
-  else { if (PF) hipLaunchKernelGGL((ln_bwd_kernel<8, true>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts); else hipLaunchKernelGGL((ln_bwd_kernel<8, false>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts); }
+  else if (nv <= 256) hipLaunchKernelGGL((ln_bwd_kernel<4, false>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts);
+  else hipLaunchKernelGGL((ln_bwd_kernel<8, false>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts);
   return (int)hipGetLastError();
 }
 
