@@ -372,11 +372,14 @@ def test_optimizers(kind):
 def test_normalize_u8_and_casts():
     from distributeddeeplearningspark_amd.data.ingest import DeviceFeeder
 
-    x = torch.randint(0, 256, (2, 8, 8, 3), dtype=torch.uint8, device=DEV)
     f = DeviceFeeder(DEV)
-    y = f.normalize(x)
-    ref = (x.float() - f.mean) * f.invstd
-    close(y, ref, what="normalize_u8")
+    # 4-pixel RGB kernel (pixel count % 4 == 0, incl. an ImageNet-size batch) and the per-element kernel
+    for shape in ((2, 8, 8, 3), (1, 5, 5, 3), (16, 224, 224, 3)):
+        x = torch.randint(0, 256, shape, dtype=torch.uint8, device=DEV)
+        y = f.normalize(x)
+        ref = (x.float() - f.mean) * f.invstd
+        close(y, ref, what=f"normalize_u8 {shape}")
+        assert torch.equal(y, ref.to(torch.bfloat16)), shape  # same fp32 formula, RNE to bf16
     a = torch.randn(1003, device=DEV)
     b = torch.empty(1003, dtype=torch.bfloat16, device=DEV)
     _C().cast_f32_bf16(a, b)
