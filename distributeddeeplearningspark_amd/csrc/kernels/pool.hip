@@ -138,6 +138,65 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const uint4* __restric
   }
 }
 
+// 3x3 / stride 2 / pad 1 (the ResNet stem pool): one lane per 2x2 block of input pixels.  The block's
+// pixels are covered by the same <= 2x2 windows (rows 2i, 2i+1 by windows i, i+1), so their four
+// (argmax, dy) pairs are loaded once for four outputs instead of once per covered pixel (9 loads
+// per block before).
+__global__ __launch_bounds__(256) void maxpool_bwd_k3s2p1_kernel(const uint4* __restrict__ dy,
+                                                                  const uint2* __restrict__ am, uint4* __restrict__ dx,
+                                                                  int N, int H, int W, int CV, int Ho, int Wo) {
+  const int HB = (H + 1) >> 1, WB = (W + 1) >> 1;
+  const uint32_t total = (uint32_t)N * HB * WB * CV;  // < 2^31 (launcher)
+  for (uint32_t v = blockIdx.x * 256u + threadIdx.x; v < total; v += gridDim.x * 256u) {
+    const uint32_t q = v / (uint32_t)CV, cv = v - q * (uint32_t)CV;
+    const uint32_t q2 = q / (uint32_t)WB;
+    const int bj = (int)(q - q2 * (uint32_t)WB);
+    const int bi = (int)(q2 % (uint32_t)HB);
+    const int n = (int)(q2 / (uint32_t)HB);
+    uint2 a[2][2];
+    float g[2][2][8];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int oh = bi + i, ow = bj + j;
+        if (oh < Ho && ow < Wo) {
+          const uint32_t o = (((uint32_t)n * Ho + oh) * Wo + ow) * (uint32_t)CV + cv;
+          a[i][j] = am[o];
+          unpack8p(dy[o], g[i][j]);
+        } else {
+          a[i][j] = make_uint2(0xffffffffu, 0xffffffffu);  // no window index matches 0xff
+#pragma unroll
+          for (int e = 0; e < 8; ++e) g[i][j][e] = 0.f;
+        }
+      }
+#pragma unroll
+    for (int pa = 0; pa < 2; ++pa)
+#pragma unroll
+      for (int pb = 0; pb < 2; ++pb) {
+        const int h = 2 * bi + pa, w = 2 * bj + pb;
+        if (h >= H || w >= W) continue;
+        float acc[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int dr = h + 1 - 2 * (bi + i), dc = w + 1 - 2 * (bj + j);  // position inside window
+            if (dr < 0 || dr > 2 || dc < 0 || dc > 2) continue;  // compile-time after unrolling
+            const uint32_t idx = (uint32_t)(dr * 3 + dc);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const uint32_t word = e < 4 ? a[i][j].x : a[i][j].y;
+              if (((word >> ((e & 3) * 8)) & 0xffu) == idx) acc[e] += g[i][j][e];
+            }
+          }
+        dx[(((uint32_t)n * H + h) * W + w) * (uint32_t)CV + cv] = pack8p(acc);
+      }
+  }
+}
+
 int maxpool_bwd(const void* dy, const uint8_t* argmax, void* dx, int N, int H, int W, int C, int Ho, int Wo, int kh,
                 int kw, int sh, int sw, int ph, int pw, hipStream_t s) {
   const long total = (long)N * H * W * (C / 8);
@@ -145,7 +204,11 @@ int maxpool_bwd(const void* dy, const uint8_t* argmax, void* dx, int N, int H, i
 #define DDL_POOL_BWD(A, B, C_, D)                                                                              \
   hipLaunchKernelGGL((maxpool_bwd_kernel<A, B, C_, D>), dim3(pgrid(total)), dim3(256), 0, s, (const uint4*)dy,  \
                      (const uint2*)argmax, (uint4*)dx, N, H, W, C / 8, Ho, Wo, kh, kw, sh, sw, ph, pw)
-  if (kh == 3 && kw == 3 && sh == 2 && sw == 2) DDL_POOL_BWD(3, 3, 2, 2);
+  if (kh == 3 && kw == 3 && sh == 2 && sw == 2 && ph == 1 && pw == 1 && Ho == (H - 1) / 2 + 1 && Wo == (W - 1) / 2 + 1) {
+    const long blocks = (long)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
+    hipLaunchKernelGGL(maxpool_bwd_k3s2p1_kernel, dim3(pgrid(blocks)), dim3(256), 0, s, (const uint4*)dy,
+                       (const uint2*)argmax, (uint4*)dx, N, H, W, C / 8, Ho, Wo);
+  } else if (kh == 3 && kw == 3 && sh == 2 && sw == 2) DDL_POOL_BWD(3, 3, 2, 2);
   else if (kh == 2 && kw == 2 && sh == 2 && sw == 2) DDL_POOL_BWD(2, 2, 2, 2);
   else if (kh <= 16 && kw <= 16 && sh >= 1 && sw >= 1) DDL_POOL_BWD(0, 0, 0, 0);
   else return (int)hipErrorInvalidValue;

@@ -54,7 +54,8 @@ def main():
     torch.cuda.synchronize()
     pr.disable()
     st = pstats.Stats(pr)
-    st.sort_stats("tottime").print_stats(35)
+    st.sort_stats("tottime").print_stats(45)
+    st.sort_stats("cumulative").print_stats(45)
 
 
 if __name__ == "__main__":
