@@ -433,11 +433,13 @@ def test_resnet50_step_matches_reference():
             else:
                 os.environ["DDL_BACKEND"] = old
     (lc, gc), (ll, gl), (lh, gh) = res["cpu"], res["gpu_lib"], res["gpu_hip"]
-    # bf16 end-to-end through 53 conv+BN layers at batch 16: both GPU paths (HIP kernels and
-    # the PyTorch/MIOpen library path) must sit within the same band around the fp32 CPU run
-    assert abs(lh - lc) < 0.12 * max(1.0, abs(lc)), res
+    # bf16 end-to-end through 53 conv+BN layers at batch 16.  Measured on MI355X: HIP path loss
+    # 2.461 vs fp32 CPU 2.440 (0.9 %), gradient norm 571.7 vs 580.5 (1.5 %); the PyTorch/MIOpen bf16
+    # path lands at loss 2.280 (6.6 %), so it only gets the loose band.  Per-layer gradients are
+    # pinned separately (test_resnet_per_layer_gradients_match_fp32_cpu).
+    assert abs(lh - lc) < 0.04 * max(1.0, abs(lc)), res
+    assert abs(gh - gc) < 0.04 * gc, res
     assert abs(ll - lc) < 0.12 * max(1.0, abs(lc)), res
-    assert abs(gh - gc) < 0.1 * gc, res
 
 
 def test_fused_bottleneck_matches_composed_ops():
