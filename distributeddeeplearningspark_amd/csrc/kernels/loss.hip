@@ -8,6 +8,19 @@
 
 namespace ddl {
 
+__device__ __forceinline__ void xent_unpack8(const uint4& u, float* f) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    f[2 * e] = __uint_as_float(w[e] << 16);
+    f[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ uint4 xent_pack8(const float* f) {
+  return make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]),
+                    pack_bf16x2(f[6], f[7]));
+}
+
 template <bool BF16>
 __device__ __forceinline__ float ld_logit(const void* p, long i) {
   if constexpr (BF16) return bf2f(reinterpret_cast<const bf16_t*>(p)[i]);
@@ -23,9 +36,28 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const void* __restric
   const int b = blockIdx.x;
   const long base = (long)b * ld;  // row stride ld >= K (padded vocabularies); tprob rows are dense [B][K]
   __shared__ float sm[2][4];
+  // vec: bf16 logits with 16-B aligned rows and class labels (the MLM decoder: 30,522-wide rows):
+  // both passes read 8 logits per lane per 16-B load (2-B loads before) and the gradient row is
+  // written as 16-B vectors; the last K % 8 columns take the scalar loop
+  const bool vec = BF16 && tprob == nullptr && (ld % 8) == 0 && ((uintptr_t)logits % 16) == 0 &&
+                   (dlogits == nullptr || ((uintptr_t)dlogits % 16) == 0);
+  const int KV = vec ? K / 8 : 0;
   // pass 1: online max / sum-exp
   float m = -INFINITY, s = 0.f;
-  for (int k = threadIdx.x; k < K; k += 256) {
+  for (int v = threadIdx.x; v < KV; v += 256) {
+    float f[8];
+    xent_unpack8(reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(logits) + base)[v], f);
+    float mv = f[0];
+#pragma unroll
+    for (int e = 1; e < 8; ++e) mv = fmaxf(mv, f[e]);
+    const float nm = fmaxf(m, mv);
+    float acc = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc += __expf(f[e] - nm);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + acc;
+    m = nm;
+  }
+  for (int k = KV * 8 + threadIdx.x; k < K; k += 256) {
     const float x = ld_logit<BF16>(logits, base + k);
     if (x > m) {
       s = s * __expf(m - x) + 1.f;
@@ -58,7 +90,19 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const void* __restric
   // pass 2: loss terms and gradient
   float lpart = 0.f;
   const float off = smooth / (float)K;
-  for (int k = threadIdx.x; k < K; k += 256) {
+  for (int v = threadIdx.x; v < KV; v += 256) {
+    float f[8], g[8];
+    xent_unpack8(reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(logits) + base)[v], f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = v * 8 + e;
+      const float t = ignored ? 0.f : (k == lab ? 1.f - smooth : 0.f) + off;
+      lpart += t * (lse - f[e]);
+      g[e] = ignored ? 0.f : (__expf(f[e] - lse) - t) * gscale;
+    }
+    if (dlogits) reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(dlogits) + base)[v] = xent_pack8(g);
+  }
+  for (int k = KV * 8 + threadIdx.x; k < K; k += 256) {
     const float x = ld_logit<BF16>(logits, base + k);
     const float p = __expf(x - lse);
     float t;

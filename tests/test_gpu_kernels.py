@@ -335,6 +335,26 @@ def test_softmax_xent(dtype):
     close(lg2.grad, lr.grad, rtol=2e-2, atol=1e-4, what="xent(probs) grad")
 
 
+def test_softmax_xent_padded_vocab():
+    """The MLM decoder's call: bf16 logits rows padded to 30,528 columns, the first 30,522 are the
+    vocabulary (16-B vector passes + a 2-column scalar tail); dlogits' padding columns come back 0."""
+    B, V, Vp = 96, 30522, 30528
+    full = rnd(B, Vp, scale=4.0, seed=31)
+    labels = torch.randint(0, V, (B,), device=DEV)
+    labels[5] = -100  # ignored row
+    loss_rows = torch.empty(B, device=DEV)
+    dl = torch.full((B, Vp), 7.0, dtype=torch.bfloat16, device=DEV)
+    n_valid = int((labels != -100).sum())
+    _C().softmax_xent(full[:, :V], labels, None, loss_rows, dl[:, :V], 1.0 / n_valid, 0.0, -100)
+    lr = full[:, :V].float().clone().requires_grad_(True)
+    ref = F.cross_entropy(lr, labels, ignore_index=-100, reduction="sum") / n_valid
+    ref.backward()
+    assert abs(loss_rows.sum().item() / n_valid - ref.item()) < 1e-3 * max(1.0, ref.item())
+    close(dl[:, :V], lr.grad, rtol=2e-2, atol=1e-6, what="padded-vocab xent grad")
+    assert torch.all(dl[:, V:] == 0)
+    assert torch.all(dl[5] == 0)
+
+
 # ----------------------------------------------------------------------------- optimizers
 @pytest.mark.parametrize("kind", ["sgd", "sgd_nesterov", "adam", "adamw", "adam_keras", "adagrad", "rmsprop"])
 def test_optimizers(kind):
