@@ -36,7 +36,12 @@ def test_attention_fwd_bwd(S, lens, drop):
     x = qkv.clone().requires_grad_(True)
     o = T.attention(x, B, S, NH, lens=lt, drop_p=drop, seed=77)
     do = rnd(B * S, NH * 64, seed=2)
+    # leave a NaN-filled block of dqkv's size in the caching allocator: the packed-layout backward
+    # allocates dqkv without a zero fill, so any element the kernels did not store would show up
+    dirty = torch.full_like(qkv, float("nan"))
+    del dirty
     o.backward(do)
+    assert torch.isfinite(x.grad).all()
     xr = qkv.float().requires_grad_(True)
     orf = T.attention_ref(xr, B, S, NH, 0, NH * 64, 2 * NH * 64, lt, 0.125, drop, 77)
     orf.backward(do.float())
