@@ -173,7 +173,8 @@ def comm_stats(ddp, pg):
     exposed = pg.max_scalar(exposed if exposed is not None else 0.0)
     full = pg.max_scalar(full if full is not None else 0.0)
     return {"comm_ms": round(full, 3), "exposed_comm_ms": round(exposed, 3), "bucket_mb": ddp.bucket_mb,
-            "buckets": len(ddp.buckets), "reduce_dtype": "bf16" if ddp._red is not None else "fp32",
+            "buckets": len(ddp.buckets), "reduce_dtype": "bf16" if ddp.bf16_algo is not None else "fp32",
+            "bf16_algo": ddp.bf16_algo, "optimizer_overlap": ddp.overlap_optimizer and ddp.model.optimizer.ranged_ok,
             "grad_mb": round(ddp.grad_bytes / 2**20, 1), "backend": pg.backend, "forced_pg": pg.forced}
 
 

@@ -56,6 +56,7 @@ int mse_fwd_bwd(const float* pred, const float* target, long n, float* loss, flo
 // ---------------- elementwise ----------------
 int cast_f32_bf16(const float* x, void* y, long n, hipStream_t s);
 int cast_bf16_f32(const void* x, float* y, long n, hipStream_t s);
+int sum_rows_bf16(const void* x, void* y, int R, long n, hipStream_t s);
 int relu_bwd(const void* dy, const void* y, void* dx, long n, hipStream_t s);
 int add_bf16(const void* a, const void* b, void* y, long n, hipStream_t s);
 int bias_grad(const void* dy, float* db, long M, int N, int accumulate, hipStream_t s);  // db[n] (+)= sum_m dy[m][n]

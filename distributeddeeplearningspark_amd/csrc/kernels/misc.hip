@@ -42,6 +42,34 @@ int cast_bf16_f32(const void* x, float* y, long n, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// y[i] = bf16( sum_r x[r][i] ) with an fp32 accumulator: the local reduction step of the bf16-wire
+// gradient all-reduce (parallel/ddp.py: all-to-all of bf16 chunks -> this sum -> all-gather), so the
+// sum over ranks is rounded to bf16 once instead of after every ring hop.  8 columns per lane
+// (n % 8 == 0, 16-B aligned rows: host check).
+__global__ __launch_bounds__(256) void sum_rows_bf16_kernel(const uint4* __restrict__ x, uint4* __restrict__ y, int R,
+                                                            long n8) {
+  GRID_LOOP(i, n8) {
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < R; ++r) {
+      const uint4 v = x[(long)r * n8 + i];
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        a[2 * q] += __uint_as_float(w[q] << 16);
+        a[2 * q + 1] += __uint_as_float(w[q] & 0xffff0000u);
+      }
+    }
+    y[i] = make_uint4(pack_bf16x2(a[0], a[1]), pack_bf16x2(a[2], a[3]), pack_bf16x2(a[4], a[5]),
+                      pack_bf16x2(a[6], a[7]));
+  }
+}
+
+int sum_rows_bf16(const void* x, void* y, int R, long n, hipStream_t s) {
+  const long n8 = n / 8;
+  hipLaunchKernelGGL(sum_rows_bf16_kernel, dim3(mgrid(n8)), dim3(256), 0, s, (const uint4*)x, (uint4*)y, R, n8);
+  return (int)hipGetLastError();
+}
+
 __global__ void relu_bwd_kernel(const bf16_t* dy, const bf16_t* y, bf16_t* dx, long n) {
   GRID_LOOP(i, n) dx[i] = bf2f(y[i]) > 0.f ? dy[i] : (bf16_t)0;
 }

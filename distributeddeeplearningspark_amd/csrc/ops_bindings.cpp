@@ -215,6 +215,14 @@ void cast_bf16_f32_(const at::Tensor& x, const at::Tensor& y) {
   at::DeviceGuard g(x.device());
   HIP_OK(cast_bf16_f32(x.data_ptr(), y.data_ptr<float>(), x.numel(), cur_stream()));
 }
+void sum_rows_bf16_(const at::Tensor& x, const at::Tensor& y) {
+  GPU(x); BF16(x); BF16(y);
+  CK(x.dim() == 2 && x.is_contiguous() && y.is_contiguous() && y.numel() == x.size(1), "sum_rows_bf16: x [R, n], y [n]");
+  CK(x.size(1) % 8 == 0 && (reinterpret_cast<uintptr_t>(x.data_ptr()) % 16) == 0 &&
+         (reinterpret_cast<uintptr_t>(y.data_ptr()) % 16) == 0, "sum_rows_bf16: n % 8 == 0, 16-B aligned rows");
+  at::DeviceGuard g(x.device());
+  HIP_OK(sum_rows_bf16(x.data_ptr(), y.data_ptr(), (int)x.size(0), x.size(1), cur_stream()));
+}
 void relu_bwd_(const at::Tensor& dy, const at::Tensor& y, const at::Tensor& dx) {
   GPU(dy); BF16(dy); BF16(y); BF16(dx);
   CK(dy.numel() == y.numel() && dx.numel() == y.numel(), "relu_bwd: sizes");
@@ -386,6 +394,7 @@ void register_ops(py::module& m) {
   m.def("avgpool_bwd", &avgpool_bwd_);
   m.def("softmax_xent", &softmax_xent_);
   m.def("cast_f32_bf16", &cast_f32_bf16_);
+  m.def("sum_rows_bf16", &sum_rows_bf16_);
   m.def("cast_bf16_f32", &cast_bf16_f32_);
   m.def("relu_bwd", &relu_bwd_);
   m.def("add_bf16", &add_bf16_);

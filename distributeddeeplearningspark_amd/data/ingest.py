@@ -115,7 +115,19 @@ class ShardLoader:
         self._xb = [buf(self.x) for _ in range(n_buffers)]
         self._yb = [buf(self.y) for _ in range(n_buffers)] if self.y is not None else []
         self._impl.set_buffers(self._xb, self._yb)
-        self._stream = torch.cuda.Stream(self.device) if pin else None
+        # the process-wide ingest side stream (one per device: co-located workers would otherwise
+        # each claim a hardware queue per loader)
+        if pin:
+            from ..trainers import ingest_stream
+
+            self._stream = ingest_stream(self.device)
+        else:
+            self._stream = None
+        self.n_buffers = int(n_buffers)
+        # pinned slots whose H2D copy may still be in flight: (slot, event), oldest first.  A slot
+        # goes back to the C++ filler only once its copy event has completed, so the host runs up to
+        # n_buffers - 2 batches ahead of the copies instead of synchronising on every batch.
+        self._inflight: list = []
         self.epoch = 0
 
     def __len__(self):
@@ -127,23 +139,39 @@ class ShardLoader:
             return t.clone()
         with torch.cuda.stream(self._stream):
             d = t.to(self.device, non_blocking=True)
+        # the compute stream reads d: the caching allocator must not hand its block to a later
+        # side-stream copy before that read is done
+        d.record_stream(torch.cuda.current_stream(self.device))
         return d
+
+    def _reap(self, keep: int):
+        """Release completed slots; block on the oldest copies until at most ``keep`` are in flight."""
+        while self._inflight and (len(self._inflight) > keep or self._inflight[0][1].query()):
+            slot, ev = self._inflight.pop(0)
+            ev.synchronize()
+            self._impl.release(slot)
 
     def __iter__(self):
         self._impl.start_epoch(self.epoch)
         self.epoch += 1
-        while True:
-            slot, n = self._impl.next()
-            if slot < 0:
-                return
-            xd = self._to_device(self._xb[slot], n)
-            yd = self._to_device(self._yb[slot], n) if self._yb else None
-            if self._stream is not None:
-                ev = torch.cuda.Event()
-                ev.record(self._stream)
-                torch.cuda.current_stream(self.device).wait_event(ev)
-                ev.synchronize()  # slot may be refilled only after its H2D copy landed
-            self._impl.release(slot)
-            if self.x_dtype is not None and xd.is_floating_point():
-                xd = xd.to(self.x_dtype)
-            yield xd, yd
+        keep = max(0, self.n_buffers - 2)  # the filler always owns >= 2 slots
+        try:
+            while True:
+                self._reap(keep)
+                slot, n = self._impl.next()
+                if slot < 0:
+                    return
+                xd = self._to_device(self._xb[slot], n)
+                yd = self._to_device(self._yb[slot], n) if self._yb else None
+                if self._stream is not None:
+                    ev = torch.cuda.Event()
+                    ev.record(self._stream)
+                    torch.cuda.current_stream(self.device).wait_event(ev)
+                    self._inflight.append((slot, ev))
+                else:
+                    self._impl.release(slot)
+                if self.x_dtype is not None and xd.is_floating_point():
+                    xd = xd.to(self.x_dtype)
+                yield xd, yd
+        finally:
+            self._reap(0)

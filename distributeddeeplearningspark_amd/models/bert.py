@@ -479,7 +479,10 @@ class BertForMaskedLM(Model):
         self.encoder = [BertLayer(c, i, name=f"{self.name}/encoder/layer_{i}") for i in range(c.num_hidden_layers)]
         self.head = BertMLMHead(c, name=self.name + "/cls/predictions")
         self._step = 0
-        self.dropout_seed = 1234
+        # the dropout hashes are seeded per replica: data-parallel ranks must not draw the same masks
+        from ..ops.act import _process_rank
+
+        self.dropout_seed = 1234 + 7919 * _process_rank()
         self.graph_capturable = False  # dropout hashes are seeded from a host step counter
 
     def sublayers(self):

@@ -279,12 +279,20 @@ class Model(Layer):
             x = torch.from_numpy(np.ascontiguousarray(x))
         x = torch.as_tensor(x)
         if x.is_floating_point():
-            x = x.to(self.device, self.compute_dtype, non_blocking=True)
-        else:
-            x = x.to(self.device, non_blocking=True)
-            if x.dtype == torch.uint8 and x.dim() == 4:
-                x = self.normalize_images(x)
-        return x
+            return x.to(self.device, self.compute_dtype, non_blocking=True)
+        x = x.to(self.device, non_blocking=True)
+        if self.takes_integer_inputs():
+            return x  # token ids (an Embedding first layer)
+        if x.dtype == torch.uint8 and x.dim() == 4 and (self.input_mean is not None or self.input_std is not None):
+            return self.normalize_images(x)  # uint8 NHWC pixels of a model that declares its normalisation
+        # any other integer / bool feature column: its values, in the compute dtype (the Dense / Conv
+        # kernels take floating inputs only)
+        return x.to(self.compute_dtype)
+
+    def takes_integer_inputs(self) -> bool:
+        """True when the first layer consumes integer ids (``Embedding``)."""
+        subs = self.sublayers()
+        return bool(subs) and type(subs[0]).__name__ == "Embedding"
 
     def normalize_images(self, x_u8: torch.Tensor) -> torch.Tensor:
         """uint8 NHWC -> compute dtype, (x - mean) / std per channel: one HIP pass on the GPU

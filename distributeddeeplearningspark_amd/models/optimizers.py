@@ -69,12 +69,45 @@ class Optimizer:
         return grad_scale
 
     def step(self, grad_scale: float = 1.0):
-        self.iterations += 1
-        a = self.arena
-        w16 = None if a.compute is a.master else a.compute
-        self._apply(a.master, a.grad, w16, self._grad_scale(grad_scale))
+        gs = self.begin_step(grad_scale)
+        self.apply_range(0, self.arena.numel, gs)
 
-    def _apply(self, w, g, w16, gs):
+    # ---------------------------------------------------------------- ranged steps
+    # The data-parallel engine updates the arena bucket by bucket, each slice as soon as its
+    # all-reduce has landed, so the optimizer sweep over the early buckets runs under the
+    # reduction of the last one (parallel/ddp.py).  One logical step = begin_step + apply_range
+    # over a partition of [0, numel); the update of every element is identical to ``step``.
+    def begin_step(self, grad_scale: float = 1.0) -> float:
+        """Advance the step counter (host and device) once; returns the effective grad scale."""
+        self.iterations += 1
+        if self.device_step is not None and self._device_tick:
+            K.step_tick(self.device_step)
+        return self._grad_scale(grad_scale)
+
+    def apply_range(self, lo: int, hi: int, gs: float):
+        """Update arena elements [lo, hi) (lo, hi multiples of the arena alignment)."""
+        if hi <= lo:
+            return
+        a = self.arena
+        sl = slice(int(lo), int(hi))
+        w16 = None if a.compute is a.master else a.compute[sl]
+        self._apply(a.master[sl], a.grad[sl], w16, gs, {k: v[sl] for k, v in self.state.items()})
+
+    def captured_update(self, gs: float = 1.0):
+        """The device-side part of one step (step-counter tick + full update) for a hipGraph
+        capture; the host counter is advanced per replay by the caller (models/step.py)."""
+        if self.device_step is not None and self._device_tick:
+            K.step_tick(self.device_step)
+        self.apply_range(0, self.arena.numel, gs)
+
+    @property
+    def ranged_ok(self) -> bool:
+        """A global gradient norm (clipnorm) needs every bucket reduced before any update."""
+        return self.clipnorm is None
+
+    _device_tick = False  # optimizers whose kernels read the device step counter (Adam family)
+
+    def _apply(self, w, g, w16, gs, st):
         raise NotImplementedError
 
 
@@ -89,8 +122,8 @@ class SGD(Optimizer):
         if self.momentum:
             self.state["momentum"] = self._zeros()
 
-    def _apply(self, w, g, w16, gs):
-        K.sgd_(w, g, self.state.get("momentum"), w16, lr=self.lr, momentum=self.momentum, dampening=self.dampening,
+    def _apply(self, w, g, w16, gs, st):
+        K.sgd_(w, g, st.get("momentum"), w16, lr=self.lr, momentum=self.momentum, dampening=self.dampening,
                weight_decay=self.weight_decay, nesterov=self.nesterov, grad_scale=gs)
 
     def get_config(self):
@@ -110,8 +143,10 @@ class Adam(Optimizer):
         self.state["m"] = self._zeros()
         self.state["v"] = self._zeros()
 
-    def _apply(self, w, g, w16, gs):
-        K.adam_(w, g, self.state["m"], self.state["v"], w16, lr=self.lr, beta1=self.b1, beta2=self.b2, eps=self.eps,
+    _device_tick = True
+
+    def _apply(self, w, g, w16, gs, st):
+        K.adam_(w, g, st["m"], st["v"], w16, lr=self.lr, beta1=self.b1, beta2=self.b2, eps=self.eps,
                 weight_decay=self.weight_decay, decoupled=self.decoupled, keras_eps=self.keras_eps,
                 step=self.iterations, grad_scale=gs, device_step=self.device_step)
 
@@ -137,8 +172,8 @@ class Adagrad(Optimizer):
     def _alloc(self):
         self.state["acc"] = self._zeros()
 
-    def _apply(self, w, g, w16, gs):
-        K.adagrad_(w, g, self.state["acc"], w16, lr=self.lr, eps=self.eps, weight_decay=self.weight_decay,
+    def _apply(self, w, g, w16, gs, st):
+        K.adagrad_(w, g, st["acc"], w16, lr=self.lr, eps=self.eps, weight_decay=self.weight_decay,
                    grad_scale=gs)
 
 
@@ -152,8 +187,8 @@ class RMSprop(Optimizer):
     def _alloc(self):
         self.state["acc"] = self._zeros()
 
-    def _apply(self, w, g, w16, gs):
-        K.rmsprop_(w, g, self.state["acc"], w16, lr=self.lr, rho=self.rho, eps=self.eps,
+    def _apply(self, w, g, w16, gs, st):
+        K.rmsprop_(w, g, st["acc"], w16, lr=self.lr, rho=self.rho, eps=self.eps,
                    weight_decay=self.weight_decay, grad_scale=gs)
 
 

@@ -85,8 +85,7 @@ class CompiledTrainStep:
         with torch.cuda.stream(s):
             with torch.cuda.graph(g, stream=s):
                 loss = m.backward_step(self.static_x, self.static_y)
-                m.optimizer._apply(m.arena.master, m.arena.grad,
-                                   None if m.arena.compute is m.arena.master else m.arena.compute, 1.0)
+                m.optimizer.captured_update(1.0)
                 self.static_loss = loss.detach().float()
         torch.cuda.current_stream(m.device).wait_stream(s)
         from ..ops.norm import _POOL

@@ -105,9 +105,25 @@ def activation(x, name: str):
 _SEEDS = itertools.count(0x5EED)
 
 
-def next_seed(base: int = 0) -> int:
-    """A fresh 63-bit dropout seed (host counter): each call draws an independent mask."""
-    return (int(base) * 0x9E3779B97F4A7C15 + next(_SEEDS) * 0xBF58476D1CE4E5B9) & 0x7FFFFFFFFFFFFFFF
+def _process_rank() -> int:
+    """This replica's rank (torch.distributed, else RANK / DDL_WORKER_RANK), 0 when alone."""
+    import os
+
+    try:
+        import torch.distributed as dist
+
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_rank()
+    except Exception:
+        pass
+    return int(os.environ.get("RANK", os.environ.get("DDL_WORKER_RANK", "0")) or 0)
+
+
+def next_seed(base: int | None = None) -> int:
+    """A fresh 63-bit dropout seed (host counter): each call draws an independent mask.  The
+    default ``base`` is the process rank, so data-parallel replicas draw different masks."""
+    b = _process_rank() + 1 if base is None else int(base)
+    return (b * 0x9E3779B97F4A7C15 + next(_SEEDS) * 0xBF58476D1CE4E5B9) & 0x7FFFFFFFFFFFFFFF
 
 
 class _DropoutFn(torch.autograd.Function):

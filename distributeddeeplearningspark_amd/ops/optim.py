@@ -27,14 +27,13 @@ def sgd_(w, g, mom, w16, *, lr, momentum=0.0, dampening=0.0, weight_decay=0.0, n
 
 def adam_(w, g, m, v, w16, *, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0, decoupled=False,
           keras_eps=False, step=1, grad_scale=1.0, device_step=None):
-    """``device_step``: optional fp32 GPU scalar holding the step count; it is incremented
-    on the device and the bias corrections are computed from it (graph-replay safe)."""
+    """``device_step``: optional fp32 GPU scalar holding the step count, already advanced for
+    this step by :func:`step_tick` (the optimizer does it once per step, before the first
+    ranged update); the bias corrections are computed from it on the device (graph-replay safe)."""
     bc1 = 1.0 - beta1 ** step
     bc2 = 1.0 - beta2 ** step
     if use_native(w):
         mode = (1 if decoupled else 0) | (2 if keras_eps else 0)
-        if device_step is not None:
-            C().step_tick(device_step)
         C().adam_step(w, g, m, v, w16, lr, beta1, beta2, eps, weight_decay, mode, bc1, bc2, grad_scale, device_step)
         return
     d = g * grad_scale
@@ -50,6 +49,14 @@ def adam_(w, g, m, v, w16, *, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay
         w.sub_(lr * (m / bc1) / (v.sqrt() / (bc2 ** 0.5) + eps))
     if w16 is not None and w16.data_ptr() != w.data_ptr():
         w16.copy_(w)
+
+
+def step_tick(device_step):
+    """+1 on the device step counter (one launch per optimizer step)."""
+    if use_native(device_step):
+        C().step_tick(device_step)
+    else:
+        device_step.add_(1.0)
 
 
 def adagrad_(w, g, acc, w16, *, lr, eps=1e-7, weight_decay=0.0, grad_scale=1.0):

@@ -18,13 +18,24 @@ collectives over xGMI:
   tens of MB.  Default 32 MB (``bucket_mb`` / ``DDL_BUCKET_MB``); the sweep that picks
   it is ``scripts/bench_allreduce.py``.  The bucket of the first layers is cut small
   (``DDL_TAIL_BUCKET_MB``, 4 MB): it is the one reduction that cannot overlap backward.
-* ``reduce_dtype=torch.bfloat16`` (``DDL_REDUCE_DTYPE=bf16``): each ready bucket is cast
-  to a bf16 mirror slice by a HIP kernel on the compute stream, the bf16 slice is
-  all-reduced (half the xGMI bytes), and after the last wait ONE HIP cast writes the
-  reduced values back into the fp32 gradient arena.  Accumulation across ranks is then
-  bf16 (RCCL sums in the wire dtype); the default stays fp32 for parity.
+* ``reduce_dtype=torch.bfloat16`` (``DDL_REDUCE_DTYPE=bf16``): half the xGMI bytes, with
+  ONE bf16 rounding of the cross-rank sum.  A ring all-reduce in bf16 would round every
+  partial sum (N-1 bf16 additions per element at N=8, RCCL sums in the wire dtype); instead
+  each bucket is cast to bf16 (HIP), exchanged with ONE all-to-all (rank r receives every
+  rank's r-th chunk: point-to-point over all 7 xGMI links), summed locally in fp32 by a HIP
+  kernel (``sum_rows_bf16``), and the summed chunks are all-gathered in bf16 and cast back
+  into the fp32 arena — the same 2(N-1)/N wire bytes as a ring all-reduce.  The all-to-all
+  of bucket i and the local sum + all-gather of bucket i-2 are pipelined through the hooks.
+  ``DDL_BF16_ALGO=ring`` keeps the plain bf16 ring all-reduce (accuracy comparison:
+  ``tests/test_ddp_cpu.py``); the default dtype stays fp32 for parity.
 * The 1/world averaging is folded into the optimizer kernel (``grad_scale``), so there
   is no separate scaling pass over the gradients.
+* Optimizer overlap: after backward, buckets are waited for in launch order and the fused
+  optimizer updates each bucket's slice of the arena as soon as that bucket is reduced
+  (``Optimizer.apply_range``), so the update of the early buckets runs under the reduction of
+  the last one — the first layers' bucket (ResNet's stem, BERT's 94 MB word-embedding table,
+  whose lookup gradient is only final at the very end of backward) is the one all-reduce
+  that can never overlap backward, and it now overlaps the optimizer sweep instead.
 * Timing (``timing=True``): HIP events on the compute stream bracket the part of the
   step that waits for communication (end of backward -> all buckets reduced), giving the
   *exposed* communication time; :meth:`measure_allreduce` times the full-gradient
@@ -63,6 +74,68 @@ def all_reduce_flat(pg: ProcessGroup, t: torch.Tensor, bucket_bytes: int = 64 <<
     return t
 
 
+def _bf16_algo() -> str:
+    v = os.environ.get("DDL_BF16_ALGO", "a2a").lower()
+    if v not in ("a2a", "ring"):
+        raise ValueError(f"DDL_BF16_ALGO={v!r}: expected a2a or ring")
+    return v
+
+
+def _sum_rows_bf16(x: torch.Tensor, y: torch.Tensor):
+    """y = bf16(sum over rows of x) with an fp32 accumulator (HIP on the GPU)."""
+    from ..ops._native import C, use_native
+
+    if use_native(x):
+        C().sum_rows_bf16(x, y)
+    else:
+        y.copy_(x.float().sum(0))
+
+
+class _A2ABucket:
+    """bf16-wire reduction of one bucket: cast -> all-to-all -> fp32 local sum -> all-gather -> cast back.
+    ``start`` / ``middle`` / ``finish`` are the three collective phases; each collective is async and
+    the compute stream waits on it (device-side) only at the next phase."""
+
+    def __init__(self, view: torch.Tensor, pg: ProcessGroup):
+        import torch.distributed as dist
+
+        self.dist = dist
+        self.view, self.pg = view, pg
+        N = pg.world_size
+        L = view.numel()
+        chunk = -(-L // N)  # ceil(L / N) elements per rank, rounded up to 64 (16-B rows)
+        chunk = -(-chunk // 64) * 64
+        self.L, self.N, self.chunk = L, N, chunk
+        dev = view.device
+        self.send = torch.zeros(N * chunk, dtype=torch.bfloat16, device=dev)  # pad tail stays zero
+        self.recv = torch.empty(N * chunk, dtype=torch.bfloat16, device=dev)
+        self.gath = torch.empty(N * chunk, dtype=torch.bfloat16, device=dev)
+        self.mine = torch.empty(chunk, dtype=torch.bfloat16, device=dev)
+        self.w1 = self.w2 = None
+        self.phase = 0
+
+    def start(self):
+        _cast(self.view, self.send[: self.L])
+        self.w1 = self.dist.all_to_all_single(self.recv, self.send, group=self.pg.group, async_op=True)
+        self.phase = 1
+
+    def middle(self):
+        if self.phase != 1:
+            return
+        self.w1.wait()
+        _sum_rows_bf16(self.recv.view(self.N, self.chunk), self.mine)
+        self.w2 = self.dist.all_gather_into_tensor(self.gath, self.mine, group=self.pg.group, async_op=True)
+        self.phase = 2
+
+    def finish(self):
+        self.middle()
+        if self.phase != 2:
+            return
+        self.w2.wait()
+        _cast(self.gath[: self.L], self.view)
+        self.phase = 3
+
+
 def _cast(src: torch.Tensor, dst: torch.Tensor):
     """fp32 <-> bf16 over flat slices: HIP kernels on the GPU, torch on the CPU."""
     from ..ops._native import C, use_native
@@ -91,11 +164,20 @@ class DataParallel:
             raise ValueError(f"reduce_dtype {self.reduce_dtype}: expected torch.float32 or torch.bfloat16")
         model._ensure_placed()
         self.arena = model.arena
-        self._red = None  # bf16 mirror of the gradient arena (allocated once)
+        self._red = None  # bf16 mirror of the gradient arena (ring algorithm, allocated once)
+        self.bf16_algo = None
         if self.reduce_dtype == torch.bfloat16 and pg.distributed:
-            self._red = torch.zeros(self.arena.numel, dtype=torch.bfloat16, device=self.arena.grad.device)
+            # all-to-all + local fp32 sum; host-staged (co-located gloo) groups keep the ring
+            self.bf16_algo = "ring" if pg.host_staged else _bf16_algo()
+            if self.bf16_algo == "ring":
+                self._red = torch.zeros(self.arena.numel, dtype=torch.bfloat16, device=self.arena.grad.device)
         self._build_buckets()
+        self._a2a = None
+        if self.bf16_algo == "a2a":
+            self._a2a = [_A2ABucket(self.arena.grad[b["start"]: b["end"]], pg) for b in self.buckets]
         self._works = []
+        # optimizer overlap (see module doc): each bucket's arena slice is updated once it is reduced
+        self.overlap_optimizer = os.environ.get("DDL_OVERLAP_OPTIMIZER", "1") != "0"
         self.timing = bool(timing) and self.arena.grad.is_cuda
         self._events = []  # (backward done, comm done) per timed step
         if self.overlap:
@@ -105,7 +187,7 @@ class DataParallel:
     def _build_buckets(self):
         params = [p for p in self.arena.params if p.trainable]
         # bucket size is counted in WIRE bytes, so a bf16 reduce packs twice the elements
-        wire = 2 if self._red is not None else 4
+        wire = 2 if self.bf16_algo is not None else 4
         elems_per_bucket = max(self.bucket_bytes // wire, 256)
         # The bucket holding the FIRST layers launches only after the whole backward is done, so
         # its all-reduce is never hidden: it is cut from the front of the arena at a small size
@@ -136,6 +218,12 @@ class DataParallel:
             buckets[0]["end"] = self.arena.numel  # include the alignment tail
             buckets[-1]["start"] = 0
         self.buckets = buckets
+        # optimizer ranges: a partition of [0, numel) in bucket launch order (bucket i owns
+        # [start_i, start_{i-1}), so gaps of non-trainable parameters are covered too)
+        prev = self.arena.numel
+        for b in buckets:
+            b["opt_range"] = (b["start"], prev)
+            prev = b["start"]
         self.bucket_of = {}
         for i, b in enumerate(buckets):
             for p in b["params"]:
@@ -173,22 +261,50 @@ class DataParallel:
     def _launch(self, i):
         b = self.buckets[i]
         view = self.arena.grad[b["start"] : b["end"]]
+        if self._a2a is not None:
+            # second phase (local sum + all-gather) of the bucket launched two before: a fixed
+            # schedule, so every rank issues the collectives in the same order (a completion-driven
+            # choice would differ between ranks and deadlock)
+            if i >= 2:
+                self._a2a[i - 2].middle()
+            self._a2a[i].start()
+            self._works.append(None)
+            return
         if self._red is not None:
             red = self._red[b["start"] : b["end"]]
             _cast(view, red)  # on the compute stream: ordered after the bucket's last grad kernel
             view = red
         self._works.append(self.pg.all_reduce_(view, async_op=True))
 
-    def _finish(self):
+    def _wait_bucket(self, i):
+        """Compute stream waits (device-side) until bucket i is fully reduced into the fp32 arena."""
+        if self._a2a is not None:
+            self._a2a[i].finish()
+            return
+        w = self._works[i]
+        if w is not None:
+            w.wait()
+        if self._red is not None:
+            b = self.buckets[i]
+            _cast(self._red[b["start"] : b["end"]], self.arena.grad[b["start"] : b["end"]])
+
+    def _finish(self, optimizer=None, grad_scale: float = 1.0, reduced_event=None) -> bool:
+        """Launch what is left, then wait bucket by bucket.  With ``optimizer`` (ranged-capable),
+        each bucket's arena slice is updated right after its wait; returns True if it stepped.
+        ``reduced_event`` is recorded on the compute stream once the LAST bucket is reduced."""
         for i in range(self._next, len(self.buckets)):
             self._launch(i)
         self._next = len(self.buckets)
-        for w in self._works:
-            if w is not None:
-                w.wait()  # compute stream waits for the RCCL stream (no host block)
+        ranged = optimizer is not None and optimizer.ranged_ok and self.overlap_optimizer
+        gs = optimizer.begin_step(grad_scale) if ranged else None
+        for i, b in enumerate(self.buckets):
+            self._wait_bucket(i)
+            if reduced_event is not None and i == len(self.buckets) - 1:
+                reduced_event.record()
+            if ranged:
+                optimizer.apply_range(*b["opt_range"], gs)
         self._works = []
-        if self._red is not None:
-            _cast(self._red, self.arena.grad)
+        return ranged
 
     def sync_gradients(self, arena=None) -> float:
         """All-reduce every bucket (no overlap) — returns the averaging grad scale."""
@@ -230,16 +346,24 @@ class DataParallel:
             if self.timing and self.pg.distributed:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 ev[0].record()
+            stepped = False
             with phase("allreduce"):
-                if self.overlap:
-                    self._finish()
-                elif self.pg.distributed:
-                    self.sync_gradients()
+                if self.pg.distributed:
+                    if not self.overlap:
+                        self._begin()
+                    # the optimizer rides bucket by bucket behind the waits (a per-phase timer keeps
+                    # the two apart, so its phase GPU times stay attributable).  Exposed comm = end of
+                    # backward -> last bucket reduced; with the ranged optimizer that window also
+                    # holds the update of every earlier bucket, so it is an upper bound.
+                    stepped = self._finish(m.optimizer if timer is None else None, 1.0 / self.pg.world_size,
+                                           reduced_event=None if ev is None else ev[1])
             if ev is not None:
-                ev[1].record()
+                if not self.pg.distributed or not self.buckets:
+                    ev[1].record()
                 self._events.append(ev)
-            with phase("optimizer"):
-                m.optimizer.step(grad_scale=1.0 / self.pg.world_size)
+            if not stepped:
+                with phase("optimizer"):
+                    m.optimizer.step(grad_scale=1.0 / self.pg.world_size)
         return loss.detach()
 
     def exposed_comm_ms(self, reset: bool = True) -> float | None:
@@ -275,7 +399,13 @@ class DataParallel:
         """Bytes each rank puts through the all-reduce per step."""
         if not self.pg.distributed:
             return 0
-        return self.arena.grad.numel() * (2 if self._red is not None else 4)
+        return self.arena.grad.numel() * (2 if self.bf16_algo is not None else 4)
+
+    def bucket_report(self) -> list[dict]:
+        """Launch-order bucket table: index, MB on the wire, first/last parameter names."""
+        wire = 2 if self.bf16_algo is not None else 4
+        return [{"index": i, "mb": (b["end"] - b["start"]) * wire / (1 << 20), "params": len(b["params"]),
+                 "first": b["params"][0].name, "last": b["params"][-1].name} for i, b in enumerate(self.buckets)]
 
     def check_replicas(self, raise_on_mismatch: bool = True) -> bool:
         """Divergence detection: after a synchronous update every replica must

@@ -31,6 +31,10 @@ Execution (MI355X-native, not a socket parameter server):
       SynchronousDataParallel (new)  per-step bucketed gradient all-reduce, overlapped
     These are the synchronous equivalents of dist-keras' asynchronous commits
     (no stale updates are applied in the default ``mode="sync"``).
+  * ``mode="sync-grad"``: the per-step gradient all-reduce of ``SynchronousDataParallel``
+    (bucketed RCCL, overlapped with backward) under the dist-keras constructor, i.e.
+    ``ADAG(..., communication_window=1, mode='sync-grad')``; ``num_updates``
+    then counts synchronous steps.
   * ``mode="async"`` (constructor kwarg) reproduces the reference's true asynchrony:
     the driver hosts the native C++ TCP parameter server (``parallel/ps.py``,
     ``csrc/runtime/param_server.cpp``) and workers pull/commit without barriers; DynSGD's
@@ -460,6 +464,9 @@ _WORKERS = {"adag": _AdagWorker, "dynsgd": _DynSGDWorker, "downpour": _DownpourW
             "ensemble": _EnsembleWorker, "single": _EnsembleWorker, "syncdp": _SyncDPWorker}
 
 
+_MODES = ("sync", "async", "sync-grad")
+
+
 def _train_worker(rank, world, pg, cfg, blob, X, Y, sizes):
     t0 = time.time()
     model = deserialize_keras_model({k: v for k, v in blob.items() if k not in ("optimizer", "loss")})
@@ -477,6 +484,8 @@ def _train_worker(rank, world, pg, cfg, blob, X, Y, sizes):
     cls = _WORKERS[cfg["algorithm"]]
     if cfg.get("mode") == "async" and issubclass(cls, _CommitWorker):
         cls = _AsyncPSWorker
+    elif cfg.get("mode") == "sync-grad":
+        cls = _SyncDPWorker
     w = cls(cfg, model, pg, sizes)
     w.watchdog = None
     if cfg.get("watchdog_s"):
@@ -584,6 +593,12 @@ class _ShardedTrainer(Trainer):
         self.master_port = master_port
         self.device = device
         self.seed = seed
+        mode = extra.get("mode", "sync")
+        if mode not in _MODES:
+            raise ValueError(f"mode={mode!r}: expected one of {_MODES}")
+        if mode == "sync-grad" and self.communication_window != 1:
+            warnings.warn(f"mode='sync-grad' all-reduces gradients every step: communication_window="
+                          f"{self.communication_window} is ignored", RuntimeWarning, stacklevel=3)
         self.extra = extra
 
     def _cfg(self):

@@ -82,9 +82,19 @@ def save_checkpoint(directory: str, model, step: int = 0, optimizer=None, extra:
 
 def _prune(directory, keep):
     ck = sorted(d for d in os.listdir(directory) if d.startswith("step_"))
-    for d in ck[:-keep] if keep > 0 else []:
+    if keep <= 0 or not ck:
+        return
+    for d in ck[:-keep]:
         shutil.rmtree(os.path.join(directory, d), ignore_errors=True)
-        shutil.rmtree(os.path.join(directory, "ranks", d), ignore_errors=True)
+    # per-rank state is pruned against the keep window on its own: a run killed after the rank
+    # files were written but before rank 0 published that step leaves a ranks/step_<n> with no
+    # published step_<n>; anything older than the oldest kept step is stale either way
+    oldest = ck[-keep] if len(ck) >= keep else ck[0]
+    rdir = os.path.join(directory, "ranks")
+    if os.path.isdir(rdir):
+        for d in os.listdir(rdir):
+            if d.startswith("step_") and d < oldest:
+                shutil.rmtree(os.path.join(rdir, d), ignore_errors=True)
 
 
 def _rank_file(directory: str, step: int, rank: int) -> str:

@@ -23,6 +23,7 @@ def _model(hw=16):
     m = Sequential([Conv2D(16, (3, 3), input_shape=(hw, hw, 3)), Activation("relu"), Flatten(),
                     Dense(10, activation="softmax")])
     m.compile("sgd", "sparse_categorical_crossentropy")
+    m.input_mean, m.input_std = (0.0, 0.0, 0.0), (255.0, 255.0, 255.0)  # uint8 pixels -> [0, 1] on the device
     return m
 
 
@@ -61,3 +62,29 @@ def test_gpu_predictor_on_uint8_frame():
     np.testing.assert_allclose(p.sum(1), 1.0, atol=2e-2)  # bf16 softmax rows
     ref = m.predict(imgs, batch_size=70)
     np.testing.assert_allclose(p, ref, atol=1e-3)
+
+
+def test_shard_loader_host_runs_ahead_of_copies():
+    """The streaming loader hands out batches while their H2D copies are still in flight: the
+    compute stream is kept busy so the host runs several batches ahead, and every batch must
+    still equal the resident slice (the slot is reused only after its copy event completed, and
+    the batch tensors are recorded on the compute stream)."""
+    from distributeddeeplearningspark_amd.data.ingest import ShardLoader
+
+    rng = np.random.default_rng(3)
+    X = rng.integers(0, 256, (40 * 64, 96, 96, 3), dtype=np.uint8)  # 27 KB rows, 1.7 MB per batch
+    Y = np.arange(X.shape[0], dtype=np.int64)
+    loader = ShardLoader(X, Y, 64, device="cuda:0", n_buffers=4)
+    busy = torch.randn(2048, 2048, device="cuda:0")
+    sums = []
+    for xd, yd in loader:
+        for _ in range(3):  # keep the compute stream behind the host
+            busy = busy @ busy
+            busy = busy / busy.norm()
+        sums.append((xd.to(torch.int64).sum(dim=(1, 2, 3)), yd.clone()))
+    torch.cuda.synchronize()
+    assert len(sums) == 40
+    for b, (s, yd) in enumerate(sums):
+        ref = torch.from_numpy(X[b * 64:(b + 1) * 64].astype(np.int64).sum(axis=(1, 2, 3)))
+        assert torch.equal(s.cpu(), ref), b
+        assert torch.equal(yd.cpu(), torch.from_numpy(Y[b * 64:(b + 1) * 64]))
