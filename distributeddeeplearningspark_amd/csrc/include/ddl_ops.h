@@ -49,7 +49,10 @@ int avgpool_global_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream
 // loss_rows[b] = CE; dlogits = (softmax - target) * grad_scale  (same dtype as logits)
 int softmax_xent(const void* logits, int logits_bf16, const int64_t* labels, const float* target_probs,
                  float* loss_rows, void* dlogits, int B, int K, long ld, float grad_scale, float label_smoothing,
-                 int ignore_index, hipStream_t s);
+                 int ignore_index, hipStream_t s, const float* grad_scale_dev = nullptr);
+int label_count_inv(const int64_t* labels, long n, int ignore_index, float* inv, hipStream_t s);
+int rows_sum_scaled(const float* rows, long n, float scale, const float* dev, float* out, hipStream_t s);
+int scale_bf16_dev(void* x, long n, const float* s_dev, hipStream_t s);
 // loss[0] = mean((pred - target)^2); grad = 2 (pred - target) / n  (fp32, one launch)
 int mse_fwd_bwd(const float* pred, const float* target, long n, float* loss, float* grad, hipStream_t s);
 
@@ -122,6 +125,7 @@ int layernorm_bwd(const void* dy, const void* x, const float* mean, const float*
 // word-embedding gradient from tokens sorted by id (no atomics); position gradient (sum over batch)
 int embed_word_grad(const int64_t* sorted_ids, const int64_t* perm, const void* ds, float* gword, long T, int H,
                     hipStream_t s);
+int embed_word_grad_atomic(const int64_t* ids, const void* ds, float* gword, long T, int H, long V, hipStream_t s);
 int embed_pos_grad(const void* ds, float* gpos, int B, int S, int H, hipStream_t s);
 // out[n] (+)= sum_p ws[p][n]
 int colsum_partials(const float* ws, int P, int N, float* out, int accumulate, hipStream_t s, long ld = 0);

@@ -404,6 +404,28 @@ __global__ __launch_bounds__(256) void embed_word_grad_kernel(const int64_t* __r
   }
 }
 
+// word-embedding gradient without a sort: gword[ids[t]][h] += ds[t][h] as no-return fp32 atomics
+// (executed at the memory side, ~1.3 TB/s of added bytes on MI355X: 16384 x 768 tokens x columns in
+// ~40 us, vs ~105 us for the sorted one-writer walk, which also needed a radix sort of the ids).
+// Lane i of a wave adds columns 2i, 2i+1 of one token row per step (one 4-B load of a bf16 pair).
+__global__ __launch_bounds__(256) void embed_word_grad_atomic_kernel(const int64_t* __restrict__ ids,
+                                                                    const uint32_t* __restrict__ ds,
+                                                                    float* __restrict__ gword, long T, int H,
+                                                                    long V) {
+  const int HP = H >> 1;  // bf16 pairs per row
+  const long n = T * HP;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const long t = i / HP;
+    const int c = (int)(i - t * HP) * 2;
+    const int64_t id = ids[t];
+    if ((uint64_t)id >= (uint64_t)V) continue;  // an out-of-vocabulary id adds nothing (never a wild write)
+    const uint32_t w = ds[i];
+    float* g = gword + id * H + c;
+    atomicAdd(g, __uint_as_float(w << 16));
+    atomicAdd(g + 1, __uint_as_float(w & 0xffff0000u));
+  }
+}
+
 // position-embedding gradient: gpos[s][h] += sum_b ds[b*S + s][h]  (column sums, no atomics)
 __global__ __launch_bounds__(256) void embed_pos_grad_kernel(const bf16_t* __restrict__ ds, float* __restrict__ gpos,
                                                             int B, int S, int H) {
@@ -520,6 +542,15 @@ int embed_word_grad(const int64_t* sorted_ids, const int64_t* perm, const void* 
   const long waves = (T + kEmbChunk - 1) / kEmbChunk;
   hipLaunchKernelGGL(embed_word_grad_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, sorted_ids, perm,
                      reinterpret_cast<const bf16_t*>(ds), gword, T, H);
+  return (int)hipGetLastError();
+}
+
+int embed_word_grad_atomic(const int64_t* ids, const void* ds, float* gword, long T, int H, long V, hipStream_t s) {
+  if (T <= 0) return 0;
+  const long n = T * (H / 2);
+  const long blocks = std::min<long>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(embed_word_grad_atomic_kernel, dim3((unsigned)blocks), dim3(256), 0, s, ids,
+                     reinterpret_cast<const uint32_t*>(ds), gword, T, H, V);
   return (int)hipGetLastError();
 }
 

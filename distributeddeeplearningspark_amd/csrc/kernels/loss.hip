@@ -32,8 +32,9 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const void* __restric
                                                             const int64_t* __restrict__ labels,
                                                             const float* __restrict__ tprob, float* loss_rows,
                                                             void* dlogits, int K, long ld, float gscale, float smooth,
-                                                            int ignore_index) {
+                                                            int ignore_index, const float* __restrict__ gscale_dev) {
   const int b = blockIdx.x;
+  if (gscale_dev) gscale *= gscale_dev[0];  // device-resident factor (e.g. 1 / #valid labels: no host sync)
   const long base = (long)b * ld;  // row stride ld >= K (padded vocabularies); tprob rows are dense [B][K]
   __shared__ float sm[2][4];
   // vec: bf16 logits with 16-B aligned rows and class labels (the MLM decoder: 30,522-wide rows):
@@ -130,14 +131,58 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const void* __restric
 
 int softmax_xent(const void* logits, int logits_bf16, const int64_t* labels, const float* target_probs,
                  float* loss_rows, void* dlogits, int B, int K, long ld, float grad_scale, float label_smoothing,
-                 int ignore_index, hipStream_t s) {
+                 int ignore_index, hipStream_t s, const float* grad_scale_dev) {
   if (B <= 0) return 0;
   if (logits_bf16)
     hipLaunchKernelGGL(softmax_xent_kernel<true>, dim3(B), dim3(256), 0, s, logits, labels, target_probs, loss_rows,
-                       dlogits, K, ld, grad_scale, label_smoothing, ignore_index);
+                       dlogits, K, ld, grad_scale, label_smoothing, ignore_index, grad_scale_dev);
   else
     hipLaunchKernelGGL(softmax_xent_kernel<false>, dim3(B), dim3(256), 0, s, logits, labels, target_probs, loss_rows,
-                       dlogits, K, ld, grad_scale, label_smoothing, ignore_index);
+                       dlogits, K, ld, grad_scale, label_smoothing, ignore_index, grad_scale_dev);
+  return (int)hipGetLastError();
+}
+
+// inv[0] = 1 / max(1, #labels != ignore_index): the masked-LM loss normaliser computed on the device,
+// so a batch without a host-side num_masked costs no device -> host sync
+__global__ __launch_bounds__(1024) void label_count_inv_kernel(const int64_t* __restrict__ labels, long n, int ignore,
+                                                               float* __restrict__ inv) {
+  __shared__ float part[16];
+  float c = 0.f;
+  for (long i = threadIdx.x; i < n; i += 1024) c += labels[i] != (int64_t)ignore ? 1.f : 0.f;
+  c = warp_sum(c);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < 16; ++w) t += part[w];
+    inv[0] = 1.f / fmaxf(t, 1.f);
+  }
+}
+
+int label_count_inv(const int64_t* labels, long n, int ignore_index, float* inv, hipStream_t s) {
+  hipLaunchKernelGGL(label_count_inv_kernel, dim3(1), dim3(1024), 0, s, labels, n, ignore_index, inv);
+  return (int)hipGetLastError();
+}
+
+// out[0] = scale * sum(rows) with scale = host factor * (dev ? dev[0] : 1): the per-row losses of the
+// fused softmax-xent reduced to the scalar loss in one launch (no ATen reduce + divide)
+__global__ __launch_bounds__(1024) void rows_sum_scaled_kernel(const float* __restrict__ rows, long n, float scale,
+                                                               const float* __restrict__ dev, float* __restrict__ out) {
+  __shared__ float part[16];
+  float a = 0.f;
+  for (long i = threadIdx.x; i < n; i += 1024) a += rows[i];
+  a = warp_sum(a);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = a;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < 16; ++w) t += part[w];
+    out[0] = t * scale * (dev ? dev[0] : 1.f);
+  }
+}
+
+int rows_sum_scaled(const float* rows, long n, float scale, const float* dev, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(rows_sum_scaled_kernel, dim3(1), dim3(1024), 0, s, rows, n, scale, dev, out);
   return (int)hipGetLastError();
 }
 

@@ -70,6 +70,26 @@ int sum_rows_bf16(const void* x, void* y, int R, long n, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// x *= s_dev[0] in place (bf16): an upstream gradient that lives on the device (a loss node's
+// incoming gradient), applied without reading it back to the host
+__global__ __launch_bounds__(256) void scale_bf16_dev_kernel(uint4* __restrict__ x, long n8, const float* __restrict__ sd) {
+  const float sc = sd[0];
+  GRID_LOOP(i, n8) {
+    const uint4 v = x[i];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      o[q] = pack_bf16x2(__uint_as_float(w[q] << 16) * sc, __uint_as_float(w[q] & 0xffff0000u) * sc);
+    x[i] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+int scale_bf16_dev(void* x, long n, const float* s_dev, hipStream_t s) {
+  hipLaunchKernelGGL(scale_bf16_dev_kernel, dim3(mgrid(n / 8)), dim3(256), 0, s, (uint4*)x, n / 8, s_dev);
+  return (int)hipGetLastError();
+}
+
 __global__ void relu_bwd_kernel(const bf16_t* dy, const bf16_t* y, bf16_t* dx, long n) {
   GRID_LOOP(i, n) dx[i] = bf2f(y[i]) > 0.f ? dy[i] : (bf16_t)0;
 }

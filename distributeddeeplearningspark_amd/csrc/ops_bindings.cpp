@@ -179,7 +179,7 @@ void avgpool_bwd_(const at::Tensor& dy, const at::Tensor& dx) {
 // ---------------------------------------------------------------- loss
 void softmax_xent_(const at::Tensor& logits, c10::optional<at::Tensor> labels, c10::optional<at::Tensor> probs,
                    const at::Tensor& loss_rows, c10::optional<at::Tensor> dlogits, double grad_scale, double smoothing,
-                   int64_t ignore_index) {
+                   int64_t ignore_index, c10::optional<at::Tensor> grad_scale_dev) {
   GPU(logits);
   CK(logits.dim() == 2 && logits.stride(1) == 1 && logits.stride(0) >= logits.size(1),
      "softmax_xent: logits [B,K] with unit column stride");
@@ -196,10 +196,35 @@ void softmax_xent_(const at::Tensor& logits, c10::optional<at::Tensor> labels, c
     CK(dlogits->scalar_type() == logits.scalar_type() && dlogits->dim() == 2 && dlogits->size(0) == B &&
            dlogits->stride(0) == ld && dlogits->stride(1) == 1,
        "dlogits: same layout as logits");
+  if (grad_scale_dev) { F32(*grad_scale_dev); CK(grad_scale_dev->numel() == 1 && grad_scale_dev->is_cuda(), "grad_scale_dev: one fp32 on the GPU"); }
   at::DeviceGuard g(logits.device());
   HIP_OK(softmax_xent(logits.data_ptr(), bf ? 1 : 0, optr<const int64_t>(labels), optr<const float>(probs),
                       loss_rows.data_ptr<float>(), optr<void>(dlogits), B, K, ld, (float)grad_scale, (float)smoothing,
-                      (int)ignore_index, cur_stream()));
+                      (int)ignore_index, cur_stream(), optr<const float>(grad_scale_dev)));
+}
+
+void label_count_inv_(const at::Tensor& labels, int64_t ignore_index, const at::Tensor& inv) {
+  GPU(labels); F32(inv);
+  CK(labels.scalar_type() == at::kLong && labels.is_contiguous() && inv.numel() == 1, "label_count_inv: int64 labels, inv [1]");
+  at::DeviceGuard g(labels.device());
+  HIP_OK(label_count_inv(labels.data_ptr<int64_t>(), labels.numel(), (int)ignore_index, inv.data_ptr<float>(), cur_stream()));
+}
+
+void rows_sum_scaled_(const at::Tensor& rows, double scale, c10::optional<at::Tensor> dev, const at::Tensor& out) {
+  GPU(rows); F32(rows); F32(out);
+  CK(rows.is_contiguous() && out.numel() == 1, "rows_sum_scaled: rows contiguous, out [1]");
+  if (dev) { F32(*dev); CK(dev->numel() == 1, "rows_sum_scaled: dev [1]"); }
+  at::DeviceGuard g(rows.device());
+  HIP_OK(rows_sum_scaled(rows.data_ptr<float>(), rows.numel(), (float)scale, optr<const float>(dev), out.data_ptr<float>(),
+                         cur_stream()));
+}
+
+void scale_bf16_dev_(const at::Tensor& x, const at::Tensor& s_dev) {
+  GPU(x); BF16(x); F32(s_dev);
+  CK(x.is_contiguous() && x.numel() % 8 == 0 && (reinterpret_cast<uintptr_t>(x.data_ptr()) % 16) == 0 && s_dev.numel() == 1,
+     "scale_bf16_dev: contiguous, 16-B aligned, numel % 8 == 0; s_dev [1]");
+  at::DeviceGuard g(x.device());
+  HIP_OK(scale_bf16_dev(x.data_ptr(), x.numel(), s_dev.data_ptr<float>(), cur_stream()));
 }
 
 // ---------------------------------------------------------------- elementwise
@@ -392,7 +417,12 @@ void register_ops(py::module& m) {
   m.def("maxpool_bwd", &maxpool_bwd_);
   m.def("avgpool_fwd", &avgpool_fwd_);
   m.def("avgpool_bwd", &avgpool_bwd_);
-  m.def("softmax_xent", &softmax_xent_);
+  m.def("softmax_xent", &softmax_xent_, "fused softmax cross-entropy", py::arg("logits"), py::arg("labels"),
+        py::arg("probs"), py::arg("loss_rows"), py::arg("dlogits"), py::arg("grad_scale"), py::arg("smoothing"),
+        py::arg("ignore_index"), py::arg("grad_scale_dev") = py::none());
+  m.def("label_count_inv", &label_count_inv_);
+  m.def("rows_sum_scaled", &rows_sum_scaled_);
+  m.def("scale_bf16_dev", &scale_bf16_dev_);
   m.def("cast_f32_bf16", &cast_f32_bf16_);
   m.def("sum_rows_bf16", &sum_rows_bf16_);
   m.def("cast_bf16_f32", &cast_bf16_f32_);

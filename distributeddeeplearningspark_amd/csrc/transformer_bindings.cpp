@@ -150,6 +150,16 @@ void embed_word_grad_(const at::Tensor& sorted_ids, const at::Tensor& perm, cons
                          gword.data_ptr<float>(), T, (int)H, cur_stream()));
 }
 
+void embed_word_grad_atomic_(const at::Tensor& ids, const at::Tensor& ds, const at::Tensor& gword) {
+  GPU(ds); I64(ids); BF16(ds); F32(gword);
+  const int64_t T = ids.numel(), H = ds.size(-1);
+  CK(ids.is_contiguous() && ds.is_contiguous() && gword.is_contiguous() && ds.numel() == T * H &&
+         gword.dim() == 2 && gword.size(1) == H && H % 2 == 0, "embed_word_grad_atomic: ids [T], ds [T, H], gword [V, H]");
+  at::DeviceGuard g(ds.device());
+  HIP_OK(embed_word_grad_atomic(ids.data_ptr<int64_t>(), ds.data_ptr(), gword.data_ptr<float>(), T, (int)H,
+                                gword.size(0), cur_stream()));
+}
+
 void embed_pos_grad_(const at::Tensor& ds, const at::Tensor& gpos, int64_t B, int64_t S) {
   GPU(ds); BF16(ds); F32(gpos);
   const int64_t H = ds.size(-1);
@@ -215,6 +225,7 @@ void register_transformer(py::module& m) {
         py::arg("gamma"), py::arg("dx"), py::arg("dx_drop"), py::arg("drop_p"), py::arg("seed"), py::arg("ws"),
         py::arg("in_drop_p") = 0.0, py::arg("in_seed") = 0, py::arg("parts") = 2);
   m.def("embed_word_grad", &embed_word_grad_);
+  m.def("embed_word_grad_atomic", &embed_word_grad_atomic_);
   m.def("embed_pos_grad", &embed_pos_grad_);
   m.def("colsum_partials", &colsum_partials_, py::arg("ws"), py::arg("P"), py::arg("N"), py::arg("out"),
         py::arg("accumulate"), py::arg("ld") = 0);

@@ -256,9 +256,8 @@ class _EmbeddingsFn(torch.autograd.Function):
             ws = torch.empty((C().ln_partial_rows(T_), 2, H), dtype=torch.float32, device=e.device)
             C().layernorm_bwd(dy.contiguous(), e, mean, rstd, layer.ln_g.master, de, None, 0.0, 0, ws, ctx.p, ctx.seed)
             _ln_param_grads(ws, H, layer.ln_g, layer.ln_b)
-            # word rows: tokens sorted by id, one writer per id (no atomics); positions: sum over batch
-            srt = torch.sort(ids.reshape(-1))
-            C().embed_word_grad(srt.values, srt.indices, de, layer.word.grad)
+            # word rows: no-return fp32 atomics straight into the arena (no id sort); positions: sum over batch
+            C().embed_word_grad_atomic(ids.reshape(-1).contiguous(), de, layer.word.grad)
             C().embed_pos_grad(de, layer.pos.grad, T_ // S, S)
             nt = c.type_vocab_size
             if nt <= 2:
@@ -390,10 +389,12 @@ class _MLMHeadFn(torch.autograd.Function):
     forward sweep of the fused xent kernel (1/n_valid folded in)."""
 
     @staticmethod
-    def forward(ctx, hm, anchor, head, emb, labels, n_valid):
+    def forward(ctx, hm, anchor, head, emb, labels, n_valid, model=None):
+        """``n_valid``: host count of the non-ignored labels, or None (GPU: the normaliser is
+        counted on the device — no host sync)."""
         c = head.cfg
         V, Vp, H, eps = c.vocab_size, c.vocab_padded, c.hidden_size, c.layer_norm_eps
-        ctx.head, ctx.emb = head, emb
+        ctx.head, ctx.emb, ctx.model = head, emb, model
         ctx.native = use_native(hm)
         labels = labels.reshape(-1)
         if not ctx.native:
@@ -414,9 +415,17 @@ class _MLMHeadFn(torch.autograd.Function):
         logits = G.linear_fwd(t2, emb.word.data, bias=head.dec_b.master)  # [M, Vp] (pad rows of E are zero)
         loss_rows = torch.empty(M, dtype=torch.float32, device=dev)
         dlogits = torch.empty_like(logits)
-        C().softmax_xent(logits[:, :V], labels.long(), None, loss_rows, dlogits[:, :V], 1.0 / n_valid, 0.0, -100)
+        labels = labels.long().contiguous()
+        inv = None
+        if n_valid is None:  # 1 / #valid labels on the device
+            inv = torch.empty(1, dtype=torch.float32, device=dev)
+            C().label_count_inv(labels, -100, inv)
+        host_scale = 1.0 if inv is not None else 1.0 / n_valid
+        C().softmax_xent(logits[:, :V], labels, None, loss_rows, dlogits[:, :V], host_scale, 0.0, -100, inv)
         ctx.save_for_backward(hm, pre, t, t2, mt, rt, dlogits)
-        return loss_rows.sum() / n_valid
+        loss = torch.empty(1, dtype=torch.float32, device=dev)
+        C().rows_sum_scaled(loss_rows, host_scale, inv, loss)
+        return loss.view(())
 
     @staticmethod
     def backward(ctx, dloss):
@@ -436,11 +445,12 @@ class _MLMHeadFn(torch.autograd.Function):
                 prm.grad.add_(g)
             if head.grad_hook is not None:
                 head.grad_hook()
-            return grads[0].to(hm.dtype), None, None, None, None, None
+            return grads[0].to(hm.dtype), None, None, None, None, None, None
         hm, pre, t, t2, mt, rt, dlogits = ctx.saved_tensors
-        scale = float(dloss)  # 1.0 in training (host value of a 0-d tensor set by autograd)
-        if scale != 1.0:
-            dlogits = (dlogits.float() * scale).to(dlogits.dtype)
+        # the incoming gradient is exactly 1 when a training step called loss.backward() (the model
+        # flags it); otherwise it is applied on the device — never read back to the host
+        if not getattr(ctx.model, "_unit_loss_grad", False):
+            C().scale_bf16_dev(dlogits, dloss.detach().reshape(1).float().contiguous())
         M = hm.shape[0]
         _wgrad(dlogits, t2, emb.word.grad)  # tied decoder: dE += dlogits^T t2
         _bias_grad(dlogits, head.dec_b.grad)
@@ -450,15 +460,15 @@ class _MLMHeadFn(torch.autograd.Function):
         ws = torch.empty((P_, 2, H), dtype=torch.float32, device=hm.device)
         C().layernorm_bwd(dt2, t, mt, rt, head.ln_g.master, dt, None, 0.0, 0, ws)
         _ln_param_grads(ws, H, head.ln_g, head.ln_b)
-        # t = gelu(pre): d(pre) = dt * gelu'(pre) — GEMM-free here, one fused elementwise via the dgrad epilogue
-        # of the transform is not available (t is produced by the GELU epilogue), so apply it on the host side:
-        dpre = (dt.float() * _gelu_grad(pre.float())).to(torch.bfloat16)
+        # t = gelu(pre): d(pre) = dt * gelu'(pre), one HIP elementwise pass (layer_ops.hip act_bwd, GELU code)
+        dpre = torch.empty_like(dt)
+        C().act_bwd(dt, pre, dpre, C().ACT_CODES["gelu"])
         _wgrad(dpre, hm, head.t_w.grad)
         _bias_grad(dpre, head.t_b.grad)
         dhm = _dgrad(dpre, head.t_w.data)
         if head.grad_hook is not None:
             head.grad_hook()
-        return dhm, None, None, None, None, None
+        return dhm, None, None, None, None, None, None
 
 
 def _gelu_grad(x):
@@ -537,24 +547,38 @@ class BertForMaskedLM(Model):
         hm = h.index_select(0, flat)
         labels = y["labels"].reshape(-1).long()
         n_valid = y.get("num_masked")
-        if n_valid is None:
-            n_valid = int((labels != -100).sum().item())
-        n_valid = max(1, int(n_valid))
-        loss = _MLMHeadFn.apply(hm, self.head.ln_g.data, self.head, self.embeddings, labels, n_valid)
+        if n_valid is None and not use_native(hm):
+            n_valid = int((labels != -100).sum().item())  # CPU tensors: no device sync involved
+        if n_valid is not None:
+            n_valid = max(1, int(n_valid))
+        loss = _MLMHeadFn.apply(hm, self.head.ln_g.data, self.head, self.embeddings, labels, n_valid, self)
         if training:
             self._step += 1
         return loss
 
     def forward(self, x, training=False, logits=False):
-        """Full-sequence MLM logits [B, S, V] (inference / evaluation)."""
+        """Full-sequence MLM logits [B, S, V] (inference / evaluation).  GPU: the head is the
+        training path's HIP kernels — transform GEMM with the GELU epilogue, LayerNorm, tied
+        decoder GEMM with the bias epilogue, one HIP cast to fp32."""
         c = self.config
+        B, S = x["input_ids"].shape
         with torch.no_grad():
             h = self.encode(x, False)
-            hf = h.float()
             hd = self.head
-            lg = mlm_head_ref(hf, hd.t_w.master, hd.t_b.master, hd.ln_g.master, hd.ln_b.master,
+            if use_native(h):
+                T_, H, V = h.shape[0], c.hidden_size, c.vocab_size
+                pre = torch.empty((T_, H), dtype=torch.bfloat16, device=h.device)
+                t = G.linear_fwd(h, hd.t_w.data, bias=hd.t_b.master, act=G.ACT_GELU, aux=pre)
+                t2 = torch.empty_like(t)
+                mt = torch.empty(T_, dtype=torch.float32, device=h.device)
+                rt = torch.empty_like(mt)
+                C().layernorm_fwd(t, hd.ln_g.master, hd.ln_b.master, t2, mt, rt, c.layer_norm_eps)
+                lg16 = G.linear_fwd(t2, self.embeddings.word.data, bias=hd.dec_b.master)  # [T, Vp]
+                lg = torch.empty((T_, lg16.shape[1]), dtype=torch.float32, device=h.device)
+                C().cast_bf16_f32(lg16, lg)
+                return lg.view(B, S, -1)[..., :V]
+            lg = mlm_head_ref(h.float(), hd.t_w.master, hd.t_b.master, hd.ln_g.master, hd.ln_b.master,
                               self.embeddings.word.master, hd.dec_b.master, c.layer_norm_eps, c.vocab_size)
-        B, S = x["input_ids"].shape
         return lg.view(B, S, -1)
 
     def get_config(self):

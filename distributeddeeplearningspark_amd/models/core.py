@@ -363,8 +363,17 @@ class Model(Layer):
         reset_workspaces(self.device)
         self.arena.zero_grad()
         loss = self.compute_loss(x, y, training=True)
-        loss.backward()
+        self.backward_unit(loss)
         return loss
+
+    def backward_unit(self, loss):
+        """``loss.backward()`` with the model told that the seed gradient is exactly 1 (loss nodes
+        may then skip applying it, with no device -> host read of the seed)."""
+        self._unit_loss_grad = True
+        try:
+            loss.backward()
+        finally:
+            self._unit_loss_grad = False
 
     def train_on_batch(self, x, y, grad_sync=None, grad_scale: float = 1.0) -> float:
         if self.optimizer is None:

@@ -341,7 +341,7 @@ class DataParallel:
             with phase("forward"):
                 loss = m.compute_loss(x, y, training=True)
             with phase("backward"):
-                loss.backward()
+                m.backward_unit(loss)
             ev = None
             if self.timing and self.pg.distributed:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
