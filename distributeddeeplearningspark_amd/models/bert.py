@@ -40,6 +40,7 @@ from ..ops import gemm as G
 from ..ops import transformer as T
 from ..ops._native import C, use_native
 from ..ops._ref import ref_grads
+from ..ops.streams import on_grad_stream
 from . import params as P
 from .core import Layer, Model
 
@@ -113,7 +114,9 @@ def _bias_grad(d2, gb):
 # Every BERT GEMM (fused-epilogue or plain) runs on the hand-written MFMA kernels; the
 # hipBLASLt route tried in round 1 measured slower end-to-end and was removed (PERFORMANCE.md).
 def _wgrad(d2, x2, gw):
-    G.linear_wgrad(d2, x2, gw)
+    # weight gradients run on the side stream beside the data-gradient chain (ops/streams.py)
+    with on_grad_stream(d2.device, d2, x2):
+        G.linear_wgrad(d2, x2, gw)
 
 
 def _dgrad(dy, w):
@@ -257,7 +260,9 @@ class _EmbeddingsFn(torch.autograd.Function):
             C().layernorm_bwd(dy.contiguous(), e, mean, rstd, layer.ln_g.master, de, None, 0.0, 0, ws, ctx.p, ctx.seed)
             _ln_param_grads(ws, H, layer.ln_g, layer.ln_b)
             # word rows: no-return fp32 atomics straight into the arena (no id sort); positions: sum over batch
-            C().embed_word_grad_atomic(ids.reshape(-1).contiguous(), de, layer.word.grad)
+            # (side stream: ordered after the tied decoder's wgrad into the same rows)
+            with on_grad_stream(de.device, de, ids):
+                C().embed_word_grad_atomic(ids.reshape(-1).contiguous(), de, layer.word.grad)
             C().embed_pos_grad(de, layer.pos.grad, T_ // S, S)
             nt = c.type_vocab_size
             if nt <= 2:

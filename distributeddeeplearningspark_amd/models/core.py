@@ -369,11 +369,14 @@ class Model(Layer):
     def backward_unit(self, loss):
         """``loss.backward()`` with the model told that the seed gradient is exactly 1 (loss nodes
         may then skip applying it, with no device -> host read of the seed)."""
+        from ..ops.streams import join
+
         self._unit_loss_grad = True
         try:
             loss.backward()
         finally:
             self._unit_loss_grad = False
+        join(self.device)  # side-stream weight gradients (ops/streams.py) land before anyone reads them
 
     def train_on_batch(self, x, y, grad_sync=None, grad_scale: float = 1.0) -> float:
         if self.optimizer is None:

@@ -27,6 +27,7 @@ import torch.nn.functional as F
 from . import gemm as G
 from ._native import C, use_native
 from ._ref import accumulate, ref_grads
+from .streams import on_grad_stream
 
 
 def _pair(v):
@@ -378,21 +379,22 @@ class _Conv2dFn(torch.autograd.Function):
                 d2 = torch.empty_like(dy)
                 C().relu_bwd(dy, y, d2)
                 dy = d2
-            if gb is not None:
-                if pad_co:
-                    tb = torch.zeros(g.Co, dtype=torch.float32, device=dy.device)
-                    C().bias_grad(dy, tb, g.Co, True)
-                    gb.add_(tb[: ctx.co])
-                else:
-                    C().bias_grad(dy, gb, g.Co, True)
             padded = g.Ci != ctx.ci or pad_co
-            if gw is not None:
-                if padded:
-                    tmp = torch.zeros((g.Co, g.KH, g.KW, g.Ci), dtype=torch.float32, device=dy.device)
-                    conv_wgrad_native(dy, x, g, tmp)
-                    gw.add_(tmp[: ctx.co, ..., : ctx.ci])
-                else:
-                    conv_wgrad_native(dy, x, g, gw)
+            with on_grad_stream(dy.device, dy, x, default=False):  # parameter gradients beside the data-gradient
+                if gb is not None:
+                    if pad_co:
+                        tb = torch.zeros(g.Co, dtype=torch.float32, device=dy.device)
+                        C().bias_grad(dy, tb, g.Co, True)
+                        gb.add_(tb[: ctx.co])
+                    else:
+                        C().bias_grad(dy, gb, g.Co, True)
+                if gw is not None:
+                    if padded:
+                        tmp = torch.zeros((g.Co, g.KH, g.KW, g.Ci), dtype=torch.float32, device=dy.device)
+                        conv_wgrad_native(dy, x, g, tmp)
+                        gw.add_(tmp[: ctx.co, ..., : ctx.ci])
+                    else:
+                        conv_wgrad_native(dy, x, g, gw)
             if ctx.needs_dx:
                 dx = conv_dgrad_native(dy, w, g)
                 if g.Ci != ctx.ci:

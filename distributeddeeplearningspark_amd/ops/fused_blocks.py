@@ -20,6 +20,7 @@ from . import conv as CV
 from . import gemm as G
 from ._native import C
 from .norm import new_stats_workspace, partials_workspace
+from .streams import on_grad_stream
 
 
 class _ConvBNState:
@@ -94,7 +95,10 @@ def bn_backward(unit, st, dy, want_dres):
 
 def conv_backward(unit, st, dyc, x, need_dx, resid=None, resid_mask=None):
     conv = unit.conv
-    CV.conv_wgrad_native(dyc, x, st.g, conv.kernel.grad)
+    # the weight gradient only feeds the optimizer / all-reduce: it runs on the side stream
+    # (ops/streams.py) beside the data-gradient and BatchNorm sweeps of the layers below
+    with on_grad_stream(dyc.device, dyc, x, default=False):
+        CV.conv_wgrad_native(dyc, x, st.g, conv.kernel.grad)
     if conv.grad_hook is not None:
         conv.grad_hook()
     if not need_dx:
@@ -212,9 +216,10 @@ class _StemS2DFn(torch.autograd.Function):
         dyc, _ = bn_backward(unit, st, dy.contiguous(), False)
         conv = unit.conv
         g = st.g
-        tmp = torch.zeros((g.Co, 4, 4, 16), dtype=torch.float32, device=dy.device)
-        CV.conv_wgrad_native(dyc, xs, g, tmp)
-        conv.kernel.grad.add_(_s2d_weight_grad(tmp, ctx.cc))
+        with on_grad_stream(dy.device, dyc, xs, default=False):
+            tmp = torch.zeros((g.Co, 4, 4, 16), dtype=torch.float32, device=dy.device)
+            CV.conv_wgrad_native(dyc, xs, g, tmp)
+            conv.kernel.grad.add_(_s2d_weight_grad(tmp, ctx.cc))
         if conv.grad_hook is not None:
             conv.grad_hook()
         ctx.st = None
@@ -256,12 +261,13 @@ class _ConvBNFn(torch.autograd.Function):
         dyc, _ = bn_backward(unit, st, dy.contiguous(), False)
         conv = unit.conv
         g = st.g
-        if g.Ci != ctx.ci:
-            tmp = torch.zeros((g.Co, g.KH, g.KW, g.Ci), dtype=torch.float32, device=dy.device)
-            CV.conv_wgrad_native(dyc, x, g, tmp)
-            conv.kernel.grad.add_(tmp[..., : ctx.ci])
-        else:
-            CV.conv_wgrad_native(dyc, x, g, conv.kernel.grad)
+        with on_grad_stream(dy.device, dyc, x, default=False):
+            if g.Ci != ctx.ci:
+                tmp = torch.zeros((g.Co, g.KH, g.KW, g.Ci), dtype=torch.float32, device=dy.device)
+                CV.conv_wgrad_native(dyc, x, g, tmp)
+                conv.kernel.grad.add_(tmp[..., : ctx.ci])
+            else:
+                CV.conv_wgrad_native(dyc, x, g, conv.kernel.grad)
         if conv.grad_hook is not None:
             conv.grad_hook()
         dx = None

@@ -13,6 +13,7 @@ import torch.nn.functional as F
 
 from . import gemm as G
 from ._native import C, use_native
+from .streams import on_grad_stream
 from ._ref import accumulate, ref_grads
 
 
@@ -91,15 +92,16 @@ class _LinearFn(torch.autograd.Function):
                 t = torch.empty_like(d2)
                 C().relu_bwd(d2, y, t)
                 d2 = t
-            if gb is not None:
-                C().bias_grad(d2, gb, N, True) if Np == N else gb.add_(d2[:, :N].float().sum(0))
-            if gw is not None:
-                if Np == N and Kp == K:
-                    G.linear_wgrad(d2, x2, gw)
-                else:
-                    tmp = torch.zeros((Np, Kp), dtype=torch.float32, device=d2.device)
-                    G.linear_wgrad(d2, x2, tmp)
-                    gw.add_(tmp[:N, :K])
+            with on_grad_stream(d2.device, d2, x2, default=False):  # parameter gradients beside the data-gradient
+                if gb is not None:
+                    C().bias_grad(d2, gb, N, True) if Np == N else gb.add_(d2[:, :N].float().sum(0))
+                if gw is not None:
+                    if Np == N and Kp == K:
+                        G.linear_wgrad(d2, x2, gw)
+                    else:
+                        tmp = torch.zeros((Np, Kp), dtype=torch.float32, device=d2.device)
+                        G.linear_wgrad(d2, x2, tmp)
+                        gw.add_(tmp[:N, :K])
             if ctx.needs_dx:
                 dxp = G.linear_dgrad(d2, w)
                 dx = (dxp[:, :K].contiguous() if Kp != K else dxp).view(ctx.xshape)

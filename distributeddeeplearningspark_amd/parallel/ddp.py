@@ -259,6 +259,15 @@ class DataParallel:
             self._next += 1
 
     def _launch(self, i):
+        from ..ops.streams import on_grad_stream
+
+        # launched from the weight-gradient side stream (after it has waited for the compute
+        # stream): RCCL then orders the bucket after its side-stream weight gradients AND the
+        # compute-stream BatchNorm / bias gradients (ops/streams.py)
+        with on_grad_stream(self.arena.grad.device):
+            self._launch_on_stream(i)
+
+    def _launch_on_stream(self, i):
         b = self.buckets[i]
         view = self.arena.grad[b["start"] : b["end"]]
         if self._a2a is not None:
@@ -292,9 +301,12 @@ class DataParallel:
         """Launch what is left, then wait bucket by bucket.  With ``optimizer`` (ranged-capable),
         each bucket's arena slice is updated right after its wait; returns True if it stepped.
         ``reduced_event`` is recorded on the compute stream once the LAST bucket is reduced."""
+        from ..ops.streams import join
+
         for i in range(self._next, len(self.buckets)):
             self._launch(i)
         self._next = len(self.buckets)
+        join(self.arena.grad.device)  # the updates below read every weight gradient
         ranged = optimizer is not None and optimizer.ranged_ok and self.overlap_optimizer
         gs = optimizer.begin_step(grad_scale) if ranged else None
         for i, b in enumerate(self.buckets):
