@@ -214,7 +214,9 @@ def bench_nyiso(args):
         "config": {"model": f"nyiso_{cell.lower()}", "algorithm": "ADAG", "workers": args.workers, "batch": 32,
                    "communication_window": 5, "epochs": args.epochs, "units": 128, "input": [25, 1],
                    "workers_per_gpu": wpg, "num_updates": r["updates"], "mape_pct": round(r["mape"], 4),
-                   "worker_s": r["worker_s"], "reference": ref},
+                   "wall_incl_executor_start_s": r.get("wall_incl_executor_start_s"),
+                   "executor_start_s": r.get("executor_start_s"), "worker_s": r["worker_s"],
+                   "commit_s": r.get("commit_s"), "commit_wait_s": r.get("commit_wait_s"), "reference": ref},
     }), flush=True)
 
 

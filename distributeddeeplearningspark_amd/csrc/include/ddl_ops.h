@@ -202,4 +202,11 @@ int etl_minmax(const double* x, double* y, long n, double o_min, double scale, d
 int etl_one_hot(const int64_t* labels, double* y, long n, int K, int* bad, hipStream_t s);
 int etl_argmax(const double* x, long rows, int K, long ld, int64_t* out, hipStream_t s);
 
+
+// dist-keras commit rounds (optim.hip): X = scale (W - center) [, W -= X]; center += sum_j X_j [, W = center]
+constexpr int kMaxCommitPeers = 16;
+struct CommitPtrs { const float* p[kMaxCommitPeers]; };
+int commit_delta(float* W, const float* center, float* X, void* w16, long n, float scale, int elastic, hipStream_t s);
+int commit_apply(const CommitPtrs& xs, int nx, float* center, float* W, void* w16, long n, hipStream_t s);
+
 }  // namespace ddl

@@ -194,4 +194,60 @@ int sumsq_f32(const float* x, long n, float* out, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+
+// ------------------------------ dist-keras commit rounds (ADAG / DynSGD / DOWNPOUR / EASGD) ------------------------------
+// The reference's commit arithmetic (residual = (W - W_pulled) / window, PS center += residual, pull;
+// ddl_mnist_aztk.py:216-219 via distkeras' ADAGWorker) as two flat sweeps around the exchange:
+//   commit_delta:  X = scale * (W - center); elastic (EASGD family): W -= X        (before the exchange)
+//   commit_apply:  center += sum_j X_j over the exchanged buffers; W = center      (after it)
+// X_j are either the all-reduced buffer (one pointer) or the peer replicas' buffers of workers
+// co-located on this GPU, mapped through IPC handles (parallel/colocated.py): the reduction over
+// workers is then this one kernel reading the peers' HBM directly, with no host staging.
+__global__ __launch_bounds__(256) void commit_delta_kernel(float4* __restrict__ W, const float4* __restrict__ center,
+                                                           float4* __restrict__ X, void* w16, long n, float scale,
+                                                           int elastic) {
+  DDL_FLAT_FOR(i, n) {
+    float4 w = W[i];
+    const float4 c = center[i];
+    const float4 x = make_float4(scale * (w.x - c.x), scale * (w.y - c.y), scale * (w.z - c.z), scale * (w.w - c.w));
+    X[i] = x;
+    if (elastic) {
+      w = make_float4(w.x - x.x, w.y - x.y, w.z - x.z, w.w - x.w);
+      W[i] = w;
+      if (w16) store_bf16x4(w16, i, w);
+    }
+  }
+}
+
+int commit_delta(float* W, const float* center, float* X, void* w16, long n, float scale, int elastic, hipStream_t s) {
+  hipLaunchKernelGGL(commit_delta_kernel, dim3(ogrid(n >> 2)), dim3(256), 0, s, (float4*)W, (const float4*)center,
+                     (float4*)X, w16, n, scale, elastic);
+  return (int)hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void commit_apply_kernel(CommitPtrs xs, int nx, float4* __restrict__ center,
+                                                           float4* __restrict__ W, void* w16, long n) {
+  DDL_FLAT_FOR(i, n) {
+    float4 c = center[i];
+    for (int j = 0; j < nx; ++j) {
+      const float4 x = reinterpret_cast<const float4*>(xs.p[j])[i];
+      c.x += x.x;
+      c.y += x.y;
+      c.z += x.z;
+      c.w += x.w;
+    }
+    center[i] = c;
+    if (W) {
+      W[i] = c;
+      if (w16) store_bf16x4(w16, i, c);
+    }
+  }
+}
+
+int commit_apply(const CommitPtrs& xs, int nx, float* center, float* W, void* w16, long n, hipStream_t s) {
+  hipLaunchKernelGGL(commit_apply_kernel, dim3(ogrid(n >> 2)), dim3(256), 0, s, xs, nx, (float4*)center, (float4*)W,
+                     w16, n);
+  return (int)hipGetLastError();
+}
+
 }  // namespace ddl

@@ -336,6 +336,33 @@ void adam_step_(const at::Tensor& w, const at::Tensor& g, const at::Tensor& m, c
                    w.numel(), (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (int)mode, (float)bc1,
                    (float)bc2, (float)gscale, optr<float>(tstep), cur_stream()));
 }
+void commit_delta_(const at::Tensor& W, const at::Tensor& center, const at::Tensor& X, c10::optional<at::Tensor> w16,
+                   double scale, bool elastic) {
+  GPU(W); F32(W); F32(center); F32(X);
+  CK(W.is_contiguous() && center.is_contiguous() && X.is_contiguous() && center.numel() == W.numel() &&
+         X.numel() == W.numel() && W.numel() % 4 == 0, "commit_delta: contiguous fp32 of one size (n % 4 == 0)");
+  if (w16) { BF16(*w16); CK(w16->numel() == W.numel(), "commit_delta: w16 size"); }
+  at::DeviceGuard g(W.device());
+  HIP_OK(commit_delta(W.data_ptr<float>(), center.data_ptr<float>(), X.data_ptr<float>(), optr<void>(w16), W.numel(),
+                      (float)scale, elastic ? 1 : 0, cur_stream()));
+}
+void commit_apply_(const std::vector<at::Tensor>& xs, const at::Tensor& center, c10::optional<at::Tensor> W,
+                   c10::optional<at::Tensor> w16) {
+  GPU(center); F32(center);
+  CK(center.is_contiguous() && center.numel() % 4 == 0, "commit_apply: contiguous center, n % 4 == 0");
+  CK(!xs.empty() && xs.size() <= (size_t)kMaxCommitPeers, "commit_apply: 1..16 exchange buffers");
+  CommitPtrs ptrs{};
+  for (size_t j = 0; j < xs.size(); ++j) {
+    F32(xs[j]);
+    CK(xs[j].is_cuda() && xs[j].is_contiguous() && xs[j].numel() == center.numel(), "commit_apply: exchange buffer size");
+    ptrs.p[j] = xs[j].data_ptr<float>();
+  }
+  if (W) { F32(*W); CK(W->is_contiguous() && W->numel() == center.numel(), "commit_apply: W size"); }
+  if (w16) { BF16(*w16); CK(W && w16->numel() == center.numel(), "commit_apply: w16 needs W, same size"); }
+  at::DeviceGuard g(center.device());
+  HIP_OK(commit_apply(ptrs, (int)xs.size(), center.data_ptr<float>(), W ? W->data_ptr<float>() : nullptr,
+                      optr<void>(w16), center.numel(), cur_stream()));
+}
 void mse_fwd_bwd_(const at::Tensor& pred, const at::Tensor& target, const at::Tensor& loss, const at::Tensor& grad) {
   F32(pred); F32(target); F32(loss); F32(grad);
   CK(pred.is_cuda() && pred.numel() == target.numel() && grad.numel() == pred.numel() && loss.numel() == 1,
@@ -439,6 +466,8 @@ void register_ops(py::module& m) {
         py::arg("bc1"), py::arg("bc2"), py::arg("gscale"), py::arg("tstep") = py::none());
   m.def("step_tick", &step_tick_);
   m.def("mse_fwd_bwd", &mse_fwd_bwd_);
+  m.def("commit_delta", &commit_delta_);
+  m.def("commit_apply", &commit_apply_);
   m.def("etl_minmax", &etl_minmax_);
   m.def("etl_one_hot", &etl_one_hot_);
   m.def("etl_argmax", &etl_argmax_);

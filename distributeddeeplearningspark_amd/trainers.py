@@ -250,20 +250,33 @@ class _CommitWorker(_Worker):
         it0, rnd = self._resume()
         ex = self.resumed_extra or {}
         center = ex["center"].clone() if "center" in ex else a.master.detach().clone()
+        self._exchange = None
+        if a.master.is_cuda and self.pg.distributed:
+            from .parallel.colocated import ColocatedExchange, colocated_ok
+
+            if colocated_ok(self.pg):  # replicas sharing this GPU: device-side exchange (IPC)
+                xc = ColocatedExchange(self.pg, a.numel, a.master.device)
+                self._exchange = xc if xc.available else None
         it = 0
-        for xb, yb in self.batches(feed):
-            it += 1
-            if it <= it0:  # resumed: these batches were consumed before the checkpoint
-                continue
-            self._tick(it)
-            self.train_batch(xb, yb)
-            if it % self.k == 0 and rnd < self.rounds:
+        try:
+            for xb, yb in self.batches(feed):
+                it += 1
+                if it <= it0:  # resumed: these batches were consumed before the checkpoint
+                    continue
+                self._tick(it)
+                self.train_batch(xb, yb)
+                if it % self.k == 0 and rnd < self.rounds:
+                    self.commit(center, rnd)
+                    rnd += 1
+                    self._maybe_checkpoint(rnd, it, center)
+            while rnd < self.rounds:  # my shard is exhausted: join the remaining rounds with a zero delta
                 self.commit(center, rnd)
                 rnd += 1
-                self._maybe_checkpoint(rnd, it, center)
-        while rnd < self.rounds:  # my shard is exhausted: join the remaining rounds with a zero delta
-            self.commit(center, rnd)
-            rnd += 1
+        finally:
+            if self._exchange is not None:
+                self.wait_s, self.xfer_s = self._exchange.wait_s, self._exchange.xfer_s
+                self._exchange.close()
+                self._exchange = None
         return center
 
     def _contributors(self, rnd):
@@ -276,12 +289,41 @@ class _CommitWorker(_Worker):
         finally:
             self.commit_s += time.perf_counter() - t0
 
+    def _scale(self, contrib, mine):
+        """Per-worker factor of the committed delta (0 for a worker whose shard is exhausted)."""
+        if not mine:
+            return 0.0
+        rule = self.rule
+        if rule in ("easgd", "aeasgd", "eamsgd"):
+            return float(self.cfg["alpha"])
+        if rule == "adag":
+            return 1.0 / self.k
+        if rule == "dynsgd":
+            return 1.0 / (contrib.index(self.pg.rank) + 1)  # staleness = workers committing before me
+        return 1.0
+
     def _commit(self, center, rnd):
         a, pg = self.arena, self.pg
         contrib = self._contributors(rnd)
         mine = pg.rank in contrib
         W = a.master.detach()
         rule = self.rule
+        if W.is_cuda:
+            # fused HIP commit: X = s (W - center) [W -= X] -> exchange -> center += sum X [W = center]
+            elastic = rule in ("easgd", "aeasgd", "eamsgd")
+            w16 = None if a.compute is a.master else a.compute
+            scale = self._scale(contrib, mine)
+            if self._exchange is not None:
+                self._exchange.commit(W, center, scale, elastic, w16)
+                return
+            from .ops._native import C
+
+            if getattr(self, "_xbuf", None) is None or self._xbuf.numel() != W.numel():
+                self._xbuf = torch.empty_like(W)
+            C().commit_delta(W, center, self._xbuf, w16 if elastic else None, scale, elastic)
+            self._allreduce(self._xbuf)
+            C().commit_apply([self._xbuf], center, None if elastic else W, None if elastic else w16)
+            return
         with torch.no_grad():
             if rule in ("easgd", "aeasgd", "eamsgd"):
                 e = (W - center) * self.cfg["alpha"] if mine else torch.zeros_like(W)
@@ -500,7 +542,8 @@ def _train_worker(rank, world, pg, cfg, blob, X, Y, sizes):
     if model.device.type == "cuda":
         torch.cuda.synchronize(model.device)
     out = {"rank": rank, "history": w.losses(), "num_updates": w.num_updates(), "time": time.time() - t0,
-           "commit_s": w.commit_s, "graph": bool(w._step is not None and w._step.captured),
+           "commit_s": w.commit_s, "commit_wait_s": getattr(w, "wait_s", None),
+           "commit_xfer_s": getattr(w, "xfer_s", None), "graph": bool(w._step is not None and w._step.captured),
            "ingest": "stream" if feed.streaming else "resident", "timed_s": getattr(w, "timed_s", None),
            "timed_steps": getattr(w, "timed_steps", 0)}
     if rank == 0 or cfg["algorithm"] == "ensemble":

@@ -153,7 +153,7 @@ def main():
     print("Number of parameter server updates: " + str(trainer.parameter_server.num_updates))
     rs = getattr(trainer, "_results", [])
     print("Workers:", [{k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()
-                        if k in ("rank", "time", "commit_s", "graph", "ingest")} for r in rs])
+                        if k in ("rank", "time", "commit_s", "commit_wait_s", "commit_xfer_s", "graph", "ingest")} for r in rs])
     return trainer, trained_model
 
 
