@@ -56,7 +56,8 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
           c10::optional<at::Tensor> resid, int64_t ldr, int64_t relu, c10::optional<py::dict> geom,
           c10::optional<py::dict> outmap, int64_t b_kdiv, int64_t b_tap_stride,
           c10::optional<at::Tensor> stats, c10::optional<at::Tensor> aux, double drop_p, int64_t drop_seed,
-          c10::optional<at::Tensor> resid_mask) {
+          c10::optional<at::Tensor> resid_mask, c10::optional<at::Tensor> bnr_x, c10::optional<at::Tensor> bnr_mask,
+          c10::optional<at::Tensor> bnr_mean) {
   CHECK_CUDA(a);
   CHECK_CUDA(b);
   CHECK_CUDA(c);
@@ -176,6 +177,24 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
     TORCH_CHECK(stats->numel() >= (int64_t)kStatShards * 2 * N, "stats workspace too small");
     p.stats = stats->data_ptr<float>();
   }
+  if (bnr_x) {
+    TORCH_CHECK(tile == kTileStream && stats.has_value() && bnr_mean.has_value(),
+                "gemm: the fused BN-backward reduction needs the streaming kernel, a stats workspace and the mean");
+    CHECK_CUDA(*bnr_x);
+    CHECK_BF16(*bnr_x);
+    TORCH_CHECK(bnr_x->is_contiguous() && bnr_x->numel() >= (M - 1) * ldc + N && ((uintptr_t)bnr_x->data_ptr() % 16) == 0,
+                "gemm: bnr_x must be a 16-B aligned bf16 [M][ldc]");
+    CHECK_F32(*bnr_mean);
+    TORCH_CHECK(bnr_mean->numel() >= N && ((uintptr_t)bnr_mean->data_ptr() % 16) == 0, "gemm: bnr_mean [N], 16-B aligned");
+    p.bnr_x = bnr_x->data_ptr();
+    p.bnr_mean = bnr_mean->data_ptr<float>();
+    if (bnr_mask) {
+      TORCH_CHECK(bnr_mask->scalar_type() == at::kByte && bnr_mask->is_contiguous() && ldc % 8 == 0 &&
+                      bnr_mask->numel() >= ((M - 1) * ldc + N + 7) / 8,
+                  "gemm: bnr_mask must be uint8 [M * ldc / 8]");
+      p.bnr_mask = bnr_mask->data_ptr<uint8_t>();
+    }
+  }
   (void)bm;
   if (tile == kTileConv3)
     TORCH_CHECK(conv3x3_halo_ok(p) && epi == EPI_BF16, "gemm conv3x3: needs a 3x3 / stride-1 / pad-1 KC_GATHER x KC "
@@ -201,7 +220,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("relu") = false, py::arg("geom") = py::none(), py::arg("outmap") = py::none(),
         py::arg("b_kdiv") = 0, py::arg("b_tap_stride") = 0, py::arg("stats") = py::none(),
         py::arg("aux") = py::none(), py::arg("drop_p") = 0.0, py::arg("drop_seed") = 0,
-        py::arg("resid_mask") = py::none());
+        py::arg("resid_mask") = py::none(), py::arg("bnr_x") = py::none(), py::arg("bnr_mask") = py::none(),
+        py::arg("bnr_mean") = py::none());
   m.attr("ACT_NONE") = (int)ACT_NONE;
   m.attr("ACT_RELU") = (int)ACT_RELU;
   m.attr("ACT_GELU") = (int)ACT_GELU;

@@ -89,6 +89,14 @@ struct GemmParams {
   uint32_t drop_thresh;
   float drop_scale;
   unsigned long long drop_seed;
+  // fused BatchNorm-backward reduction of the STORED output d (the gradient arriving at a BN whose
+  // input is bnr_x; streaming kernel only): instead of the forward statistics, ``stats`` receives
+  //   stats[shard][0][n] += sum_m d(m,n) * relu(m,n),  stats[shard][1][n] += sum_m d * relu * (x(m,n) - mean[n])
+  // with relu(m,n) the bn.hip mode-3 bit of bnr_mask (all ones when null) — the partial sums of
+  // bn_bwd_reduce, so that sweep (a full read of d and x) is skipped for that BN.
+  const void* bnr_x;        // bf16 [M][ldc]
+  const uint8_t* bnr_mask;  // bit (m*ldc + n) of the ReLU mask, or null
+  const float* bnr_mean;    // [N] batch mean of bnr_x
 };
 
 enum Activation : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_GELU_BWD = 3 };

@@ -102,7 +102,7 @@ __device__ __forceinline__ void stage_a(const bf16_t* __restrict__ A, long lda, 
 
 }  // namespace gst
 
-template <int WN, int K, int BMODE, bool RES>
+template <int WN, int K, int BMODE, bool RES, bool BNR = false>
 __global__ __launch_bounds__(gst::THREADS, 2) void gemm_stream_kernel(const GemmParams p) {
   using namespace gst;
   using CF = Cfg<WN, K>;
@@ -156,6 +156,14 @@ __global__ __launch_bounds__(gst::THREADS, 2) void gemm_stream_kernel(const Gemm
 #pragma unroll
   for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
   const int oc = threadIdx.x % CF::OCPR, orow = threadIdx.x / CF::OCPR;
+  // BNR: batch mean of the 8 columns this thread reads out (loaded once)
+  float bmu[8];
+  if constexpr (BNR) {
+    const float4 a = *reinterpret_cast<const float4*>(p.bnr_mean + n0 + oc * 8);
+    const float4 b = *reinterpret_cast<const float4*>(p.bnr_mean + n0 + oc * 8 + 4);
+    bmu[0] = a.x; bmu[1] = a.y; bmu[2] = a.z; bmu[3] = a.w;
+    bmu[4] = b.x; bmu[5] = b.y; bmu[6] = b.z; bmu[7] = b.w;
+  }
   bf16_t* __restrict__ Cout = reinterpret_cast<bf16_t*>(p.c);
 
   for (int i = 0; i < nloc; ++i) {
@@ -184,6 +192,19 @@ __global__ __launch_bounds__(gst::THREADS, 2) void gemm_stream_kernel(const Gemm
           else if constexpr (CF::RN == 2) rmsk[mb] = *reinterpret_cast<const uint32_t*>(mp);
           else rmsk[mb] = *reinterpret_cast<const uint64_t*>(mp);
         }
+      }
+    }
+    // BNR: the BN input x and its ReLU-mask byte at this thread's read-out vectors (issued with the
+    // residual, ahead of the refill, for the same reason)
+    uint4 bx[BNR ? CF::S : 1];
+    uint32_t bm8[BNR ? CF::S : 1];
+    if constexpr (BNR) {
+#pragma unroll
+      for (int ps = 0; ps < CF::S; ++ps) {
+        const int m = min(m0 + orow + ps * CF::RPP, p.M - 1);
+        const long idx = (long)m * p.ldc + n0 + oc * 8;
+        bx[ps] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(p.bnr_x) + idx);
+        bm8[ps] = p.bnr_mask ? (uint32_t)p.bnr_mask[idx >> 3] : 0xffu;
       }
     }
     const int ahead = i + CF::NBUF - 1;
@@ -245,7 +266,21 @@ __global__ __launch_bounds__(gst::THREADS, 2) void gemm_stream_kernel(const Gemm
       const uint4 v = *reinterpret_cast<const uint4*>(stg + r * (CF::NB * 2) + ((oc ^ sw<CF::OCPR>(r)) << 4));
       if (m < p.M) {
         *reinterpret_cast<uint4*>(Cout + (long)m * p.ldc + n0 + oc * 8) = v;
-        if (p.stats) {
+        if constexpr (BNR) {  // BN-backward partial sums of the stored gradient (see GemmParams)
+          const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+          const uint32_t xv[4] = {bx[ps].x, bx[ps].y, bx[ps].z, bx[ps].w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int e = 2 * q + h;
+              const float d = ((bm8[ps] >> e) & 1u) ? __uint_as_float(h ? (wv[q] & 0xffff0000u) : (wv[q] << 16)) : 0.f;
+              const float xe = __uint_as_float(h ? (xv[q] & 0xffff0000u) : (xv[q] << 16));
+              s1[e] += d;
+              s2[e] += d * (xe - bmu[e]);
+            }
+          }
+        } else if (p.stats) {
           const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
@@ -313,10 +348,16 @@ int launch_ws(const GemmParams& p, hipStream_t s) {
   const int panels = p.N / CF::NB;
   const int mt = (p.M + gst::BM - 1) / gst::BM;
   const int gx = std::max(1, std::min(mt, 2 * num_cus() / std::max(1, panels)));
-  if (p.resid)
+  if (p.bnr_x) {
+    if (p.resid)
+      hipLaunchKernelGGL((gemm_stream_kernel<WN, K, BMODE, true, true>), dim3(gx, panels), dim3(gst::THREADS), 0, s, p);
+    else
+      hipLaunchKernelGGL((gemm_stream_kernel<WN, K, BMODE, false, true>), dim3(gx, panels), dim3(gst::THREADS), 0, s, p);
+  } else if (p.resid) {
     hipLaunchKernelGGL((gemm_stream_kernel<WN, K, BMODE, true>), dim3(gx, panels), dim3(gst::THREADS), 0, s, p);
-  else
+  } else {
     hipLaunchKernelGGL((gemm_stream_kernel<WN, K, BMODE, false>), dim3(gx, panels), dim3(gst::THREADS), 0, s, p);
+  }
   return (int)hipGetLastError();
 }
 
@@ -354,12 +395,16 @@ int gemm_stream_panel(int N, int K) {
 int launch_gemm_stream(const GemmParams& p, int epi, hipStream_t s) {
   int nb = gemm_stream_panel(p.N, p.K);
   if (p.resid && p.K == 128 && nb == 256) nb = 128;  // 256-wide panel + residual prefetch would spill
+  // the fused BN-backward reduction prefetches x and the mask per read-out vector: narrower panels keep
+  // those variants spill-free (128 wide up to K = 128, 64 at K = 256; A is re-read once more per panel)
+  if (p.bnr_x && nb > (p.K >= 256 ? 64 : 128)) nb = p.K >= 256 ? 64 : 128;
   const bool ok = nb && epi == EPI_BF16 && p.a_mode == OP_KC && (p.b_mode == OP_KC || p.b_mode == OP_RC) &&
                   !p.om.enabled && !p.aux && !p.drop_thresh && (p.relu == ACT_NONE || p.relu == ACT_RELU) &&
                   p.beta == 0.f && p.k_split >= p.K && p.lda % 8 == 0 && p.ldc % 8 == 0 &&
                   (p.b_mode == OP_RC || p.ldb % 8 == 0) && (!p.resid || p.ldr % 4 == 0) &&
                   ((uintptr_t)p.a % 16 == 0) && ((uintptr_t)p.c % 16 == 0) &&
-                  (p.b_mode == OP_RC || (uintptr_t)p.b % 16 == 0) && (!p.resid || (uintptr_t)p.resid % 8 == 0);
+                  (p.b_mode == OP_RC || (uintptr_t)p.b % 16 == 0) && (!p.resid || (uintptr_t)p.resid % 8 == 0) &&
+                  (!p.bnr_x || (p.stats && (uintptr_t)p.bnr_x % 16 == 0 && (uintptr_t)p.bnr_mean % 16 == 0));
   if (!ok) return (int)hipErrorInvalidValue;
   return p.b_mode == OP_KC ? launch_panel<OP_KC>(p, nb, s) : launch_panel<OP_RC>(p, nb, s);
 }

@@ -14,6 +14,8 @@ Reference semantics are unchanged: ``relu(bn3(conv3(relu(bn2(conv2(relu(bn1(conv
 """
 from __future__ import annotations
 
+import weakref
+
 import torch
 
 from . import conv as CV
@@ -24,9 +26,35 @@ from .streams import on_grad_stream
 
 
 class _ConvBNState:
-    """Per-(conv,BN) forward results needed by the backward."""
+    """Per-(conv,BN) forward results needed by the backward.  ``pre_reduced``: the BN-backward
+    partial sums [32, 2, C] already accumulated by the producer of this BN's output gradient
+    (the next block's conv1 data-gradient epilogue), so ``bn_backward`` skips its reduce sweep."""
 
-    __slots__ = ("g", "yc", "y", "mean", "invstd", "scale", "shift", "mode", "mask")
+    __slots__ = ("g", "yc", "y", "mean", "invstd", "scale", "shift", "mode", "mask", "pre_reduced", "__weakref__")
+
+    def __init__(self):
+        self.pre_reduced = None
+
+
+# Block outputs -> the (ConvBN unit, state) of the BN that produced them (weak references only): the
+# next bottleneck looks its input up here so that, in backward, its conv1 data-gradient (which
+# produces THIS BN's output gradient) can also accumulate this BN's backward partial sums.
+_PRODUCERS: dict = {}
+
+
+def _register_output(y, unit, st):
+    _PRODUCERS[y.data_ptr()] = (weakref.ref(y), unit, weakref.ref(st))
+    if len(_PRODUCERS) > 4096:  # stale entries of freed tensors
+        for k in [k for k, v in _PRODUCERS.items() if v[0]() is None]:
+            del _PRODUCERS[k]
+
+
+def _producer_of(x):
+    e = _PRODUCERS.get(x.data_ptr())
+    if e is None or e[0]() is not x:
+        return None
+    st = e[2]()
+    return None if st is None else (e[1], st)
 
 
 def _bn_forward(layer_bn, yc, stats, resid, relu, training, mask=None, apply=True, res_affine=None):
@@ -79,9 +107,12 @@ def bn_backward(unit, st, dy, want_dres):
     bn = unit.bn
     Cc = st.yc.shape[-1]
     M = st.yc.numel() // Cc
-    ws = partials_workspace(M, Cc, dy.device)
     y = st.y if st.mode == 1 else (st.mask if st.mode == 3 else None)
-    C().bn_bwd_reduce(dy, st.yc, y, st.scale, st.shift, st.mean, ws, Cc, st.mode)
+    if st.pre_reduced is not None:  # partial sums already accumulated by dy's producer (no reduce sweep)
+        ws, st.pre_reduced = st.pre_reduced, None
+    else:
+        ws = partials_workspace(M, Cc, dy.device)
+        C().bn_bwd_reduce(dy, st.yc, y, st.scale, st.shift, st.mean, ws, Cc, st.mode)
     coef = torch.empty(3 * Cc, dtype=torch.float32, device=dy.device)
     C().bn_bwd_finalize(ws, M, Cc, None if bn.gamma is None else bn.gamma.master, st.mean, st.invstd,
                         None if bn.gamma is None else bn.gamma.grad, None if bn.beta is None else bn.beta.grad, coef)
@@ -93,7 +124,7 @@ def bn_backward(unit, st, dy, want_dres):
     return dyc, dres
 
 
-def conv_backward(unit, st, dyc, x, need_dx, resid=None, resid_mask=None):
+def conv_backward(unit, st, dyc, x, need_dx, resid=None, resid_mask=None, bnr=None):
     conv = unit.conv
     # the weight gradient only feeds the optimizer / all-reduce: it runs on the side stream
     # (ops/streams.py) beside the data-gradient and BatchNorm sweeps of the layers below
@@ -103,12 +134,13 @@ def conv_backward(unit, st, dyc, x, need_dx, resid=None, resid_mask=None):
         conv.grad_hook()
     if not need_dx:
         return None
-    return CV.conv_dgrad_native(dyc, conv.kernel.data, st.g, resid=resid, resid_mask=resid_mask)
+    return CV.conv_dgrad_native(dyc, conv.kernel.data, st.g, resid=resid, resid_mask=resid_mask, bnr=bnr)
 
 
 class _BottleneckFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, anchor, block):
+        ctx.prev = _producer_of(x) if _FUSE_BNR else None  # the BN whose output is this block's input
         x = x.contiguous()
         # the downsample BN is not applied on its own: its scale/shift normalise the shortcut inside
         # the block-output apply sweep (one write + one read of the shortcut tensor saved)
@@ -121,6 +153,7 @@ class _BottleneckFn(torch.autograd.Function):
         ctx.block, ctx.states = block, (s_down, s1, s2, s3)
         ctx.save_for_backward(x)
         ctx.needs_dx = ctx.needs_input_grad[0]
+        _register_output(s3.y, block.c3, s3)
         return s3.y
 
     @staticmethod
@@ -140,13 +173,27 @@ class _BottleneckFn(torch.autograd.Function):
         if s_down is not None:
             ddc, _ = bn_backward(b.down, s_down, dsc, False)
             dsc = conv_backward(b.down, s_down, ddc, x, ctx.needs_dx)
-        # dX = dgrad(conv1) + dShortcut: the residual add rides in the conv1 dgrad epilogue
+        # dX = dgrad(conv1) + dShortcut: the residual add rides in the conv1 dgrad epilogue, and so do the
+        # backward partial sums of the BN that produced X (previous block's bn3, mode 3) when that GEMM
+        # runs on the streaming kernel — that BN's backward then skips its reduce sweep over dX and yc
+        bnr = None
+        if ctx.needs_dx and ctx.prev is not None and ctx.prev[1].mode == 3:
+            pst = ctx.prev[1]
+            bnr = {"x": pst.yc, "mask": pst.mask, "mean": pst.mean,
+                   "ws": new_stats_workspace(pst.yc.shape[-1], dout.device)}
         if masked_sc:
-            dx = conv_backward(b.c1, s1, d1c, x, ctx.needs_dx, resid=dout, resid_mask=s3.mask)
+            dx = conv_backward(b.c1, s1, d1c, x, ctx.needs_dx, resid=dout, resid_mask=s3.mask, bnr=bnr)
         else:
-            dx = conv_backward(b.c1, s1, d1c, x, ctx.needs_dx, resid=dsc)
-        ctx.states = None
+            dx = conv_backward(b.c1, s1, d1c, x, ctx.needs_dx, resid=dsc, bnr=bnr)
+        if bnr is not None and bnr.get("done"):
+            ctx.prev[1].pre_reduced = bnr["ws"]
+        ctx.states = ctx.prev = None
         return dx, None, None
+
+
+import os as _os
+
+_FUSE_BNR = _os.environ.get("DDL_FUSE_BN_REDUCE", "1") != "0"
 
 
 def bottleneck(block, x, anchor):

@@ -110,7 +110,7 @@ def choose_split(M: int, N: int, K: int, tile: int, allow: bool, rounds: float |
 
 def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, beta=0.0, bias=None, resid=None,
          ldr=0, relu=False, geom=None, outmap=None, b_kdiv=0, b_tap_stride=0, stats=None, tile=None, k_split=None,
-         bn_cap=128, aux=None, drop_p=0.0, drop_seed=0, split_rounds=None, resid_mask=None):
+         bn_cap=128, aux=None, drop_p=0.0, drop_seed=0, split_rounds=None, resid_mask=None, bnr=None):
     """Raw launcher with automatic tile / split-K choice.
 
     With ``epi == EPI_F32`` and a split-K decomposition the launch switches to the
@@ -132,8 +132,14 @@ def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, bet
         if beta not in (0.0, 1.0):
             raise ValueError("split-K fp32 gemm supports beta in {0,1} (beta=0 needs a zeroed C)")
         epi = EPI_F32_ATOMIC
+    if bnr is not None:  # fused BN-backward reduce of the output (streaming kernel only; see linear_dgrad)
+        if tile != TILE_STREAM:
+            raise ValueError("bnr: the fused BN-backward reduction runs on the streaming kernel only")
+        stats = bnr["ws"]
     C().gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, tile, k_split, alpha, beta, bias, resid, ldr,
-             int(relu), geom, outmap, b_kdiv, b_tap_stride, stats, aux, float(drop_p), int(drop_seed), resid_mask)
+             int(relu), geom, outmap, b_kdiv, b_tap_stride, stats, aux, float(drop_p), int(drop_seed), resid_mask,
+             None if bnr is None else bnr["x"], None if bnr is None else bnr.get("mask"),
+             None if bnr is None else bnr["mean"])
     return c
 
 
@@ -174,12 +180,15 @@ def splitk_workspace(M, N, device):
 _SPLITK_DGRAD = _os.environ.get("DDL_DGRAD_SPLITK", "1") != "0"
 
 
-def linear_dgrad(dy, w, out=None, resid=None, gelu_pre=None, stats=None, resid_mask=None):
+def linear_dgrad(dy, w, out=None, resid=None, gelu_pre=None, stats=None, resid_mask=None, bnr=None):
     """dx[M,K] = dy[M,N] @ w[N,K] (* gelu'(gelu_pre)) (+resid) -> bf16 (w read row-contiguous).
 
     ``stats`` ([32, 2, K] fp32, zeroed): per-column sums / sums of squares of the output;
     ``resid_mask``: uint8 ReLU bit mask of ``resid`` (bn.hip mode-3 layout) — only the masked
-    residual is added."""
+    residual is added; ``bnr`` = {"x", "mask", "mean", "ws"}: when this GEMM runs on the streaming
+    kernel, its epilogue also accumulates the BatchNorm-backward partial sums of the output
+    (``GemmParams.bnr_*``) into ``ws`` and ``bnr["done"]`` is set — the consumer BN then skips its
+    reduce sweep; otherwise ``bnr`` is left untouched."""
     M, N = dy.shape
     K = w.shape[1]
     if out is None:
@@ -205,6 +214,12 @@ def linear_dgrad(dy, w, out=None, resid=None, gelu_pre=None, stats=None, resid_m
         wt = transpose(w)
         return gemm(dy, wt, out, M, K, N, KC, KC, dy.stride(0), wt.stride(0), out.stride(0), EPI_BF16, resid=resid,
                     ldr=ldr, relu=act, aux=gelu_pre, stats=stats, resid_mask=resid_mask)
+    if bnr is not None and stats is None and use_stream(M, K, N, KC, RC, EPI_BF16, dy.stride(0), out.stride(0),
+                                                        aux=gelu_pre, relu=act, resid=resid, ldr=ldr):
+        gemm(dy, w, out, M, K, N, KC, RC, dy.stride(0), w.stride(0), out.stride(0), EPI_BF16, resid=resid, ldr=ldr,
+             relu=act, aux=gelu_pre, resid_mask=resid_mask, tile=TILE_STREAM, bnr=bnr)
+        bnr["done"] = True
+        return out
     return gemm(dy, w, out, M, K, N, KC, RC, dy.stride(0), w.stride(0), out.stride(0), EPI_BF16, resid=resid,
                 ldr=ldr, relu=act, aux=gelu_pre, stats=stats, resid_mask=resid_mask)
 

@@ -608,3 +608,68 @@ def test_conv3x3_halo_kernel(N, H, W, Ci, Co, bias_relu, monkeypatch):
     G.gemm(x, w, y2.view(g.M, Co), g.M, Co, 9 * Ci, G.KC_GATHER, G.KC, 0, 9 * Ci, Co, G.EPI_BF16, bias=b,
            relu=bias_relu, geom=g.fwd_geom)
     close(y, y2, rtol=1e-2, atol=1e-2, what="halo vs implicit GEMM")
+
+
+@pytest.mark.parametrize("M,N,K,resid", [(16384, 256, 64, True), (20000, 512, 128, True), (16384, 1024, 256, False)])
+def test_stream_dgrad_fused_bn_backward_reduce(M, N, K, resid):
+    """linear_dgrad on the streaming kernel with ``bnr``: the output equals the plain launch, and the
+    workspace holds sum_m d*relu and sum_m d*relu*(x - mean) of the STORED output (fp64 reference),
+    with relu the mode-3 bit mask — the partial sums bn_bwd_reduce would have produced."""
+    from distributeddeeplearningspark_amd.ops import gemm as G
+    from distributeddeeplearningspark_amd.ops.norm import SHARDS
+
+    gen = torch.Generator().manual_seed(M + N)
+    dy = torch.randn(M, K, generator=gen).to(DEV, torch.bfloat16)
+    w = (torch.randn(K, N, generator=gen) / K ** 0.5).to(DEV, torch.bfloat16)
+    r = torch.randn(M, N, generator=gen).to(DEV, torch.bfloat16) if resid else None
+    x = torch.randn(M, N, generator=gen).to(DEV, torch.bfloat16)
+    keep = torch.rand(M, N, generator=gen) > 0.4
+    bits = (keep.reshape(-1, 8).to(torch.uint8) << torch.arange(8, dtype=torch.uint8)).sum(1, dtype=torch.uint8)
+    mask = bits.to(DEV)
+    mean = torch.randn(N, generator=gen).to(DEV)
+    assert G.use_stream(M, N, K, G.KC, G.RC, G.EPI_BF16, K, N, resid=r, ldr=N if resid else 0)
+    ws = torch.zeros((SHARDS, 2, N), dtype=torch.float32, device=DEV)
+    bnr = {"x": x, "mask": mask, "mean": mean, "ws": ws}
+    out = G.linear_dgrad(dy, w, resid=r, bnr=bnr)
+    assert bnr.get("done")
+    ref_out = G.linear_dgrad(dy, w, resid=r)
+    assert torch.equal(out, ref_out)
+    d = out.double().cpu() * keep.double()
+    s1 = d.sum(0)
+    s2 = (d * (x.double().cpu() - mean.double().cpu())).sum(0)
+    got = ws.double().cpu().sum(0)
+    close(got[0], s1, rtol=1e-4, atol=1e-2 * s1.abs().mean().item(), what="sum d")
+    close(got[1], s2, rtol=1e-4, atol=1e-2 * s2.abs().mean().item(), what="sum d (x - mean)")
+
+
+def test_bottleneck_chain_fused_bn_reduce_matches_unfused(monkeypatch):
+    """Two identity-chained bottlenecks at stage-1 shapes (M = 64 x 16 x 16 = 16384 rows: the second
+    block's conv1 data-gradient runs on the streaming kernel and accumulates the first block's bn3
+    backward sums, whose reduce sweep is then skipped): every gradient equals the unfused run."""
+    from distributeddeeplearningspark_amd.models.resnet import ResNet
+    from distributeddeeplearningspark_amd.ops import fused_blocks as FB
+
+    torch.manual_seed(2)
+    x = torch.randn(64, 64, 64, 3)
+    y = torch.randint(0, 10, (64,))
+    out = {}
+    for fuse in (True, False):
+        monkeypatch.setattr(FB, "_FUSE_BNR", fuse)
+        m = ResNet(blocks=(2,), input_shape=(64, 64, 3), num_classes=10)
+        m.compile("sgd", "sparse_categorical_crossentropy")
+        m.place(DEV, seed=3)
+        xd, yd = m.to_input(x), m.to_target(y)
+        m.backward_step(xd, yd)  # warm-up (workspace pool sizing)
+        from torch.profiler import ProfilerActivity, profile
+
+        torch.cuda.synchronize()
+        with profile(activities=[ProfilerActivity.CUDA]) as prof:
+            loss = m.backward_step(xd, yd)
+            torch.cuda.synchronize()
+        n_reduce = sum(1 for e in prof.events() if "bn_bwd_reduce" in e.name)
+        out[fuse] = (float(loss), m.arena.grad.float().cpu().clone(), n_reduce)
+    (l1, g1, r1), (l0, g0, r0) = out[True], out[False]
+    assert r1 == r0 - 1, (r1, r0)  # block 1's bn3 reduce sweep was absorbed by block 2's conv1 dgrad
+    assert abs(l1 - l0) < 1e-5 * max(1.0, abs(l0))
+    rel = ((g1 - g0).norm() / g0.norm()).item()
+    assert rel < 2e-3, rel
