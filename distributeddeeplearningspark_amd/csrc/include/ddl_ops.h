@@ -38,7 +38,7 @@ int bn_bwd_dx(const void* dy, const void* x, const void* y, const float* scale, 
 
 // ---------------- pooling (NHWC) ----------------
 int maxpool_fwd(const void* x, void* y, uint8_t* argmax, int N, int H, int W, int C, int Ho, int Wo, int kh, int kw,
-                int sh, int sw, int ph, int pw, hipStream_t s);
+                int sh, int sw, int ph, int pw, hipStream_t s, const float* scale = nullptr, const float* shift = nullptr);
 int maxpool_bwd(const void* dy, const uint8_t* argmax, void* dx, int N, int H, int W, int C, int Ho, int Wo, int kh,
                 int kw, int sh, int sw, int ph, int pw, hipStream_t s);
 int avgpool_global_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t s);

@@ -21,10 +21,15 @@ __device__ __forceinline__ uint4 pack8p(const float* f) {
 // KH_/KW_/SH_/SW_: compile-time window and stride (0 = the runtime value): with constants the loops
 // unroll and the window loads issue together instead of one dependent load per loop trip
 // (stem-pool backward 242 -> 212 us, 2x2 / 2 backward 17.2 -> 12.1 us; scripts/bench_pool.py).
-template <int KH_, int KW_, int SH_, int SW_>
+// AFF: the input is a pre-BatchNorm tensor; relu(x * scale[c] + shift[c]) is applied to every loaded
+// element (the ResNet stem: its BN-apply sweep — a full write and re-read of the largest activation —
+// folds into the pool; padding windows are skipped, never compared, so no padded value is transformed).
+template <int KH_, int KW_, int SH_, int SW_, bool AFF = false>
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint4* __restrict__ x, uint4* __restrict__ y,
                                                            uint2* __restrict__ am, int N, int H, int W, int CV, int Ho,
-                                                           int Wo, int kh_, int kw_, int sh_, int sw_, int ph, int pw) {
+                                                           int Wo, int kh_, int kw_, int sh_, int sw_, int ph, int pw,
+                                                           const float* __restrict__ asc = nullptr,
+                                                           const float* __restrict__ ash = nullptr) {
   const int kh = KH_ ? KH_ : kh_, kw = KW_ ? KW_ : kw_, sh = SH_ ? SH_ : sh_, sw = SW_ ? SW_ : sw_;
   // 32-bit index math (the launcher guarantees total < 2^31): 64-bit divisions cost ~10x more
   const uint32_t total = (uint32_t)N * Ho * Wo * CV;
@@ -40,6 +45,13 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint4* __restric
       best[i] = -INFINITY;
       arg[i] = 0;
     }
+    float sc[8], sf[8];
+    if constexpr (AFF) {
+      const float4 a0 = reinterpret_cast<const float4*>(asc)[2 * cv], a1 = reinterpret_cast<const float4*>(asc)[2 * cv + 1];
+      const float4 b0 = reinterpret_cast<const float4*>(ash)[2 * cv], b1 = reinterpret_cast<const float4*>(ash)[2 * cv + 1];
+      sc[0] = a0.x; sc[1] = a0.y; sc[2] = a0.z; sc[3] = a0.w; sc[4] = a1.x; sc[5] = a1.y; sc[6] = a1.z; sc[7] = a1.w;
+      sf[0] = b0.x; sf[1] = b0.y; sf[2] = b0.z; sf[3] = b0.w; sf[4] = b1.x; sf[5] = b1.y; sf[6] = b1.z; sf[7] = b1.w;
+    }
 #pragma unroll
     for (int r = 0; r < kh; ++r) {
       const int ih = oh * sh - ph + r;
@@ -50,6 +62,10 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint4* __restric
         if ((unsigned)iw >= (unsigned)W) continue;
         float f[8];
         unpack8p(x[(((uint32_t)n * H + ih) * W + iw) * (uint32_t)CV + cv], f);  // < 2^31 (launcher)
+        if constexpr (AFF) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) f[i] = fmaxf(f[i] * sc[i] + sf[i], 0.f);
+        }
         const uint8_t idx = (uint8_t)(r * kw + s);
 #pragma unroll
         for (int i = 0; i < 8; ++i)
@@ -74,9 +90,15 @@ static unsigned pgrid(long n) {
 }
 
 int maxpool_fwd(const void* x, void* y, uint8_t* argmax, int N, int H, int W, int C, int Ho, int Wo, int kh, int kw,
-                int sh, int sw, int ph, int pw, hipStream_t s) {
+                int sh, int sw, int ph, int pw, hipStream_t s, const float* scale, const float* shift) {
   const long total = (long)N * Ho * Wo * (C / 8);
   if (total >= (1L << 31) || (long)N * H * W * (C / 8) >= (1L << 31)) return (int)hipErrorInvalidValue;
+  if (scale) {  // fused BN + ReLU on load (generic window loop)
+    if (!shift || kh > 16 || kw > 16) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL((maxpool_fwd_kernel<0, 0, 0, 0, true>), dim3(pgrid(total)), dim3(256), 0, s, (const uint4*)x,
+                       (uint4*)y, (uint2*)argmax, N, H, W, C / 8, Ho, Wo, kh, kw, sh, sw, ph, pw, scale, shift);
+    return (int)hipGetLastError();
+  }
 #define DDL_POOL_FWD(A, B, C_, D)                                                                          \
   hipLaunchKernelGGL((maxpool_fwd_kernel<A, B, C_, D>), dim3(pgrid(total)), dim3(256), 0, s, (const uint4*)x, \
                      (uint4*)y, (uint2*)argmax, N, H, W, C / 8, Ho, Wo, kh, kw, sh, sw, ph, pw)

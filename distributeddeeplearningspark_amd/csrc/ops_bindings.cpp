@@ -137,7 +137,7 @@ void bn_bwd_dx_(const at::Tensor& dy, const at::Tensor& x, c10::optional<at::Ten
 
 // ---------------------------------------------------------------- pooling
 void maxpool_fwd_(const at::Tensor& x, const at::Tensor& y, const at::Tensor& am, int64_t kh, int64_t kw, int64_t sh,
-                  int64_t sw, int64_t ph, int64_t pw) {
+                  int64_t sw, int64_t ph, int64_t pw, c10::optional<at::Tensor> scale, c10::optional<at::Tensor> shift) {
   GPU(x); BF16(x); BF16(y);
   CK(am.scalar_type() == at::kByte && am.is_contiguous(), "argmax must be uint8");
   CK(x.dim() == 4 && y.dim() == 4, "maxpool: NHWC tensors");
@@ -145,8 +145,15 @@ void maxpool_fwd_(const at::Tensor& x, const at::Tensor& y, const at::Tensor& am
   CK(C % 8 == 0 && y.size(0) == N && y.size(3) == C && am.numel() == y.numel(), "maxpool: shapes");
   CK(kh * kw <= 256, "maxpool: window too large for byte argmax");
   at::DeviceGuard g(x.device());
+  CK(scale.has_value() == shift.has_value(), "maxpool: scale and shift together");
+  if (scale) {
+    F32(*scale); F32(*shift);
+    CK(scale->numel() == C && shift->numel() == C && scale->is_contiguous() && shift->is_contiguous() &&
+           ((uintptr_t)scale->data_ptr() % 16) == 0 && ((uintptr_t)shift->data_ptr() % 16) == 0,
+       "maxpool: per-channel scale / shift [C], 16-B aligned");
+  }
   HIP_OK(maxpool_fwd(x.data_ptr(), y.data_ptr(), am.data_ptr<uint8_t>(), N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw,
-                     cur_stream()));
+                     cur_stream(), optr<const float>(scale), optr<const float>(shift)));
 }
 
 void maxpool_bwd_(const at::Tensor& dy, const at::Tensor& am, const at::Tensor& dx, int64_t kh, int64_t kw, int64_t sh,
@@ -440,7 +447,9 @@ void register_ops(py::module& m) {
   m.def("bn_bwd_reduce", &bn_bwd_reduce_);
   m.def("bn_bwd_finalize", &bn_bwd_finalize_);
   m.def("bn_bwd_dx", &bn_bwd_dx_);
-  m.def("maxpool_fwd", &maxpool_fwd_);
+  m.def("maxpool_fwd", &maxpool_fwd_, "NHWC max pool (byte argmax); optional fused BN affine + ReLU on load",
+        py::arg("x"), py::arg("y"), py::arg("am"), py::arg("kh"), py::arg("kw"), py::arg("sh"), py::arg("sw"),
+        py::arg("ph"), py::arg("pw"), py::arg("scale") = py::none(), py::arg("shift") = py::none());
   m.def("maxpool_bwd", &maxpool_bwd_);
   m.def("avgpool_fwd", &avgpool_fwd_);
   m.def("avgpool_bwd", &avgpool_bwd_);

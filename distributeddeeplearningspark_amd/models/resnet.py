@@ -143,13 +143,16 @@ class ResNet(Model):
         return True
 
     def forward(self, x, training=False, logits=False):
+        y = None
         if training and use_native(x) and _fused():
-            from ..ops.fused_blocks import convbn_relu
+            from ..ops.fused_blocks import convbn_relu, stem_pool
 
-            y = convbn_relu(self.stem, x, self.stem.conv.kernel.data)
-        else:
-            y = self.stem.call(x, training)
-        y = pool_ops.max_pool2d(y, 3, 2, 1)
+            # stem conv + BN + ReLU + max pool in one node (the pool applies the BN on load)
+            y = stem_pool(self.stem, x, self.stem.conv.kernel.data)
+            if y is None:
+                y = pool_ops.max_pool2d(convbn_relu(self.stem, x, self.stem.conv.kernel.data), 3, 2, 1)
+        if y is None:
+            y = pool_ops.max_pool2d(self.stem.call(x, training), 3, 2, 1)
         for b in self.stages:
             y = b.call(y, training)
         y = pool_ops.global_avg_pool(y)

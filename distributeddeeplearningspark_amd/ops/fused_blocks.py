@@ -233,6 +233,67 @@ def _s2d_weight_grad(g4, Cc):
     return g[:, :7, :7, :]
 
 
+class _StemPoolFn(torch.autograd.Function):
+    """ResNet stem conv (7x7 s2 p3 through space-to-depth) + BN + ReLU + 3x3/2 max pool as ONE node:
+    the BN affine and ReLU are applied by the pool as it loads the conv output (maxpool_fwd with
+    scale/shift), so the stem's BN-apply sweep — a write and a re-read of the largest activation of
+    the network (batch 256: 411 MB each way) — is gone.  Backward: pool gather -> BN backward (ReLU
+    mask recomputed from the conv output, mode 2) -> weight gradient, as before."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, unit, k, s, p):
+        x = x.contiguous()
+        N, H, W, Cc = x.shape
+        conv = unit.conv
+        Ho, Wo = (H + 6 + 1) // 2, (W + 6 + 1) // 2
+        xs = torch.empty((N, Ho, Wo, 16), dtype=x.dtype, device=x.device)
+        C().s2d_pad(x, xs, 3)
+        w4 = _s2d_weight(conv.kernel.data.detach())
+        g = CV.geometry(N, Ho, Wo, 16, conv.filters, 4, 4, (1, 1), (0, 0), (1, 1))
+        stats = new_stats_workspace(conv.filters, x.device)
+        yc = CV.conv_fwd_native(xs, w4, g, stats=stats)
+        st = _ConvBNState()
+        st.g, st.yc = g, yc
+        st.y, st.mean, st.invstd, st.scale, st.shift = _bn_forward(unit.bn, yc, stats, None, True, True, apply=False)
+        st.mode = 2
+        _, Hc, Wc, Co = yc.shape
+        Hp, Wp = (Hc + 2 * p - k) // s + 1, (Wc + 2 * p - k) // s + 1
+        y = torch.empty((N, Hp, Wp, Co), dtype=yc.dtype, device=yc.device)
+        am = torch.empty((N, Hp, Wp, Co), dtype=torch.uint8, device=yc.device)
+        C().maxpool_fwd(yc, y, am, k, k, s, s, p, p, st.scale, st.shift)
+        ctx.unit, ctx.st, ctx.cc, ctx.pool = unit, st, Cc, (k, s, p)
+        ctx.save_for_backward(xs, am)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xs, am = ctx.saved_tensors
+        unit, st = ctx.unit, ctx.st
+        k, s, p = ctx.pool
+        d = torch.empty_like(st.yc)
+        C().maxpool_bwd(dy.contiguous(), am, d, k, k, s, s, p, p)
+        dyc, _ = bn_backward(unit, st, d, False)
+        conv = unit.conv
+        g = st.g
+        with on_grad_stream(dy.device, dyc, xs, default=False):
+            tmp = torch.zeros((g.Co, 4, 4, 16), dtype=torch.float32, device=dy.device)
+            CV.conv_wgrad_native(dyc, xs, g, tmp)
+            conv.kernel.grad.add_(_s2d_weight_grad(tmp, ctx.cc))
+        if conv.grad_hook is not None:
+            conv.grad_hook()
+        ctx.st = None
+        return None, None, None, None, None, None  # the stem input is data: no gradient
+
+
+def stem_pool(unit, x, anchor, k=3, s=2, p=1):
+    """Stem conv+BN+ReLU followed by a k x k / s max pool, fused when the space-to-depth stem applies
+    (``DDL_STEM_POOL=0`` keeps the separate apply + pool); returns None when not applicable."""
+    if (_os.environ.get("DDL_STEM_POOL", "1") == "0" or x.requires_grad or not _stem_s2d_ok(unit.conv, x.shape[-1])
+            or unit.conv.filters % 8):
+        return None
+    return _StemPoolFn.apply(x, anchor, unit, k, s, p)
+
+
 class _StemS2DFn(torch.autograd.Function):
     """ResNet stem conv (7x7 s2 p3, 3 channels) + BN (+ReLU) through space-to-depth."""
 

@@ -673,3 +673,27 @@ def test_bottleneck_chain_fused_bn_reduce_matches_unfused(monkeypatch):
     assert abs(l1 - l0) < 1e-5 * max(1.0, abs(l0))
     rel = ((g1 - g0).norm() / g0.norm()).item()
     assert rel < 2e-3, rel
+
+
+def test_stem_pool_fusion_matches_separate_apply_and_pool(monkeypatch):
+    """Stem conv + BN + ReLU + 3x3/2 max pool as one node (the pool applies the BN affine + ReLU on
+    load) vs the separate BN-apply sweep + pool: same loss and gradients up to bf16 rounding of the
+    applied activation (the fused pool compares fp32 values, the separate path rounded them first)."""
+    from distributeddeeplearningspark_amd.models.resnet import ResNet
+
+    torch.manual_seed(3)
+    x = torch.randn(8, 64, 64, 3)
+    y = torch.randint(0, 10, (8,))
+    out = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("DDL_STEM_POOL", fused)
+        m = ResNet(blocks=(1,), input_shape=(64, 64, 3), num_classes=10)
+        m.compile("sgd", "sparse_categorical_crossentropy")
+        m.place(DEV, seed=4)
+        loss = m.backward_step(m.to_input(x), m.to_target(y))
+        out[fused] = (float(loss), m.arena.grad.float().cpu().clone(),
+                      m.stem.bn._states["moving_mean"].float().cpu().clone())
+    (l1, g1, r1), (l0, g0, r0) = out["1"], out["0"]
+    assert abs(l1 - l0) < 2e-3 * max(1.0, abs(l0)), (l1, l0)
+    assert ((g1 - g0).norm() / g0.norm()).item() < 2e-2
+    torch.testing.assert_close(r1, r0)  # the same batch statistics / running-stat update
