@@ -48,6 +48,9 @@ def main():
                     help="ResNet-50 through the DataFrame/trainer API: an ImageNet-shape uint8 frame, one partition "
                          "per rank, SynchronousDataParallel(...).train(df); the timed window is the trainer's own "
                          "steps after --warmup (barrier + synchronize on both sides)")
+    ap.add_argument("--executor-pool", action="store_true",
+                    help="--via-dataframe at N = 1: train in an executor process (the Spark-executor path: shard "
+                         "handed over through shared memory) instead of in the driver")
     ap.add_argument("--ingest", default="auto", choices=["auto", "resident", "stream"],
                     help="--via-dataframe: shard residency in HBM or the pinned-ring stream (ShardLoader)")
     ap.add_argument("--seq", type=int, default=512)
@@ -232,6 +235,8 @@ def bench_via_dataframe(args, pg):
     from distributeddeeplearningspark_amd.trainers import SynchronousDataParallel
 
     rank, world = pg.rank, pg.world_size
+    if args.executor_pool:
+        os.environ["DDL_FORCE_POOL"] = "1"
     per_rank = args.batch * (args.warmup + args.steps)
     rng = np.random.default_rng(7)
     n = per_rank * world
@@ -259,7 +264,8 @@ def bench_via_dataframe(args, pg):
             "data": "synthetic uint8 ImageNet-shape DataFrame via SynchronousDataParallel.train",
             "config": {"model": "resnet50", "global_batch": gb, "seq_len": None, "image": args.image,
                        "per_gpu_batch": args.batch, "parallelism": f"dp{world}", "optimizer": "sgd-momentum",
-                       "path": "dataframe", "ingest": res[0]["ingest"],
+                       "path": "dataframe" + ("+executor-pool" if args.executor_pool else ""),
+                       "ingest": res[0]["ingest"],
                        "final_loss": round(float(res[0]["history"][-1]), 4)},
         }), flush=True)
     pg.shutdown()

@@ -18,6 +18,13 @@ number of tasks.  The driver talks to them over an authenticated local socket
 * Any task failure, worker death or timeout tears the whole pool down (a collective of
   the surviving ranks may be stuck); the launcher's restart logic then starts a new one.
 * ``DDL_EXECUTOR_POOL=0`` disables caching (a fresh pool per call, stopped afterwards).
+* Partition arrays do not travel through the task pickle: every numpy array of at least
+  ``DDL_SHM_MIN_MB`` (default 1 MB) in a task's arguments is placed in POSIX shared memory
+  (``/dev/shm``) once and the executors map it as a zero-copy ``np.ndarray`` view — the analog of
+  the reference's cached partitions living on the executors (``repartition(num_workers)`` +
+  ``cache()``, ``ddl_mnist_aztk.py:155-161``).  Blocks are cached per source array (a repeated
+  ``train`` / ``predict`` on the same cached frame re-sends only a descriptor) and unlinked when the
+  source array is freed or the pool shuts down.
 """
 from __future__ import annotations
 
@@ -34,6 +41,114 @@ from multiprocessing.connection import Client, Listener
 
 _POOLS: dict = {}
 _LOCK = threading.Lock()
+
+
+# ============================================================================ shared-memory shards
+class ShmArray:
+    """Picklable descriptor of a numpy array held in a POSIX shared-memory block."""
+
+    __slots__ = ("name", "shape", "dtype", "offset")
+
+    def __init__(self, name, shape, dtype, offset=0):
+        self.name, self.shape, self.dtype, self.offset = name, tuple(shape), str(dtype), int(offset)
+
+    def __getstate__(self):
+        return (self.name, self.shape, self.dtype, self.offset)
+
+    def __setstate__(self, st):
+        self.name, self.shape, self.dtype, self.offset = st
+
+
+_SHM_BLOCKS: dict = {}  # key -> (SharedMemory, ShmArray, weakref.finalize)
+_SHM_LOCK = threading.Lock()
+
+
+def _shm_min_bytes() -> int:
+    return int(float(os.environ.get("DDL_SHM_MIN_MB", "1")) * (1 << 20))
+
+
+def _release_block(key):
+    with _SHM_LOCK:
+        e = _SHM_BLOCKS.pop(key, None)
+    if e is not None:
+        try:
+            e[0].close()
+            e[0].unlink()
+        except Exception:
+            pass
+
+
+def share_array(a):
+    """The shared-memory descriptor of ``a`` (copied into /dev/shm once per source array)."""
+    import weakref
+
+    import numpy as np
+    from multiprocessing import shared_memory
+
+    base = a
+    while isinstance(getattr(base, "base", None), np.ndarray):
+        base = base.base
+    key = (id(base), a.__array_interface__["data"][0], a.shape, a.strides, a.dtype.str)
+    with _SHM_LOCK:
+        e = _SHM_BLOCKS.get(key)
+    if e is not None:
+        return e[1]
+    c = np.ascontiguousarray(a)
+    shm = shared_memory.SharedMemory(create=True, size=max(1, c.nbytes))
+    np.ndarray(c.shape, c.dtype, buffer=shm.buf)[...] = c
+    desc = ShmArray(shm.name, c.shape, c.dtype)
+    try:
+        fin = weakref.finalize(base, _release_block, key)
+    except TypeError:  # not weak-referenceable: lives until the pool shuts down
+        fin = None
+    with _SHM_LOCK:
+        _SHM_BLOCKS[key] = (shm, desc, fin)
+    return desc
+
+
+def release_all_shared():
+    for key in list(_SHM_BLOCKS):
+        _release_block(key)
+
+
+def _share_args(obj):
+    import numpy as np
+
+    if isinstance(obj, np.ndarray) and obj.nbytes >= _shm_min_bytes() and obj.dtype != object:
+        return share_array(obj)
+    if isinstance(obj, tuple):
+        return tuple(_share_args(o) for o in obj)
+    if isinstance(obj, list):
+        return [_share_args(o) for o in obj]
+    if isinstance(obj, dict):
+        return {k: _share_args(v) for k, v in obj.items()}
+    return obj
+
+
+def _map_args(obj, opened):
+    """Executor side: descriptors -> zero-copy ndarray views (the SharedMemory objects stay open
+    in ``opened`` for the duration of the task)."""
+    import numpy as np
+    from multiprocessing import shared_memory
+
+    if isinstance(obj, ShmArray):
+        shm = opened.get(obj.name)
+        if shm is None:
+            shm = opened[obj.name] = shared_memory.SharedMemory(name=obj.name)
+            try:  # the driver owns the block: this process's resource tracker must not unlink it at exit
+                from multiprocessing import resource_tracker
+
+                resource_tracker.unregister(shm._name, "shared_memory")
+            except Exception:
+                pass
+        return np.ndarray(obj.shape, np.dtype(obj.dtype), buffer=shm.buf, offset=obj.offset)
+    if isinstance(obj, tuple):
+        return tuple(_map_args(o, opened) for o in obj)
+    if isinstance(obj, list):
+        return [_map_args(o, opened) for o in obj]
+    if isinstance(obj, dict):
+        return {k: _map_args(v, opened) for k, v in obj.items()}
+    return obj
 
 
 class PoolFailure(RuntimeError):
@@ -124,7 +239,8 @@ class ExecutorPool:
         except (TypeError, OSError):
             pass
         for r in range(self.world):
-            payload = pickle.dumps((fn, args_per_rank[r]), protocol=pickle.HIGHEST_PROTOCOL)
+            payload = pickle.dumps((fn, _share_args(args_per_rank[r])), protocol=pickle.HIGHEST_PROTOCOL)
+            self.last_payload_bytes = len(payload)
             self._conns[r].send(("task", paths, payload, env))
         results, errors = {}, {}
         deadline = time.time() + timeout_s
@@ -232,6 +348,7 @@ def shutdown_all():
         pools = list(_POOLS.values())
     for p in pools:
         p.shutdown()
+    release_all_shared()
 
 
 atexit.register(shutdown_all)
@@ -270,11 +387,24 @@ def _executor_main(port, authkey_hex, rank, world, pg_port, device, backend, thr
         for pth in paths:
             if pth not in sys.path:
                 sys.path.append(pth)
+        opened = {}
         try:
             fn, args = pickle.loads(payload)
+            # this file runs as __main__ in the executor: unpickled descriptors are instances of the
+            # PACKAGE module's ShmArray, so map them with that module's helper
+            from distributeddeeplearningspark_amd.parallel import executors as _pkg
+
+            args = _pkg._map_args(args, opened)
             out = ("ok", fn(int(rank), int(world), pg, *args))
         except BaseException:  # report every failure to the driver
             out = ("error", traceback.format_exc())
+        finally:
+            args = None
+            for shm in opened.values():
+                try:
+                    shm.close()
+                except BufferError:  # a view is still referenced by the task's result: leave it mapped
+                    pass
         try:
             conn.send(out)
         except Exception:

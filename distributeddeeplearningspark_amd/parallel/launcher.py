@@ -104,7 +104,9 @@ def _run_once(fn, num_workers, args_per_rank, device, timeout_s, attempt):
         res = fn(pg.rank, pg.world_size, pg, *args_per_rank[pg.rank])
         return pg.all_gather_object(res)
     devices = plan_devices(num_workers, device)
-    if num_workers == 1:
+    # DDL_FORCE_POOL=1: a single worker still runs in an executor process (the executor-pool path
+    # of the DataFrame bench at N = 1)
+    if num_workers == 1 and os.environ.get("DDL_FORCE_POOL", "0") != "1":
         import torch
 
         dev = torch.device(devices[0])

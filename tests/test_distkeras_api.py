@@ -342,3 +342,42 @@ def test_integer_feature_column_trains_and_predicts_as_float(spark):
     p = np.stack([r["prediction"].toArray() for r in out.collect()])
     ref = trained.predict(X.astype(np.float32), batch_size=64)
     np.testing.assert_allclose(p, ref, rtol=1e-5, atol=1e-5)
+
+
+def test_partitions_reach_executors_through_shared_memory(spark, monkeypatch):
+    """Executor-pool tasks carry shard DESCRIPTORS, not pickled arrays: the arrays are placed in
+    /dev/shm once and mapped zero-copy by the executors (parallel/executors.py); the training
+    result equals the pickle path, a repeated train() re-uses the blocks, and they are unlinked
+    when the pool shuts down."""
+    import glob
+
+    from distributeddeeplearningspark_amd.parallel import executors as EX
+    from distributeddeeplearningspark_amd.sql.dataframe import from_columns
+    from distributeddeeplearningspark_amd.trainers import ADAG
+
+    rng = np.random.default_rng(5)
+    X = rng.normal(size=(4096, 64)).astype(np.float32)  # 1 MB
+    y = (X[:, :1] * 0.5).astype(np.float32)
+    df = from_columns({"features": X, "label": y}, num_partitions=2)
+    out = {}
+    for mode, thr in (("shm", "0.01"), ("pickle", "100000")):
+        monkeypatch.setenv("DDL_SHM_MIN_MB", thr)
+        m = Sequential([Dense(1, input_shape=(64,))])
+        m.compile("sgd", "mean_squared_error")
+        tr = ADAG(keras_model=m, worker_optimizer="sgd", loss="mean_squared_error", num_workers=2, batch_size=64,
+                  communication_window=2, num_epoch=1, features_col="features", label_col="label", device="cpu")
+        w = tr.train(df).get_weights()
+        pool = next(iter(EX._POOLS.values()))
+        out[mode] = (w, pool.last_payload_bytes, len(EX._SHM_BLOCKS))
+        if mode == "shm":
+            blocks = len(EX._SHM_BLOCKS)
+            tr.train(df)  # same cached frame: no new blocks
+            assert len(EX._SHM_BLOCKS) == blocks
+            names = [e[1].name for e in EX._SHM_BLOCKS.values()]
+        EX.shutdown_all()
+    w_shm, bytes_shm, nblocks = out["shm"]
+    w_pk, bytes_pk, _ = out["pickle"]
+    assert nblocks >= 2 and bytes_shm < bytes_pk / 10, (bytes_shm, bytes_pk)
+    for a, b in zip(w_shm, w_pk):
+        np.testing.assert_array_equal(a, b)
+    assert not any(glob.glob("/dev/shm/" + n) for n in names)  # unlinked with the pool
