@@ -43,7 +43,11 @@ struct Conv3Tiling {
 // s-2, which every wave left before the barrier opening step s-1 — one barrier per tap (plus one
 // per 64-channel chunk for the halo reload).  NB = 2 (BN = 128: a third 16-KB slot would cost the
 // second workgroup per CU): the slot was read in step s-1, so each step also closes on a barrier.
-template <int BN, int EPI, int NB>
+// FR: 16-pixel fragments per wave along the tile's pixels (the two pixel waves split the tile at
+// FR * 16): 8 covers a full 256-pixel tile; 7 serves the 196-pixel tiles every ResNet-50 stage
+// plans (7 rows of 28, one 14x14 image, four 7x7 images) — with 8 the second pixel wave spent 3 of
+// its 8 fragments on rows past the tile, so every tap paid 16 MFMA blocks for 12.25 of work.
+template <int BN, int EPI, int NB, int FR = 8>
 __global__ __launch_bounds__(NTHREADS, 2) void conv3x3_halo_kernel(const GemmParams p, const Conv3Tiling t) {
   constexpr int RN = BN / 32;  // channel fragments per wave (2 waves along N)
   constexpr int B_BYTES = BN * BK * 2;
@@ -67,11 +71,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv3x3_halo_kernel(const GemmPar
   const int wm = wid >> 1, wn = wid & 1;
   const int wn0 = wn * (BN / 2);
 
-  // halo row of each of this lane's 8 pixel fragments (tap (0,0) = top-left of the 3x3 window)
-  int abase[8];
+  // halo row of each of this lane's FR pixel fragments (tap (0,0) = top-left of the 3x3 window)
+  int abase[FR];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int px = wm * 128 + 16 * i + (lane & 15);
+  for (int i = 0; i < FR; ++i) {
+    const int px = wm * (16 * FR) + 16 * i + (lane & 15);
     if (px < t.P) {
       const int im = px / (t.rows * t.w);
       const int rem = px - im * t.rows * t.w;
@@ -122,9 +126,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv3x3_halo_kernel(const GemmPar
     B.dma(buf, tap * C + kc * 64, g, 0, 0, wid);
   };
 
-  f32x4 acc[8][RN];
+  f32x4 acc[FR][RN];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < FR; ++i)
 #pragma unroll
     for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -141,17 +145,17 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv3x3_halo_kernel(const GemmPar
     const int toff = r * t.ww + c3;
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
-      bf16x8 af[8], bfr[RN];
+      bf16x8 af[FR], bfr[RN];
 #pragma unroll
       for (int j = 0; j < RN; ++j) bfr[j] = B.frag(lb, kk, j, wn0, lane);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
+      for (int i = 0; i < FR; ++i) {
         const int row = abase[i] + toff;
         const int ch = kk * 4 + (lane >> 4);
         af[i] = *reinterpret_cast<const bf16x8*>(halo + row * 128 + ((ch ^ (row & 6)) << 4));
       }
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < FR; ++i)
 #pragma unroll
         for (int j = 0; j < RN; ++j) acc[i][j] = mfma16x16x32(bfr[j], af[i], acc[i][j]);  // D^T (bf16 epilogue)
     }
@@ -162,7 +166,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv3x3_halo_kernel(const GemmPar
     if (tap == 8 && s + 1 < steps) stage_halo(kc + 1);
   }
 
-  gemm_epilogue<8, RN, EPI>(p, acc, m0 + wm * 128, n0 + wn0, lane, bid, mend);
+  gemm_epilogue<FR, RN, EPI>(p, acc, m0 + wm * (16 * FR), n0 + wn0, lane, bid, mend);
 }
 
 Conv3Tiling plan(const GemmParams& p) {
@@ -189,18 +193,29 @@ Conv3Tiling plan(const GemmParams& p) {
   return t;
 }
 
-template <int BN, int EPI, int NB>
-int launch(const GemmParams& p, const Conv3Tiling& t, hipStream_t s) {
+template <int BN, int EPI, int NB, int FR>
+int launch_fr(const GemmParams& p, const Conv3Tiling& t, hipStream_t s) {
   const int blocks = t.tiles_img * t.tiles_row * ((p.N + BN - 1) / BN);
   const size_t lds = (size_t)t.hr_pad * 128 + NB * BN * BK * 2;
   static bool attr = [] {  // dynamic LDS above 64 KB must be allowed explicitly (at most 80 KB here)
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_halo_kernel<BN, EPI, NB>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_halo_kernel<BN, EPI, NB, FR>),
                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                C3_MAX_HALO_ROWS * 128 + NB * BN * BK * 2) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL((conv3x3_halo_kernel<BN, EPI, NB>), dim3(blocks), dim3(NTHREADS), lds, s, p, t);
+  hipLaunchKernelGGL((conv3x3_halo_kernel<BN, EPI, NB, FR>), dim3(blocks), dim3(NTHREADS), lds, s, p, t);
   return (int)hipGetLastError();
+}
+
+// fragments per pixel wave: the fewest that cover half the tile (7 for the 196-pixel ResNet tiles)
+template <int BN, int EPI, int NB>
+int launch(const GemmParams& p, const Conv3Tiling& t, hipStream_t s) {
+  static const bool fr_off = [] {  // DDL_CONV3X3_FR8=1: always 8 fragments (A/B knob)
+    const char* e = getenv("DDL_CONV3X3_FR8");
+    return e && e[0] == '1';
+  }();
+  if (!fr_off && t.P <= 2 * 16 * 7) return launch_fr<BN, EPI, NB, 7>(p, t, s);
+  return launch_fr<BN, EPI, NB, 8>(p, t, s);
 }
 
 }  // namespace

@@ -204,21 +204,43 @@ def test_bert_tiny_gpu_matches_cpu():
     assert rel < 5e-2, rel
 
 
-def test_bert_base_layer_shapes_run():
-    """BERT-base geometry (H=768, 12 heads, I=3072, S=512) forward+backward of 2 layers."""
+def test_bert_base_layer_shapes_match_fp32_cpu():
+    """BERT-base geometry (H=768, 12 heads, I=3072, S=512, the 30,522-word tied decoder) with 2
+    encoder layers, dropout ON (same hash masks on both paths): one training step on the HIP path
+    vs the fp32 CPU reference — the loss, the whole flat gradient arena, and the cosine of every
+    weight matrix's gradient (so a wrong term in one BERT-base-shaped kernel cannot hide in the norm)."""
     from distributeddeeplearningspark_amd.models.bert import BertConfig, BertForMaskedLM
 
     cfg = BertConfig(num_hidden_layers=2)
-    m = BertForMaskedLM(cfg)
-    m.compile("adamw", "sparse_categorical_crossentropy")
-    m.place(DEV, seed=0)
     B, S, Pm = 2, 512, 80
-    ids = torch.randint(0, cfg.vocab_size, (B, S))
-    pos = torch.stack([torch.randperm(S)[:Pm].sort().values for _ in range(B)])
-    loss = m.train_on_batch({"input_ids": ids}, {"positions": pos, "labels": torch.gather(ids, 1, pos),
-                                                  "num_masked": B * Pm})
-    assert math.isfinite(loss) and abs(loss - math.log(cfg.vocab_size)) < 1.5, loss
-    assert torch.isfinite(m.arena.master).all()
+    g = torch.Generator().manual_seed(11)
+    ids = torch.randint(0, cfg.vocab_size, (B, S), generator=g)
+    pos = torch.stack([torch.randperm(S, generator=g)[:Pm].sort().values for _ in range(B)])
+    labels = torch.gather(ids, 1, pos)
+    res = {}
+    for dev in ("cpu", DEV):
+        m = BertForMaskedLM(cfg)
+        m.compile("adamw", "sparse_categorical_crossentropy")
+        m.place(dev, seed=0)
+        x = m.to_input({"input_ids": ids})
+        y = m.to_target({"positions": pos, "labels": labels, "num_masked": B * Pm})
+        loss = m.backward_step(x, y)
+        res[dev] = (float(loss.detach()), m.arena.grad.detach().float().cpu().clone(),
+                    {p.name: p.grad.detach().float().cpu().reshape(-1).clone() for p in m.arena.params
+                     if p.trainable and len(p.shape) == 2})
+    (lc, gc, pc), (lg, gg, pg) = res["cpu"], res[DEV]
+    assert math.isfinite(lg) and abs(lg - math.log(cfg.vocab_size)) < 1.5, lg
+    assert abs(lc - lg) < 1e-2 * abs(lc), (lc, lg)
+    rel = ((gg - gc).norm() / gc.norm()).item()
+    assert rel < 5e-2, rel
+    bad = []
+    for name, a in pc.items():
+        if a.norm() < 1e-8:
+            continue
+        cos = torch.nn.functional.cosine_similarity(pg[name], a, dim=0).item()
+        if cos < 0.97:
+            bad.append((name, round(cos, 4)))
+    assert not bad, bad
 
 
 def test_embed_word_grad_sorted_runs_and_pos_grad():
