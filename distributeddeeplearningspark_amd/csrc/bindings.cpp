@@ -57,7 +57,7 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
           c10::optional<py::dict> outmap, int64_t b_kdiv, int64_t b_tap_stride,
           c10::optional<at::Tensor> stats, c10::optional<at::Tensor> aux, double drop_p, int64_t drop_seed,
           c10::optional<at::Tensor> resid_mask, c10::optional<at::Tensor> bnr_x, c10::optional<at::Tensor> bnr_mask,
-          c10::optional<at::Tensor> bnr_mean) {
+          c10::optional<at::Tensor> bnr_mean, int64_t rsub_h, int64_t rsub_w) {
   CHECK_CUDA(a);
   CHECK_CUDA(b);
   CHECK_CUDA(c);
@@ -136,6 +136,15 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
     CHECK_CUDA(*resid);
     CHECK_BF16(*resid);
     p.resid = resid->data_ptr();
+  }
+  if (rsub_h > 0) {
+    TORCH_CHECK(resid.has_value() && epi == EPI_BF16 && !outmap.has_value() && !resid_mask.has_value() && rsub_w > 0 &&
+                    M % (rsub_h * rsub_w) == 0,
+                "gemm: a stride-2 residual needs resid (bf16, no outmap / mask) and M = N * rsub_h * rsub_w");
+    const int64_t hs = (rsub_h + 1) / 2, ws_ = (rsub_w + 1) / 2;
+    TORCH_CHECK(resid->numel() >= ((M / (rsub_h * rsub_w)) * hs * ws_ - 1) * ldr + N, "gemm: stride-2 residual too small");
+    p.rsub_h = (int)rsub_h;
+    p.rsub_w = (int)rsub_w;
   }
   if (resid_mask) {
     TORCH_CHECK(resid.has_value() && epi == EPI_BF16 && !outmap.has_value(), "gemm: resid_mask needs a residual (bf16, no outmap)");
@@ -221,7 +230,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("b_kdiv") = 0, py::arg("b_tap_stride") = 0, py::arg("stats") = py::none(),
         py::arg("aux") = py::none(), py::arg("drop_p") = 0.0, py::arg("drop_seed") = 0,
         py::arg("resid_mask") = py::none(), py::arg("bnr_x") = py::none(), py::arg("bnr_mask") = py::none(),
-        py::arg("bnr_mean") = py::none());
+        py::arg("bnr_mean") = py::none(), py::arg("rsub_h") = 0, py::arg("rsub_w") = 0);
   m.attr("ACT_NONE") = (int)ACT_NONE;
   m.attr("ACT_RELU") = (int)ACT_RELU;
   m.attr("ACT_GELU") = (int)ACT_GELU;

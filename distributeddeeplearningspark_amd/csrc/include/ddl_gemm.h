@@ -97,6 +97,12 @@ struct GemmParams {
   const void* bnr_x;        // bf16 [M][ldc]
   const uint8_t* bnr_mask;  // bit (m*ldc + n) of the ReLU mask, or null
   const float* bnr_mean;    // [N] batch mean of bnr_x
+  // stride-2 residual: when rsub_h > 0 the output rows m = (n, i, j) form an [N][rsub_h][rsub_w] grid
+  // and ``resid`` lives on its stride-2 subgrid ([N][(rsub_h+1)/2][(rsub_w+1)/2], row stride ldr):
+  // rows with even (i, j) add resid row ((n * Hs + i/2) * Ws + j/2), the others add nothing — the
+  // data-gradient of a ResNet stride-2 1x1 downsample shortcut, added at half resolution instead of
+  // being scattered (with zeros) to full resolution first
+  int rsub_h, rsub_w;
 };
 
 enum Activation : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_GELU_BWD = 3 };

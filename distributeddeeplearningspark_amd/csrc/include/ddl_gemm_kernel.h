@@ -470,8 +470,15 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
           for (int e = 0; e < 4; ++e)
             v[e] = drop_keep(p.drop_seed, base + e, p.drop_thresh) ? v[e] * p.drop_scale : 0.f;
         }
-        if (!LITE && p.resid) {
-          const bf16_t* r = reinterpret_cast<const bf16_t*>(p.resid) + (long)m * p.ldr + n;
+        long rrow = m;  // residual row of output row m (stride-2 subgrid: -1 = nothing to add)
+        if (!LITE && p.resid && p.rsub_h) {
+          int rn_, ri_, rj_;
+          pix_decompose((uint32_t)m, p.rsub_h, p.rsub_w, rn_, ri_, rj_);
+          rrow = ((ri_ | rj_) & 1) ? -1L
+                                   : ((long)rn_ * ((p.rsub_h + 1) >> 1) + (ri_ >> 1)) * ((p.rsub_w + 1) >> 1) + (rj_ >> 1);
+        }
+        if (!LITE && p.resid && rrow >= 0) {
+          const bf16_t* r = reinterpret_cast<const bf16_t*>(p.resid) + rrow * p.ldr + n;
           float rv4[4];
           if (full) {
             const uint2 rv = *reinterpret_cast<const uint2*>(r);

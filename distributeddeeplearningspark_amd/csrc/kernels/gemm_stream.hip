@@ -180,13 +180,21 @@ __global__ __launch_bounds__(gst::THREADS, 2) void gemm_stream_kernel(const Gemm
 #pragma unroll
       for (int mb = 0; mb < BM / 16; ++mb) {
         const int m = min(m0 + 16 * mb + (lane & 15), p.M - 1);
-        const long row = (long)m * p.ldr + n0 + WN * w;
+        long rrow = m;  // stride-2 residual subgrid (GemmParams::rsub_h): odd rows add nothing
+        bool rodd = false;
+        if (p.rsub_h) {
+          int rn_, ri_, rj_;
+          pix_decompose((uint32_t)m, p.rsub_h, p.rsub_w, rn_, ri_, rj_);
+          rodd = (ri_ | rj_) & 1;
+          rrow = rodd ? 0L : ((long)rn_ * ((p.rsub_h + 1) >> 1) + (ri_ >> 1)) * ((p.rsub_w + 1) >> 1) + (rj_ >> 1);
+        }
+        const long row = rrow * p.ldr + n0 + WN * w;
 #pragma unroll
         for (int rn = 0; rn < CF::RN; ++rn)
           rres[mb][rn] = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(p.resid) + row + 16 * rn +
                                                          4 * (lane >> 4));
-        rmsk[mb] = ~0ull;
-        if (has_mask) {
+        rmsk[mb] = rodd ? 0ull : ~0ull;
+        if (has_mask && !rodd) {
           const uint8_t* mp = p.resid_mask + (row >> 3);
           if constexpr (CF::RN == 1) rmsk[mb] = *reinterpret_cast<const uint16_t*>(mp);
           else if constexpr (CF::RN == 2) rmsk[mb] = *reinterpret_cast<const uint32_t*>(mp);

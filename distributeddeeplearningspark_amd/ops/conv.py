@@ -230,14 +230,15 @@ def class_filter(w, g: ConvGeometry, cl):
     return w.reshape(g.Co, g.T, g.Ci).index_select(1, _tap_index(cl, w.device)).permute(2, 1, 0).contiguous()
 
 
-def conv_dgrad_native(dy, w, g: ConvGeometry, resid=None, resid_mask=None, bnr=None):
+def conv_dgrad_native(dy, w, g: ConvGeometry, resid=None, resid_mask=None, bnr=None, rsub=None):
     """dx = conv^T(dy, w) (+ resid, fused into the epilogue when the layout allows; with
     ``resid_mask`` (1x1 / stride 1 only) only where the residual's ReLU bit is set).  ``bnr``:
     fused BN-backward reduction of dx (pointwise convs on the streaming kernel; see
-    ``gemm.linear_dgrad``)."""
+    ``gemm.linear_dgrad``).  ``rsub = (H, W)``: ``resid`` is on the stride-2 subgrid of dx (pointwise
+    convs only)."""
     dev = dy.device
-    if resid_mask is not None and not g.is_pointwise:
-        raise ValueError("resid_mask is supported for pointwise (1x1, stride 1) data-gradients only")
+    if (resid_mask is not None or rsub is not None) and not g.is_pointwise:
+        raise ValueError("resid_mask / rsub are supported for pointwise (1x1, stride 1) data-gradients only")
     if resid is None:
         g2 = _dgrad_as_forward(g)
         if g2 is not None:
@@ -245,7 +246,8 @@ def conv_dgrad_native(dy, w, g: ConvGeometry, resid=None, resid_mask=None, bnr=N
     if g.is_pointwise:
         dx = torch.empty((g.N, g.H, g.W, g.Ci), dtype=torch.bfloat16, device=dev)
         G.linear_dgrad(dy.view(g.M, g.Co), w.view(g.Co, g.Ci), out=dx.view(-1, g.Ci),
-                       resid=None if resid is None else resid.view(-1, g.Ci), resid_mask=resid_mask, bnr=bnr)
+                       resid=None if resid is None else resid.view(-1, g.Ci), resid_mask=resid_mask, bnr=bnr,
+                       rsub=rsub)
         return dx
     dx = (torch.zeros if g.dgrad_needs_zero else torch.empty)((g.N, g.H, g.W, g.Ci), dtype=torch.bfloat16, device=dev)
     strided = g.sh > 1 or g.sw > 1

@@ -124,7 +124,7 @@ def bn_backward(unit, st, dy, want_dres):
     return dyc, dres
 
 
-def conv_backward(unit, st, dyc, x, need_dx, resid=None, resid_mask=None, bnr=None):
+def conv_backward(unit, st, dyc, x, need_dx, resid=None, resid_mask=None, bnr=None, rsub=None):
     conv = unit.conv
     # the weight gradient only feeds the optimizer / all-reduce: it runs on the side stream
     # (ops/streams.py) beside the data-gradient and BatchNorm sweeps of the layers below
@@ -134,7 +134,7 @@ def conv_backward(unit, st, dyc, x, need_dx, resid=None, resid_mask=None, bnr=No
         conv.grad_hook()
     if not need_dx:
         return None
-    return CV.conv_dgrad_native(dyc, conv.kernel.data, st.g, resid=resid, resid_mask=resid_mask, bnr=bnr)
+    return CV.conv_dgrad_native(dyc, conv.kernel.data, st.g, resid=resid, resid_mask=resid_mask, bnr=bnr, rsub=rsub)
 
 
 class _BottleneckFn(torch.autograd.Function):
@@ -170,9 +170,21 @@ class _BottleneckFn(torch.autograd.Function):
         d2c, _ = bn_backward(b.c2, s2, d2, False)
         d1 = conv_backward(b.c2, s2, d2c, s1.y, True)
         d1c, _ = bn_backward(b.c1, s1, d1, False)
+        rsub = None
         if s_down is not None:
             ddc, _ = bn_backward(b.down, s_down, dsc, False)
-            dsc = conv_backward(b.down, s_down, ddc, x, ctx.needs_dx)
+            gd = s_down.g
+            if (_HALF_RES_SC and ctx.needs_dx and s1.g.is_pointwise and gd.KH == 1 and gd.KW == 1
+                    and (gd.sh, gd.sw) == (2, 2) and (gd.ph, gd.pw) == (0, 0)):
+                # stride-2 1x1 shortcut: its data-gradient stays at half resolution ([N, H/2, W/2, Cin], a plain
+                # GEMM) and conv1's dgrad epilogue adds it at the even pixels — instead of a scatter GEMM that
+                # writes a full-resolution tensor of 3/4 zeros which that epilogue then reads back
+                conv_backward(b.down, s_down, ddc, x, False)  # weight gradient only
+                wd = b.down.conv.kernel.data
+                dsc = G.linear_dgrad(ddc.view(gd.M, gd.Co), wd.view(gd.Co, gd.Ci))
+                rsub = (gd.H, gd.W)
+            else:
+                dsc = conv_backward(b.down, s_down, ddc, x, ctx.needs_dx)
         # dX = dgrad(conv1) + dShortcut: the residual add rides in the conv1 dgrad epilogue, and so do the
         # backward partial sums of the BN that produced X (previous block's bn3, mode 3) when that GEMM
         # runs on the streaming kernel — that BN's backward then skips its reduce sweep over dX and yc
@@ -184,7 +196,7 @@ class _BottleneckFn(torch.autograd.Function):
         if masked_sc:
             dx = conv_backward(b.c1, s1, d1c, x, ctx.needs_dx, resid=dout, resid_mask=s3.mask, bnr=bnr)
         else:
-            dx = conv_backward(b.c1, s1, d1c, x, ctx.needs_dx, resid=dsc, bnr=bnr)
+            dx = conv_backward(b.c1, s1, d1c, x, ctx.needs_dx, resid=dsc, bnr=bnr, rsub=rsub)
         if bnr is not None and bnr.get("done"):
             ctx.prev[1].pre_reduced = bnr["ws"]
         ctx.states = ctx.prev = None
@@ -194,6 +206,7 @@ class _BottleneckFn(torch.autograd.Function):
 import os as _os
 
 _FUSE_BNR = _os.environ.get("DDL_FUSE_BN_REDUCE", "1") != "0"
+_HALF_RES_SC = _os.environ.get("DDL_HALF_RES_SHORTCUT", "1") != "0"
 
 
 def bottleneck(block, x, anchor):

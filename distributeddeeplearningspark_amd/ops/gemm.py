@@ -110,7 +110,7 @@ def choose_split(M: int, N: int, K: int, tile: int, allow: bool, rounds: float |
 
 def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, beta=0.0, bias=None, resid=None,
          ldr=0, relu=False, geom=None, outmap=None, b_kdiv=0, b_tap_stride=0, stats=None, tile=None, k_split=None,
-         bn_cap=128, aux=None, drop_p=0.0, drop_seed=0, split_rounds=None, resid_mask=None, bnr=None):
+         bn_cap=128, aux=None, drop_p=0.0, drop_seed=0, split_rounds=None, resid_mask=None, bnr=None, rsub=None):
     """Raw launcher with automatic tile / split-K choice.
 
     With ``epi == EPI_F32`` and a split-K decomposition the launch switches to the
@@ -139,7 +139,7 @@ def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, bet
     C().gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, tile, k_split, alpha, beta, bias, resid, ldr,
              int(relu), geom, outmap, b_kdiv, b_tap_stride, stats, aux, float(drop_p), int(drop_seed), resid_mask,
              None if bnr is None else bnr["x"], None if bnr is None else bnr.get("mask"),
-             None if bnr is None else bnr["mean"])
+             None if bnr is None else bnr["mean"], *(rsub or (0, 0)))
     return c
 
 
@@ -180,7 +180,7 @@ def splitk_workspace(M, N, device):
 _SPLITK_DGRAD = _os.environ.get("DDL_DGRAD_SPLITK", "1") != "0"
 
 
-def linear_dgrad(dy, w, out=None, resid=None, gelu_pre=None, stats=None, resid_mask=None, bnr=None):
+def linear_dgrad(dy, w, out=None, resid=None, gelu_pre=None, stats=None, resid_mask=None, bnr=None, rsub=None):
     """dx[M,K] = dy[M,N] @ w[N,K] (* gelu'(gelu_pre)) (+resid) -> bf16 (w read row-contiguous).
 
     ``stats`` ([32, 2, K] fp32, zeroed): per-column sums / sums of squares of the output;
@@ -188,7 +188,8 @@ def linear_dgrad(dy, w, out=None, resid=None, gelu_pre=None, stats=None, resid_m
     residual is added; ``bnr`` = {"x", "mask", "mean", "ws"}: when this GEMM runs on the streaming
     kernel, its epilogue also accumulates the BatchNorm-backward partial sums of the output
     (``GemmParams.bnr_*``) into ``ws`` and ``bnr["done"]`` is set — the consumer BN then skips its
-    reduce sweep; otherwise ``bnr`` is left untouched."""
+    reduce sweep; otherwise ``bnr`` is left untouched.  ``rsub = (H, W)``: the rows are an
+    [N][H][W] grid and ``resid`` lives on its stride-2 subgrid (``GemmParams.rsub_h``)."""
     M, N = dy.shape
     K = w.shape[1]
     if out is None:
@@ -196,7 +197,7 @@ def linear_dgrad(dy, w, out=None, resid=None, gelu_pre=None, stats=None, resid_m
     act = ACT_GELU_BWD if gelu_pre is not None else ACT_NONE
     ldr = resid.stride(0) if resid is not None else 0
     tiles = math.ceil(M / 64) * math.ceil(K / 64)
-    if (_SPLITK_DGRAD and gelu_pre is None and resid is None and N >= 4096 and tiles <= 1024 and K % 8 == 0
+    if (_SPLITK_DGRAD and gelu_pre is None and resid is None and rsub is None and N >= 4096 and tiles <= 1024 and K % 8 == 0
             and out.is_contiguous() and out.dtype == torch.bfloat16 and dy.device.type == "cuda"):
         # few output tiles over a long reduction (BERT's MLM decoder: [masked tokens, 768] over the
         # 30,522-word vocabulary ran on 240 workgroups of ~480 K-steps): split the reduction over
@@ -213,15 +214,15 @@ def linear_dgrad(dy, w, out=None, resid=None, gelu_pre=None, stats=None, resid_m
         # of paired transposed LDS reads: the BERT-size data-gradients run ~1.4x faster this way
         wt = transpose(w)
         return gemm(dy, wt, out, M, K, N, KC, KC, dy.stride(0), wt.stride(0), out.stride(0), EPI_BF16, resid=resid,
-                    ldr=ldr, relu=act, aux=gelu_pre, stats=stats, resid_mask=resid_mask)
+                    ldr=ldr, relu=act, aux=gelu_pre, stats=stats, resid_mask=resid_mask, rsub=rsub)
     if bnr is not None and stats is None and use_stream(M, K, N, KC, RC, EPI_BF16, dy.stride(0), out.stride(0),
                                                         aux=gelu_pre, relu=act, resid=resid, ldr=ldr):
         gemm(dy, w, out, M, K, N, KC, RC, dy.stride(0), w.stride(0), out.stride(0), EPI_BF16, resid=resid, ldr=ldr,
-             relu=act, aux=gelu_pre, resid_mask=resid_mask, tile=TILE_STREAM, bnr=bnr)
+             relu=act, aux=gelu_pre, resid_mask=resid_mask, tile=TILE_STREAM, bnr=bnr, rsub=rsub)
         bnr["done"] = True
         return out
     return gemm(dy, w, out, M, K, N, KC, RC, dy.stride(0), w.stride(0), out.stride(0), EPI_BF16, resid=resid,
-                ldr=ldr, relu=act, aux=gelu_pre, stats=stats, resid_mask=resid_mask)
+                ldr=ldr, relu=act, aux=gelu_pre, stats=stats, resid_mask=resid_mask, rsub=rsub)
 
 
 def transpose(w):

@@ -698,3 +698,23 @@ def test_stem_pool_fusion_matches_separate_apply_and_pool(monkeypatch):
     assert abs(l1 - l0) < 2e-3 * max(1.0, abs(l0)), (l1, l0)
     assert ((g1 - g0).norm() / g0.norm()).item() < 2e-2
     torch.testing.assert_close(r1, r0)  # the same batch statistics / running-stat update
+
+
+@pytest.mark.parametrize("N,H,W,K,C", [(16, 56, 56, 128, 256), (8, 14, 14, 512, 1024), (64, 28, 28, 256, 512)])
+def test_dgrad_stride2_subgrid_residual(N, H, W, K, C):
+    """linear_dgrad with ``rsub=(H, W)``: the residual lives on the stride-2 subgrid and is added only at
+    even (i, j) — equal to scattering it to full resolution (zeros elsewhere) and adding that (both the
+    streaming kernel, K <= 256, and the LDS-DMA kernel, K = 512)."""
+    from distributeddeeplearningspark_amd.ops import gemm as G
+
+    Hs, Ws = (H + 1) // 2, (W + 1) // 2
+    M = N * H * W
+    dy = rnd(M, K, seed=31)
+    w = rnd(K, C, seed=32, scale=K ** -0.5)
+    rs = rnd(N * Hs * Ws, C, seed=33)
+    out = G.linear_dgrad(dy, w, resid=rs, rsub=(H, W))
+    full = torch.zeros(N, H, W, C, dtype=torch.bfloat16, device=DEV)
+    full[:, ::2, ::2, :] = rs.view(N, Hs, Ws, C)
+    ref = G.linear_dgrad(dy, w, resid=full.view(M, C))
+    close(out, ref, rtol=1e-2, atol=1e-2, what="stride-2 residual")
+    assert torch.equal(out.view(N, H, W, C)[:, 1::2], ref.view(N, H, W, C)[:, 1::2])
