@@ -57,7 +57,8 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
           c10::optional<py::dict> outmap, int64_t b_kdiv, int64_t b_tap_stride,
           c10::optional<at::Tensor> stats, c10::optional<at::Tensor> aux, double drop_p, int64_t drop_seed,
           c10::optional<at::Tensor> resid_mask, c10::optional<at::Tensor> bnr_x, c10::optional<at::Tensor> bnr_mask,
-          c10::optional<at::Tensor> bnr_mean, int64_t rsub_h, int64_t rsub_w) {
+          c10::optional<at::Tensor> bnr_mean, int64_t rsub_h, int64_t rsub_w, c10::optional<at::Tensor> a_scale,
+          c10::optional<at::Tensor> a_shift, c10::optional<at::Tensor> b_scale, c10::optional<at::Tensor> b_shift) {
   CHECK_CUDA(a);
   CHECK_CUDA(b);
   CHECK_CUDA(c);
@@ -204,6 +205,24 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
       p.bnr_mask = bnr_mask->data_ptr<uint8_t>();
     }
   }
+  auto norm_pair = [&](const c10::optional<at::Tensor>& sc, const c10::optional<at::Tensor>& sh, int64_t n,
+                       const char* what) -> std::pair<const float*, const float*> {
+    if (!sc && !sh) return {nullptr, nullptr};
+    TORCH_CHECK(sc && sh, "gemm: ", what, " scale and shift together");
+    CHECK_CUDA(*sc);
+    CHECK_F32(*sc);
+    CHECK_F32(*sh);
+    TORCH_CHECK(sc->numel() >= n && sh->numel() >= n && ((uintptr_t)sc->data_ptr() % 16) == 0 &&
+                    ((uintptr_t)sh->data_ptr() % 16) == 0,
+                "gemm: ", what, " scale / shift must cover the channels and be 16-B aligned");
+    return {sc->data_ptr<float>(), sh->data_ptr<float>()};
+  };
+  std::tie(p.a_scale, p.a_shift) = norm_pair(a_scale, a_shift, K, "A normalise-on-load");
+  std::tie(p.b_scale, p.b_shift) = norm_pair(b_scale, b_shift, N, "B normalise-on-load");
+  if (p.a_scale) TORCH_CHECK(tile == kTileStream && a_mode == OP_KC, "gemm: A normalise-on-load needs the streaming kernel");
+  if (p.b_scale)
+    TORCH_CHECK(a_mode == OP_RC && b_mode == OP_RC && epi != EPI_BF16 && K % 64 == 0 && k_split % 64 == 0,
+                "gemm: B normalise-on-load needs a plain RC x RC fp32 GEMM over whole K-tiles");
   (void)bm;
   if (tile == kTileConv3)
     TORCH_CHECK(conv3x3_halo_ok(p) && epi == EPI_BF16, "gemm conv3x3: needs a 3x3 / stride-1 / pad-1 KC_GATHER x KC "
@@ -230,7 +249,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("b_kdiv") = 0, py::arg("b_tap_stride") = 0, py::arg("stats") = py::none(),
         py::arg("aux") = py::none(), py::arg("drop_p") = 0.0, py::arg("drop_seed") = 0,
         py::arg("resid_mask") = py::none(), py::arg("bnr_x") = py::none(), py::arg("bnr_mask") = py::none(),
-        py::arg("bnr_mean") = py::none(), py::arg("rsub_h") = 0, py::arg("rsub_w") = 0);
+        py::arg("bnr_mean") = py::none(), py::arg("rsub_h") = 0, py::arg("rsub_w") = 0,
+        py::arg("a_scale") = py::none(), py::arg("a_shift") = py::none(), py::arg("b_scale") = py::none(),
+        py::arg("b_shift") = py::none());
   m.attr("ACT_NONE") = (int)ACT_NONE;
   m.attr("ACT_RELU") = (int)ACT_RELU;
   m.attr("ACT_GELU") = (int)ACT_GELU;

@@ -103,6 +103,15 @@ struct GemmParams {
   // data-gradient of a ResNet stride-2 1x1 downsample shortcut, added at half resolution instead of
   // being scattered (with zeros) to full resolution first
   int rsub_h, rsub_w;
+  // normalise-on-load (BatchNorm + ReLU of the PRODUCER folded into this GEMM's operand read):
+  // an operand element of channel c becomes relu(v * scale[c] + shift[c]) before the MFMA.  The channel
+  // is k for a K-contiguous A operand (a_scale: streaming kernel, A tiles transformed in LDS) and the
+  // operand row for a row-contiguous B operand (b_scale: LDS-DMA kernel, transformed in the fragment).
+  // The pre-BN tensor is then the only copy: the producer's BN-apply sweep is not run.
+  const float* a_scale;
+  const float* a_shift;
+  const float* b_scale;
+  const float* b_shift;
 };
 
 enum Activation : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_GELU_BWD = 3 };

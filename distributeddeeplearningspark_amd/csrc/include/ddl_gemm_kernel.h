@@ -348,6 +348,21 @@ struct Operand {
   }
 };
 
+// normalise-on-load of a fragment whose 8 values share one channel (row-contiguous B operand)
+__device__ __forceinline__ bf16x8 norm_frag(const bf16x8 f, float sc, float sh) {
+  const s16x8 v = __builtin_bit_cast(s16x8, f);
+  s16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {
+    const float a = fmaxf(__uint_as_float((uint32_t)(uint16_t)v[j] << 16) * sc + sh, 0.f);
+    const float b = fmaxf(__uint_as_float((uint32_t)(uint16_t)v[j + 1] << 16) * sc + sh, 0.f);
+    const uint32_t pk = pack_bf16x2(a, b);
+    o[j] = (short)(pk & 0xffffu);
+    o[j + 1] = (short)(pk >> 16);
+  }
+  return __builtin_bit_cast(bf16x8, o);
+}
+
 // Epilogue shared by the GEMM kernels.  mb / nb: first row / column of this wave's
 // RM x RN fragment block; rows >= mend (default p.M) are not stored (tile-local row limits of
 // the halo conv kernel).  bf16 epilogue: acc holds D^T fragments (lane owns 4 consecutive
@@ -675,7 +690,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams
 // ddl_zero_page).  ST = 1: one LDS stage per block (32 KB at 128x128, so 4 blocks share a CU
 // and each block's load latency hides under the others' MFMAs); ST = 2: two stages, the next
 // K-tile's DMA in flight under the current tile's MFMAs (counted vmcnt, raw barriers).
-template <int BM, int BN, int AMODE, int BMODE, int EPI, int ST>
+// BNORM (row-contiguous B only): GemmParams::b_scale / b_shift normalise every B fragment (one channel
+// per lane and fragment: 2 registers per fragment column, loaded once) — a weight gradient reading the
+// pre-BatchNorm output of the layer below instead of its applied copy.
+template <int BM, int BN, int AMODE, int BMODE, int EPI, int ST, bool BNORM = false>
 __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_kernel(const GemmParams p) {
   constexpr int WTM = BM / 2, WTN = BN / 2;
   constexpr int RM = WTM / 16, RN = WTN / 16;
@@ -707,6 +725,21 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
   }
   A.init(p.a, p.lda, p.M, m0, p.K, p.g, kbeg);
   B.init(p.b, p.ldb, p.N, n0, p.K, p.g, kbeg);
+  static_assert(!BNORM || BMODE == OP_RC, "normalise-on-load: row-contiguous B only");
+  float bsc[BNORM ? RN : 1], bsh[BNORM ? RN : 1];
+  if constexpr (BNORM) {
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      const int n = min(n0 + wn0 + 16 * j + (lane & 15), p.N - 1);
+      bsc[j] = p.b_scale[n];
+      bsh[j] = p.b_shift[n];
+    }
+  }
+  auto bfrag = [&](const char* lb, int kk, int j) {
+    const bf16x8 f = B.frag(lb, kk, j, wn0, lane);
+    if constexpr (BNORM) return norm_frag(f, bsc[j], bsh[j]);
+    else return f;
+  };
 
   f32x4 acc[RM][RN];
 #pragma unroll
@@ -749,7 +782,7 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
 #pragma unroll
         for (int i = 0; i < RM; ++i) af[i] = A.frag(la, kk, i, wm0, lane);
 #pragma unroll
-        for (int j = 0; j < RN; ++j) bf[j] = B.frag(lb, kk, j, wn0, lane);
+        for (int j = 0; j < RN; ++j) bf[j] = bfrag(lb, kk, j);
 #pragma unroll
         for (int i = 0; i < RM; ++i)
 #pragma unroll
@@ -791,7 +824,7 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
 #pragma unroll
       for (int i = 0; i < RM; ++i) af[i] = A.frag(la, kk, i, wm0, lane);
 #pragma unroll
-      for (int j = 0; j < RN; ++j) bf[j] = B.frag(lb, kk, j, wn0, lane);
+      for (int j = 0; j < RN; ++j) bf[j] = bfrag(lb, kk, j);
 #pragma unroll
       for (int i = 0; i < RM; ++i)
 #pragma unroll
@@ -853,19 +886,20 @@ inline int device_cus() {
   return cus;
 }
 
-template <int BM, int BN, int AMODE, int BMODE, int EPI, int ST>
+template <int BM, int BN, int AMODE, int BMODE, int EPI, int ST, bool BNORM = false>
 inline int launch_ring(const dim3 grid, const GemmParams& p, hipStream_t s) {
   constexpr int lds = ST * (BM + BN) * BK * 2 + tap_table_bytes<AMODE, BMODE>();
   static bool attr = [] {  // dynamic LDS above 64 KB must be allowed explicitly
-    return lds <= 65536 || hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_dma_kernel<BM, BN, AMODE, BMODE, EPI, ST>),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
+    return lds <= 65536 ||
+           hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_dma_kernel<BM, BN, AMODE, BMODE, EPI, ST, BNORM>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, AMODE, BMODE, EPI, ST>), grid, dim3(NTHREADS), lds, s, p);
+  hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, AMODE, BMODE, EPI, ST, BNORM>), grid, dim3(NTHREADS), lds, s, p);
   return (int)hipGetLastError();
 }
 
-template <int BM, int BN, int AMODE, int BMODE, int EPI>
+template <int BM, int BN, int AMODE, int BMODE, int EPI, bool BNORM = false>
 inline int launch_tile(const GemmParams& p, hipStream_t s) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
   const int splits = (p.K + p.k_split - 1) / p.k_split;
@@ -885,16 +919,18 @@ inline int launch_tile(const GemmParams& p, hipStream_t s) {
     const int st = one_stage ? 1
                              : (wgrad_stages() ? wgrad_stages()
                                                : (plain ? 3 : (gather_stages() ? gather_stages() : 1)));
-    if (dm == 1 && st == 3) return launch_ring<BM, BN, AMODE, BMODE, EPI, 3>(grid, p, s);
-    if (dm == 1 && st == 4) return launch_ring<BM, BN, AMODE, BMODE, EPI, 4>(grid, p, s);
+    if (dm == 1 && st == 3) return launch_ring<BM, BN, AMODE, BMODE, EPI, 3, BNORM>(grid, p, s);
+    if (dm == 1 && st == 4) return launch_ring<BM, BN, AMODE, BMODE, EPI, 4, BNORM>(grid, p, s);
   }
   constexpr int TAPB = tap_table_bytes<AMODE, BMODE>();
   if (dm == 1 || (dm == 2 && one_stage)) {
-    hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, AMODE, BMODE, EPI, 1>), grid, dim3(NTHREADS), (BM + BN) * BK * 2 + TAPB,
-                       s, p);
+    hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, AMODE, BMODE, EPI, 1, BNORM>), grid, dim3(NTHREADS),
+                       (BM + BN) * BK * 2 + TAPB, s, p);
   } else if (dm == 2) {
-    hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, AMODE, BMODE, EPI, 2>), grid, dim3(NTHREADS),
+    hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, AMODE, BMODE, EPI, 2, BNORM>), grid, dim3(NTHREADS),
                        2 * (BM + BN) * BK * 2 + TAPB, s, p);
+  } else if (BNORM) {
+    return (int)hipErrorInvalidValue;  // the register-staged kernel has no normalise-on-load
   } else {
     const size_t lds = (one_stage ? 1 : 2) * (BM + BN) * BK * 2 + TAPB;
     hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, AMODE, BMODE, EPI>), grid, dim3(NTHREADS), lds, s, p);
@@ -907,13 +943,13 @@ inline bool needs_full_epilogue(const GemmParams& p) {
   return p.om.enabled || p.resid || p.aux || p.drop_thresh || p.relu > ACT_RELU;
 }
 
-template <int AMODE, int BMODE, int EPI>
+template <int AMODE, int BMODE, int EPI, bool BNORM = false>
 inline int launch_modes(const GemmParams& p, int tile, hipStream_t s) {
   switch (tile) {
-    case 0: return launch_tile<128, 128, AMODE, BMODE, EPI>(p, s);
-    case 1: return launch_tile<128, 64, AMODE, BMODE, EPI>(p, s);
-    case 2: return launch_tile<64, 128, AMODE, BMODE, EPI>(p, s);
-    default: return launch_tile<64, 64, AMODE, BMODE, EPI>(p, s);
+    case 0: return launch_tile<128, 128, AMODE, BMODE, EPI, BNORM>(p, s);
+    case 1: return launch_tile<128, 64, AMODE, BMODE, EPI, BNORM>(p, s);
+    case 2: return launch_tile<64, 128, AMODE, BMODE, EPI, BNORM>(p, s);
+    default: return launch_tile<64, 64, AMODE, BMODE, EPI, BNORM>(p, s);
   }
 }
 

@@ -13,6 +13,10 @@ int launch_gemm_bf16(const GemmParams& p, int epi, int tile, void* stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (p.M <= 0 || p.N <= 0) return 0;
   if (p.bnr_x && tile != kTileStream) return (int)hipErrorInvalidValue;  // fused BN-backward reduce: streaming kernel only
+  if (p.a_scale && tile != kTileStream) return (int)hipErrorInvalidValue;  // normalise-on-load of A: streaming kernel
+  if (p.b_scale && !(p.a_mode == OP_RC && p.b_mode == OP_RC && (epi == EPI_F32 || epi == EPI_F32_ATOMIC) &&
+                     tile <= 3 && p.K % 64 == 0 && p.k_split % 64 == 0))
+    return (int)hipErrorInvalidValue;  // normalise-on-load of B: plain RC x RC weight gradients, whole K-tiles
   const bool plain = (p.a_mode == OP_KC || p.a_mode == OP_RC) && (p.b_mode == OP_KC || p.b_mode == OP_RC);
   if (tile == kTile256) {  // 256x256 ping-pong kernel: plain operands, K and k_split multiples of 64
     if (!plain || p.K % 64 || p.k_split % 64 || p.om.enabled) return (int)hipErrorInvalidValue;

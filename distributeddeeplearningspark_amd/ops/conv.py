@@ -141,9 +141,16 @@ def splitk_fwd_ok(g: ConvGeometry) -> bool:
     return math.ceil(g.M / 64) * math.ceil(g.Co / 64) <= _SPLITK_MAX_TILES
 
 
-def conv_fwd_native(x, w, g: ConvGeometry, bias=None, relu=False, stats=None):
+def conv_fwd_native(x, w, g: ConvGeometry, bias=None, relu=False, stats=None, x_norm=None):
+    """``x_norm = (scale, shift)``: x is pre-BatchNorm and normalised on load (pointwise convs on the
+    streaming kernel: :func:`norm_on_load_ok`)."""
     y = torch.empty((g.N, g.Ho, g.Wo, g.Co), dtype=torch.bfloat16, device=x.device)
     y2 = y.view(g.M, g.Co)
+    if x_norm is not None:
+        if not norm_on_load_ok(g):
+            raise ValueError("conv_fwd_native: normalise-on-load not supported for this geometry")
+        G.linear_fwd(x.view(g.M, g.Ci), w.view(g.Co, g.Ci), bias=bias, relu=relu, out=y2, stats=stats, x_norm=x_norm)
+        return y
     if splitk_fwd_ok(g):
         ws = G.splitk_workspace(g.M, g.Co, x.device)
         K = g.T * g.Ci
@@ -290,11 +297,20 @@ def conv_dgrad_native(dy, w, g: ConvGeometry, resid=None, resid_mask=None, bnr=N
     return dx
 
 
-def conv_wgrad_native(dy, x, g: ConvGeometry, gw):
-    """gw[Co, KH, KW, Ci] (fp32) += dW."""
+def norm_on_load_ok(g: ConvGeometry) -> bool:
+    """A pointwise conv can read a pre-BatchNorm input and normalise it on load in BOTH its forward
+    (streaming kernel) and its weight gradient (RC x RC GEMM over whole 64-pixel K-tiles)."""
+    return (g.is_pointwise and g.M % 64 == 0 and _os.environ.get("DDL_NORM_ON_LOAD", "1") != "0"
+            and G.norm_on_load_fwd_ok(g.M, g.Co, g.Ci, g.Ci, g.Co))
+
+
+def conv_wgrad_native(dy, x, g: ConvGeometry, gw, x_norm=None):
+    """gw[Co, KH, KW, Ci] (fp32) += dW.  ``x_norm``: x is pre-BatchNorm (pointwise convs only)."""
     gw2 = gw.view(g.Co, g.T * g.Ci)
+    if x_norm is not None and not g.is_pointwise:
+        raise ValueError("conv_wgrad_native: normalise-on-load for pointwise convs only")
     if g.is_pointwise:
-        G.linear_wgrad(dy.view(g.M, g.Co), x.view(g.M, g.Ci), gw2)
+        G.linear_wgrad(dy.view(g.M, g.Co), x.view(g.M, g.Ci), gw2, x_norm=x_norm)
     elif g.implicit_wgrad and g.Ci < 128 and _WIDE_WGRAD:
         # narrow inputs (64 channels): a 128-wide tile spans two taps, so the tap is resolved per
         # 16-B vector (GATHER8) instead of per tile — twice the MFMA work per LDS fragment read

@@ -25,6 +25,11 @@ from .norm import new_stats_workspace, partials_workspace
 from .streams import on_grad_stream
 
 
+def _norm_of(st):
+    """(scale, shift) when the unit's BN output was NOT materialised (its consumer normalises on load)."""
+    return None if st.y is not None else (st.scale, st.shift)
+
+
 class _ConvBNState:
     """Per-(conv,BN) forward results needed by the backward.  ``pre_reduced``: the BN-backward
     partial sums [32, 2, C] already accumulated by the producer of this BN's output gradient
@@ -81,16 +86,17 @@ def _bn_forward(layer_bn, yc, stats, resid, relu, training, mask=None, apply=Tru
     return y, mean, invstd, scale, shift
 
 
-def convbn_forward(unit, x, resid=None, relu=True, apply=True, res_affine=None):
+def convbn_forward(unit, x, resid=None, relu=True, apply=True, res_affine=None, x_norm=None):
     """conv (fused statistics) + BN (+resid)(+relu) for a ``models.resnet.ConvBN`` unit.
-    ``apply=False``: statistics and scale/shift only (``st.y`` is None: the consumer applies them)."""
+    ``apply=False``: statistics and scale/shift only (``st.y`` is None: the consumer applies them).
+    ``x_norm``: x is the pre-BN output of the previous unit, normalised on load by this conv."""
     conv, bn = unit.conv, unit.bn
     N, H, W, Ci = x.shape
     kh, kw = conv.kernel_size
     p = conv.padding if isinstance(conv.padding, tuple) else (kh // 2, kw // 2)
     g = CV.geometry(N, H, W, Ci, conv.filters, kh, kw, conv.strides, p, conv.dilation_rate)
     stats = new_stats_workspace(conv.filters, x.device)
-    yc = CV.conv_fwd_native(x, conv.kernel.data, g, stats=stats)
+    yc = CV.conv_fwd_native(x, conv.kernel.data, g, stats=stats, x_norm=x_norm)
     st = _ConvBNState()
     st.g, st.yc = g, yc
     # ReLU after a residual add: the backward mask cannot be recomputed from yc alone, so the
@@ -124,12 +130,12 @@ def bn_backward(unit, st, dy, want_dres):
     return dyc, dres
 
 
-def conv_backward(unit, st, dyc, x, need_dx, resid=None, resid_mask=None, bnr=None, rsub=None):
+def conv_backward(unit, st, dyc, x, need_dx, resid=None, resid_mask=None, bnr=None, rsub=None, x_norm=None):
     conv = unit.conv
     # the weight gradient only feeds the optimizer / all-reduce: it runs on the side stream
     # (ops/streams.py) beside the data-gradient and BatchNorm sweeps of the layers below
     with on_grad_stream(dyc.device, dyc, x, default=False):
-        CV.conv_wgrad_native(dyc, x, st.g, conv.kernel.grad)
+        CV.conv_wgrad_native(dyc, x, st.g, conv.kernel.grad, x_norm=x_norm)
     if conv.grad_hook is not None:
         conv.grad_hook()
     if not need_dx:
@@ -147,9 +153,19 @@ class _BottleneckFn(torch.autograd.Function):
         s_down = convbn_forward(block.down, x, relu=False, apply=False) if block.down is not None else None
         sc = s_down.yc if s_down is not None else x
         s1 = convbn_forward(block.c1, x, relu=True)
-        s2 = convbn_forward(block.c2, s1.y, relu=True)
-        s3 = convbn_forward(block.c3, s2.y, resid=sc, relu=True,
-                            res_affine=None if s_down is None else (s_down.scale, s_down.shift))
+        # normalise-on-load: conv3 (1x1) reads bn2's PRE-BN input and applies bn2 + ReLU as it loads it, in
+        # its forward (streaming kernel) and its weight gradient — bn2's apply sweep (a write and a re-read
+        # of the block's width-channel tensor) is not run
+        c2 = block.c2.conv
+        kh2, kw2 = c2.kernel_size
+        p2 = c2.padding if isinstance(c2.padding, tuple) else (kh2 // 2, kw2 // 2)
+        g2 = CV.geometry(x.shape[0], s1.g.Ho, s1.g.Wo, s1.g.Co, c2.filters, kh2, kw2, c2.strides, p2, c2.dilation_rate)
+        n3 = _NORM_ON_LOAD and CV.norm_on_load_ok(CV.geometry(x.shape[0], g2.Ho, g2.Wo, c2.filters,
+                                                              block.c3.conv.filters, 1, 1, (1, 1), (0, 0), (1, 1)))
+        s2 = convbn_forward(block.c2, s1.y, relu=True, apply=not n3)
+        s3 = convbn_forward(block.c3, s2.yc if n3 else s2.y, resid=sc, relu=True,
+                            res_affine=None if s_down is None else (s_down.scale, s_down.shift),
+                            x_norm=(s2.scale, s2.shift) if n3 else None)
         ctx.block, ctx.states = block, (s_down, s1, s2, s3)
         ctx.save_for_backward(x)
         ctx.needs_dx = ctx.needs_input_grad[0]
@@ -166,7 +182,7 @@ class _BottleneckFn(torch.autograd.Function):
         # backward writing it out, conv1's data-gradient epilogue adds dout under the bit mask
         masked_sc = s_down is None and s3.mode == 3 and s1.g.is_pointwise
         d3c, dsc = bn_backward(b.c3, s3, dout, want_dres=not masked_sc)
-        d2 = conv_backward(b.c3, s3, d3c, s2.y, True)
+        d2 = conv_backward(b.c3, s3, d3c, s2.yc if s2.y is None else s2.y, True, x_norm=_norm_of(s2))
         d2c, _ = bn_backward(b.c2, s2, d2, False)
         d1 = conv_backward(b.c2, s2, d2c, s1.y, True)
         d1c, _ = bn_backward(b.c1, s1, d1, False)
@@ -207,6 +223,7 @@ import os as _os
 
 _FUSE_BNR = _os.environ.get("DDL_FUSE_BN_REDUCE", "1") != "0"
 _HALF_RES_SC = _os.environ.get("DDL_HALF_RES_SHORTCUT", "1") != "0"
+_NORM_ON_LOAD = _os.environ.get("DDL_NORM_ON_LOAD", "1") != "0"
 
 
 def bottleneck(block, x, anchor):

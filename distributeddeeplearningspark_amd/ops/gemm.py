@@ -110,7 +110,8 @@ def choose_split(M: int, N: int, K: int, tile: int, allow: bool, rounds: float |
 
 def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, beta=0.0, bias=None, resid=None,
          ldr=0, relu=False, geom=None, outmap=None, b_kdiv=0, b_tap_stride=0, stats=None, tile=None, k_split=None,
-         bn_cap=128, aux=None, drop_p=0.0, drop_seed=0, split_rounds=None, resid_mask=None, bnr=None, rsub=None):
+         bn_cap=128, aux=None, drop_p=0.0, drop_seed=0, split_rounds=None, resid_mask=None, bnr=None, rsub=None,
+         a_norm=None, b_norm=None):
     """Raw launcher with automatic tile / split-K choice.
 
     With ``epi == EPI_F32`` and a split-K decomposition the launch switches to the
@@ -139,7 +140,8 @@ def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, bet
     C().gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, tile, k_split, alpha, beta, bias, resid, ldr,
              int(relu), geom, outmap, b_kdiv, b_tap_stride, stats, aux, float(drop_p), int(drop_seed), resid_mask,
              None if bnr is None else bnr["x"], None if bnr is None else bnr.get("mask"),
-             None if bnr is None else bnr["mean"], *(rsub or (0, 0)))
+             None if bnr is None else bnr["mean"], *(rsub or (0, 0)), *(a_norm or (None, None)),
+             *(b_norm or (None, None)))
     return c
 
 
@@ -150,10 +152,12 @@ ACT_NONE, ACT_RELU, ACT_GELU, ACT_GELU_BWD = 0, 1, 2, 3
 
 
 def linear_fwd(x2, w, bias=None, relu=False, out=None, resid=None, stats=None, act=None, aux=None, drop_p=0.0,
-               drop_seed=0):
+               drop_seed=0, x_norm=None):
     """y[M,N] = x2[M,K] @ w[N,K]^T (+bias) -> act -> dropout (+resid) -> bf16.
 
-    ``act``: ACT_RELU / ACT_GELU (``aux`` receives the bf16 pre-activation)."""
+    ``act``: ACT_RELU / ACT_GELU (``aux`` receives the bf16 pre-activation).  ``x_norm = (scale,
+    shift)``: x2 is a pre-BatchNorm tensor, normalised on load as relu(x * scale + shift) per channel
+    (streaming kernel only: check :func:`norm_on_load_fwd_ok` first)."""
     M, K = x2.shape
     N = w.shape[0]
     if out is None:
@@ -161,7 +165,12 @@ def linear_fwd(x2, w, bias=None, relu=False, out=None, resid=None, stats=None, a
     act = (ACT_RELU if relu else ACT_NONE) if act is None else act
     return gemm(x2, w, out, M, N, K, KC, KC, x2.stride(0), w.stride(0), out.stride(0), EPI_BF16, bias=bias, relu=act,
                 resid=resid, ldr=(resid.stride(0) if resid is not None else 0), stats=stats, aux=aux, drop_p=drop_p,
-                drop_seed=drop_seed)
+                drop_seed=drop_seed, a_norm=x_norm, tile=TILE_STREAM if x_norm is not None else None)
+
+
+def norm_on_load_fwd_ok(M, N, K, lda, ldc) -> bool:
+    """A forward 1x1 conv / Linear y = x W^T can normalise x on load (the streaming kernel runs it)."""
+    return use_stream(M, N, K, KC, KC, EPI_BF16, lda, ldc)
 
 
 _SPLITK_WS = {}
@@ -236,14 +245,17 @@ def transpose(w):
     return out
 
 
-def linear_wgrad(dy, x2, gw):
-    """gw[N,K] += dy[M,N]^T @ x2[M,K]  (fp32 accumulation into the gradient arena)."""
+def linear_wgrad(dy, x2, gw, x_norm=None):
+    """gw[N,K] += dy[M,N]^T @ x2[M,K]  (fp32 accumulation into the gradient arena).  ``x_norm``: x2 is
+    pre-BatchNorm, normalised on load per channel (needs M % 64 == 0: whole K-tiles)."""
     M, N = dy.shape
     K = x2.shape[1]
+    if x_norm is not None and M % 64:
+        raise ValueError("linear_wgrad: normalise-on-load needs M % 64 == 0")
     # measured on the ResNet-50 1x1 weight gradients: one workgroup round (half the fp32 atomics
     # of two rounds) is 5-15 % faster — these GEMMs are bound by the split-K atomics, not MFMA
     return gemm(dy, x2, gw, N, K, M, RC, RC, dy.stride(0), x2.stride(0), gw.stride(0), EPI_F32, beta=1.0,
-                split_rounds=_LINEAR_WGRAD_ROUNDS)
+                split_rounds=_LINEAR_WGRAD_ROUNDS, b_norm=x_norm)
 
 
 def matmul(a, b, trans_a=False, trans_b=False, out=None, alpha=1.0):

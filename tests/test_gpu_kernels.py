@@ -718,3 +718,60 @@ def test_dgrad_stride2_subgrid_residual(N, H, W, K, C):
     ref = G.linear_dgrad(dy, w, resid=full.view(M, C))
     close(out, ref, rtol=1e-2, atol=1e-2, what="stride-2 residual")
     assert torch.equal(out.view(N, H, W, C)[:, 1::2], ref.view(N, H, W, C)[:, 1::2])
+
+
+@pytest.mark.parametrize("M,K,N", [(16384, 64, 256), (20480, 128, 512), (16384, 256, 1024)])
+def test_normalise_on_load_fwd_and_wgrad(M, K, N):
+    """A pre-BatchNorm input normalised on load — relu(x * scale + shift) per channel — in the forward
+    1x1 GEMM (streaming kernel, A tile transformed in LDS) and in the weight gradient (RC x RC, B fragment
+    transformed): both equal the same GEMMs on the materialised bf16 activation (the transform rounds to
+    bf16 exactly as the BN-apply sweep does, so the operands are bit-identical)."""
+    from distributeddeeplearningspark_amd.ops import gemm as G
+    from distributeddeeplearningspark_amd.ops._native import C as _C
+
+    x = rnd(M, K, seed=41)
+    w = rnd(N, K, seed=42, scale=K ** -0.5)
+    sc = (torch.rand(K, generator=torch.Generator().manual_seed(43)) + 0.5).to(DEV)
+    sh = (torch.randn(K, generator=torch.Generator().manual_seed(44)) * 0.5).to(DEV)
+    xa = torch.empty_like(x)
+    _C().bn_apply(x, sc, sh, None, xa, K, True, None, None, None)
+    assert G.norm_on_load_fwd_ok(M, N, K, K, N)
+    y = G.linear_fwd(x, w, x_norm=(sc, sh))
+    y_ref = G.linear_fwd(xa, w)
+    close(y, y_ref, rtol=1e-2, atol=1e-2, what="fwd normalise-on-load")
+    dy = rnd(M, N, seed=45)
+    gw = torch.zeros(N, K, device=DEV)
+    gw_ref = torch.zeros(N, K, device=DEV)
+    G.linear_wgrad(dy, x, gw, x_norm=(sc, sh))
+    G.linear_wgrad(dy, xa, gw_ref)
+    close(gw, gw_ref, rtol=1e-3, atol=1e-3, what="wgrad normalise-on-load")
+
+
+def test_bottleneck_norm_on_load_matches_applied(monkeypatch):
+    """Stage-1 bottlenecks (M = 64 x 16 x 16 rows): conv3 reading bn2's pre-BN tensor with the apply
+    folded into its loads gives the same loss, gradients and running statistics as the applied path."""
+    from distributeddeeplearningspark_amd.models.resnet import ResNet
+    from distributeddeeplearningspark_amd.ops import fused_blocks as FB
+
+    torch.manual_seed(6)
+    x = torch.randn(64, 64, 64, 3)
+    y = torch.randint(0, 10, (64,))
+    out = {}
+    for on in (True, False):
+        monkeypatch.setattr(FB, "_NORM_ON_LOAD", on)
+        m = ResNet(blocks=(2,), input_shape=(64, 64, 3), num_classes=10)
+        m.compile("sgd", "sparse_categorical_crossentropy")
+        m.place(DEV, seed=8)
+        xd, yd = m.to_input(x), m.to_target(y)
+        from torch.profiler import ProfilerActivity, profile
+
+        torch.cuda.synchronize()
+        with profile(activities=[ProfilerActivity.CUDA]) as prof:
+            loss = m.backward_step(xd, yd)
+            torch.cuda.synchronize()
+        n_apply = sum(1 for e in prof.events() if "bn_apply" in e.name)
+        out[on] = (float(loss), m.arena.grad.float().cpu().clone(), n_apply)
+    (l1, g1, a1), (l0, g0, a0) = out[True], out[False]
+    assert a1 == a0 - 2, (a1, a0)  # both blocks' bn2 apply sweeps are gone
+    assert abs(l1 - l0) < 1e-4 * max(1.0, abs(l0))
+    assert ((g1 - g0).norm() / g0.norm()).item() < 5e-3
