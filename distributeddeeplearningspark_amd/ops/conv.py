@@ -300,7 +300,7 @@ def conv_dgrad_native(dy, w, g: ConvGeometry, resid=None, resid_mask=None, bnr=N
 def norm_on_load_ok(g: ConvGeometry) -> bool:
     """A pointwise conv can read a pre-BatchNorm input and normalise it on load in BOTH its forward
     (streaming kernel) and its weight gradient (RC x RC GEMM over whole 64-pixel K-tiles)."""
-    return (g.is_pointwise and g.M % 64 == 0 and _os.environ.get("DDL_NORM_ON_LOAD", "1") != "0"
+    return (g.is_pointwise and g.M % 64 == 0
             and G.norm_on_load_fwd_ok(g.M, g.Co, g.Ci, g.Ci, g.Co))
 
 

@@ -223,7 +223,11 @@ import os as _os
 
 _FUSE_BNR = _os.environ.get("DDL_FUSE_BN_REDUCE", "1") != "0"
 _HALF_RES_SC = _os.environ.get("DDL_HALF_RES_SHORTCUT", "1") != "0"
-_NORM_ON_LOAD = _os.environ.get("DDL_NORM_ON_LOAD", "1") != "0"
+# Normalise-on-load is opt-in (DDL_NORM_ON_LOAD=1): it removes bn2's apply sweep (-0.27 ms/step on
+# ResNet-50 b256) but the per-fragment scale/shift/ReLU VALU in the RC x RC weight gradient (+0.22 ms)
+# and the LDS transform pass + narrower panels of the streaming forward (+0.20 ms) cost more
+# (profiles/r3/ab/norm_on_load_kstats_diff.txt: 23.12 vs 22.91 ms/step).
+_NORM_ON_LOAD = _os.environ.get("DDL_NORM_ON_LOAD", "0") == "1"
 
 
 def bottleneck(block, x, anchor):
