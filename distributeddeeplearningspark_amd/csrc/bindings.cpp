@@ -58,7 +58,8 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
           c10::optional<at::Tensor> stats, c10::optional<at::Tensor> aux, double drop_p, int64_t drop_seed,
           c10::optional<at::Tensor> resid_mask, c10::optional<at::Tensor> bnr_x, c10::optional<at::Tensor> bnr_mask,
           c10::optional<at::Tensor> bnr_mean, int64_t rsub_h, int64_t rsub_w, c10::optional<at::Tensor> a_scale,
-          c10::optional<at::Tensor> a_shift, c10::optional<at::Tensor> b_scale, c10::optional<at::Tensor> b_shift) {
+          c10::optional<at::Tensor> a_shift, c10::optional<at::Tensor> b_scale, c10::optional<at::Tensor> b_shift,
+          c10::optional<at::Tensor> bnr_scale, c10::optional<at::Tensor> bnr_shift) {
   CHECK_CUDA(a);
   CHECK_CUDA(b);
   CHECK_CUDA(c);
@@ -188,8 +189,12 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
     p.stats = stats->data_ptr<float>();
   }
   if (bnr_x) {
-    TORCH_CHECK(tile == kTileStream && stats.has_value() && bnr_mean.has_value(),
-                "gemm: the fused BN-backward reduction needs the streaming kernel, a stats workspace and the mean");
+    TORCH_CHECK(stats.has_value() && bnr_mean.has_value() && epi == EPI_BF16 && tile != kTile256,
+                "gemm: the fused BN-backward reduction needs a stats workspace, the mean and a bf16 epilogue");
+    TORCH_CHECK(tile == kTileStream || (N % 4 == 0 && ldc % 8 == 0 && !bias && relu == 0 && !resid && !outmap && !aux &&
+                                        drop_p == 0.0 && (a_mode == OP_KC || (a_mode == OP_KC_GATHER && b_mode == OP_KC))),
+                "gemm: BN-backward reduce outside the streaming kernel: plain or gathered-A data-gradient, N % 4 == 0, "
+                "ldc % 8 == 0, no bias / activation / residual / output map");
     CHECK_CUDA(*bnr_x);
     CHECK_BF16(*bnr_x);
     TORCH_CHECK(bnr_x->is_contiguous() && bnr_x->numel() >= (M - 1) * ldc + N && ((uintptr_t)bnr_x->data_ptr() % 16) == 0,
@@ -203,6 +208,17 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
                       bnr_mask->numel() >= ((M - 1) * ldc + N + 7) / 8,
                   "gemm: bnr_mask must be uint8 [M * ldc / 8]");
       p.bnr_mask = bnr_mask->data_ptr<uint8_t>();
+    }
+    if (bnr_scale || bnr_shift) {  // mode-2 mask (ReLU of the BN output recomputed from x)
+      TORCH_CHECK(bnr_scale && bnr_shift && !bnr_mask && tile != kTileStream,
+                  "gemm: bnr scale/shift (no mask bits; not on the streaming kernel)");
+      CHECK_F32(*bnr_scale);
+      CHECK_F32(*bnr_shift);
+      TORCH_CHECK(bnr_scale->numel() >= N && bnr_shift->numel() >= N && ((uintptr_t)bnr_scale->data_ptr() % 16) == 0 &&
+                      ((uintptr_t)bnr_shift->data_ptr() % 16) == 0,
+                  "gemm: bnr scale / shift [N], 16-B aligned");
+      p.bnr_scale = bnr_scale->data_ptr<float>();
+      p.bnr_shift = bnr_shift->data_ptr<float>();
     }
   }
   auto norm_pair = [&](const c10::optional<at::Tensor>& sc, const c10::optional<at::Tensor>& sh, int64_t n,
@@ -251,7 +267,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("resid_mask") = py::none(), py::arg("bnr_x") = py::none(), py::arg("bnr_mask") = py::none(),
         py::arg("bnr_mean") = py::none(), py::arg("rsub_h") = 0, py::arg("rsub_w") = 0,
         py::arg("a_scale") = py::none(), py::arg("a_shift") = py::none(), py::arg("b_scale") = py::none(),
-        py::arg("b_shift") = py::none());
+        py::arg("b_shift") = py::none(), py::arg("bnr_scale") = py::none(), py::arg("bnr_shift") = py::none());
   m.attr("ACT_NONE") = (int)ACT_NONE;
   m.attr("ACT_RELU") = (int)ACT_RELU;
   m.attr("ACT_GELU") = (int)ACT_GELU;

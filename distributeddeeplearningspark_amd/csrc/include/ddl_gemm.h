@@ -33,6 +33,10 @@ enum EpilogueMode : int {
   // kernel's VGPR allocation (134 -> occupancy 3 blocks/CU for the 128x128 conv kernel); the
   // launcher picks it whenever the call does not use the extra features.
   EPI_BF16_LITE = 3,
+  // bf16 store of alpha*acc plus the fused BatchNorm-backward partial sums of the stored values
+  // (GemmParams::bnr_*) — the LDS-DMA GEMM and halo-conv kernels' form of the streaming kernel's BNR
+  // read-out (selected by the launchers when bnr_x is set on a non-streaming tile)
+  EPI_BF16_BNR = 4,
 };
 
 constexpr int kMaxTaps = 64;
@@ -90,13 +94,17 @@ struct GemmParams {
   float drop_scale;
   unsigned long long drop_seed;
   // fused BatchNorm-backward reduction of the STORED output d (the gradient arriving at a BN whose
-  // input is bnr_x; streaming kernel only): instead of the forward statistics, ``stats`` receives
+  // input is bnr_x): instead of the forward statistics, ``stats`` receives
   //   stats[shard][0][n] += sum_m d(m,n) * relu(m,n),  stats[shard][1][n] += sum_m d * relu * (x(m,n) - mean[n])
-  // with relu(m,n) the bn.hip mode-3 bit of bnr_mask (all ones when null) — the partial sums of
-  // bn_bwd_reduce, so that sweep (a full read of d and x) is skipped for that BN.
+  // with relu(m,n) the bn.hip mode-3 bit of bnr_mask, or (mode 2) x(m,n) * bnr_scale[n] + bnr_shift[n] > 0,
+  // or all ones when neither is given — the partial sums of bn_bwd_reduce, so that sweep (a full read of
+  // d and x) is skipped for that BN.  Streaming kernel: mask bits only; LDS-DMA GEMM / halo conv:
+  // EPI_BF16_BNR, either mask form.
   const void* bnr_x;        // bf16 [M][ldc]
   const uint8_t* bnr_mask;  // bit (m*ldc + n) of the ReLU mask, or null
   const float* bnr_mean;    // [N] batch mean of bnr_x
+  const float* bnr_scale;   // [N] BN scale / shift of the forward (mode-2 mask), or null
+  const float* bnr_shift;
   // stride-2 residual: when rsub_h > 0 the output rows m = (n, i, j) form an [N][rsub_h][rsub_w] grid
   // and ``resid`` lives on its stride-2 subgrid ([N][(rsub_h+1)/2][(rsub_w+1)/2], row stride ldr):
   // rows with even (i, j) add resid row ((n * Hs + i/2) * Ws + j/2), the others add nothing — the

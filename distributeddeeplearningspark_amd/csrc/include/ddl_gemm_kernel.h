@@ -348,6 +348,77 @@ struct Operand {
   }
 };
 
+// bf16-output epilogues take D^T fragments (a lane owns 4 consecutive columns of one row)
+constexpr bool epi_dt(int epi) { return epi == EPI_BF16 || epi == EPI_BF16_LITE || epi == EPI_BF16_BNR; }
+
+// EPI_BF16_BNR: bf16 store of alpha*acc + the BatchNorm-backward partial sums of the stored gradient
+// (GemmParams::bnr_*), accumulated like the forward statistics (16-lane shuffle, one atomic per
+// column and shard).  Column-outer so that only one column group's mean / scale / shift is live.
+template <int RM, int RN>
+__device__ __forceinline__ void gemm_epilogue_bnr(const GemmParams& p, f32x4 (&acc)[RM][RN], const int mb,
+                                                  const int nb, const int lane, const int bid, const int mlim) {
+  const int mrow = lane & 15;
+  const int ncol = 4 * (lane >> 4);
+  const bf16_t* X = reinterpret_cast<const bf16_t*>(p.bnr_x);
+  float* st = p.stats + (long)(bid % kStatShards) * 2 * p.N;
+#pragma unroll
+  for (int j = 0; j < RN; ++j) {
+    const int n = nb + 16 * j + ncol;  // host check: N % 4 == 0, so n < N covers n .. n+3
+    const bool nok = n < p.N;
+    float mu[4] = {0.f, 0.f, 0.f, 0.f}, sc[4] = {0.f, 0.f, 0.f, 0.f}, sh[4] = {0.f, 0.f, 0.f, 0.f};
+    if (nok) {
+      const float4 a = *reinterpret_cast<const float4*>(p.bnr_mean + n);
+      mu[0] = a.x; mu[1] = a.y; mu[2] = a.z; mu[3] = a.w;
+      if (p.bnr_scale) {
+        const float4 b = *reinterpret_cast<const float4*>(p.bnr_scale + n);
+        const float4 c = *reinterpret_cast<const float4*>(p.bnr_shift + n);
+        sc[0] = b.x; sc[1] = b.y; sc[2] = b.z; sc[3] = b.w;
+        sh[0] = c.x; sh[1] = c.y; sh[2] = c.z; sh[3] = c.w;
+      }
+    }
+    float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {
+      const int m = mb + 16 * i + mrow;
+      if (!nok || m >= mlim) continue;
+      const long off = (long)m * p.ldc + n;
+      const uint2 xv = *reinterpret_cast<const uint2*>(X + off);
+      uint32_t mbits = 0xfu;
+      if (p.bnr_mask) mbits = (uint32_t)p.bnr_mask[off >> 3] >> (off & 7);
+      float x[4];
+      x[0] = __uint_as_float(xv.x << 16);
+      x[1] = __uint_as_float(xv.x & 0xffff0000u);
+      x[2] = __uint_as_float(xv.y << 16);
+      x[3] = __uint_as_float(xv.y & 0xffff0000u);
+      bf16_t o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[e] = f2bf(acc[i][j][e] * p.alpha);
+        bool keep = (mbits >> e) & 1u;
+        if (p.bnr_scale) keep = (x[e] * sc[e] + sh[e]) > 0.f;
+        const float d = keep ? bf2f(o[e]) : 0.f;
+        s1[e] += d;
+        s2[e] += d * (x[e] - mu[e]);
+      }
+      *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.c) + off) =
+          make_uint2((uint32_t)o[0] | ((uint32_t)o[1] << 16), (uint32_t)o[2] | ((uint32_t)o[3] << 16));
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float a = s1[e], b = s2[e];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        a += __shfl_xor(a, o, 64);
+        b += __shfl_xor(b, o, 64);
+      }
+      if (mrow == 0 && nok) {
+        atomicAdd(st + n + e, a);
+        atomicAdd(st + p.N + n + e, b);
+      }
+    }
+  }
+}
+
 // normalise-on-load of a fragment whose 8 values share one channel (row-contiguous B operand)
 __device__ __forceinline__ bf16x8 norm_frag(const bf16x8 f, float sc, float sh) {
   const s16x8 v = __builtin_bit_cast(s16x8, f);
@@ -371,6 +442,10 @@ template <int RM, int RN, int EPI>
 __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[RM][RN], const int mb, const int nb,
                                               const int lane, const int bid, int mend = -1) {
   const int mlim = mend < 0 ? p.M : mend;
+  if constexpr (EPI == EPI_BF16_BNR) {
+    gemm_epilogue_bnr<RM, RN>(p, acc, mb, nb, lane, bid, mlim);
+    return;
+  }
   // ---------------------------------- epilogue ----------------------------------
   constexpr bool BF = EPI == EPI_BF16 || EPI == EPI_BF16_LITE;
   constexpr bool LITE = EPI == EPI_BF16_LITE;
@@ -668,7 +743,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams
       for (int i = 0; i < RM; ++i)
 #pragma unroll
         for (int j = 0; j < RN; ++j) {
-          if constexpr (EPI == EPI_BF16 || EPI == EPI_BF16_LITE)
+          if constexpr (epi_dt(EPI))
             acc[i][j] = mfma16x16x32(bf[j], af[i], acc[i][j]);  // D^T: 4 consecutive n per lane (vector stores)
           else
             acc[i][j] = mfma16x16x32(af[i], bf[j], acc[i][j]);  // D: 16 consecutive n per row (coalesced atomics)
@@ -787,7 +862,7 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
         for (int i = 0; i < RM; ++i)
 #pragma unroll
           for (int j = 0; j < RN; ++j) {
-            if constexpr (EPI == EPI_BF16 || EPI == EPI_BF16_LITE)
+            if constexpr (epi_dt(EPI))
               acc[i][j] = mfma16x16x32(bf[j], af[i], acc[i][j]);
             else
               acc[i][j] = mfma16x16x32(af[i], bf[j], acc[i][j]);
@@ -829,7 +904,7 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
       for (int i = 0; i < RM; ++i)
 #pragma unroll
         for (int j = 0; j < RN; ++j) {
-          if constexpr (EPI == EPI_BF16 || EPI == EPI_BF16_LITE)
+          if constexpr (epi_dt(EPI))
             acc[i][j] = mfma16x16x32(bf[j], af[i], acc[i][j]);
           else
             acc[i][j] = mfma16x16x32(af[i], bf[j], acc[i][j]);

@@ -47,7 +47,7 @@ struct Conv3Tiling {
 // FR * 16): 8 covers a full 256-pixel tile; 7 serves the 196-pixel tiles every ResNet-50 stage
 // plans (7 rows of 28, one 14x14 image, four 7x7 images) — with 8 the second pixel wave spent 3 of
 // its 8 fragments on rows past the tile, so every tap paid 16 MFMA blocks for 12.25 of work.
-template <int BN, int EPI, int NB, int FR = 8>
+template <int BN, int EPI, int NB, int FR = 8, bool PRIO = false>
 __global__ __launch_bounds__(NTHREADS, 2) void conv3x3_halo_kernel(const GemmParams p, const Conv3Tiling t) {
   constexpr int RN = BN / 32;  // channel fragments per wave (2 waves along N)
   constexpr int B_BYTES = BN * BK * 2;
@@ -154,10 +154,12 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv3x3_halo_kernel(const GemmPar
         const int ch = kk * 4 + (lane >> 4);
         af[i] = *reinterpret_cast<const bf16x8*>(halo + row * 128 + ((ch ^ (row & 6)) << 4));
       }
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < FR; ++i)
 #pragma unroll
         for (int j = 0; j < RN; ++j) acc[i][j] = mfma16x16x32(bfr[j], af[i], acc[i][j]);  // D^T (bf16 epilogue)
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     }
     if (NB == 2 || tap == 8) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -193,18 +195,30 @@ Conv3Tiling plan(const GemmParams& p) {
   return t;
 }
 
-template <int BN, int EPI, int NB, int FR>
-int launch_fr(const GemmParams& p, const Conv3Tiling& t, hipStream_t s) {
+template <int BN, int EPI, int NB, int FR, bool PRIO>
+int launch_fr_p(const GemmParams& p, const Conv3Tiling& t, hipStream_t s) {
   const int blocks = t.tiles_img * t.tiles_row * ((p.N + BN - 1) / BN);
   const size_t lds = (size_t)t.hr_pad * 128 + NB * BN * BK * 2;
-  static bool attr = [] {  // dynamic LDS above 64 KB must be allowed explicitly (at most 80 KB here)
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_halo_kernel<BN, EPI, NB, FR>),
+  static bool attr = [] {  // dynamic LDS above 64 KB must be allowed explicitly (at most 96 KB here)
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_halo_kernel<BN, EPI, NB, FR, PRIO>),
                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                C3_MAX_HALO_ROWS * 128 + NB * BN * BK * 2) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL((conv3x3_halo_kernel<BN, EPI, NB, FR>), dim3(blocks), dim3(NTHREADS), lds, s, p, t);
+  hipLaunchKernelGGL((conv3x3_halo_kernel<BN, EPI, NB, FR, PRIO>), dim3(blocks), dim3(NTHREADS), lds, s, p, t);
   return (int)hipGetLastError();
+}
+
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e && e[0] ? atoi(e) : dflt;
+}
+
+// DDL_CONV3X3_PRIO=1: raise the wave priority over the MFMA block (experiment knob)
+template <int BN, int EPI, int NB, int FR>
+int launch_fr(const GemmParams& p, const Conv3Tiling& t, hipStream_t s) {
+  static const bool prio = env_int("DDL_CONV3X3_PRIO", 0) == 1;
+  return prio ? launch_fr_p<BN, EPI, NB, FR, true>(p, t, s) : launch_fr_p<BN, EPI, NB, FR, false>(p, t, s);
 }
 
 // fragments per pixel wave: the fewest that cover half the tile (7 for the 196-pixel ResNet tiles)
@@ -246,7 +260,9 @@ int launch_conv3x3(const GemmParams& p, int epi, hipStream_t s) {
     return e ? atoi(e) : 0;
   }();
   const bool bn128 = p.N % 128 == 0 && (force_bn ? force_bn == 128 : (long)tiles_px * (p.N / 128) >= 2L * 256);
-  if (bn128) return launch<128, EPI_BF16_LITE, 2>(p, t, s);
+  static const int nb128 = env_int("DDL_CONV3X3_NB", 2);  // 3: third weight slot (1 workgroup per CU)
+  if (p.bnr_x) return bn128 ? launch<128, EPI_BF16_BNR, 2>(p, t, s) : launch<64, EPI_BF16_BNR, 3>(p, t, s);
+  if (bn128) return nb128 == 3 ? launch<128, EPI_BF16_LITE, 3>(p, t, s) : launch<128, EPI_BF16_LITE, 2>(p, t, s);
   return launch<64, EPI_BF16_LITE, 3>(p, t, s);
 }
 

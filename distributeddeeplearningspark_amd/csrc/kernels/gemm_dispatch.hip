@@ -12,7 +12,11 @@ int launch_conv3x3(const GemmParams& p, int epi, hipStream_t s);
 int launch_gemm_bf16(const GemmParams& p, int epi, int tile, void* stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (p.M <= 0 || p.N <= 0) return 0;
-  if (p.bnr_x && tile != kTileStream) return (int)hipErrorInvalidValue;  // fused BN-backward reduce: streaming kernel only
+  if (p.bnr_x && tile != kTileStream &&  // fused BN-backward reduce on the other kernels: EPI_BF16_BNR
+      (tile == kTile256 || epi != EPI_BF16 || p.om.enabled || p.resid || p.aux || p.drop_thresh || p.bias || p.relu || p.N % 4 || p.ldc % 8 ||
+       !(p.a_mode == OP_KC || p.a_mode == OP_KC_GATHER) || (p.a_mode == OP_KC_GATHER && p.b_mode != OP_KC)))
+    return (int)hipErrorInvalidValue;
+  if (p.bnr_scale && tile == kTileStream) return (int)hipErrorInvalidValue;  // streaming kernel: mask bits only
   if (p.a_scale && tile != kTileStream) return (int)hipErrorInvalidValue;  // normalise-on-load of A: streaming kernel
   if (p.b_scale && !(p.a_mode == OP_RC && p.b_mode == OP_RC && (epi == EPI_F32 || epi == EPI_F32_ATOMIC) &&
                      tile <= 3 && p.K % 64 == 0 && p.k_split % 64 == 0))

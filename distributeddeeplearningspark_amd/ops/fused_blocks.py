@@ -182,9 +182,16 @@ class _BottleneckFn(torch.autograd.Function):
         # backward writing it out, conv1's data-gradient epilogue adds dout under the bit mask
         masked_sc = s_down is None and s3.mode == 3 and s1.g.is_pointwise
         d3c, dsc = bn_backward(b.c3, s3, dout, want_dres=not masked_sc)
-        d2 = conv_backward(b.c3, s3, d3c, s2.yc if s2.y is None else s2.y, True, x_norm=_norm_of(s2))
+        # the data-gradients of conv3 and conv2 produce bn2's / bn1's output gradients: their epilogues also
+        # accumulate those BNs' backward partial sums (ReLU mask recomputed from yc), so bn_backward skips the
+        # reduce sweep wherever the kernel that ran could take it (bnr["done"])
+        bnr2 = _bnr_mode2(s2, dout.device)
+        d2 = conv_backward(b.c3, s3, d3c, s2.yc if s2.y is None else s2.y, True, x_norm=_norm_of(s2), bnr=bnr2)
+        _take_reduced(s2, bnr2)
         d2c, _ = bn_backward(b.c2, s2, d2, False)
-        d1 = conv_backward(b.c2, s2, d2c, s1.y, True)
+        bnr1 = _bnr_mode2(s1, dout.device)
+        d1 = conv_backward(b.c2, s2, d2c, s1.y, True, bnr=bnr1)
+        _take_reduced(s1, bnr1)
         d1c, _ = bn_backward(b.c1, s1, d1, False)
         rsub = None
         if s_down is not None:
@@ -222,12 +229,27 @@ class _BottleneckFn(torch.autograd.Function):
 import os as _os
 
 _FUSE_BNR = _os.environ.get("DDL_FUSE_BN_REDUCE", "1") != "0"
+# bn1 / bn2 of every bottleneck: reduce fused into the conv2 / conv3 data-gradient epilogues
+_FUSE_BNR_INNER = _os.environ.get("DDL_FUSE_BN_REDUCE_INNER", "1") != "0"
 _HALF_RES_SC = _os.environ.get("DDL_HALF_RES_SHORTCUT", "1") != "0"
 # Normalise-on-load is opt-in (DDL_NORM_ON_LOAD=1): it removes bn2's apply sweep (-0.27 ms/step on
 # ResNet-50 b256) but the per-fragment scale/shift/ReLU VALU in the RC x RC weight gradient (+0.22 ms)
 # and the LDS transform pass + narrower panels of the streaming forward (+0.20 ms) cost more
 # (profiles/r3/ab/norm_on_load_kstats_diff.txt: 23.12 vs 22.91 ms/step).
 _NORM_ON_LOAD = _os.environ.get("DDL_NORM_ON_LOAD", "0") == "1"
+
+
+def _bnr_mode2(st, device):
+    """BN-backward reduce request for a ReLU BN without residual (mode 2) — see ``gemm.linear_dgrad``."""
+    if not _FUSE_BNR_INNER or st.mode != 2:
+        return None
+    return {"x": st.yc, "scale": st.scale, "shift": st.shift, "mean": st.mean,
+            "ws": new_stats_workspace(st.yc.shape[-1], device)}
+
+
+def _take_reduced(st, bnr):
+    if bnr is not None and bnr.get("done"):
+        st.pre_reduced = bnr["ws"]
 
 
 def bottleneck(block, x, anchor):

@@ -123,7 +123,7 @@ def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, bet
         if use_stream(M, N, K, a_mode, b_mode, epi, lda, ldc, outmap=outmap, aux=aux, drop_p=drop_p, relu=relu,
                       beta=beta, resid=resid, ldr=ldr):
             tile = TILE_STREAM
-        elif outmap is None and use_tile256(M, N, K, a_mode, b_mode, epi):
+        elif outmap is None and bnr is None and use_tile256(M, N, K, a_mode, b_mode, epi):
             tile = TILE256
         else:
             tile = choose_tile(M, N, bn_cap)
@@ -133,15 +133,16 @@ def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, bet
         if beta not in (0.0, 1.0):
             raise ValueError("split-K fp32 gemm supports beta in {0,1} (beta=0 needs a zeroed C)")
         epi = EPI_F32_ATOMIC
-    if bnr is not None:  # fused BN-backward reduce of the output (streaming kernel only; see linear_dgrad)
-        if tile != TILE_STREAM:
-            raise ValueError("bnr: the fused BN-backward reduction runs on the streaming kernel only")
+    if bnr is not None:  # fused BN-backward reduce of the output (see linear_dgrad / GemmParams.bnr_*)
+        if tile == TILE256:
+            raise ValueError("bnr: not on the 256x256 kernel")
         stats = bnr["ws"]
     C().gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, tile, k_split, alpha, beta, bias, resid, ldr,
              int(relu), geom, outmap, b_kdiv, b_tap_stride, stats, aux, float(drop_p), int(drop_seed), resid_mask,
              None if bnr is None else bnr["x"], None if bnr is None else bnr.get("mask"),
              None if bnr is None else bnr["mean"], *(rsub or (0, 0)), *(a_norm or (None, None)),
-             *(b_norm or (None, None)))
+             *(b_norm or (None, None)), None if bnr is None else bnr.get("scale"),
+             None if bnr is None else bnr.get("shift"))
     return c
 
 
@@ -194,10 +195,12 @@ def linear_dgrad(dy, w, out=None, resid=None, gelu_pre=None, stats=None, resid_m
 
     ``stats`` ([32, 2, K] fp32, zeroed): per-column sums / sums of squares of the output;
     ``resid_mask``: uint8 ReLU bit mask of ``resid`` (bn.hip mode-3 layout) — only the masked
-    residual is added; ``bnr`` = {"x", "mask", "mean", "ws"}: when this GEMM runs on the streaming
-    kernel, its epilogue also accumulates the BatchNorm-backward partial sums of the output
-    (``GemmParams.bnr_*``) into ``ws`` and ``bnr["done"]`` is set — the consumer BN then skips its
-    reduce sweep; otherwise ``bnr`` is left untouched.  ``rsub = (H, W)``: the rows are an
+    residual is added; ``bnr`` = {"x", "mask", "mean", "ws"} (mode-3 bit mask) or {"x", "scale",
+    "shift", "mean", "ws"} (mode 2: ReLU recomputed from x): the GEMM's epilogue also accumulates the
+    BatchNorm-backward partial sums of the output (``GemmParams.bnr_*``) into ``ws`` and
+    ``bnr["done"]`` is set — the consumer BN then skips its reduce sweep.  Where no kernel can
+    (a residual on a non-streaming tile, mode 2 on the streaming kernel, split-K) ``bnr`` is left
+    untouched.  ``rsub = (H, W)``: the rows are an
     [N][H][W] grid and ``resid`` lives on its stride-2 subgrid (``GemmParams.rsub_h``)."""
     M, N = dy.shape
     K = w.shape[1]
@@ -222,16 +225,32 @@ def linear_dgrad(dy, w, out=None, resid=None, gelu_pre=None, stats=None, resid_m
         # transpose the (small) weight once so the GEMM reads B K-contiguous with ds_read_b128 instead
         # of paired transposed LDS reads: the BERT-size data-gradients run ~1.4x faster this way
         wt = transpose(w)
-        return gemm(dy, wt, out, M, K, N, KC, KC, dy.stride(0), wt.stride(0), out.stride(0), EPI_BF16, resid=resid,
-                    ldr=ldr, relu=act, aux=gelu_pre, stats=stats, resid_mask=resid_mask, rsub=rsub)
-    if bnr is not None and stats is None and use_stream(M, K, N, KC, RC, EPI_BF16, dy.stride(0), out.stride(0),
-                                                        aux=gelu_pre, relu=act, resid=resid, ldr=ldr):
+        fb = _bnr_plain_ok(bnr, stats, resid, gelu_pre, K)
+        gemm(dy, wt, out, M, K, N, KC, KC, dy.stride(0), wt.stride(0), out.stride(0), EPI_BF16, resid=resid,
+             ldr=ldr, relu=act, aux=gelu_pre, stats=stats, resid_mask=resid_mask, rsub=rsub, bnr=bnr if fb else None)
+        if fb:
+            bnr["done"] = True
+        return out
+    if (bnr is not None and stats is None and "scale" not in bnr
+            and use_stream(M, K, N, KC, RC, EPI_BF16, dy.stride(0), out.stride(0), aux=gelu_pre, relu=act,
+                           resid=resid, ldr=ldr)):
         gemm(dy, w, out, M, K, N, KC, RC, dy.stride(0), w.stride(0), out.stride(0), EPI_BF16, resid=resid, ldr=ldr,
              relu=act, aux=gelu_pre, resid_mask=resid_mask, tile=TILE_STREAM, bnr=bnr, rsub=rsub)
         bnr["done"] = True
         return out
-    return gemm(dy, w, out, M, K, N, KC, RC, dy.stride(0), w.stride(0), out.stride(0), EPI_BF16, resid=resid,
-                ldr=ldr, relu=act, aux=gelu_pre, stats=stats, resid_mask=resid_mask, rsub=rsub)
+    fb = _bnr_plain_ok(bnr, stats, resid, gelu_pre, K) and not use_stream(
+        M, K, N, KC, RC, EPI_BF16, dy.stride(0), out.stride(0), aux=gelu_pre, relu=act, resid=resid, ldr=ldr)
+    gemm(dy, w, out, M, K, N, KC, RC, dy.stride(0), w.stride(0), out.stride(0), EPI_BF16, resid=resid,
+         ldr=ldr, relu=act, aux=gelu_pre, stats=stats, resid_mask=resid_mask, rsub=rsub, bnr=bnr if fb else None)
+    if fb:
+        bnr["done"] = True
+    return out
+
+
+def _bnr_plain_ok(bnr, stats, resid, gelu_pre, ncols) -> bool:
+    """The LDS-DMA GEMM's EPI_BF16_BNR epilogue can take this data-gradient's BN-backward reduce."""
+    return (bnr is not None and stats is None and resid is None and gelu_pre is None and ncols % 8 == 0
+            and bnr["x"].is_contiguous())
 
 
 def transpose(w):

@@ -642,6 +642,107 @@ def test_stream_dgrad_fused_bn_backward_reduce(M, N, K, resid):
     close(got[1], s2, rtol=1e-4, atol=1e-2 * s2.abs().mean().item(), what="sum d (x - mean)")
 
 
+def _bnr_reference(out, x, mean, keep):
+    d = out.double().cpu().reshape(-1, out.shape[-1]) * keep.double()
+    return d.sum(0), (d * (x.double().cpu().reshape(d.shape) - mean.double().cpu())).sum(0)
+
+
+@pytest.mark.parametrize("M,N,K,mode", [(8192, 512, 128, 2), (8192, 512, 128, 3), (2048, 256, 192, 2)])
+def test_dma_dgrad_fused_bn_backward_reduce(M, N, K, mode):
+    """linear_dgrad on the LDS-DMA GEMM (transposed-weight KC x KC path for M >= 4096, KC x RC below)
+    with ``bnr``: EPI_BF16_BNR stores the same output as the plain launch and accumulates the BN-backward
+    partial sums with the mode-2 (x * scale + shift > 0) or mode-3 (bit) ReLU mask."""
+    from distributeddeeplearningspark_amd.ops import gemm as G
+    from distributeddeeplearningspark_amd.ops.norm import SHARDS
+
+    gen = torch.Generator().manual_seed(M + N + mode)
+    dy = torch.randn(M, N, generator=gen).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, K, generator=gen) / N ** 0.5).to(DEV, torch.bfloat16)
+    x = torch.randn(M, K, generator=gen).to(DEV, torch.bfloat16)
+    mean = torch.randn(K, generator=gen).to(DEV)
+    ws = torch.zeros((SHARDS, 2, K), dtype=torch.float32, device=DEV)
+    bnr = {"x": x, "mean": mean, "ws": ws}
+    if mode == 2:
+        scale = (torch.rand(K, generator=gen) + 0.5).to(DEV)
+        shift = torch.randn(K, generator=gen).to(DEV) * 0.5
+        bnr.update(scale=scale, shift=shift)
+        keep = (x.float() * scale + shift > 0).cpu()
+    else:
+        keep = torch.rand(M, K, generator=gen) > 0.4
+        bnr["mask"] = (keep.reshape(-1, 8).to(torch.uint8) << torch.arange(8, dtype=torch.uint8)).sum(
+            1, dtype=torch.uint8).to(DEV)
+    assert not G.use_stream(M, K, N, G.KC, G.RC, G.EPI_BF16, N, K)
+    out = G.linear_dgrad(dy, w, bnr=bnr)
+    assert bnr.get("done")
+    assert torch.equal(out, G.linear_dgrad(dy, w))
+    s1, s2 = _bnr_reference(out, x, mean, keep)
+    got = ws.double().cpu().sum(0)
+    close(got[0], s1, rtol=1e-4, atol=1e-2 * s1.abs().mean().item(), what="sum d")
+    close(got[1], s2, rtol=1e-4, atol=1e-2 * s2.abs().mean().item(), what="sum d (x - mean)")
+
+
+@pytest.mark.parametrize("N,H,C", [(96, 14, 128), (160, 16, 64)])
+def test_conv_dgrad_fused_bn_backward_reduce(monkeypatch, N, H, C):
+    """A stride-1 3x3 data-gradient run as a forward conv (halo kernel at 128 channels, the gathered
+    implicit GEMM at 64) with a mode-2 ``bnr``: same dx as without, and the BN-backward partial sums."""
+    from distributeddeeplearningspark_amd.ops import conv as CV
+    from distributeddeeplearningspark_amd.ops.norm import SHARDS
+
+    g = CV.geometry(N, H, H, C, C, 3, 3, (1, 1), (1, 1), (1, 1))
+    assert CV.halo3_ok(g) == (C >= 128) and not CV.splitk_fwd_ok(g)  # (small grids take the split-K path)
+    gen = torch.Generator().manual_seed(H * C)
+    dy = torch.randn(N, H, H, C, generator=gen).to(DEV, torch.bfloat16)
+    w = (torch.randn(C, 3, 3, C, generator=gen) * 0.05).to(DEV, torch.bfloat16)
+    x = torch.randn(N, H, H, C, generator=gen).to(DEV, torch.bfloat16)
+    mean = torch.randn(C, generator=gen).to(DEV) * 0.1
+    scale = (torch.rand(C, generator=gen) + 0.5).to(DEV)
+    shift = torch.randn(C, generator=gen).to(DEV) * 0.5
+    ws = torch.zeros((SHARDS, 2, C), dtype=torch.float32, device=DEV)
+    bnr = {"x": x, "scale": scale, "shift": shift, "mean": mean, "ws": ws}
+    dx = CV.conv_dgrad_native(dy, w, g, bnr=bnr)
+    assert bnr.get("done")
+    assert torch.equal(dx, CV.conv_dgrad_native(dy, w, g))
+    keep = (x.float() * scale + shift > 0).cpu().reshape(-1, C)
+    s1, s2 = _bnr_reference(dx, x, mean, keep)
+    got = ws.double().cpu().sum(0)
+    close(got[0], s1, rtol=1e-4, atol=1e-2 * s1.abs().mean().item(), what="sum d")
+    close(got[1], s2, rtol=1e-4, atol=1e-2 * s2.abs().mean().item(), what="sum d (x - mean)")
+
+
+def test_bottleneck_inner_fused_bn_reduce_matches_unfused(monkeypatch):
+    """bn1 / bn2 backward reduces fused into the conv2 / conv3 data-gradient epilogues (stage 1: the 64-channel
+    gathered conv2 dgrad; stage 2: the transposed-weight conv3 dgrad): fewer reduce sweeps, same gradients.
+    (At this batch the stage-1 conv2 dgrads take the split-K path and stage 1's conv3 dgrads the streaming
+    kernel, neither of which fuses a mode-2 reduce: the two stage-2 conv3 dgrads do.)"""
+    from distributeddeeplearningspark_amd.models.resnet import ResNet
+    from distributeddeeplearningspark_amd.ops import fused_blocks as FB
+
+    torch.manual_seed(4)
+    x = torch.randn(64, 64, 64, 3)
+    y = torch.randint(0, 10, (64,))
+    out = {}
+    for fuse in (True, False):
+        monkeypatch.setattr(FB, "_FUSE_BNR_INNER", fuse)
+        m = ResNet(blocks=(2, 2), input_shape=(64, 64, 3), num_classes=10)
+        m.compile("sgd", "sparse_categorical_crossentropy")
+        m.place(DEV, seed=5)
+        xd, yd = m.to_input(x), m.to_target(y)
+        m.backward_step(xd, yd)
+        from torch.profiler import ProfilerActivity, profile
+
+        torch.cuda.synchronize()
+        with profile(activities=[ProfilerActivity.CUDA]) as prof:
+            loss = m.backward_step(xd, yd)
+            torch.cuda.synchronize()
+        n_reduce = sum(1 for e in prof.events() if "bn_bwd_reduce" in e.name)
+        out[fuse] = (float(loss), m.arena.grad.float().cpu().clone(), n_reduce)
+    (l1, g1, r1), (l0, g0, r0) = out[True], out[False]
+    assert r1 <= r0 - 2, (r1, r0)
+    assert abs(l1 - l0) < 1e-4 * max(1.0, abs(l0))
+    rel = ((g1 - g0).norm() / g0.norm()).item()
+    assert rel < 5e-3, rel
+
+
 def test_bottleneck_chain_fused_bn_reduce_matches_unfused(monkeypatch):
     """Two identity-chained bottlenecks at stage-1 shapes (M = 64 x 16 x 16 = 16384 rows: the second
     block's conv1 data-gradient runs on the streaming kernel and accumulates the first block's bn3
