@@ -713,15 +713,18 @@ def test_bottleneck_inner_fused_bn_reduce_matches_unfused(monkeypatch):
     """bn1 / bn2 backward reduces fused into the conv2 / conv3 data-gradient epilogues (stage 1: the 64-channel
     gathered conv2 dgrad; stage 2: the transposed-weight conv3 dgrad): fewer reduce sweeps, same gradients.
     (At this batch the stage-1 conv2 dgrads take the split-K path and stage 1's conv3 dgrads the streaming
-    kernel, neither of which fuses a mode-2 reduce: the two stage-2 conv3 dgrads do.)"""
+    kernel, neither of which fuses a mode-2 reduce: the two stage-2 conv3 dgrads do.)  Gradients are held
+    to the unfused path's own run-to-run spread (tests/noise.py: BN-statistics atomics + bf16 rounding)."""
+    from noise import assert_scalar_within_noise, assert_within_noise
+
     from distributeddeeplearningspark_amd.models.resnet import ResNet
     from distributeddeeplearningspark_amd.ops import fused_blocks as FB
 
     torch.manual_seed(4)
     x = torch.randn(64, 64, 64, 3)
     y = torch.randint(0, 10, (64,))
-    out = {}
-    for fuse in (True, False):
+    out = []
+    for fuse in (False, True, False):
         monkeypatch.setattr(FB, "_FUSE_BNR_INNER", fuse)
         m = ResNet(blocks=(2, 2), input_shape=(64, 64, 3), num_classes=10)
         m.compile("sgd", "sparse_categorical_crossentropy")
@@ -735,26 +738,28 @@ def test_bottleneck_inner_fused_bn_reduce_matches_unfused(monkeypatch):
             loss = m.backward_step(xd, yd)
             torch.cuda.synchronize()
         n_reduce = sum(1 for e in prof.events() if "bn_bwd_reduce" in e.name)
-        out[fuse] = (float(loss), m.arena.grad.float().cpu().clone(), n_reduce)
-    (l1, g1, r1), (l0, g0, r0) = out[True], out[False]
+        out.append((float(loss.detach()), m.arena.grad.float().cpu().clone(), n_reduce))
+    (l0, g0, r0), (l1, g1, r1), (l0b, g0b, _) = out
     assert r1 <= r0 - 2, (r1, r0)
-    assert abs(l1 - l0) < 1e-4 * max(1.0, abs(l0))
-    rel = ((g1 - g0).norm() / g0.norm()).item()
-    assert rel < 5e-3, rel
+    assert_scalar_within_noise(l1, l0, l0b, floor=2e-5)
+    assert_within_noise(g1, g0, g0b, floor=2e-3, what="arena gradients")
 
 
 def test_bottleneck_chain_fused_bn_reduce_matches_unfused(monkeypatch):
     """Two identity-chained bottlenecks at stage-1 shapes (M = 64 x 16 x 16 = 16384 rows: the second
     block's conv1 data-gradient runs on the streaming kernel and accumulates the first block's bn3
-    backward sums, whose reduce sweep is then skipped): every gradient equals the unfused run."""
+    backward sums, whose reduce sweep is then skipped): gradients equal the unfused run's up to that
+    run's own spread (tests/noise.py)."""
+    from noise import assert_scalar_within_noise, assert_within_noise
+
     from distributeddeeplearningspark_amd.models.resnet import ResNet
     from distributeddeeplearningspark_amd.ops import fused_blocks as FB
 
     torch.manual_seed(2)
     x = torch.randn(64, 64, 64, 3)
     y = torch.randint(0, 10, (64,))
-    out = {}
-    for fuse in (True, False):
+    out = []
+    for fuse in (False, True, False):
         monkeypatch.setattr(FB, "_FUSE_BNR", fuse)
         m = ResNet(blocks=(2,), input_shape=(64, 64, 3), num_classes=10)
         m.compile("sgd", "sparse_categorical_crossentropy")
@@ -768,13 +773,11 @@ def test_bottleneck_chain_fused_bn_reduce_matches_unfused(monkeypatch):
             loss = m.backward_step(xd, yd)
             torch.cuda.synchronize()
         n_reduce = sum(1 for e in prof.events() if "bn_bwd_reduce" in e.name)
-        out[fuse] = (float(loss), m.arena.grad.float().cpu().clone(), n_reduce)
-    (l1, g1, r1), (l0, g0, r0) = out[True], out[False]
+        out.append((float(loss.detach()), m.arena.grad.float().cpu().clone(), n_reduce))
+    (l0, g0, r0), (l1, g1, r1), (l0b, g0b, _) = out
     assert r1 == r0 - 1, (r1, r0)  # block 1's bn3 reduce sweep was absorbed by block 2's conv1 dgrad
-    # (the forward itself carries atomic-order noise in the BN statistics: ~1e-5 of the loss run to run)
-    assert abs(l1 - l0) < 1e-4 * max(1.0, abs(l0))
-    rel = ((g1 - g0).norm() / g0.norm()).item()
-    assert rel < 5e-3, rel
+    assert_scalar_within_noise(l1, l0, l0b, floor=2e-5)
+    assert_within_noise(g1, g0, g0b, floor=2e-3, what="arena gradients")
 
 
 def test_stem_pool_fusion_matches_separate_apply_and_pool(monkeypatch):
@@ -850,15 +853,18 @@ def test_normalise_on_load_fwd_and_wgrad(M, K, N):
 
 def test_bottleneck_norm_on_load_matches_applied(monkeypatch):
     """Stage-1 bottlenecks (M = 64 x 16 x 16 rows): conv3 reading bn2's pre-BN tensor with the apply
-    folded into its loads gives the same loss, gradients and running statistics as the applied path."""
+    folded into its loads gives the same loss and gradients as the applied path, up to the applied
+    path's own run-to-run spread (tests/noise.py; the fused path also skips one bf16 rounding)."""
+    from noise import assert_scalar_within_noise, assert_within_noise
+
     from distributeddeeplearningspark_amd.models.resnet import ResNet
     from distributeddeeplearningspark_amd.ops import fused_blocks as FB
 
     torch.manual_seed(6)
     x = torch.randn(64, 64, 64, 3)
     y = torch.randint(0, 10, (64,))
-    out = {}
-    for on in (True, False):
+    out = []
+    for on in (False, True, False):
         monkeypatch.setattr(FB, "_NORM_ON_LOAD", on)
         m = ResNet(blocks=(2,), input_shape=(64, 64, 3), num_classes=10)
         m.compile("sgd", "sparse_categorical_crossentropy")
@@ -871,8 +877,8 @@ def test_bottleneck_norm_on_load_matches_applied(monkeypatch):
             loss = m.backward_step(xd, yd)
             torch.cuda.synchronize()
         n_apply = sum(1 for e in prof.events() if "bn_apply" in e.name)
-        out[on] = (float(loss), m.arena.grad.float().cpu().clone(), n_apply)
-    (l1, g1, a1), (l0, g0, a0) = out[True], out[False]
+        out.append((float(loss.detach()), m.arena.grad.float().cpu().clone(), n_apply))
+    (l0, g0, a0), (l1, g1, a1), (l0b, g0b, _) = out
     assert a1 == a0 - 2, (a1, a0)  # both blocks' bn2 apply sweeps are gone
-    assert abs(l1 - l0) < 1e-4 * max(1.0, abs(l0))
-    assert ((g1 - g0).norm() / g0.norm()).item() < 5e-3
+    assert_scalar_within_noise(l1, l0, l0b, floor=1e-4)
+    assert_within_noise(g1, g0, g0b, floor=3e-3, what="arena gradients")

@@ -27,8 +27,14 @@ def _run(s2d):
 
 
 def test_stem_s2d_matches_padded_path():
-    l1, s1, g1 = _run(True)
+    """The s2d stem accumulates in a different order than the padded one, so its bf16 outputs differ by
+    rounding; the gradients are held to the padded path's own run-to-run spread (tests/noise.py) with a
+    1 % floor (measured spread of a single two-path comparison: 3.1 % on the stem kernel)."""
+    from noise import assert_within_noise
+
     l0, s0, g0 = _run(False)
+    l1, s1, g1 = _run(True)
+    l0b, s0b, g0b = _run(False)
     assert abs(l1 - l0) < 1e-2 * max(1.0, abs(l0)), (l1, l0)
-    assert ((s1 - s0).norm() / s0.norm()).item() < 3e-2
-    assert ((g1 - g0).norm() / g0.norm()).item() < 3e-2
+    assert_within_noise(s1, s0, s0b, floor=1e-2, what="stem kernel gradient")
+    assert_within_noise(g1, g0, g0b, floor=1e-2, what="arena gradients")
