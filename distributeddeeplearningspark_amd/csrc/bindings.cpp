@@ -247,6 +247,48 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
   HIP_OK(launch_gemm_bf16(p, (int)epi, (int)tile, cur_stream()));
 }
 
+// 3x3 / stride-1 / pad-1 weight gradient, halo kernel (conv3x3.hip): gw[Co][3][3][Ci] (fp32) += dW.
+// ws: fp32 slab workspace of splits * Co * 9 * Ci floats (plain stores + reduce kernel), or None (atomics).
+void conv3x3_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& gw, const c10::optional<at::Tensor>& ws,
+                   int64_t splits, int64_t tpb, bool pp) {
+  CHECK_CUDA(dy);
+  CHECK_CUDA(x);
+  CHECK_CUDA(gw);
+  CHECK_BF16(dy);
+  CHECK_BF16(x);
+  CHECK_F32(gw);
+  CHECK_CONTIG(dy);
+  CHECK_CONTIG(x);
+  CHECK_CONTIG(gw);
+  TORCH_CHECK(x.dim() == 4 && gw.dim() == 4 && gw.size(1) == 3 && gw.size(2) == 3 && gw.size(3) == x.size(3),
+              "conv3x3_wgrad: x [N, H, W, Ci], gw [Co, 3, 3, Ci]");
+  const int n = (int)x.size(0), h = (int)x.size(1), w = (int)x.size(2), ci = (int)x.size(3), co = (int)gw.size(0);
+  TORCH_CHECK(dy.numel() == (int64_t)n * h * w * co, "conv3x3_wgrad: dy must be [N, H, W, Co] (stride 1, pad 1)");
+  TORCH_CHECK(conv3x3_wgrad_ok(n, h, w, ci, co), "conv3x3_wgrad: needs Ci, Co % 64 == 0 and a <= 256-pixel row tiling");
+  int s_plan = 0, t_plan = 0, ntiles = 0;
+  conv3x3_wgrad_plan(n, h, w, ci, co, 1, 1, s_plan, t_plan, ntiles);
+  TORCH_CHECK(splits >= 1 && tpb >= 1 && (splits - 1) * tpb < ntiles && splits * tpb >= ntiles,
+              "conv3x3_wgrad: splits x tiles-per-split must cover the pixel tiles exactly once");
+  float* wsp = nullptr;
+  if (ws) {
+    CHECK_CUDA(*ws);
+    CHECK_F32(*ws);
+    TORCH_CHECK(ws->is_contiguous() && ws->numel() >= splits * co * 9 * (int64_t)ci, "conv3x3_wgrad: workspace too small");
+    wsp = ws->data_ptr<float>();
+  }
+  at::DeviceGuard guard(x.device());
+  HIP_OK(launch_conv3x3_wgrad(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                              gw.data_ptr<float>(), wsp, n, h, w, ci, co, (int)splits, (int)tpb, pp, cur_stream()));
+}
+
+py::object conv3x3_wgrad_plan_py(int64_t n, int64_t h, int64_t w, int64_t ci, int64_t co, int64_t blocks_per_cu,
+                                 int64_t cus) {
+  if (!conv3x3_wgrad_ok((int)n, (int)h, (int)w, (int)ci, (int)co)) return py::none();
+  int splits = 0, tpb = 0, ntiles = 0;
+  conv3x3_wgrad_plan((int)n, (int)h, (int)w, (int)ci, (int)co, (int)blocks_per_cu, (int)cus, splits, tpb, ntiles);
+  return py::make_tuple(splits, tpb);
+}
+
 }  // namespace
 
 void register_ops(py::module& m);      // ops_bindings.cpp style registrations (elementwise, norms, ...)
@@ -268,6 +310,12 @@ PYBIND11_MODULE(_C, m) {
         py::arg("bnr_mean") = py::none(), py::arg("rsub_h") = 0, py::arg("rsub_w") = 0,
         py::arg("a_scale") = py::none(), py::arg("a_shift") = py::none(), py::arg("b_scale") = py::none(),
         py::arg("b_shift") = py::none(), py::arg("bnr_scale") = py::none(), py::arg("bnr_shift") = py::none());
+  m.def("conv3x3_wgrad", &conv3x3_wgrad, "3x3 stride-1 weight gradient (halo kernel): gw += dW", py::arg("dy"),
+        py::arg("x"), py::arg("gw"), py::arg("ws"), py::arg("splits"), py::arg("tpb"), py::arg("pp") = false);
+  m.def("conv3x3_wgrad_plan", &conv3x3_wgrad_plan_py,
+        "(splits, tiles per split) of the 3x3 weight-gradient halo kernel, or None when it does not apply",
+        py::arg("n"), py::arg("h"), py::arg("w"), py::arg("ci"), py::arg("co"), py::arg("blocks_per_cu"),
+        py::arg("cus"));
   m.attr("ACT_NONE") = (int)ACT_NONE;
   m.attr("ACT_RELU") = (int)ACT_RELU;
   m.attr("ACT_GELU") = (int)ACT_GELU;

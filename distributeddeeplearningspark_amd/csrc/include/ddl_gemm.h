@@ -132,6 +132,16 @@ constexpr int kTileConv3 = 6;   // tile id of the 3x3 stride-1 halo convolution 
 // the halo kernel applies to this (KC_GATHER x KC, 3x3 / stride 1 / pad 1) GEMM
 bool conv3x3_halo_ok(const GemmParams& p);
 
+// 3x3 / stride-1 / pad-1 weight gradient with the input halo in LDS (conv3x3.hip): applicability, split plan
+// (pixel-tile splits and tiles per workgroup) and launch; ws = [splits][Co][9 Ci] fp32 slabs reduced into gw by
+// a second kernel, or nullptr for atomic accumulation into gw [Co][9 Ci]; pp: the 512-thread ping-pong form
+// (plan it with blocks_per_cu = 1)
+bool conv3x3_wgrad_ok(int n, int h, int w, int ci, int co);
+void conv3x3_wgrad_plan(int n, int h, int w, int ci, int co, int blocks_per_cu, int cus, int& splits, int& tpb,
+                        int& ntiles);
+int launch_conv3x3_wgrad(const uint16_t* dy, const uint16_t* x, float* gw, float* ws, int n, int h, int w, int ci,
+                         int co, int splits, int tpb, bool pp, void* stream);
+
 // panel width of the streaming kernel for (N, K), 0 when it does not apply
 int gemm_stream_panel(int N, int K);
 

@@ -232,7 +232,508 @@ int launch(const GemmParams& p, const Conv3Tiling& t, hipStream_t s) {
   return launch_fr<BN, EPI, NB, 8>(p, t, s);
 }
 
+// ------------------------------------------------------------------------------------------------
+// 3x3 stride-1 pad-1 WEIGHT gradient with the input halo in LDS:
+//   dW[co][tap][ci] += sum_p dy[p][co] * x[p + tap][ci]      (M = Co, N = 9 Ci, K = pixels)
+// The gathered implicit GEMM (RC x RC_GATHER) re-fetches every input pixel once per tap and per
+// 128-column tile and runs at 12-17 % MFMA (profiles/r2/pmc_conv3x3_halo_v2.txt: 56 % of wave time
+// parked).  Here a workgroup owns a 64 co x 64 ci x 9 tap output block and walks pixel tiles (the
+// forward kernel's row tiling, <= 256 pixels): per tile it stages dy [Ppad][64 co] (the RC image the
+// GEMM kernels read with ds_read_b64_tr_b16) and the x halo once, and all nine taps read their B
+// fragments from the halo at tap-shifted rows — 36 MFMAs per 40 transposed LDS reads per wave and
+// 32-pixel step, no per-tap global traffic.  Waves: 2 (co) x 2 (ci), 32 x 32 x 9 taps each.
+//
+// Halo image CHUNK-major: [8 chunks of 8 channels][SC rows][16 B], SC = 64 G + 4 rows.  A transposed
+// fragment read touches rows b + {0..3, 8..11} of two chunks; same-parity rows of one chunk fall on
+// distinct banks and SC = 4 (mod 8) puts the second chunk on the other 32 banks, so the read is
+// conflict-free with NO swizzle — which makes a tap shift a constant byte offset (toff * 16, an
+// immediate of ds_read: WW is a template parameter) instead of per-read swizzle arithmetic.  The LDS-DMA
+// fills 64 consecutive rows of one chunk per wave-instruction (G groups x 8 chunks); the 4 rows between
+// chunk images are never written or read.
+struct WgradArgs {
+  const bf16_t* dy;  // [M][Co]
+  const bf16_t* x;   // [N][H][W][Ci]
+  float* out;        // SLAB: [splits][Co][9 Ci] partial slabs (plain stores); else [Co][9 Ci] (+= by atomics)
+  int n, h, w, ci, co;
+  int ntiles, tpb;   // pixel tiles and tiles per workgroup (blockIdx split s walks [s tpb, (s+1) tpb))
+};
+
+// One pixel tile of the weight-gradient product (both kernels below): KT 32-pixel steps x 9 taps x
+// 2 x 2 MFMAs per wave, software-pipelined — the next tap's B fragments (and at tap 8 the next step's A
+// fragments and tap-0 B fragments, whose halo rows were read one step ahead) are issued before the
+// current tap's MFMAs, so a wave alone on its SIMD (the ping-pong kernel's computing half) does not
+// stall on LDS latency at every tap or step boundary.
+template <int WW, int SC, int KT>
+__device__ __forceinline__ void wgrad_tile_mma(f32x4 (&acc)[9][2][2], const char* halo, const char* dyl,
+                                               const int* hbt, const int (&ao)[2][2], const int boff, const int k1) {
+  auto tr2 = [](const char* p1, const char* p2) {
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DDL_LDS s16x4*)p1);
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DDL_LDS s16x4*)p2);
+    s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, r);
+  };
+  constexpr int JS = 2 * SC * 16;  // next 16-channel fragment: two chunks on
+  int hb1 = hbt[k1], hb2 = hbt[k1 + 4];
+  int nhb1 = hbt[(KT > 1 ? 32 : 0) + k1], nhb2 = hbt[(KT > 1 ? 32 : 0) + k1 + 4];
+  bf16x8 af[2], bf[2];
+  af[0] = tr2(dyl + ao[0][0], dyl + ao[0][1]);
+  af[1] = tr2(dyl + ao[1][0], dyl + ao[1][1]);
+  {
+    const char* b1 = halo + boff + hb1 * 16;
+    const char* b2 = halo + boff + hb2 * 16;
+    bf[0] = tr2(b1, b2);
+    bf[1] = tr2(b1 + JS, b2 + JS);
+  }
+#pragma unroll 1
+  for (int kk = 0; kk < KT; ++kk) {
+    const char* b1 = halo + boff + hb1 * 16;
+    const char* b2 = halo + boff + hb2 * 16;
+    const int kn = kk + 1 < KT ? kk + 1 : kk;  // clamped: the last step re-reads its own rows
+    const int kn2 = kk + 2 < KT ? kk + 2 : KT - 1;
+    bf16x8 an[2];
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      bf16x8 bn[2];
+      if (tap < 8) {
+        const int toff = (((tap + 1) / 3) * WW + ((tap + 1) % 3)) * 16;
+        bn[0] = tr2(b1 + toff, b2 + toff);
+        bn[1] = tr2(b1 + toff + JS, b2 + toff + JS);
+      } else {
+        const char* n1 = halo + boff + nhb1 * 16;
+        const char* n2 = halo + boff + nhb2 * 16;
+        bn[0] = tr2(n1, n2);
+        bn[1] = tr2(n1 + JS, n2 + JS);
+        const char* ab = dyl + kn * 4096;
+        an[0] = tr2(ab + ao[0][0], ab + ao[0][1]);
+        an[1] = tr2(ab + ao[1][0], ab + ao[1][1]);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[tap][i][j] = mfma16x16x32(af[i], bf[j], acc[tap][i][j]);
+      __builtin_amdgcn_sched_barrier(0);
+      bf[0] = bn[0];
+      bf[1] = bn[1];
+    }
+    af[0] = an[0];
+    af[1] = an[1];
+    hb1 = nhb1;
+    hb2 = nhb2;
+    nhb1 = hbt[kn2 * 32 + k1];
+    nhb2 = hbt[kn2 * 32 + k1 + 4];
+  }
+}
+
+template <int G, int KT>
+constexpr int wgrad_lds_bytes() { return 8 * (64 * G + 4) * 16 + KT * 32 * 128 + KT * 32 * 4; }
+
+template <int WW, int G, int KT, bool SLAB>
+__global__ __launch_bounds__(NTHREADS, 2) void conv3x3_wgrad_kernel(const WgradArgs a, const Conv3Tiling t) {
+  constexpr int SC = 64 * G + 4;  // rows per chunk image
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* halo = smem;
+  char* dyl = smem + 8 * SC * 16;
+  int* hbt = reinterpret_cast<int*>(dyl + KT * 32 * 128);  // halo row of each tile pixel (tap (0, 0))
+  const int ci_tiles = a.ci / 64;
+  int bid, split;
+  grid_tile(bid, split);
+  const int tco = bid / ci_tiles, tci = bid - tco * ci_tiles;
+  const int co0 = tco * 64, ci0 = tci * 64;
+  const int tp_beg = split * a.tpb, tp_end = min(a.ntiles, tp_beg + a.tpb);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm0 = (wid >> 1) * 32, wn0 = (wid & 1) * 32;
+  const int M = a.n * a.h * a.w;
+
+  // tile-independent tables: the halo row of every tile pixel (pixels past the tile read row 0, finite
+  // data, against zero dy rows), and this lane's halo rows (g * 64 + lane) decoded to (image, y, x)
+  for (int px = threadIdx.x; px < KT * 32; px += NTHREADS) {
+    int r = 0;
+    if (px < t.P) {
+      const int im = px / (t.rows * t.w);
+      const int rem = px - im * t.rows * t.w;
+      const int oy = rem / t.w, ox = rem - oy * t.w;
+      r = im * t.hh * WW + oy * WW + ox;
+    }
+    hbt[px] = r;
+  }
+  int hcode[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int hrow = g * 64 + lane;
+    hcode[g] = -1;
+    if (hrow < t.hr) {
+      const int im = hrow / (t.hh * WW);
+      const int rem = hrow - im * t.hh * WW;
+      const int hy = rem / WW, hx = rem - hy * WW;
+      hcode[g] = (im << 20) | (hy << 10) | hx;
+    }
+  }
+  __syncthreads();  // the pixel table is read by every wave
+  const uint32_t halo_lds = lds_addr(halo);
+  const uint32_t dy_lds = lds_addr(dyl) + (uint32_t)__builtin_amdgcn_readfirstlane(wid) * 1024u;
+
+  auto stage = [&](int tp) {
+    const int timg = tp / t.tiles_row, trow = tp - timg * t.tiles_row;
+    const int img0 = timg * t.img, oy0 = trow * t.rows;
+    const int m0 = (img0 * a.h + oy0) * a.w;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int code = hcode[g];
+      const int n = img0 + (code >> 20), iy = oy0 + ((code >> 10) & 1023) - 1, ix = (code & 1023) - 1;
+      const bool ok = code >= 0 && n < a.n && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
+      const bf16_t* src = a.x + ((n * a.h + iy) * a.w + ix) * a.ci + ci0;
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {  // this wave's chunks: wid and wid + 4
+        const int c = wid + 4 * h2;
+        dma16(ok ? (const void*)(src + c * 8) : (const void*)ddl_zero_page,
+              halo_lds + (uint32_t)__builtin_amdgcn_readfirstlane(c * SC * 16 + g * 1024));
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < KT; ++j) {
+      const int r = (wid + 4 * j) * 8 + (lane >> 3);
+      const int m = m0 + r;
+      const bool ok = r < t.P && m < M;
+      const int chunk = (lane & 7) ^ (rc_swz<64>(r) << 1);
+      const void* src = ok ? (const void*)(a.dy + (long)m * a.co + co0 + chunk * 8) : (const void*)ddl_zero_page;
+      dma16(src, dy_lds + (uint32_t)(j * 4096));
+    }
+  };
+
+  f32x4 acc[9][2][2];
+#pragma unroll
+  for (int tp = 0; tp < 9; ++tp)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[tp][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // per-lane fragment geometry (the RC fragment of ddl_gemm_kernel.h): k rows 8 (lane>>4) + q and + 4,
+  // columns 4 (lane & 3) .. + 3 of each 16-wide fragment
+  const int g4 = lane >> 4, q = (lane & 15) >> 2, pq = lane & 3;
+  const int k1 = 8 * g4 + q;  // + 32 kk; rc_swz<64> of it does not depend on kk
+  int ao[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      const int k = k1 + 4 * h2, col = wm0 + 16 * i + 4 * pq;
+      ao[i][h2] = k * 128 + ((((col >> 3) ^ (rc_swz<64>(k) << 1))) << 4) + (col & 7) * 2;
+    }
+  // B: chunk (wn0 / 8 + 2 j + pq / 2), byte (pq & 1) * 8 of the row
+  const int boff = ((wn0 >> 3) + (pq >> 1)) * (SC * 16) + (pq & 1) * 8;
+
+  for (int tp = tp_beg; tp < tp_end; ++tp) {
+    stage(tp);
+    wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();  // this tile's dy and halo (and, first time, the pixel table) landed
+    wgrad_tile_mma<WW, SC, KT>(acc, halo, dyl, hbt, ao, boff, k1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave is done reading this tile before the next one lands
+  }
+
+  // D orientation: acc[tap][i][j][e] = dW[co0 + wm0 + 16i + 4(lane>>4) + e][tap][ci0 + wn0 + 16j + (lane&15)]
+  // -> each wave-instruction covers 4 rows x 64 contiguous bytes
+  const long ldo = 9L * a.ci;
+  float* out = a.out + (SLAB ? (long)split * a.co * ldo : 0L);
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int co = co0 + wm0 + 16 * i + 4 * g4 + e;
+          const int ci = ci0 + wn0 + 16 * j + (lane & 15);
+          float* c = out + (long)co * ldo + tap * a.ci + ci;
+          if constexpr (SLAB) *c = acc[tap][i][j][e];
+          else atomicAdd(c, acc[tap][i][j][e]);
+        }
+}
+
+// Ping-pong form: ONE 512-thread workgroup per CU, two halves of 4 waves with an LDS tile buffer each.
+// Phases alternate: half A computes a pixel tile while half B's LDS-DMA of its next tile lands, then the
+// roles swap (one workgroup barrier per phase) — the load latency hides under the other half's MFMAs
+// within the workgroup, as the two co-resident workgroups of the kernel above do, but both halves
+// accumulate the SAME 64 x 64 x 9 output block: they are merged through LDS at the end and the CU writes
+// one partial slab (or one set of atomics) instead of two — half the split-K output traffic.
+template <int G, int KT>
+constexpr int wgrad_pp_lds_bytes() { return 2 * (8 * (64 * G + 4) * 16 + KT * 32 * 128) + KT * 32 * 4; }
+
+template <int WW, int G, int KT, bool SLAB>
+__global__ __launch_bounds__(512, 1) void conv3x3_wgrad_pp_kernel(const WgradArgs a, const Conv3Tiling t) {
+  constexpr int SC = 64 * G + 4;
+  constexpr int BUF = 8 * SC * 16 + KT * 32 * 128;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int* hbt = reinterpret_cast<int*>(smem + 2 * BUF);
+  const int ci_tiles = a.ci / 64;
+  int bid, split;
+  grid_tile(bid, split);
+  const int tco = bid / ci_tiles, tci = bid - tco * ci_tiles;
+  const int co0 = tco * 64, ci0 = tci * 64;
+  const int tp_beg = split * a.tpb, tp_end = min(a.ntiles, tp_beg + a.tpb);
+  const int nt = max(0, tp_end - tp_beg);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int grp = __builtin_amdgcn_readfirstlane(wid >> 2), w4 = wid & 3;
+  const int wm0 = (w4 >> 1) * 32, wn0 = (w4 & 1) * 32;
+  const int M = a.n * a.h * a.w;
+  char* halo = smem + grp * BUF;
+  char* dyl = halo + 8 * SC * 16;
+
+  for (int px = threadIdx.x; px < KT * 32; px += 512) {
+    int r = 0;
+    if (px < t.P) {
+      const int im = px / (t.rows * t.w);
+      const int rem = px - im * t.rows * t.w;
+      const int oy = rem / t.w, ox = rem - oy * t.w;
+      r = im * t.hh * WW + oy * WW + ox;
+    }
+    hbt[px] = r;
+  }
+  int hcode[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int hrow = g * 64 + lane;
+    hcode[g] = -1;
+    if (hrow < t.hr) {
+      const int im = hrow / (t.hh * WW);
+      const int rem = hrow - im * t.hh * WW;
+      const int hy = rem / WW, hx = rem - hy * WW;
+      hcode[g] = (im << 20) | (hy << 10) | hx;
+    }
+  }
+  const uint32_t halo_lds = lds_addr(halo);
+  const uint32_t dy_lds = lds_addr(dyl) + (uint32_t)__builtin_amdgcn_readfirstlane(w4) * 1024u;
+  auto stage = [&](int tp) {  // this half's 4 waves stage tile tp into its buffer
+    const int timg = tp / t.tiles_row, trow = tp - timg * t.tiles_row;
+    const int img0 = timg * t.img, oy0 = trow * t.rows;
+    const int m0 = (img0 * a.h + oy0) * a.w;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int code = hcode[g];
+      const int n = img0 + (code >> 20), iy = oy0 + ((code >> 10) & 1023) - 1, ix = (code & 1023) - 1;
+      const bool ok = code >= 0 && n < a.n && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
+      const bf16_t* src = a.x + ((n * a.h + iy) * a.w + ix) * a.ci + ci0;
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int c = w4 + 4 * h2;
+        dma16(ok ? (const void*)(src + c * 8) : (const void*)ddl_zero_page,
+              halo_lds + (uint32_t)__builtin_amdgcn_readfirstlane(c * SC * 16 + g * 1024));
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < KT; ++j) {
+      const int r = (w4 + 4 * j) * 8 + (lane >> 3);
+      const int m = m0 + r;
+      const bool ok = r < t.P && m < M;
+      const int chunk = (lane & 7) ^ (rc_swz<64>(r) << 1);
+      const void* src = ok ? (const void*)(a.dy + (long)m * a.co + co0 + chunk * 8) : (const void*)ddl_zero_page;
+      dma16(src, dy_lds + (uint32_t)(j * 4096));
+    }
+  };
+
+  f32x4 acc[9][2][2];
+#pragma unroll
+  for (int tp = 0; tp < 9; ++tp)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[tp][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int g4 = lane >> 4, q = (lane & 15) >> 2, pq = lane & 3;
+  const int k1 = 8 * g4 + q;
+  int ao[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      const int k = k1 + 4 * h2, col = wm0 + 16 * i + 4 * pq;
+      ao[i][h2] = k * 128 + ((((col >> 3) ^ (rc_swz<64>(k) << 1))) << 4) + (col & 7) * 2;
+    }
+  const int boff = ((wn0 >> 3) + (pq >> 1)) * (SC * 16) + (pq & 1) * 8;
+
+  // phase ph: half (ph & 1) computes tile tp_beg + ph from its buffer while the other half's next tile
+  // (staged right after the previous phase) lands; ONE call site of the tile body, uniform branches only
+  if (grp < nt) stage(tp_beg + grp);
+  if (grp == 0) wait_vmcnt<0>();
+  __syncthreads();  // the pixel table, and half A's first tile
+  for (int ph = 0; ph < nt; ++ph) {
+    const bool mine = (ph & 1) == grp;
+    if (mine) wgrad_tile_mma<WW, SC, KT>(acc, halo, dyl, hbt, ao, boff, k1);
+    else wait_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (mine && ph + 2 < nt) stage(tp_beg + ph + 2);  // this half's buffer is free again
+  }
+  wait_vmcnt<0>();
+
+  // merge the halves through LDS (both tile buffers are free): entry e = tap*4 + 2i + j in four rounds of 9;
+  // half B sends rounds 0-1 to half A, half A sends rounds 2-3 to half B; each then writes what it kept
+  DDL_LDS f32x4* xm = (DDL_LDS f32x4*)(smem);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int sender = r < 2 ? 1 : 0;
+    if (grp == sender) {
+#pragma unroll
+      for (int el = 0; el < 9; ++el) {
+        const int e = 9 * r + el;
+        xm[(el * 4 + w4) * 64 + lane] = acc[e >> 2][(e >> 1) & 1][e & 1];
+      }
+    }
+    __syncthreads();
+    if (grp != sender) {
+#pragma unroll
+      for (int el = 0; el < 9; ++el) {
+        const int e = 9 * r + el;
+        acc[e >> 2][(e >> 1) & 1][e & 1] += xm[(el * 4 + w4) * 64 + lane];
+      }
+    }
+    __syncthreads();
+  }
+
+  const long ldo = 9L * a.ci;
+  float* out = a.out + (SLAB ? (long)split * a.co * ldo : 0L);
+#pragma unroll
+  for (int e = 0; e < 36; ++e) {
+    const int tap = e >> 2, i = (e >> 1) & 1, j = e & 1;
+    if ((grp == 0) != (e < 18)) continue;  // half A wrote rounds 0-1 (entries 0..17)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int co = co0 + wm0 + 16 * i + 4 * g4 + v;
+      const int ci = ci0 + wn0 + 16 * j + (lane & 15);
+      float* c = out + (long)co * ldo + tap * a.ci + ci;
+      if constexpr (SLAB) *c = acc[tap][i][j][v];
+      else atomicAdd(c, acc[tap][i][j][v]);
+    }
+  }
+}
+
+// gw[i] += sum over the slabs of ws[s][i]: float4 per lane, the slabs split into groups of G whose
+// partial sums are added atomically (one group when there are few slabs)
+__global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(const float4* __restrict__ ws, float* __restrict__ gw,
+                                                                long n4, int slabs, int per_group) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const int s0 = blockIdx.y * per_group, s1 = min(slabs, s0 + per_group);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int s = s0; s < s1; ++s) {
+    const float4 v = ws[(long)s * n4 + i];
+    acc.x += v.x;
+    acc.y += v.y;
+    acc.z += v.z;
+    acc.w += v.w;
+  }
+  float* o = gw + 4 * i;
+  if (gridDim.y == 1) {
+    float4 g = *reinterpret_cast<float4*>(o);
+    g.x += acc.x;
+    g.y += acc.y;
+    g.z += acc.z;
+    g.w += acc.w;
+    *reinterpret_cast<float4*>(o) = g;
+  } else {
+    atomicAdd(o, acc.x);
+    atomicAdd(o + 1, acc.y);
+    atomicAdd(o + 2, acc.z);
+    atomicAdd(o + 3, acc.w);
+  }
+}
+
+template <int WW, int G, int KT, bool SLAB>
+int launch_wgrad_v(const WgradArgs& a, const Conv3Tiling& t, dim3 grid, bool pp, hipStream_t s) {
+  if (pp) {
+    constexpr int lds = wgrad_pp_lds_bytes<G, KT>();
+    static_assert(lds <= 160 * 1024, "one workgroup per CU");
+    static bool attr = [] {
+      return hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_wgrad_pp_kernel<WW, G, KT, SLAB>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
+    }();
+    (void)attr;
+    hipLaunchKernelGGL((conv3x3_wgrad_pp_kernel<WW, G, KT, SLAB>), grid, dim3(512), lds, s, a, t);
+    return (int)hipGetLastError();
+  }
+  constexpr int lds = wgrad_lds_bytes<G, KT>();
+  static_assert(lds <= 80 * 1024, "two workgroups per CU");
+  static bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_wgrad_kernel<WW, G, KT, SLAB>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL((conv3x3_wgrad_kernel<WW, G, KT, SLAB>), grid, dim3(NTHREADS), lds, s, a, t);
+  return (int)hipGetLastError();
+}
+
+// Instantiated tilings (halo width WW, 64-row halo groups G, 32-pixel steps KT): the ResNet-50 stages at
+// 224^2 (56, 28, 14 and 7 pixels wide; every one plans 196- or 224-pixel tiles).  Others take the GEMM path.
+int wgrad_variant(const Conv3Tiling& t) {
+  const int G = (t.hr + 63) / 64, KT = (t.P + 31) / 32;
+  if (KT != 7) return -1;
+  if (t.ww == 58 && G == 6) return 0;
+  if (t.ww == 30 && G == 5) return 1;
+  if (t.ww == 16 && G == 4) return 2;
+  if (t.ww == 9 && G == 6) return 3;
+  return -1;
+}
+
+template <bool SLAB>
+int launch_wgrad(const WgradArgs& a, const Conv3Tiling& t, dim3 grid, bool pp, hipStream_t s) {
+  switch (wgrad_variant(t)) {
+    case 0: return launch_wgrad_v<58, 6, 7, SLAB>(a, t, grid, pp, s);
+    case 1: return launch_wgrad_v<30, 5, 7, SLAB>(a, t, grid, pp, s);
+    case 2: return launch_wgrad_v<16, 4, 7, SLAB>(a, t, grid, pp, s);
+    case 3: return launch_wgrad_v<9, 6, 7, SLAB>(a, t, grid, pp, s);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
 }  // namespace
+
+// Plan of the 3x3 weight-gradient halo kernel: tiles, splits and the slab workspace size (floats;
+// 0 = atomics).  blocks_per_cu: workgroups the split aims for per CU (the kernel fits 2).
+bool conv3x3_wgrad_ok(int n, int h, int w, int ci, int co) {
+  if (ci % 64 || co % 64 || n <= 0 || (long)n * h * w * std::max(ci, co) >= (1L << 31)) return false;
+  GemmParams p{};
+  p.g.n = n;
+  p.g.hi = h;
+  p.g.wi = w;
+  const Conv3Tiling t = plan(p);
+  return t.rows > 0 && t.P >= 64 && t.P <= 256 && t.hr <= C3_MAX_HALO_ROWS && wgrad_variant(t) >= 0;
+}
+
+void conv3x3_wgrad_plan(int n, int h, int w, int ci, int co, int blocks_per_cu, int cus, int& splits, int& tpb,
+                        int& ntiles) {
+  GemmParams p{};
+  p.g.n = n;
+  p.g.hi = h;
+  p.g.wi = w;
+  const Conv3Tiling t = plan(p);
+  ntiles = t.tiles_img * t.tiles_row;
+  const int pairs = (co / 64) * (ci / 64);
+  const int want = std::max(1, (blocks_per_cu * cus + pairs - 1) / pairs);
+  tpb = std::max(1, (ntiles + std::min(want, ntiles) - 1) / std::min(want, ntiles));
+  splits = (ntiles + tpb - 1) / tpb;
+}
+
+int launch_conv3x3_wgrad(const bf16_t* dy, const bf16_t* x, float* gw, float* ws, int n, int h, int w, int ci, int co,
+                         int splits, int tpb, bool pp, void* stream) {
+  const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  GemmParams p{};
+  p.g.n = n;
+  p.g.hi = h;
+  p.g.wi = w;
+  const Conv3Tiling t = plan(p);
+  WgradArgs a{dy, x, ws ? ws : gw, n, h, w, ci, co, t.tiles_img * t.tiles_row, tpb};
+  const dim3 grid((co / 64) * (ci / 64), splits);
+  int rc = ws ? launch_wgrad<true>(a, t, grid, pp, s) : launch_wgrad<false>(a, t, grid, pp, s);
+  if (rc || !ws) return rc;
+  const long n4 = (long)co * 9 * ci / 4;
+  const int per_group = n4 >= 65536 ? splits : 16;  // enough workgroups either way
+  const dim3 rgrid((unsigned)((n4 + 255) / 256), (unsigned)((splits + per_group - 1) / per_group));
+  hipLaunchKernelGGL(wgrad_slab_reduce_kernel, rgrid, dim3(256), 0, s, reinterpret_cast<const float4*>(ws), gw, n4,
+                     splits, per_group);
+  return (int)hipGetLastError();
+}
 
 // The halo kernel applies to this GEMM (host check; the Python side mirrors it in ops/conv.py).
 bool conv3x3_halo_ok(const GemmParams& p) {

@@ -125,6 +125,32 @@ def halo3_ok(g: ConvGeometry) -> bool:
     return False
 
 
+_WG3 = _os.environ.get("DDL_WGRAD3X3", "1") != "0"
+_WG3_BPC = int(_os.environ.get("DDL_WGRAD3X3_BPC", "2"))  # workgroups per CU the pixel split aims for
+_WG3_SLAB = _os.environ.get("DDL_WGRAD3X3_SLAB", "1") == "1"  # partial slabs + reduce instead of atomics
+_WG3_PP = _os.environ.get("DDL_WGRAD3X3_PP", "0") == "1"  # 512-thread ping-pong form (one workgroup per CU)
+
+
+@lru_cache(maxsize=None)
+def _device_cus(index: int) -> int:
+    return torch.cuda.get_device_properties(index).multi_processor_count
+
+
+@lru_cache(maxsize=1024)
+def _wgrad3_plan(N, H, W, Ci, Co, bpc, cus):
+    return C().conv3x3_wgrad_plan(N, H, W, Ci, Co, bpc, cus)
+
+
+def wgrad3_plan(g: ConvGeometry, device=None):
+    """(splits, tiles per split) of the 3x3 / stride-1 / pad-1 weight-gradient halo kernel, or None
+    (csrc/kernels/conv3x3.hip: C, Co % 64 == 0 and one of its instantiated row tilings)."""
+    if not (_WG3 and g.KH == 3 and g.KW == 3 and (g.sh, g.sw) == (1, 1) and (g.ph, g.pw) == (1, 1)
+            and (g.dh, g.dw) == (1, 1) and g.Ci % 64 == 0 and g.Co % 64 == 0):
+        return None
+    idx = torch.cuda.current_device() if device is None else torch.device(device).index or 0
+    return _wgrad3_plan(g.N, g.H, g.W, g.Ci, g.Co, 1 if _WG3_PP else _WG3_BPC, _device_cus(idx))
+
+
 _SPLITK_FWD = _os.environ.get("DDL_CONV_SPLITK", "1") != "0"
 _SPLITK_MAX_TILES = int(_os.environ.get("DDL_CONV_SPLITK_TILES", "512"))
 _SPLITK_WG = int(_os.environ.get("DDL_CONV_SPLITK_WG", "1024"))  # workgroups the split aims for
@@ -316,8 +342,14 @@ def conv_wgrad_native(dy, x, g: ConvGeometry, gw, x_norm=None):
     gw2 = gw.view(g.Co, g.T * g.Ci)
     if x_norm is not None and not g.is_pointwise:
         raise ValueError("conv_wgrad_native: normalise-on-load for pointwise convs only")
+    plan = None if g.is_pointwise else wgrad3_plan(g, dy.device)
     if g.is_pointwise:
         G.linear_wgrad(dy.view(g.M, g.Co), x.view(g.M, g.Ci), gw2, x_norm=x_norm)
+    elif plan is not None:
+        # 3x3 / stride 1: halo kernel (csrc/kernels/conv3x3.hip), 64 co x 64 ci x 9 taps per workgroup
+        splits, tpb = plan
+        ws = torch.empty(splits * g.Co * 9 * g.Ci, dtype=torch.float32, device=dy.device) if _WG3_SLAB else None
+        C().conv3x3_wgrad(dy.contiguous(), x.contiguous(), gw, ws, splits, tpb, _WG3_PP)
     elif g.implicit_wgrad and g.Ci < 128 and _WIDE_WGRAD:
         # narrow inputs (64 channels): a 128-wide tile spans two taps, so the tap is resolved per
         # 16-B vector (GATHER8) instead of per tile — twice the MFMA work per LDS fragment read

@@ -882,3 +882,34 @@ def test_bottleneck_norm_on_load_matches_applied(monkeypatch):
     assert a1 == a0 - 2, (a1, a0)  # both blocks' bn2 apply sweeps are gone
     assert_scalar_within_noise(l1, l0, l0b, floor=1e-4)
     assert_within_noise(g1, g0, g0b, floor=3e-3, what="arena gradients")
+
+@pytest.mark.parametrize("N,H,W,Ci,Co", [(2, 56, 56, 64, 64), (3, 28, 28, 128, 64), (2, 14, 14, 64, 128),
+                                         (9, 7, 7, 128, 128), (1, 14, 14, 256, 192)])
+@pytest.mark.parametrize("slab,pp", [(False, False), (True, False), (True, True), (False, True)])
+def test_conv3x3_wgrad_halo_kernel(N, H, W, Ci, Co, slab, pp, monkeypatch):
+    """3x3 stride-1 weight-gradient halo kernel (csrc/kernels/conv3x3.hip) vs the fp32 PyTorch weight
+    gradient of the same bf16 operands: every ResNet-50 row tiling (56/28/14/7 wide), a partial last
+    group of images (N = 9 at 7x7), several 64-channel tiles each way, atomics and partial slabs, and
+    accumulation into a non-zero gradient; the two-workgroups-per-CU form and the 512-thread ping-pong form
+    (two halves accumulating the same block, merged through LDS)."""
+    from distributeddeeplearningspark_amd.ops import conv as CV
+
+    monkeypatch.setattr(CV, "_WG3_SLAB", slab)
+    monkeypatch.setattr(CV, "_WG3_PP", pp)
+    g = CV.geometry(N, H, W, Ci, Co, 3, 3, (1, 1), (1, 1), (1, 1))
+    plan = CV.wgrad3_plan(g)
+    assert plan is not None
+    x = rnd(N, H, W, Ci, seed=3)
+    dy = rnd(N, H, W, Co, scale=0.5, seed=4)
+    gw0 = torch.randn(Co, 3, 3, Ci, device=DEV)
+    gw = gw0.clone()
+    CV.conv_wgrad_native(dy, x, g, gw)
+    ref = torch.nn.grad.conv2d_weight(x.float().cpu().permute(0, 3, 1, 2), (Co, Ci, 3, 3),
+                                      dy.float().cpu().permute(0, 3, 1, 2), stride=1, padding=1)
+    ref = ref.permute(0, 2, 3, 1) + gw0.cpu()
+    close(gw, ref, rtol=1e-3, atol=1e-2, what=f"wgrad3 halo slab={slab} pp={pp}")
+    # the gathered implicit GEMM agrees on the same problem
+    monkeypatch.setattr(CV, "_WG3", False)
+    gw2 = gw0.clone()
+    CV.conv_wgrad_native(dy, x, g, gw2)
+    close(gw, gw2, rtol=1e-3, atol=1e-2, what="wgrad3 halo vs gathered GEMM")
