@@ -128,7 +128,7 @@ def halo3_ok(g: ConvGeometry) -> bool:
 _WG3 = _os.environ.get("DDL_WGRAD3X3", "1") != "0"
 _WG3_BPC = int(_os.environ.get("DDL_WGRAD3X3_BPC", "2"))  # workgroups per CU the pixel split aims for
 _WG3_SLAB = _os.environ.get("DDL_WGRAD3X3_SLAB", "1") == "1"  # partial slabs + reduce instead of atomics
-_WG3_PP = _os.environ.get("DDL_WGRAD3X3_PP", "0") == "1"  # 512-thread ping-pong form (one workgroup per CU)
+_WG3_PP = _os.environ.get("DDL_WGRAD3X3_PP", "1") == "1"  # 512-thread ping-pong form (one workgroup per CU)
 
 
 @lru_cache(maxsize=None)
