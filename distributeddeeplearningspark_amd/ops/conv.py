@@ -103,6 +103,7 @@ def _im2col(x, g: ConvGeometry, taps_h, taps_w, ho, wo, sh, sw, kpad):
 
 
 _HALO3 = _os.environ.get("DDL_CONV3X3", "1") != "0"
+_C64PP = _os.environ.get("DDL_CONV3X3_C64PP", "0") == "1"  # opt-in until it beats the implicit GEMM
 
 
 def halo3_ok(g: ConvGeometry) -> bool:
@@ -113,9 +114,11 @@ def halo3_ok(g: ConvGeometry) -> bool:
             and (g.dh, g.dw) == (1, 1) and g.Ci % 64 == 0 and g.Co % 64 == 0 and g.implicit_fwd):
         return False
     if g.Ci == 64 and g.Co == 64 and _os.environ.get("DDL_CONV3X3_C64", "0") != "1":
-        # one 64-channel chunk: the halo prologue is not amortised; measured 0.128 vs 0.120 ms at
-        # 56x56 (ResNet stage 1) — the implicit GEMM keeps these
-        return False
+        # one 64-channel chunk: the per-tap halo kernel cannot amortise its halo prologue (measured 0.128 vs
+        # 0.120 ms for the implicit GEMM at 56x56); the resident-filter ping-pong kernel (conv3x3.hip,
+        # conv3x3_c64_pp_kernel) takes the 56x56 and 32x32 row tilings it is instantiated for
+        if not (_C64PP and g.H == g.W and g.H in (56, 32)):
+            return False
     H, W = g.H, g.W
     if H * W <= 256:
         return H * W * max(1, min(256 // (H * W), 384 // ((H + 2) * (W + 2)))) >= 64

@@ -913,3 +913,47 @@ def test_conv3x3_wgrad_halo_kernel(N, H, W, Ci, Co, slab, pp, monkeypatch):
     gw2 = gw0.clone()
     CV.conv_wgrad_native(dy, x, g, gw2)
     close(gw, gw2, rtol=1e-3, atol=1e-2, what="wgrad3 halo vs gathered GEMM")
+
+
+@pytest.mark.parametrize("N,H", [(40, 56), (3, 56), (160, 32)])
+def test_conv3x3_c64_resident_filter_kernel(N, H, monkeypatch):
+    """64 -> 64 channel 3x3 stride-1 convolution on the resident-filter ping-pong kernel (conv3x3.hip,
+    conv3x3_c64_pp_kernel) vs fp32 PyTorch: the forward with bias + ReLU + fused BN statistics, and the
+    data-gradient (run as a forward conv through the flipped filter) with the fused mode-2 BN-backward
+    reduce.  N = 40 at 56x56 gives 3 pixel tiles per workgroup (both halves of the ping-pong), N = 3 one."""
+    from distributeddeeplearningspark_amd.ops import conv as CV
+    from distributeddeeplearningspark_amd.ops.norm import SHARDS
+
+    monkeypatch.setattr(CV, "_C64PP", True)
+    C = 64
+    g = CV.geometry(N, H, H, C, C, 3, 3, (1, 1), (1, 1), (1, 1))
+    assert CV.halo3_ok(g)
+    x = rnd(N, H, H, C, seed=5)
+    w = rnd(C, 3, 3, C, scale=0.05, seed=6)
+    b = torch.randn(C, device=DEV) * 0.1
+    st = torch.zeros((32, 2, C), dtype=torch.float32, device=DEV)
+    y = CV.conv_fwd_native(x, w, g, bias=b, relu=True, stats=st)
+    ref = CV.conv_ref(x.float(), w.float(), b, (1, 1), (1, 1), (1, 1), relu=True)
+    close(y, ref, what="c64 conv")
+    yf = y.float().reshape(-1, C)
+    close(st.sum(0)[0], yf.sum(0), rtol=1e-3, atol=1e-1, what="c64 stats sum")
+    close(st.sum(0)[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-1, what="c64 stats sumsq")
+    # data-gradient with the fused BN-backward reduce (mode 2)
+    gen = torch.Generator().manual_seed(H)
+    dy = torch.randn(N, H, H, C, generator=gen).to(DEV, torch.bfloat16)
+    xb = torch.randn(N, H, H, C, generator=gen).to(DEV, torch.bfloat16)
+    mean = torch.randn(C, generator=gen).to(DEV) * 0.1
+    scale = (torch.rand(C, generator=gen) + 0.5).to(DEV)
+    shift = torch.randn(C, generator=gen).to(DEV) * 0.5
+    ws = torch.zeros((SHARDS, 2, C), dtype=torch.float32, device=DEV)
+    bnr = {"x": xb, "scale": scale, "shift": shift, "mean": mean, "ws": ws}
+    dx = CV.conv_dgrad_native(dy, w, g, bnr=bnr)
+    assert bnr.get("done")
+    dref = torch.nn.grad.conv2d_input((N, C, H, H), w.float().cpu().permute(0, 3, 1, 2),
+                                      dy.float().cpu().permute(0, 3, 1, 2), stride=1, padding=1).permute(0, 2, 3, 1)
+    close(dx, dref, what="c64 dgrad")
+    keep = (xb.float() * scale + shift > 0).cpu().reshape(-1, C)
+    s1, s2 = _bnr_reference(dx, xb, mean, keep)
+    got = ws.double().cpu().sum(0)
+    close(got[0], s1, rtol=1e-4, atol=1e-2 * s1.abs().mean().item(), what="c64 sum d")
+    close(got[1], s2, rtol=1e-4, atol=1e-2 * s2.abs().mean().item(), what="c64 sum d (x - mean)")
