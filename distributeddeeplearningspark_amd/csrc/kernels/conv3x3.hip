@@ -481,36 +481,35 @@ __device__ __forceinline__ void wgrad_tile_mma(f32x4 (&acc)[9][2][2], const char
     return __builtin_bit_cast(bf16x8, r);
   };
   constexpr int JS = 2 * SC * 16;  // next 16-channel fragment: two chunks on
-  int hb1 = hbt[k1], hb2 = hbt[k1 + 4];
-  int nhb1 = hbt[(KT > 1 ? 32 : 0) + k1], nhb2 = hbt[(KT > 1 ? 32 : 0) + k1 + 4];
-  bf16x8 af[2], bf[2];
-  af[0] = tr2(dyl + ao[0][0], dyl + ao[0][1]);
-  af[1] = tr2(dyl + ao[1][0], dyl + ao[1][1]);
-  {
-    const char* b1 = halo + boff + hb1 * 16;
-    const char* b2 = halo + boff + hb2 * 16;
+  auto bload = [&](int r1, int r2, int tap, bf16x8 (&bf)[2]) {
+    const int toff = ((tap / 3) * WW + (tap % 3)) * 16;
+    const char* b1 = halo + boff + r1 * 16 + toff;
+    const char* b2 = halo + boff + r2 * 16 + toff;
     bf[0] = tr2(b1, b2);
     bf[1] = tr2(b1 + JS, b2 + JS);
-  }
+  };
+  // B fragments run TWO taps ahead of the MFMAs (a tap is only 4 MFMAs = 64 cycles, less than the
+  // transposed reads' latency): slot t % 3 holds tap t, and 9 % 3 == 0 keeps the slots aligned across
+  // steps; the next step's A fragments are read at tap 7
+  int hb1 = hbt[k1], hb2 = hbt[k1 + 4];
+  const int k1n = (KT > 1 ? 32 : 0) + k1;
+  int nhb1 = hbt[k1n], nhb2 = hbt[k1n + 4];
+  bf16x8 af[2], bs[3][2];
+  af[0] = tr2(dyl + ao[0][0], dyl + ao[0][1]);
+  af[1] = tr2(dyl + ao[1][0], dyl + ao[1][1]);
+  bload(hb1, hb2, 0, bs[0]);
+  bload(hb1, hb2, 1, bs[1]);
 #pragma unroll 1
   for (int kk = 0; kk < KT; ++kk) {
-    const char* b1 = halo + boff + hb1 * 16;
-    const char* b2 = halo + boff + hb2 * 16;
     const int kn = kk + 1 < KT ? kk + 1 : kk;  // clamped: the last step re-reads its own rows
     const int kn2 = kk + 2 < KT ? kk + 2 : KT - 1;
+    const int nnhb1 = hbt[kn2 * 32 + k1], nnhb2 = hbt[kn2 * 32 + k1 + 4];
     bf16x8 an[2];
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
-      bf16x8 bn[2];
-      if (tap < 8) {
-        const int toff = (((tap + 1) / 3) * WW + ((tap + 1) % 3)) * 16;
-        bn[0] = tr2(b1 + toff, b2 + toff);
-        bn[1] = tr2(b1 + toff + JS, b2 + toff + JS);
-      } else {
-        const char* n1 = halo + boff + nhb1 * 16;
-        const char* n2 = halo + boff + nhb2 * 16;
-        bn[0] = tr2(n1, n2);
-        bn[1] = tr2(n1 + JS, n2 + JS);
+      if (tap + 2 <= 8) bload(hb1, hb2, tap + 2, bs[(tap + 2) % 3]);
+      else bload(nhb1, nhb2, tap - 7, bs[(tap + 2) % 3]);
+      if (tap == 7) {
         const char* ab = dyl + kn * 4096;
         an[0] = tr2(ab + ao[0][0], ab + ao[0][1]);
         an[1] = tr2(ab + ao[1][0], ab + ao[1][1]);
@@ -518,17 +517,15 @@ __device__ __forceinline__ void wgrad_tile_mma(f32x4 (&acc)[9][2][2], const char
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[tap][i][j] = mfma16x16x32(af[i], bf[j], acc[tap][i][j]);
+        for (int j = 0; j < 2; ++j) acc[tap][i][j] = mfma16x16x32(af[i], bs[tap % 3][j], acc[tap][i][j]);
       __builtin_amdgcn_sched_barrier(0);
-      bf[0] = bn[0];
-      bf[1] = bn[1];
     }
     af[0] = an[0];
     af[1] = an[1];
     hb1 = nhb1;
     hb2 = nhb2;
-    nhb1 = hbt[kn2 * 32 + k1];
-    nhb2 = hbt[kn2 * 32 + k1 + 4];
+    nhb1 = nnhb1;
+    nhb2 = nnhb2;
   }
 }
 
