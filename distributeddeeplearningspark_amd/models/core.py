@@ -555,6 +555,16 @@ class Sequential(Model):
                 break
             relu_next = isinstance(nxt, Activation) and nxt.activation_name == "relu"
             if isinstance(l, Conv2D) and l.activation_name == "linear" and isinstance(nxt, BatchNormalization):
+                relu2 = isinstance(nxt2, Activation) and nxt2.activation_name == "relu"
+                unit = self._convbn_unit(l, nxt, x) if (training and use_native(x)) else None
+                if unit is not None:
+                    # conv + BN (+ReLU) as ONE autograd node with a hand-scheduled backward
+                    # (ops/fused_blocks.py: half the Python / autograd work per layer)
+                    from ..ops.fused_blocks import convbn_relu
+
+                    x = convbn_relu(unit, x, l.kernel.data, relu=relu2)
+                    i += 3 if relu2 else 2
+                    continue
                 stats = new_stats_workspace(l.filters, x.device) if (training and use_native(x)) else None
                 y = l.call(x, training, stats=stats)
                 relu2 = isinstance(nxt2, Activation) and nxt2.activation_name == "relu"
@@ -572,6 +582,26 @@ class Sequential(Model):
             x = l.call(x, training)
             i += 1
         return x
+
+    def _convbn_unit(self, conv, bn, x):
+        """The (conv, BN) pair as a ``fused_blocks`` unit when the fused training node applies: no conv
+        bias, stride 1 or an even split of "same" padding (no explicit pre-pad), dilation 1, both
+        trainable; ``DDL_FUSE_CONVBN=0`` keeps the two-node path."""
+        import os
+
+        if os.environ.get("DDL_FUSE_CONVBN", "1") == "0" or conv.bias is not None or conv.dilation_rate != (1, 1):
+            return None
+        if not (conv.trainable and bn.trainable and bn.gamma is not None and bn.beta is not None):
+            return None
+        (ph, pw), extra = conv._pads(x.shape[1], x.shape[2])
+        if extra is not None:
+            return None
+        cache = self.__dict__.setdefault("_convbn_units", {})
+        key = (id(conv), ph, pw)
+        u = cache.get(key)
+        if u is None:
+            u = cache[key] = _ConvBNUnit(conv, bn, (ph, pw))
+        return u
 
     def get_config(self):
         return {"name": self.name, "layers": [{"class_name": type(l).__name__, "config": l.get_config()}
@@ -596,3 +626,24 @@ def model_from_json(s: str) -> Model:
         m.input_mean = None if norm.get("mean") is None else tuple(norm["mean"])
         m.input_std = None if norm.get("std") is None else tuple(norm["std"])
     return m
+
+
+class _PaddedConv:
+    """View of a Conv2D layer with its padding resolved to a (ph, pw) tuple (every other attribute,
+    the gradient hook included, read through to the layer at use time)."""
+
+    def __init__(self, conv, pads):
+        self.__dict__["_conv"] = conv
+        self.__dict__["padding"] = pads
+
+    def __getattr__(self, name):
+        return getattr(self.__dict__["_conv"], name)
+
+
+class _ConvBNUnit:
+    """(conv, BN) pair in the shape ``ops.fused_blocks`` expects of a ResNet ConvBN unit."""
+
+    def __init__(self, conv, bn, pads):
+        self.conv = _PaddedConv(conv, pads)
+        self.bn = bn
+

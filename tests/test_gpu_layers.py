@@ -268,3 +268,45 @@ def test_bert_tiny_predict_runs_only_hip_kernels():
                            m.embeddings.word.master.cpu(), hd.dec_b.master.cpu(), m.config.layer_norm_eps, 1100)
     err = (lg.reshape(-1, 1100).cpu() - ref).abs().max().item()
     assert err < 0.05 * ref.abs().max().item() + 0.05, err
+
+
+def test_sequential_fused_convbn_matches_two_node_path(monkeypatch):
+    """Sequential Conv2D -> BatchNormalization -> ReLU trains through ONE fused autograd node
+    (ops/fused_blocks.py, models/core.py:_convbn_unit) — VGG-style blocks incl. a 3-channel input, a
+    stride-2 "same" conv (asymmetric padding: keeps the two-node path) and a 2x2 pool: same loss,
+    gradients and BN running statistics as the two-node path (DDL_FUSE_CONVBN=0)."""
+    from distributeddeeplearningspark_amd.models import layers as L
+    from distributeddeeplearningspark_amd.models.core import Sequential
+
+    def build():
+        torch.manual_seed(0)
+        m = Sequential([L.Conv2D(64, (3, 3), input_shape=(16, 16, 3), padding="same", use_bias=False),
+                        L.BatchNormalization(momentum=0.9, epsilon=1e-5), L.Activation("relu"),
+                        L.Conv2D(64, (3, 3), padding="same", use_bias=False), L.BatchNormalization(), L.Activation("relu"),
+                        L.MaxPooling2D((2, 2)),
+                        L.Conv2D(128, (3, 3), strides=2, padding="same", use_bias=False), L.BatchNormalization(),
+                        L.Activation("relu"),
+                        L.Conv2D(128, (3, 3), padding="same", use_bias=False), L.BatchNormalization(),
+                        L.Flatten(), L.Dense(10, activation="softmax")])
+        m.compile("sgd", "sparse_categorical_crossentropy")
+        m.place(DEV, seed=0)
+        return m
+
+    g = torch.Generator().manual_seed(1)
+    x, y = torch.randn(8, 16, 16, 3, generator=g), torch.randint(0, 10, (8,), generator=g)
+    res = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("DDL_FUSE_CONVBN", fuse)
+        m = build()
+        xd, yd = m.to_input(x), m.to_target(y)
+        loss = float(m.backward_step(xd, yd))
+        stats = [l._states["moving_mean"].float().cpu().clone() for l in m.layers if isinstance(l, L.BatchNormalization)]
+        res[fuse] = (loss, m.arena.grad.detach().float().cpu().clone(), stats)
+        if fuse == "1":
+            assert len(m.__dict__.get("_convbn_units", {})) == 3  # the stride-2 conv keeps two nodes
+    (l1, g1, s1), (l0, g0, s0) = res["1"], res["0"]
+    assert abs(l1 - l0) < 1e-3 * abs(l0), (l1, l0)
+    rel = ((g1 - g0).norm() / g0.norm()).item()
+    assert rel < 1e-2, rel
+    for a, b in zip(s1, s0):
+        assert torch.allclose(a, b, rtol=1e-3, atol=1e-4)
