@@ -120,6 +120,10 @@ struct GemmParams {
   const float* a_shift;
   const float* b_scale;
   const float* b_shift;
+  // tile raster of the LDS-DMA GEMM kernel: > 1 walks groups of group_m M-tiles across all N-tiles
+  // (M fastest inside a group) so the tiles resident on one XCD share fewer A rows and B columns
+  // (set by launch_gemm_bf16 from DDL_GEMM_GROUP_M; 0 = row-major over the tiles)
+  int group_m;
 };
 
 enum Activation : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_GELU_BWD = 3 };

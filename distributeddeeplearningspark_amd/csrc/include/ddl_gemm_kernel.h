@@ -673,6 +673,25 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
   }
 }
 
+// Output tile of logical block bid: row-major over the tiles, or (GemmParams::group_m > 1) groups of
+// group_m M-tiles walked M-fastest across all N-tiles, so the tiles resident together on one XCD share
+// fewer A rows and B columns in its L2.
+template <int BM>
+__device__ __forceinline__ void tile_raster(const GemmParams& p, int bid, int tiles_n, int& tm, int& tn) {
+  if (p.group_m > 1) {
+    const int tiles_m = (p.M + BM - 1) / BM;
+    const int per = p.group_m * tiles_n;
+    const int grp = bid / per, first = grp * p.group_m;
+    const int gm = min(tiles_m - first, p.group_m);
+    const int r = bid - grp * per;
+    tm = first + r % gm;
+    tn = r / gm;
+  } else {
+    tm = bid / tiles_n;
+    tn = bid - tm * tiles_n;
+  }
+}
+
 template <int BM, int BN, int AMODE, int BMODE, int EPI>
 __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams p) {
   constexpr int WTM = BM / 2, WTN = BN / 2;
@@ -690,7 +709,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams
   const int tiles_n = (p.N + BN - 1) / BN;
   int bid, split;
   grid_tile(bid, split);
-  const int tm = bid / tiles_n, tn = bid - tm * tiles_n;
+  int tm, tn;
+  tile_raster<BM>(p, bid, tiles_n, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const int kbeg = split * p.k_split;
   const int kend = min(p.K, kbeg + p.k_split);
@@ -781,7 +801,8 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
   const int tiles_n = (p.N + BN - 1) / BN;
   int bid, split;
   grid_tile(bid, split);
-  const int tm = bid / tiles_n, tn = bid - tm * tiles_n;
+  int tm, tn;
+  tile_raster<BM>(p, bid, tiles_n, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const int kbeg = split * p.k_split;
   const int kend = min(p.K, kbeg + p.k_split);

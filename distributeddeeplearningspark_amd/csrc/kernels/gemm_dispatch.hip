@@ -1,6 +1,7 @@
 // Host-side dispatch of the implicit-GEMM kernel family.
 #include "ddl_gemm.h"
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 namespace ddl {
 int launch_gemm_plain_akc(const GemmParams& p, int epi, int tile, hipStream_t s);
 int launch_gemm_plain_arc(const GemmParams& p, int epi, int tile, hipStream_t s);
@@ -9,9 +10,18 @@ int launch_gemm256(const GemmParams& p, int epi, hipStream_t s);
 int launch_gemm_stream(const GemmParams& p, int epi, hipStream_t s);
 int launch_conv3x3(const GemmParams& p, int epi, hipStream_t s);
 
-int launch_gemm_bf16(const GemmParams& p, int epi, int tile, void* stream) {
+int launch_gemm_bf16(const GemmParams& p_in, int epi, int tile, void* stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (p.M <= 0 || p.N <= 0) return 0;
+  if (p_in.M <= 0 || p_in.N <= 0) return 0;
+  // DDL_GEMM_GROUP_M: grouped tile raster (GemmParams::group_m; 0 = row-major).  8 measured +1-2 % on
+  // BERT-base (835K vs 817-824K tok/s), ResNet-50 neutral; 128-tile GEMM 8192^3 810 -> 1089 TF/s
+  // (profiles/r3/ab/gemm_group_m.jsonl, profiles/r3/gemm_group_m_micro.txt)
+  static const int group_m = [] {
+    const char* e = getenv("DDL_GEMM_GROUP_M");
+    return e ? atoi(e) : 8;
+  }();
+  GemmParams p = p_in;
+  p.group_m = group_m;
   if (p.bnr_x && tile != kTileStream &&  // fused BN-backward reduce on the other kernels: EPI_BF16_BNR
       (tile == kTile256 || epi != EPI_BF16 || p.om.enabled || p.resid || p.aux || p.drop_thresh || p.bias || p.relu || p.N % 4 || p.ldc % 8 ||
        !(p.a_mode == OP_KC || p.a_mode == OP_KC_GATHER) || (p.a_mode == OP_KC_GATHER && p.b_mode != OP_KC)))
