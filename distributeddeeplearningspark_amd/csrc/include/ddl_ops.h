@@ -105,6 +105,7 @@ struct AttnParams {
   const uint16_t* dout; long lddo;  // dO
   float* dvec;                      // [B][H][S] scratch: rowsum(dO * O)
   uint16_t* dqkv; long lddqkv;      // gradient of the qkv buffer (same column layout)
+  int xcd_remap;                    // set by the launchers (DDL_ATTN_XCD): blocks of one (b, h) share an XCD
 };
 int attn_fwd(const AttnParams& p, hipStream_t s);
 int attn_bwd(const AttnParams& p, hipStream_t s);

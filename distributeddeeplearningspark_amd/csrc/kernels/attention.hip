@@ -103,18 +103,38 @@ __device__ __forceinline__ bool keep_bits(uint32_t h, int j, uint32_t th16) {
 }
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// Block -> (query/key block, head, sequence).  With xcd_remap the linear block id goes through the
+// XCD-aware bijection first, so the S / 128 blocks of one (b, h) — which all stream the same K / V (or
+// Q / dO) tiles — are dealt to ONE XCD and share its L2; in grid order they land on S / 128 different XCDs.
+__device__ __forceinline__ void attn_block(const AttnParams& p, int& xb, int& h, int& b) {
+  if (p.xcd_remap) {
+    const int nx = gridDim.x, ny = gridDim.y;
+    const int lin = xcd_remap(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), nx * ny * gridDim.z);
+    xb = lin % nx;
+    const int t = lin / nx;
+    h = t % ny;
+    b = t / ny;
+  } else {
+    xb = blockIdx.x;
+    h = blockIdx.y;
+    b = blockIdx.z;
+  }
+}
+
 // ================================================================ forward
 template <int MINB>
 __global__ __launch_bounds__(THREADS, MINB) void attn_fwd_kernel(const AttnParams p) {
   __shared__ __attribute__((aligned(16))) char lds[2][2][TILE_BYTES];
-  const int h = blockIdx.y, b = blockIdx.z, S = p.S;
+  int xb, h, b;
+  attn_block(p, xb, h, b);
+  const int S = p.S;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
   const long tok0 = (long)b * S;
   const bf16_t* Q = p.qkv + tok0 * p.ld + p.q_off + h * HD;
   const bf16_t* K = p.qkv + tok0 * p.ld + p.k_off + h * HD;
   const bf16_t* V = p.qkv + tok0 * p.ld + p.v_off + h * HD;
   const int len = p.lens ? min(max(p.lens[b], 0), S) : S;
-  const int q0 = blockIdx.x * BLOCK_ROWS + w * 32;
+  const int q0 = xb * BLOCK_ROWS + w * 32;
   const int bh = b * p.H + h;
 
   bf16x8 qf[2][2];
@@ -285,7 +305,9 @@ __global__ __launch_bounds__(THREADS, MINB) void attn_bwd_dkdv_kernel(const Attn
   __shared__ __attribute__((aligned(16))) float s_lse[2][TQ];
   __shared__ __attribute__((aligned(16))) float s_d[2][TQ];
   __shared__ __attribute__((aligned(16))) uint32_t s_rk[2][TQ];
-  const int h = blockIdx.y, b = blockIdx.z, S = p.S;
+  int xb, h, b;
+  attn_block(p, xb, h, b);
+  const int S = p.S;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
   const long tok0 = (long)b * S;
   const int bh = b * p.H + h;
@@ -296,7 +318,7 @@ __global__ __launch_bounds__(THREADS, MINB) void attn_bwd_dkdv_kernel(const Attn
   const float* lse = p.lse + (long)bh * S;
   const float* dv = p.dvec + (long)bh * S;
   const int len = p.lens ? min(max(p.lens[b], 0), S) : S;
-  const int k0 = blockIdx.x * BLOCK_ROWS + w * 32;
+  const int k0 = xb * BLOCK_ROWS + w * 32;
   bf16_t* dK = p.dqkv + tok0 * p.lddqkv + p.k_off + h * HD;
   bf16_t* dV = p.dqkv + tok0 * p.lddqkv + p.v_off + h * HD;
 
@@ -316,7 +338,7 @@ __global__ __launch_bounds__(THREADS, MINB) void attn_bwd_dkdv_kernel(const Attn
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) adv[jt][dt] = adk[jt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const bool any_key = blockIdx.x * BLOCK_ROWS < len;  // block-uniform
+  const bool any_key = xb * BLOCK_ROWS < len;  // block-uniform
   const int nqt = any_key ? S / TQ : 0;
   float r_lse = 0.f, r_d = 0.f;
   uint32_t r_rk = 0u;
@@ -436,7 +458,9 @@ __global__ __launch_bounds__(THREADS, MINB) void attn_bwd_dkdv_kernel(const Attn
 template <int MINB>
 __global__ __launch_bounds__(THREADS, MINB) void attn_bwd_dq_kernel(const AttnParams p) {
   __shared__ __attribute__((aligned(16))) char lds[2][2][TILE_BYTES];  // [buf][K, V]
-  const int h = blockIdx.y, b = blockIdx.z, S = p.S;
+  int xb, h, b;
+  attn_block(p, xb, h, b);
+  const int S = p.S;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
   const long tok0 = (long)b * S;
   const int bh = b * p.H + h;
@@ -445,7 +469,7 @@ __global__ __launch_bounds__(THREADS, MINB) void attn_bwd_dq_kernel(const AttnPa
   const bf16_t* V = p.qkv + tok0 * p.ld + p.v_off + h * HD;
   const bf16_t* dO = p.dout + tok0 * p.lddo + h * HD;
   const int len = p.lens ? min(max(p.lens[b], 0), S) : S;
-  const int q0 = blockIdx.x * BLOCK_ROWS + w * 32;
+  const int q0 = xb * BLOCK_ROWS + w * 32;
   bf16_t* dQ = p.dqkv + tok0 * p.lddqkv + p.q_off + h * HD;
 
   bf16x8 qf[2][2], df[2][2];
@@ -553,8 +577,15 @@ __global__ __launch_bounds__(THREADS, MINB) void attn_bwd_dq_kernel(const AttnPa
 
 }  // namespace
 
-int attn_fwd(const AttnParams& p, hipStream_t s) {
-  if (p.B <= 0) return 0;
+static int attn_xcd() {
+  static const int v = getenv("DDL_ATTN_XCD") ? atoi(getenv("DDL_ATTN_XCD")) : 1;
+  return v;
+}
+
+int attn_fwd(const AttnParams& p_in, hipStream_t s) {
+  if (p_in.B <= 0) return 0;
+  AttnParams p = p_in;
+  p.xcd_remap = attn_xcd();
   static const int occ = getenv("DDL_ATTN_FWD_OCC") ? atoi(getenv("DDL_ATTN_FWD_OCC")) : 2;
   if (occ == 3)
     hipLaunchKernelGGL(attn_fwd_kernel<3>, dim3(p.S / BLOCK_ROWS, p.H, p.B), dim3(THREADS), 0, s, p);
@@ -563,8 +594,10 @@ int attn_fwd(const AttnParams& p, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-int attn_bwd(const AttnParams& p, hipStream_t s) {
-  if (p.B <= 0) return 0;
+int attn_bwd(const AttnParams& p_in, hipStream_t s) {
+  if (p_in.B <= 0) return 0;
+  AttnParams p = p_in;
+  p.xcd_remap = attn_xcd();
   const long rows = (long)p.B * p.S * p.H;
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s, p, rows);
   static const int dkdv_occ = getenv("DDL_ATTN_DKDV_OCC") ? atoi(getenv("DDL_ATTN_DKDV_OCC")) : 2;
