@@ -304,7 +304,8 @@ __device__ __forceinline__ void store_mask_bits(uint8_t* __restrict__ mask, long
 
 // Streaming sweeps use the column-fixed mapping of ColGeom: a lane keeps ONE 8-channel
 // vector (per-channel parameters live in registers, no per-element index division) and
-// walks rows; two rows are in flight per lane.
+// walks rows; R rows are in flight per lane (all R loads issued before the first use).
+template <int R>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const uint4* __restrict__ x, const float* __restrict__ scale,
                                                         const float* __restrict__ shift, const uint4* __restrict__ res,
                                                         uint4* __restrict__ y, uint8_t* __restrict__ mask, long M,
@@ -323,22 +324,22 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint4* __restrict__
     load8f(res_shift + g.cv * 8, rsh);
   }
   const long step = (long)gridDim.x * g.RT;
-  for (long r = (long)blockIdx.x * g.RT + g.rt; r < M; r += 2 * step) {
-    const bool two = r + step < M;
-    const long i0 = r * g.CV + g.cv, i1 = (r + step) * g.CV + g.cv;
-    const uint4 x0 = x[i0];
-    const uint4 x1 = two ? x[i1] : x0;
-    uint4 r0 = x0, r1 = x0;
-    if (res) {
-      r0 = res[i0];
-      r1 = two ? res[i1] : r0;
-    }
-    float f[8], q[8];
+  for (long r = (long)blockIdx.x * g.RT + g.rt; r < M; r += R * step) {
+    long ix[R];
+    uint4 xv[R], rv[R];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if (h == 1 && !two) break;
-      unpack8(h ? x1 : x0, f);
-      if (res) unpack8(h ? r1 : r0, q);
+    for (int h = 0; h < R; ++h) {
+      const bool ok = r + h * step < M;  // row h of this lane exists (row 0 always does)
+      ix[h] = (ok ? r + h * step : r) * g.CV + g.cv;
+      xv[h] = x[ix[h]];
+      if (res) rv[h] = res[ix[h]];
+    }
+#pragma unroll
+    for (int h = 0; h < R; ++h) {
+      if (h > 0 && r + h * step >= M) break;
+      float f[8], q[8];
+      unpack8(xv[h], f);
+      if (res) unpack8(rv[h], q);
       uint32_t bits = 0;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -348,25 +349,36 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint4* __restrict__
         if (relu) o = fmaxf(o, 0.f);
         f[i] = o;
       }
-      y[h ? i1 : i0] = pack8(f);
-      if (mask) store_mask_bits(mask, h ? i1 : i0, bits, g.CT * g.RT == 256);
+      y[ix[h]] = pack8(f);
+      if (mask) store_mask_bits(mask, ix[h], bits, g.CT * g.RT == 256);
     }
   }
 }
 
-static dim3 stream_grid(long M, int C) {
+static dim3 stream_grid(long M, int C, int rows = 2) {
   const int CV = C >> 3, CT = CV < 256 ? CV : 256, RT = 256 / CT;
   const int gy = (CV + CT - 1) / CT;
-  long gx = (M + 2 * RT - 1) / (2 * RT);
+  long gx = (M + rows * RT - 1) / (rows * RT);
   const long cap = 4096 / gy > 1 ? 4096 / gy : 1;
   if (gx > cap) gx = cap;
   return dim3((unsigned)(gx > 0 ? gx : 1), (unsigned)gy);
 }
 
+// rows in flight per lane of the apply / dx sweeps: DDL_BN_ROWS = 2 (default) or 4 (A/B knob, read per
+// launch so a test can switch it)
+static int bn_rows() {
+  const char* e = getenv("DDL_BN_ROWS");
+  return e && atoi(e) == 4 ? 4 : 2;
+}
+
 int bn_apply(const void* x, const float* scale, const float* shift, const void* resid, void* y, void* mask, long M,
              int C, int relu, hipStream_t s, const float* res_scale, const float* res_shift) {
-  hipLaunchKernelGGL(bn_apply_kernel, stream_grid(M, C), dim3(256), 0, s, (const uint4*)x, scale, shift,
-                     (const uint4*)resid, (uint4*)y, (uint8_t*)mask, M, C, relu, res_scale, res_shift);
+  if (bn_rows() == 4)
+    hipLaunchKernelGGL(bn_apply_kernel<4>, stream_grid(M, C, 4), dim3(256), 0, s, (const uint4*)x, scale, shift,
+                       (const uint4*)resid, (uint4*)y, (uint8_t*)mask, M, C, relu, res_scale, res_shift);
+  else
+    hipLaunchKernelGGL(bn_apply_kernel<2>, stream_grid(M, C), dim3(256), 0, s, (const uint4*)x, scale, shift,
+                       (const uint4*)resid, (uint4*)y, (uint8_t*)mask, M, C, relu, res_scale, res_shift);
   return (int)hipGetLastError();
 }
 
@@ -493,6 +505,7 @@ int bn_bwd_finalize(const float* ws, int S, long M, int C, const float* gamma, c
   return (int)hipGetLastError();
 }
 
+template <int R>
 __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const uint4* __restrict__ dy, const uint4* __restrict__ x,
                                                          const uint4* __restrict__ y, const float* __restrict__ scale,
                                                          const float* __restrict__ shift,
@@ -513,32 +526,41 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const uint4* __restrict_
     for (int i = 0; i < 8; ++i) sc[i] = sh[i] = 0.f;
   }
   const long step = (long)gridDim.x * g.RT;
-  for (long r = (long)blockIdx.x * g.RT + g.rt; r < M; r += 2 * step) {
-    const bool two = r + step < M;
-    const long i0 = r * g.CV + g.cv, i1 = (r + step) * g.CV + g.cv;
-    const uint4 d0 = dy[i0], x0 = x[i0];
-    const uint4 d1 = two ? dy[i1] : d0, x1 = two ? x[i1] : x0;
-    const uint32_t m0 = mask_byte(y, i0, mode), m1 = two ? mask_byte(y, i1, mode) : m0;
+  for (long r = (long)blockIdx.x * g.RT + g.rt; r < M; r += R * step) {
+    long ix[R];
+    uint4 dv[R], xv[R];
+    uint32_t mb[R];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if (h == 1 && !two) break;
-      const long idx = h ? i1 : i0;
-      float d[8], xv[8], o[8];
-      unpack8(h ? d1 : d0, d);
-      unpack8(h ? x1 : x0, xv);
-      relu_mask(d, xv, y, idx, sc, sh, mode, h ? m1 : m0);
-      if (dres) dres[idx] = pack8(d);
+    for (int h = 0; h < R; ++h) {
+      const bool ok = r + h * step < M;
+      ix[h] = (ok ? r + h * step : r) * g.CV + g.cv;
+      dv[h] = dy[ix[h]];
+      xv[h] = x[ix[h]];
+      mb[h] = mask_byte(y, ix[h], mode);
+    }
 #pragma unroll
-      for (int i = 0; i < 8; ++i) o[i] = A[i] * d[i] + B[i] * xv[i] + K[i];
-      dx[idx] = pack8(o);
+    for (int h = 0; h < R; ++h) {
+      if (h > 0 && r + h * step >= M) break;
+      float d[8], xf[8], o[8];
+      unpack8(dv[h], d);
+      unpack8(xv[h], xf);
+      relu_mask(d, xf, y, ix[h], sc, sh, mode, mb[h]);
+      if (dres) dres[ix[h]] = pack8(d);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = A[i] * d[i] + B[i] * xf[i] + K[i];
+      dx[ix[h]] = pack8(o);
     }
   }
 }
 
 int bn_bwd_dx(const void* dy, const void* x, const void* y, const float* scale, const float* shift, const float* coef,
               void* dx, void* dres, long M, int C, int mode, hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_dx_kernel, stream_grid(M, C), dim3(256), 0, s, (const uint4*)dy, (const uint4*)x,
-                     (const uint4*)y, scale, shift, coef, (uint4*)dx, (uint4*)dres, M, C, mode);
+  if (bn_rows() == 4)
+    hipLaunchKernelGGL(bn_bwd_dx_kernel<4>, stream_grid(M, C, 4), dim3(256), 0, s, (const uint4*)dy,
+                       (const uint4*)x, (const uint4*)y, scale, shift, coef, (uint4*)dx, (uint4*)dres, M, C, mode);
+  else
+    hipLaunchKernelGGL(bn_bwd_dx_kernel<2>, stream_grid(M, C), dim3(256), 0, s, (const uint4*)dy, (const uint4*)x,
+                       (const uint4*)y, scale, shift, coef, (uint4*)dx, (uint4*)dres, M, C, mode);
   return (int)hipGetLastError();
 }
 

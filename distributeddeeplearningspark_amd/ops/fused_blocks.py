@@ -73,10 +73,8 @@ def _bn_forward(layer_bn, yc, stats, resid, relu, training, mask=None, apply=Tru
     gamma = None if bn.gamma is None else bn.gamma.master
     beta = None if bn.beta is None else bn.beta.master
     rm, rv = bn._states["moving_mean"], bn._states["moving_variance"]
-    scale = torch.empty(Cc, dtype=torch.float32, device=dev)
-    shift = torch.empty(Cc, dtype=torch.float32, device=dev)
-    mean = torch.empty(Cc, dtype=torch.float32, device=dev)
-    invstd = torch.empty(Cc, dtype=torch.float32, device=dev)
+    # one allocation for the four per-channel vectors (host cost per BN: VGG-16 runs launch-bound)
+    scale, shift, mean, invstd = torch.empty(4, Cc, dtype=torch.float32, device=dev).unbind(0)
     C().bn_finalize(stats, M, Cc, gamma, beta, bn.epsilon, 1.0 - bn.momentum, rm, rv, mean, invstd, scale, shift)
     if not apply:
         return None, mean, invstd, scale, shift

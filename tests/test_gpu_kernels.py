@@ -282,6 +282,37 @@ def test_bn_apply_dual(Cc):
     assert (bits != ref).float().mean().item() < 1e-3
 
 
+@pytest.mark.parametrize("rows", ["2", "4"])
+@pytest.mark.parametrize("M,Cc", [(300007, 64), (100003, 512), (4099, 2048)])
+def test_bn_sweeps_grid_stride(monkeypatch, M, Cc, rows):
+    """bn_apply (residual + bit mask) and bn_bwd_dx (modes 2 and 3, residual-gradient output) on row
+    counts where the capped grid walks several R-row groups per lane with a ragged last group, vs
+    fp32 torch on the same bf16 inputs; both sweep forms (DDL_BN_ROWS: rows in flight per lane)."""
+    monkeypatch.setenv("DDL_BN_ROWS", rows)
+    x = rnd(M, Cc, seed=23)
+    r = rnd(M, Cc, seed=24)
+    dy = rnd(M, Cc, seed=25)
+    s, t = torch.rand(Cc, device=DEV) + 0.5, torch.randn(Cc, device=DEV) * 0.1
+    coef = torch.randn(3 * Cc, device=DEV)
+    A, B, K = coef.view(3, Cc)
+    y = torch.empty_like(x)
+    mask = torch.zeros(-(-x.numel() // 32) * 4, dtype=torch.uint8, device=DEV)
+    _C().bn_apply(x, s, t, r, y, Cc, True, mask)
+    pre = x.float() * s + t + r.float()
+    close(y, torch.relu(pre), rtol=1e-2, atol=1e-2, what="apply")
+    e = torch.arange(x.numel(), device=DEV)
+    bits = (mask.long()[e >> 3] >> (e & 7)) & 1
+    assert (bits != (pre.flatten() > 0).long()).float().mean().item() < 1e-3
+    dx, dres = torch.empty_like(x), torch.empty_like(x)
+    _C().bn_bwd_dx(dy, x, mask, s, t, coef, dx, dres, Cc, 3)
+    d = dy.float() * (bits.view(M, Cc) > 0)
+    close(dres, d, rtol=1e-2, atol=1e-2, what="dx mode 3 dres")
+    close(dx, A * d + B * x.float() + K, rtol=2e-2, atol=2e-2, what="dx mode 3")
+    _C().bn_bwd_dx(dy, x, None, s, t, coef, dx, None, Cc, 2)
+    d = dy.float() * ((x.float() * s + t) > 0)
+    close(dx, A * d + B * x.float() + K, rtol=2e-2, atol=2e-2, what="dx mode 2")
+
+
 # ----------------------------------------------------------------------------- pooling
 @pytest.mark.parametrize("k,s,p,H", [(3, 2, 1, 16), (2, 2, 0, 24), (3, 2, 1, 15)])
 def test_maxpool(k, s, p, H):
