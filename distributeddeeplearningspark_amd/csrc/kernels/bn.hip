@@ -305,7 +305,20 @@ __device__ __forceinline__ void store_mask_bits(uint8_t* __restrict__ mask, long
 // Streaming sweeps use the column-fixed mapping of ColGeom: a lane keeps ONE 8-channel
 // vector (per-channel parameters live in registers, no per-element index division) and
 // walks rows; R rows are in flight per lane (all R loads issued before the first use).
-template <int R>
+// bf16x8 store of the streaming sweeps; NT: nontemporal (streaming cache policy: the output is not
+// kept in L2 / Infinity Cache ahead of the reads of the sweep)
+template <bool NT>
+__device__ __forceinline__ void store16(uint4* __restrict__ p, const uint4 v) {
+  if constexpr (NT) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
+  } else {
+    *p = v;
+  }
+}
+
+template <int R, bool NT>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const uint4* __restrict__ x, const float* __restrict__ scale,
                                                         const float* __restrict__ shift, const uint4* __restrict__ res,
                                                         uint4* __restrict__ y, uint8_t* __restrict__ mask, long M,
@@ -349,7 +362,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint4* __restrict__
         if (relu) o = fmaxf(o, 0.f);
         f[i] = o;
       }
-      y[ix[h]] = pack8(f);
+      store16<NT>(y + ix[h], pack8(f));
       if (mask) store_mask_bits(mask, ix[h], bits, g.CT * g.RT == 256);
     }
   }
@@ -370,15 +383,19 @@ static int bn_rows() {
   const char* e = getenv("DDL_BN_ROWS");
   return e && atoi(e) == 4 ? 4 : 2;
 }
+// DDL_BN_NT=1: nontemporal output stores in those sweeps (A/B knob, read per launch)
+static bool bn_nt() {
+  const char* e = getenv("DDL_BN_NT");
+  return e && atoi(e) == 1;
+}
 
 int bn_apply(const void* x, const float* scale, const float* shift, const void* resid, void* y, void* mask, long M,
              int C, int relu, hipStream_t s, const float* res_scale, const float* res_shift) {
-  if (bn_rows() == 4)
-    hipLaunchKernelGGL(bn_apply_kernel<4>, stream_grid(M, C, 4), dim3(256), 0, s, (const uint4*)x, scale, shift,
-                       (const uint4*)resid, (uint4*)y, (uint8_t*)mask, M, C, relu, res_scale, res_shift);
-  else
-    hipLaunchKernelGGL(bn_apply_kernel<2>, stream_grid(M, C), dim3(256), 0, s, (const uint4*)x, scale, shift,
-                       (const uint4*)resid, (uint4*)y, (uint8_t*)mask, M, C, relu, res_scale, res_shift);
+  const int rows = bn_rows();
+  auto k = rows == 4 ? (bn_nt() ? bn_apply_kernel<4, true> : bn_apply_kernel<4, false>)
+                     : (bn_nt() ? bn_apply_kernel<2, true> : bn_apply_kernel<2, false>);
+  hipLaunchKernelGGL(k, stream_grid(M, C, rows), dim3(256), 0, s, (const uint4*)x, scale, shift, (const uint4*)resid,
+                     (uint4*)y, (uint8_t*)mask, M, C, relu, res_scale, res_shift);
   return (int)hipGetLastError();
 }
 
@@ -505,7 +522,7 @@ int bn_bwd_finalize(const float* ws, int S, long M, int C, const float* gamma, c
   return (int)hipGetLastError();
 }
 
-template <int R>
+template <int R, bool NT>
 __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const uint4* __restrict__ dy, const uint4* __restrict__ x,
                                                          const uint4* __restrict__ y, const float* __restrict__ scale,
                                                          const float* __restrict__ shift,
@@ -545,22 +562,21 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const uint4* __restrict_
       unpack8(dv[h], d);
       unpack8(xv[h], xf);
       relu_mask(d, xf, y, ix[h], sc, sh, mode, mb[h]);
-      if (dres) dres[ix[h]] = pack8(d);
+      if (dres) store16<NT>(dres + ix[h], pack8(d));
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] = A[i] * d[i] + B[i] * xf[i] + K[i];
-      dx[ix[h]] = pack8(o);
+      store16<NT>(dx + ix[h], pack8(o));
     }
   }
 }
 
 int bn_bwd_dx(const void* dy, const void* x, const void* y, const float* scale, const float* shift, const float* coef,
               void* dx, void* dres, long M, int C, int mode, hipStream_t s) {
-  if (bn_rows() == 4)
-    hipLaunchKernelGGL(bn_bwd_dx_kernel<4>, stream_grid(M, C, 4), dim3(256), 0, s, (const uint4*)dy,
-                       (const uint4*)x, (const uint4*)y, scale, shift, coef, (uint4*)dx, (uint4*)dres, M, C, mode);
-  else
-    hipLaunchKernelGGL(bn_bwd_dx_kernel<2>, stream_grid(M, C), dim3(256), 0, s, (const uint4*)dy, (const uint4*)x,
-                       (const uint4*)y, scale, shift, coef, (uint4*)dx, (uint4*)dres, M, C, mode);
+  const int rows = bn_rows();
+  auto k = rows == 4 ? (bn_nt() ? bn_bwd_dx_kernel<4, true> : bn_bwd_dx_kernel<4, false>)
+                     : (bn_nt() ? bn_bwd_dx_kernel<2, true> : bn_bwd_dx_kernel<2, false>);
+  hipLaunchKernelGGL(k, stream_grid(M, C, rows), dim3(256), 0, s, (const uint4*)dy, (const uint4*)x, (const uint4*)y,
+                     scale, shift, coef, (uint4*)dx, (uint4*)dres, M, C, mode);
   return (int)hipGetLastError();
 }
 

@@ -282,13 +282,14 @@ def test_bn_apply_dual(Cc):
     assert (bits != ref).float().mean().item() < 1e-3
 
 
-@pytest.mark.parametrize("rows", ["2", "4"])
+@pytest.mark.parametrize("rows", ["2", "4", "4nt"])
 @pytest.mark.parametrize("M,Cc", [(300007, 64), (100003, 512), (4099, 2048)])
 def test_bn_sweeps_grid_stride(monkeypatch, M, Cc, rows):
     """bn_apply (residual + bit mask) and bn_bwd_dx (modes 2 and 3, residual-gradient output) on row
     counts where the capped grid walks several R-row groups per lane with a ragged last group, vs
-    fp32 torch on the same bf16 inputs; both sweep forms (DDL_BN_ROWS: rows in flight per lane)."""
-    monkeypatch.setenv("DDL_BN_ROWS", rows)
+    fp32 torch on the same bf16 inputs; every sweep form (DDL_BN_ROWS: rows in flight per lane, DDL_BN_NT: nontemporal stores)."""
+    monkeypatch.setenv("DDL_BN_ROWS", rows[0])
+    monkeypatch.setenv("DDL_BN_NT", "1" if rows.endswith("nt") else "0")
     x = rnd(M, Cc, seed=23)
     r = rnd(M, Cc, seed=24)
     dy = rnd(M, Cc, seed=25)
