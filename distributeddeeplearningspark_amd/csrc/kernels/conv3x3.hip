@@ -870,14 +870,22 @@ int launch_wgrad_v(const WgradArgs& a, const Conv3Tiling& t, dim3 grid, bool pp,
 }
 
 // Instantiated tilings (halo width WW, 64-row halo groups G, 32-pixel steps KT): the ResNet-50 stages at
-// 224^2 (56, 28, 14 and 7 pixels wide; every one plans 196- or 224-pixel tiles).  Others take the GEMM path.
+// 224^2 (56, 28, 14 and 7 pixels wide; every one plans 196- or 224-pixel tiles) and VGG-16's 8 / 4 / 2
+// pixel blocks.  Others take the GEMM path.
 int wgrad_variant(const Conv3Tiling& t) {
   const int G = (t.hr + 63) / 64, KT = (t.P + 31) / 32;
-  if (KT != 7) return -1;
-  if (t.ww == 58 && G == 6) return 0;
-  if (t.ww == 30 && G == 5) return 1;
-  if (t.ww == 16 && G == 4) return 2;
-  if (t.ww == 9 && G == 6) return 3;
+  if (KT == 7) {
+    if (t.ww == 58 && G == 6) return 0;
+    if (t.ww == 30 && G == 5) return 1;
+    if (t.ww == 16 && G == 4) return 2;
+    if (t.ww == 9 && G == 6) return 3;
+  }
+  // VGG-16 (CIFAR, batch 256) blocks 3-5: 8x8 (3 images per tile), 4x4 (10), 2x2 (24) — whole images
+  // per tile, the last tile partial (its missing images read zero halo rows against zero dy rows).  The
+  // 32x32 / 16x16 blocks (KT = 8, G = 6) need 166 KB for the ping-pong pair: they stay on the GEMM.
+  if (KT == 6 && t.ww == 10 && G == 5) return 4;
+  if (KT == 5 && t.ww == 6 && G == 6) return 5;
+  if (KT == 3 && t.ww == 4 && G == 6) return 6;
   return -1;
 }
 
@@ -888,6 +896,9 @@ int launch_wgrad(const WgradArgs& a, const Conv3Tiling& t, dim3 grid, bool pp, h
     case 1: return launch_wgrad_v<30, 5, 7, SLAB>(a, t, grid, pp, s);
     case 2: return launch_wgrad_v<16, 4, 7, SLAB>(a, t, grid, pp, s);
     case 3: return launch_wgrad_v<9, 6, 7, SLAB>(a, t, grid, pp, s);
+    case 4: return launch_wgrad_v<10, 5, 6, SLAB>(a, t, grid, pp, s);
+    case 5: return launch_wgrad_v<6, 6, 5, SLAB>(a, t, grid, pp, s);
+    case 6: return launch_wgrad_v<4, 6, 3, SLAB>(a, t, grid, pp, s);
     default: return (int)hipErrorInvalidValue;
   }
 }
