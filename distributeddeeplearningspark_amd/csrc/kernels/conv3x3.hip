@@ -171,18 +171,20 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv3x3_halo_kernel(const GemmPar
   gemm_epilogue<FR, RN, EPI>(p, acc, m0 + wm * (16 * FR), n0 + wn0, lane, bid, mend);
 }
 
-Conv3Tiling plan(const GemmParams& p) {
+// max_px: pixels per tile (256 for the forward / data-gradient kernels; 224 for the weight gradient, whose
+// ping-pong pair of 256-pixel tiles would not fit the LDS — the same tilings for every ResNet-50 stage)
+Conv3Tiling plan(const GemmParams& p, int max_px = 256) {
   const ConvGeom& g = p.g;
   Conv3Tiling t{};
   const int H = g.hi, W = g.wi;
   t.w = W;
-  if (H * W <= 256) {
+  if (H * W <= max_px) {
     t.rows = H;
-    t.img = std::max(1, std::min(256 / (H * W), C3_MAX_HALO_ROWS / ((H + 2) * (W + 2))));
+    t.img = std::max(1, std::min(max_px / (H * W), C3_MAX_HALO_ROWS / ((H + 2) * (W + 2))));
   } else {
     t.img = 1;
     t.rows = 0;
-    for (int r = std::min(H, 256 / std::max(W, 1)); r >= 1; --r)
+    for (int r = std::min(H, max_px / std::max(W, 1)); r >= 1; --r)
       if (H % r == 0 && (r + 2) * (W + 2) <= C3_MAX_HALO_ROWS) { t.rows = r; break; }
   }
   t.P = t.img * t.rows * t.w;
@@ -872,6 +874,8 @@ int launch_wgrad_v(const WgradArgs& a, const Conv3Tiling& t, dim3 grid, bool pp,
 // Instantiated tilings (halo width WW, 64-row halo groups G, 32-pixel steps KT): the ResNet-50 stages at
 // 224^2 (56, 28, 14 and 7 pixels wide; every one plans 196- or 224-pixel tiles) and VGG-16's 8 / 4 / 2
 // pixel blocks.  Others take the GEMM path.
+constexpr int kWgradPx = 224;
+
 int wgrad_variant(const Conv3Tiling& t) {
   const int G = (t.hr + 63) / 64, KT = (t.P + 31) / 32;
   if (KT == 7) {
@@ -882,7 +886,10 @@ int wgrad_variant(const Conv3Tiling& t) {
   }
   // VGG-16 (CIFAR, batch 256) blocks 3-5: 8x8 (3 images per tile), 4x4 (10), 2x2 (24) — whole images
   // per tile, the last tile partial (its missing images read zero halo rows against zero dy rows).  The
-  // 32x32 / 16x16 blocks (KT = 8, G = 6) need 166 KB for the ping-pong pair: they stay on the GEMM.
+  // 32x32 / 16x16 blocks take 128-pixel row tiles (kWgradPx: 256-pixel tiles would need 166 KB of LDS for
+  // the ping-pong pair).
+  if (KT == 4 && t.ww == 34 && G == 4) return 7;  // 32x32: 4 rows per tile
+  if (KT == 4 && t.ww == 18 && G == 3) return 8;  // 16x16: 8 rows per tile
   if (KT == 6 && t.ww == 10 && G == 5) return 4;
   if (KT == 5 && t.ww == 6 && G == 6) return 5;
   if (KT == 3 && t.ww == 4 && G == 6) return 6;
@@ -899,6 +906,8 @@ int launch_wgrad(const WgradArgs& a, const Conv3Tiling& t, dim3 grid, bool pp, h
     case 4: return launch_wgrad_v<10, 5, 6, SLAB>(a, t, grid, pp, s);
     case 5: return launch_wgrad_v<6, 6, 5, SLAB>(a, t, grid, pp, s);
     case 6: return launch_wgrad_v<4, 6, 3, SLAB>(a, t, grid, pp, s);
+    case 7: return launch_wgrad_v<34, 4, 4, SLAB>(a, t, grid, pp, s);
+    case 8: return launch_wgrad_v<18, 3, 4, SLAB>(a, t, grid, pp, s);
     default: return (int)hipErrorInvalidValue;
   }
 }
@@ -913,7 +922,7 @@ bool conv3x3_wgrad_ok(int n, int h, int w, int ci, int co) {
   p.g.n = n;
   p.g.hi = h;
   p.g.wi = w;
-  const Conv3Tiling t = plan(p);
+  const Conv3Tiling t = plan(p, kWgradPx);
   return t.rows > 0 && t.P >= 64 && t.P <= 256 && t.hr <= C3_MAX_HALO_ROWS && wgrad_variant(t) >= 0;
 }
 
@@ -923,7 +932,7 @@ void conv3x3_wgrad_plan(int n, int h, int w, int ci, int co, int blocks_per_cu, 
   p.g.n = n;
   p.g.hi = h;
   p.g.wi = w;
-  const Conv3Tiling t = plan(p);
+  const Conv3Tiling t = plan(p, kWgradPx);
   ntiles = t.tiles_img * t.tiles_row;
   const int pairs = (co / 64) * (ci / 64);
   const int want = std::max(1, (blocks_per_cu * cus + pairs - 1) / pairs);
@@ -938,7 +947,7 @@ int launch_conv3x3_wgrad(const bf16_t* dy, const bf16_t* x, float* gw, float* ws
   p.g.n = n;
   p.g.hi = h;
   p.g.wi = w;
-  const Conv3Tiling t = plan(p);
+  const Conv3Tiling t = plan(p, kWgradPx);
   WgradArgs a{dy, x, ws ? ws : gw, n, h, w, ci, co, t.tiles_img * t.tiles_row, tpb};
   const dim3 grid((co / 64) * (ci / 64), splits);
   int rc = ws ? launch_wgrad<true>(a, t, grid, pp, s) : launch_wgrad<false>(a, t, grid, pp, s);

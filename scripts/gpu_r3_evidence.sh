@@ -27,7 +27,7 @@ timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/ev_bench.lo
 grep '^{' gpurun_out/ev_bench.log
 ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/ev_prof -- python3 $R/bench.py --steps 5 --warmup 2 > $R/gpurun_out/ev_prof.log 2>&1 ) || { echo "rocprof failed"; exit 1; }
 f=$(find gpurun_out/ev_prof -name "*kernel_stats.csv" | head -1)
-python scripts/prof_summary.py $f 7 gpurun_out/ev_kstats.csv | head -12
+python scripts/prof_summary.py $f 7 gpurun_out/ev_kstats.csv > gpurun_out/ev_ksum.txt; head -12 gpurun_out/ev_ksum.txt
 for m in bert vgg16; do
   timeout -k 10 300 python bench.py --model $m --steps 20 --warmup 5 > gpurun_out/ev_bench_$m.log 2>&1 || { tail gpurun_out/ev_bench_$m.log; exit 1; }
   grep '^{' gpurun_out/ev_bench_$m.log

@@ -917,12 +917,13 @@ def test_bottleneck_norm_on_load_matches_applied(monkeypatch):
 
 @pytest.mark.parametrize("N,H,W,Ci,Co", [(2, 56, 56, 64, 64), (3, 28, 28, 128, 64), (2, 14, 14, 64, 128),
                                          (9, 7, 7, 128, 128), (1, 14, 14, 256, 192),
-                                         (7, 8, 8, 128, 64), (13, 4, 4, 64, 128), (30, 2, 2, 128, 64)])
+                                         (7, 8, 8, 128, 64), (13, 4, 4, 64, 128), (30, 2, 2, 128, 64),
+                                         (2, 32, 32, 64, 64), (3, 16, 16, 64, 128)])
 @pytest.mark.parametrize("slab,pp", [(False, False), (True, False), (True, True), (False, True)])
 def test_conv3x3_wgrad_halo_kernel(N, H, W, Ci, Co, slab, pp, monkeypatch):
     """3x3 stride-1 weight-gradient halo kernel (csrc/kernels/conv3x3.hip) vs the fp32 PyTorch weight
     gradient of the same bf16 operands: every ResNet-50 row tiling (56/28/14/7 wide), the VGG-16 CIFAR
-    whole-image tilings (8x8 / 4x4 / 2x2: 3 / 10 / 24 images per tile), a partial last group of images
+    whole-image tilings (8x8 / 4x4 / 2x2: 3 / 10 / 24 images per tile) and 128-pixel row tilings (32x32 / 16x16), a partial last group of images
     (N = 9 at 7x7, N = 7 / 13 / 30 at the VGG sizes), several 64-channel tiles each way, atomics and partial slabs, and
     accumulation into a non-zero gradient; the two-workgroups-per-CU form and the 512-thread ping-pong form
     (two halves accumulating the same block, merged through LDS)."""
