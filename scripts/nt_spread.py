@@ -23,13 +23,18 @@ def main():
     for rep in range(4):
         for nt in ("0", "1"):
             os.environ["DDL_BN_NT"] = nt
-            loss = m.backward_step(xi, yt)
+            loss = m.backward_step(xi, yt).detach()
             g = m.arena.grad.clone()
             out.setdefault(nt, []).append((round(float(loss), 5), round(g.norm().item(), 3)))
             out.setdefault(nt + "_grads", []).append(g)
     g0, g1 = out.pop("0_grads"), out.pop("1_grads")
-    out["max_rel_diff_nt0_runs"] = max(((a - g0[0]).norm() / g0[0].norm()).item() for a in g0[1:])
-    out["max_rel_diff_nt1_vs_nt0"] = max(((a - g0[0]).norm() / g0[0].norm()).item() for a in g1)
+    rel = lambda a, b: round(((a - b).norm() / b.norm()).item(), 5)
+    out["rel_diff_nt0_consecutive"] = [rel(g0[i + 1], g0[i]) for i in range(len(g0) - 1)]
+    out["rel_diff_nt1_vs_nt0_same_rep"] = [rel(a, b) for a, b in zip(g1, g0)]
+    # where along the arena the runs part (the arena's layer order: first decile = stem side)
+    n = g0[0].numel()
+    out["rel_diff_by_arena_decile_nt0"] = [rel(g0[1][k * n // 10:(k + 1) * n // 10], g0[0][k * n // 10:(k + 1) * n // 10])
+                                           for k in range(10)]
     print(json.dumps(out))
 
 
