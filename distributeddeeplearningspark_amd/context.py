@@ -20,6 +20,21 @@ from .sql.dataframe import DataFrame, Row, from_columns
 from .sql.readwriter import DataFrameReader
 
 
+def _warm_device(device: str):
+    """Initialise this process's HIP context and the native kernels on ``device`` (the one-GPU
+    form of pre-started executors: the in-process replica group trains here)."""
+    import torch
+
+    from .ops._native import C
+
+    d = torch.device(device)
+    if d.type == "cuda":
+        torch.cuda.set_device(d)
+        torch.zeros(1, device=d).add_(1)
+        C()
+        torch.cuda.synchronize(d)
+
+
 class SparkConf:
     def __init__(self, loadDefaults: bool = True):
         self._conf: dict[str, str] = {}
@@ -110,11 +125,22 @@ class SparkContext:
         from .parallel.executors import get_pool
         from .parallel.launcher import backend_for, plan_devices
 
+        from .parallel import replicas
+
         n = self.num_workers()
         if n <= 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1:
             return None
         device = device or self._conf.get("spark.ddl.device") or os.environ.get("DDL_DEVICE", "auto")
         devices = plan_devices(n, device)
+        if replicas.applies({"algorithm": "adag"}, devices):
+            # co-located workers train as in-process replica groups (parallel/replicas.py): one executor
+            # per GPU, or none at all on one GPU — the driver's own HIP context is warmed up instead
+            groups = replicas.plan(devices)
+            if len(groups) == 1:
+                self._local_warm = threading.Thread(target=_warm_device, args=(devices[0],), daemon=True)
+                self._local_warm.start()
+                return None
+            devices = [devices[g[0]] for g in groups]
         self._executors = get_pool(devices, backend_for(devices))
         return self._executors
 
@@ -124,6 +150,10 @@ class SparkContext:
         pool = getattr(self, "_executors", None)
         if pool is not None and not pool.closed:
             pool.wait_ready()
+        warm = getattr(self, "_local_warm", None)
+        if warm is not None:
+            warm.join()
+            self._local_warm = None
         return self
 
     @classmethod

@@ -210,4 +210,34 @@ struct CommitPtrs { const float* p[kMaxCommitPeers]; };
 int commit_delta(float* W, const float* center, float* X, void* w16, long n, float scale, int elastic, hipStream_t s);
 int commit_apply(const CommitPtrs& xs, int nx, float* center, float* W, void* w16, long n, hipStream_t s);
 
+// Deterministic-reduction mode (DDL_DETERMINISTIC=1, ops/determinism.py): every launcher that would add
+// partial sums with fp32 atomics from several workgroups instead reduces in a fixed order (one writer per
+// output element, partial rows summed by index).  Process-wide switch, set from Python.
+void set_deterministic(int on);
+int deterministic();
+// word-embedding gradient, deterministic: tokens sorted by id (stable), ONE writer per run of equal ids
+// (the wave whose chunk holds the run's first position walks the whole run in order)
+int embed_word_grad_det(const int64_t* sorted_ids, const int64_t* perm, const void* ds, float* gword, long T, int H,
+                        long V, hipStream_t s);
+
+// in-process replica groups (replica.hip): one commit kernel over R replicas' arenas, and the device-side
+// mini-batch fetch / loss record of a graph-replayed replica step
+constexpr int kMaxReplicas = 16;
+struct ReplicaPtrs {
+  float* w[kMaxReplicas];
+  void* w16[kMaxReplicas];
+  float scale[kMaxReplicas];
+};
+int commit_replicas(const ReplicaPtrs& rp, int nr, float* center, float* sum, long n, int elastic, int mode,
+                    hipStream_t s);
+constexpr int kMaxBatchCopies = 4;
+struct BatchCopy {
+  const void* src[kMaxBatchCopies];
+  void* dst[kMaxBatchCopies];
+  long bytes[kMaxBatchCopies];  // bytes of ONE mini-batch of copy q
+  long nbatch;                  // mini-batches per epoch
+};
+int batch_fetch(const BatchCopy& bc, int ncopy, const int* ctr, hipStream_t s);
+int step_record(const float* loss, float* hist, int cap, int* ctr, hipStream_t s);
+
 }  // namespace ddl

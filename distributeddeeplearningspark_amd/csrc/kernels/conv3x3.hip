@@ -25,6 +25,7 @@
 // Each wave: 8 pixel fragments (128 pixels) x BN/32 channel fragments of 16; per tap and
 // 64-channel chunk 8 x (BN/32) x 2 v_mfma_f32_16x16x32_bf16.
 #include "ddl_gemm_kernel.h"
+#include "ddl_ops.h"
 
 namespace ddl {
 namespace {
@@ -953,7 +954,8 @@ int launch_conv3x3_wgrad(const bf16_t* dy, const bf16_t* x, float* gw, float* ws
   int rc = ws ? launch_wgrad<true>(a, t, grid, pp, s) : launch_wgrad<false>(a, t, grid, pp, s);
   if (rc || !ws) return rc;
   const long n4 = (long)co * 9 * ci / 4;
-  const int per_group = n4 >= 65536 ? splits : 16;  // enough workgroups either way
+  // deterministic mode: every slab of an element summed by one lane in split order (no atomics)
+  const int per_group = (n4 >= 65536 || deterministic()) ? splits : 16;  // enough workgroups either way
   const dim3 rgrid((unsigned)((n4 + 255) / 256), (unsigned)((splits + per_group - 1) / per_group));
   hipLaunchKernelGGL(wgrad_slab_reduce_kernel, rgrid, dim3(256), 0, s, reinterpret_cast<const float4*>(ws), gw, n4,
                      splits, per_group);

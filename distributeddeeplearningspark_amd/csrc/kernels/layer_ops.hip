@@ -10,6 +10,7 @@
 // regenerates the mask instead of storing it.
 #include "ddl_common.h"
 #include "ddl_act.h"
+#include "ddl_ops.h"
 
 namespace ddl {
 namespace {
@@ -122,11 +123,11 @@ __global__ void avgpool2d_bwd_kernel(const T* __restrict__ dy, T* __restrict__ d
 
 // db[n] += sum_m dy[m][n] (fp32): 64 columns x 4 row-lanes per workgroup, 256 rows per chunk
 __global__ __launch_bounds__(256) void colsum_f32_kernel(const float* __restrict__ dy, float* __restrict__ db, long M,
-                                                         int N) {
+                                                         int N, long chunk) {
   __shared__ float part[4][64];
   const int col = blockIdx.x * 64 + (threadIdx.x & 63), rl = threadIdx.x >> 6;
-  const long r0 = (long)blockIdx.y * 256;
-  const long r1 = min(M, r0 + 256);
+  const long r0 = (long)blockIdx.y * chunk;
+  const long r1 = min(M, r0 + chunk);
   float s = 0.f;
   if (col < N)
     for (long r = r0 + rl; r < r1; r += 4) s += dy[r * N + col];
@@ -324,8 +325,9 @@ int embedding_scatter(const int64_t* ids, const void* dy, float* gw, long n, int
 
 int colsum_f32(const float* dy, float* db, long M, int N, hipStream_t s) {
   if (M <= 0 || N <= 0) return 0;
-  const dim3 grid((unsigned)((N + 63) / 64), (unsigned)((M + 255) / 256));
-  hipLaunchKernelGGL(colsum_f32_kernel, grid, dim3(256), 0, s, dy, db, M, N);
+  const long chunk = deterministic() ? M : 256;  // deterministic: one writer per column
+  const dim3 grid((unsigned)((N + 63) / 64), (unsigned)((M + chunk - 1) / chunk));
+  hipLaunchKernelGGL(colsum_f32_kernel, grid, dim3(256), 0, s, dy, db, M, N, chunk);
   return (int)hipGetLastError();
 }
 

@@ -270,10 +270,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
 // not accumulating)
 constexpr int kColsumRows = 128;
 __global__ __launch_bounds__(1024) void colsum_kernel(const float* __restrict__ ws, int P, int N, long ld,
-                                                      float* __restrict__ out) {
+                                                      float* __restrict__ out, int chunk) {
   __shared__ float red[16][65];
   const int n = blockIdx.x * 64 + threadIdx.x;
-  const int p0 = blockIdx.y * kColsumRows, p1 = min(P, p0 + kColsumRows);
+  const int p0 = blockIdx.y * chunk, p1 = min(P, p0 + chunk);
   float s = 0.f;
   if (n < N)
     for (int p = p0 + threadIdx.y; p < p1; p += 16) s += ws[(long)p * ld + n];
@@ -404,6 +404,40 @@ __global__ __launch_bounds__(256) void embed_word_grad_kernel(const int64_t* __r
   }
 }
 
+// Deterministic word-embedding gradient (DDL_DETERMINISTIC=1): tokens sorted by id with a STABLE sort, so
+// the rows of one id are in token order; the wave whose 32-position chunk holds a run's FIRST position
+// sums the whole run (possibly crossing into later chunks) in order and is its only writer — no atomics,
+// the same bits on every run.  A frequent id ([MASK]) makes its wave walk a long run: this mode trades
+// speed for reproducibility.
+__global__ __launch_bounds__(256) void embed_word_grad_det_kernel(const int64_t* __restrict__ sorted_ids,
+                                                                 const int64_t* __restrict__ perm,
+                                                                 const bf16_t* __restrict__ ds,
+                                                                 float* __restrict__ gword, long T, int H, long V) {
+  const long c0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * kEmbChunk;
+  const int lane = threadIdx.x & 63;
+  if (c0 >= T) return;
+  const long c1 = min(T, c0 + kEmbChunk);
+  for (long j0 = c0; j0 < c1; ++j0) {
+    const int64_t id = sorted_ids[j0];
+    if (j0 > 0 && sorted_ids[j0 - 1] == id) continue;  // not a run start: another wave (or an earlier j0) owns it
+    if ((uint64_t)id >= (uint64_t)V) continue;          // out-of-vocabulary ids add nothing (never a wild write)
+    long j1 = j0 + 1;
+    while (j1 < T && sorted_ids[j1] == id) ++j1;
+    for (int c = lane * 8; c < H; c += 512) {
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (long j = j0; j < j1; ++j) {
+        float d[8];
+        unpack8(*reinterpret_cast<const uint4*>(ds + perm[j] * H + c), d);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += d[e];
+      }
+      float* g = gword + id * H + c;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[e] += acc[e];
+    }
+  }
+}
+
 // word-embedding gradient without a sort: gword[ids[t]][h] += ds[t][h] as no-return fp32 atomics
 // (executed at the memory side, ~1.3 TB/s of added bytes on MI355X: 16384 x 768 tokens x columns in
 // ~40 us, vs ~105 us for the sorted one-writer walk, which also needed a radix sort of the ids).
@@ -521,8 +555,10 @@ int colsum_partials(const float* ws, int P, int N, float* out, int accumulate, h
     const hipError_t e = hipMemsetAsync(out, 0, sizeof(float) * (size_t)N, s);
     if (e != hipSuccess) return (int)e;
   }
-  hipLaunchKernelGGL(colsum_kernel, dim3((N + 63) / 64, (P + kColsumRows - 1) / kColsumRows), dim3(64, 16), 0, s, ws,
-                     P, N, ld > 0 ? ld : (long)N, out);
+  // deterministic mode: one row chunk -> one writer per column, partial rows summed in a fixed order
+  const int chunk = deterministic() ? (P > 0 ? P : 1) : kColsumRows;
+  hipLaunchKernelGGL(colsum_kernel, dim3((N + 63) / 64, (P + chunk - 1) / chunk), dim3(64, 16), 0, s, ws, P, N,
+                     ld > 0 ? ld : (long)N, out, chunk);
   return (int)hipGetLastError();
 }
 
@@ -542,6 +578,16 @@ int embed_word_grad(const int64_t* sorted_ids, const int64_t* perm, const void* 
   const long waves = (T + kEmbChunk - 1) / kEmbChunk;
   hipLaunchKernelGGL(embed_word_grad_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, sorted_ids, perm,
                      reinterpret_cast<const bf16_t*>(ds), gword, T, H);
+  return (int)hipGetLastError();
+}
+
+int embed_word_grad_det(const int64_t* sorted_ids, const int64_t* perm, const void* ds, float* gword, long T, int H,
+                        long V, hipStream_t s) {
+  if (T <= 0) return 0;
+  if (H % 8) return (int)hipErrorInvalidValue;
+  const long waves = (T + kEmbChunk - 1) / kEmbChunk;
+  hipLaunchKernelGGL(embed_word_grad_det_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, sorted_ids, perm,
+                     reinterpret_cast<const bf16_t*>(ds), gword, T, H, V);
   return (int)hipGetLastError();
 }
 

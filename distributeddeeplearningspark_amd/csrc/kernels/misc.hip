@@ -7,6 +7,11 @@
 
 namespace ddl {
 
+// deterministic-reduction switch (ddl_ops.h); read by the launchers on the host, never by a kernel
+static int g_deterministic = 0;
+void set_deterministic(int on) { g_deterministic = on ? 1 : 0; }
+int deterministic() { return g_deterministic; }
+
 static unsigned mgrid(long n) {
   long g = (n + 255) / 256;
   if (g > 8192) g = 8192;
@@ -157,6 +162,7 @@ int bias_grad(const void* dy, float* db, long M, int N, int accumulate, hipStrea
   long ys = M / 64;
   if (ys < 1) ys = 1;
   if (ys > 256) ys = 256;
+  if (deterministic()) ys = 1;  // one workgroup per column block: a single writer per column
   if (N % 8 == 0 && (reinterpret_cast<uintptr_t>(dy) & 15) == 0) {
     hipLaunchKernelGGL(bias_grad_vec_kernel, dim3((N + 255) / 256, (unsigned)ys), dim3(256), 0, s,
                        (const bf16_t*)dy, db, M, N);

@@ -189,8 +189,8 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float4* x, long n4, fl
 
 int sumsq_f32(const float* x, long n, float* out, hipStream_t s) {
   if (n % 4) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(sumsq_kernel, dim3(ogrid(n / 4) > 1024 ? 1024 : ogrid(n / 4)), dim3(256), 0, s, (const float4*)x,
-                     n / 4, out);
+  const unsigned blocks = deterministic() ? 1u : (ogrid(n / 4) > 1024 ? 1024 : ogrid(n / 4));
+  hipLaunchKernelGGL(sumsq_kernel, dim3(blocks), dim3(256), 0, s, (const float4*)x, n / 4, out);
   return (int)hipGetLastError();
 }
 

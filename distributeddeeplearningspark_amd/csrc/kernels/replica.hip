@@ -1,0 +1,139 @@
+// Kernels of the in-process replica group (parallel/replicas.py): R dist-keras workers co-located on
+// one MI355X run as R model replicas of ONE process, each step replayed from a hipGraph with no host
+// work per mini-batch, and a commit round is ONE kernel over the R replicas' flat weight arenas.
+//
+// The reference runs num_processes = 2 replicas per executor (ddl_mnist_aztk.py:49-53,66;
+// ddl_nyiso_aztk.py:51-55) that commit window-normalised deltas to the parameter server
+// (ddl_mnist_aztk.py:216-219).  Here the "server" is the center variable in HBM and the commit is
+//   X_r = s_r (W_r - c)                    (s_r: 1/window for ADAG, 1/(rank order + 1) DynSGD, ...)
+//   c  += X_0 + X_1 + ... + X_{R-1}        (accumulated in replica order: the sum of the IPC exchange path)
+//   W_r = c                                (elastic family instead: W_r -= X_r)
+// in one flat sweep that reads each W_r and the center once.
+//
+// batch_fetch / step_record keep a graph-replayed step free of host state: the step index lives in a
+// device int32 (one per replica), the fetch copies the resident shard's mini-batch (index % batches
+// per epoch, trailing partial batch dropped as the dist-keras worker does) into the graph's static
+// input buffers, and the record appends the step's loss to a device history and advances the index.
+#include "ddl_common.h"
+#include "ddl_ops.h"
+
+namespace ddl {
+
+namespace {
+
+unsigned rgrid(long n4) {
+  long g = (n4 + 255) / 256;
+  if (g > 2048) g = 2048;
+  return (unsigned)(g > 0 ? g : 1);
+}
+
+__device__ __forceinline__ void st_bf16x4(void* w16, long i4, const float4& w) {
+  uint2 o;
+  o.x = pack_bf16x2(w.x, w.y);
+  o.y = pack_bf16x2(w.z, w.w);
+  reinterpret_cast<uint2*>(w16)[i4] = o;
+}
+
+// mode 0: full commit on this GPU (center += sum X_r; W_r = center or W_r -= X_r)
+// mode 1: partial sum only (sum = sum X_r, elastic W_r -= X_r): the per-GPU share of a multi-GPU round,
+//         all-reduced over RCCL before mode 2
+// mode 2: apply an all-reduced sum (center += sum; non-elastic W_r = center)
+__global__ __launch_bounds__(256) void commit_replicas_kernel(ReplicaPtrs rp, int nr, float4* __restrict__ center,
+                                                              float4* __restrict__ sum, long n4, int elastic,
+                                                              int mode) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    const float4 c0 = center[i];
+    float4 acc = mode == 1 ? make_float4(0.f, 0.f, 0.f, 0.f) : c0;
+    if (mode == 2) {
+      const float4 s = sum[i];
+      acc.x += s.x;
+      acc.y += s.y;
+      acc.z += s.z;
+      acc.w += s.w;
+    } else {
+      for (int r = 0; r < nr; ++r) {
+        float4* W = reinterpret_cast<float4*>(rp.w[r]);
+        float4 w = W[i];
+        const float sc = rp.scale[r];
+        const float4 x = make_float4(sc * (w.x - c0.x), sc * (w.y - c0.y), sc * (w.z - c0.z), sc * (w.w - c0.w));
+        acc.x += x.x;
+        acc.y += x.y;
+        acc.z += x.z;
+        acc.w += x.w;
+        if (elastic) {
+          w = make_float4(w.x - x.x, w.y - x.y, w.z - x.z, w.w - x.w);
+          W[i] = w;
+          if (rp.w16[r]) st_bf16x4(rp.w16[r], i, w);
+        }
+      }
+    }
+    if (mode == 1) {
+      sum[i] = acc;
+      continue;
+    }
+    center[i] = acc;
+    if (!elastic) {
+      for (int r = 0; r < nr; ++r) {
+        reinterpret_cast<float4*>(rp.w[r])[i] = acc;
+        if (rp.w16[r]) st_bf16x4(rp.w16[r], i, acc);
+      }
+    }
+  }
+}
+
+// one workgroup per copy; 16-B vectors when both sides are aligned and the batch is a multiple of 16 B
+__global__ __launch_bounds__(256) void batch_fetch_kernel(BatchCopy bc, int ncopy, const int* __restrict__ ctr) {
+  const int q = blockIdx.y;
+  if (q >= ncopy) return;
+  const long nb = bc.nbatch;
+  const long b = (long)(*ctr) % nb;
+  const long bytes = bc.bytes[q];
+  const char* src = reinterpret_cast<const char*>(bc.src[q]) + b * bytes;
+  char* dst = reinterpret_cast<char*>(bc.dst[q]);
+  const bool vec = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) | (uintptr_t)bytes) & 15) == 0;
+  const long stride = (long)gridDim.x * 256;
+  if (vec) {
+    const long n16 = bytes >> 4;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n16; i += stride)
+      reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+  } else {
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < bytes; i += stride) dst[i] = src[i];
+  }
+}
+
+// hist[ctr] = loss (while ctr < cap); ctr += 1 — one lane, vector memory only
+__global__ void step_record_kernel(const float* __restrict__ loss, float* __restrict__ hist, int cap, int* ctr) {
+  if (threadIdx.x == 0) {
+    const int c = *ctr;
+    if (hist && c < cap) hist[c] = *loss;
+    *ctr = c + 1;
+  }
+}
+
+}  // namespace
+
+int commit_replicas(const ReplicaPtrs& rp, int nr, float* center, float* sum, long n, int elastic, int mode,
+                    hipStream_t s) {
+  if (n % 4 || nr < 0 || nr > kMaxReplicas || (mode != 0 && !sum)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(commit_replicas_kernel, dim3(rgrid(n >> 2)), dim3(256), 0, s, rp, nr, (float4*)center,
+                     (float4*)sum, n >> 2, elastic, mode);
+  return (int)hipGetLastError();
+}
+
+int batch_fetch(const BatchCopy& bc, int ncopy, const int* ctr, hipStream_t s) {
+  if (ncopy < 1 || ncopy > kMaxBatchCopies || bc.nbatch < 1) return (int)hipErrorInvalidValue;
+  long most = 0;
+  for (int q = 0; q < ncopy; ++q) most = bc.bytes[q] > most ? bc.bytes[q] : most;
+  long blocks = (most / 16 + 255) / 256;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 256) blocks = 256;
+  hipLaunchKernelGGL(batch_fetch_kernel, dim3((unsigned)blocks, (unsigned)ncopy), dim3(256), 0, s, bc, ncopy, ctr);
+  return (int)hipGetLastError();
+}
+
+int step_record(const float* loss, float* hist, int cap, int* ctr, hipStream_t s) {
+  hipLaunchKernelGGL(step_record_kernel, dim3(1), dim3(64), 0, s, loss, hist, cap, ctr);
+  return (int)hipGetLastError();
+}
+
+}  // namespace ddl

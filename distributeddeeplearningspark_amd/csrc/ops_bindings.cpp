@@ -370,6 +370,64 @@ void commit_apply_(const std::vector<at::Tensor>& xs, const at::Tensor& center, 
   HIP_OK(commit_apply(ptrs, (int)xs.size(), center.data_ptr<float>(), W ? W->data_ptr<float>() : nullptr,
                       optr<void>(w16), center.numel(), cur_stream()));
 }
+// mode 0: full commit on one GPU; 1: partial sum into `sum` (multi-GPU round); 2: apply the all-reduced `sum`
+void commit_replicas_(const std::vector<at::Tensor>& ws, const std::vector<c10::optional<at::Tensor>>& w16s,
+                      const std::vector<double>& scales, const at::Tensor& center, c10::optional<at::Tensor> sum,
+                      bool elastic, int64_t mode) {
+  GPU(center); F32(center);
+  CK(center.numel() % 4 == 0, "commit_replicas: n % 4 == 0");
+  CK(ws.size() <= (size_t)kMaxReplicas && w16s.size() == ws.size() && scales.size() == ws.size(),
+     "commit_replicas: up to 16 replicas, one w16 (or None) and one scale each");
+  CK(mode >= 0 && mode <= 2 && (mode == 0 || sum), "commit_replicas: mode 0 / 1 / 2 (1 and 2 need sum)");
+  ReplicaPtrs rp{};
+  for (size_t r = 0; r < ws.size(); ++r) {
+    F32(ws[r]);
+    CK(ws[r].device() == center.device() && ws[r].numel() == center.numel(), "commit_replicas: replica arena size");
+    rp.w[r] = ws[r].data_ptr<float>();
+    if (w16s[r]) {
+      BF16(*w16s[r]);
+      CK(w16s[r]->device() == center.device() && w16s[r]->numel() == center.numel(), "commit_replicas: w16 size");
+      rp.w16[r] = w16s[r]->data_ptr();
+    }
+    rp.scale[r] = (float)scales[r];
+  }
+  if (sum) { F32(*sum); CK(sum->device() == center.device() && sum->numel() == center.numel(), "commit_replicas: sum"); }
+  at::DeviceGuard g(center.device());
+  HIP_OK(commit_replicas(rp, (int)ws.size(), center.data_ptr<float>(), optr<float>(sum), center.numel(),
+                         elastic ? 1 : 0, (int)mode, cur_stream()));
+}
+// copies mini-batch (ctr % nbatch) of each resident shard srcs[q] ([nbatch * rows, ...]) into dsts[q]
+void batch_fetch_(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts, const at::Tensor& ctr,
+                  int64_t nbatch) {
+  CK(!srcs.empty() && srcs.size() <= (size_t)kMaxBatchCopies && dsts.size() == srcs.size(), "batch_fetch: 1..4 copies");
+  CK(ctr.is_cuda() && ctr.scalar_type() == at::kInt && ctr.numel() == 1, "batch_fetch: int32 step counter");
+  CK(nbatch >= 1, "batch_fetch: nbatch >= 1");
+  BatchCopy bc{};
+  bc.nbatch = nbatch;
+  for (size_t q = 0; q < srcs.size(); ++q) {
+    const at::Tensor &s = srcs[q], &d = dsts[q];
+    CK(s.is_cuda() && d.is_cuda() && s.is_contiguous() && d.is_contiguous() && s.scalar_type() == d.scalar_type() &&
+           s.device() == ctr.device() && d.device() == ctr.device(),
+       "batch_fetch: contiguous GPU tensors of one dtype on the counter's device");
+    const long bytes = (long)d.numel() * (long)d.element_size();
+    CK((long)s.numel() * (long)s.element_size() >= bytes * nbatch, "batch_fetch: shard smaller than nbatch batches");
+    bc.src[q] = s.data_ptr();
+    bc.dst[q] = d.data_ptr();
+    bc.bytes[q] = bytes;
+  }
+  at::DeviceGuard g(ctr.device());
+  HIP_OK(batch_fetch(bc, (int)srcs.size(), ctr.data_ptr<int>(), cur_stream()));
+}
+void step_record_(const at::Tensor& loss, c10::optional<at::Tensor> hist, const at::Tensor& ctr) {
+  F32(loss);
+  CK(loss.is_cuda() && loss.numel() == 1, "step_record: one fp32 loss on the GPU");
+  CK(ctr.is_cuda() && ctr.scalar_type() == at::kInt && ctr.numel() == 1 && ctr.device() == loss.device(),
+     "step_record: int32 step counter on the loss device");
+  if (hist) { F32(*hist); CK(hist->device() == loss.device(), "step_record: history device"); }
+  at::DeviceGuard g(loss.device());
+  HIP_OK(step_record(loss.data_ptr<float>(), optr<float>(hist), hist ? (int)hist->numel() : 0, ctr.data_ptr<int>(),
+                     cur_stream()));
+}
 void mse_fwd_bwd_(const at::Tensor& pred, const at::Tensor& target, const at::Tensor& loss, const at::Tensor& grad) {
   F32(pred); F32(target); F32(loss); F32(grad);
   CK(pred.is_cuda() && pred.numel() == target.numel() && grad.numel() == pred.numel() && loss.numel() == 1,
@@ -477,6 +535,11 @@ void register_ops(py::module& m) {
   m.def("mse_fwd_bwd", &mse_fwd_bwd_);
   m.def("commit_delta", &commit_delta_);
   m.def("commit_apply", &commit_apply_);
+  m.def("commit_replicas", &commit_replicas_, "one commit round over R co-located replicas", py::arg("ws"),
+        py::arg("w16s"), py::arg("scales"), py::arg("center"), py::arg("sum") = py::none(), py::arg("elastic") = false,
+        py::arg("mode") = 0);
+  m.def("batch_fetch", &batch_fetch_);
+  m.def("step_record", &step_record_);
   m.def("etl_minmax", &etl_minmax_);
   m.def("etl_one_hot", &etl_one_hot_);
   m.def("etl_argmax", &etl_argmax_);

@@ -150,6 +150,18 @@ void embed_word_grad_(const at::Tensor& sorted_ids, const at::Tensor& perm, cons
                          gword.data_ptr<float>(), T, (int)H, cur_stream()));
 }
 
+// deterministic word-embedding gradient from a STABLE sort of the ids (DDL_DETERMINISTIC=1)
+void embed_word_grad_det_(const at::Tensor& sorted_ids, const at::Tensor& perm, const at::Tensor& ds,
+                          const at::Tensor& gword) {
+  GPU(ds); I64(sorted_ids); I64(perm); BF16(ds); F32(gword);
+  const int64_t T = sorted_ids.numel(), H = ds.size(-1);
+  CK(perm.numel() == T && ds.numel() == T * H && gword.dim() == 2 && gword.size(1) == H && H % 8 == 0,
+     "embed_word_grad_det: sorted_ids / perm [T], ds [T, H], gword [V, H]");
+  at::DeviceGuard g(ds.device());
+  HIP_OK(embed_word_grad_det(sorted_ids.data_ptr<int64_t>(), perm.data_ptr<int64_t>(), ds.data_ptr(),
+                             gword.data_ptr<float>(), T, (int)H, gword.size(0), cur_stream()));
+}
+
 void embed_word_grad_atomic_(const at::Tensor& ids, const at::Tensor& ds, const at::Tensor& gword) {
   GPU(ds); I64(ids); BF16(ds); F32(gword);
   const int64_t T = ids.numel(), H = ds.size(-1);
@@ -226,6 +238,9 @@ void register_transformer(py::module& m) {
         py::arg("in_drop_p") = 0.0, py::arg("in_seed") = 0, py::arg("parts") = 2);
   m.def("embed_word_grad", &embed_word_grad_);
   m.def("embed_word_grad_atomic", &embed_word_grad_atomic_);
+  m.def("embed_word_grad_det", &embed_word_grad_det_);
+  m.def("set_deterministic", [](bool on) { set_deterministic(on ? 1 : 0); });
+  m.def("deterministic", []() { return deterministic() != 0; });
   m.def("embed_pos_grad", &embed_pos_grad_);
   m.def("colsum_partials", &colsum_partials_, py::arg("ws"), py::arg("P"), py::arg("N"), py::arg("out"),
         py::arg("accumulate"), py::arg("ld") = 0);

@@ -36,6 +36,7 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
+from ..ops import determinism as _det
 from ..ops import gemm as G
 from ..ops import transformer as T
 from ..ops._native import C, use_native
@@ -262,7 +263,11 @@ class _EmbeddingsFn(torch.autograd.Function):
             # word rows: no-return fp32 atomics straight into the arena (no id sort); positions: sum over batch
             # (side stream: ordered after the tied decoder's wgrad into the same rows)
             with on_grad_stream(de.device, de, ids):
-                C().embed_word_grad_atomic(ids.reshape(-1).contiguous(), de, layer.word.grad)
+                if _det.enabled():  # stable id sort + one writer per run of equal ids (fixed order)
+                    sids, perm = torch.sort(ids.reshape(-1), stable=True)
+                    C().embed_word_grad_det(sids, perm, de, layer.word.grad)
+                else:
+                    C().embed_word_grad_atomic(ids.reshape(-1).contiguous(), de, layer.word.grad)
             C().embed_pos_grad(de, layer.pos.grad, T_ // S, S)
             nt = c.type_vocab_size
             if nt <= 2:
@@ -367,11 +372,16 @@ class _BertLayerFn(torch.autograd.Function):
         # ---- FFN block
         ds2, ds2d = ln_back(dout, s2, m2, r2, L.ln2_g, L.ln2_b, seeds[2], L.out_b)
         _wgrad(ds2d, f, L.out_w.grad)
-        st = torch.zeros((32, 2, c.intermediate_size), dtype=torch.float32, device=dev)
-        # d(pre) = (ds2d W2) * gelu'(pre); its column sums (bias grad of W1) come from the epilogue statistics
-        dpre = G.linear_dgrad(ds2d, L.out_w.data, gelu_pre=pre, stats=st)
-        _wgrad(dpre, a, L.i_w.grad)
-        C().colsum_partials(st.view(32, -1), 32, c.intermediate_size, L.i_b.grad, True, 2 * c.intermediate_size)
+        if _det.enabled():  # deterministic mode: no atomic epilogue statistics; one-writer column sums
+            dpre = G.linear_dgrad(ds2d, L.out_w.data, gelu_pre=pre)
+            _wgrad(dpre, a, L.i_w.grad)
+            _bias_grad(dpre, L.i_b.grad)
+        else:
+            st = torch.zeros((32, 2, c.intermediate_size), dtype=torch.float32, device=dev)
+            # d(pre) = (ds2d W2) * gelu'(pre); its column sums (bias grad of W1) come from the epilogue statistics
+            dpre = G.linear_dgrad(ds2d, L.out_w.data, gelu_pre=pre, stats=st)
+            _wgrad(dpre, a, L.i_w.grad)
+            C().colsum_partials(st.view(32, -1), 32, c.intermediate_size, L.i_b.grad, True, 2 * c.intermediate_size)
         da = G.linear_dgrad(dpre, L.i_w.data, resid=ds2)  # + residual gradient
         # ---- attention block
         ds1, ds1d = ln_back(da, s1, m1, r1, L.ln1_g, L.ln1_b, seeds[1], L.o_b)

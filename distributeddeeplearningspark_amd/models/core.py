@@ -283,10 +283,12 @@ class Model(Layer):
         x = x.to(self.device, non_blocking=True)
         if self.takes_integer_inputs():
             return x  # token ids (an Embedding first layer)
-        if x.dtype == torch.uint8 and x.dim() == 4 and (self.input_mean is not None or self.input_std is not None):
-            return self.normalize_images(x)  # uint8 NHWC pixels of a model that declares its normalisation
-        # any other integer / bool feature column: its values, in the compute dtype (the Dense / Conv
-        # kernels take floating inputs only)
+        if x.dtype == torch.uint8 and x.dim() == 4:
+            # uint8 NHWC pixels: (x - input_mean) / input_std per channel, or x / 255 when the model
+            # declares no normalisation (the Keras-style default for image batches)
+            return self.normalize_images(x)
+        # any other integer / bool feature column (2-D / 3-D: counts, ids, flags): its values, in the
+        # compute dtype (the Dense / Conv kernels take floating inputs only)
         return x.to(self.compute_dtype)
 
     def takes_integer_inputs(self) -> bool:

@@ -11,7 +11,7 @@
 from __future__ import annotations
 
 from .core import Sequential
-from .layers import (GRU, LSTM, Activation, AveragePooling2D, BatchNormalization, Conv2D, Dense, Dropout, Flatten,
+from .layers import (GRU, LSTM, Activation, BatchNormalization, Conv2D, Dense, Dropout, Flatten,
                      MaxPooling2D)
 
 
@@ -78,6 +78,3 @@ def vgg16(nb_classes: int = 10, input_shape=(32, 32, 3), batch_norm: bool = True
     m.add(Dropout(0.5))
     m.add(Dense(nb_classes, activation="softmax"))
     return m
-
-
-_ = AveragePooling2D

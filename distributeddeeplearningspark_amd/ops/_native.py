@@ -24,6 +24,11 @@ def _load():
         _ERR = e
         return
     _warn_if_stale()
+    if hasattr(_C, "set_deterministic"):  # the launchers' reduction-order switch (ops/determinism.py)
+        from . import determinism
+
+        _C.set_deterministic(determinism._STATE["on"])
+        determinism._STATE["native_synced"] = determinism._STATE["on"]
 
 
 def _warn_if_stale():

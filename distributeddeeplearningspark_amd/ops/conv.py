@@ -24,6 +24,7 @@ from functools import lru_cache
 import torch
 import torch.nn.functional as F
 
+from . import determinism as _det
 from . import gemm as G
 from ._native import C, use_native
 from ._ref import accumulate, ref_grads
@@ -165,7 +166,7 @@ def splitk_fwd_ok(g: ConvGeometry) -> bool:
     walk taps x channels alone (measured 77 us for VGG-16's 512-channel 2x2 layers on 88
     workgroups), so the K loop is split over workgroups into an fp32 workspace and a finalize pass
     adds bias / ReLU / statistics."""
-    if not (_SPLITK_FWD and g.implicit_fwd and g.T * g.Ci >= 1024 and g.Co % 8 == 0):
+    if not (_SPLITK_FWD and g.implicit_fwd and g.T * g.Ci >= 1024 and g.Co % 8 == 0) or _det.enabled():
         return False
     return math.ceil(g.M / 64) * math.ceil(g.Co / 64) <= _SPLITK_MAX_TILES
 
@@ -351,7 +352,8 @@ def conv_wgrad_native(dy, x, g: ConvGeometry, gw, x_norm=None):
     elif plan is not None:
         # 3x3 / stride 1: halo kernel (csrc/kernels/conv3x3.hip), 64 co x 64 ci x 9 taps per workgroup
         splits, tpb = plan
-        ws = torch.empty(splits * g.Co * 9 * g.Ci, dtype=torch.float32, device=dy.device) if _WG3_SLAB else None
+        slab = _WG3_SLAB or _det.enabled()  # deterministic mode: never the atomic accumulation
+        ws = torch.empty(splits * g.Co * 9 * g.Ci, dtype=torch.float32, device=dy.device) if slab else None
         C().conv3x3_wgrad(dy.contiguous(), x.contiguous(), gw, ws, splits, tpb, _WG3_PP)
     elif g.implicit_wgrad and g.Ci < 128 and _WIDE_WGRAD:
         # narrow inputs (64 channels): a 128-wide tile spans two taps, so the tap is resolved per

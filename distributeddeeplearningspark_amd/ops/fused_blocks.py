@@ -19,6 +19,7 @@ import weakref
 import torch
 
 from . import conv as CV
+from . import determinism as _det
 from . import gemm as G
 from ._native import C
 from .norm import new_stats_workspace, partials_workspace
@@ -75,6 +76,9 @@ def _bn_forward(layer_bn, yc, stats, resid, relu, training, mask=None, apply=Tru
     rm, rv = bn._states["moving_mean"], bn._states["moving_variance"]
     # one allocation for the four per-channel vectors (host cost per BN: VGG-16 runs launch-bound)
     scale, shift, mean, invstd = torch.empty(4, Cc, dtype=torch.float32, device=dev).unbind(0)
+    if stats is None:  # deterministic mode: no fused (atomic) statistics; fixed-order partial rows instead
+        stats = partials_workspace(M, Cc, dev)
+        C().bn_stats(yc, stats, Cc)
     C().bn_finalize(stats, M, Cc, gamma, beta, bn.epsilon, 1.0 - bn.momentum, rm, rv, mean, invstd, scale, shift)
     if not apply:
         return None, mean, invstd, scale, shift
@@ -112,8 +116,12 @@ def bn_backward(unit, st, dy, want_dres):
     Cc = st.yc.shape[-1]
     M = st.yc.numel() // Cc
     y = st.y if st.mode == 1 else (st.mask if st.mode == 3 else None)
-    if st.pre_reduced is not None:  # partial sums already accumulated by dy's producer (no reduce sweep)
-        ws, st.pre_reduced = st.pre_reduced, None
+    pre, st.pre_reduced = st.pre_reduced, None
+    if pre is not None and _same_tensor(pre[1], dy):
+        # partial sums already accumulated by dy's producer (no reduce sweep) — valid only when dy IS the
+        # gradient that producer reduced: a second consumer of this BN's output makes autograd sum the
+        # gradients into a new tensor, and then the sweep runs on the sum
+        ws = pre[0]
     else:
         ws = partials_workspace(M, Cc, dy.device)
         C().bn_bwd_reduce(dy, st.yc, y, st.scale, st.shift, st.mean, ws, Cc, st.mode)
@@ -132,7 +140,9 @@ def conv_backward(unit, st, dyc, x, need_dx, resid=None, resid_mask=None, bnr=No
     conv = unit.conv
     # the weight gradient only feeds the optimizer / all-reduce: it runs on the side stream
     # (ops/streams.py) beside the data-gradient and BatchNorm sweeps of the layers below
-    with on_grad_stream(dyc.device, dyc, x, default=False):
+    # (every tensor the side-stream kernel reads is recorded on that stream, the normalise-on-load
+    # scale / shift included: the main stream may drop them before the side stream has run)
+    with on_grad_stream(dyc.device, dyc, x, *(x_norm or ()), default=False):
         CV.conv_wgrad_native(dyc, x, st.g, conv.kernel.grad, x_norm=x_norm)
     if conv.grad_hook is not None:
         conv.grad_hook()
@@ -185,11 +195,11 @@ class _BottleneckFn(torch.autograd.Function):
         # reduce sweep wherever the kernel that ran could take it (bnr["done"])
         bnr2 = _bnr_mode2(s2, dout.device)
         d2 = conv_backward(b.c3, s3, d3c, s2.yc if s2.y is None else s2.y, True, x_norm=_norm_of(s2), bnr=bnr2)
-        _take_reduced(s2, bnr2)
+        _take_reduced(s2, bnr2, d2)
         d2c, _ = bn_backward(b.c2, s2, d2, False)
         bnr1 = _bnr_mode2(s1, dout.device)
         d1 = conv_backward(b.c2, s2, d2c, s1.y, True, bnr=bnr1)
-        _take_reduced(s1, bnr1)
+        _take_reduced(s1, bnr1, d1)
         d1c, _ = bn_backward(b.c1, s1, d1, False)
         rsub = None
         if s_down is not None:
@@ -210,7 +220,7 @@ class _BottleneckFn(torch.autograd.Function):
         # backward partial sums of the BN that produced X (previous block's bn3, mode 3) when that GEMM
         # runs on the streaming kernel — that BN's backward then skips its reduce sweep over dX and yc
         bnr = None
-        if ctx.needs_dx and ctx.prev is not None and ctx.prev[1].mode == 3:
+        if ctx.needs_dx and ctx.prev is not None and ctx.prev[1].mode == 3 and not _det.enabled():
             pst = ctx.prev[1]
             bnr = {"x": pst.yc, "mask": pst.mask, "mean": pst.mean,
                    "ws": new_stats_workspace(pst.yc.shape[-1], dout.device)}
@@ -219,7 +229,7 @@ class _BottleneckFn(torch.autograd.Function):
         else:
             dx = conv_backward(b.c1, s1, d1c, x, ctx.needs_dx, resid=dsc, bnr=bnr, rsub=rsub)
         if bnr is not None and bnr.get("done"):
-            ctx.prev[1].pre_reduced = bnr["ws"]
+            ctx.prev[1].pre_reduced = (bnr["ws"], dx)
         ctx.states = ctx.prev = None
         return dx, None, None
 
@@ -239,15 +249,21 @@ _NORM_ON_LOAD = _os.environ.get("DDL_NORM_ON_LOAD", "0") == "1"
 
 def _bnr_mode2(st, device):
     """BN-backward reduce request for a ReLU BN without residual (mode 2) — see ``gemm.linear_dgrad``."""
-    if not _FUSE_BNR_INNER or st.mode != 2:
+    if not _FUSE_BNR_INNER or st.mode != 2 or _det.enabled():
         return None
     return {"x": st.yc, "scale": st.scale, "shift": st.shift, "mean": st.mean,
             "ws": new_stats_workspace(st.yc.shape[-1], device)}
 
 
-def _take_reduced(st, bnr):
+def _take_reduced(st, bnr, d):
     if bnr is not None and bnr.get("done"):
-        st.pre_reduced = bnr["ws"]
+        st.pre_reduced = (bnr["ws"], d)
+
+
+def _same_tensor(a, b) -> bool:
+    """b is the very gradient tensor a (same storage, shape and version), not a sum formed from it."""
+    return (a.data_ptr() == b.data_ptr() and a.shape == b.shape and a.stride() == b.stride()
+            and a._version == b._version)
 
 
 def bottleneck(block, x, anchor):

@@ -14,6 +14,7 @@ import math
 
 import torch
 
+from . import determinism as _det
 from ._native import C
 
 KC, RC, KC_GATHER, RC_GATHER, RC_TAPS, KC_GATHER8, RC_GATHER8 = 0, 1, 2, 3, 4, 5, 6
@@ -129,6 +130,8 @@ def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, bet
             tile = choose_tile(M, N, bn_cap)
     if k_split is None:
         k_split = choose_split(M, N, K, tile, allow=(epi != EPI_BF16), rounds=split_rounds)
+    if _det.enabled():  # deterministic mode: the whole K in one workgroup (no atomic split-K partial sums)
+        k_split = max(64, math.ceil(K / 64) * 64)
     if epi == EPI_F32 and k_split < K:
         if beta not in (0.0, 1.0):
             raise ValueError("split-K fp32 gemm supports beta in {0,1} (beta=0 needs a zeroed C)")
@@ -180,7 +183,9 @@ _SPLITK_WS = {}
 def splitk_workspace(M, N, device):
     """Persistent zeroed fp32 [M, N] accumulator of a split-K bf16 GEMM: ``splitk_finalize`` zeroes
     it again as it reads it, so consecutive calls (one stream) need no fill launch."""
-    key = (M, N, str(device))
+    from . import scope as _scope
+
+    key = (M, N, str(device) + _scope.tag())
     ws = _SPLITK_WS.get(key)
     if ws is None:
         ws = _SPLITK_WS[key] = torch.zeros((M, N), dtype=torch.float32, device=device)
@@ -209,7 +214,7 @@ def linear_dgrad(dy, w, out=None, resid=None, gelu_pre=None, stats=None, resid_m
     act = ACT_GELU_BWD if gelu_pre is not None else ACT_NONE
     ldr = resid.stride(0) if resid is not None else 0
     tiles = math.ceil(M / 64) * math.ceil(K / 64)
-    if (_SPLITK_DGRAD and gelu_pre is None and resid is None and rsub is None and N >= 4096 and tiles <= 1024 and K % 8 == 0
+    if (_SPLITK_DGRAD and not _det.enabled() and gelu_pre is None and resid is None and rsub is None and N >= 4096 and tiles <= 1024 and K % 8 == 0
             and out.is_contiguous() and out.dtype == torch.bfloat16 and dy.device.type == "cuda"):
         # few output tiles over a long reduction (BERT's MLM decoder: [masked tokens, 768] over the
         # 30,522-word vocabulary ran on 240 workgroups of ~480 K-steps): split the reduction over

@@ -11,6 +11,8 @@ from __future__ import annotations
 
 import torch
 
+from . import determinism as _det
+from . import scope as _scope
 from ._native import C, use_native
 from ._ref import accumulate, ref_grads
 
@@ -27,7 +29,7 @@ class _StatsPool:
         self.buf, self.used, self.demand = {}, {}, {}
 
     def get(self, C_, device):
-        key = str(device)
+        key = str(device) + _scope.tag()
         n = -(-SHARDS * 2 * C_ // 64) * 64
         self.demand[key] = self.demand.get(key, 0) + n
         buf, used = self.buf.get(key), self.used.get(key, 0)
@@ -37,7 +39,7 @@ class _StatsPool:
         return buf[used : used + SHARDS * 2 * C_].view(SHARDS, 2, C_)
 
     def reset(self, device):
-        key = str(device)
+        key = str(device) + _scope.tag()
         want = self.demand.get(key, 0)
         buf = self.buf.get(key)
         if want and (buf is None or buf.numel() < want):
@@ -52,6 +54,10 @@ _POOL = _StatsPool()
 
 
 def new_stats_workspace(C_, device):
+    """[32, 2, C] zeroed workspace for statistics fused into a GEMM epilogue (atomic shards), or None in
+    the deterministic mode: the consumer then runs the fixed-order ``bn_stats`` sweep instead."""
+    if _det.enabled():
+        return None
     if torch.device(device).type == "cuda":
         return _POOL.get(C_, device)
     return torch.zeros((SHARDS, 2, C_), dtype=torch.float32, device=device)

@@ -17,7 +17,7 @@ Protocol:
   * collectives of gradient buckets are launched with :func:`on_grad_stream` too, so RCCL orders
     them after the side-stream weight gradients AND the main-stream BatchNorm parameter gradients.
 
-Where it pays is measured per model (``scripts/gpu_r3_ab.sh``, interleaved on one box,
+Where it pays is measured per model (interleaved A/B on one box,
 ``profiles/r3/ab_wgrad_stream.jsonl``): BERT-base +2.5-2.8 % tokens/s (the wgrad GEMMs overlap the
 attention / LayerNorm backward); ResNet-50 unchanged (every bottleneck kernel already fills the chip,
 so the side stream's workgroups only take slots the main stream frees); VGG-16 slower (its step is
@@ -38,6 +38,10 @@ _PENDING: dict = {}
 
 
 def enabled(default: bool = True) -> bool:
+    from . import scope as _scope
+
+    if _scope.tag():  # replica-group steps run on their own streams: no shared side stream
+        return False
     v = os.environ.get("DDL_WGRAD_STREAM", "auto")
     return default if v == "auto" else v != "0"
 

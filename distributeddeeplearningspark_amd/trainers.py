@@ -42,7 +42,6 @@ Execution (MI355X-native, not a socket parameter server):
 """
 from __future__ import annotations
 
-import copy
 import os
 import time
 import warnings
@@ -134,6 +133,14 @@ class _ShardFeed:
             else:
                 for b in range(nb):
                     yield self.X[b * bs:(b + 1) * bs], self.Y[b * bs:(b + 1) * bs]
+
+
+def _allreduce_sum(pg, t):
+    """In-place sum of a flat fp32 buffer over the workers' group (bucketed, RCCL on GPUs)."""
+    if pg.distributed:
+        from .parallel.ddp import all_reduce_flat
+
+        all_reduce_flat(pg, t, 64 << 20)
 
 
 class _Worker:
@@ -345,10 +352,7 @@ class _CommitWorker(_Worker):
             a.sync_compute()
 
     def _allreduce(self, t):
-        if self.pg.distributed:
-            from .parallel.ddp import all_reduce_flat
-
-            all_reduce_flat(self.pg, t, 64 << 20)
+        _allreduce_sum(self.pg, t)
 
 
 class _AsyncPSWorker(_Worker):
@@ -433,7 +437,7 @@ class _AveragingWorker(_Worker):
         W = self.arena.master.detach()
         with torch.no_grad():
             if self.pg.distributed:
-                _CommitWorker._allreduce(self, W)
+                _allreduce_sum(self.pg, W)
                 W.div_(self.pg.world_size)
             self.arena.sync_compute()
         return W.clone()
@@ -670,9 +674,13 @@ class _ShardedTrainer(Trainer):
         if cfg.get("mode") == "async" and issubclass(_WORKERS[self.algorithm], _CommitWorker):
             server = self._start_async_server(cfg)
         try:
-            args = [(cfg, self.master_model, Xs[r], Ys[r], sizes) for r in range(self.num_workers)]
-            results = run_workers(_train_worker, self.num_workers, args, device=self.device,
-                                  max_restarts=self.extra.get("max_restarts"))
+            devices = self._replica_devices(cfg, server)
+            if devices is not None:
+                results = self._train_replica_groups(cfg, Xs, Ys, sizes, devices)
+            else:
+                args = [(cfg, self.master_model, Xs[r], Ys[r], sizes) for r in range(self.num_workers)]
+                results = run_workers(_train_worker, self.num_workers, args, device=self.device,
+                                      max_restarts=self.extra.get("max_restarts"))
         finally:
             if server is not None:
                 center, n_upd = server.center().numpy().copy(), server.num_updates
@@ -691,6 +699,37 @@ class _ShardedTrainer(Trainer):
         model = ps.get_model()
         self.record_training_end()
         return model
+
+    def _replica_devices(self, cfg, server):
+        """The worker -> device plan when the co-located workers run as in-process replica groups
+        (``parallel/replicas.py``), else None (one OS process per worker)."""
+        from .parallel import replicas as _rep
+        from .parallel.launcher import plan_devices
+
+        if server is not None or self.num_workers < 2 or int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            return None
+        if cfg.get("checkpoint_dir") or cfg.get("watchdog_s") or self.extra.get("max_restarts"):
+            return None  # per-rank checkpoints / watchdog / restart live on the process-per-worker path
+        devices = plan_devices(self.num_workers, self.device)
+        return devices if _rep.applies(cfg, devices) else None
+
+    def _train_replica_groups(self, cfg, Xs, Ys, sizes, devices):
+        from .parallel import comm
+        from .parallel import replicas as _rep
+
+        groups = _rep.plan(devices)
+        if len(groups) == 1:  # one device: the replicas train in this process (no executor hop)
+            g = groups[0]
+            dev = torch.device(devices[g[0]])
+            if dev.type == "cuda":
+                torch.cuda.set_device(dev)
+            pg = comm.ProcessGroup(0, 1, 0, dev, None)
+            res = _rep.train_group(0, 1, pg, cfg, self.master_model, [Xs[r] for r in g], [Ys[r] for r in g], g, sizes)
+        else:  # one executor process per device, partial sums all-reduced over RCCL
+            args = [(cfg, self.master_model, [Xs[r] for r in g], [Ys[r] for r in g], g, sizes) for g in groups]
+            per = run_workers(_rep.train_group, len(groups), args, device=self.device)
+            res = [x for grp in per for x in grp]
+        return sorted(res, key=lambda r: r["rank"])
 
 
     def _start_async_server(self, cfg):
@@ -849,4 +888,3 @@ SyncDP = SynchronousDataParallel
 __all__ = ["Trainer", "SingleTrainer", "AveragingTrainer", "EnsembleTrainer", "DistributedTrainer",
            "AsynchronousDistributedTrainer", "ADAG", "DynSGD", "DOWNPOUR", "EASGD", "AEASGD", "EAMSGD",
            "SynchronousDataParallel", "SyncDP", "ParameterServer"]
-_ = copy

@@ -317,6 +317,23 @@ def test_async_two_workers_train(spark, algo):
     assert acc > 0.5, acc
 
 
+def test_uint8_images_are_scaled_unless_normalisation_declared():
+    """4-D uint8 NHWC batches are images: x / 255 by default, (x - mean) / std when the model
+    declares input_mean / input_std; 2-D integer columns keep their values."""
+    from distributeddeeplearningspark_amd.models import Conv2D, Flatten
+
+    m = Sequential([Conv2D(2, (3, 3), input_shape=(4, 4, 3)), Flatten(), Dense(1)])
+    m.place("cpu")
+    x = np.arange(2 * 4 * 4 * 3, dtype=np.uint8).reshape(2, 4, 4, 3) * 2
+    torch.testing.assert_close(m.to_input(x), torch.from_numpy(x.astype(np.float32) / 255.0))
+    m.input_mean, m.input_std = (10.0, 20.0, 30.0), (2.0, 4.0, 8.0)
+    ref = (x.astype(np.float32) - np.array([10.0, 20.0, 30.0], np.float32)) / np.array([2.0, 4.0, 8.0], np.float32)
+    torch.testing.assert_close(m.to_input(x), torch.from_numpy(ref))
+    flat = Sequential([Dense(1, input_shape=(6,))])
+    flat.place("cpu")
+    torch.testing.assert_close(flat.to_input(np.full((2, 6), 7, np.uint8)), torch.full((2, 6), 7.0))
+
+
 def test_integer_feature_column_trains_and_predicts_as_float(spark):
     """uint8 / int64 2-D feature columns reach Dense as their values in the compute dtype
     (partition_arrays keeps column dtypes; Model.to_input casts non-image integers)."""
@@ -381,3 +398,32 @@ def test_partitions_reach_executors_through_shared_memory(spark, monkeypatch):
     for a, b in zip(w_shm, w_pk):
         np.testing.assert_array_equal(a, b)
     assert not any(glob.glob("/dev/shm/" + n) for n in names)  # unlinked with the pool
+
+
+def test_shared_shards_follow_in_place_mutation(spark, monkeypatch):
+    """A shard cached in /dev/shm is re-validated by content hash: modifying the user's array in place
+    between two train() calls trains on the NEW values (no stale shared-memory copy)."""
+    from distributeddeeplearningspark_amd.parallel import executors as EX
+    from distributeddeeplearningspark_amd.sql.dataframe import from_columns
+    from distributeddeeplearningspark_amd.trainers import ADAG
+
+    rng = np.random.default_rng(6)
+    X = rng.normal(size=(4096, 64)).astype(np.float32)
+    y = (X[:, :1] * 0.5).astype(np.float32)
+
+    def train(thr):
+        monkeypatch.setenv("DDL_SHM_MIN_MB", thr)
+        m = Sequential([Dense(1, input_shape=(64,))])
+        m.set_weights([np.full((64, 1), 0.01, np.float32), np.zeros(1, np.float32)])
+        tr = ADAG(keras_model=m, worker_optimizer="sgd", loss="mean_squared_error", num_workers=2, batch_size=64,
+                  communication_window=2, num_epoch=1, features_col="features", label_col="label", device="cpu")
+        return tr.train(from_columns({"features": X, "label": y}, num_partitions=2)).get_weights()
+
+    train("0.01")  # blocks created for the original values
+    X *= 3.0  # in place: same buffer, same id, new content
+    w_shm = train("0.01")
+    EX.shutdown_all()
+    w_ref = train("100000")  # pickle path: always ships the current values
+    EX.shutdown_all()
+    for a, b in zip(w_shm, w_ref):
+        np.testing.assert_array_equal(a, b)

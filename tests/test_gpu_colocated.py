@@ -1,7 +1,11 @@
-"""Co-located dist-keras workers on ONE MI355X (DDL_WORKERS_PER_GPU): commits go through the
-device-side IPC exchange (parallel/colocated.py) and the fused HIP commit kernels.  The result
-must equal the host-staged gloo path (same arithmetic, one summation order), and the update
-law / replica semantics must hold for ADAG, DynSGD and EASGD."""
+"""Co-located dist-keras workers on ONE MI355X (DDL_WORKERS_PER_GPU).
+
+Default: the workers run as in-process replica groups (parallel/replicas.py: graph-replayed
+windows on one HIP stream per replica, one commit kernel over all replicas).  With
+DDL_REPLICA_GROUPS=0 they are separate processes whose commits go through the device-side IPC
+exchange (parallel/colocated.py) or, with DDL_COLOCATED_EXCHANGE=0, the host-staged gloo path.
+All three must give the same center (one summation order), the same update law and the same
+per-worker loss histories for ADAG, DynSGD and EASGD."""
 import os
 
 import numpy as np
@@ -28,11 +32,12 @@ def _model():
     return m
 
 
-def _train(algo, exchange, monkeypatch):
+def _train(algo, exchange, monkeypatch, groups="0"):
     from distributeddeeplearningspark_amd import trainers as T
     from distributeddeeplearningspark_amd.parallel.executors import shutdown_all
 
     monkeypatch.setenv("DDL_WORKERS_PER_GPU", "4")
+    monkeypatch.setenv("DDL_REPLICA_GROUPS", groups)
     monkeypatch.setenv("DDL_COLOCATED_EXCHANGE", "1" if exchange else "0")
     cls = {"adag": T.ADAG, "dynsgd": T.DynSGD, "easgd": T.EASGD}[algo]
     kw = dict(keras_model=_model(), worker_optimizer="adam", loss="mean_squared_error", num_workers=4,
@@ -54,3 +59,17 @@ def test_colocated_exchange_matches_host_staged(algo, monkeypatch):
     assert all(r["commit_wait_s"] is not None for r in res_dev), "device exchange was not used"
     assert all(r["commit_wait_s"] is None for r in res_host)
     torch.testing.assert_close(w_dev, w_host, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("algo", ["adag", "dynsgd", "easgd"])
+def test_replica_group_matches_process_workers(algo, monkeypatch):
+    w_grp, n_grp, res_grp = _train(algo, True, monkeypatch, groups="1")
+    w_ipc, n_ipc, res_ipc = _train(algo, True, monkeypatch, groups="0")
+    assert n_grp == n_ipc
+    assert all(r.get("replica_group", {}).get("replicas") == 4 for r in res_grp), "replica group not used"
+    assert all(r["graph"] for r in res_grp), "replica windows were not graph-replayed"
+    assert all(r["commit_wait_s"] is not None for r in res_ipc)
+    torch.testing.assert_close(w_grp, w_ipc, rtol=1e-4, atol=1e-5)
+    for a, b in zip(res_grp, res_ipc):
+        assert len(a["history"]) == len(b["history"])
+        np.testing.assert_allclose(a["history"], b["history"], rtol=1e-3, atol=1e-5)

@@ -1,0 +1,124 @@
+"""Convergence parity at the reference's own validation level.
+
+The reference validates by the trained model's quality: test MAPE of the NYISO GRU / LSTM
+(2.81 % / 3.59 %, ``/root/reference/ddl_nyiso_hdi.ipynb:730,934``) and MNIST accuracy
+(``/root/reference/ddl_mnist_aztk.py:223``).  Here:
+
+  (a) the NYISO workflow at the reference hyper-parameters (ADAG, 4 workers, batch 32, window 5,
+      20 epochs) trained on the GPU (replica group of 4 on one MI355X, fp32 HIP recurrences) and on
+      CPU fp32 executors (torch) from the same synthetic data and seeds reach the same test MAPE;
+  (b) the MNIST workflow with 8 co-located workers (the reference's 4 executors x 2 cores) reaches
+      >= 95 % accuracy on the synthetic, separable MNIST-shape set;
+  (c) a full-depth ResNet-50 (16 bottlenecks, 64x64) trained 150 SGD steps on a learnable synthetic
+      10-class task follows the loss curve of the same bf16 model through PyTorch/MIOpen
+      (``DDL_BACKEND=torch``) and classifies held-out samples at >= 90 %.
+The synthetic data are not the reference's CSVs (no network), so MAPE parity with the notebook is
+unpinned; parity between our two implementations of the same workflow is what these tests pin.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "examples"))
+DEV = "cuda:0"
+
+
+@pytest.fixture(autouse=True)
+def _fresh_session():
+    from distributeddeeplearningspark_amd.context import SparkContext, SparkSession
+
+    yield
+    if SparkSession._active is not None:
+        SparkSession._active.stop()
+    if SparkContext._active is not None:
+        SparkContext._active.stop()
+
+
+def _nyiso(device, tmp_path, monkeypatch):
+    import ddl_nyiso
+
+    if device != "cpu":
+        monkeypatch.setenv("DDL_WORKERS_PER_GPU", "4")
+    return ddl_nyiso.main(["--workers", "4", "--epochs", "20", "--device", device, "--hours", "11712",
+                           "--csv", str(tmp_path / f"nyiso_{device.replace(':', '')}.csv")])
+
+
+def test_nyiso_gpu_mape_matches_cpu_fp32(tmp_path, monkeypatch):
+    gpu = _nyiso("auto", tmp_path, monkeypatch)["results"]
+    cpu = _nyiso("cpu", tmp_path, monkeypatch)["results"]
+    report = {k: (round(gpu[k]["mape"], 3), round(cpu[k]["mape"], 3)) for k in ("GRU", "LSTM")}
+    print("NYISO test MAPE (gpu, cpu fp32):", report)
+    for cell in ("GRU", "LSTM"):
+        g, c = gpu[cell], cpu[cell]
+        assert g["updates"] == c["updates"] == 1440, (cell, g["updates"], c["updates"])
+        assert g["mape"] < 6.0 and c["mape"] < 6.0, report
+        assert abs(g["mape"] - c["mape"]) < 0.5, report
+
+
+def test_mnist_8_colocated_workers_accuracy(monkeypatch, capsys):
+    import ddl_mnist
+
+    monkeypatch.setattr(sys, "argv", ["ddl_mnist.py", "--executors", "4", "--processes", "2", "--epochs", "5",
+                                      "--train-rows", "60000", "--test-rows", "10000", "--workers-per-gpu", "8"])
+    trainer, _ = ddl_mnist.main()
+    out = capsys.readouterr().out
+    assert trainer.parameter_server.num_updates == 3744  # 8 x floor(5 x floor(7500 / 16) / 5)
+    acc = float(out.strip().splitlines()[-2].split(": ")[1])
+    print("MNIST 8 co-located workers: accuracy", acc, "training time", trainer.get_training_time())
+    assert acc >= 0.95, acc
+    assert all(r.get("replica_group") for r in trainer._results)
+
+
+def _templates(seed=0):
+    g = torch.Generator().manual_seed(seed)
+    # smooth class templates (4x4 random blocks upsampled) so the task needs spatial features
+    t = torch.randn(10, 3, 8, 8, generator=g)
+    t = torch.nn.functional.interpolate(t, size=(64, 64), mode="bilinear", align_corners=False)
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+def _batch(tmpl, n, g):
+    y = torch.randint(0, 10, (n,), generator=g)
+    x = tmpl[y] + 0.8 * torch.randn(n, 64, 64, 3, generator=g)
+    return x, y
+
+
+def test_resnet50_learns_synthetic_task_like_torch_path(monkeypatch):
+    from distributeddeeplearningspark_amd.models import ResNet50
+    from distributeddeeplearningspark_amd.models.optimizers import SGD
+
+    tmpl = _templates()
+    curves, accs = {}, {}
+    for name, backend in (("hip", None), ("torch", "torch")):
+        if backend:
+            monkeypatch.setenv("DDL_BACKEND", backend)
+        else:
+            monkeypatch.delenv("DDL_BACKEND", raising=False)
+        torch.manual_seed(0)
+        m = ResNet50(input_shape=(64, 64, 3), num_classes=10)
+        m.compile(SGD(lr=0.05, momentum=0.9), "sparse_categorical_crossentropy")
+        m.place(DEV, seed=1)
+        g = torch.Generator().manual_seed(2)
+        losses = []
+        for _ in range(150):
+            x, y = _batch(tmpl, 32, g)
+            losses.append(float(m.train_on_batch(m.to_input(x), m.to_target(y))))
+        xt, yt = _batch(tmpl, 512, torch.Generator().manual_seed(99))
+        pred = m.predict(xt.numpy(), batch_size=128).argmax(1)
+        curves[name] = np.array(losses)
+        accs[name] = float((pred == yt.numpy()).mean())
+    win = lambda c, a, b: float(c[a:b].mean())
+    summary = {k: [round(win(c, a, a + 10), 3) for a in (0, 30, 70, 140)] for k, c in curves.items()}
+    print("ResNet-50 64x64 synthetic task: loss windows", summary, "held-out accuracy", accs)
+    h, t = curves["hip"], curves["torch"]
+    assert np.isfinite(h).all()
+    assert win(h, 140, 150) < 0.5 * win(h, 0, 10), summary  # it learns
+    for a in (0, 30, 70, 140):  # the smoothed curve stays in a band around the library path's
+        assert abs(win(h, a, a + 10) - win(t, a, a + 10)) < max(0.35, 0.35 * win(t, a, a + 10)), summary
+    assert accs["hip"] >= 0.9, accs

@@ -1,0 +1,73 @@
+"""In-process replica groups (parallel/replicas.py) vs the process-per-worker trainers on CPU.
+
+The replica schedule (round j: contributors train k steps, exhausted workers run their leftover
+steps, then ONE commit over all replicas) must reproduce the multi-process gloo run of the same
+dist-keras trainer: same center to fp32 rounding, same num_updates and per-worker loss histories.
+Shards of unequal size make the last rounds have fewer contributors (zero commits)."""
+import numpy as np
+import pytest
+
+from distributeddeeplearningspark_amd.context import SparkSession
+from distributeddeeplearningspark_amd.models import Dense, Sequential
+
+
+@pytest.fixture(scope="module")
+def spark():
+    return SparkSession.builder.master("local[2]").getOrCreate()
+
+
+def _frame(spark, n=70):
+    rng = np.random.default_rng(3)
+    x = rng.normal(size=(n, 5)).astype(np.float32)
+    y = (x @ np.arange(1, 6, dtype=np.float32)[:, None] * 0.1 + 0.3).astype(np.float32)
+    return spark.createDataFrame({"f": list(x), "l": list(y)}).repartition(3)
+
+
+def _train(spark, monkeypatch, algo, groups, opt="adam"):
+    from distributeddeeplearningspark_amd import trainers as T
+
+    monkeypatch.setenv("DDL_REPLICA_GROUPS", groups)
+    base = Sequential([Dense(4, activation="relu", input_shape=(5,)), Dense(1)])
+    base.set_weights([np.full_like(w, 0.05 * (i + 1)) + np.linspace(-0.1, 0.1, w.size, dtype=np.float32).reshape(w.shape)
+                      for i, w in enumerate(base.get_weights())])
+    cls = getattr(T, algo)
+    kw = dict(keras_model=base, worker_optimizer=opt, loss="mean_squared_error", num_workers=3, batch_size=4,
+              num_epoch=2, features_col="f", label_col="l", device="cpu")
+    if algo != "AveragingTrainer":
+        kw["communication_window"] = 3
+    tr = cls(**kw)
+    model = tr.train(_frame(spark))
+    return tr, model.get_weights()
+
+
+@pytest.mark.parametrize("algo", ["ADAG", "DynSGD", "DOWNPOUR", "AEASGD", "AveragingTrainer"])
+def test_replica_group_matches_process_workers(spark, monkeypatch, algo):
+    tr_p, w_p = _train(spark, monkeypatch, algo, "0")
+    tr_g, w_g = _train(spark, monkeypatch, algo, "1")
+    assert tr_g._results[0].get("replica_group") == {"group": 0, "groups": 1, "replicas": 3}
+    assert "replica_group" not in tr_p._results[0]
+    assert tr_g.parameter_server.num_updates == tr_p.parameter_server.num_updates
+    if algo != "AveragingTrainer":
+        # 70 rows -> shards 24/23/23 -> 6/5/5 batches x 2 epochs -> 12/10/10 steps -> 4/3/3 commits
+        assert tr_g.parameter_server.num_updates == 10
+    hp, hg = tr_p.get_history(), tr_g.get_history()
+    assert [len(h) for h in hg] == [len(h) for h in hp] == [12, 10, 10]
+    for a, b in zip(hp, hg):
+        np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-6)
+    for a, b in zip(w_p, w_g):
+        np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-6)
+
+
+def test_replica_groups_not_used_for_async_or_syncgrad(spark, monkeypatch):
+    from distributeddeeplearningspark_amd.parallel import replicas
+
+    monkeypatch.setenv("DDL_REPLICA_GROUPS", "1")
+    assert not replicas.applies({"algorithm": "adag", "mode": "async"}, ["cpu", "cpu"])
+    assert not replicas.applies({"algorithm": "adag", "mode": "sync-grad"}, ["cpu", "cpu"])
+    assert not replicas.applies({"algorithm": "syncdp"}, ["cpu", "cpu"])
+    assert replicas.applies({"algorithm": "dynsgd"}, ["cpu", "cpu"])
+    monkeypatch.setenv("DDL_REPLICA_GROUPS", "auto")
+    assert not replicas.applies({"algorithm": "adag"}, ["cpu", "cpu"])  # CPU: processes by default
+    assert replicas.applies({"algorithm": "adag"}, ["cuda:0", "cuda:0"])
+    assert not replicas.applies({"algorithm": "adag"}, ["cuda:0", "cuda:1"])  # one worker per GPU
+    assert replicas.plan(["cuda:0", "cuda:1", "cuda:0", "cuda:1"]) == [[0, 2], [1, 3]]
