@@ -136,7 +136,8 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = True) ->
     if not rebuilt and OUT.exists() and OUT.stat().st_mtime >= max(o.stat().st_mtime for o in objs):
         return OUT
     _, tlib = _torch_paths()
-    link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(OUT),
+    tmp = OUT.with_name(OUT.name + ".tmp")  # link aside, then an atomic rename: a reader never sees half a library
+    link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(tmp),
             f"-L{tlib}", f"-Wl,-rpath,{tlib}",
             "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-lc10", "-lc10_hip", "-ltorch_python",
             f"-L{ROCM}/lib", f"-Wl,-rpath,{ROCM}/lib", "-lrocprofiler-sdk-roctx",
@@ -144,6 +145,7 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = True) ->
     r = subprocess.run(link, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed\n{' '.join(link)}\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, OUT)
     if verbose:
         print(f"[ddl-build] linked {OUT} ({len(objs)} objects)", flush=True)
     (BUILD / "manifest.json").write_text(json.dumps({"arch": ARCH, "objects": [o.name for o in objs]}, indent=1))

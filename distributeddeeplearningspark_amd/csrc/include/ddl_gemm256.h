@@ -148,7 +148,7 @@ __global__ __launch_bounds__(g256::THREADS, 1) void gemm256_kernel(const GemmPar
   __builtin_amdgcn_s_setprio(1);                                                                 \
   _Pragma("unroll") for (int kk = 0; kk < 2; ++kk) _Pragma("unroll") for (int i = 0; i < 4; ++i) \
       _Pragma("unroll") for (int j = 0; j < 2; ++j) {                                            \
-    if constexpr (EPI == EPI_BF16)                                                               \
+    if constexpr (epi_dt(EPI))                                                                   \
       acc[QM][QN][i][j] = mfma16x16x32(br[j][kk], ar[i][kk], acc[QM][QN][i][j]);                 \
     else                                                                                         \
       acc[QM][QN][i][j] = mfma16x16x32(ar[i][kk], br[j][kk], acc[QM][QN][i][j]);                 \

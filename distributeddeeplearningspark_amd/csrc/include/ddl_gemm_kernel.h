@@ -1035,8 +1035,13 @@ inline int launch_tile(const GemmParams& p, hipStream_t s) {
 }
 
 // The bf16 epilogue features a call uses beyond bias / ReLU / statistics.
+// DDL_GEMM_FULL_EPI=1 forces the full instantiation (A/B of the epilogue's code size on plain GEMMs).
 inline bool needs_full_epilogue(const GemmParams& p) {
-  return p.om.enabled || p.resid || p.aux || p.drop_thresh || p.relu > ACT_RELU;
+  static const bool force = [] {
+    const char* e = getenv("DDL_GEMM_FULL_EPI");
+    return e && atoi(e) == 1;
+  }();
+  return force || p.om.enabled || p.resid || p.aux || p.drop_thresh || p.relu > ACT_RELU;
 }
 
 template <int AMODE, int BMODE, int EPI, bool BNORM = false>

@@ -55,6 +55,9 @@ int rows_sum_scaled(const float* rows, long n, float scale, const float* dev, fl
 int scale_bf16_dev(void* x, long n, const float* s_dev, hipStream_t s);
 // loss[0] = mean((pred - target)^2); grad = 2 (pred - target) / n  (fp32, one launch)
 int mse_fwd_bwd(const float* pred, const float* target, long n, float* loss, float* grad, hipStream_t s);
+// Keras CE on probabilities: loss_rows[b] = -sum y log clip(p), dp = -scale * y / p inside the clip range
+int prob_xent(const float* p, const int64_t* labels, const float* target, float* loss_rows, float* dp, int B, int K,
+              float eps, float scale, int ignore_index, hipStream_t s);
 
 // ---------------- elementwise ----------------
 int cast_f32_bf16(const float* x, void* y, long n, hipStream_t s);

@@ -186,6 +186,42 @@ int rows_sum_scaled(const float* rows, long n, float scale, const float* dev, fl
   return (int)hipGetLastError();
 }
 
+// Keras categorical cross-entropy on PROBABILITIES (a model whose softmax output is not fused into the loss,
+// or any probability head): loss_rows[b] = -sum_k y[b][k] log(clip(p[b][k], eps, 1 - eps)) and, in the same
+// sweep, dp[b][k] = -scale * y[b][k] / p[b][k] inside the clip range (0 outside: the clip's gradient).
+// y is the one-hot row of labels[b] (sparse form; ignore_index rows contribute nothing) or target[b][k].
+// One wave per row, lanes over the classes.
+__global__ __launch_bounds__(256) void prob_xent_kernel(const float* __restrict__ p, const int64_t* __restrict__ labels,
+                                                        const float* __restrict__ target, float* __restrict__ loss_rows,
+                                                        float* __restrict__ dp, int B, int K, float eps, float scale,
+                                                        int ignore_index) {
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (b >= B) return;
+  const float* pr = p + (long)b * K;
+  float* dr = dp + (long)b * K;
+  const long lab = labels ? labels[b] : -1;
+  const bool skip = labels && (lab == ignore_index || lab < 0 || lab >= K);
+  float acc = 0.f;
+  for (int k = lane; k < K; k += 64) {
+    const float y = labels ? ((!skip && k == lab) ? 1.f : 0.f) : target[(long)b * K + k];
+    const float pv = pr[k];
+    const float pc = fminf(fmaxf(pv, eps), 1.f - eps);
+    acc -= y * __logf(pc);
+    dr[k] = (pv > eps && pv < 1.f - eps) ? -scale * y / pv : 0.f;
+  }
+  acc = warp_sum(acc);
+  if (lane == 0) loss_rows[b] = acc;
+}
+
+int prob_xent(const float* p, const int64_t* labels, const float* target, float* loss_rows, float* dp, int B, int K,
+              float eps, float scale, int ignore_index, hipStream_t s) {
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(prob_xent_kernel, dim3((B + 3) / 4), dim3(256), 0, s, p, labels, target, loss_rows, dp, B, K, eps,
+                     scale, ignore_index);
+  return (int)hipGetLastError();
+}
+
 // Mean squared error (Keras 'mean_squared_error') forward AND backward in one sweep:
 // loss[0] = mean((p - t)^2), grad = 2 (p - t) / n.  One 1024-thread workgroup (regression
 // heads are small: the reference's Dense(1) over a batch of 32).

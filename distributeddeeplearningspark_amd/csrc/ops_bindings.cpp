@@ -428,6 +428,19 @@ void step_record_(const at::Tensor& loss, c10::optional<at::Tensor> hist, const 
   HIP_OK(step_record(loss.data_ptr<float>(), optr<float>(hist), hist ? (int)hist->numel() : 0, ctr.data_ptr<int>(),
                      cur_stream()));
 }
+void prob_xent_(const at::Tensor& p, c10::optional<at::Tensor> labels, c10::optional<at::Tensor> target,
+                const at::Tensor& loss_rows, const at::Tensor& dp, double eps, double scale, int64_t ignore_index) {
+  GPU(p); F32(p); F32(loss_rows); F32(dp);
+  CK(p.dim() == 2 && dp.sizes() == p.sizes() && loss_rows.numel() == p.size(0), "prob_xent: p [B, K], dp, loss_rows [B]");
+  CK((labels.has_value()) != (target.has_value()), "prob_xent: labels OR target");
+  if (labels) CK(labels->scalar_type() == at::kLong && labels->is_contiguous() && labels->numel() == p.size(0),
+                 "prob_xent: int64 labels [B]");
+  if (target) { F32(*target); CK(target->sizes() == p.sizes(), "prob_xent: target [B, K]"); }
+  at::DeviceGuard g(p.device());
+  HIP_OK(prob_xent(p.data_ptr<float>(), labels ? labels->data_ptr<int64_t>() : nullptr, optr<const float>(target),
+                   loss_rows.data_ptr<float>(), dp.data_ptr<float>(), (int)p.size(0), (int)p.size(1), (float)eps,
+                   (float)scale, (int)ignore_index, cur_stream()));
+}
 void mse_fwd_bwd_(const at::Tensor& pred, const at::Tensor& target, const at::Tensor& loss, const at::Tensor& grad) {
   F32(pred); F32(target); F32(loss); F32(grad);
   CK(pred.is_cuda() && pred.numel() == target.numel() && grad.numel() == pred.numel() && loss.numel() == 1,
@@ -533,6 +546,7 @@ void register_ops(py::module& m) {
         py::arg("bc1"), py::arg("bc2"), py::arg("gscale"), py::arg("tstep") = py::none());
   m.def("step_tick", &step_tick_);
   m.def("mse_fwd_bwd", &mse_fwd_bwd_);
+  m.def("prob_xent", &prob_xent_);
   m.def("commit_delta", &commit_delta_);
   m.def("commit_apply", &commit_apply_);
   m.def("commit_replicas", &commit_replicas_, "one commit round over R co-located replicas", py::arg("ws"),

@@ -353,8 +353,8 @@ class Model(Layer):
             return L.binary_crossentropy(out, yy)
         if name == "categorical_crossentropy":
             return L.categorical_crossentropy_probs(out, yy)
-        if name == "sparse_categorical_crossentropy":
-            return torch.nn.functional.nll_loss(torch.log(out.clamp_min(1e-7)), y.long().reshape(-1))
+        if name == "sparse_categorical_crossentropy":  # probability output (no fused softmax): HIP on the GPU
+            return L.prob_cross_entropy(out.reshape(out.shape[0], -1), labels=y.reshape(-1))
         raise ValueError(f"unsupported loss {name!r}")
 
     def backward_step(self, x, y):

@@ -91,7 +91,47 @@ def binary_crossentropy(pred, target, eps=1e-7):
     return -(t * torch.log(p) + (1 - t) * torch.log(1 - p)).mean()
 
 
+class _ProbXentFn(torch.autograd.Function):
+    """Keras cross-entropy on probabilities (``-sum y log clip(p, eps, 1 - eps)``, batch mean): one HIP
+    sweep writes the per-row losses and d loss / d p; a second reduces the rows (no ATen on the GPU)."""
+
+    @staticmethod
+    def forward(ctx, probs, labels, target, eps, ignore_index):
+        p = probs.float().contiguous()
+        B = p.shape[0]
+        rows = torch.empty(B, dtype=torch.float32, device=p.device)
+        dp = torch.empty_like(p)
+        C().prob_xent(p, None if labels is None else labels.to(torch.int64).contiguous(),
+                      None if target is None else target.float().contiguous(), rows, dp, float(eps), 1.0 / B,
+                      int(ignore_index))
+        loss = torch.empty((), dtype=torch.float32, device=p.device)
+        C().rows_sum_scaled(rows, 1.0 / B, None, loss.view(1))
+        ctx.save_for_backward(dp)
+        ctx.in_dtype = probs.dtype
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (dp,) = ctx.saved_tensors
+        return (dp * g).to(ctx.in_dtype), None, None, None, None
+
+
+def prob_cross_entropy(probs, labels=None, target=None, eps=1e-7, ignore_index=-100):
+    """Mean Keras CE of probability rows ``probs`` [B, K] against class ``labels`` [B] (sparse form) or
+    target rows [B, K] (``categorical_crossentropy`` on a model whose softmax is an output layer)."""
+    if (labels is None) == (target is None):
+        raise ValueError("pass exactly one of labels / target")
+    if use_native(probs):
+        return _ProbXentFn.apply(probs, labels, target, eps, ignore_index)
+    p = probs.float().clamp(eps, 1 - eps)
+    if labels is not None:
+        lab = labels.long().reshape(-1)
+        keep = (lab != ignore_index) & (lab >= 0) & (lab < p.shape[1])
+        picked = torch.log(p.gather(1, lab.clamp(0, p.shape[1] - 1)[:, None])[:, 0])
+        return -(picked * keep).sum() / p.shape[0]
+    return -(target.float() * torch.log(p)).sum(-1).mean()
+
+
 def categorical_crossentropy_probs(probs, target, eps=1e-7):
     """Keras semantics on already-softmaxed outputs: -sum(y*log(clip(p)))."""
-    p = probs.float().clamp(eps, 1 - eps)
-    return -(target.float() * torch.log(p)).sum(-1).mean()
+    return prob_cross_entropy(probs.reshape(probs.shape[0], -1), target=target.reshape(probs.shape[0], -1), eps=eps)

@@ -39,12 +39,25 @@ def timeit(fn, iters=20):
     return s.elapsed_time(e) / iters
 
 
+def _shapes(argv):
+    """Named shapes (comma list) or ad-hoc ``MxNxK[:rc]`` entries (``:rc`` = B row-contiguous)."""
+    if not argv:
+        return SHAPES
+    out = []
+    for tok in argv[0].split(","):
+        named = [s for s in SHAPES if s[0] == tok]
+        if named:
+            out += named
+            continue
+        dims, _, mode = tok.partition(":")
+        M, N, K = (int(v) for v in dims.split("x"))
+        out.append((tok, M, N, K, G.KC, G.RC if mode == "rc" else G.KC))
+    return out
+
+
 def main():
     torch.manual_seed(0)
-    only = sys.argv[1].split(",") if len(sys.argv) > 1 else None
-    for name, M, N, K, am, bm in SHAPES:
-        if only and name not in only:
-            continue
+    for name, M, N, K, am, bm in _shapes(sys.argv[1:]):
         A = torch.randn(M, K, device="cuda").to(torch.bfloat16)
         B = torch.randn(N, K, device="cuda").to(torch.bfloat16)
         a_t = A if am == G.KC else A.T.contiguous()

@@ -427,3 +427,15 @@ def test_shared_shards_follow_in_place_mutation(spark, monkeypatch):
     EX.shutdown_all()
     for a, b in zip(w_shm, w_ref):
         np.testing.assert_array_equal(a, b)
+
+
+def test_prob_cross_entropy_cpu_matches_keras_formula():
+    from distributeddeeplearningspark_amd.ops.loss import prob_cross_entropy
+
+    g = torch.Generator().manual_seed(0)
+    p = torch.softmax(torch.randn(9, 5, generator=g) * 4, -1)
+    lab = torch.randint(0, 5, (9,), generator=g)
+    y = torch.nn.functional.one_hot(lab, 5).float()
+    ref = -(y * torch.log(p.clamp(1e-7, 1 - 1e-7))).sum(-1).mean()
+    assert torch.allclose(prob_cross_entropy(p, labels=lab), ref, atol=1e-6)
+    assert torch.allclose(prob_cross_entropy(p, target=y), ref, atol=1e-6)

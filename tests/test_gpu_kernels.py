@@ -367,6 +367,41 @@ def test_softmax_xent(dtype):
     close(lg2.grad, lr.grad, rtol=2e-2, atol=1e-4, what="xent(probs) grad")
 
 
+@pytest.mark.parametrize("form", ["sparse", "dense"])
+def test_prob_xent_matches_fp32(form):
+    """Keras CE on probabilities (a softmax OUTPUT layer, not fused into the loss): the HIP sweep
+    (ops/loss.py prob_cross_entropy) vs the clipped fp32 formula, loss and d loss / d p, including
+    probabilities below the clip (zero gradient) and an ignored label."""
+    from distributeddeeplearningspark_amd.ops.loss import prob_cross_entropy
+
+    B, K = 37, 10
+    p = torch.softmax(rnd(B, K, scale=6.0, dtype=torch.float32, seed=41), dim=-1)
+    p[0, 3] = 1e-9  # below the clip
+    labels = torch.randint(0, K, (B,), device=DEV)
+    labels[0] = 3
+    y = F.one_hot(labels, K).float()
+    pg = p.clone().requires_grad_(True)
+    loss = prob_cross_entropy(pg, labels=labels) if form == "sparse" else prob_cross_entropy(pg, target=y)
+    loss.backward()
+    pr = p.clone().requires_grad_(True)
+    ref = -(y * torch.log(pr.clamp(1e-7, 1 - 1e-7))).sum(-1).mean()
+    ref.backward()
+    assert abs(loss.item() - ref.item()) < 1e-5 * max(1.0, abs(ref.item())), (loss.item(), ref.item())
+    close(pg.grad, pr.grad, rtol=1e-5, atol=1e-6, what=f"prob xent grad ({form})")
+    assert pg.grad[0, 3].item() == 0.0
+    if form == "sparse":  # ignore_index rows contribute neither loss nor gradient
+        lab2 = labels.clone()
+        lab2[1] = -100
+        pg2 = p.clone().requires_grad_(True)
+        l2 = prob_cross_entropy(pg2, labels=lab2)
+        l2.backward()
+        assert torch.all(pg2.grad[1] == 0)
+        keep = torch.ones(B, device=DEV)
+        keep[1] = 0
+        ref2 = (-(y * torch.log(p.clamp(1e-7, 1 - 1e-7))).sum(-1) * keep).sum() / B
+        assert abs(l2.item() - ref2.item()) < 1e-5
+
+
 def test_softmax_xent_padded_vocab():
     """The MLM decoder's call: bf16 logits rows padded to 30,528 columns, the first 30,522 are the
     vocabulary (16-B vector passes + a 2-column scalar tail); dlogits' padding columns come back 0."""
