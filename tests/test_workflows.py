@@ -33,14 +33,16 @@ def _update_law(rows, batch, epochs, window):
 def test_ddl_nyiso_workflow_end_to_end(tmp_path, capsys):
     import ddl_nyiso
 
-    out = ddl_nyiso.main(["--workers", "2", "--epochs", "2", "--device", "cpu", "--hours", "1500",
+    out = ddl_nyiso.main(["--workers", "2", "--epochs", "10", "--device", "cpu", "--hours", "1500",
                           "--csv", str(tmp_path / "nyiso.csv")])
     rows = out["train_rows"]
     assert len(rows) == 2 and sum(rows) == 1500 - 25 - 120  # 24 lags + 1 lead dropped, 120 test rows
     for name in ("GRU", "LSTM"):
         r = out["results"][name]
-        assert r["updates"] == _update_law(rows, 32, 2, 5), (name, r["updates"], rows)
-        assert math.isfinite(r["mape"]) and 0.0 < r["mape"] < 100.0
+        assert r["updates"] == _update_law(rows, 32, 10, 5), (name, r["updates"], rows)
+        # the model learns the series: measured 5.6 % (GRU) / 7.6 % (LSTM) test MAPE at this size (the full
+        # reference config reaches 2.75 % / 3.30 % on CPU fp32 and on the GPU, tests/test_gpu_convergence.py)
+        assert math.isfinite(r["mape"]) and 0.0 < r["mape"] < 10.0, (name, r["mape"])
         pf = out["trainers"][name].prediction_frame
         assert {"prediction", "prediction2", "labels2"} <= set(pf.columns)
         pred = np.array([row["prediction2"].toArray()[0] for row in pf.collect()])
