@@ -178,7 +178,8 @@ def comm_stats(ddp, pg):
     return {"comm_ms": round(full, 3), "exposed_comm_ms": round(exposed, 3), "bucket_mb": ddp.bucket_mb,
             "buckets": len(ddp.buckets), "reduce_dtype": "bf16" if ddp.bf16_algo is not None else "fp32",
             "bf16_algo": ddp.bf16_algo, "optimizer_overlap": ddp.overlap_optimizer and ddp.model.optimizer.ranged_ok,
-            "grad_mb": round(ddp.grad_bytes / 2**20, 1), "backend": pg.backend, "forced_pg": pg.forced}
+            "grad_mb": round(ddp.grad_bytes / 2**20, 1), "backend": pg.backend, "forced_pg": pg.forced,
+            "allreduce_fit": ddp.calibration}
 
 
 # the reference's published NYISO numbers (ddl_nyiso_hdi.ipynb:608-609,730,817-818,934)

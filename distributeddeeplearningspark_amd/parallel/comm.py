@@ -69,6 +69,10 @@ class ProcessGroup:
         dist.all_gather_object(out, obj, group=self.group)
         return out
 
+    def broadcast_object(self, obj, src: int = 0):
+        """``obj`` of rank ``src`` on every rank (small picklable objects)."""
+        return self.all_gather_object(obj)[src]
+
     def max_scalar(self, v: float) -> float:
         if not self.distributed:
             return float(v)

@@ -15,8 +15,13 @@ collectives over xGMI:
   no deadlock even if hooks arrive in a slightly different order).
 * Bucket size: xGMI is point-to-point (7 links x ~153 GB/s per MI355X); a ring
   all-reduce is bound by one link, so per-bucket latency alpha must be amortised by
-  tens of MB.  Default 32 MB (``bucket_mb`` / ``DDL_BUCKET_MB``); the sweep that picks
-  it is ``scripts/bench_allreduce.py``.  The bucket of the first layers is cut small
+  tens of MB.  Measured, not assumed: on a GPU group of world > 1 the engine times a few
+  all-reduces of 1 / 8 / 32 MB on the actual communicator at construction, fits
+  t(S) = alpha + S / beta and takes the smallest power-of-two bucket with S / beta >= 5 alpha
+  (:func:`bucket_policy`, 4-128 MB; rank 0's fit is broadcast so all ranks cut the same
+  buckets; the fit is reported as ``DataParallel.calibration`` and in ``bench.py``'s JSON).
+  ``bucket_mb`` / ``DDL_BUCKET_MB`` override it; CPU (gloo) groups use 32 MB.  The offline
+  sweep is ``scripts/bench_allreduce.py``.  The bucket of the first layers is cut small
   (``DDL_TAIL_BUCKET_MB``, 4 MB): it is the one reduction that cannot overlap backward.
 * ``reduce_dtype=torch.bfloat16`` (``DDL_REDUCE_DTYPE=bf16``): half the xGMI bytes, with
   ONE bf16 rounding of the cross-rank sum.  A ring all-reduce in bf16 would round every
@@ -72,6 +77,63 @@ def all_reduce_flat(pg: ProcessGroup, t: torch.Tensor, bucket_bytes: int = 64 <<
     if average:
         t.div_(pg.world_size)
     return t
+
+
+def bucket_policy(alpha_s: float, beta_bps: float, k: float = 5.0, lo_mb: float = 4.0, hi_mb: float = 128.0) -> float:
+    """Bucket size (MB) for an all-reduce cost t(S) = alpha + S / beta: the smallest bucket whose
+    bandwidth term is k x the per-call latency, S = k * alpha * beta, rounded up to a power of two and
+    clamped to [lo, hi] MB.  Small buckets overlap backward at a finer grain; below this size the per-call
+    latency of the collective (RCCL kernel launch + ring setup over the point-to-point xGMI links)
+    dominates the bytes it moves."""
+    import math
+
+    if not (alpha_s > 0 and beta_bps > 0):
+        return 32.0
+    mb = k * alpha_s * beta_bps / (1 << 20)
+    mb = 2.0 ** math.ceil(math.log2(max(mb, 1e-3)))
+    return float(min(max(mb, lo_mb), hi_mb))
+
+
+_CALIB: dict = {}
+
+
+def calibrate_allreduce(pg: ProcessGroup, device, sizes_mb=(1, 8, 32), iters: int = 3):
+    """Time fp32 all-reduces of ``sizes_mb`` on this group and fit t(S) = alpha + S / beta (least squares over
+    the medians); rank 0's fit is broadcast so every rank cuts identical buckets.  Runs once per group on GPU
+    (RCCL) groups of world > 1 only — CPU gloo groups, forced world-1 groups and co-located host-staged
+    groups keep the 32 MB default.  Returns {"alpha_us", "gbps", "bucket_mb", "points"} or None."""
+    import time
+
+    if not pg.distributed or pg.world_size < 2 or pg.host_staged or device is None or torch.device(device).type != "cuda":
+        return None
+    key = (pg.world_size, pg.rank, str(device), id(pg.group))
+    if key in _CALIB:
+        return _CALIB[key]
+    pts = []
+    for mb in sizes_mb:
+        t = torch.ones((int(mb) << 20) // 4, dtype=torch.float32, device=device)
+        pg.all_reduce_(t)  # warm-up (communicator / channel setup)
+        torch.cuda.synchronize(device)
+        ts = []
+        for _ in range(iters):
+            pg.barrier()
+            t0 = time.perf_counter()
+            pg.all_reduce_(t)
+            torch.cuda.synchronize(device)
+            ts.append(time.perf_counter() - t0)
+        ts.sort()
+        pts.append((float(mb) * (1 << 20), ts[len(ts) // 2]))
+    n = len(pts)
+    sx, sy = sum(x for x, _ in pts), sum(y for _, y in pts)
+    sxx, sxy = sum(x * x for x, _ in pts), sum(x * y for x, y in pts)
+    slope = (n * sxy - sx * sy) / max(n * sxx - sx * sx, 1e-30)
+    alpha = max((sy - slope * sx) / n, 1e-6)
+    beta = 1.0 / slope if slope > 0 else 1e12
+    res = {"alpha_us": round(alpha * 1e6, 2), "gbps": round(beta / 1e9, 2), "bucket_mb": bucket_policy(alpha, beta),
+           "points": [(int(x) >> 20, round(y * 1e3, 4)) for x, y in pts]}
+    res = pg.broadcast_object(res)
+    _CALIB[key] = res
+    return res
 
 
 def _bf16_algo() -> str:
@@ -155,8 +217,15 @@ class DataParallel:
         self.model = model
         self.pg = pg
         self.overlap = overlap and pg.distributed
+        self.calibration = None
         if bucket_mb is None:
-            bucket_mb = float(os.environ.get("DDL_BUCKET_MB", "32"))
+            env = os.environ.get("DDL_BUCKET_MB", "auto")
+            if env == "auto":
+                # measured on THIS group (RCCL over xGMI on a GPU node): see bucket_policy / calibrate_allreduce
+                self.calibration = calibrate_allreduce(pg, model.arena.grad.device if model.arena is not None else None)
+                bucket_mb = self.calibration["bucket_mb"] if self.calibration else 32.0
+            else:
+                bucket_mb = float(env)
         self.bucket_mb = float(bucket_mb)
         self.bucket_bytes = int(bucket_mb * (1 << 20))
         self.reduce_dtype = reduce_dtype if reduce_dtype is not None else _reduce_dtype_from_env()

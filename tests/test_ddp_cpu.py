@@ -286,3 +286,26 @@ def test_ranged_optimizer_equals_full_step():
                     m.optimizer.step(0.5)
             outs.append(m.arena.master.detach().clone())
         torch.testing.assert_close(outs[1], outs[0], rtol=0, atol=0, msg=name)
+
+
+def test_bucket_policy_from_measured_alpha_beta():
+    """The DDP bucket size is derived from the fitted all-reduce cost t(S) = alpha + S / beta:
+    the smallest power-of-two size with S / beta >= 5 alpha, clamped to 4-128 MB."""
+    from distributeddeeplearningspark_amd.parallel.ddp import bucket_policy
+
+    # 30 us latency at 100 GB/s (one xGMI ring): 5 * 30e-6 * 100e9 = 15 MB -> 16 MB
+    assert bucket_policy(30e-6, 100e9) == 16.0
+    # a slow, latency-heavy group gets the cap; a fast low-latency one the floor
+    assert bucket_policy(2e-3, 100e9) == 128.0
+    assert bucket_policy(2e-6, 50e9) == 4.0
+    assert bucket_policy(0.0, 1e9) == 32.0  # degenerate fit: the default
+
+
+def test_calibration_skipped_on_cpu_groups():
+    import torch as _t
+
+    from distributeddeeplearningspark_amd.parallel.comm import ProcessGroup
+    from distributeddeeplearningspark_amd.parallel.ddp import calibrate_allreduce
+
+    pg = ProcessGroup(0, 2, 0, _t.device("cpu"), "gloo")
+    assert calibrate_allreduce(pg, "cpu") is None
