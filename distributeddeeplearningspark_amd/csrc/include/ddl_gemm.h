@@ -37,6 +37,11 @@ enum EpilogueMode : int {
   // (GemmParams::bnr_*) — the LDS-DMA GEMM and halo-conv kernels' form of the streaming kernel's BNR
   // read-out (selected by the launchers when bnr_x is set on a non-streaming tile)
   EPI_BF16_BNR = 4,
+  // EPI_BF16 (every feature) through a per-wave LDS staging area: the accumulators are written to LDS
+  // once, then a ROLLED loop walks the wave's rows with each lane owning 8 consecutive columns —
+  // 16-B bias / residual loads and 16-B bf16 stores, and a code size that does not scale with the
+  // fragment count (the unrolled EPI_BF16 epilogue is ~12-25K instructions per kernel)
+  EPI_BF16_ROW = 5,
 };
 
 constexpr int kMaxTaps = 64;

@@ -191,10 +191,19 @@ __global__ __launch_bounds__(g256::THREADS, 1) void gemm256_kernel(const GemmPar
 #undef DDL_G256_MMA
   if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
 
-  gemm_epilogue<4, 2, EPI>(p, acc[0][0], m0 + ra, n0 + rb, lane, bid);
-  gemm_epilogue<4, 2, EPI>(p, acc[0][1], m0 + ra, n0 + 128 + rb, lane, bid);
-  gemm_epilogue<4, 2, EPI>(p, acc[1][0], m0 + 128 + ra, n0 + rb, lane, bid);
-  gemm_epilogue<4, 2, EPI>(p, acc[1][1], m0 + 128 + ra, n0 + 128 + rb, lane, bid);
+  // (after the re-alignment every wave has issued its last fragment read: the ring is free for the row
+  // epilogue's wave-private staging areas)
+  float* wl = reinterpret_cast<float*>(smem + wid * row_epi_bytes<2>());
+  if constexpr (EPI == EPI_BF16_ROW) {  // the four quadrants through ONE rolled row epilogue
+    const int mbs[4] = {m0 + ra, m0 + ra, m0 + 128 + ra, m0 + 128 + ra};
+    const int nbs[4] = {n0 + rb, n0 + 128 + rb, n0 + rb, n0 + 128 + rb};
+    gemm_epilogue_rows<4, 4, 2>(p, reinterpret_cast<f32x4(&)[4][4][2]>(acc), mbs, nbs, lane, bid, p.M, wl);
+    return;
+  }
+  gemm_epilogue<4, 2, EPI>(p, acc[0][0], m0 + ra, n0 + rb, lane, bid, -1, wl);
+  gemm_epilogue<4, 2, EPI>(p, acc[0][1], m0 + ra, n0 + 128 + rb, lane, bid, -1, wl);
+  gemm_epilogue<4, 2, EPI>(p, acc[1][0], m0 + 128 + ra, n0 + rb, lane, bid, -1, wl);
+  gemm_epilogue<4, 2, EPI>(p, acc[1][1], m0 + 128 + ra, n0 + 128 + rb, lane, bid, -1, wl);
 }
 
 template <int AMODE, int BMODE, int EPI>

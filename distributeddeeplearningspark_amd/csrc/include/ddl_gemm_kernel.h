@@ -349,7 +349,12 @@ struct Operand {
 };
 
 // bf16-output epilogues take D^T fragments (a lane owns 4 consecutive columns of one row)
-constexpr bool epi_dt(int epi) { return epi == EPI_BF16 || epi == EPI_BF16_LITE || epi == EPI_BF16_BNR; }
+constexpr bool epi_dt(int epi) {
+  return epi == EPI_BF16 || epi == EPI_BF16_LITE || epi == EPI_BF16_BNR || epi == EPI_BF16_ROW;
+}
+// per-wave LDS bytes the row epilogue stages through (16 rows of RN*16 columns, padded rows)
+template <int RN>
+constexpr int row_epi_bytes() { return 16 * (RN * 16 + 4) * 4; }
 
 // EPI_BF16_BNR: bf16 store of alpha*acc + the BatchNorm-backward partial sums of the stored gradient
 // (GemmParams::bnr_*), accumulated like the forward statistics (16-lane shuffle, one atomic per
@@ -434,14 +439,238 @@ __device__ __forceinline__ bf16x8 norm_frag(const bf16x8 f, float sc, float sh) 
   return __builtin_bit_cast(bf16x8, o);
 }
 
+
+__device__ __forceinline__ void epi_unpack8(const uint4& u, float* f) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    f[2 * k] = __uint_as_float(w[k] << 16);
+    f[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ uint4 epi_pack8(const float* f) {
+  return make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]), pack_bf16x2(f[6], f[7]));
+}
+
+// EPI_BF16_ROW: the full bf16 epilogue (bias / GELU fwd+bwd / dropout / residual (masked, stride-2
+// subgrid) / ReLU / statistics / output map) with the accumulators staged through a per-wave LDS area
+// (``wlds``, row_epi_bytes<RN>() bytes, wave-private).  NQ output blocks (the 256x256 kernel's four
+// quadrants; 1 elsewhere), each RM fragment rows x RN fragment columns at (mbs[q], nbs[q]).  Per block and
+// fragment row: the 16 x RN*16 accumulators go to LDS, then lane l owns the 8 columns 8 (l % LPR) of rows
+// l / LPR + k (64 / LPR): 16-B bias / residual / aux loads and 16-B bf16 stores.  The block, pass and row
+// loops are ROLLED (only the LDS writes are selected per compile-time fragment), so the code size does not
+// scale with the fragment count; element arithmetic and rounding points are those of EPI_BF16.
+template <int NQ, int RM, int RN>
+__device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, f32x4 (&acc)[NQ][RM][RN], const int (&mbs)[NQ],
+                                                   const int (&nbs)[NQ], const int lane, const int bid, const int mlim,
+                                                   float* __restrict__ wlds) {
+  constexpr int CW = RN * 16;   // columns of a block
+  constexpr int LD = CW + 4;    // padded LDS row (floats): the 16 rows of a fragment hit different banks
+  constexpr int LPR = CW / 8;   // lanes per row
+  constexpr int RPI = 64 / LPR; // rows per iteration
+  const int cl = lane % LPR, rl = lane / LPR;
+  const bool vstride_c = (p.ldc % 8) == 0;
+  const bool vstride_r = !p.resid || (p.ldr % 8) == 0;
+#pragma unroll 1
+  for (int qd = 0; qd < NQ; ++qd) {
+    int mb = mbs[0], nb = nbs[0];
+#pragma unroll
+    for (int q = 1; q < NQ; ++q)
+      if (q == qd) {
+        mb = mbs[q];
+        nb = nbs[q];
+      }
+    const int n = nb + 8 * cl;
+    const bool colfull = n + 7 < p.N;
+    const bool vec_c = colfull && vstride_c, vec_r = colfull && vstride_r;
+    float bias[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bias[e] = 0.f;
+    if (p.bias) {
+      if (colfull && (n % 4) == 0) {
+        const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n);
+        const float4 b1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
+        bias[0] = b0.x; bias[1] = b0.y; bias[2] = b0.z; bias[3] = b0.w;
+        bias[4] = b1.x; bias[5] = b1.y; bias[6] = b1.z; bias[7] = b1.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bias[e] = (n + e < p.N) ? p.bias[n + e] : 0.f;
+      }
+    }
+    float s1[8], s2[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
+#pragma unroll 1
+    for (int pass = 0; pass < RM; ++pass) {
+      // fragment row `pass` of block qd -> LDS (D^T: the lane holds 4 consecutive columns of row lane & 15)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+          if (q == qd && i == pass) {
+#pragma unroll
+            for (int j = 0; j < RN; ++j) {
+              const f32x4 a = acc[q][i][j];
+              *reinterpret_cast<float4*>(wlds + (lane & 15) * LD + 16 * j + 4 * (lane >> 4)) =
+                  make_float4(a[0] * p.alpha, a[1] * p.alpha, a[2] * p.alpha, a[3] * p.alpha);
+            }
+          }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+      for (int r = rl; r < 16; r += RPI) {
+        const int m = mb + 16 * pass + r;
+        float v[8];
+        {
+          const float4 x0 = *reinterpret_cast<const float4*>(wlds + r * LD + 8 * cl);
+          const float4 x1 = *reinterpret_cast<const float4*>(wlds + r * LD + 8 * cl + 4);
+          v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w;
+          v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+        }
+        if (m >= mlim || n >= p.N) continue;
+        long rowoff;
+        int nn = 0, ii = 0, jj = 0;
+        if (p.om.enabled) {
+          pix_decompose((uint32_t)m, p.om.gh, p.om.gw, nn, ii, jj);
+          rowoff = ((long)(nn * p.om.hy + ii * p.om.so + p.om.oh) * p.om.wy + jj * p.om.so + p.om.ow) * p.ldc;
+        } else {
+          rowoff = (long)m * p.ldc;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += bias[e];
+        if (p.relu >= ACT_GELU) {
+          bf16_t* ax = reinterpret_cast<bf16_t*>(p.aux) + (long)m * p.ldc + n;
+          if (p.relu == ACT_GELU) {
+            float pa[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              pa[e] = bf2f(f2bf(v[e]));
+              v[e] = gelu_f(pa[e]);
+            }
+            if (vec_c) {
+              *reinterpret_cast<uint4*>(ax) = epi_pack8(pa);
+            } else {
+              for (int e = 0; e < 8; ++e)
+                if (n + e < p.N) ax[e] = f2bf(pa[e]);
+            }
+          } else {
+            float pre[8];
+            if (vec_c) {
+              epi_unpack8(*reinterpret_cast<const uint4*>(ax), pre);
+            } else {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) pre[e] = (n + e < p.N) ? bf2f(ax[e]) : 0.f;
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] *= (n + e < p.N) ? gelu_grad_f(pre[e]) : 0.f;
+          }
+        }
+        if (p.drop_thresh) {
+          const unsigned long long base = (unsigned long long)m * (unsigned long long)p.N + (unsigned long long)n;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = drop_keep(p.drop_seed, base + e, p.drop_thresh) ? v[e] * p.drop_scale : 0.f;
+        }
+        if (p.resid) {
+          long rrow = m;
+          if (p.rsub_h) {
+            int rn_, ri_, rj_;
+            pix_decompose((uint32_t)m, p.rsub_h, p.rsub_w, rn_, ri_, rj_);
+            rrow = ((ri_ | rj_) & 1)
+                       ? -1L
+                       : ((long)rn_ * ((p.rsub_h + 1) >> 1) + (ri_ >> 1)) * ((p.rsub_w + 1) >> 1) + (rj_ >> 1);
+          }
+          if (rrow >= 0) {
+            const bf16_t* rp = reinterpret_cast<const bf16_t*>(p.resid) + rrow * p.ldr + n;
+            float rv[8];
+            if (vec_r) {
+              epi_unpack8(*reinterpret_cast<const uint4*>(rp), rv);
+            } else {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) rv[e] = (n + e < p.N) ? bf2f(rp[e]) : 0.f;
+            }
+            if (p.resid_mask) {  // bits n .. n+7 of the row's mask (n % 8 == 0: one byte)
+              const long bit = (long)m * p.ldr + n;
+              const uint32_t mbits = (uint32_t)p.resid_mask[bit >> 3] >> (bit & 7);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) rv[e] = ((mbits >> e) & 1u) ? rv[e] : 0.f;
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += rv[e];
+          }
+        }
+        if (p.relu == ACT_RELU) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          o[e] = bf2f(f2bf(v[e]));
+          const float rr = (n + e < p.N) ? o[e] : 0.f;
+          s1[e] += rr;
+          s2[e] += rr * rr;
+        }
+        bf16_t* c = reinterpret_cast<bf16_t*>(p.c) + rowoff + n;
+        if (vec_c) {
+          *reinterpret_cast<uint4*>(c) = epi_pack8(o);
+        } else {
+          for (int e = 0; e < 8; ++e)
+            if (n + e < p.N) c[e] = f2bf(o[e]);
+        }
+        if (p.om.enabled && p.om.zero_siblings) {  // this class is the only one with taps: zero the rest
+          bf16_t* cb = reinterpret_cast<bf16_t*>(p.c);
+          for (int a = 0; a < p.om.so; ++a) {
+            const int hy = ii * p.om.so + a;
+            if (hy >= p.om.hy) break;
+            for (int b = 0; b < p.om.so; ++b) {
+              const int wy = jj * p.om.so + b;
+              if (wy >= p.om.wy || (a == p.om.oh && b == p.om.ow)) continue;
+              bf16_t* z = cb + ((long)(nn * p.om.hy + hy) * p.om.wy + wy) * p.ldc + n;
+              if (vec_c) {
+                *reinterpret_cast<uint4*>(z) = make_uint4(0, 0, 0, 0);
+              } else {
+                for (int e = 0; e < 8; ++e)
+                  if (n + e < p.N) z[e] = 0;
+              }
+            }
+          }
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();  // every lane read this pass before the next overwrites the area
+    }
+    if (p.stats) {  // lanes sharing cl hold the same 8 columns: reduce over the row lanes, one atomic per column
+      float* st = p.stats + (long)(bid % kStatShards) * 2 * p.N;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float a = s1[e], b = s2[e];
+#pragma unroll
+        for (int o = LPR; o < 64; o <<= 1) {
+          a += __shfl_xor(a, o, 64);
+          b += __shfl_xor(b, o, 64);
+        }
+        if (rl == 0 && n + e < p.N) {
+          atomicAdd(st + n + e, a);
+          atomicAdd(st + p.N + n + e, b);
+        }
+      }
+    }
+  }
+}
+
 // Epilogue shared by the GEMM kernels.  mb / nb: first row / column of this wave's
 // RM x RN fragment block; rows >= mend (default p.M) are not stored (tile-local row limits of
 // the halo conv kernel).  bf16 epilogue: acc holds D^T fragments (lane owns 4 consecutive
 // columns of one row); fp32 epilogues: D fragments (16 consecutive columns per row).
 template <int RM, int RN, int EPI>
 __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[RM][RN], const int mb, const int nb,
-                                              const int lane, const int bid, int mend = -1) {
+                                              const int lane, const int bid, int mend = -1, float* wlds = nullptr) {
   const int mlim = mend < 0 ? p.M : mend;
+  if constexpr (EPI == EPI_BF16_ROW) {
+    const int mbs[1] = {mb}, nbs[1] = {nb};
+    gemm_epilogue_rows<1, RM, RN>(p, reinterpret_cast<f32x4(&)[1][RM][RN]>(acc), mbs, nbs, lane, bid, mlim, wlds);
+    return;
+  }
   if constexpr (EPI == EPI_BF16_BNR) {
     gemm_epilogue_bnr<RM, RN>(p, acc, mb, nb, lane, bid, mlim);
     return;
@@ -776,7 +1005,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams
     __syncthreads();
   }
 
-  gemm_epilogue<RM, RN, EPI>(p, acc, m0 + wm0, n0 + wn0, lane, bid);
+  gemm_epilogue<RM, RN, EPI>(p, acc, m0 + wm0, n0 + wn0, lane, bid, -1,
+                             reinterpret_cast<float*>(smem + wid * row_epi_bytes<RN>()));
 }
 
 // LDS-DMA variant of the same kernel: identical tiles, operand modes, fragments and epilogue,
@@ -891,7 +1121,9 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
       }
       slot = slot + 1 == ST ? 0 : slot + 1;
     }
-    gemm_epilogue<RM, RN, EPI>(p, acc, m0 + wm0, n0 + wn0, lane, bid);
+    if constexpr (EPI == EPI_BF16_ROW) __syncthreads();  // the ring slots become the staging area
+    gemm_epilogue<RM, RN, EPI>(p, acc, m0 + wm0, n0 + wn0, lane, bid, -1,
+                               reinterpret_cast<float*>(smem + wid * row_epi_bytes<RN>()));
     return;
   }
   if (nk > 0) {
@@ -941,7 +1173,9 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
     }
   }
 
-  gemm_epilogue<RM, RN, EPI>(p, acc, m0 + wm0, n0 + wn0, lane, bid);
+  // (ST 1 / 2: the loop's closing barrier already freed the stages for the row epilogue's staging area)
+  gemm_epilogue<RM, RN, EPI>(p, acc, m0 + wm0, n0 + wn0, lane, bid, -1,
+                             reinterpret_cast<float*>(smem + wid * row_epi_bytes<RN>()));
 }
 
 // DDL_GEMM_DMA: 0 = register-staged kernel, 1 = LDS-DMA single stage (default), 2 = LDS-DMA double stage
@@ -1032,6 +1266,15 @@ inline int launch_tile(const GemmParams& p, hipStream_t s) {
     hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, AMODE, BMODE, EPI>), grid, dim3(NTHREADS), lds, s, p);
   }
   return (int)hipGetLastError();
+}
+
+// DDL_GEMM_ROW_EPI=1: the full bf16 epilogue runs as the LDS-staged row epilogue (EPI_BF16_ROW)
+inline bool row_epilogue() {
+  static const bool on = [] {
+    const char* e = getenv("DDL_GEMM_ROW_EPI");
+    return e && atoi(e) == 1;
+  }();
+  return on;
 }
 
 // The bf16 epilogue features a call uses beyond bias / ReLU / statistics.

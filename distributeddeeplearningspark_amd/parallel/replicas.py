@@ -40,7 +40,9 @@ ELASTIC = ("easgd", "aeasgd", "eamsgd")
 
 def mode() -> str:
     """``DDL_REPLICA_GROUPS``: ``auto`` (default: replicas co-located on a GPU run in one process),
-    ``1`` (also on the CPU: one process for all workers), ``0`` (one OS process per worker)."""
+    ``1`` (also on the CPU: one process for all workers), ``0`` (one OS process per worker), or an integer
+    G > 1 (CPU tests of the multi-group path: the workers are dealt round-robin to G processes, as they are
+    to the GPUs of a node)."""
     return os.environ.get("DDL_REPLICA_GROUPS", "auto")
 
 
@@ -52,13 +54,18 @@ def applies(cfg, devices) -> bool:
     m = mode()
     if m == "0" or len(devices) < 2:
         return False
-    if m == "1":
+    if m == "1" or (m.isdigit() and int(m) > 1):
         return True
     return devices[0] != "cpu" and len(set(devices)) < len(devices)
 
 
 def plan(devices) -> list[list[int]]:
-    """Replica ids per group, one group per distinct device, in device order."""
+    """Replica ids per group, one group per distinct device, in device order (CPU workers with
+    ``DDL_REPLICA_GROUPS=G``: G round-robin groups)."""
+    m = mode()
+    if devices and devices[0] == "cpu" and m.isdigit() and int(m) > 1:
+        g = min(int(m), len(devices))
+        return [[r for r in range(len(devices)) if r % g == k] for k in range(g)]
     order: list[str] = []
     for d in devices:
         if d not in order:

@@ -725,9 +725,9 @@ class _ShardedTrainer(Trainer):
                 torch.cuda.set_device(dev)
             pg = comm.ProcessGroup(0, 1, 0, dev, None)
             res = _rep.train_group(0, 1, pg, cfg, self.master_model, [Xs[r] for r in g], [Ys[r] for r in g], g, sizes)
-        else:  # one executor process per device, partial sums all-reduced over RCCL
+        else:  # one executor process per device, partial sums all-reduced over RCCL (gloo on CPU)
             args = [(cfg, self.master_model, [Xs[r] for r in g], [Ys[r] for r in g], g, sizes) for g in groups]
-            per = run_workers(_rep.train_group, len(groups), args, device=self.device)
+            per = run_workers(_rep.train_group, len(groups), args, device="cpu" if devices[0] == "cpu" else self.device)
             res = [x for grp in per for x in grp]
         return sorted(res, key=lambda r: r["rank"])
 

@@ -40,11 +40,15 @@ def _train(spark, monkeypatch, algo, groups, opt="adam"):
     return tr, model.get_weights()
 
 
-@pytest.mark.parametrize("algo", ["ADAG", "DynSGD", "DOWNPOUR", "AEASGD", "AveragingTrainer"])
-def test_replica_group_matches_process_workers(spark, monkeypatch, algo):
+@pytest.mark.parametrize("algo,groups", [("ADAG", "1"), ("DynSGD", "1"), ("DOWNPOUR", "1"), ("AEASGD", "1"),
+                                         ("AveragingTrainer", "1"), ("ADAG", "2"), ("DynSGD", "2"), ("AEASGD", "2")])
+def test_replica_group_matches_process_workers(spark, monkeypatch, algo, groups):
+    """groups "1": all three workers in this process; "2": two processes holding replicas {0, 2} and {1}
+    whose per-process partial sums are all-reduced (the multi-GPU form of the commit round)."""
     tr_p, w_p = _train(spark, monkeypatch, algo, "0")
-    tr_g, w_g = _train(spark, monkeypatch, algo, "1")
-    assert tr_g._results[0].get("replica_group") == {"group": 0, "groups": 1, "replicas": 3}
+    tr_g, w_g = _train(spark, monkeypatch, algo, groups)
+    ng = int(groups)
+    assert tr_g._results[0].get("replica_group") == {"group": 0, "groups": ng, "replicas": 3 if ng == 1 else 2}
     assert "replica_group" not in tr_p._results[0]
     assert tr_g.parameter_server.num_updates == tr_p.parameter_server.num_updates
     if algo != "AveragingTrainer":
