@@ -59,7 +59,7 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
           c10::optional<at::Tensor> resid_mask, c10::optional<at::Tensor> bnr_x, c10::optional<at::Tensor> bnr_mask,
           c10::optional<at::Tensor> bnr_mean, int64_t rsub_h, int64_t rsub_w, c10::optional<at::Tensor> a_scale,
           c10::optional<at::Tensor> a_shift, c10::optional<at::Tensor> b_scale, c10::optional<at::Tensor> b_shift,
-          c10::optional<at::Tensor> bnr_scale, c10::optional<at::Tensor> bnr_shift) {
+          c10::optional<at::Tensor> bnr_scale, c10::optional<at::Tensor> bnr_shift, int64_t split_stride) {
   CHECK_CUDA(a);
   CHECK_CUDA(b);
   CHECK_CUDA(c);
@@ -243,6 +243,12 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
   if (tile == kTileConv3)
     TORCH_CHECK(conv3x3_halo_ok(p) && epi == EPI_BF16, "gemm conv3x3: needs a 3x3 / stride-1 / pad-1 KC_GATHER x KC "
                 "conv with C % 64 == 0, N % 64 == 0, no split-K and at most bias/ReLU/statistics in the epilogue");
+  if (split_stride > 0) {
+    const int64_t splits = (K + k_split - 1) / k_split;
+    TORCH_CHECK(epi == EPI_F32 && beta == 0.0 && split_stride >= M * ldc && c.numel() >= splits * split_stride,
+                "gemm: split-K slabs need EPI_F32, beta = 0 and a workspace of splits x split_stride floats");
+    p.split_stride = split_stride;
+  }
   at::DeviceGuard guard(a.device());
   HIP_OK(launch_gemm_bf16(p, (int)epi, (int)tile, cur_stream()));
 }
@@ -309,7 +315,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("resid_mask") = py::none(), py::arg("bnr_x") = py::none(), py::arg("bnr_mask") = py::none(),
         py::arg("bnr_mean") = py::none(), py::arg("rsub_h") = 0, py::arg("rsub_w") = 0,
         py::arg("a_scale") = py::none(), py::arg("a_shift") = py::none(), py::arg("b_scale") = py::none(),
-        py::arg("b_shift") = py::none(), py::arg("bnr_scale") = py::none(), py::arg("bnr_shift") = py::none());
+        py::arg("b_shift") = py::none(), py::arg("bnr_scale") = py::none(), py::arg("bnr_shift") = py::none(),
+        py::arg("split_stride") = 0);
   m.def("conv3x3_wgrad", &conv3x3_wgrad, "3x3 stride-1 weight gradient (halo kernel): gw += dW", py::arg("dy"),
         py::arg("x"), py::arg("gw"), py::arg("ws"), py::arg("splits"), py::arg("tpb"), py::arg("pp") = false);
   m.def("conv3x3_wgrad_plan", &conv3x3_wgrad_plan_py,

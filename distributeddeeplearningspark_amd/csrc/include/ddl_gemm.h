@@ -129,6 +129,10 @@ struct GemmParams {
   // (M fastest inside a group) so the tiles resident on one XCD share fewer A rows and B columns
   // (set by launch_gemm_bf16 from DDL_GEMM_GROUP_M; 0 = row-major over the tiles)
   int group_m;
+  // split-K through partial SLABS (plain stores, EPI_F32 only): split s writes its partial C at
+  // c + s * split_stride (elements, ldc unchanged); a reduce pass sums the slabs in split order
+  // (slab_reduce: deterministic, and ~4x the store rate of the fp32 atomics it replaces).  0 = off.
+  long split_stride;
 };
 
 enum Activation : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_GELU_BWD = 3 };

@@ -200,10 +200,10 @@ __global__ __launch_bounds__(g256::THREADS, 1) void gemm256_kernel(const GemmPar
     gemm_epilogue_rows<4, 4, 2>(p, reinterpret_cast<f32x4(&)[4][4][2]>(acc), mbs, nbs, lane, bid, p.M, wl);
     return;
   }
-  gemm_epilogue<4, 2, EPI>(p, acc[0][0], m0 + ra, n0 + rb, lane, bid, -1, wl);
-  gemm_epilogue<4, 2, EPI>(p, acc[0][1], m0 + ra, n0 + 128 + rb, lane, bid, -1, wl);
-  gemm_epilogue<4, 2, EPI>(p, acc[1][0], m0 + 128 + ra, n0 + rb, lane, bid, -1, wl);
-  gemm_epilogue<4, 2, EPI>(p, acc[1][1], m0 + 128 + ra, n0 + 128 + rb, lane, bid, -1, wl);
+  gemm_epilogue<4, 2, EPI>(p, acc[0][0], m0 + ra, n0 + rb, lane, bid, -1, wl, (long)split * p.split_stride);
+  gemm_epilogue<4, 2, EPI>(p, acc[0][1], m0 + ra, n0 + 128 + rb, lane, bid, -1, wl, (long)split * p.split_stride);
+  gemm_epilogue<4, 2, EPI>(p, acc[1][0], m0 + 128 + ra, n0 + rb, lane, bid, -1, wl, (long)split * p.split_stride);
+  gemm_epilogue<4, 2, EPI>(p, acc[1][1], m0 + 128 + ra, n0 + 128 + rb, lane, bid, -1, wl, (long)split * p.split_stride);
 }
 
 template <int AMODE, int BMODE, int EPI>

@@ -664,7 +664,8 @@ __device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, f32x4 (&
 // columns of one row); fp32 epilogues: D fragments (16 consecutive columns per row).
 template <int RM, int RN, int EPI>
 __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[RM][RN], const int mb, const int nb,
-                                              const int lane, const int bid, int mend = -1, float* wlds = nullptr) {
+                                              const int lane, const int bid, int mend = -1, float* wlds = nullptr,
+                                              long coff = 0) {
   const int mlim = mend < 0 ? p.M : mend;
   if constexpr (EPI == EPI_BF16_ROW) {
     const int mbs[1] = {mb}, nbs[1] = {nb};
@@ -691,7 +692,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
         for (int e = 0; e < 4; ++e) {
           const int m = mb + 16 * i + 4 * (lane >> 4) + e;
           if (m >= mlim) continue;
-          float* c = reinterpret_cast<float*>(p.c) + (long)m * p.ldc + n;
+          float* c = reinterpret_cast<float*>(p.c) + coff + (long)m * p.ldc + n;
           const float v = acc[i][j][e] * p.alpha;
           if constexpr (EPI == EPI_F32) *c = (p.beta != 0.f) ? v + p.beta * *c : v;
           else atomicAdd(c, v);
@@ -1006,7 +1007,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams
   }
 
   gemm_epilogue<RM, RN, EPI>(p, acc, m0 + wm0, n0 + wn0, lane, bid, -1,
-                             reinterpret_cast<float*>(smem + wid * row_epi_bytes<RN>()));
+                             reinterpret_cast<float*>(smem + wid * row_epi_bytes<RN>()), (long)split * p.split_stride);
 }
 
 // LDS-DMA variant of the same kernel: identical tiles, operand modes, fragments and epilogue,
@@ -1123,7 +1124,7 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
     }
     if constexpr (EPI == EPI_BF16_ROW) __syncthreads();  // the ring slots become the staging area
     gemm_epilogue<RM, RN, EPI>(p, acc, m0 + wm0, n0 + wn0, lane, bid, -1,
-                               reinterpret_cast<float*>(smem + wid * row_epi_bytes<RN>()));
+                               reinterpret_cast<float*>(smem + wid * row_epi_bytes<RN>()), (long)split * p.split_stride);
     return;
   }
   if (nk > 0) {
@@ -1175,7 +1176,7 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
 
   // (ST 1 / 2: the loop's closing barrier already freed the stages for the row epilogue's staging area)
   gemm_epilogue<RM, RN, EPI>(p, acc, m0 + wm0, n0 + wn0, lane, bid, -1,
-                             reinterpret_cast<float*>(smem + wid * row_epi_bytes<RN>()));
+                             reinterpret_cast<float*>(smem + wid * row_epi_bytes<RN>()), (long)split * p.split_stride);
 }
 
 // DDL_GEMM_DMA: 0 = register-staged kernel, 1 = LDS-DMA single stage (default), 2 = LDS-DMA double stage

@@ -66,6 +66,8 @@ int sum_rows_bf16(const void* x, void* y, int R, long n, hipStream_t s);
 int relu_bwd(const void* dy, const void* y, void* dx, long n, hipStream_t s);
 int add_bf16(const void* a, const void* b, void* y, long n, hipStream_t s);
 int bias_grad(const void* dy, float* db, long M, int N, int accumulate, hipStream_t s);  // db[n] (+)= sum_m dy[m][n]
+// c = beta * c + sum over split-K partial slabs ws[splits][M][N] (split order, one writer per element)
+int slab_reduce(const float* ws, int splits, float* c, long M, int N, long ldc, float beta, hipStream_t s);
 // y[C][R] = x[R][C]^T (bf16; R, C, ldx multiples of 8)
 int transpose_bf16(const void* x, void* y, int R, int C, long ldx, hipStream_t s);
 int im2col(const void* x, void* col, int n, int hi, int wi, int c, int ho, int wo, int sh, int sw, int ntaps,

@@ -157,6 +157,50 @@ __global__ __launch_bounds__(256) void bias_grad_vec_kernel(const bf16_t* dy, fl
   }
 }
 
+// c[m][n] = beta * c[m][n] + sum_s ws[s][m][n] (slabs [splits][M][N], contiguous), summed in split order by
+// ONE lane per element: the reduce of split-K partial slabs (GemmParams::split_stride).  float4 per lane
+// when N and ldc are multiples of 4.
+__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ ws, int splits, float* __restrict__ c,
+                                                          long M, int N, long ldc, float beta, int vec) {
+  const long slab = M * (long)N;
+  if (vec) {
+    const long n4 = slab >> 2;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+      float4 a = reinterpret_cast<const float4*>(ws)[i];
+      for (int sp = 1; sp < splits; ++sp) {
+        const float4 b = reinterpret_cast<const float4*>(ws + sp * slab)[i];
+        a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+      }
+      const long e = i << 2, m = e / N, n = e - m * N;
+      float4* cp = reinterpret_cast<float4*>(c + m * ldc + n);
+      if (beta != 0.f) {
+        const float4 o = *cp;
+        a.x += beta * o.x; a.y += beta * o.y; a.z += beta * o.z; a.w += beta * o.w;
+      }
+      *cp = a;
+    }
+  } else {
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < slab; i += (long)gridDim.x * 256) {
+      float a = ws[i];
+      for (int sp = 1; sp < splits; ++sp) a += ws[sp * slab + i];
+      const long m = i / N, n = i - m * N;
+      float* cp = c + m * ldc + n;
+      *cp = (beta != 0.f) ? a + beta * *cp : a;
+    }
+  }
+}
+
+int slab_reduce(const float* ws, int splits, float* c, long M, int N, long ldc, float beta, hipStream_t s) {
+  if (splits < 1 || M <= 0 || N <= 0) return (int)hipErrorInvalidValue;
+  const int vec = (N % 4 == 0 && ldc % 4 == 0 && ((uintptr_t)c & 15) == 0 && ((uintptr_t)ws & 15) == 0) ? 1 : 0;
+  long work = vec ? (M * N) >> 2 : M * N;
+  long blocks = (work + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)(blocks > 0 ? blocks : 1)), dim3(256), 0, s, ws, splits, c, M, N,
+                     ldc, beta, vec);
+  return (int)hipGetLastError();
+}
+
 int bias_grad(const void* dy, float* db, long M, int N, int accumulate, hipStream_t s) {
   if (!accumulate) hipMemsetAsync(db, 0, sizeof(float) * N, s);
   long ys = M / 64;

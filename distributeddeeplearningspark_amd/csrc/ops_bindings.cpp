@@ -441,6 +441,15 @@ void prob_xent_(const at::Tensor& p, c10::optional<at::Tensor> labels, c10::opti
                    loss_rows.data_ptr<float>(), dp.data_ptr<float>(), (int)p.size(0), (int)p.size(1), (float)eps,
                    (float)scale, (int)ignore_index, cur_stream()));
 }
+void slab_reduce_(const at::Tensor& ws, int64_t splits, const at::Tensor& c, int64_t M, int64_t N, int64_t ldc,
+                  double beta) {
+  GPU(ws); F32(ws); GPU(c);
+  CK(c.scalar_type() == at::kFloat, "slab_reduce: fp32 c");
+  CK(splits >= 1 && ws.numel() >= splits * M * N && ldc >= N && c.numel() >= (M - 1) * ldc + N,
+     "slab_reduce: ws [splits, M, N], c [M, ldc]");
+  at::DeviceGuard g(ws.device());
+  HIP_OK(slab_reduce(ws.data_ptr<float>(), (int)splits, c.data_ptr<float>(), M, (int)N, ldc, (float)beta, cur_stream()));
+}
 void mse_fwd_bwd_(const at::Tensor& pred, const at::Tensor& target, const at::Tensor& loss, const at::Tensor& grad) {
   F32(pred); F32(target); F32(loss); F32(grad);
   CK(pred.is_cuda() && pred.numel() == target.numel() && grad.numel() == pred.numel() && loss.numel() == 1,
@@ -547,6 +556,7 @@ void register_ops(py::module& m) {
   m.def("step_tick", &step_tick_);
   m.def("mse_fwd_bwd", &mse_fwd_bwd_);
   m.def("prob_xent", &prob_xent_);
+  m.def("slab_reduce", &slab_reduce_);
   m.def("commit_delta", &commit_delta_);
   m.def("commit_apply", &commit_apply_);
   m.def("commit_replicas", &commit_replicas_, "one commit round over R co-located replicas", py::arg("ws"),

@@ -130,23 +130,51 @@ def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, bet
             tile = choose_tile(M, N, bn_cap)
     if k_split is None:
         k_split = choose_split(M, N, K, tile, allow=(epi != EPI_BF16), rounds=split_rounds)
-    if _det.enabled():  # deterministic mode: the whole K in one workgroup (no atomic split-K partial sums)
-        k_split = max(64, math.ceil(K / 64) * 64)
+    split_stride = 0
+    if k_split < K and epi != EPI_F32 and _det.enabled():
+        k_split = max(64, math.ceil(K / 64) * 64)  # deterministic mode: no atomic split-K partial sums
+    out, slab_beta = c, None
     if epi == EPI_F32 and k_split < K:
         if beta not in (0.0, 1.0):
             raise ValueError("split-K fp32 gemm supports beta in {0,1} (beta=0 needs a zeroed C)")
-        epi = EPI_F32_ATOMIC
+        if tile in (0, 1, 2, 3, TILE256) and (_det.enabled() or _SPLITK_SLABS):
+            # partial slabs (plain stores) + an ordered reduce: deterministic, and the slab stores run at
+            # the HBM store rate where fp32 atomics run at ~1.3 TB/s (GemmParams::split_stride)
+            splits = math.ceil(K / k_split)
+            out, split_stride, slab_beta, ldc_c = _slab_workspace(splits * M * N, c.device), M * N, beta, ldc
+            ldc, beta = N, 0.0
+        else:
+            epi = EPI_F32_ATOMIC
     if bnr is not None:  # fused BN-backward reduce of the output (see linear_dgrad / GemmParams.bnr_*)
         if tile == TILE256:
             raise ValueError("bnr: not on the 256x256 kernel")
         stats = bnr["ws"]
-    C().gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, tile, k_split, alpha, beta, bias, resid, ldr,
+    C().gemm(a, b, out, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, tile, k_split, alpha, beta, bias, resid, ldr,
              int(relu), geom, outmap, b_kdiv, b_tap_stride, stats, aux, float(drop_p), int(drop_seed), resid_mask,
              None if bnr is None else bnr["x"], None if bnr is None else bnr.get("mask"),
              None if bnr is None else bnr["mean"], *(rsub or (0, 0)), *(a_norm or (None, None)),
              *(b_norm or (None, None)), None if bnr is None else bnr.get("scale"),
-             None if bnr is None else bnr.get("shift"))
+             None if bnr is None else bnr.get("shift"), split_stride)
+    if split_stride:
+        C().slab_reduce(out, math.ceil(K / k_split), c, M, N, ldc_c, float(slab_beta))
     return c
+
+
+# DDL_SPLITK_SLABS=1: fp32 split-K GEMMs (weight gradients) through partial slabs instead of fp32 atomics
+_SPLITK_SLABS = _os.environ.get("DDL_SPLITK_SLABS", "0") == "1"
+_SLAB_WS: dict = {}
+
+
+def _slab_workspace(n, device):
+    """Per-(device, stream, replica scope) fp32 workspace of split-K partial slabs (grown on demand; calls on
+    one stream are ordered, so one buffer per stream is enough)."""
+    from . import scope as _scope
+
+    key = (str(device), torch.cuda.current_stream(device).cuda_stream if device.type == "cuda" else 0, _scope.tag())
+    ws = _SLAB_WS.get(key)
+    if ws is None or ws.numel() < n:
+        ws = _SLAB_WS[key] = torch.empty(max(n, 1 << 20), dtype=torch.float32, device=device)
+    return ws[:n]
 
 
 # ----------------------------------------------------------------------------------------

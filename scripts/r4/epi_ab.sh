@@ -30,4 +30,22 @@ import json,sys
 for l in open('gpurun_out/r4/epi/gemm_$f.jsonl'):
     if l.startswith('{'):
         d=json.loads(l); print(d['shape'], {k:d[k]['tflops'] for k in ('g256','t128','torch') if k in d})"; done
+# split-K slabs vs fp32 atomics (weight gradients): test, then interleaved BERT / ResNet A/B
+timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 200 --timeout-method thread -k "slabs" > gpurun_out/r4/epi/tests_slabs.log 2>&1
+src=$?; tail -2 gpurun_out/r4/epi/tests_slabs.log
+[ $src -ne 0 ] && [ $src -ne 1 ] && exit $src
+for i in 1 2; do
+  for v in 0 1; do
+    DDL_SPLITK_SLABS=$v timeout -k 10 300 python bench.py --model bert --steps 10 --warmup 3 2>/dev/null | grep '^{' | sed "s/^/slabs=$v /" >> gpurun_out/r4/epi/bert_slabs.txt || exit 1
+    DDL_SPLITK_SLABS=$v timeout -k 10 300 python bench.py --steps 15 --warmup 4 2>/dev/null | grep '^{' | sed "s/^/slabs=$v /" >> gpurun_out/r4/epi/resnet_slabs.txt || exit 1
+  done
+done
+python - <<'PY'
+import json
+for f in ("bert_slabs", "resnet_slabs"):
+    for line in open(f"gpurun_out/r4/epi/{f}.txt"):
+        tag, js = line.split(" ", 1)
+        d = json.loads(js)
+        print(f, tag, round(d["value"]), d["ms_per_step"])
+PY
 exit $rc

@@ -1027,3 +1027,28 @@ def test_conv3x3_c64_resident_filter_kernel(N, H, monkeypatch):
     got = ws.double().cpu().sum(0)
     close(got[0], s1, rtol=1e-4, atol=1e-2 * s1.abs().mean().item(), what="c64 sum d")
     close(got[1], s2, rtol=1e-4, atol=1e-2 * s2.abs().mean().item(), what="c64 sum d (x - mean)")
+
+
+@pytest.mark.parametrize("M,N,K", [(768, 2304, 16384), (256, 64, 200704), (104, 72, 5000)])
+def test_splitk_slabs_match_atomics(M, N, K, monkeypatch):
+    """fp32 split-K weight gradients through partial slabs + ordered reduce (GemmParams::split_stride)
+    equal the fp32-atomic form and the fp32 reference, accumulate into a pre-filled gradient (beta = 1),
+    and repeat bit for bit."""
+    from distributeddeeplearningspark_amd.ops import gemm as G
+
+    dy = rnd(K, N, seed=51)
+    x = rnd(K, M, seed=52)
+    g0 = torch.randn(N, M, device=DEV)
+    ref = g0 + dy.float().T @ x.float()
+    outs = {}
+    for slabs in (False, True):
+        monkeypatch.setattr(G, "_SPLITK_SLABS", slabs)
+        reps = []
+        for _ in range(2):
+            gw = g0.clone()
+            G.linear_wgrad(dy, x, gw)
+            reps.append(gw)
+        outs[slabs] = reps
+    assert torch.equal(outs[True][0], outs[True][1]), "slab split-K must be bitwise reproducible"
+    close(outs[True][0], ref, rtol=2e-3, atol=0.5, what="slabs vs fp32")
+    close(outs[True][0], outs[False][0], rtol=1e-4, atol=1e-3, what="slabs vs atomics")
