@@ -24,6 +24,12 @@ SHAPES = [  # name, M, N, K, a_mode, b_mode
     ("rn50_l3_1x1_1024to256", 50176, 256, 1024, G.KC, G.KC),
     ("rn50_l3_1x1_256to1024", 50176, 1024, 256, G.KC, G.KC),
     ("rn50_l2_dgrad_512to128", 200704, 128, 512, G.KC, G.RC),
+    # weight gradients: dW[N_out, K_in] += dY^T X over the token / pixel dimension (RC x RC, fp32, split-K)
+    ("bert_qkv_wgrad", 2304, 768, T, G.RC, G.RC, "f32"),
+    ("bert_ffn1_wgrad", 3072, 768, T, G.RC, G.RC, "f32"),
+    ("bert_ffn2_wgrad", 768, 3072, T, G.RC, G.RC, "f32"),
+    ("rn50_wgrad_1x1_64to256", 256, 64, 802816, G.RC, G.RC, "f32"),
+    ("rn50_wgrad_1x1_1024to256", 256, 1024, 50176, G.RC, G.RC, "f32"),
 ]
 
 
@@ -57,28 +63,36 @@ def _shapes(argv):
 
 def main():
     torch.manual_seed(0)
-    for name, M, N, K, am, bm in _shapes(sys.argv[1:]):
+    for shp in _shapes(sys.argv[1:]):
+        name, M, N, K, am, bm = shp[:6]
+        f32 = len(shp) > 6 and shp[6] == "f32"
+        epi = G.EPI_F32 if f32 else G.EPI_BF16
         A = torch.randn(M, K, device="cuda").to(torch.bfloat16)
         B = torch.randn(N, K, device="cuda").to(torch.bfloat16)
         a_t = A if am == G.KC else A.T.contiguous()
         b_t = B if bm == G.KC else B.T.contiguous()
-        out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+        out = torch.zeros(M, N, dtype=torch.float32 if f32 else torch.bfloat16, device="cuda")
         ref = (A[:256].float() @ B.float().T)
         runs = {}
         variants = {"g256": G.TILE256, "t128": G.choose_tile(M, N)}
-        if M >= 256 and N >= 256 and K % 64 == 0:
-            pass
-        else:
+        if f32:  # weight gradients: the production tile choice (gemm picks tile and split-K) and 128x128
+            variants = {"auto": None, "t128": 0}
+        elif not (M >= 256 and N >= 256 and K % 64 == 0):
             variants.pop("g256")
+        def run(tile):
+            if f32 and tile is None:  # the production call (tile, split-K rounds, slabs / atomics)
+                return G.linear_wgrad(a_t, b_t, out)
+            return G.gemm(a_t, b_t, out, M, N, K, am, bm, a_t.stride(0), b_t.stride(0), N, epi,
+                          beta=1.0 if f32 else 0.0, tile=tile)
         for v, tile in variants.items():
-            G.gemm(a_t, b_t, out, M, N, K, am, bm, a_t.stride(0), b_t.stride(0), N, G.EPI_BF16, tile=tile)
+            out.zero_()
+            run(tile)
             err = ((out[:256].float() - ref).norm() / ref.norm()).item()
             runs[v] = {"err": err, "ms": []}
         runs["torch"] = {"ms": []}
         for _ in range(5):
             for v, tile in variants.items():
-                runs[v]["ms"].append(timeit(lambda: G.gemm(a_t, b_t, out, M, N, K, am, bm, a_t.stride(0),
-                                                             b_t.stride(0), N, G.EPI_BF16, tile=tile)))
+                runs[v]["ms"].append(timeit(lambda: run(tile)))
             runs["torch"]["ms"].append(timeit(lambda: torch.matmul(A, B.T)))
         flop = 2.0 * M * N * K
         res = {"shape": name, "M": M, "N": N, "K": K}
