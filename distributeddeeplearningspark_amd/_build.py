@@ -57,6 +57,12 @@ def _common_flags():
     ]
 
 
+# Per-kernel-file flags.  attention.hip: no SLP vectorisation (it packs the softmax row sums and the
+# O rescale into v_pk_add/v_pk_mul_f32, which cost 20+ cycles each beside MFMAs on gfx950) and no NaN
+# semantics for fmaxf (drops a canonicalising v_max per MFMA output in the running row maximum).
+_FILE_FLAGS = {"attention.hip": ["-fno-slp-vectorize", "-fno-honor-nans"]}
+
+
 def _binding_flags():
     import pybind11
     import torch
@@ -121,7 +127,7 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = True) ->
     hdr = _hdr_digest()
     base = _common_flags()
     bflags = base + _binding_flags()
-    tasks = [(s, base) for s in kern] + [(s, bflags) for s in rt] + [(s, bflags) for s in binding]
+    tasks = [(s, base + _FILE_FLAGS.get(s.name, [])) for s in kern] + [(s, bflags) for s in rt] + [(s, bflags) for s in binding]
     jobs = jobs or int(os.environ.get("MAX_JOBS", min(8, os.cpu_count() or 4)))
     objs, rebuilt = [], False
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:

@@ -103,7 +103,7 @@ struct AttnParams {
   const int* lens;                // [B] valid keys per sequence (nullable)
   int B, H, S;
   float scale, scale_log2;        // softmax scale, scale * log2(e)
-  uint32_t drop_thresh;           // attention-probability dropout (0 = off)
+  uint32_t drop_t8;               // attention-probability dropout: keep iff hash byte >= t8 (0 = off)
   float drop_scale;
   unsigned long long drop_seed;
   // backward only

@@ -24,6 +24,8 @@
 // keys (nullable -> all valid).
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "ddl_common.h"
 #include "ddl_ops.h"
 
@@ -82,8 +84,11 @@ __device__ __forceinline__ bf16x8 pack8(const f32x4& a, const f32x4& b) {
 
 __device__ __forceinline__ bf16x8 ldg_frag(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
-// Attention-probability dropout: keep (b, h, i, j) iff mix32(row_key(bh, i) + j) >= thresh.
-// The per-(row) key is hashed once, every element costs one 32-bit mix (vs a 64-bit hash).
+// Attention-probability dropout, rate quantised to 1/256 (uint8 thresholds): key j of query row r
+// is kept iff byte (j & 3) of hash24(row_key(r) + j / 4) is >= t8, and the kept probabilities are
+// scaled by 256 / (256 - t8).  One 32-bit hash serves four consecutive keys, and hash24 mixes with
+// 24-bit multiplies (v_mul_u32_u24, full rate) where a 32-bit mix costs two quarter-rate
+// v_mul_lo_u32; the per-row key keeps the full 32-bit mix (computed once per row).
 __device__ __forceinline__ uint32_t mix32(uint32_t x) {
   x ^= x >> 16;
   x *= 0x7feb352du;
@@ -95,11 +100,18 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
 __device__ __forceinline__ uint32_t row_key(unsigned long long seed, int bh, int S, int i) {
   return mix32((uint32_t)seed ^ mix32((uint32_t)(bh * S + i) + (uint32_t)(seed >> 32)));
 }
-// one 32-bit mix serves two neighbouring keys: key j uses the low (j even) / high (j odd) 16 bits
-// of mix32(rk + j/2), compared against th16 = thresh >> 16
-__device__ __forceinline__ uint32_t pair_hash(uint32_t rk, int j) { return mix32(rk + ((uint32_t)j >> 1)); }
-__device__ __forceinline__ bool keep_bits(uint32_t h, int j, uint32_t th16) {
-  return ((j & 1) ? (h >> 16) : (h & 0xffffu)) >= th16;
+__device__ __forceinline__ uint32_t hash24(uint32_t x) {
+  x ^= x >> 16;
+  x = __umul24(x, 0x7feb35u);
+  x ^= x >> 15;
+  x = __umul24(x, 0x846ca7u);
+  return x ^ (x >> 16);
+}
+__device__ __forceinline__ bool keep_byte(uint32_t h, int e, uint32_t t8) { return ((h >> (8 * e)) & 0xffu) >= t8; }
+// value of lane (lane & ~3) + E within each quad of lanes (DPP quad_perm [E,E,E,E])
+template <int E>
+__device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, E * 0x55, 0xf, 0xf, false);
 }
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
@@ -122,7 +134,16 @@ __device__ __forceinline__ void attn_block(const AttnParams& p, int& xb, int& h,
 }
 
 // ================================================================ forward
-template <int MINB>
+// Lazy rescaling: the running maximum m that a row's exponentials are taken against only moves when
+// a tile's scores exceed it by more than TAU (log2 units), so P = exp2(s*scale - m) <= 2^TAU (bf16
+// keeps its relative precision; O and l accumulate in fp32).  The common tile therefore needs no
+// cross-lane maximum (each lane tests its own 16 scores of the row against m) and no rescale of O
+// (64 packed multiplies per tile beside the MFMAs); the wave-uniform branch into the rescale is
+// taken on the first tile and rarely after.  Full tiles and the last partial tile (key padding) are
+// separate instantiations of the tile body, dropout is a template parameter: no branches inside it.
+constexpr float TAU = 8.f;
+
+template <int MINB, bool DROP>
 __global__ __launch_bounds__(THREADS, MINB) void attn_fwd_kernel(const AttnParams p) {
   __shared__ __attribute__((aligned(16))) char lds[2][2][TILE_BYTES];
   int xb, h, b;
@@ -136,6 +157,7 @@ __global__ __launch_bounds__(THREADS, MINB) void attn_fwd_kernel(const AttnParam
   const int len = p.lens ? min(max(p.lens[b], 0), S) : S;
   const int q0 = xb * BLOCK_ROWS + w * 32;
   const int bh = b * p.H + h;
+  const float sl = p.scale_log2;
 
   bf16x8 qf[2][2];
 #pragma unroll
@@ -149,94 +171,91 @@ __global__ __launch_bounds__(THREADS, MINB) void attn_fwd_kernel(const AttnParam
 #pragma unroll
     for (int it = 0; it < 2; ++it) o[dt][it] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
-  uint32_t rk[2];
+  uint32_t hk[2] = {0u, 0u};  // dropout: row key + the lane's key group (keys 4g..4g+3 of every 16)
+  if constexpr (DROP) {
 #pragma unroll
-  for (int it = 0; it < 2; ++it) rk[it] = row_key(p.drop_seed, bh, S, q0 + 16 * it + li);
-
-  const int nkt = (len + TQ - 1) / TQ;
-  if (nkt > 0) {
-    dma_tile(K, p.ld, 0, len, lds[0][0]);
-    dma_tile(V, p.ld, 0, len, lds[0][1]);
+    for (int it = 0; it < 2; ++it) hk[it] = row_key(p.drop_seed, bh, S, q0 + 16 * it + li) + (uint32_t)g;
   }
-  wait_vmcnt<0>();
-  __syncthreads();
-  for (int t = 0; t < nkt; ++t) {
-    const char* kl = lds[t & 1][0];
-    const char* vl = lds[t & 1][1];
-    const bool more = t + 1 < nkt;
-    if (more) {
-      dma_tile(K, p.ld, (t + 1) * TQ, len, lds[(t + 1) & 1][0]);
-      dma_tile(V, p.ld, (t + 1) * TQ, len, lds[(t + 1) & 1][1]);
-    }
-    // the 64-key tile as two 32-key online-softmax steps (one half's scores live at a time)
+  const uint32_t t8 = p.drop_t8;
+
+  // one 64-key tile: S^T[j = kb + 16jt + 4g + e][i = 16it + li] for all four 16-key groups jt, then
+  // P^T and O^T[d][i] += sum_j V^T[d][j] P^T[j][i] per 32-key MFMA step kk (jt = 2kk, 2kk + 1)
+  auto tile = [&](const char* kl, const char* vl, const int kb, auto masked) {
+    constexpr bool MASK = decltype(masked)::value;
+    f32x4 s[4][2];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      // S^T[j = 32kk + 16j2 + 4g + e][i = 16it + li]
-      f32x4 s[2][2];
-#pragma unroll
-      for (int j2 = 0; j2 < 2; ++j2) {
-        const int jt = 2 * kk + j2;
-        const bf16x8 k0 = frag_row(kl, 16 * jt + li, 0, g), k1 = frag_row(kl, 16 * jt + li, 1, g);
-#pragma unroll
-        for (int it = 0; it < 2; ++it) {
-          f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
-          a = mfma16x16x32(k0, qf[it][0], a);
-          s[j2][it] = mfma16x16x32(k1, qf[it][1], a);
-        }
-      }
-      const int kb = t * TQ + 32 * kk;
-      const bool full = kb + 32 <= len;  // half fully inside the valid keys (wave-uniform)
+    for (int jt = 0; jt < 4; ++jt) {
+      const bf16x8 k0 = frag_row(kl, 16 * jt + li, 0, g), k1 = frag_row(kl, 16 * jt + li, 1, g);
 #pragma unroll
       for (int it = 0; it < 2; ++it) {
-        float mx = -INFINITY;
-        if (!full) {
+        f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
+        a = mfma16x16x32(k0, qf[it][0], a);
+        s[jt][it] = mfma16x16x32(k1, qf[it][1], a);
+      }
+    }
+    if constexpr (MASK) {
 #pragma unroll
-          for (int j2 = 0; j2 < 2; ++j2)
+      for (int jt = 0; jt < 4; ++jt)
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-              if (kb + 16 * j2 + 4 * g + e >= len) s[j2][it][e] = -INFINITY;
-        }
+        for (int it = 0; it < 2; ++it)
 #pragma unroll
-        for (int j2 = 0; j2 < 2; ++j2)
+          for (int e = 0; e < 4; ++e)
+            if (kb + 16 * jt + 4 * g + e >= len) s[jt][it][e] = -INFINITY;
+    }
+    float lmx[2];
+    bool need = false;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) mx = fmaxf(mx, s[j2][it][e]);
+    for (int it = 0; it < 2; ++it) {
+      float mx = s[0][it][0];
+#pragma unroll
+      for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) mx = fmaxf(mx, s[jt][it][e]);
+      lmx[it] = mx;
+      need = need || (mx * sl > m[it] + TAU);
+    }
+    if (__any(need)) {  // wave-uniform: move the maximum of every row of the wave, rescale O and l
+#pragma unroll
+      for (int it = 0; it < 2; ++it) {
+        float mx = lmx[it];
         mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        const float mn = fmaxf(m[it], mx * p.scale_log2);  // running max of the scaled (log2) scores
-        const float alpha = fexp2(m[it] - mn);
+        const float mn = fmaxf(m[it], mx * sl);
+        const float alpha = m[it] == -INFINITY ? 0.f : fexp2(m[it] - mn);
         m[it] = mn;
+        l[it] *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[dt][it] *= alpha;
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int it = 0; it < 2; ++it) {
         float rs = 0.f;
 #pragma unroll
         for (int j2 = 0; j2 < 2; ++j2)
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const float pv = fexp2(fmaf(s[j2][it][e], p.scale_log2, -mn));
-            s[j2][it][e] = pv;
+            const float pv = fexp2(fmaf(s[2 * kk + j2][it][e], sl, -m[it]));
+            s[2 * kk + j2][it][e] = pv;
             rs += pv;
           }
-        l[it] = l[it] * alpha + rs;
-        if (!__all(alpha == 1.f)) {  // the running max moved for some query of the wave
-#pragma unroll
-          for (int dt = 0; dt < 4; ++dt) o[dt][it] *= alpha;
-        }
+        l[it] += rs;  // the softmax denominator sums the probabilities before dropout
       }
-      if (p.drop_thresh) {
-        const uint32_t th16 = p.drop_thresh >> 16;
+      if constexpr (DROP) {
 #pragma unroll
         for (int it = 0; it < 2; ++it)
 #pragma unroll
-          for (int j2 = 0; j2 < 2; ++j2)
+          for (int j2 = 0; j2 < 2; ++j2) {
+            const uint32_t hh = hash24(hk[it] + (uint32_t)((kb >> 2) + 8 * kk + 4 * j2));
 #pragma unroll
-            for (int e = 0; e < 4; e += 2) {
-              const int j = kb + 16 * j2 + 4 * g + e;
-              const uint32_t h = pair_hash(rk[it], j);
-              s[j2][it][e] = keep_bits(h, j, th16) ? s[j2][it][e] * p.drop_scale : 0.f;
-              s[j2][it][e + 1] = keep_bits(h, j + 1, th16) ? s[j2][it][e + 1] * p.drop_scale : 0.f;
-            }
+            for (int e = 0; e < 4; ++e)
+              if (!keep_byte(hh, e, t8)) s[2 * kk + j2][it][e] = 0.f;
+          }
       }
-      // O^T[d][i] += sum_j V^T[d][j] P^T[j][i]
-      const bf16x8 pb0 = pack8(s[0][0], s[1][0]);
-      const bf16x8 pb1 = pack8(s[0][1], s[1][1]);
+      const bf16x8 pb0 = pack8(s[2 * kk][0], s[2 * kk + 1][0]);
+      const bf16x8 pb1 = pack8(s[2 * kk][1], s[2 * kk + 1][1]);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const bf16x8 va = frag_col(vl, 32 * kk + 4 * g, 32 * kk + 16 + 4 * g, 16 * dt, lane);
@@ -244,15 +263,34 @@ __global__ __launch_bounds__(THREADS, MINB) void attn_fwd_kernel(const AttnParam
         o[dt][1] = mfma16x16x32(va, pb1, o[dt][1]);
       }
     }
+  };
+
+  const int nkt = (len + TQ - 1) / TQ, nfull = len / TQ;
+  if (nkt > 0) {
+    dma_tile(K, p.ld, 0, len, lds[0][0]);
+    dma_tile(V, p.ld, 0, len, lds[0][1]);
+  }
+  wait_vmcnt<0>();
+  __syncthreads();
+  // full tiles in one loop (one instantiation: no register copies at the back edge), then the
+  // partial tile of a padded sequence
+  for (int t = 0; t < nfull; ++t) {
+    if (t + 1 < nkt) {
+      dma_tile(K, p.ld, (t + 1) * TQ, len, lds[(t + 1) & 1][0]);
+      dma_tile(V, p.ld, (t + 1) * TQ, len, lds[(t + 1) & 1][1]);
+    }
+    tile(lds[t & 1][0], lds[t & 1][1], t * TQ, std::false_type{});
     wait_vmcnt<0>();
     __syncthreads();
   }
+  if (nfull < nkt) tile(lds[nfull & 1][0], lds[nfull & 1][1], nfull * TQ, std::true_type{});
+  const float num = DROP ? p.drop_scale : 1.f;  // the dropout scale folds into the normalisation
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
     float lt = l[it];
     lt += __shfl_xor(lt, 16, 64);
     lt += __shfl_xor(lt, 32, 64);
-    const float inv = lt > 0.f ? 1.f / lt : 0.f;
+    const float inv = lt > 0.f ? num / lt : 0.f;
     const int i = q0 + 16 * it + li;
     bf16_t* orow = p.o + (tok0 + i) * p.ldo + h * HD;
 #pragma unroll
@@ -295,11 +333,13 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const AttnParams p, l
 }
 
 // ================================================================ backward: dK, dV
-// MINB = resident blocks per CU the register allocation is capped for: 1 (351 registers, no
-// spills) or 2 (256 registers with ~31 dwords of scratch spills, twice the waves to hide latency);
-// picked at launch by DDL_ATTN_DKDV_OCC (default 2: attention backward with dropout 0.276 -> 0.259 ms
-// per BERT-base layer, BERT 645K -> 650K tok/s)
-template <int MINB>
+// MINB = resident blocks per CU the register allocation is capped for: 1 (no spills) or 2 (twice the
+// waves to hide latency); picked at launch by DDL_ATTN_DKDV_OCC (default 2).  Dropout is a template
+// parameter; key padding is a second instantiation of the q-tile loop, chosen per workgroup (only
+// workgroups whose 128 keys straddle the padding pay for the mask).  A lane holds P[i][j] for four
+// consecutive queries i of one key j, and the dropout bytes of a (query, 4-key group) come from one
+// hash: lane r of each quad hashes query row r, the quad shares the four hashes by DPP broadcast.
+template <int MINB, bool DROP>
 __global__ __launch_bounds__(THREADS, MINB) void attn_bwd_dkdv_kernel(const AttnParams p) {
   __shared__ __attribute__((aligned(16))) char lds[2][2][TILE_BYTES];  // [buf][Q, dO]
   __shared__ __attribute__((aligned(16))) float s_lse[2][TQ];
@@ -321,6 +361,8 @@ __global__ __launch_bounds__(THREADS, MINB) void attn_bwd_dkdv_kernel(const Attn
   const int k0 = xb * BLOCK_ROWS + w * 32;
   bf16_t* dK = p.dqkv + tok0 * p.lddqkv + p.k_off + h * HD;
   bf16_t* dV = p.dqkv + tok0 * p.lddqkv + p.v_off + h * HD;
+  const float sl = p.scale_log2, dsc = p.drop_scale;
+  const uint32_t t8 = p.drop_t8;
 
   // K / V fragments as the B operand of S = Q K^T and dP = dO V^T: [d][j = 16jt + li]
   bf16x8 kf[2][2], vf[2][2];
@@ -348,99 +390,118 @@ __global__ __launch_bounds__(THREADS, MINB) void attn_bwd_dkdv_kernel(const Attn
     if (threadIdx.x < TQ) {
       s_lse[0][threadIdx.x] = lse[threadIdx.x];
       s_d[0][threadIdx.x] = dv[threadIdx.x];
-      s_rk[0][threadIdx.x] = row_key(p.drop_seed, bh, S, threadIdx.x);
+      if constexpr (DROP) s_rk[0][threadIdx.x] = row_key(p.drop_seed, bh, S, threadIdx.x);
     }
   }
   wait_vmcnt<0>();
   __syncthreads();
-  for (int t = 0; t < nqt; ++t) {
-    const int buf = t & 1;
-    const char* ql = lds[buf][0];
-    const char* dl = lds[buf][1];
-    const bool more = t + 1 < nqt;
-    if (more) {
-      dma_tile(Q, p.ld, (t + 1) * TQ, S, lds[buf ^ 1][0]);
-      dma_tile(dO, p.lddo, (t + 1) * TQ, S, lds[buf ^ 1][1]);
-      if (threadIdx.x < TQ) {
-        r_lse = lse[(t + 1) * TQ + threadIdx.x];
-        r_d = dv[(t + 1) * TQ + threadIdx.x];
-        r_rk = row_key(p.drop_seed, bh, S, (t + 1) * TQ + threadIdx.x);
-      }
-    }
-    // The 64-query tile is processed as two 32-query halves: S / dP of one half (16 fp32 per
-    // lane each) are consumed by the dV / dK MFMAs before the next half is formed, which keeps
-    // the kernel inside 256 registers at 2 workgroups/CU without scratch spills.
-    const bool kfull = k0 + 32 <= len;  // this wave's 32 keys all valid (wave-uniform)
-    const uint32_t th16 = p.drop_thresh >> 16;
+
+  auto qloop = [&](auto masked) {
+    constexpr bool MASK = decltype(masked)::value;
+    bool jok[2];  // key padding (MASK only): this lane's key of group jt is valid
 #pragma unroll
-    for (int kq = 0; kq < 2; ++kq) {
-      // S, dP: [i = 32kq + 16i2 + 4g + e][j = 16jt + li]
-      f32x4 s[2][2], dp[2][2];
-#pragma unroll
-      for (int i2 = 0; i2 < 2; ++i2) {
-        const int it = 2 * kq + i2;
-        const bf16x8 q0f = frag_row(ql, 16 * it + li, 0, g), q1f = frag_row(ql, 16 * it + li, 1, g);
-        const bf16x8 d0f = frag_row(dl, 16 * it + li, 0, g), d1f = frag_row(dl, 16 * it + li, 1, g);
-#pragma unroll
-        for (int jt = 0; jt < 2; ++jt) {
-          f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f}, c = f32x4{0.f, 0.f, 0.f, 0.f};
-          a = mfma16x16x32(q0f, kf[jt][0], a);
-          s[i2][jt] = mfma16x16x32(q1f, kf[jt][1], a);
-          c = mfma16x16x32(d0f, vf[jt][0], c);
-          dp[i2][jt] = mfma16x16x32(d1f, vf[jt][1], c);
+    for (int jt = 0; jt < 2; ++jt) jok[jt] = k0 + 16 * jt + li < len;
+    for (int t = 0; t < nqt; ++t) {
+      const int buf = t & 1;
+      const char* ql = lds[buf][0];
+      const char* dl = lds[buf][1];
+      const bool more = t + 1 < nqt;
+      if (more) {
+        dma_tile(Q, p.ld, (t + 1) * TQ, S, lds[buf ^ 1][0]);
+        dma_tile(dO, p.lddo, (t + 1) * TQ, S, lds[buf ^ 1][1]);
+        if (threadIdx.x < TQ) {
+          r_lse = lse[(t + 1) * TQ + threadIdx.x];
+          r_d = dv[(t + 1) * TQ + threadIdx.x];
+          if constexpr (DROP) r_rk = row_key(p.drop_seed, bh, S, (t + 1) * TQ + threadIdx.x);
         }
       }
-      // P, dS (dropout-scaled P kept in s[] for dV); the lane's 4 query rows of a 16-row group
-      // are consecutive, so their lse / D / dropout keys are one 16-B LDS read each
+      // The 64-query tile is processed as two 32-query halves: S / dP of one half (16 fp32 per
+      // lane each) are consumed by the dV / dK MFMAs before the next half is formed.
 #pragma unroll
-      for (int i2 = 0; i2 < 2; ++i2) {
-        const int il0 = 16 * (2 * kq + i2) + 4 * g;
-        const f32x4 lq4 = *reinterpret_cast<const f32x4*>(&s_lse[buf][il0]);
-        const f32x4 dq4 = *reinterpret_cast<const f32x4*>(&s_d[buf][il0]);
-        const uint4 rk4 = *reinterpret_cast<const uint4*>(&s_rk[buf][il0]);
-        const uint32_t rkv[4] = {rk4.x, rk4.y, rk4.z, rk4.w};
+      for (int kq = 0; kq < 2; ++kq) {
+        // S, dP: [i = 32kq + 16i2 + 4g + e][j = 16jt + li]
+        f32x4 s[2][2], dp[2][2];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
+        for (int i2 = 0; i2 < 2; ++i2) {
+          const int it = 2 * kq + i2;
+          const bf16x8 q0f = frag_row(ql, 16 * it + li, 0, g), q1f = frag_row(ql, 16 * it + li, 1, g);
+          const bf16x8 d0f = frag_row(dl, 16 * it + li, 0, g), d1f = frag_row(dl, 16 * it + li, 1, g);
 #pragma unroll
           for (int jt = 0; jt < 2; ++jt) {
-            const int j = k0 + 16 * jt + li;
-            float pv = fexp2(fmaf(s[i2][jt][e], p.scale_log2, -lq4[e]));
-            if (!kfull && j >= len) pv = 0.f;
-            float keep = 1.f;
-            if (p.drop_thresh) keep = keep_bits(pair_hash(rkv[e], j), j, th16) ? p.drop_scale : 0.f;
-            dp[i2][jt][e] = pv * (dp[i2][jt][e] * keep - dq4[e]);  // dS
-            s[i2][jt][e] = pv * keep;                              // dropped P (for dV)
+            f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f}, c = f32x4{0.f, 0.f, 0.f, 0.f};
+            a = mfma16x16x32(q0f, kf[jt][0], a);
+            s[i2][jt] = mfma16x16x32(q1f, kf[jt][1], a);
+            c = mfma16x16x32(d0f, vf[jt][0], c);
+            dp[i2][jt] = mfma16x16x32(d1f, vf[jt][1], c);
+          }
+        }
+        // P, dS (dropout-scaled P kept in s[] for dV); the lane's 4 query rows of a 16-row group
+        // are consecutive, so their lse / D are one 16-B LDS read each
+#pragma unroll
+        for (int i2 = 0; i2 < 2; ++i2) {
+          const int il0 = 16 * (2 * kq + i2) + 4 * g;
+          const f32x4 lq4 = *reinterpret_cast<const f32x4*>(&s_lse[buf][il0]);
+          const f32x4 dq4 = *reinterpret_cast<const f32x4*>(&s_d[buf][il0]);
+          uint32_t hq[2][4];  // [jt][e]: dropout hash of (query il0 + e, key group of j)
+          if constexpr (DROP) {
+            const uint32_t rkr = s_rk[buf][il0 + (li & 3)];
+#pragma unroll
+            for (int jt = 0; jt < 2; ++jt) {
+              const uint32_t hm = hash24(rkr + (uint32_t)((k0 + 16 * jt + li) >> 2));
+              hq[jt][0] = quad_bcast<0>(hm);
+              hq[jt][1] = quad_bcast<1>(hm);
+              hq[jt][2] = quad_bcast<2>(hm);
+              hq[jt][3] = quad_bcast<3>(hm);
+            }
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+#pragma unroll
+            for (int jt = 0; jt < 2; ++jt) {
+              float pv = fexp2(fmaf(s[i2][jt][e], sl, -lq4[e]));
+              if constexpr (MASK) pv = jok[jt] ? pv : 0.f;
+              float dpv = dp[i2][jt][e], pd = pv;
+              if constexpr (DROP) {
+                const bool keep = keep_byte(hq[jt][e], li & 3, t8);
+                dpv = keep ? dpv * dsc : 0.f;
+                pd = keep ? pv * dsc : 0.f;
+              }
+              dp[i2][jt][e] = pv * (dpv - dq4[e]);  // dS
+              s[i2][jt][e] = pd;                    // dropped P (for dV)
+            }
+          }
+        }
+        // dV[j][d] += sum_i Pd[i][j] dO[i][d] ; dK[j][d] += sum_i dS[i][j] Q[i][d]
+        bf16x8 pa[2], sa[2];
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt) {
+          pa[jt] = pack8(s[0][jt], s[1][jt]);
+          sa[jt] = pack8(dp[0][jt], dp[1][jt]);
+        }
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const bf16x8 db = frag_col(dl, 32 * kq + 4 * g, 32 * kq + 16 + 4 * g, 16 * dt, lane);
+          const bf16x8 qb2 = frag_col(ql, 32 * kq + 4 * g, 32 * kq + 16 + 4 * g, 16 * dt, lane);
+#pragma unroll
+          for (int jt = 0; jt < 2; ++jt) {
+            adv[jt][dt] = mfma16x16x32(pa[jt], db, adv[jt][dt]);
+            adk[jt][dt] = mfma16x16x32(sa[jt], qb2, adk[jt][dt]);
           }
         }
       }
-      // dV[j][d] += sum_i Pd[i][j] dO[i][d] ; dK[j][d] += sum_i dS[i][j] Q[i][d]
-      bf16x8 pa[2], sa[2];
-#pragma unroll
-      for (int jt = 0; jt < 2; ++jt) {
-        pa[jt] = pack8(s[0][jt], s[1][jt]);
-        sa[jt] = pack8(dp[0][jt], dp[1][jt]);
-      }
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const bf16x8 db = frag_col(dl, 32 * kq + 4 * g, 32 * kq + 16 + 4 * g, 16 * dt, lane);
-        const bf16x8 qb2 = frag_col(ql, 32 * kq + 4 * g, 32 * kq + 16 + 4 * g, 16 * dt, lane);
-#pragma unroll
-        for (int jt = 0; jt < 2; ++jt) {
-          adv[jt][dt] = mfma16x16x32(pa[jt], db, adv[jt][dt]);
-          adk[jt][dt] = mfma16x16x32(sa[jt], qb2, adk[jt][dt]);
+      if (more) {
+        if (threadIdx.x < TQ) {
+          s_lse[buf ^ 1][threadIdx.x] = r_lse;
+          s_d[buf ^ 1][threadIdx.x] = r_d;
+          if constexpr (DROP) s_rk[buf ^ 1][threadIdx.x] = r_rk;
         }
       }
+      wait_vmcnt<0>();
+      __syncthreads();
     }
-    if (more) {
-      if (threadIdx.x < TQ) {
-        s_lse[buf ^ 1][threadIdx.x] = r_lse;
-        s_d[buf ^ 1][threadIdx.x] = r_d;
-        s_rk[buf ^ 1][threadIdx.x] = r_rk;
-      }
-    }
-    wait_vmcnt<0>();
-    __syncthreads();
-  }
+  };
+  if ((xb + 1) * BLOCK_ROWS <= len) qloop(std::false_type{});
+  else qloop(std::true_type{});
 #pragma unroll
   for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
@@ -455,7 +516,7 @@ __global__ __launch_bounds__(THREADS, MINB) void attn_bwd_dkdv_kernel(const Attn
 }
 
 // ================================================================ backward: dQ
-template <int MINB>
+template <int MINB, bool DROP>
 __global__ __launch_bounds__(THREADS, MINB) void attn_bwd_dq_kernel(const AttnParams p) {
   __shared__ __attribute__((aligned(16))) char lds[2][2][TILE_BYTES];  // [buf][K, V]
   int xb, h, b;
@@ -471,10 +532,12 @@ __global__ __launch_bounds__(THREADS, MINB) void attn_bwd_dq_kernel(const AttnPa
   const int len = p.lens ? min(max(p.lens[b], 0), S) : S;
   const int q0 = xb * BLOCK_ROWS + w * 32;
   bf16_t* dQ = p.dqkv + tok0 * p.lddqkv + p.q_off + h * HD;
+  const float sl = p.scale_log2, dsc = p.drop_scale;
+  const uint32_t t8 = p.drop_t8;
 
   bf16x8 qf[2][2], df[2][2];
   float lq[2], dq[2];
-  uint32_t rk[2];
+  uint32_t hk[2] = {0u, 0u};  // dropout: row key + the lane's key group
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
     const int i = q0 + 16 * it + li;
@@ -485,7 +548,7 @@ __global__ __launch_bounds__(THREADS, MINB) void attn_bwd_dq_kernel(const AttnPa
     }
     lq[it] = p.lse[(long)bh * S + i];
     dq[it] = p.dvec[(long)bh * S + i];
-    rk[it] = row_key(p.drop_seed, bh, S, i);
+    if constexpr (DROP) hk[it] = row_key(p.drop_seed, bh, S, i) + (uint32_t)g;
   }
   f32x4 acc[2][4];  // dQ[i = 16it + 4g + e][d = 16dt + li]
 #pragma unroll
@@ -493,28 +556,12 @@ __global__ __launch_bounds__(THREADS, MINB) void attn_bwd_dq_kernel(const AttnPa
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) acc[it][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nkt = (len + TQ - 1) / TQ;
-  if (nkt > 0) {
-    dma_tile(K, p.ld, 0, len, lds[0][0]);
-    dma_tile(V, p.ld, 0, len, lds[0][1]);
-  }
-  wait_vmcnt<0>();
-  __syncthreads();
-  for (int t = 0; t < nkt; ++t) {
-    const char* kl = lds[t & 1][0];
-    const char* vl = lds[t & 1][1];
-    const bool more = t + 1 < nkt;
-    if (more) {
-      dma_tile(K, p.ld, (t + 1) * TQ, len, lds[(t + 1) & 1][0]);
-      dma_tile(V, p.ld, (t + 1) * TQ, len, lds[(t + 1) & 1][1]);
-    }
-    const int kb = t * TQ;
-    const bool full = kb + TQ <= len;
-    const uint32_t th16 = p.drop_thresh >> 16;
-    // the 64-key tile as two 32-key halves (S^T / dP^T of one half live at a time)
+  // one 64-key tile as two 32-key halves (S^T / dP^T of one half live at a time)
+  auto tile = [&](const char* kl, const char* vl, const int kb, auto masked) {
+    constexpr bool MASK = decltype(masked)::value;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      // S^T, dP^T: [j = 32kk + 16j2 + 4g + e][i = 16it + li]
+      // S^T, dP^T: [j = kb + 32kk + 16j2 + 4g + e][i = 16it + li]
       f32x4 s[2][2], dp[2][2];
 #pragma unroll
       for (int j2 = 0; j2 < 2; ++j2) {
@@ -533,25 +580,20 @@ __global__ __launch_bounds__(THREADS, MINB) void attn_bwd_dq_kernel(const AttnPa
 #pragma unroll
       for (int j2 = 0; j2 < 2; ++j2)
 #pragma unroll
-        for (int it = 0; it < 2; ++it)
+        for (int it = 0; it < 2; ++it) {
+          uint32_t hh = 0u;
+          if constexpr (DROP) hh = hash24(hk[it] + (uint32_t)((kb >> 2) + 8 * kk + 4 * j2));
 #pragma unroll
-          for (int e = 0; e < 4; e += 2) {
-            const int j = kb + 16 * (2 * kk + j2) + 4 * g + e;
-            float p0 = fexp2(fmaf(s[j2][it][e], p.scale_log2, -lq[it]));
-            float p1 = fexp2(fmaf(s[j2][it][e + 1], p.scale_log2, -lq[it]));
-            if (!full) {
-              if (j >= len) p0 = 0.f;
-              if (j + 1 >= len) p1 = 0.f;
+          for (int e = 0; e < 4; ++e) {
+            float pv = fexp2(fmaf(s[j2][it][e], sl, -lq[it]));
+            if constexpr (MASK) {
+              if (kb + 32 * kk + 16 * j2 + 4 * g + e >= len) pv = 0.f;
             }
-            float k0v = 1.f, k1v = 1.f;
-            if (p.drop_thresh) {
-              const uint32_t h = pair_hash(rk[it], j);
-              k0v = keep_bits(h, j, th16) ? p.drop_scale : 0.f;
-              k1v = keep_bits(h, j + 1, th16) ? p.drop_scale : 0.f;
-            }
-            s[j2][it][e] = p0 * (dp[j2][it][e] * k0v - dq[it]);  // dS^T
-            s[j2][it][e + 1] = p1 * (dp[j2][it][e + 1] * k1v - dq[it]);
+            float dpv = dp[j2][it][e];
+            if constexpr (DROP) dpv = keep_byte(hh, e, t8) ? dpv * dsc : 0.f;
+            s[j2][it][e] = pv * (dpv - dq[it]);  // dS^T
           }
+        }
       // dQ[i][d] += sum_j dS[i][j] K[j][d]
       const bf16x8 a0 = pack8(s[0][0], s[1][0]);
       const bf16x8 a1 = pack8(s[0][1], s[1][1]);
@@ -562,9 +604,27 @@ __global__ __launch_bounds__(THREADS, MINB) void attn_bwd_dq_kernel(const AttnPa
         acc[1][dt] = mfma16x16x32(a1, kb2, acc[1][dt]);
       }
     }
+  };
+
+  const int nkt = (len + TQ - 1) / TQ, nfull = len / TQ;
+  if (nkt > 0) {
+    dma_tile(K, p.ld, 0, len, lds[0][0]);
+    dma_tile(V, p.ld, 0, len, lds[0][1]);
+  }
+  wait_vmcnt<0>();
+  __syncthreads();
+  // full tiles in one loop (one instantiation: no register copies at the back edge), then the
+  // partial tile of a padded sequence
+  for (int t = 0; t < nfull; ++t) {
+    if (t + 1 < nkt) {
+      dma_tile(K, p.ld, (t + 1) * TQ, len, lds[(t + 1) & 1][0]);
+      dma_tile(V, p.ld, (t + 1) * TQ, len, lds[(t + 1) & 1][1]);
+    }
+    tile(lds[t & 1][0], lds[t & 1][1], t * TQ, std::false_type{});
     wait_vmcnt<0>();
     __syncthreads();
   }
+  if (nfull < nkt) tile(lds[nfull & 1][0], lds[nfull & 1][1], nfull * TQ, std::true_type{});
 #pragma unroll
   for (int it = 0; it < 2; ++it)
 #pragma unroll
@@ -582,15 +642,22 @@ static int attn_xcd() {
   return v;
 }
 
+#define DDL_ATTN_LAUNCH(KERNEL, grid, MINB, drop, s, p)                                   \
+  do {                                                                                   \
+    if (drop) hipLaunchKernelGGL((KERNEL<MINB, true>), grid, dim3(THREADS), 0, s, p);    \
+    else hipLaunchKernelGGL((KERNEL<MINB, false>), grid, dim3(THREADS), 0, s, p);        \
+  } while (0)
+
 int attn_fwd(const AttnParams& p_in, hipStream_t s) {
   if (p_in.B <= 0) return 0;
   AttnParams p = p_in;
   p.xcd_remap = attn_xcd();
-  static const int occ = getenv("DDL_ATTN_FWD_OCC") ? atoi(getenv("DDL_ATTN_FWD_OCC")) : 2;
-  if (occ == 3)
-    hipLaunchKernelGGL(attn_fwd_kernel<3>, dim3(p.S / BLOCK_ROWS, p.H, p.B), dim3(THREADS), 0, s, p);
-  else
-    hipLaunchKernelGGL(attn_fwd_kernel<2>, dim3(p.S / BLOCK_ROWS, p.H, p.B), dim3(THREADS), 0, s, p);
+  const dim3 grid(p.S / BLOCK_ROWS, p.H, p.B);
+  const bool drop = p.drop_t8 != 0;
+  static const int occ = getenv("DDL_ATTN_FWD_OCC") ? atoi(getenv("DDL_ATTN_FWD_OCC")) : 3;
+  if (occ == 2) DDL_ATTN_LAUNCH(attn_fwd_kernel, grid, 2, drop, s, p);
+  else if (occ == 4) DDL_ATTN_LAUNCH(attn_fwd_kernel, grid, 4, drop, s, p);
+  else DDL_ATTN_LAUNCH(attn_fwd_kernel, grid, 3, drop, s, p);
   return (int)hipGetLastError();
 }
 
@@ -599,19 +666,15 @@ int attn_bwd(const AttnParams& p_in, hipStream_t s) {
   AttnParams p = p_in;
   p.xcd_remap = attn_xcd();
   const long rows = (long)p.B * p.S * p.H;
+  const dim3 grid(p.S / BLOCK_ROWS, p.H, p.B);
+  const bool drop = p.drop_t8 != 0;
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s, p, rows);
   static const int dkdv_occ = getenv("DDL_ATTN_DKDV_OCC") ? atoi(getenv("DDL_ATTN_DKDV_OCC")) : 2;
-  if (dkdv_occ == 3)
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<3>, dim3(p.S / BLOCK_ROWS, p.H, p.B), dim3(THREADS), 0, s, p);
-  else if (dkdv_occ != 1)
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<2>, dim3(p.S / BLOCK_ROWS, p.H, p.B), dim3(THREADS), 0, s, p);
-  else
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<1>, dim3(p.S / BLOCK_ROWS, p.H, p.B), dim3(THREADS), 0, s, p);
+  if (dkdv_occ == 1) DDL_ATTN_LAUNCH(attn_bwd_dkdv_kernel, grid, 1, drop, s, p);
+  else DDL_ATTN_LAUNCH(attn_bwd_dkdv_kernel, grid, 2, drop, s, p);
   static const int dq_occ = getenv("DDL_ATTN_DQ_OCC") ? atoi(getenv("DDL_ATTN_DQ_OCC")) : 2;
-  if (dq_occ == 3)
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<3>, dim3(p.S / BLOCK_ROWS, p.H, p.B), dim3(THREADS), 0, s, p);
-  else
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<2>, dim3(p.S / BLOCK_ROWS, p.H, p.B), dim3(THREADS), 0, s, p);
+  if (dq_occ == 3) DDL_ATTN_LAUNCH(attn_bwd_dq_kernel, grid, 3, drop, s, p);
+  else DDL_ATTN_LAUNCH(attn_bwd_dq_kernel, grid, 2, drop, s, p);
   return (int)hipGetLastError();
 }
 

@@ -4,6 +4,7 @@
 #include <ATen/DeviceGuard.h>
 
 #include <algorithm>
+#include <cmath>
 
 #include "ddl_ops.h"
 
@@ -30,7 +31,6 @@ T* optr(const c10::optional<at::Tensor>& t) {
   return t ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
 }
 
-uint32_t thresh_of(double p) { return p > 0 ? (uint32_t)std::min(4294967295.0, p * 4294967296.0) : 0u; }
 
 // qkv: [B*S, ld] bf16 (row stride ld, 2-D view allowed), heads of 64
 AttnParams make_params(const at::Tensor& qkv, int64_t B, int64_t S, int64_t H, int64_t q_off, int64_t k_off,
@@ -68,8 +68,10 @@ AttnParams make_params(const at::Tensor& qkv, int64_t B, int64_t S, int64_t H, i
   p.S = (int)S;
   p.scale = (float)scale;
   p.scale_log2 = (float)(scale * 1.4426950408889634);
-  p.drop_thresh = thresh_of(drop_p);
-  p.drop_scale = drop_p > 0 ? (float)(1.0 / (1.0 - drop_p)) : 1.f;
+  // attention dropout rate quantised to 1/256 (ops/transformer.py attn_drop_t8); the kept
+  // probabilities are scaled by the inverse of the quantised keep rate
+  p.drop_t8 = drop_p > 0 ? (uint32_t)std::min(255.0, std::max(1.0, std::nearbyint(drop_p * 256.0))) : 0u;
+  p.drop_scale = p.drop_t8 ? (float)(256.0 / (256.0 - p.drop_t8)) : 1.f;
   p.drop_seed = (unsigned long long)seed;
   return p;
 }

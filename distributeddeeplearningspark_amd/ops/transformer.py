@@ -59,18 +59,38 @@ def mix32_ref(x: torch.Tensor) -> torch.Tensor:
     return x ^ (x >> 16)
 
 
+def hash24_ref(x: torch.Tensor) -> torch.Tensor:
+    """``hash24`` of csrc/kernels/attention.hip: the 32-bit mix with 24-bit multiplies (v_mul_u32_u24)."""
+    m = 0xFFFFFFFF
+    x = x & m
+    x = x ^ (x >> 16)
+    x = ((x & 0xFFFFFF) * 0x7FEB35) & m
+    x = x ^ (x >> 15)
+    x = ((x & 0xFFFFFF) * 0x846CA7) & m
+    return x ^ (x >> 16)
+
+
+def attn_drop_t8(p: float) -> int:
+    """Attention dropout threshold byte: the rate is quantised to t8 / 256 (p = 0.1 -> 26 / 256)."""
+    return min(255, max(1, int(round(p * 256.0)))) if p > 0 else 0
+
+
+def attn_drop_scale(p: float) -> float:
+    """Scale of the kept attention probabilities: the inverse of the quantised keep rate."""
+    t8 = attn_drop_t8(p)
+    return 256.0 / (256.0 - t8) if t8 else 1.0
+
+
 def attn_keep_ref(seed: int, row: torch.Tensor, j: torch.Tensor, p: float) -> torch.Tensor:
-    """Attention-probability dropout mask.  One 32-bit hash h = mix32(row_key(row) + j // 2)
-    serves a pair of keys: key j keeps iff its 16-bit half (low for even j, high for odd j)
-    is >= floor(p * 2^32) >> 16, with row_key = mix32(seed_lo ^ mix32(row + seed_hi)) and
-    row = (b*H + h)*S + i."""
+    """Attention-probability dropout mask.  One 32-bit hash h = hash24(row_key(row) + j // 4)
+    serves four consecutive keys: key j keeps iff byte j % 4 of h is >= attn_drop_t8(p), with
+    row_key = mix32(seed_lo ^ mix32(row + seed_hi)) and row = (b*H + h)*S + i."""
     s = seed & 0xFFFFFFFFFFFFFFFF
     lo, hi = s & 0xFFFFFFFF, s >> 32
     rk = mix32_ref(lo ^ mix32_ref(row.to(torch.int64) + hi))
     j = j.to(torch.int64)
-    h = mix32_ref(rk + (j >> 1))
-    bits = torch.where((j & 1) == 1, h >> 16, h & 0xFFFF)
-    return bits >= (drop_thresh(p) >> 16)
+    h = hash24_ref(rk + (j >> 2))
+    return ((h >> (8 * (j & 3))) & 0xFF) >= attn_drop_t8(p)
 
 
 def attention_ref(qkv, B, S, H, q_off, k_off, v_off, lens=None, scale=0.125, drop_p=0.0, seed=0):
@@ -93,7 +113,7 @@ def attention_ref(qkv, B, S, H, q_off, k_off, v_off, lens=None, scale=0.125, dro
         i = torch.arange(S, device=qkv.device).view(1, 1, S, 1)
         j = torch.arange(S, device=qkv.device).view(1, 1, 1, S)
         keep = attn_keep_ref(seed, bh * S + i, j, drop_p)
-        p = torch.where(keep, p / (1.0 - drop_p), torch.zeros((), device=p.device))
+        p = torch.where(keep, p * attn_drop_scale(drop_p), torch.zeros((), device=p.device))
     o = torch.einsum("bhij,bhjd->bhid", p, v)
     return o.permute(0, 2, 1, 3).reshape(B * S, H * 64)
 

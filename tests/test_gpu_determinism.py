@@ -91,10 +91,11 @@ def test_deterministic_flag_reaches_native_launchers():
 
 
 def _stage_of(name: str) -> str:
-    for key in ("stage1", "stage2", "stage3", "stage4"):
-        if key in name:
-            return key
-    return "stem" if ("conv1" in name or "bn_conv1" in name or "stem" in name) else "head"
+    """'resnet50/s3b2/c1/conv/kernel' -> 'stage3'; 'resnet50/stem/...' -> 'stem'; 'resnet50/fc/...' -> 'head'."""
+    part = name.split("/")[1] if "/" in name else name
+    if len(part) >= 2 and part[0] == "s" and part[1].isdigit():
+        return "stage" + part[1]
+    return "stem" if part == "stem" else "head"
 
 
 def test_resnet50_full_depth_gradient_direction_per_stage():

@@ -49,6 +49,31 @@ def test_attention_fwd_bwd(S, lens, drop):
     close(x.grad, xr.grad, what="attn dqkv")
 
 
+def test_attention_running_max_moves():
+    """Scores whose row maximum keeps growing along the keys (K rows scaled up with j, a spike in the
+    last tile): the forward's lazily moved running maximum must rescale O / l every time a tile
+    exceeds it by more than its threshold, and stay exact when it does not."""
+    from distributeddeeplearningspark_amd.ops import transformer as T
+
+    B, S, NH = 2, 512, 2
+    W = 3 * NH * 64
+    qkv = rnd(B * S, W, seed=5).float()
+    ramp = torch.linspace(0.25, 6.0, S, device=DEV).repeat(B)[:, None]
+    qkv[:, NH * 64 : 2 * NH * 64] *= ramp  # keys
+    qkv[:, : NH * 64] *= 3.0  # queries
+    qkv[S - 3, NH * 64 : 2 * NH * 64] = qkv[S - 3, : NH * 64] * 2.0  # a spike late in sequence 0
+    qkv = qkv.to(torch.bfloat16)
+    x = qkv.clone().requires_grad_(True)
+    o = T.attention(x, B, S, NH, drop_p=0.1, seed=5)
+    do = rnd(B * S, NH * 64, seed=6)
+    o.backward(do)
+    xr = qkv.float().requires_grad_(True)
+    orf = T.attention_ref(xr, B, S, NH, 0, NH * 64, 2 * NH * 64, None, 0.125, 0.1, 5)
+    orf.backward(do.float())
+    close(o, orf, what="attn fwd (moving max)")
+    close(x.grad, xr.grad, what="attn dqkv (moving max)")
+
+
 def test_attention_head_offsets_strided():
     """q/k/v blocks at arbitrary column offsets of a wider buffer (ld > 3*H*64)."""
     from distributeddeeplearningspark_amd.ops import transformer as T
