@@ -1201,6 +1201,11 @@ inline int wgrad_stages() {
   static const int st = stages_env("DDL_WGRAD_STAGES");
   return st;
 }
+// the same for the plain bf16-output kernels (default 1: single stage, 4 workgroups per CU)
+inline int gemm_stages() {
+  static const int st = stages_env("DDL_GEMM_STAGES");
+  return st;
+}
 // the same for the gathered fp32 kernels only (conv weight gradients, split-K small-grid forward)
 inline int gather_stages() {
   static const int st = stages_env("DDL_GATHER_STAGES");
@@ -1250,6 +1255,11 @@ inline int launch_tile(const GemmParams& p, hipStream_t s) {
     const int st = one_stage ? 1
                              : (wgrad_stages() ? wgrad_stages()
                                                : (plain ? 3 : (gather_stages() ? gather_stages() : 1)));
+    if (dm == 1 && st == 3) return launch_ring<BM, BN, AMODE, BMODE, EPI, 3, BNORM>(grid, p, s);
+    if (dm == 1 && st == 4) return launch_ring<BM, BN, AMODE, BMODE, EPI, 4, BNORM>(grid, p, s);
+  } else if constexpr (AMODE == OP_KC || AMODE == OP_RC) {
+    // DDL_GEMM_STAGES=3/4: the one-barrier LDS ring for the plain bf16-output GEMMs too (A/B)
+    const int st = one_stage ? 1 : gemm_stages();
     if (dm == 1 && st == 3) return launch_ring<BM, BN, AMODE, BMODE, EPI, 3, BNORM>(grid, p, s);
     if (dm == 1 && st == 4) return launch_ring<BM, BN, AMODE, BMODE, EPI, 4, BNORM>(grid, p, s);
   }

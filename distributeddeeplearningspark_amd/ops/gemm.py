@@ -22,8 +22,11 @@ EPI_BF16, EPI_F32, EPI_F32_ATOMIC = 0, 1, 2
 TILE256 = 4  # 256x256 ping-pong kernel (csrc/include/ddl_gemm256.h): plain KC/RC operands, K % 64 == 0
 TILE_STREAM = 5  # weight-stationary streaming kernel (csrc/kernels/gemm_stream.hip): K in {64, 128, 256}
 TILE_CONV3 = 6  # 3x3 stride-1 halo convolution (csrc/kernels/conv3x3.hip): KC_GATHER x KC, no split-K
+TILE_W4 = 7  # four-wave 256x256 kernel, 128x128 wave tiles (csrc/include/ddl_gemm_w4.h): plain KC/RC, K % 64 == 0
+TILE_W4N = 8  # four-wave 256x128 kernel, 128x64 wave tiles
 _TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), TILE256: (256, 256), TILE_STREAM: (64, 256),
-          TILE_CONV3: (224, 128)}
+          TILE_CONV3: (224, 128), TILE_W4: (256, 256), TILE_W4N: (256, 128)}
+_ONE_PER_CU = (TILE256, TILE_W4, TILE_W4N)  # kernels running one workgroup per CU
 _CU = 256
 import os as _os
 
@@ -32,6 +35,7 @@ import os as _os
 # shapes (K <= 3072 with <= 2.25 workgroup rounds), so it is opt-in (DDL_GEMM256=1) and
 # auto-selected only for GEMMs with many tiles AND a long K loop.
 _USE256 = _os.environ.get("DDL_GEMM256", "auto")
+_USE_W4 = _os.environ.get("DDL_GEMM_W4", "0")  # four-wave 256-row kernel routing (use_w4); opt-in until measured
 
 
 _USE_STREAM = _os.environ.get("DDL_GEMM_STREAM", "1")
@@ -81,6 +85,22 @@ def use_tile256(M: int, N: int, K: int, a_mode: int, b_mode: int, epi: int) -> b
     return epi == EPI_BF16 and tiles >= 4 * _CU and K >= 4096
 
 
+def use_w4(M: int, N: int, K: int, a_mode: int, b_mode: int, epi: int):
+    """Tile id of the four-wave 256-row kernel for this GEMM, or None.  DDL_GEMM_W4: 0 = off, 1 = when its
+    tiles fill whole rounds of the chip (256x256 first, then 256x128), 2 = 256x256 whenever it applies."""
+    if _USE_W4 == "0" or a_mode > RC or b_mode > RC or K % 64 or M < 256 or N < 128 or epi != EPI_BF16:
+        return None
+    t256 = math.ceil(M / 256) * math.ceil(N / 256)
+    if _USE_W4 == "2":
+        return TILE_W4 if N >= 256 else TILE_W4N
+    if N >= 256 and t256 >= _CU and (t256 % _CU == 0 or t256 >= 6 * _CU):
+        return TILE_W4
+    t128 = math.ceil(M / 256) * math.ceil(N / 128)
+    if t128 >= _CU and (t128 % _CU == 0 or t128 >= 6 * _CU):
+        return TILE_W4N
+    return None
+
+
 def choose_tile(M: int, N: int, bn_cap: int = 128) -> int:
     bn = 128 if (N > 64 and bn_cap >= 128) else 64
     bm = 128 if M > 64 else 64
@@ -101,7 +121,7 @@ def choose_split(M: int, N: int, K: int, tile: int, allow: bool, rounds: float |
         return kfull
     bm, bn = _TILES[tile]
     tiles = math.ceil(M / bm) * math.ceil(N / bn)
-    per_cu = 1 if tile == TILE256 else 2  # resident workgroups per CU
+    per_cu = 1 if tile in _ONE_PER_CU else 2  # resident workgroups per CU
     if tiles >= per_cu * _CU or K < 1024:
         return kfull
     splits = min(math.ceil((rounds or _SPLIT_ROUNDS) * per_cu * _CU / tiles), max(1, K // 512))
@@ -112,8 +132,9 @@ def choose_split(M: int, N: int, K: int, tile: int, allow: bool, rounds: float |
 def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, beta=0.0, bias=None, resid=None,
          ldr=0, relu=False, geom=None, outmap=None, b_kdiv=0, b_tap_stride=0, stats=None, tile=None, k_split=None,
          bn_cap=128, aux=None, drop_p=0.0, drop_seed=0, split_rounds=None, resid_mask=None, bnr=None, rsub=None,
-         a_norm=None, b_norm=None):
-    """Raw launcher with automatic tile / split-K choice.
+         a_norm=None, b_norm=None, slabs=None):
+    """Raw launcher with automatic tile / split-K choice.  ``slabs``: force (True) or forbid (False) the
+    partial-slab split-K path of fp32 outputs (default: deterministic mode or DDL_SPLITK_SLABS).
 
     With ``epi == EPI_F32`` and a split-K decomposition the launch switches to the
     atomic epilogue, which *accumulates* into ``c``: callers that need ``c = A@B``
@@ -124,6 +145,8 @@ def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, bet
         if use_stream(M, N, K, a_mode, b_mode, epi, lda, ldc, outmap=outmap, aux=aux, drop_p=drop_p, relu=relu,
                       beta=beta, resid=resid, ldr=ldr):
             tile = TILE_STREAM
+        elif outmap is None and bnr is None and use_w4(M, N, K, a_mode, b_mode, epi) is not None:
+            tile = use_w4(M, N, K, a_mode, b_mode, epi)
         elif outmap is None and bnr is None and use_tile256(M, N, K, a_mode, b_mode, epi):
             tile = TILE256
         else:
@@ -137,7 +160,8 @@ def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, bet
     if epi == EPI_F32 and k_split < K:
         if beta not in (0.0, 1.0):
             raise ValueError("split-K fp32 gemm supports beta in {0,1} (beta=0 needs a zeroed C)")
-        if tile in (0, 1, 2, 3, TILE256) and (_det.enabled() or _SPLITK_SLABS):
+        use_slabs = (_det.enabled() or _SPLITK_SLABS) if slabs is None else (slabs or _det.enabled())
+        if tile in (0, 1, 2, 3) + _ONE_PER_CU and use_slabs:
             # partial slabs (plain stores) + an ordered reduce: deterministic, and the slab stores run at
             # the HBM store rate where fp32 atomics run at ~1.3 TB/s (GemmParams::split_stride)
             splits = math.ceil(K / k_split)
@@ -146,8 +170,8 @@ def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, bet
         else:
             epi = EPI_F32_ATOMIC
     if bnr is not None:  # fused BN-backward reduce of the output (see linear_dgrad / GemmParams.bnr_*)
-        if tile == TILE256:
-            raise ValueError("bnr: not on the 256x256 kernel")
+        if tile in _ONE_PER_CU:
+            raise ValueError("bnr: not on the 256-row kernels")
         stats = bnr["ws"]
     C().gemm(a, b, out, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, tile, k_split, alpha, beta, bias, resid, ldr,
              int(relu), geom, outmap, b_kdiv, b_tap_stride, stats, aux, float(drop_p), int(drop_seed), resid_mask,

@@ -79,6 +79,10 @@ def main():
             variants = {"auto": None, "t128": 0}
         elif not (M >= 256 and N >= 256 and K % 64 == 0):
             variants.pop("g256")
+        if M >= 256 and N >= 128 and K % 64 == 0:  # the four-wave 256-row kernels (ddl_gemm_w4.h)
+            if N >= 256:
+                variants["w4"] = G.TILE_W4
+            variants["w4n"] = G.TILE_W4N
         def run(tile):
             if f32 and tile is None:  # the production call (tile, split-K rounds, slabs / atomics)
                 return G.linear_wgrad(a_t, b_t, out)

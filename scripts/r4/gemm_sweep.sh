@@ -11,4 +11,4 @@ import json
 for l in open('gpurun_out/r4/gemm/$tag.jsonl'):
     if l.startswith('{'):
         d=json.loads(l); print('$tag', d['shape'], {k:d[k]['tflops'] for k in d if isinstance(d[k], dict)})"; }
-run default DDL_X=0 && run dma2 DDL_GEMM_DMA=2 && run slabs DDL_SPLITK_SLABS=1 && run slabs_r2 DDL_SPLITK_SLABS=1 DDL_LINEAR_WGRAD_ROUNDS=2
+run default DDL_X=0 && run ring3 DDL_GEMM_STAGES=3 && run ring4 DDL_GEMM_STAGES=4 && run dma2 DDL_GEMM_DMA=2 && run wg_ring3 DDL_WGRAD_STAGES=3 && run slabs DDL_SPLITK_SLABS=1 && run slabs_r2 DDL_SPLITK_SLABS=1 DDL_LINEAR_WGRAD_ROUNDS=2

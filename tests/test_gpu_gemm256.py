@@ -1,10 +1,14 @@
-"""256x256 ping-pong GEMM (csrc/include/ddl_gemm256.h) against fp32 references: every
-operand layout, every epilogue, tails in M and N, split-K."""
+"""The 256-row GEMM kernels against fp32 references: the 256x256 ping-pong kernel
+(csrc/include/ddl_gemm256.h) and the four-wave 256x256 / 256x128 kernels (ddl_gemm_w4.h) — every
+operand layout, every epilogue, tails in M and N, split-K (atomics and partial slabs)."""
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
+
+
+TILES = [4, 7, 8]  # G.TILE256, G.TILE_W4, G.TILE_W4N
 
 
 def rnd(*shape, seed=0, scale=1.0):
@@ -24,7 +28,8 @@ def close(a, b, rtol=2e-2, atol=2e-2, what=""):
                                    (4096, 256, 1024)])
 @pytest.mark.parametrize("a_rc", [False, True])
 @pytest.mark.parametrize("b_rc", [False, True])
-def test_gemm256_layouts(M, N, K, a_rc, b_rc):
+@pytest.mark.parametrize("tile", TILES)
+def test_gemm256_layouts(M, N, K, a_rc, b_rc, tile):
     from distributeddeeplearningspark_amd.ops import gemm as G
 
     if (a_rc and M % 8) or (b_rc and N % 8):
@@ -35,11 +40,12 @@ def test_gemm256_layouts(M, N, K, a_rc, b_rc):
     b_t = B.T.contiguous() if b_rc else B
     out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
     G.gemm(a_t, b_t, out, M, N, K, G.RC if a_rc else G.KC, G.RC if b_rc else G.KC, a_t.stride(0), b_t.stride(0), N,
-           G.EPI_BF16, tile=G.TILE256)
-    close(out, ref, what=f"g256 {M}x{N}x{K} a_rc={a_rc} b_rc={b_rc}")
+           G.EPI_BF16, tile=tile)
+    close(out, ref, what=f"tile {tile} {M}x{N}x{K} a_rc={a_rc} b_rc={b_rc}")
 
 
-def test_gemm256_epilogues():
+@pytest.mark.parametrize("tile", TILES)
+def test_gemm256_epilogues(tile):
     from distributeddeeplearningspark_amd.ops import gemm as G
     from distributeddeeplearningspark_amd.ops import transformer as T
 
@@ -50,35 +56,39 @@ def test_gemm256_epilogues():
     pre_r = A.float() @ B.float().T + bias
     out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
     G.gemm(A, B, out, M, N, K, G.KC, G.KC, K, K, N, G.EPI_BF16, bias=bias, resid=res, ldr=N, relu=True,
-           tile=G.TILE256)
+           tile=tile)
     close(out, torch.relu(pre_r + res.float()), what="bias+resid+relu")
     aux = torch.empty_like(out)
-    G.gemm(A, B, out, M, N, K, G.KC, G.KC, K, K, N, G.EPI_BF16, bias=bias, relu=G.ACT_GELU, aux=aux, tile=G.TILE256)
+    G.gemm(A, B, out, M, N, K, G.KC, G.KC, K, K, N, G.EPI_BF16, bias=bias, relu=G.ACT_GELU, aux=aux, tile=tile)
     close(aux, pre_r, what="gelu aux")
     close(out, torch.nn.functional.gelu(pre_r), what="gelu")
     G.gemm(A, B, out, M, N, K, G.KC, G.KC, K, K, N, G.EPI_BF16, bias=bias, resid=res, ldr=N, drop_p=0.1, drop_seed=7,
-           tile=G.TILE256)
+           tile=tile)
     close(out, res.float() + T.dropout_ref(pre_r, 0.1, 7), what="dropout+resid")
     st = torch.zeros(32, 2, N, device=DEV)
-    G.gemm(A, B, out, M, N, K, G.KC, G.KC, K, K, N, G.EPI_BF16, stats=st, tile=G.TILE256)
+    G.gemm(A, B, out, M, N, K, G.KC, G.KC, K, K, N, G.EPI_BF16, stats=st, tile=tile)
     o = out.float()
     close(st.sum(0)[0], o.sum(0), rtol=1e-3, atol=1e-1, what="stats sum")
     close(st.sum(0)[1], (o * o).sum(0), rtol=1e-3, atol=1e-1, what="stats sumsq")
 
 
-def test_gemm256_fp32_and_splitk():
+@pytest.mark.parametrize("tile", TILES)
+def test_gemm256_fp32_and_splitk(tile):
     from distributeddeeplearningspark_amd.ops import gemm as G
 
     # wgrad-shaped: dW[N1,K1] += dy[T,N1]^T x[T,K1] with a long reduction (split-K, atomics)
     T_, N1, K1 = 16384, 768, 3072
     dy, x = rnd(T_, N1, seed=6), rnd(T_, K1, seed=7)
     gw = torch.full((N1, K1), 0.25, device=DEV)
-    G.gemm(dy, x, gw, N1, K1, T_, G.RC, G.RC, N1, K1, K1, G.EPI_F32, beta=1.0, tile=G.TILE256)
-    close(gw, 0.25 + dy.float().T @ x.float(), rtol=1e-3, atol=5e-2, what="g256 split-K fp32")
+    G.gemm(dy, x, gw, N1, K1, T_, G.RC, G.RC, N1, K1, K1, G.EPI_F32, beta=1.0, tile=tile)
+    close(gw, 0.25 + dy.float().T @ x.float(), rtol=1e-3, atol=5e-2, what="split-K fp32 atomics")
+    gs = torch.full((N1, K1), 0.25, device=DEV)
+    G.gemm(dy, x, gs, N1, K1, T_, G.RC, G.RC, N1, K1, K1, G.EPI_F32, beta=1.0, tile=tile, slabs=True)
+    close(gs, 0.25 + dy.float().T @ x.float(), rtol=1e-3, atol=5e-2, what="split-K fp32 slabs")
     out = torch.empty(512, 512, device=DEV)
     A, B = rnd(512, 256, seed=8), rnd(512, 256, seed=9)
-    G.gemm(A, B, out, 512, 512, 256, G.KC, G.KC, 256, 256, 512, G.EPI_F32, tile=G.TILE256)
-    close(out, A.float() @ B.float().T, rtol=1e-3, atol=1e-2, what="g256 fp32 store")
+    G.gemm(A, B, out, 512, 512, 256, G.KC, G.KC, 256, 256, 512, G.EPI_F32, tile=tile)
+    close(out, A.float() @ B.float().T, rtol=1e-3, atol=1e-2, what="fp32 store")
 
 
 def test_gemm256_auto_selected_for_bert_shapes():
@@ -87,3 +97,19 @@ def test_gemm256_auto_selected_for_bert_shapes():
     assert G.use_tile256(16384, 16384, 8192, G.KC, G.KC, G.EPI_BF16)
     assert not G.use_tile256(512, 512, 768, G.KC, G.KC, G.EPI_BF16)
     assert not G.use_tile256(16384, 3072, 100, G.KC, G.KC, G.EPI_BF16)
+
+
+def test_w4_routing():
+    from distributeddeeplearningspark_amd.ops import gemm as G
+
+    old = G._USE_W4
+    try:
+        G._USE_W4 = "1"
+        assert G.use_w4(16384, 3072, 768, G.KC, G.KC, G.EPI_BF16) == G.TILE_W4  # 768 tiles: 3 rounds
+        assert G.use_w4(16384, 2304, 768, G.KC, G.KC, G.EPI_BF16) == G.TILE_W4N  # 1152 256x128 tiles
+        assert G.use_w4(16384, 768, 768, G.KC, G.KC, G.EPI_BF16) is None  # 384 tiles: 1.5 rounds
+        assert G.use_w4(16384, 3072, 100, G.KC, G.KC, G.EPI_BF16) is None  # K % 64
+        G._USE_W4 = "0"
+        assert G.use_w4(16384, 3072, 768, G.KC, G.KC, G.EPI_BF16) is None
+    finally:
+        G._USE_W4 = old
