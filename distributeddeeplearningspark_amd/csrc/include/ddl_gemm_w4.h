@@ -9,9 +9,8 @@
 //   * per 32-deep k-step a wave reads 16 fragments (16 KB) for 64 MFMAs, half the LDS bytes per
 //     MFMA of the 64x64 wave tile, and the DMA bytes per MFMA halve with the 256-wide block;
 //   * operands go global -> LDS by LDS-DMA (global_load_lds_dwordx4, no VGPR round trip) into a
-//     ring of ST K-tile stages (BN 256: 2 x 64 KB, BN 128: 3 x 48 KB), one barrier per K-tile,
-//     loads for tile t + ST - 1 issued right after the barrier that frees their slot, so a
-//     K-tile of MFMAs (2048 / 1024 cycles per wave) covers the fetch latency;
+//     ring of K-tile stages (BN 256: 2 x 64 KB, BN 128: 3 x 48 KB) with one barrier per K-tile;
+//     a K-tile of MFMAs (2048 / 1024 cycles per wave) covers each fetch (two at BN 128);
 //   * the 128-row half-tile images, swizzles and fragment readers are the 256x256 kernel's
 //     (ddl_gemm256.h): ds_read_b128 for K-contiguous operands, ds_read_b64_tr_b16 for
 //     row-contiguous ones, conflict-free.
@@ -44,7 +43,7 @@ __device__ __forceinline__ void stage(const bf16_t* __restrict__ ptr, long ld, i
       const int k = blk * 4 + (lane >> 4);
       const int ch = (lane & 15) ^ g256::rc_sw(k);
       const int gc = min(r0 + ch * 8, rows - 8);
-      src = ptr + (long)(k0 + k) * ld + gc;
+      src = (ptr + (long)k0 * ld) + ((long)k * ld + gc);  // the second term is K-tile invariant (hoisted)
     }
     __builtin_amdgcn_global_load_lds((const void*)src, (g256::lds_t*)(slot + blk * 1024), 16, 0, 0);
   }
@@ -98,36 +97,46 @@ __global__ __launch_bounds__(w4::THREADS, 1) void gemm_w4_kernel(const GemmParam
 #pragma unroll
     for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // fragments of one 32-deep k-step: A rows 16i of the wave's A half, B columns bc + 16j
+  auto frags = [&](int st, int kk, bf16x8 (&af)[8], bf16x8 (&bfr)[RN]) {
+    const char* sa = slot(st, wr);
+    const char* sb = slot(st, bh);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) af[i] = g256::frag<AMODE>(sa, 16 * i, kk, lane);
+#pragma unroll
+    for (int j = 0; j < RN; ++j) bfr[j] = g256::frag<BMODE>(sb, bc + 16 * j, kk, lane);
+  };
+  auto mma = [&](const bf16x8 (&af)[8], const bf16x8 (&bfr)[RN]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        if constexpr (epi_dt(EPI))
+          acc[i][j] = mfma16x16x32(bfr[j], af[i], acc[i][j]);
+        else
+          acc[i][j] = mfma16x16x32(af[i], bfr[j], acc[i][j]);
+      }
+  };
+  // Ring of ST stages, one barrier per K-tile at its start: tile t has landed for this wave (tile
+  // t + 1 may stay in flight at ST = 3), the barrier publishes it to every wave and proves every wave
+  // is done with tile t - 1, whose slot is refilled with tile t + ST - 1 right away.  (Double-buffering
+  // the fragments across K-tiles makes the compiler rotate the accumulators through VGPRs every
+  // iteration — 190 extra moves per 64 MFMAs at BN 128 — so the k-steps read their fragments in place.)
 #pragma unroll
   for (int s = 0; s < ST - 1; ++s)
     if (s < nk) stage_tile(s, s);
   int cur = 0;
   for (int t = 0; t < nk; ++t) {
-    // tile t landed for this wave (tile t + 1 may stay in flight at ST = 3); the barrier publishes
-    // it to every wave and proves every wave has consumed tile t - 1, whose slot is refilled next
     if (ST >= 3 && t + 1 < nk) wait_vmcnt<PER>();
     else wait_vmcnt<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (t + ST - 1 < nk) stage_tile(t + ST - 1, cur == 0 ? ST - 1 : cur - 1);
-    const char* sa = slot(cur, wr);
-    const char* sb = slot(cur, bh);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8 af[8], bfr[RN];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) af[i] = g256::frag<AMODE>(sa, 16 * i, kk, lane);
-#pragma unroll
-      for (int j = 0; j < RN; ++j) bfr[j] = g256::frag<BMODE>(sb, bc + 16 * j, kk, lane);
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < RN; ++j) {
-          if constexpr (epi_dt(EPI))
-            acc[i][j] = mfma16x16x32(bfr[j], af[i], acc[i][j]);
-          else
-            acc[i][j] = mfma16x16x32(af[i], bfr[j], acc[i][j]);
-        }
+      frags(cur, kk, af, bfr);
+      mma(af, bfr);
     }
     cur = cur + 1 == ST ? 0 : cur + 1;
   }
