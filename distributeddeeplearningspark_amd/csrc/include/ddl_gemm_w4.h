@@ -14,8 +14,9 @@
 //   * the 128-row half-tile images, swizzles and fragment readers are the 256x256 kernel's
 //     (ddl_gemm256.h): ds_read_b128 for K-contiguous operands, ds_read_b64_tr_b16 for
 //     row-contiguous ones, conflict-free.
-// Epilogue: the shared gemm_epilogue (bias / GELU / dropout / residual / ReLU / BN statistics / fp32
-// or split-K partial slabs / atomics) on the 8 x BN/32 fragment array of each wave.
+// Epilogue: the shared gemm_epilogue on the 8 x BN/32 fragment array of each wave — the slim one (bias /
+// ReLU / BN statistics), the LDS-staged row epilogue for everything else (GELU / dropout / residual),
+// fp32 stores, split-K partial slabs or atomics.
 #pragma once
 #include "ddl_gemm256.h"
 
@@ -141,6 +142,8 @@ __global__ __launch_bounds__(w4::THREADS, 1) void gemm_w4_kernel(const GemmParam
     cur = cur + 1 == ST ? 0 : cur + 1;
   }
   if constexpr (EPI == EPI_BF16_ROW) __syncthreads();  // the ring becomes the row epilogue's staging area
+  static_assert(EPI != EPI_BF16, "w4: the full bf16 epilogue runs as EPI_BF16_ROW (on the 8 x RN array the "
+                                 "unrolled one spills ~260 dwords per lane)");
   gemm_epilogue<8, RN, EPI>(p, acc, m0 + 128 * wr, n0 + (BN / 2) * wc, lane, bid, -1,
                             reinterpret_cast<float*>(smem + wid * row_epi_bytes<RN>()), (long)split * p.split_stride);
 }

@@ -3,10 +3,8 @@
 namespace ddl {
 template <int BN, int AM, int BM>
 static int launch_epi(const GemmParams& p, int epi, hipStream_t s) {
-  if (epi == EPI_BF16)  // the slim epilogue when no residual / GELU / dropout / output map is used (code size)
-    return !needs_full_epilogue(p) ? launch_w4<BN, AM, BM, EPI_BF16_LITE>(p, s)
-                                   : (row_epilogue() ? launch_w4<BN, AM, BM, EPI_BF16_ROW>(p, s)
-                                                     : launch_w4<BN, AM, BM, EPI_BF16>(p, s));
+  if (epi == EPI_BF16)  // slim epilogue, or the LDS-staged row epilogue for residual / GELU / dropout
+    return !needs_full_epilogue(p) ? launch_w4<BN, AM, BM, EPI_BF16_LITE>(p, s) : launch_w4<BN, AM, BM, EPI_BF16_ROW>(p, s);
   if (epi == EPI_F32) return launch_w4<BN, AM, BM, EPI_F32>(p, s);
   return launch_w4<BN, AM, BM, EPI_F32_ATOMIC>(p, s);
 }
