@@ -36,6 +36,7 @@ import os as _os
 # auto-selected only for GEMMs with many tiles AND a long K loop.
 _USE256 = _os.environ.get("DDL_GEMM256", "auto")
 _USE_W4 = _os.environ.get("DDL_GEMM_W4", "0")  # four-wave 256-row kernel routing (use_w4); opt-in until measured
+_USE_W4_WGRAD = _os.environ.get("DDL_GEMM_W4_WGRAD", "0")  # ... for the fp32 weight gradients: "256" / "128"
 
 
 _USE_STREAM = _os.environ.get("DDL_GEMM_STREAM", "1")
@@ -88,7 +89,15 @@ def use_tile256(M: int, N: int, K: int, a_mode: int, b_mode: int, epi: int) -> b
 def use_w4(M: int, N: int, K: int, a_mode: int, b_mode: int, epi: int):
     """Tile id of the four-wave 256-row kernel for this GEMM, or None.  DDL_GEMM_W4: 0 = off, 1 = when its
     tiles fill whole rounds of the chip (256x256 first, then 256x128), 2 = 256x256 whenever it applies."""
-    if _USE_W4 == "0" or a_mode > RC or b_mode > RC or K % 64 or M < 256 or N < 128 or epi != EPI_BF16:
+    if a_mode > RC or b_mode > RC or K % 64 or M < 256 or N < 128:
+        return None
+    if epi == EPI_F32:  # weight gradients (split-K over the long token dimension): DDL_GEMM_W4_WGRAD=256 / 128
+        if _USE_W4_WGRAD == "256" and N >= 256 and K >= 2048:
+            return TILE_W4
+        if _USE_W4_WGRAD == "128" and K >= 2048:
+            return TILE_W4N
+        return None
+    if _USE_W4 == "0" or epi != EPI_BF16:
         return None
     t256 = math.ceil(M / 256) * math.ceil(N / 256)
     if _USE_W4 == "2":
@@ -145,7 +154,8 @@ def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, bet
         if use_stream(M, N, K, a_mode, b_mode, epi, lda, ldc, outmap=outmap, aux=aux, drop_p=drop_p, relu=relu,
                       beta=beta, resid=resid, ldr=ldr):
             tile = TILE_STREAM
-        elif outmap is None and bnr is None and use_w4(M, N, K, a_mode, b_mode, epi) is not None:
+        elif (outmap is None and bnr is None and a_norm is None and b_norm is None
+              and use_w4(M, N, K, a_mode, b_mode, epi) is not None):
             tile = use_w4(M, N, K, a_mode, b_mode, epi)
         elif outmap is None and bnr is None and use_tile256(M, N, K, a_mode, b_mode, epi):
             tile = TILE256
