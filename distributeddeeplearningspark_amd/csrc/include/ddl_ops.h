@@ -15,7 +15,8 @@ constexpr int kMaxPartials = 512;  // partial rows of a column-reduction sweep
 //   * fused conv-epilogue statistics: S = kBnShards, zeroed, accumulated with atomics;
 //   * bn_stats / bn_bwd_reduce sweeps: S = bn_partial_rows(M, C), every row written (no zeroing).
 int bn_partial_rows(long M, int C);
-int splitk_finalize(float* ws, void* y, const float* bias, float* stats, long M, int C, int relu, hipStream_t s);
+int splitk_finalize(float* ws, void* y, const float* bias, float* stats, long M, int C, int relu, int splits,
+                    long slab_stride, hipStream_t s);  // splits > 0: ws = `splits` slabs slab_stride floats apart
 int bn_stats(const void* x, float* ws, long M, int C, hipStream_t s);
 // ws -> mean/invstd (saved for backward), scale/shift for apply, running stats update
 int bn_finalize(const float* ws, int S, long M, int C, const float* gamma, const float* beta, float eps,

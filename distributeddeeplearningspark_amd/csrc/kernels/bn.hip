@@ -106,13 +106,15 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const uint4* __restrict__
 }
 
 // Split-K bf16 finalize: y = bf16(ws + bias) (ReLU) and ws = 0, plus per-column statistics of the ROUNDED
+// output (slab form, splits > 0: ws holds `splits` partial slabs `slab_stride` floats apart, summed in
+// split order and left as they are — the GEMM overwrites them next time)
 // output accumulated into the [kStatShards][2][C] workspace of the GEMM epilogue (shard =
 // block % kStatShards).  Convolutions whose output tiles cannot fill the chip (VGG / ResNet layers
 // at 2x2-4x4 spatial) run their K loop split over workgroups into an fp32 workspace; this pass
 // completes them with the epilogue the un-split GEMM would have applied.
 __global__ __launch_bounds__(256) void splitk_finalize_kernel(float4* __restrict__ ws, uint4* __restrict__ y,
                                                               const float* __restrict__ bias, float* stats, long M,
-                                                              int C, int relu) {
+                                                              int C, int relu, int splits, long slab_stride) {
   ColGeom g(C);
   float acc[16];
 #pragma unroll
@@ -126,10 +128,19 @@ __global__ __launch_bounds__(256) void splitk_finalize_kernel(float4* __restrict
     const long step = (long)gridDim.x * g.RT;
     for (long r = (long)blockIdx.x * g.RT + g.rt; r < M; r += step) {
       const long idx = r * g.CV + g.cv;
-      const float4 u = ws[2 * idx], v = ws[2 * idx + 1];
-      // leave the workspace zeroed for the next split-K accumulation (no fill launch per call)
-      ws[2 * idx] = make_float4(0.f, 0.f, 0.f, 0.f);
-      ws[2 * idx + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 u = ws[2 * idx], v = ws[2 * idx + 1];
+      if (splits > 0) {
+        const long st4 = slab_stride >> 2;
+        for (int sp = 1; sp < splits; ++sp) {
+          const float4 a = ws[sp * st4 + 2 * idx], c = ws[sp * st4 + 2 * idx + 1];
+          u.x += a.x; u.y += a.y; u.z += a.z; u.w += a.w;
+          v.x += c.x; v.y += c.y; v.z += c.z; v.w += c.w;
+        }
+      } else {
+        // leave the workspace zeroed for the next split-K accumulation (no fill launch per call)
+        ws[2 * idx] = make_float4(0.f, 0.f, 0.f, 0.f);
+        ws[2 * idx + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
       float f[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -170,13 +181,14 @@ __global__ __launch_bounds__(256) void splitk_finalize_kernel(float4* __restrict
   }
 }
 
-int splitk_finalize(float* ws, void* y, const float* bias, float* stats, long M, int C, int relu, hipStream_t s) {
+int splitk_finalize(float* ws, void* y, const float* bias, float* stats, long M, int C, int relu, int splits,
+                    long slab_stride, hipStream_t s) {
   const int CV = C >> 3, CT = CV < 256 ? CV : 256, RT = 256 / CT;
   const int gy = (CV + CT - 1) / CT;
   long gx = (M + 4 * RT - 1) / (4 * RT);  // >= 4 rows per lane
   if (gx > 1024) gx = 1024;
   hipLaunchKernelGGL(splitk_finalize_kernel, dim3((unsigned)(gx > 0 ? gx : 1), (unsigned)gy), dim3(256), 0, s,
-                     (float4*)ws, (uint4*)y, bias, stats, M, C, relu);
+                     (float4*)ws, (uint4*)y, bias, stats, M, C, relu, splits, slab_stride);
   return (int)hipGetLastError();
 }
 

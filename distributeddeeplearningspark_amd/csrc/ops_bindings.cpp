@@ -38,14 +38,17 @@ void bn_stats_(const at::Tensor& x, const at::Tensor& ws, int64_t C) {
 }
 
 void splitk_finalize_(const at::Tensor& ws, const at::Tensor& y, int64_t C, c10::optional<at::Tensor> bias, bool relu,
-                      c10::optional<at::Tensor> stats) {
+                      c10::optional<at::Tensor> stats, int64_t splits) {
   GPU(ws); F32(ws); BF16(y);
-  CK(C % 8 == 0 && ws.numel() % C == 0 && y.numel() == ws.numel() && y.is_contiguous(), "splitk_finalize: shapes");
+  CK(C % 8 == 0 && y.numel() % C == 0 && y.is_contiguous() && ws.is_contiguous(), "splitk_finalize: shapes");
+  // splits == 0: ws is the [M, C] atomic accumulator (zeroed again); splits > 0: `splits` [M, C] slabs
+  CK(splits >= 0 && ws.numel() >= std::max<int64_t>(splits, 1) * y.numel() && (splits > 0 || ws.numel() == y.numel()),
+     "splitk_finalize: workspace size");
   if (bias) { F32(*bias); CK(bias->numel() == C, "splitk_finalize: bias [C]"); }
   if (stats) { F32(*stats); CK(stats->numel() == (int64_t)kBnShards * 2 * C, "splitk_finalize: stats [32, 2, C]"); }
   at::DeviceGuard g(ws.device());
-  HIP_OK(splitk_finalize(ws.data_ptr<float>(), y.data_ptr(), optr<const float>(bias), optr<float>(stats), ws.numel() / C,
-                         (int)C, relu ? 1 : 0, cur_stream()));
+  HIP_OK(splitk_finalize(ws.data_ptr<float>(), y.data_ptr(), optr<const float>(bias), optr<float>(stats), y.numel() / C,
+                         (int)C, relu ? 1 : 0, (int)splits, (long)y.numel(), cur_stream()));
 }
 
 int64_t bn_partial_rows_(int64_t M, int64_t C) { return bn_partial_rows(M, (int)C); }
@@ -518,7 +521,8 @@ void sumsq_(const at::Tensor& x, const at::Tensor& out) {
 void register_ops(py::module& m) {
   m.attr("BN_SHARDS") = (int)kBnShards;
   m.def("bn_stats", &bn_stats_);
-  m.def("splitk_finalize", &splitk_finalize_);
+  m.def("splitk_finalize", &splitk_finalize_, py::arg("ws"), py::arg("y"), py::arg("C"), py::arg("bias"), py::arg("relu"),
+        py::arg("stats"), py::arg("splits") = 0);
   m.def("bn_partial_rows", &bn_partial_rows_);
   m.def("bn_finalize", &bn_finalize_);
   m.def("bn_apply", &bn_apply_, py::arg("x"), py::arg("scale"), py::arg("shift"), py::arg("resid"), py::arg("y"),

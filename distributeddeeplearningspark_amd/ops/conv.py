@@ -188,9 +188,12 @@ def conv_fwd_native(x, w, g: ConvGeometry, bias=None, relu=False, stats=None, x_
         K = g.T * g.Ci
         tiles = math.ceil(g.M / 64) * math.ceil(g.Co / 64)
         splits = max(2, min(math.ceil(_SPLITK_WG / tiles), K // 512))  # ~4 workgroups per CU, >= 8 K-tiles each
-        G.gemm(x, w, ws, g.M, g.Co, K, G.KC_GATHER, G.KC, 0, K, g.Co, G.EPI_F32, geom=g.fwd_geom, tile=3,
-               k_split=math.ceil(K / splits / 64) * 64)
-        C().splitk_finalize(ws, y2, g.Co, bias, bool(relu), stats)
+        r = G.gemm(x, w, ws, g.M, g.Co, K, G.KC_GATHER, G.KC, 0, K, g.Co, G.EPI_F32, geom=g.fwd_geom, tile=3,
+                   k_split=math.ceil(K / splits / 64) * 64, defer_slabs=True)
+        if isinstance(r, tuple):  # partial slabs (DDL_SPLITK_SLABS): summed by the finalize itself
+            C().splitk_finalize(r[0], y2, g.Co, bias, bool(relu), stats, r[1])
+        else:
+            C().splitk_finalize(ws, y2, g.Co, bias, bool(relu), stats)
         return y
     fb = (bnr is not None and bias is None and not relu and stats is None and g.Co % 8 == 0
           and bnr["x"].is_contiguous() and not g.is_pointwise and (halo3_ok(g) or g.implicit_fwd))

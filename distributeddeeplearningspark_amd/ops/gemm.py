@@ -141,9 +141,11 @@ def choose_split(M: int, N: int, K: int, tile: int, allow: bool, rounds: float |
 def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, beta=0.0, bias=None, resid=None,
          ldr=0, relu=False, geom=None, outmap=None, b_kdiv=0, b_tap_stride=0, stats=None, tile=None, k_split=None,
          bn_cap=128, aux=None, drop_p=0.0, drop_seed=0, split_rounds=None, resid_mask=None, bnr=None, rsub=None,
-         a_norm=None, b_norm=None, slabs=None):
+         a_norm=None, b_norm=None, slabs=None, defer_slabs=False):
     """Raw launcher with automatic tile / split-K choice.  ``slabs``: force (True) or forbid (False) the
-    partial-slab split-K path of fp32 outputs (default: deterministic mode or DDL_SPLITK_SLABS).
+    partial-slab split-K path of fp32 outputs (default: deterministic mode or DDL_SPLITK_SLABS);
+    ``defer_slabs``: when that path is taken, skip the reduce and return ``(slabs, splits)`` for a
+    consumer that sums them itself (``splitk_finalize``).
 
     With ``epi == EPI_F32`` and a split-K decomposition the launch switches to the
     atomic epilogue, which *accumulates* into ``c``: callers that need ``c = A@B``
@@ -190,6 +192,8 @@ def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, bet
              *(b_norm or (None, None)), None if bnr is None else bnr.get("scale"),
              None if bnr is None else bnr.get("shift"), split_stride)
     if split_stride:
+        if defer_slabs:
+            return out, math.ceil(K / k_split)
         C().slab_reduce(out, math.ceil(K / k_split), c, M, N, ldc_c, float(slab_beta))
     return c
 
@@ -283,9 +287,12 @@ def linear_dgrad(dy, w, out=None, resid=None, gelu_pre=None, stats=None, resid_m
         # workgroups into an fp32 workspace, then round (+ statistics) in one finalize pass
         ws = splitk_workspace(M, K, dy.device)
         splits = max(2, min(math.ceil(2048 / tiles), N // 512))
-        gemm(dy, w, ws, M, K, N, KC, RC, dy.stride(0), w.stride(0), K, EPI_F32, tile=3,
-             k_split=math.ceil(N / splits / 64) * 64)
-        C().splitk_finalize(ws, out, K, None, False, stats)
+        r = gemm(dy, w, ws, M, K, N, KC, RC, dy.stride(0), w.stride(0), K, EPI_F32, tile=3,
+                 k_split=math.ceil(N / splits / 64) * 64, defer_slabs=True)
+        if isinstance(r, tuple):  # partial slabs (DDL_SPLITK_SLABS): summed by the finalize itself
+            C().splitk_finalize(r[0], out, K, None, False, stats, r[1])
+        else:
+            C().splitk_finalize(ws, out, K, None, False, stats)
         return out
     if M >= _WT_MIN_M and not use_stream(M, K, N, KC, RC, EPI_BF16, dy.stride(0), out.stride(0), aux=gelu_pre,
                                           relu=act, resid=resid, ldr=ldr):

@@ -163,12 +163,15 @@ def test_dgrad_masked_residual(M, N, K):
     close(out, ref, what=f"masked residual dgrad {M}x{N}x{K}")
 
 
+@pytest.mark.parametrize("slabs", [False, True])
 @pytest.mark.parametrize("M", [300, 2458])
-def test_linear_dgrad_splitk(M):
+def test_linear_dgrad_splitk(M, slabs, monkeypatch):
     """Long-reduction data-gradient on few output tiles (BERT's MLM decoder: masked tokens x 768
-    over the vocabulary) runs split-K into the fp32 workspace: values, statistics, and the
-    workspace left zeroed for the next call (two calls, same shape)."""
+    over the vocabulary) runs split-K into the fp32 workspace (or partial slabs summed by the
+    finalize): values, statistics, and the workspace left zeroed for the next call (two calls)."""
     from distributeddeeplearningspark_amd.ops import gemm as G
+
+    monkeypatch.setattr(G, "_SPLITK_SLABS", slabs)
 
     V, H = 8200, 768
     for seed in (50, 52):
@@ -182,11 +185,16 @@ def test_linear_dgrad_splitk(M):
     assert G.splitk_workspace(M, H, dy.device).abs().max().item() == 0.0
 
 
+@pytest.mark.parametrize("slabs", [False, True])
 @pytest.mark.parametrize("relu", [False, True])
-def test_conv_splitk_forward_stats(relu):
+def test_conv_splitk_forward_stats(relu, slabs, monkeypatch):
     """Split-K forward of a small-grid conv: bias, ReLU and the fused per-channel statistics of the
-    rounded bf16 output ([32, 2, C] sharded sums, as the GEMM epilogue writes them)."""
+    rounded bf16 output ([32, 2, C] sharded sums, as the GEMM epilogue writes them); with partial
+    slabs the finalize sums them itself."""
     from distributeddeeplearningspark_amd.ops import conv as CV
+    from distributeddeeplearningspark_amd.ops import gemm as G
+
+    monkeypatch.setattr(G, "_SPLITK_SLABS", slabs)
 
     N, H, Ci, Co = 16, 4, 512, 256
     g = CV.geometry(N, H, H, Ci, Co, 3, 3, (1, 1), (1, 1), (1, 1))
