@@ -8,8 +8,4 @@ bash scripts/r4/attn.sh; rc=$?; echo "[batch1] attn.sh rc=$rc"; fatal $rc attn
 bash scripts/r4/w4.sh; rc=$?; echo "[batch1] w4.sh rc=$rc"; fatal $rc w4
 DDL_GEMM_W4=1 timeout -k 10 300 python bench.py --model bert --steps 10 --warmup 3 > gpurun_out/r4/bench_bert_w4.json 2> gpurun_out/r4/bench_bert_w4.err
 rc=$?; echo "[batch1] bert w4 rc=$rc"; cat gpurun_out/r4/bench_bert_w4.json; fatal $rc bert_w4
-DDL_GEMM_W4=1 timeout -k 10 300 python bench.py --steps 10 --warmup 3 > gpurun_out/r4/bench_rn50_w4.json 2> gpurun_out/r4/bench_rn50_w4.err
-rc=$?; echo "[batch1] rn50 w4 rc=$rc"; cat gpurun_out/r4/bench_rn50_w4.json; fatal $rc rn50_w4
-timeout -k 10 300 python bench.py --steps 10 --warmup 3 > gpurun_out/r4/bench_rn50.json 2> gpurun_out/r4/bench_rn50.err
-rc=$?; echo "[batch1] rn50 rc=$rc"; cat gpurun_out/r4/bench_rn50.json
 exit 0
