@@ -122,8 +122,8 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
   }
   TORCH_CHECK(drop_p >= 0.0 && drop_p < 1.0, "gemm: dropout p in [0, 1)");
   if (drop_p > 0.0) {
-    p.drop_thresh = (uint32_t)std::min(4294967295.0, drop_p * 4294967296.0);
-    p.drop_scale = (float)(1.0 / (1.0 - drop_p));
+    p.drop_thresh = drop_t8(drop_p);  // threshold byte: the rate quantised to 1/256 (ddl_ops.h)
+    p.drop_scale = drop_scale8(p.drop_thresh);
     p.drop_seed = (unsigned long long)drop_seed;
   }
   p.ldr = ldr;

@@ -42,25 +42,53 @@ __device__ __forceinline__ float warp_max(float v) {
   return v;
 }
 
-// Counter-based dropout: element `idx` of a call with seed `seed` is kept iff
-// hash(seed + idx) >= thresh (thresh = p * 2^32).  Stateless, so backward passes
-// regenerate the mask instead of storing it.
-// Counter hash of the dropout masks (x = seed + element index): the 64-bit counter is folded to
-// 32 bits (high word times the golden-ratio constant) and mixed by a 32-bit finaliser (xor-shift /
-// multiply, 'lowbias32').  Three 32-bit multiplies instead of the two 64-bit ones (~4 v_mul each)
-// of murmur's fmix64, which made the dropout-carrying LayerNorm / GEMM epilogues VALU-heavy.
+// Counter-based dropout with uint8 thresholds: element `idx` of a call with seed `seed` is kept iff
+// byte (idx & 3) of drop_hash4(seed + idx / 4) >= t8, and the kept values are scaled by 256 / (256 - t8)
+// (the rate is quantised to 1/256: drop_t8 in ddl_ops.h).  Stateless, so backward passes regenerate
+// the mask instead of storing it.  One hash serves four consecutive elements: the 64-bit counter is
+// folded with a 24-bit multiply, premixed by one 32-bit multiply and finished with 24-bit multiplies
+// (v_mul_u32_u24, full rate) — the previous per-element hash spent three quarter-rate v_mul_lo_u32
+// on every element of the dropout-carrying LayerNorm / GEMM epilogues.
 // Mirrored bit for bit by ops/transformer.py:drop_hash_ref.
-__device__ __forceinline__ uint32_t drop_hash(uint64_t x) {
-  uint32_t h = (uint32_t)x ^ ((uint32_t)(x >> 32) * 0x9E3779B9u);
-  h ^= h >> 16;
-  h *= 0x7FEB352Du;
-  h ^= h >> 15;
-  h *= 0x846CA68Bu;
-  h ^= h >> 16;
-  return h;
+__device__ __forceinline__ uint32_t drop_hash4(uint64_t q) {
+  uint32_t x = ((uint32_t)q ^ __umul24((uint32_t)(q >> 32), 0x9E3779u)) * 0x9E3779B1u;
+  x ^= x >> 16;
+  x = __umul24(x, 0x7feb35u);
+  x ^= x >> 15;
+  x = __umul24(x, 0x846ca7u);
+  return x ^ (x >> 16);
 }
-__device__ __forceinline__ bool drop_keep(uint64_t seed, uint64_t idx, uint32_t thresh) {
-  return drop_hash(seed + idx) >= thresh;
+__device__ __forceinline__ bool drop_byte_keep(uint32_t h, uint32_t j, uint32_t t8) {
+  return ((h >> (8u * (j & 3u))) & 0xffu) >= t8;
+}
+__device__ __forceinline__ bool drop_keep(uint64_t seed, uint64_t idx, uint32_t t8) {
+  return drop_byte_keep(drop_hash4(seed + (idx >> 2)), (uint32_t)idx, t8);
+}
+// keep bits (bit e) of the 4 / 8 consecutive elements base, base + 1, ...: 1 / 2 hashes when base is
+// 4-aligned, one more otherwise
+__device__ __forceinline__ uint32_t drop_bits4(uint64_t seed, uint64_t base, uint32_t t8) {
+  const uint64_t q = seed + (base >> 2);
+  const uint32_t off = (uint32_t)base & 3u;
+  const uint32_t h0 = drop_hash4(q), h1 = off ? drop_hash4(q + 1) : 0u;
+  uint32_t bits = 0u;
+#pragma unroll
+  for (uint32_t e = 0; e < 4; ++e) {
+    const uint32_t j = off + e;
+    bits |= (drop_byte_keep(j < 4 ? h0 : h1, j, t8) ? 1u : 0u) << e;
+  }
+  return bits;
+}
+__device__ __forceinline__ uint32_t drop_bits8(uint64_t seed, uint64_t base, uint32_t t8) {
+  const uint64_t q = seed + (base >> 2);
+  const uint32_t off = (uint32_t)base & 3u;
+  const uint32_t h0 = drop_hash4(q), h1 = drop_hash4(q + 1), h2 = off ? drop_hash4(q + 2) : 0u;
+  uint32_t bits = 0u;
+#pragma unroll
+  for (uint32_t e = 0; e < 8; ++e) {
+    const uint32_t j = off + e;
+    bits |= (drop_byte_keep(j < 4 ? h0 : (j < 8 ? h1 : h2), j, t8) ? 1u : 0u) << e;
+  }
+  return bits;
 }
 
 // erf-form GELU and its derivative (BERT "gelu"; not the tanh approximation)

@@ -94,7 +94,8 @@ struct GemmParams {
   float* stats;
   void* aux;          // bf16 [M][ldc]: pre-activation (ACT_GELU out / ACT_GELU_BWD in)
   // dropout applied after bias/activation and before the residual add:
-  // keep element (m, n) iff drop_hash(drop_seed + m*N + n) >= drop_thresh, kept values * drop_scale
+  // keep element (m, n) iff drop_keep(drop_seed, m*N + n, drop_thresh) (ddl_common.h: drop_thresh is the
+  // threshold byte t8), kept values * drop_scale
   uint32_t drop_thresh;
   float drop_scale;
   unsigned long long drop_seed;

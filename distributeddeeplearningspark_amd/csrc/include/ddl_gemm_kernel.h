@@ -567,8 +567,9 @@ __device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, f32x4 (&
         }
         if (p.drop_thresh) {
           const unsigned long long base = (unsigned long long)m * (unsigned long long)p.N + (unsigned long long)n;
+          const uint32_t kb = drop_bits8(p.drop_seed, base, p.drop_thresh);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = drop_keep(p.drop_seed, base + e, p.drop_thresh) ? v[e] * p.drop_scale : 0.f;
+          for (int e = 0; e < 8; ++e) v[e] = ((kb >> e) & 1u) ? v[e] * p.drop_scale : 0.f;
         }
         if (p.resid) {
           long rrow = m;
@@ -786,9 +787,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
         }
         if (!LITE && p.drop_thresh) {
           const unsigned long long base = (unsigned long long)m * (unsigned long long)p.N + (unsigned long long)n;
+          const uint32_t kb = drop_bits4(p.drop_seed, base, p.drop_thresh);
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            v[e] = drop_keep(p.drop_seed, base + e, p.drop_thresh) ? v[e] * p.drop_scale : 0.f;
+          for (int e = 0; e < 4; ++e) v[e] = ((kb >> e) & 1u) ? v[e] * p.drop_scale : 0.f;
         }
         long rrow = m;  // residual row of output row m (stride-2 subgrid: -1 = nothing to add)
         if (!LITE && p.resid && p.rsub_h) {

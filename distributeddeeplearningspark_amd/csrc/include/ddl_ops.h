@@ -7,6 +7,16 @@
 
 namespace ddl {
 
+// Dropout rate -> threshold byte (the rate is quantised to 1/256, as uint8-threshold dropout does: p = 0.1
+// keeps 230 / 256) and the scale of the kept values, the inverse of the quantised keep rate
+// (ddl_common.h:drop_keep, ops/transformer.py:drop_thresh / drop_scale).
+inline uint32_t drop_t8(double p) {
+  if (!(p > 0.0)) return 0u;
+  const double t = p * 256.0 + 0.5;
+  return t < 1.0 ? 1u : (t >= 255.0 ? 255u : (uint32_t)t);
+}
+inline float drop_scale8(uint32_t t8) { return t8 ? (float)(256.0 / (256.0 - (double)t8)) : 1.f; }
+
 constexpr int kBnShards = 32;     // == kStatShards: sharded atomic sums of the fused GEMM-epilogue statistics
 constexpr int kMaxPartials = 512;  // partial rows of a column-reduction sweep
 
@@ -177,7 +187,7 @@ int act_bwd(const void* dy, const void* ref, void* dx, long n, int code, int bf1
 // softmax over the last axis of [R][N]; dx = y * (dy - <dy, y>)
 int softmax_rows_fwd(const void* x, void* y, long R, int N, int bf16, hipStream_t s);
 int softmax_rows_bwd(const void* dy, const void* y, void* dx, long R, int N, int bf16, hipStream_t s);
-// y = keep(i) ? x * scale : 0 with keep(i) = drop_hash(seed + i) >= thresh (also the backward)
+// y = keep(i) ? x * scale : 0 with keep(i) = drop_keep(seed, i, thresh), thresh = drop_t8(p) (also the backward)
 int dropout_apply(const void* x, void* y, long n, unsigned long long seed, uint32_t thresh, float scale, int bf16,
                   hipStream_t s);
 // NHWC average pooling, padding excluded from the divisor

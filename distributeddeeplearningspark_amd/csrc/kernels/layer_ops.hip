@@ -6,7 +6,7 @@
 // Activation codes (ddl_ops.h ActCode): derivatives are taken from the forward OUTPUT y
 // (tanh 1-y^2, sigmoid y(1-y), hard_sigmoid 0.2 on (0,1), relu y>0, elu y+1 below 0,
 // selu, softplus 1-e^-y), except GELU which needs its input x.
-// Dropout keeps element i iff drop_hash(seed + i) >= thresh (ddl_common.h): the backward
+// Dropout keeps element i iff drop_keep(seed, i, t8) (ddl_common.h): the backward
 // regenerates the mask instead of storing it.
 #include "ddl_common.h"
 #include "ddl_act.h"

@@ -107,11 +107,11 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
       if (c < nv) {
         float o[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          o[e] = (v[u][e] - mu) * rs * gm[u][e] + bt[u][e];
-          if (thresh)  // output dropout (BERT embeddings), element index row*H + n
-            o[e] = drop_keep(seed, (unsigned long long)row * (unsigned long long)H + c * 8 + e, thresh) ? o[e] * dscale
-                                                                                                     : 0.f;
+        for (int e = 0; e < 8; ++e) o[e] = (v[u][e] - mu) * rs * gm[u][e] + bt[u][e];
+        if (thresh) {  // output dropout (BERT embeddings), element index row*H + n
+          const uint32_t kb = drop_bits8(seed, (unsigned long long)row * (unsigned long long)H + c * 8, thresh);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = ((kb >> e) & 1u) ? o[e] * dscale : 0.f;
         }
         *reinterpret_cast<uint4*>(y + row * H + c * 8) = pack8f(o);
       }
@@ -191,8 +191,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
         unpack8(PF ? cx[u] : *reinterpret_cast<const uint4*>(x + row * H + c * 8), xv);
         if (in_thresh) {  // dy arrives through the forward's output dropout
           const unsigned long long base = (unsigned long long)row * (unsigned long long)H + c * 8;
+          const uint32_t kb = drop_bits8(in_seed, base, in_thresh);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) d[e] = drop_keep(in_seed, base + e, in_thresh) ? d[e] * in_scale : 0.f;
+          for (int e = 0; e < 8; ++e) d[e] = ((kb >> e) & 1u) ? d[e] * in_scale : 0.f;
         }
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -223,8 +224,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
         *reinterpret_cast<uint4*>(dx + row * H + c * 8) = packed;
         if (dxd) {
           const unsigned long long base = (unsigned long long)row * (unsigned long long)H + c * 8;
+          const uint32_t kb = drop_bits8(seed, base, thresh);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) o[e] = drop_keep(seed, base + e, thresh) ? o[e] * dscale : 0.f;
+          for (int e = 0; e < 8; ++e) o[e] = ((kb >> e) & 1u) ? o[e] * dscale : 0.f;
           packed = pack8f(o);
           *reinterpret_cast<uint4*>(dxd + row * H + c * 8) = packed;
         }
@@ -493,8 +495,8 @@ static bool ln_prefetch() {
 int layernorm_fwd(const void* x, const float* gamma, const float* beta, void* y, float* mean, float* rstd, long M,
                   int H, float eps, float drop_p, unsigned long long seed, hipStream_t s) {
   if (M <= 0) return 0;
-  const uint32_t th = drop_p > 0.f ? (uint32_t)std::min(4294967295.0, (double)drop_p * 4294967296.0) : 0u;
-  const float ds = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  const uint32_t th = drop_t8(drop_p);
+  const float ds = drop_scale8(th);
   const int nv = H / 8;
   const bool PF = ln_prefetch();
   // grid-stride: gamma / beta loaded once per wave (DDL_LN_FWD_BLOCKS: experiment knob, read once)
@@ -531,13 +533,13 @@ int layernorm_bwd(const void* dy, const void* x, const float* mean, const float*
                   void* dx_drop, float drop_p, unsigned long long seed, float* ws, int P, long M, int H,
                   float in_drop_p, unsigned long long in_seed, int parts, hipStream_t s) {
   if (M <= 0) return 0;
-  const uint32_t ith = in_drop_p > 0.f ? (uint32_t)std::min(4294967295.0, (double)in_drop_p * 4294967296.0) : 0u;
-  const float iscale = in_drop_p > 0.f ? 1.f / (1.f - in_drop_p) : 1.f;
+  const uint32_t ith = drop_t8(in_drop_p);
+  const float iscale = drop_scale8(ith);
   const int nv = H / 8;
   const bool PF = ln_prefetch();
   const dim3 grid((unsigned)(P / 4));
-  const uint32_t thresh = drop_p > 0.f ? (uint32_t)std::min(4294967295.0, (double)drop_p * 4294967296.0) : 0u;
-  const float dscale = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  const uint32_t thresh = drop_t8(drop_p);
+  const float dscale = drop_scale8(thresh);
   auto DY = reinterpret_cast<const bf16_t*>(dy);
   auto X = reinterpret_cast<const bf16_t*>(x);
   auto DX = reinterpret_cast<bf16_t*>(dx);

@@ -74,10 +74,10 @@ void dropout_(const at::Tensor& x, const at::Tensor& y, double p, int64_t seed) 
   float_kind(y, "dropout y");
   same(x, y, "dropout");
   CK(p >= 0.0 && p < 1.0, "dropout: rate must be in [0, 1)");
-  const uint32_t thresh = (uint32_t)std::min(p * 4294967296.0, 4294967295.0);
+  const uint32_t thresh = drop_t8(p);  // rate quantised to 1/256 (ddl_ops.h)
   at::DeviceGuard g(x.device());
-  HIP_OK(dropout_apply(x.data_ptr(), y.data_ptr(), x.numel(), (unsigned long long)seed, thresh,
-                       (float)(1.0 / (1.0 - p)), bf, cur_stream()));
+  HIP_OK(dropout_apply(x.data_ptr(), y.data_ptr(), x.numel(), (unsigned long long)seed, thresh, drop_scale8(thresh),
+                       bf, cur_stream()));
 }
 
 void avgpool2d_fwd_(const at::Tensor& x, const at::Tensor& y, int64_t kh, int64_t kw, int64_t sh, int64_t sw,

@@ -70,8 +70,8 @@ AttnParams make_params(const at::Tensor& qkv, int64_t B, int64_t S, int64_t H, i
   p.scale_log2 = (float)(scale * 1.4426950408889634);
   // attention dropout rate quantised to 1/256 (ops/transformer.py attn_drop_t8); the kept
   // probabilities are scaled by the inverse of the quantised keep rate
-  p.drop_t8 = drop_p > 0 ? (uint32_t)std::min(255.0, std::max(1.0, std::nearbyint(drop_p * 256.0))) : 0u;
-  p.drop_scale = p.drop_t8 ? (float)(256.0 / (256.0 - p.drop_t8)) : 1.f;
+  p.drop_t8 = drop_t8(drop_p);
+  p.drop_scale = drop_scale8(p.drop_t8);
   p.drop_seed = (unsigned long long)seed;
   return p;
 }

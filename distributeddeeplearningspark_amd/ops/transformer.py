@@ -17,22 +17,33 @@ from ._native import C, use_native
 from ._ref import accumulate, ref_grads
 
 def drop_hash_ref(seed: int, idx: torch.Tensor) -> torch.Tensor:
-    """``drop_hash`` of ddl_common.h on int64 tensors (returns the 32-bit hash as int64)."""
+    """The dropout byte of element ``idx`` (ddl_common.h ``drop_keep``): byte ``idx % 4`` of
+    ``drop_hash4(seed + idx // 4)``, on int64 tensors (values 0..255)."""
     s = seed & 0xFFFFFFFFFFFFFFFF
     if s >= 1 << 63:
         s -= 1 << 64
-    x = idx.to(torch.int64) + s  # wraps mod 2^64 like the device's uint64 add
+    idx = idx.to(torch.int64)
+    q = (idx >> 2) + s  # wraps mod 2^64 like the device's uint64 add
     m = 0xFFFFFFFF
-    h = (x & m) ^ ((((x >> 32) & m) * 0x9E3779B9) & m)
-    h = h ^ (h >> 16)
-    h = (h * 0x7FEB352D) & m
-    h = h ^ (h >> 15)
-    h = (h * 0x846CA68B) & m
-    return h ^ (h >> 16)
+    x = (q & m) ^ ((((q >> 32) & 0xFFFFFF) * 0x9E3779) & m)
+    x = (x * 0x9E3779B1) & m  # (int64 products wrap; the low 32 bits are exact)
+    x = x ^ (x >> 16)
+    x = ((x & 0xFFFFFF) * 0x7FEB35) & m
+    x = x ^ (x >> 15)
+    x = ((x & 0xFFFFFF) * 0x846CA7) & m
+    x = x ^ (x >> 16)
+    return (x >> (8 * (idx & 3))) & 0xFF
 
 
 def drop_thresh(p: float) -> int:
-    return min(0xFFFFFFFF, int(p * 4294967296.0)) if p > 0 else 0
+    """Threshold byte of a dropout rate: the rate is quantised to 1/256 (ddl_ops.h ``drop_t8``)."""
+    return min(255, max(1, math.floor(p * 256.0 + 0.5))) if p > 0 else 0
+
+
+def drop_scale(p: float) -> float:
+    """Scale of the kept values: the inverse of the quantised keep rate (ddl_ops.h ``drop_scale8``)."""
+    t8 = drop_thresh(p)
+    return 256.0 / (256.0 - t8) if t8 else 1.0
 
 
 def keep_mask_ref(seed: int, idx: torch.Tensor, p: float) -> torch.Tensor:
@@ -44,7 +55,7 @@ def dropout_ref(x: torch.Tensor, p: float, seed: int) -> torch.Tensor:
     if p <= 0:
         return x
     idx = torch.arange(x.numel(), device=x.device).view(x.shape)
-    return torch.where(keep_mask_ref(seed, idx, p), x / (1.0 - p), torch.zeros((), dtype=x.dtype, device=x.device))
+    return torch.where(keep_mask_ref(seed, idx, p), x * drop_scale(p), torch.zeros((), dtype=x.dtype, device=x.device))
 
 
 # ============================================================================ attention
@@ -71,14 +82,13 @@ def hash24_ref(x: torch.Tensor) -> torch.Tensor:
 
 
 def attn_drop_t8(p: float) -> int:
-    """Attention dropout threshold byte: the rate is quantised to t8 / 256 (p = 0.1 -> 26 / 256)."""
-    return min(255, max(1, int(round(p * 256.0)))) if p > 0 else 0
+    """Attention dropout threshold byte (the same quantisation as every dropout here: drop_thresh)."""
+    return drop_thresh(p)
 
 
 def attn_drop_scale(p: float) -> float:
     """Scale of the kept attention probabilities: the inverse of the quantised keep rate."""
-    t8 = attn_drop_t8(p)
-    return 256.0 / (256.0 - t8) if t8 else 1.0
+    return drop_scale(p)
 
 
 def attn_keep_ref(seed: int, row: torch.Tensor, j: torch.Tensor, p: float) -> torch.Tensor:

@@ -17,9 +17,33 @@ def test_dropout_hash_mask_statistics_and_determinism():
     assert torch.equal(k1, k2)
     assert abs(k1.float().mean().item() - 0.9) < 0.005
     assert (k1 != k3).float().mean().item() > 0.1  # different seed, different mask
-    # the low 32 bits behave uniformly
-    u = T.drop_hash_ref(7, idx).double() / 2**32
-    assert abs(u.mean().item() - 0.5) < 0.01
+    # the dropout bytes behave uniformly
+    u = T.drop_hash_ref(7, idx).double() / 256
+    assert abs(u.mean().item() - 255 / 512) < 0.01
+    assert T.drop_thresh(0.1) == 26 and T.drop_thresh(0.25) == 64 and T.drop_scale(0.25) == 256 / 192
+
+
+def _drop_byte_py(seed: int, idx: int) -> int:
+    """Plain-integer transcription of ddl_common.h drop_keep's byte (uint64 / uint32 wraparound)."""
+    M32 = 0xFFFFFFFF
+    q = (seed + (idx >> 2)) & 0xFFFFFFFFFFFFFFFF
+    x = ((q & M32) ^ (((q >> 32) & 0xFFFFFF) * 0x9E3779 & M32)) * 0x9E3779B1 & M32
+    x ^= x >> 16
+    x = (x & 0xFFFFFF) * 0x7FEB35 & M32
+    x ^= x >> 15
+    x = (x & 0xFFFFFF) * 0x846CA7 & M32
+    x ^= x >> 16
+    return (x >> (8 * (idx & 3))) & 0xFF
+
+
+def test_dropout_hash_ref_matches_integer_transcription():
+    """The int64-tensor reference (signed wraparound) equals the unsigned integer definition, for seeds
+    that overflow int64 and element indices past 2^32."""
+    rng = np.random.default_rng(5)
+    for seed in (0, 7, 2**40 + 3, 2**63 + 12345, 2**64 - 5):
+        idx = [int(v) for v in rng.integers(0, 2**34, size=64)] + [0, 1, 2, 3, 4, 5]
+        got = T.drop_hash_ref(seed, torch.tensor(idx, dtype=torch.int64)).tolist()
+        assert got == [_drop_byte_py(seed, i) for i in idx], seed
 
 
 def test_attention_ref_matches_sdpa():
