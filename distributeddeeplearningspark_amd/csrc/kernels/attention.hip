@@ -654,7 +654,7 @@ int attn_fwd(const AttnParams& p_in, hipStream_t s) {
   p.xcd_remap = attn_xcd();
   const dim3 grid(p.S / BLOCK_ROWS, p.H, p.B);
   const bool drop = p.drop_t8 != 0;
-  static const int occ = getenv("DDL_ATTN_FWD_OCC") ? atoi(getenv("DDL_ATTN_FWD_OCC")) : 3;
+  static const int occ = getenv("DDL_ATTN_FWD_OCC") ? atoi(getenv("DDL_ATTN_FWD_OCC")) : 2;
   if (occ == 2) DDL_ATTN_LAUNCH(attn_fwd_kernel, grid, 2, drop, s, p);
   else if (occ == 4) DDL_ATTN_LAUNCH(attn_fwd_kernel, grid, 4, drop, s, p);
   else DDL_ATTN_LAUNCH(attn_fwd_kernel, grid, 3, drop, s, p);

@@ -161,6 +161,8 @@ def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, bet
             tile = use_w4(M, N, K, a_mode, b_mode, epi)
         elif outmap is None and bnr is None and use_tile256(M, N, K, a_mode, b_mode, epi):
             tile = TILE256
+        elif epi == EPI_F32 and a_mode <= RC and b_mode <= RC and big_wgrad(M, N, K) and _SPLITK_SLABS_MODE != "0":
+            tile = 0  # 128x128 + split-K slabs (see _SPLITK_SLABS_MODE)
         else:
             tile = choose_tile(M, N, bn_cap)
     if k_split is None:
@@ -172,7 +174,8 @@ def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, bet
     if epi == EPI_F32 and k_split < K:
         if beta not in (0.0, 1.0):
             raise ValueError("split-K fp32 gemm supports beta in {0,1} (beta=0 needs a zeroed C)")
-        use_slabs = (_det.enabled() or _SPLITK_SLABS) if slabs is None else (slabs or _det.enabled())
+        auto = _SPLITK_SLABS_MODE == "auto" and tile == 0 and big_wgrad(M, N, K) and math.ceil(K / k_split) <= 16
+        use_slabs = (_det.enabled() or _SPLITK_SLABS or auto) if slabs is None else (slabs or _det.enabled())
         if tile in (0, 1, 2, 3) + _ONE_PER_CU and use_slabs:
             # partial slabs (plain stores) + an ordered reduce: deterministic, and the slab stores run at
             # the HBM store rate where fp32 atomics run at ~1.3 TB/s (GemmParams::split_stride)
@@ -198,8 +201,19 @@ def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, bet
     return c
 
 
-# DDL_SPLITK_SLABS=1: fp32 split-K GEMMs (weight gradients) through partial slabs instead of fp32 atomics
-_SPLITK_SLABS = _os.environ.get("DDL_SPLITK_SLABS", "0") == "1"
+# DDL_SPLITK_SLABS=1: fp32 split-K GEMMs (weight gradients) through partial slabs instead of fp32 atomics;
+# "auto" (default): slabs for the large-output long-reduction weight gradients (big_wgrad), atomics for the
+# rest — measured (profiles/r4/gemm_sweep.txt): BERT-base weight gradients on 128x128 tiles 536-649 TF/s
+# with atomics, 638-724 with slabs; ResNet-50 1x1 weight gradients (hundreds of splits of a small output,
+# where the slab reduce has too little parallelism) 283 / 570 with atomics, 166 / 532 with slabs
+_SPLITK_SLABS_MODE = _os.environ.get("DDL_SPLITK_SLABS", "auto")
+_SPLITK_SLABS = _SPLITK_SLABS_MODE == "1"
+
+
+def big_wgrad(M: int, N: int, K: int) -> bool:
+    """An fp32 GEMM with more than 2^20 outputs over a long reduction (BERT's QKV / FFN weight gradients):
+    128x128 tiles split over K into partial slabs beat smaller tiles with fp32 atomics."""
+    return M * N > (1 << 20) and K >= 8192 and M >= 512 and N >= 512
 _SLAB_WS: dict = {}
 
 
