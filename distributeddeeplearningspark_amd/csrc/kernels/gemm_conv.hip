@@ -4,6 +4,8 @@ namespace ddl {
 int launch_gemm_conv(const GemmParams& p, int epi, int tile, hipStream_t s) {
   if (p.a_mode == OP_KC_GATHER && p.b_mode == OP_KC && epi == EPI_F32_ATOMIC)  // split-K small-grid forward
     return launch_modes<OP_KC_GATHER, OP_KC, EPI_F32_ATOMIC>(p, tile, s);
+  if (p.a_mode == OP_KC_GATHER && p.b_mode == OP_KC && epi == EPI_F32)  // ... into partial slabs
+    return launch_modes<OP_KC_GATHER, OP_KC, EPI_F32>(p, tile, s);
   if (p.a_mode == OP_KC_GATHER && p.b_mode == OP_KC && p.bnr_x)  // stride-1 dgrad as a forward conv + BN reduce
     return launch_modes<OP_KC_GATHER, OP_KC, EPI_BF16_BNR>(p, tile, s);
   if (p.a_mode == OP_KC_GATHER && p.b_mode == OP_KC)

@@ -361,8 +361,11 @@ def linear_wgrad(dy, x2, gw, x_norm=None):
         raise ValueError("linear_wgrad: normalise-on-load needs M % 64 == 0")
     # measured on the ResNet-50 1x1 weight gradients: one workgroup round (half the fp32 atomics
     # of two rounds) is 5-15 % faster — these GEMMs are bound by the split-K atomics, not MFMA
+    # (the large BERT weight gradients, on 128x128 tiles with partial slabs, take two rounds: 8 splits
+    # measured 642-739 TF/s vs 629-689 at one round, profiles/r4/wgrad_slabs_ab.txt)
+    rounds = None if (x_norm is None and big_wgrad(N, K, M) and _SPLITK_SLABS_MODE == "auto") else _LINEAR_WGRAD_ROUNDS
     return gemm(dy, x2, gw, N, K, M, RC, RC, dy.stride(0), x2.stride(0), gw.stride(0), EPI_F32, beta=1.0,
-                split_rounds=_LINEAR_WGRAD_ROUNDS, b_norm=x_norm)
+                split_rounds=rounds, b_norm=x_norm)
 
 
 def matmul(a, b, trans_a=False, trans_b=False, out=None, alpha=1.0):

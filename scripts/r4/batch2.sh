@@ -5,6 +5,8 @@ cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out/r4
 export TMPDIR=/tmp
 fatal() { case $1 in 124|134|137|139) echo "[batch2] fatal rc=$1 in $2"; exit $1;; esac; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -q -k "splitk or slabs" --timeout 120 --timeout-method thread > gpurun_out/r4/b2_splitk.log 2>&1
+rc=$?; tail -2 gpurun_out/r4/b2_splitk.log; fatal $rc splitk
 timeout -k 10 900 python -u -m pytest tests/test_gpu_determinism.py tests/test_gpu_colocated.py tests/test_gpu_convergence.py \
   -v -s --timeout 400 --timeout-method thread > gpurun_out/r4/b2_tests.log 2>&1
 rc=$?; grep -E "PASS|FAIL|ERROR|cosine|passed|failed|MAPE|accuracy" gpurun_out/r4/b2_tests.log | tail -40; fatal $rc tests
