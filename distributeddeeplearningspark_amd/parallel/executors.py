@@ -205,7 +205,7 @@ class ExecutorPool:
         self.closed = False
         self._ready = False
         self.tasks_run = 0
-        threads = max(1, (os.cpu_count() or 2) // self.world)
+        threads = max(1, cpu_budget() // self.world)
         pg_port = free_port()
         env = dict(os.environ)
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -343,6 +343,20 @@ class ExecutorPool:
             self._listener.close()
         except Exception:
             pass
+
+
+def cpu_budget() -> int:
+    """CPUs this process may use: the affinity mask, capped by OMP_NUM_THREADS when that is set (a batch
+    slot's CPU share shows up there, while os.cpu_count() and the affinity can report the whole host:
+    sizing per-executor torch threads from those oversubscribed a 16-CPU share 12x)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 2
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
 
 
 def pool_key(devices, backend):
