@@ -69,7 +69,7 @@ def test_mnist_8_colocated_workers_accuracy(monkeypatch, capsys):
     trainer, _ = ddl_mnist.main()
     out = capsys.readouterr().out
     assert trainer.parameter_server.num_updates == 3744  # 8 x floor(5 x floor(7500 / 16) / 5)
-    acc = float(out.strip().splitlines()[-2].split(": ")[1])
+    acc = float(next(line for line in out.splitlines() if line.startswith("Accuracy: ")).split(": ")[1])
     print("MNIST 8 co-located workers: accuracy", acc, "training time", trainer.get_training_time())
     assert acc >= 0.95, acc
     assert all(r.get("replica_group") for r in trainer._results)
