@@ -102,7 +102,9 @@ def test_resnet50_learns_synthetic_task_like_torch_path(monkeypatch):
             monkeypatch.delenv("DDL_BACKEND", raising=False)
         torch.manual_seed(0)
         m = ResNet50(input_shape=(64, 64, 3), num_classes=10)
-        m.compile(SGD(lr=0.05, momentum=0.9), "sparse_categorical_crossentropy")
+        # lr 0.05 diverged on both paths (loss 17-33 in the first windows, round 4); at 0.01 the fp32 CPU
+        # path reads loss windows 4.0 / 0.11 / 0.11 / 0.00 and held-out accuracy 1.0
+        m.compile(SGD(lr=0.01, momentum=0.9), "sparse_categorical_crossentropy")
         m.place(DEV, seed=1)
         g = torch.Generator().manual_seed(2)
         losses = []
