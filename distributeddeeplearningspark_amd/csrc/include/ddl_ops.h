@@ -76,7 +76,10 @@ int cast_bf16_f32(const void* x, float* y, long n, hipStream_t s);
 int sum_rows_bf16(const void* x, void* y, int R, long n, hipStream_t s);
 int relu_bwd(const void* dy, const void* y, void* dx, long n, hipStream_t s);
 int add_bf16(const void* a, const void* b, void* y, long n, hipStream_t s);
-int bias_grad(const void* dy, float* db, long M, int N, int accumulate, hipStream_t s);  // db[n] (+)= sum_m dy[m][n]
+// db[n] (+)= sum_m dy[m][n]; deterministic mode: det_ws (bias_grad_rows(M) x N floats) holds per-workgroup
+// partial rows summed in order by colsum_partials (without it: one workgroup per column block)
+int bias_grad(const void* dy, float* db, long M, int N, int accumulate, hipStream_t s, float* det_ws = nullptr);
+int bias_grad_rows(long M);
 // c = beta * c + sum over split-K partial slabs ws[splits][M][N] (split order, one writer per element)
 int slab_reduce(const float* ws, int splits, float* c, long M, int N, long ldc, float beta, hipStream_t s);
 // y[C][R] = x[R][C]^T (bf16; R, C, ldx multiples of 8)
@@ -234,7 +237,8 @@ int deterministic();
 // word-embedding gradient, deterministic: tokens sorted by id (stable), ONE writer per run of equal ids
 // (the wave whose chunk holds the run's first position walks the whole run in order)
 int embed_word_grad_det(const int64_t* sorted_ids, const int64_t* perm, const void* ds, float* gword, long T, int H,
-                        long V, hipStream_t s);
+                        long V, float* part, hipStream_t s);  // part: embed_word_grad_det_ws(T, H) floats
+long embed_word_grad_det_ws(long T, int H);
 
 // in-process replica groups (replica.hip): one commit kernel over R replicas' arenas, and the device-side
 // mini-batch fetch / loss record of a graph-replayed replica step

@@ -289,6 +289,25 @@ __global__ __launch_bounds__(1024) void colsum_kernel(const float* __restrict__ 
   }
 }
 
+// deterministic mode: 16 columns x 64 row-lanes per workgroup (4x the workgroups of colsum_kernel's
+// one-chunk form, a quarter of the serial loop), rows summed in a fixed order, one writer per column
+__global__ __launch_bounds__(1024) void colsum_det_kernel(const float* __restrict__ ws, int P, int N, long ld,
+                                                          float* __restrict__ out) {
+  __shared__ float red[64][17];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int n = blockIdx.x * 16 + tx;
+  float s = 0.f;
+  if (n < N)
+    for (int p = ty; p < P; p += 64) s += ws[(long)p * ld + n];
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && n < N) {
+    float t = 0.f;
+    for (int r = 0; r < 64; ++r) t += red[r][tx];
+    out[n] += t;
+  }
+}
+
 __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restrict__ ids,
                                                         const int64_t* __restrict__ types,
                                                         const bf16_t* __restrict__ word, const bf16_t* __restrict__ pos,
@@ -406,37 +425,90 @@ __global__ __launch_bounds__(256) void embed_word_grad_kernel(const int64_t* __r
   }
 }
 
-// Deterministic word-embedding gradient (DDL_DETERMINISTIC=1): tokens sorted by id with a STABLE sort, so
-// the rows of one id are in token order; the wave whose 32-position chunk holds a run's FIRST position
-// sums the whole run (possibly crossing into later chunks) in order and is its only writer — no atomics,
-// the same bits on every run.  A frequent id ([MASK]) makes its wave walk a long run: this mode trades
-// speed for reproducibility.
+// Deterministic word-embedding gradient over the (stable) sorted ids, two passes with a fixed partition:
+// pass 1 — one wave per 64-position chunk of the sorted array sums each same-id segment of its chunk in
+// position order; a run that starts and ends inside the chunk is written to gword by that wave (its
+// only writer), a run crossing a chunk boundary leaves its segment sums in `part` (the chunk's first
+// segment when it continues a run, its last segment when it starts one);
+// pass 2 — the wave of the chunk where a crossing run starts adds its segments chunk by chunk, in order,
+// and writes the row once.  No atomics, the same bits on every run, and a frequent id ([MASK]: 15 % of
+// the tokens) costs its owner one row add per chunk instead of a serial walk over all its tokens.
+constexpr int kDetChunk = 64;
+__device__ __forceinline__ void emb_seg_sum(const int64_t* perm, const bf16_t* ds, int H, long j0, long j1, int c,
+                                            float (&acc)[8]) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  for (long j = j0; j < j1; ++j) {
+    float d[8];
+    unpack8(*reinterpret_cast<const uint4*>(ds + perm[j] * H + c), d);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += d[e];
+  }
+}
+
 __global__ __launch_bounds__(256) void embed_word_grad_det_kernel(const int64_t* __restrict__ sorted_ids,
                                                                  const int64_t* __restrict__ perm,
                                                                  const bf16_t* __restrict__ ds,
-                                                                 float* __restrict__ gword, long T, int H, long V) {
-  const long c0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * kEmbChunk;
+                                                                 float* __restrict__ gword, float* __restrict__ part,
+                                                                 long T, int H, long V) {
+  const long ch = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const long c0 = ch * kDetChunk;
   const int lane = threadIdx.x & 63;
   if (c0 >= T) return;
-  const long c1 = min(T, c0 + kEmbChunk);
-  for (long j0 = c0; j0 < c1; ++j0) {
+  const long c1 = min(T, c0 + kDetChunk);
+  float* first = part + (2 * ch) * (long)H;  // segment continuing a run from the previous chunk
+  float* last = first + H;                   // segment starting a run that continues into the next chunk
+  long j0 = c0;
+  while (j0 < c1) {
     const int64_t id = sorted_ids[j0];
-    if (j0 > 0 && sorted_ids[j0 - 1] == id) continue;  // not a run start: another wave (or an earlier j0) owns it
-    if ((uint64_t)id >= (uint64_t)V) continue;          // out-of-vocabulary ids add nothing (never a wild write)
     long j1 = j0 + 1;
-    while (j1 < T && sorted_ids[j1] == id) ++j1;
-    for (int c = lane * 8; c < H; c += 512) {
-      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      for (long j = j0; j < j1; ++j) {
-        float d[8];
-        unpack8(*reinterpret_cast<const uint4*>(ds + perm[j] * H + c), d);
+    while (j1 < c1 && sorted_ids[j1] == id) ++j1;
+    const bool starts = j0 == 0 || sorted_ids[j0 - 1] != id;
+    const bool ends = j1 == T || sorted_ids[j1] != id;
+    if ((uint64_t)id < (uint64_t)V) {
+      for (int c = lane * 8; c < H; c += 512) {
+        float acc[8];
+        emb_seg_sum(perm, ds, H, j0, j1, c, acc);
+        float* dst = starts && ends ? gword + id * H + c : (starts ? last + c : first + c);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e] += d[e];
+        for (int e = 0; e < 8; ++e) dst[e] = starts && ends ? dst[e] + acc[e] : acc[e];
       }
-      float* g = gword + id * H + c;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) g[e] += acc[e];
     }
+    j0 = j1;
+  }
+}
+
+__global__ __launch_bounds__(256) void embed_word_grad_det_join_kernel(const int64_t* __restrict__ sorted_ids,
+                                                                      float* __restrict__ gword,
+                                                                      const float* __restrict__ part, long T, int H,
+                                                                      long V) {
+  const long ch = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const long c0 = ch * kDetChunk;
+  const int lane = threadIdx.x & 63;
+  if (c0 >= T) return;
+  const long e = min(T, c0 + kDetChunk) - 1;  // the chunk's last position
+  const int64_t id = sorted_ids[e];
+  if (e + 1 >= T || sorted_ids[e + 1] != id) return;  // its last run ends inside the chunk
+  long s = e;
+  while (s > c0 && sorted_ids[s - 1] == id) --s;
+  if (s == c0 && c0 > 0 && sorted_ids[c0 - 1] == id) return;  // the run started in an earlier chunk
+  if ((uint64_t)id >= (uint64_t)V) return;
+  const long nch = (T + kDetChunk - 1) / kDetChunk;
+  for (int c = lane * 8; c < H; c += 512) {
+    float acc[8];
+    const float* l = part + (2 * ch + 1) * (long)H + c;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = l[k];
+    for (long q = ch + 1; q < nch; ++q) {  // the continuing segments, chunk by chunk
+      const float* f = part + (2 * q) * (long)H + c;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += f[k];
+      const long qe = min(T, (q + 1) * kDetChunk);
+      if (qe >= T || sorted_ids[qe] != id) break;  // the run ends in chunk q
+    }
+    float* g = gword + id * H + c;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g[k] += acc[k];
   }
 }
 
@@ -557,8 +629,12 @@ int colsum_partials(const float* ws, int P, int N, float* out, int accumulate, h
     const hipError_t e = hipMemsetAsync(out, 0, sizeof(float) * (size_t)N, s);
     if (e != hipSuccess) return (int)e;
   }
-  // deterministic mode: one row chunk -> one writer per column, partial rows summed in a fixed order
-  const int chunk = deterministic() ? (P > 0 ? P : 1) : kColsumRows;
+  // deterministic mode: one writer per column, partial rows summed in a fixed order
+  if (deterministic()) {
+    hipLaunchKernelGGL(colsum_det_kernel, dim3((N + 15) / 16), dim3(1024), 0, s, ws, P, N, ld > 0 ? ld : (long)N, out);
+    return (int)hipGetLastError();
+  }
+  const int chunk = kColsumRows;
   hipLaunchKernelGGL(colsum_kernel, dim3((N + 63) / 64, (P + chunk - 1) / chunk), dim3(64, 16), 0, s, ws, P, N,
                      ld > 0 ? ld : (long)N, out, chunk);
   return (int)hipGetLastError();
@@ -584,14 +660,17 @@ int embed_word_grad(const int64_t* sorted_ids, const int64_t* perm, const void* 
 }
 
 int embed_word_grad_det(const int64_t* sorted_ids, const int64_t* perm, const void* ds, float* gword, long T, int H,
-                        long V, hipStream_t s) {
+                        long V, float* part, hipStream_t s) {
   if (T <= 0) return 0;
   if (H % 8) return (int)hipErrorInvalidValue;
-  const long waves = (T + kEmbChunk - 1) / kEmbChunk;
+  const long waves = (T + kDetChunk - 1) / kDetChunk;
   hipLaunchKernelGGL(embed_word_grad_det_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, sorted_ids, perm,
-                     reinterpret_cast<const bf16_t*>(ds), gword, T, H, V);
+                     reinterpret_cast<const bf16_t*>(ds), gword, part, T, H, V);
+  hipLaunchKernelGGL(embed_word_grad_det_join_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, sorted_ids,
+                     gword, part, T, H, V);
   return (int)hipGetLastError();
 }
+long embed_word_grad_det_ws(long T, int H) { return 2 * ((T + kDetChunk - 1) / kDetChunk) * (long)H; }
 
 int embed_word_grad_atomic(const int64_t* ids, const void* ds, float* gword, long T, int H, long V, hipStream_t s) {
   if (T <= 0) return 0;

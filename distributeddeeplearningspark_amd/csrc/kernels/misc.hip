@@ -127,7 +127,9 @@ __global__ void bias_grad_kernel(const bf16_t* dy, float* db, long M, int N) {
 // Vector form for N % 8 == 0 and 16-byte aligned rows: a block covers 256 columns as 32 lanes of
 // 8 bf16 (one 16-byte load each) x 8 row-lanes, reduces the row-lanes through LDS and issues one
 // atomic per column per block.  The scalar form above moved 2 bytes per lane per load.
-__global__ __launch_bounds__(256) void bias_grad_vec_kernel(const bf16_t* dy, float* db, long M, int N) {
+// pout != nullptr (deterministic mode): each workgroup stores its column totals to pout[blockIdx.y][n]
+// instead of adding them into db; colsum_partials then sums the rows in index order, one writer per column
+__global__ __launch_bounds__(256) void bias_grad_vec_kernel(const bf16_t* dy, float* db, long M, int N, float* pout) {
   __shared__ float part[8][257];
   const int cg = threadIdx.x & 31, rl = threadIdx.x >> 5;
   const int n0 = blockIdx.x * 256 + cg * 8;
@@ -153,7 +155,8 @@ __global__ __launch_bounds__(256) void bias_grad_vec_kernel(const bf16_t* dy, fl
     float t = 0.f;
 #pragma unroll
     for (int r = 0; r < 8; ++r) t += part[r][c];
-    atomicAdd(db + n, t);
+    if (pout) pout[(long)blockIdx.y * N + n] = t;
+    else atomicAdd(db + n, t);
   }
 }
 
@@ -201,15 +204,29 @@ int slab_reduce(const float* ws, int splits, float* c, long M, int N, long ldc, 
   return (int)hipGetLastError();
 }
 
-int bias_grad(const void* dy, float* db, long M, int N, int accumulate, hipStream_t s) {
-  if (!accumulate) hipMemsetAsync(db, 0, sizeof(float) * N, s);
+int bias_grad_rows(long M) {
   long ys = M / 64;
   if (ys < 1) ys = 1;
   if (ys > 256) ys = 256;
-  if (deterministic()) ys = 1;  // one workgroup per column block: a single writer per column
-  if (N % 8 == 0 && (reinterpret_cast<uintptr_t>(dy) & 15) == 0) {
+  return (int)ys;
+}
+
+int bias_grad(const void* dy, float* db, long M, int N, int accumulate, hipStream_t s, float* det_ws) {
+  if (!accumulate) hipMemsetAsync(db, 0, sizeof(float) * N, s);
+  long ys = bias_grad_rows(M);
+  const bool vec = N % 8 == 0 && (reinterpret_cast<uintptr_t>(dy) & 15) == 0;
+  if (deterministic()) {
+    if (vec && det_ws) {  // per-workgroup partial rows, then an in-order column sum (one writer per column)
+      hipLaunchKernelGGL(bias_grad_vec_kernel, dim3((N + 255) / 256, (unsigned)ys), dim3(256), 0, s,
+                         (const bf16_t*)dy, db, M, N, det_ws);
+      const int e = (int)hipGetLastError();
+      return e ? e : colsum_partials(det_ws, (int)ys, N, db, 1, s);
+    }
+    ys = 1;  // no workspace: one workgroup per column block, a single writer per column
+  }
+  if (vec) {
     hipLaunchKernelGGL(bias_grad_vec_kernel, dim3((N + 255) / 256, (unsigned)ys), dim3(256), 0, s,
-                       (const bf16_t*)dy, db, M, N);
+                       (const bf16_t*)dy, db, M, N, (float*)nullptr);
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(bias_grad_kernel, dim3((N + 255) / 256, (unsigned)ys), dim3(256), 0, s, (const bf16_t*)dy, db, M,

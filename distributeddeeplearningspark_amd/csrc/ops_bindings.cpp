@@ -284,7 +284,11 @@ void bias_grad_(const at::Tensor& dy, const at::Tensor& db, int64_t N, bool accu
   // the kernels read dy as a dense [M][N] array (row stride N, 16-B vectors): no strided views
   CK(dy.is_contiguous() && db.is_contiguous(), "bias_grad: dy and db must be contiguous");
   at::DeviceGuard g(dy.device());
-  HIP_OK(bias_grad(dy.data_ptr(), db.data_ptr<float>(), dy.numel() / N, (int)N, accumulate ? 1 : 0, cur_stream()));
+  const long M = dy.numel() / N;
+  at::Tensor ws;  // deterministic mode: partial rows from the caching allocator (stream-ordered)
+  if (deterministic()) ws = at::empty({(int64_t)bias_grad_rows(M) * N}, dy.options().dtype(at::kFloat));
+  HIP_OK(bias_grad(dy.data_ptr(), db.data_ptr<float>(), M, (int)N, accumulate ? 1 : 0, cur_stream(),
+                   ws.defined() ? ws.data_ptr<float>() : nullptr));
 }
 void im2col_(const at::Tensor& x, const at::Tensor& col, int64_t ho, int64_t wo, int64_t sh, int64_t sw,
              std::vector<int> dh, std::vector<int> dw, int64_t kpad) {

@@ -160,8 +160,9 @@ void embed_word_grad_det_(const at::Tensor& sorted_ids, const at::Tensor& perm, 
   CK(perm.numel() == T && ds.numel() == T * H && gword.dim() == 2 && gword.size(1) == H && H % 8 == 0,
      "embed_word_grad_det: sorted_ids / perm [T], ds [T, H], gword [V, H]");
   at::DeviceGuard g(ds.device());
+  at::Tensor part = at::empty({embed_word_grad_det_ws(T, (int)H)}, ds.options().dtype(at::kFloat));
   HIP_OK(embed_word_grad_det(sorted_ids.data_ptr<int64_t>(), perm.data_ptr<int64_t>(), ds.data_ptr(),
-                             gword.data_ptr<float>(), T, (int)H, gword.size(0), cur_stream()));
+                             gword.data_ptr<float>(), T, (int)H, gword.size(0), part.data_ptr<float>(), cur_stream()));
 }
 
 void embed_word_grad_atomic_(const at::Tensor& ids, const at::Tensor& ds, const at::Tensor& gword) {

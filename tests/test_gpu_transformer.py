@@ -293,6 +293,34 @@ def test_embed_word_grad_sorted_runs_and_pos_grad():
     close(gp, ds.float().view(B, S, H).sum(0), rtol=1e-3, atol=1e-3, what="pos grad")
 
 
+@pytest.mark.parametrize("T", [1000, 4096, 64, 65])
+def test_embed_word_grad_deterministic(T):
+    """Deterministic (two-pass, fixed-partition) word gradient against index_add: a hot id whose run
+    crosses many 64-position chunks, runs ending exactly at chunk edges, out-of-vocabulary ids (skipped),
+    and bit-identical results on a repeat."""
+    from distributeddeeplearningspark_amd.ops._native import C
+
+    V, H = 300, 768
+    g = torch.Generator().manual_seed(T)
+    ids = torch.randint(0, V, (T,), generator=g)
+    ids[torch.rand(T, generator=g) < 0.3] = 103
+    ids[: min(T, 64)] = 7 if T >= 128 else ids[: min(T, 64)]  # a run filling exactly the first chunk
+    if T > 10:
+        ids[3] = V + 5  # out of vocabulary
+    ids = ids.to(DEV)
+    ds = rnd(T, H, seed=22)
+    srt = torch.sort(ids, stable=True)
+    outs = []
+    for _ in range(2):
+        gw = torch.full((V, H), 0.25, device=DEV)
+        C().embed_word_grad_det(srt.values, srt.indices, ds, gw)
+        outs.append(gw)
+    ok = ids < V
+    ref = torch.full((V, H), 0.25, device=DEV).index_add_(0, ids[ok], ds.float()[ok])
+    close(outs[0], ref, rtol=1e-3, atol=1e-3, what="deterministic word grad")
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("R,Cc", [(768, 3072), (3072, 768), (200, 96), (8, 8)])
 def test_transpose_bf16_kernel(R, Cc):
     from distributeddeeplearningspark_amd.ops import gemm as G
@@ -315,12 +343,25 @@ def test_linear_dgrad_transposed_weight_path():
     close(dx, dy.float() @ w.float(), what="dgrad KCxKC")
 
 
+@pytest.mark.parametrize("det", [False, True])
 @pytest.mark.parametrize("M,N,off", [(16384, 768, 0), (4096, 3072, 0), (333, 2304, 0), (257, 100, 0), (64, 768, 3)])
-def test_bias_grad_vector_and_scalar_paths(M, N, off):
+def test_bias_grad_vector_and_scalar_paths(M, N, off, det):
     """Column sums of a bf16 [M, N] gradient (vector kernel for N % 8 == 0 on 16-byte aligned rows,
-    scalar kernel otherwise) accumulated into fp32, vs an fp32 PyTorch reference."""
+    scalar kernel otherwise) accumulated into fp32, vs an fp32 PyTorch reference; in deterministic mode
+    (per-workgroup partial rows + an in-order column sum) also bit-identical on a repeat."""
     from distributeddeeplearningspark_amd.ops._native import C
+    from distributeddeeplearningspark_amd.ops.determinism import deterministic
 
+    if det:
+        with deterministic(True):
+            flat = rnd(M * N + off, seed=5)
+            dy = flat[off:].view(M, N)
+            a, b = torch.zeros(N, device=DEV), torch.zeros(N, device=DEV)
+            C().bias_grad(dy, a, N, False)
+            C().bias_grad(dy, b, N, False)
+            close(a, dy.float().sum(0), rtol=1e-4, atol=1e-2, what="bias_grad det")
+            assert torch.equal(a, b)
+        return
     flat = rnd(M * N + off, seed=5)
     dy = flat[off:].view(M, N)
     db = torch.randn(N, device=DEV)
