@@ -825,7 +825,20 @@ __global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(const float4* __
   if (i >= n4) return;
   const int s0 = blockIdx.y * per_group, s1 = min(slabs, s0 + per_group);
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int s = s0; s < s1; ++s) {
+  int s = s0;
+  for (; s + 3 < s1; s += 4) {  // four slab loads in flight; adds in slab order (same bits)
+    float4 v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = ws[(long)(s + q) * n4 + i];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      acc.x += v[q].x;
+      acc.y += v[q].y;
+      acc.z += v[q].z;
+      acc.w += v[q].w;
+    }
+  }
+  for (; s < s1; ++s) {
     const float4 v = ws[(long)s * n4 + i];
     acc.x += v.x;
     acc.y += v.y;
