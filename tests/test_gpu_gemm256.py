@@ -108,7 +108,7 @@ def test_w4_routing():
         assert G.use_w4(16384, 3072, 768, G.KC, G.KC, G.EPI_BF16) == G.TILE_W4  # 768 tiles: 3 rounds
         assert G.use_w4(16384, 2304, 768, G.KC, G.KC, G.EPI_BF16) is None  # 576 / 1152 tiles: partial rounds
         assert G.use_w4(65536, 768, 768, G.KC, G.KC, G.EPI_BF16) == G.TILE_W4  # 768 256x256 tiles: 3 rounds
-        assert G.use_w4(65536, 384, 768, G.KC, G.KC, G.EPI_BF16) == G.TILE_W4N  # 768 256x128 tiles
+        assert G.use_w4(65536, 128, 768, G.KC, G.KC, G.EPI_BF16) == G.TILE_W4N  # 256 256x128 tiles: one round
         assert G.use_w4(16384, 768, 768, G.KC, G.KC, G.EPI_BF16) is None  # 384 tiles: 1.5 rounds
         assert G.use_w4(16384, 3072, 100, G.KC, G.KC, G.EPI_BF16) is None  # K % 64
         G._USE_W4 = "0"
