@@ -26,8 +26,13 @@ constexpr int NTHREADS = 256;
 #ifndef DDL_WGRAD_MIN_BLOCKS
 #define DDL_WGRAD_MIN_BLOCKS 2
 #endif
+#ifndef DDL_DMA_BF16_MIN_BLOCKS
+#define DDL_DMA_BF16_MIN_BLOCKS 4  // resident workgroups per CU the bf16-output kernels' registers are capped for
+#endif
 template <int EPI>
-constexpr int dma_min_blocks() { return (EPI == EPI_F32 || EPI == EPI_F32_ATOMIC) ? DDL_WGRAD_MIN_BLOCKS : 4; }
+constexpr int dma_min_blocks() {
+  return (EPI == EPI_F32 || EPI == EPI_F32_ATOMIC) ? DDL_WGRAD_MIN_BLOCKS : DDL_DMA_BF16_MIN_BLOCKS;
+}
 
 // Simple, exact division helper (used where the divisor is a power of two or tiny loops are fine)
 __device__ __forceinline__ void pix_decompose(uint32_t p, uint32_t ho, uint32_t wo, int& n, int& i, int& j) {
