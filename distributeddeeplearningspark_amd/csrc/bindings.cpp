@@ -74,7 +74,7 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
   if (b_mode == OP_RC || b_mode == OP_RC_TAPS) TORCH_CHECK(ldb % 8 == 0, "gemm: ldb must be a multiple of 8");
   TORCH_CHECK(((uintptr_t)a.data_ptr() % 16) == 0 && ((uintptr_t)b.data_ptr() % 16) == 0, "gemm: operands must be 16-B aligned");
   TORCH_CHECK(k_split > 0 && k_split % 64 == 0, "gemm: k_split must be a positive multiple of 64");
-  TORCH_CHECK(tile >= 0 && tile <= kTileW4N, "gemm: bad tile id");
+  TORCH_CHECK(tile >= 0 && tile <= kTile256P, "gemm: bad tile id");
   if (tile == kTileStream) {
     TORCH_CHECK(a_mode == OP_KC && (b_mode == OP_KC || b_mode == OP_RC) && epi == EPI_BF16 && !outmap.has_value() &&
                     relu <= ACT_RELU && drop_p == 0.0 && beta == 0.0 && k_split >= K,
@@ -83,7 +83,7 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
     TORCH_CHECK(ldc % 8 == 0 && ((uintptr_t)c.data_ptr() % 16) == 0, "gemm stream: 16-B aligned output rows");
     TORCH_CHECK(!resid || (ldr % 4 == 0 && ((uintptr_t)resid->data_ptr() % 8) == 0), "gemm stream: resid alignment");
   }
-  if (tile == kTile256 || tile == kTileW4 || tile == kTileW4N) {
+  if (tile == kTile256 || tile == kTile256P || tile == kTileW4 || tile == kTileW4N) {
     TORCH_CHECK(a_mode <= OP_RC && b_mode <= OP_RC && !outmap.has_value(), "gemm256: plain KC/RC operands only");
     TORCH_CHECK(K % 64 == 0 && k_split % 64 == 0, "gemm256: K and k_split must be multiples of 64");
     TORCH_CHECK(M >= 8 && N >= 8, "gemm256: M, N >= 8");
@@ -189,7 +189,7 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
     p.stats = stats->data_ptr<float>();
   }
   if (bnr_x) {
-    TORCH_CHECK(stats.has_value() && bnr_mean.has_value() && epi == EPI_BF16 && tile != kTile256 && tile != kTileW4 && tile != kTileW4N,
+    TORCH_CHECK(stats.has_value() && bnr_mean.has_value() && epi == EPI_BF16 && tile != kTile256 && tile != kTile256P && tile != kTileW4 && tile != kTileW4N,
                 "gemm: the fused BN-backward reduction needs a stats workspace, the mean and a bf16 epilogue");
     TORCH_CHECK(tile == kTileStream || (N % 4 == 0 && ldc % 8 == 0 && !bias && relu == 0 && !resid && !outmap && !aux &&
                                         drop_p == 0.0 && (a_mode == OP_KC || (a_mode == OP_KC_GATHER && b_mode == OP_KC))),

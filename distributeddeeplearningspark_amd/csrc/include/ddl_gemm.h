@@ -144,6 +144,7 @@ constexpr int kTileStream = 5;  // tile id of the weight-stationary streaming ke
 constexpr int kTileConv3 = 6;   // tile id of the 3x3 stride-1 halo convolution kernel (conv3x3.hip)
 constexpr int kTileW4 = 7;      // four-wave 256x256 kernel, 128x128 per wave (ddl_gemm_w4.h)
 constexpr int kTileW4N = 8;     // four-wave 256x128 kernel, 128x64 per wave
+constexpr int kTile256P = 9;    // the 256x256 ping-pong kernel in its persistent form (one workgroup per CU)
 
 // the halo kernel applies to this (KC_GATHER x KC, 3x3 / stride 1 / pad 1) GEMM
 bool conv3x3_halo_ok(const GemmParams& p);

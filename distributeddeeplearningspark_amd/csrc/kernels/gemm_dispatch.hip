@@ -6,7 +6,7 @@ namespace ddl {
 int launch_gemm_plain_akc(const GemmParams& p, int epi, int tile, hipStream_t s);
 int launch_gemm_plain_arc(const GemmParams& p, int epi, int tile, hipStream_t s);
 int launch_gemm_conv(const GemmParams& p, int epi, int tile, hipStream_t s);
-int launch_gemm256(const GemmParams& p, int epi, hipStream_t s);
+int launch_gemm256(const GemmParams& p, int epi, hipStream_t s, bool persist);
 int launch_gemm_w4(const GemmParams& p, int epi, int tile, hipStream_t s);
 int launch_gemm_stream(const GemmParams& p, int epi, hipStream_t s);
 int launch_conv3x3(const GemmParams& p, int epi, hipStream_t s);
@@ -24,7 +24,7 @@ int launch_gemm_bf16(const GemmParams& p_in, int epi, int tile, void* stream) {
   GemmParams p = p_in;
   p.group_m = group_m;
   if (p.bnr_x && tile != kTileStream &&  // fused BN-backward reduce on the other kernels: EPI_BF16_BNR
-      (tile == kTile256 || tile == kTileW4 || tile == kTileW4N || epi != EPI_BF16 || p.om.enabled || p.resid || p.aux || p.drop_thresh || p.bias || p.relu || p.N % 4 || p.ldc % 8 ||
+      (tile == kTile256 || tile == kTile256P || tile == kTileW4 || tile == kTileW4N || epi != EPI_BF16 || p.om.enabled || p.resid || p.aux || p.drop_thresh || p.bias || p.relu || p.N % 4 || p.ldc % 8 ||
        !(p.a_mode == OP_KC || p.a_mode == OP_KC_GATHER) || (p.a_mode == OP_KC_GATHER && p.b_mode != OP_KC)))
     return (int)hipErrorInvalidValue;
   if (p.bnr_scale && tile == kTileStream) return (int)hipErrorInvalidValue;  // streaming kernel: mask bits only
@@ -33,9 +33,9 @@ int launch_gemm_bf16(const GemmParams& p_in, int epi, int tile, void* stream) {
                      tile <= 3 && p.K % 64 == 0 && p.k_split % 64 == 0))
     return (int)hipErrorInvalidValue;  // normalise-on-load of B: plain RC x RC weight gradients, whole K-tiles
   const bool plain = (p.a_mode == OP_KC || p.a_mode == OP_RC) && (p.b_mode == OP_KC || p.b_mode == OP_RC);
-  if (tile == kTile256) {  // 256x256 ping-pong kernel: plain operands, K and k_split multiples of 64
+  if (tile == kTile256 || tile == kTile256P) {  // 256x256 ping-pong kernel: plain operands, K and k_split % 64
     if (!plain || p.K % 64 || p.k_split % 64 || p.om.enabled) return (int)hipErrorInvalidValue;
-    return launch_gemm256(p, epi, s);
+    return launch_gemm256(p, epi, s, tile == kTile256P);
   }
   if (tile == kTileW4 || tile == kTileW4N) {  // four-wave 256-row kernels: the same preconditions
     if (!plain || p.K % 64 || p.k_split % 64 || p.om.enabled) return (int)hipErrorInvalidValue;

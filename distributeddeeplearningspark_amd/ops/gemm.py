@@ -24,9 +24,10 @@ TILE_STREAM = 5  # weight-stationary streaming kernel (csrc/kernels/gemm_stream.
 TILE_CONV3 = 6  # 3x3 stride-1 halo convolution (csrc/kernels/conv3x3.hip): KC_GATHER x KC, no split-K
 TILE_W4 = 7  # four-wave 256x256 kernel, 128x128 wave tiles (csrc/include/ddl_gemm_w4.h): plain KC/RC, K % 64 == 0
 TILE_W4N = 8  # four-wave 256x128 kernel, 128x64 wave tiles
+TILE256P = 9  # the 256x256 ping-pong kernel in its persistent form (un-split GEMMs with more tiles than CUs)
 _TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), TILE256: (256, 256), TILE_STREAM: (64, 256),
-          TILE_CONV3: (224, 128), TILE_W4: (256, 256), TILE_W4N: (256, 128)}
-_ONE_PER_CU = (TILE256, TILE_W4, TILE_W4N)  # kernels running one workgroup per CU
+          TILE_CONV3: (224, 128), TILE_W4: (256, 256), TILE_W4N: (256, 128), TILE256P: (256, 256)}
+_ONE_PER_CU = (TILE256, TILE_W4, TILE_W4N, TILE256P)  # kernels running one workgroup per CU
 _CU = 256
 import os as _os
 

@@ -1,6 +1,7 @@
 """The 256-row GEMM kernels against fp32 references: the 256x256 ping-pong kernel
-(csrc/include/ddl_gemm256.h) and the four-wave 256x256 / 256x128 kernels (ddl_gemm_w4.h) — every
-operand layout, every epilogue, tails in M and N, split-K (atomics and partial slabs)."""
+(csrc/include/ddl_gemm256.h), in its persistent form too, and the four-wave 256x256 / 256x128 kernels
+(ddl_gemm_w4.h) — every operand layout, every epilogue, tails in M and N, split-K (atomics and partial
+slabs).  The persistent form engages with more tiles than CUs: the shapes marked below have 272-289 tiles."""
 import pytest
 import torch
 
@@ -8,7 +9,7 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-TILES = [4, 7, 8]  # G.TILE256, G.TILE_W4, G.TILE_W4N
+TILES = [4, 7, 8, 9]  # G.TILE256, G.TILE_W4, G.TILE_W4N, G.TILE256P
 
 
 def rnd(*shape, seed=0, scale=1.0):
@@ -25,7 +26,7 @@ def close(a, b, rtol=2e-2, atol=2e-2, what=""):
 
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 768), (1000, 520, 256), (300, 2304, 128),
-                                   (4096, 256, 1024)])
+                                   (4096, 256, 1024), (4200, 4104, 192)])
 @pytest.mark.parametrize("a_rc", [False, True])
 @pytest.mark.parametrize("b_rc", [False, True])
 @pytest.mark.parametrize("tile", TILES)
@@ -49,7 +50,7 @@ def test_gemm256_epilogues(tile):
     from distributeddeeplearningspark_amd.ops import gemm as G
     from distributeddeeplearningspark_amd.ops import transformer as T
 
-    M, N, K = 768, 1024, 512
+    M, N, K = (4352, 4096, 256) if tile == 9 else (768, 1024, 512)  # persistent: 272 tiles
     A, B = rnd(M, K, seed=3), rnd(N, K, seed=4, scale=0.1)
     bias = torch.randn(N, device=DEV) * 0.1
     res = rnd(M, N, seed=5)
@@ -85,9 +86,10 @@ def test_gemm256_fp32_and_splitk(tile):
     gs = torch.full((N1, K1), 0.25, device=DEV)
     G.gemm(dy, x, gs, N1, K1, T_, G.RC, G.RC, N1, K1, K1, G.EPI_F32, beta=1.0, tile=tile, slabs=True)
     close(gs, 0.25 + dy.float().T @ x.float(), rtol=1e-3, atol=5e-2, what="split-K fp32 slabs")
-    out = torch.empty(512, 512, device=DEV)
-    A, B = rnd(512, 256, seed=8), rnd(512, 256, seed=9)
-    G.gemm(A, B, out, 512, 512, 256, G.KC, G.KC, 256, 256, 512, G.EPI_F32, tile=tile)
+    M = 4352 if tile == 9 else 512  # persistent: 272 tiles
+    out = torch.empty(M, 4096 if tile == 9 else 512, device=DEV)
+    A, B = rnd(M, 256, seed=8), rnd(out.shape[1], 256, seed=9)
+    G.gemm(A, B, out, M, out.shape[1], 256, G.KC, G.KC, 256, 256, out.shape[1], G.EPI_F32, tile=tile)
     close(out, A.float() @ B.float().T, rtol=1e-3, atol=1e-2, what="fp32 store")
 
 
