@@ -191,10 +191,10 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
   if (bnr_x) {
     TORCH_CHECK(stats.has_value() && bnr_mean.has_value() && epi == EPI_BF16 && tile != kTile256 && tile != kTile256P && tile != kTileW4 && tile != kTileW4N,
                 "gemm: the fused BN-backward reduction needs a stats workspace, the mean and a bf16 epilogue");
-    TORCH_CHECK(tile == kTileStream || (N % 4 == 0 && ldc % 8 == 0 && !bias && relu == 0 && !resid && !outmap && !aux &&
+    TORCH_CHECK(tile == kTileStream || (N % 4 == 0 && ldc % 8 == 0 && !bias && relu == 0 && !aux &&
                                         drop_p == 0.0 && (a_mode == OP_KC || (a_mode == OP_KC_GATHER && b_mode == OP_KC))),
                 "gemm: BN-backward reduce outside the streaming kernel: plain or gathered-A data-gradient, N % 4 == 0, "
-                "ldc % 8 == 0, no bias / activation / residual / output map");
+                "ldc % 8 == 0, no bias / activation (a residual and a parity-class output map are allowed)");
     CHECK_CUDA(*bnr_x);
     CHECK_BF16(*bnr_x);
     TORCH_CHECK(bnr_x->is_contiguous() && bnr_x->numel() >= (M - 1) * ldc + N && ((uintptr_t)bnr_x->data_ptr() % 16) == 0,
@@ -210,8 +210,8 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
       p.bnr_mask = bnr_mask->data_ptr<uint8_t>();
     }
     if (bnr_scale || bnr_shift) {  // mode-2 mask (ReLU of the BN output recomputed from x)
-      TORCH_CHECK(bnr_scale && bnr_shift && !bnr_mask && tile != kTileStream,
-                  "gemm: bnr scale/shift (no mask bits; not on the streaming kernel)");
+      TORCH_CHECK(bnr_scale && bnr_shift && !bnr_mask && (tile != kTileStream || !resid),
+                  "gemm: bnr scale/shift (no mask bits; no residual on the streaming kernel)");
       CHECK_F32(*bnr_scale);
       CHECK_F32(*bnr_shift);
       TORCH_CHECK(bnr_scale->numel() >= N && bnr_shift->numel() >= N && ((uintptr_t)bnr_scale->data_ptr() % 16) == 0 &&

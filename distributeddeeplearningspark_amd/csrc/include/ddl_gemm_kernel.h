@@ -361,9 +361,11 @@ constexpr bool epi_dt(int epi) {
 template <int RN>
 constexpr int row_epi_bytes() { return 16 * (RN * 16 + 4) * 4; }
 
-// EPI_BF16_BNR: bf16 store of alpha*acc + the BatchNorm-backward partial sums of the stored gradient
-// (GemmParams::bnr_*), accumulated like the forward statistics (16-lane shuffle, one atomic per
-// column and shard).  Column-outer so that only one column group's mean / scale / shift is live.
+// EPI_BF16_BNR: bf16 store of alpha*acc (+ the residual: optional ReLU bit mask / stride-2 subgrid, as the
+// full epilogue adds it) + the BatchNorm-backward partial sums of the stored gradient (GemmParams::bnr_*),
+// accumulated like the forward statistics (16-lane shuffle, one atomic per column and shard).  Output rows
+// may scatter through the OutMap (a strided data-gradient's parity class): x, the mask and the store then
+// use the destination row.  Column-outer so that only one column group's mean / scale / shift is live.
 template <int RM, int RN>
 __device__ __forceinline__ void gemm_epilogue_bnr(const GemmParams& p, f32x4 (&acc)[RM][RN], const int mb,
                                                   const int nb, const int lane, const int bid, const int mlim) {
@@ -371,6 +373,31 @@ __device__ __forceinline__ void gemm_epilogue_bnr(const GemmParams& p, f32x4 (&a
   const int ncol = 4 * (lane >> 4);
   const bf16_t* X = reinterpret_cast<const bf16_t*>(p.bnr_x);
   float* st = p.stats + (long)(bid % kStatShards) * 2 * p.N;
+  // per-row destination and residual row offsets, once per row (the loops below are column-outer; the
+  // OutMap / stride-2 subgrid decompositions are two integer divisions each)
+  long rowoff[RM], resoff[RM];
+#pragma unroll
+  for (int i = 0; i < RM; ++i) {
+    const int m = mb + 16 * i + mrow;
+    if (p.om.enabled) {
+      int nn, ii, jj;
+      pix_decompose((uint32_t)m, p.om.gh, p.om.gw, nn, ii, jj);
+      rowoff[i] = ((long)(nn * p.om.hy + ii * p.om.so + p.om.oh) * p.om.wy + jj * p.om.so + p.om.ow) * p.ldc;
+    } else {
+      rowoff[i] = (long)m * p.ldc;
+    }
+    resoff[i] = -1;
+    if (p.resid) {
+      long rrow = m;
+      if (p.rsub_h) {
+        int rn_, ri_, rj_;
+        pix_decompose((uint32_t)m, p.rsub_h, p.rsub_w, rn_, ri_, rj_);
+        rrow = ((ri_ | rj_) & 1) ? -1L
+                                 : ((long)rn_ * ((p.rsub_h + 1) >> 1) + (ri_ >> 1)) * ((p.rsub_w + 1) >> 1) + (rj_ >> 1);
+      }
+      resoff[i] = rrow < 0 ? -1L : rrow * p.ldr;
+    }
+  }
 #pragma unroll
   for (int j = 0; j < RN; ++j) {
     const int n = nb + 16 * j + ncol;  // host check: N % 4 == 0, so n < N covers n .. n+3
@@ -391,10 +418,26 @@ __device__ __forceinline__ void gemm_epilogue_bnr(const GemmParams& p, f32x4 (&a
     for (int i = 0; i < RM; ++i) {
       const int m = mb + 16 * i + mrow;
       if (!nok || m >= mlim) continue;
-      const long off = (long)m * p.ldc + n;
+      const long off = rowoff[i] + n;
       const uint2 xv = *reinterpret_cast<const uint2*>(X + off);
       uint32_t mbits = 0xfu;
       if (p.bnr_mask) mbits = (uint32_t)p.bnr_mask[off >> 3] >> (off & 7);
+      float rv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (p.resid) {
+        if (resoff[i] >= 0) {
+          const uint2 r2 = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(p.resid) + resoff[i] + n);
+          rv[0] = __uint_as_float(r2.x << 16);
+          rv[1] = __uint_as_float(r2.x & 0xffff0000u);
+          rv[2] = __uint_as_float(r2.y << 16);
+          rv[3] = __uint_as_float(r2.y & 0xffff0000u);
+          if (p.resid_mask) {
+            const long bit = (long)m * p.ldr + n;
+            const uint32_t rb = (uint32_t)p.resid_mask[bit >> 3] >> (bit & 7);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) rv[e] = ((rb >> e) & 1u) ? rv[e] : 0.f;
+          }
+        }
+      }
       float x[4];
       x[0] = __uint_as_float(xv.x << 16);
       x[1] = __uint_as_float(xv.x & 0xffff0000u);
@@ -403,7 +446,7 @@ __device__ __forceinline__ void gemm_epilogue_bnr(const GemmParams& p, f32x4 (&a
       bf16_t o[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        o[e] = f2bf(acc[i][j][e] * p.alpha);
+        o[e] = f2bf(__fmul_rn(acc[i][j][e], p.alpha) + rv[e]);  // (no fma contraction: the full epilogue's rounding)
         bool keep = (mbits >> e) & 1u;
         if (p.bnr_scale) keep = (x[e] * sc[e] + sh[e]) > 0.f;
         const float d = keep ? bf2f(o[e]) : 0.f;

@@ -44,8 +44,19 @@ int bn_bwd_reduce(const void* dy, const void* x, const void* y, const float* sca
 int bn_bwd_finalize(const float* ws, int S, long M, int C, const float* gamma, const float* mean, const float* invstd,
                     float* dgamma, float* dbeta, float* coef, hipStream_t s);
 // pass 3: dx = A*dy' + B*x + K;  optionally dres = dy' (masked gradient of the residual branch)
+// x2 / mean2 / ws2 (optional): the same sweep writes the backward partial sums of a second BN fed by dy'
+// (ws2 [bn_partial_rows(M, C)][2][C]: sum dy', sum dy' * (x2 - mean2)) — see bn.hip
 int bn_bwd_dx(const void* dy, const void* x, const void* y, const float* scale, const float* shift,
-              const float* coef, void* dx, void* dres, long M, int C, int mode, hipStream_t s);
+              const float* coef, void* dx, void* dres, long M, int C, int mode, hipStream_t s,
+              const void* x2 = nullptr, const float* mean2 = nullptr, float* ws2 = nullptr);
+
+// ResNet stem: BN backward through the fused 3x3 / 2 / pad-1 max pool (pooled gradient dy + argmax bytes, the
+// BN output gradient recomputed per pixel, never stored): dx == nullptr -> reduce partials into ws
+// [S][2][C] (one row per workgroup); else dx = A d' + B x + K (coef) — bn.hip
+bool pool3s2_bn_bwd_ok(int N, int H, int W, int C, int Ho, int Wo);
+int pool3s2_bn_bwd(const void* dy, const uint8_t* am, const void* x, const float* scale, const float* shift,
+                   const float* mean, const float* coef, float* ws, int S, void* dx, int N, int H, int W, int C, int Ho,
+                   int Wo, hipStream_t s);
 
 // ---------------- pooling (NHWC) ----------------
 int maxpool_fwd(const void* x, void* y, uint8_t* argmax, int N, int H, int W, int C, int Ho, int Wo, int kh, int kw,

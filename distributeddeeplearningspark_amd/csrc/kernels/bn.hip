@@ -535,14 +535,27 @@ int bn_bwd_finalize(const float* ws, int S, long M, int C, const float* gamma, c
   return (int)hipGetLastError();
 }
 
-template <int R, bool NT>
+// RED: the same sweep also produces the backward partial sums of a SECOND BatchNorm that consumes the
+// masked gradient d (the ResNet downsample BN, whose input gradient is the block output's masked
+// gradient): row blockIdx.x of ws2[S][2][C] gets sum d and sum d * (x2 - mean2) — that BN's reduce sweep
+// (a read of d and x2) and the write of d itself (dres) are then not needed.  Grid = col_grid (S rows).
+template <int R, bool NT, bool RED>
 __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const uint4* __restrict__ dy, const uint4* __restrict__ x,
                                                          const uint4* __restrict__ y, const float* __restrict__ scale,
                                                          const float* __restrict__ shift,
                                                          const float* __restrict__ coef, uint4* __restrict__ dx,
-                                                         uint4* __restrict__ dres, long M, int C, int mode) {
+                                                         uint4* __restrict__ dres, long M, int C, int mode,
+                                                         const uint4* __restrict__ x2, const float* __restrict__ mean2,
+                                                         float* ws2) {
   ColGeom g(C);
-  if (!g.active) return;
+  float acc[RED ? 16 : 1];
+  float mu2[RED ? 8 : 1];
+  if constexpr (RED) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    if (g.active) load8f(mean2 + g.cv * 8, mu2);
+  }
+  if (g.active) {  // (inactive threads still join the RED block's LDS tree below)
   const int c = g.cv * 8;
   float A[8], B[8], K[8], sc[8], sh[8];
   load8f(coef + c, A);
@@ -558,7 +571,7 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const uint4* __restrict_
   const long step = (long)gridDim.x * g.RT;
   for (long r = (long)blockIdx.x * g.RT + g.rt; r < M; r += R * step) {
     long ix[R];
-    uint4 dv[R], xv[R];
+    uint4 dv[R], xv[R], x2v[RED ? R : 1];
     uint32_t mb[R];
 #pragma unroll
     for (int h = 0; h < R; ++h) {
@@ -566,6 +579,7 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const uint4* __restrict_
       ix[h] = (ok ? r + h * step : r) * g.CV + g.cv;
       dv[h] = dy[ix[h]];
       xv[h] = x[ix[h]];
+      if constexpr (RED) x2v[h] = x2[ix[h]];
       mb[h] = mask_byte(y, ix[h], mode);
     }
 #pragma unroll
@@ -576,20 +590,177 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const uint4* __restrict_
       unpack8(xv[h], xf);
       relu_mask(d, xf, y, ix[h], sc, sh, mode, mb[h]);
       if (dres) store16<NT>(dres + ix[h], pack8(d));
+      if constexpr (RED) {
+        float x2f[8];
+        unpack8(x2v[h], x2f);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          acc[i] += d[i];
+          acc[8 + i] += d[i] * (x2f[i] - mu2[i]);
+        }
+      }
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] = A[i] * d[i] + B[i] * xf[i] + K[i];
       store16<NT>(dx + ix[h], pack8(o));
     }
   }
+  }  // g.active
+  if constexpr (RED) col_reduce_store(acc, g, ws2, C);
 }
 
 int bn_bwd_dx(const void* dy, const void* x, const void* y, const float* scale, const float* shift, const float* coef,
-              void* dx, void* dres, long M, int C, int mode, hipStream_t s) {
+              void* dx, void* dres, long M, int C, int mode, hipStream_t s, const void* x2, const float* mean2,
+              float* ws2) {
   const int rows = bn_rows();
-  auto k = rows == 4 ? (bn_nt() ? bn_bwd_dx_kernel<4, true> : bn_bwd_dx_kernel<4, false>)
-                     : (bn_nt() ? bn_bwd_dx_kernel<2, true> : bn_bwd_dx_kernel<2, false>);
+  if (x2) {  // fused second-BN reduce: partial row per block, so the reduction's grid (S = bn_partial_rows)
+    auto k = rows == 4 ? (bn_nt() ? bn_bwd_dx_kernel<4, true, true> : bn_bwd_dx_kernel<4, false, true>)
+                       : (bn_nt() ? bn_bwd_dx_kernel<2, true, true> : bn_bwd_dx_kernel<2, false, true>);
+    hipLaunchKernelGGL(k, col_grid(M, C), dim3(256), 0, s, (const uint4*)dy, (const uint4*)x, (const uint4*)y, scale,
+                       shift, coef, (uint4*)dx, (uint4*)dres, M, C, mode, (const uint4*)x2, mean2, ws2);
+    return (int)hipGetLastError();
+  }
+  auto k = rows == 4 ? (bn_nt() ? bn_bwd_dx_kernel<4, true, false> : bn_bwd_dx_kernel<4, false, false>)
+                     : (bn_nt() ? bn_bwd_dx_kernel<2, true, false> : bn_bwd_dx_kernel<2, false, false>);
   hipLaunchKernelGGL(k, stream_grid(M, C, rows), dim3(256), 0, s, (const uint4*)dy, (const uint4*)x, (const uint4*)y,
-                     scale, shift, coef, (uint4*)dx, (uint4*)dres, M, C, mode);
+                     scale, shift, coef, (uint4*)dx, (uint4*)dres, M, C, mode, (const uint4*)nullptr,
+                     (const float*)nullptr, (float*)nullptr);
+  return (int)hipGetLastError();
+}
+
+}  // namespace ddl
+
+namespace ddl {
+
+// ResNet stem backward through its fused 3x3 / stride-2 / pad-1 max pool (the pool applied the BN affine +
+// ReLU on load, _StemPoolFn): the BN's output gradient d is the pool's gather of the pooled gradient dy over
+// the (<= 2 x 2) windows whose argmax byte names the pixel — recomputed here from dy and the argmax in both
+// passes instead of being written out (411 MB at batch 256) and read back twice:
+//   DX = false: backward partial sums sum d' and sum d' (x - mean) (d' = d under the ReLU mask recomputed
+//               from x: mode 2) into partial row blockIdx.x of ws[S][2][C] — the reduce sweep;
+//   DX = true : dx = A d' + B x + K with the finalize's coefficients — the dx sweep.
+// A thread owns a 2 x 2 pixel block of one 8-channel vector (the four pooled outputs that can cover it are
+// loaded once); the ColGeom mapping keeps that vector fixed per thread for the column reduction.
+template <bool DX>
+__global__ __launch_bounds__(256) void pool3s2_bn_bwd_kernel(const uint4* __restrict__ dy, const uint2* __restrict__ am,
+                                                              const uint4* __restrict__ x, const float* __restrict__ scale,
+                                                              const float* __restrict__ shift, const float* __restrict__ mean,
+                                                              const float* __restrict__ coef, float* ws,
+                                                              uint4* __restrict__ dx, int N, int H, int W, int Ho, int Wo,
+                                                              int C) {
+  ColGeom g(C);
+  float acc[DX ? 1 : 16];
+  if constexpr (!DX) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  }
+  if (g.active) {
+    const int CV = g.CV, cv = g.cv, c = cv * 8;
+    float sc[8], sh[8], p0[8], p1[8], p2[8];
+    load8f(scale + c, sc);
+    load8f(shift + c, sh);
+    if constexpr (DX) {
+      load8f(coef + c, p0);
+      load8f(coef + C + c, p1);
+      load8f(coef + 2 * C + c, p2);
+    } else {
+      load8f(mean + c, p0);
+    }
+    const int HB = (H + 1) >> 1, WB = (W + 1) >> 1;
+    const uint32_t nq = (uint32_t)N * HB * WB;  // < 2^31 / CV (launcher)
+    for (uint32_t q = blockIdx.x * (uint32_t)g.RT + g.rt; q < nq; q += gridDim.x * (uint32_t)g.RT) {
+      const uint32_t q2 = q / (uint32_t)WB;
+      const int bj = (int)(q - q2 * (uint32_t)WB);
+      const int bi = (int)(q2 % (uint32_t)HB);
+      const int n = (int)(q2 / (uint32_t)HB);
+      uint2 a[2][2];
+      uint4 gv[2][2], xv[2][2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int oh = bi + i, ow = bj + j;
+          if (oh < Ho && ow < Wo) {
+            const uint32_t o = (((uint32_t)n * Ho + oh) * Wo + ow) * (uint32_t)CV + cv;
+            a[i][j] = am[o];
+            gv[i][j] = dy[o];
+          } else {
+            a[i][j] = make_uint2(0xffffffffu, 0xffffffffu);  // no window index matches 0xff
+            gv[i][j] = make_uint4(0, 0, 0, 0);
+          }
+          const int h = 2 * bi + i, w = 2 * bj + j;  // pixel (pa, pb) = (i, j) of the block
+          xv[i][j] = (h < H && w < W) ? x[(((uint32_t)n * H + h) * W + w) * (uint32_t)CV + cv] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+      for (int pa = 0; pa < 2; ++pa)
+#pragma unroll
+        for (int pb = 0; pb < 2; ++pb) {
+          const int h = 2 * bi + pa, w = 2 * bj + pb;
+          if (h >= H || w >= W) continue;
+          float d[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) d[e] = 0.f;
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const int dr = h + 1 - 2 * (bi + i), dc = w + 1 - 2 * (bj + j);  // position inside window
+              if (dr < 0 || dr > 2 || dc < 0 || dc > 2) continue;             // compile-time after unrolling
+              const uint32_t idx = (uint32_t)(dr * 3 + dc);
+              float gf[8];
+              unpack8(gv[i][j], gf);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) {
+                const uint32_t word = e < 4 ? a[i][j].x : a[i][j].y;
+                if (((word >> ((e & 3) * 8)) & 0xffu) == idx) d[e] += gf[e];
+              }
+            }
+          float xf[8];
+          unpack8(xv[pa][pb], xf);
+          // d is the bf16 value the separate pool backward would have stored (at most two windows add)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) d[e] = (xf[e] * sc[e] + sh[e]) > 0.f ? bf2f(f2bf(d[e])) : 0.f;
+          if constexpr (DX) {
+            float o[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = p0[e] * d[e] + p1[e] * xf[e] + p2[e];
+            dx[(((uint32_t)n * H + h) * W + w) * (uint32_t)CV + cv] = pack8(o);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              acc[e] += d[e];
+              acc[8 + e] += d[e] * (xf[e] - p0[e]);
+            }
+          }
+        }
+    }
+  }
+  if constexpr (!DX) col_reduce_store(acc, g, ws, C);
+}
+
+bool pool3s2_bn_bwd_ok(int N, int H, int W, int C, int Ho, int Wo) {
+  return C % 8 == 0 && C / 8 <= 256 && Ho == (H - 1) / 2 + 1 && Wo == (W - 1) / 2 + 1 &&
+         (long)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8) < (1L << 31) && (long)N * H * W * (C / 8) < (1L << 31);
+}
+
+int pool3s2_bn_bwd(const void* dy, const uint8_t* am, const void* x, const float* scale, const float* shift,
+                   const float* mean, const float* coef, float* ws, int S, void* dx, int N, int H, int W, int C, int Ho,
+                   int Wo, hipStream_t s) {
+  if (!pool3s2_bn_bwd_ok(N, H, W, C, Ho, Wo)) return (int)hipErrorInvalidValue;
+  const int CV = C / 8, CT = CV, RT = 256 / CT;
+  const long nq = (long)N * ((H + 1) / 2) * ((W + 1) / 2);
+  if (dx) {
+    long gx = (nq + RT - 1) / RT;
+    if (gx > 4096) gx = 4096;
+    hipLaunchKernelGGL(pool3s2_bn_bwd_kernel<true>, dim3((unsigned)gx), dim3(256), 0, s, (const uint4*)dy,
+                       (const uint2*)am, (const uint4*)x, scale, shift, mean, coef, ws, (uint4*)dx, N, H, W, Ho, Wo, C);
+  } else {  // one partial row per block: S blocks (the caller's workspace rows; more than a reduce sweep's 512:
+            // each thread's 2 x 2 gather is latency-bound, so the sweep needs the extra waves in flight)
+    if (S < 1) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(pool3s2_bn_bwd_kernel<false>, dim3((unsigned)S), dim3(256), 0,
+                       s, (const uint4*)dy, (const uint2*)am, (const uint4*)x, scale, shift, mean, coef, ws,
+                       (uint4*)nullptr, N, H, W, Ho, Wo, C);
+  }
+  (void)CT;
   return (int)hipGetLastError();
 }
 

@@ -24,10 +24,11 @@ int launch_gemm_bf16(const GemmParams& p_in, int epi, int tile, void* stream) {
   GemmParams p = p_in;
   p.group_m = group_m;
   if (p.bnr_x && tile != kTileStream &&  // fused BN-backward reduce on the other kernels: EPI_BF16_BNR
-      (tile == kTile256 || tile == kTile256P || tile == kTileW4 || tile == kTileW4N || epi != EPI_BF16 || p.om.enabled || p.resid || p.aux || p.drop_thresh || p.bias || p.relu || p.N % 4 || p.ldc % 8 ||
+      (tile == kTile256 || tile == kTile256P || tile == kTileW4 || tile == kTileW4N || epi != EPI_BF16 || p.om.zero_siblings ||
+       (p.resid && (p.ldr % 4 || (uintptr_t)p.resid % 8)) || p.aux || p.drop_thresh || p.bias || p.relu || p.N % 4 || p.ldc % 8 ||
        !(p.a_mode == OP_KC || p.a_mode == OP_KC_GATHER) || (p.a_mode == OP_KC_GATHER && p.b_mode != OP_KC)))
     return (int)hipErrorInvalidValue;
-  if (p.bnr_scale && tile == kTileStream) return (int)hipErrorInvalidValue;  // streaming kernel: mask bits only
+  if (p.bnr_scale && tile == kTileStream && p.resid) return (int)hipErrorInvalidValue;  // streaming: mode 2 w/o residual
   if (p.a_scale && tile != kTileStream) return (int)hipErrorInvalidValue;  // normalise-on-load of A: streaming kernel
   if (p.b_scale && !(p.a_mode == OP_RC && p.b_mode == OP_RC && (epi == EPI_F32 || epi == EPI_F32_ATOMIC) &&
                      tile <= 3 && p.K % 64 == 0 && p.k_split % 64 == 0))

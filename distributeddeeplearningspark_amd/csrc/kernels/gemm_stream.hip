@@ -105,7 +105,9 @@ __device__ __forceinline__ void stage_a(const bf16_t* __restrict__ A, long lda, 
 // ANORM: GemmParams::a_scale / a_shift — each landed A tile is normalised in place in LDS (BN affine +
 // ReLU of the layer that produced A) before any wave reads its fragments: thread t owns logical 16-B
 // chunk t % CPR (8 channels, parameters in registers) of rows t / CPR, t / CPR + 256 / CPR, ...
-template <int WN, int K, int BMODE, bool RES, bool BNR = false, bool ANORM = false>
+// BNR: 0 off; 1 the ReLU mask of the BN-backward reduce from GemmParams::bnr_mask (bits, or all ones);
+// 2 recomputed from the BN input as x * bnr_scale + bnr_shift > 0 (a BN without residual: mode 2)
+template <int WN, int K, int BMODE, bool RES, int BNR = 0, bool ANORM = false>
 __global__ __launch_bounds__(gst::THREADS, 2) void gemm_stream_kernel(const GemmParams p) {
   using namespace gst;
   using CF = Cfg<WN, K>;
@@ -169,11 +171,20 @@ __global__ __launch_bounds__(gst::THREADS, 2) void gemm_stream_kernel(const Gemm
   const int oc = threadIdx.x % CF::OCPR, orow = threadIdx.x / CF::OCPR;
   // BNR: batch mean of the 8 columns this thread reads out (loaded once)
   float bmu[8];
-  if constexpr (BNR) {
+  float bsc[BNR == 2 ? 8 : 1], bsh[BNR == 2 ? 8 : 1];
+  if constexpr (BNR != 0) {
     const float4 a = *reinterpret_cast<const float4*>(p.bnr_mean + n0 + oc * 8);
     const float4 b = *reinterpret_cast<const float4*>(p.bnr_mean + n0 + oc * 8 + 4);
     bmu[0] = a.x; bmu[1] = a.y; bmu[2] = a.z; bmu[3] = a.w;
     bmu[4] = b.x; bmu[5] = b.y; bmu[6] = b.z; bmu[7] = b.w;
+  }
+  if constexpr (BNR == 2) {
+    const float4 a0 = *reinterpret_cast<const float4*>(p.bnr_scale + n0 + oc * 8);
+    const float4 a1 = *reinterpret_cast<const float4*>(p.bnr_scale + n0 + oc * 8 + 4);
+    const float4 b0 = *reinterpret_cast<const float4*>(p.bnr_shift + n0 + oc * 8);
+    const float4 b1 = *reinterpret_cast<const float4*>(p.bnr_shift + n0 + oc * 8 + 4);
+    bsc[0] = a0.x; bsc[1] = a0.y; bsc[2] = a0.z; bsc[3] = a0.w; bsc[4] = a1.x; bsc[5] = a1.y; bsc[6] = a1.z; bsc[7] = a1.w;
+    bsh[0] = b0.x; bsh[1] = b0.y; bsh[2] = b0.z; bsh[3] = b0.w; bsh[4] = b1.x; bsh[5] = b1.y; bsh[6] = b1.z; bsh[7] = b1.w;
   }
   bf16_t* __restrict__ Cout = reinterpret_cast<bf16_t*>(p.c);
 
@@ -223,7 +234,8 @@ __global__ __launch_bounds__(gst::THREADS, 2) void gemm_stream_kernel(const Gemm
         const int m = min(m0 + orow + ps * CF::RPP, p.M - 1);
         const long idx = (long)m * p.ldc + n0 + oc * 8;
         bx[ps] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(p.bnr_x) + idx);
-        bm8[ps] = p.bnr_mask ? (uint32_t)p.bnr_mask[idx >> 3] : 0xffu;
+        if constexpr (BNR == 1) bm8[ps] = p.bnr_mask ? (uint32_t)p.bnr_mask[idx >> 3] : 0xffu;
+        else bm8[ps] = 0xffu;
       }
     }
     const int ahead = i + CF::NBUF - 1;
@@ -313,8 +325,11 @@ __global__ __launch_bounds__(gst::THREADS, 2) void gemm_stream_kernel(const Gemm
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
               const int e = 2 * q + h;
-              const float d = ((bm8[ps] >> e) & 1u) ? __uint_as_float(h ? (wv[q] & 0xffff0000u) : (wv[q] << 16)) : 0.f;
               const float xe = __uint_as_float(h ? (xv[q] & 0xffff0000u) : (xv[q] << 16));
+              bool keep;
+              if constexpr (BNR == 2) keep = xe * bsc[e] + bsh[e] > 0.f;  // the forward's own fmaf: same bits
+              else keep = (bm8[ps] >> e) & 1u;
+              const float d = keep ? __uint_as_float(h ? (wv[q] & 0xffff0000u) : (wv[q] << 16)) : 0.f;
               s1[e] += d;
               s2[e] += d * (xe - bmu[e]);
             }
@@ -389,13 +404,16 @@ int launch_ws(const GemmParams& p, hipStream_t s) {
   const int gx = std::max(1, std::min(mt, 2 * num_cus() / std::max(1, panels)));
   if (p.a_scale) {  // normalise-on-load of A (no residual / BN-reduce variants: a forward conv)
     if (p.resid || p.bnr_x) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL((gemm_stream_kernel<WN, K, BMODE, false, false, true>), dim3(gx, panels), dim3(gst::THREADS), 0, s,
+    hipLaunchKernelGGL((gemm_stream_kernel<WN, K, BMODE, false, 0, true>), dim3(gx, panels), dim3(gst::THREADS), 0, s,
                        p);
+  } else if (p.bnr_x && p.bnr_scale) {  // mode 2 (no residual: a BN + ReLU without a shortcut)
+    if (p.resid) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL((gemm_stream_kernel<WN, K, BMODE, false, 2>), dim3(gx, panels), dim3(gst::THREADS), 0, s, p);
   } else if (p.bnr_x) {
     if (p.resid)
-      hipLaunchKernelGGL((gemm_stream_kernel<WN, K, BMODE, true, true>), dim3(gx, panels), dim3(gst::THREADS), 0, s, p);
+      hipLaunchKernelGGL((gemm_stream_kernel<WN, K, BMODE, true, 1>), dim3(gx, panels), dim3(gst::THREADS), 0, s, p);
     else
-      hipLaunchKernelGGL((gemm_stream_kernel<WN, K, BMODE, false, true>), dim3(gx, panels), dim3(gst::THREADS), 0, s, p);
+      hipLaunchKernelGGL((gemm_stream_kernel<WN, K, BMODE, false, 1>), dim3(gx, panels), dim3(gst::THREADS), 0, s, p);
   } else if (p.resid) {
     hipLaunchKernelGGL((gemm_stream_kernel<WN, K, BMODE, true>), dim3(gx, panels), dim3(gst::THREADS), 0, s, p);
   } else {
@@ -449,6 +467,8 @@ int launch_gemm_stream(const GemmParams& p, int epi, hipStream_t s) {
                   ((uintptr_t)p.a % 16 == 0) && ((uintptr_t)p.c % 16 == 0) &&
                   (p.b_mode == OP_RC || (uintptr_t)p.b % 16 == 0) && (!p.resid || (uintptr_t)p.resid % 8 == 0) &&
                   (!p.bnr_x || (p.stats && (uintptr_t)p.bnr_x % 16 == 0 && (uintptr_t)p.bnr_mean % 16 == 0)) &&
+                  (!p.bnr_scale || (p.bnr_shift && !p.resid && (uintptr_t)p.bnr_scale % 16 == 0 &&
+                                    (uintptr_t)p.bnr_shift % 16 == 0)) &&
                   (!p.a_scale || (p.a_shift && (uintptr_t)p.a_scale % 16 == 0 && (uintptr_t)p.a_shift % 16 == 0));
   if (!ok) return (int)hipErrorInvalidValue;
   return p.b_mode == OP_KC ? launch_panel<OP_KC>(p, nb, s) : launch_panel<OP_RC>(p, nb, s);

@@ -138,6 +138,55 @@ void bn_bwd_dx_(const at::Tensor& dy, const at::Tensor& x, c10::optional<at::Ten
                    (int)C, (int)mode, cur_stream()));
 }
 
+// bn_bwd_dx plus the fused reduce of a second BN consuming dy' (the ResNet downsample BN): x2 [M, C] bf16,
+// mean2 [C], ws2 [bn_partial_rows(M, C)][2][C] (every row written)
+void bn_bwd_dx_red_(const at::Tensor& dy, const at::Tensor& x, c10::optional<at::Tensor> y,
+                    c10::optional<at::Tensor> scale, c10::optional<at::Tensor> shift, const at::Tensor& coef,
+                    const at::Tensor& dx, int64_t C, int64_t mode, const at::Tensor& x2, const at::Tensor& mean2,
+                    const at::Tensor& ws2) {
+  GPU(dy); BF16(dy); BF16(x); BF16(dx); F32(coef); BF16(x2); F32(mean2); F32(ws2);
+  CK(dy.numel() == x.numel() && dx.numel() == x.numel() && x2.numel() == x.numel() && x.numel() % C == 0 && C % 8 == 0,
+     "bn_bwd_dx_red: shapes");
+  CK(coef.numel() >= 3 * C && mean2.numel() >= C, "bn_bwd_dx_red: coef / mean2 size");
+  CK(ws2.numel() >= (int64_t)bn_partial_rows(x.numel() / C, (int)C) * 2 * C, "bn_bwd_dx_red: workspace too small");
+  if (mode == 1) { CK(y.has_value(), "mode 1 needs y"); BF16(*y); CK(y->numel() == x.numel(), "bn_bwd_dx_red: y shape"); }
+  if (mode == 3) CK(y.has_value() && y->scalar_type() == at::kByte && y->numel() >= x.numel() / 8,
+                    "mode 3 needs the uint8 bit mask of bn_apply");
+  CK(mode >= 0 && mode <= 3, "bn_bwd_dx_red: mode");
+  if (mode == 2) { CK(scale.has_value() && shift.has_value(), "mode 2 needs scale/shift"); F32(*scale); F32(*shift); }
+  at::DeviceGuard g(x.device());
+  HIP_OK(bn_bwd_dx(dy.data_ptr(), x.data_ptr(), optr<const void>(y), optr<const float>(scale),
+                   optr<const float>(shift), coef.data_ptr<float>(), dx.data_ptr(), nullptr, x.numel() / C, (int)C,
+                   (int)mode, cur_stream(), x2.data_ptr(), mean2.data_ptr<float>(), ws2.data_ptr<float>()));
+}
+
+// stem BN backward through the 3x3 / 2 / pad-1 max pool: dy [N, Ho, Wo, C] pooled gradient, am its argmax
+// bytes, x [N, H, W, C] the pre-BN conv output; phase 0: reduce partials into ws; phase 1: dx with coef
+void pool3s2_bn_bwd_(const at::Tensor& dy, const at::Tensor& am, const at::Tensor& x, const at::Tensor& scale,
+                     const at::Tensor& shift, const at::Tensor& mean, const at::Tensor& coef_or_ws,
+                     c10::optional<at::Tensor> dx) {
+  GPU(dy); BF16(dy); BF16(x); F32(scale); F32(shift); F32(mean); F32(coef_or_ws);
+  CK(dy.dim() == 4 && x.dim() == 4 && dy.size(0) == x.size(0) && dy.size(3) == x.size(3) && dy.is_contiguous() &&
+     x.is_contiguous(), "pool3s2_bn_bwd: NHWC dy / x");
+  CK(am.scalar_type() == at::kByte && am.numel() == dy.numel() && am.is_contiguous(), "pool3s2_bn_bwd: argmax bytes");
+  const int N = (int)x.size(0), H = (int)x.size(1), W = (int)x.size(2), C = (int)x.size(3);
+  const int Ho = (int)dy.size(1), Wo = (int)dy.size(2);
+  CK(pool3s2_bn_bwd_ok(N, H, W, C, Ho, Wo), "pool3s2_bn_bwd: 3x3 / 2 / pad-1 pool, C % 8 == 0, C <= 2048");
+  CK(scale.numel() >= C && shift.numel() >= C && mean.numel() >= C, "pool3s2_bn_bwd: per-channel vectors");
+  if (dx) {
+    BF16(*dx);
+    CK(dx->numel() == x.numel() && dx->is_contiguous() && coef_or_ws.numel() >= 3 * C, "pool3s2_bn_bwd: dx / coef");
+  } else {
+    CK(coef_or_ws.numel() % (2 * C) == 0 && coef_or_ws.numel() / (2 * C) <= 16384, "pool3s2_bn_bwd: ws [S][2][C]");
+  }
+  at::DeviceGuard g(x.device());
+  HIP_OK(pool3s2_bn_bwd(dy.data_ptr(), am.data_ptr<uint8_t>(), x.data_ptr(), scale.data_ptr<float>(),
+                        shift.data_ptr<float>(), mean.data_ptr<float>(), dx ? coef_or_ws.data_ptr<float>() : nullptr,
+                        dx ? nullptr : coef_or_ws.data_ptr<float>(), (int)(coef_or_ws.numel() / (2 * C)),
+                        dx ? dx->data_ptr() : nullptr, N, H, W, C, Ho, Wo,
+                        cur_stream()));
+}
+
 // ---------------------------------------------------------------- pooling
 void maxpool_fwd_(const at::Tensor& x, const at::Tensor& y, const at::Tensor& am, int64_t kh, int64_t kw, int64_t sh,
                   int64_t sw, int64_t ph, int64_t pw, c10::optional<at::Tensor> scale, c10::optional<at::Tensor> shift) {
@@ -535,6 +584,11 @@ void register_ops(py::module& m) {
   m.def("bn_bwd_reduce", &bn_bwd_reduce_);
   m.def("bn_bwd_finalize", &bn_bwd_finalize_);
   m.def("bn_bwd_dx", &bn_bwd_dx_);
+  m.def("bn_bwd_dx_red", &bn_bwd_dx_red_);
+  m.def("pool3s2_bn_bwd", &pool3s2_bn_bwd_);
+  m.def("pool3s2_bn_bwd_ok", [](int64_t N, int64_t H, int64_t W, int64_t C, int64_t Ho, int64_t Wo) {
+    return pool3s2_bn_bwd_ok((int)N, (int)H, (int)W, (int)C, (int)Ho, (int)Wo);
+  });
   m.def("maxpool_fwd", &maxpool_fwd_, "NHWC max pool (byte argmax); optional fused BN affine + ReLU on load",
         py::arg("x"), py::arg("y"), py::arg("am"), py::arg("kh"), py::arg("kw"), py::arg("sh"), py::arg("sw"),
         py::arg("ph"), py::arg("pw"), py::arg("scale") = py::none(), py::arg("shift") = py::none());

@@ -244,6 +244,11 @@ def _dgrad_as_forward(g: ConvGeometry):
 
 
 _KC_DGRAD = _os.environ.get("DDL_DGRAD_KC", "1") != "0"
+# BN-backward reduce fused into the parity-class GEMMs of a strided data-gradient (EPI_BF16_BNR with OutMap):
+# opt-in — correct (tests/test_gpu_kernels.py) but the BNR epilogue costs the short class GEMMs more than the
+# three reduce sweeps it removes (ResNet-50 11,942-11,948 vs 12,029-12,040 img/s interleaved,
+# profiles/r4/fuse_bn/ab_strided_bnr.txt)
+_STRIDED_BNR = _os.environ.get("DDL_STRIDED_BNR", "0") == "1"
 _WIDE_WGRAD = _os.environ.get("DDL_WGRAD_WIDE", "1") != "0"
 # gathered weight gradients: split-K workgroup rounds and tile (experiments: DDL_WGRAD_ROUNDS,
 # DDL_WGRAD_TILE=128 forces 128x128 tiles where M, N >= 128 instead of choose_tile's fill rule)
@@ -298,6 +303,11 @@ def conv_dgrad_native(dy, w, g: ConvGeometry, resid=None, resid_mask=None, bnr=N
         return dx
     dx = (torch.zeros if g.dgrad_needs_zero else torch.empty)((g.N, g.H, g.W, g.Ci), dtype=torch.bfloat16, device=dev)
     strided = g.sh > 1 or g.sw > 1
+    # fused BN-backward reduce of dx over the parity classes (each class's EPI_BF16_BNR epilogue adds the partial
+    # sums of the pixels it writes, through the OutMap): every pixel must be written by exactly one class
+    cls_bnr = (bnr if _STRIDED_BNR and bnr is not None and strided and resid is None and g.implicit_dgrad and _KC_DGRAD
+               and not g.dgrad_needs_zero and not g.dgrad_zero_siblings and g.Ci % 8 == 0
+               and bnr["x"].is_contiguous() else None)
     for cl in g.classes:
         nt = len(cl["wt"])
         if nt == 0:
@@ -315,7 +325,7 @@ def conv_dgrad_native(dy, w, g: ConvGeometry, resid=None, resid_mask=None, bnr=N
             geom = dict(n=g.N, hi=g.Ho, wi=g.Wo, c=g.Co, ho=cl["Hc"], wo=cl["Wc"], sh=1, sw=1, tap_c=g.Co,
                         dh=cl["dh"], dw=cl["dw"])
             G.gemm(dy, wkc, dx, Mc, g.Ci, nt * g.Co, G.KC_GATHER, G.KC, 0, nt * g.Co, g.Ci, G.EPI_BF16,
-                   geom=geom, outmap=om, resid=r, ldr=g.Ci if r is not None else 0)
+                   geom=geom, outmap=om, resid=r, ldr=g.Ci if r is not None else 0, bnr=cls_bnr)
         elif g.implicit_dgrad:
             geom = dict(n=g.N, hi=g.Ho, wi=g.Wo, c=g.Co, ho=cl["Hc"], wo=cl["Wc"], sh=1, sw=1, tap_c=g.Co,
                         dh=cl["dh"], dw=cl["dw"], wt=cl["wt"])
@@ -334,6 +344,8 @@ def conv_dgrad_native(dy, w, g: ConvGeometry, resid=None, resid_mask=None, bnr=N
                    ldr=g.Ci if r is not None else 0)
     if resid is not None and strided:
         C().add_bf16(dx, resid, dx)
+    if cls_bnr is not None:
+        cls_bnr["done"] = True
     return dx
 
 

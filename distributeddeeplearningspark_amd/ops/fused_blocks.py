@@ -111,26 +111,44 @@ def convbn_forward(unit, x, resid=None, relu=True, apply=True, res_affine=None, 
     return st
 
 
-def bn_backward(unit, st, dy, want_dres):
+def bn_backward(unit, st, dy, want_dres, red2=None, dy_mask=None, reduced=None):
+    """BN backward of ``st`` for output gradient ``dy``: (dx, dres or None).
+
+    ``red2 = (x2, mean2, ws2)``: the dx sweep also writes the reduce partials of a second BN fed by the
+    masked gradient (``bn_bwd_dx_red``; the ResNet downsample BN).  ``dy_mask``: the gradient this BN
+    sees is ``dy`` under that ReLU bit mask (mode 3), i.e. the masked gradient is never materialised;
+    ``reduced``: the partial-sum workspace already holds this BN's reduce (the red2 of the producer)."""
     bn = unit.bn
     Cc = st.yc.shape[-1]
     M = st.yc.numel() // Cc
+    mode = st.mode
     y = st.y if st.mode == 1 else (st.mask if st.mode == 3 else None)
+    if dy_mask is not None:
+        if st.mode != 0:
+            raise ValueError("bn_backward: dy_mask applies to a BN without its own ReLU")
+        mode, y = 3, dy_mask
     pre, st.pre_reduced = st.pre_reduced, None
-    if pre is not None and _same_tensor(pre[1], dy):
+    if reduced is not None:
+        ws = reduced
+    elif pre is not None and _same_tensor(pre[1], dy):
         # partial sums already accumulated by dy's producer (no reduce sweep) — valid only when dy IS the
         # gradient that producer reduced: a second consumer of this BN's output makes autograd sum the
         # gradients into a new tensor, and then the sweep runs on the sum
         ws = pre[0]
     else:
         ws = partials_workspace(M, Cc, dy.device)
-        C().bn_bwd_reduce(dy, st.yc, y, st.scale, st.shift, st.mean, ws, Cc, st.mode)
+        C().bn_bwd_reduce(dy, st.yc, y, st.scale, st.shift, st.mean, ws, Cc, mode)
     coef = torch.empty(3 * Cc, dtype=torch.float32, device=dy.device)
     C().bn_bwd_finalize(ws, M, Cc, None if bn.gamma is None else bn.gamma.master, st.mean, st.invstd,
                         None if bn.gamma is None else bn.gamma.grad, None if bn.beta is None else bn.beta.grad, coef)
     dyc = torch.empty_like(dy)
     dres = torch.empty_like(dy) if want_dres else None
-    C().bn_bwd_dx(dy, st.yc, y, st.scale, st.shift, coef, dyc, dres, Cc, st.mode)
+    if red2 is not None:
+        if dres is not None:
+            raise ValueError("bn_backward: red2 replaces dres")
+        C().bn_bwd_dx_red(dy, st.yc, y, st.scale, st.shift, coef, dyc, Cc, mode, red2[0], red2[1], red2[2])
+    else:
+        C().bn_bwd_dx(dy, st.yc, y, st.scale, st.shift, coef, dyc, dres, Cc, mode)
     if bn.grad_hook is not None:
         bn.grad_hook()
     return dyc, dres
@@ -189,7 +207,18 @@ class _BottleneckFn(torch.autograd.Function):
         # identity shortcut: its gradient is dout masked by the block-output ReLU; instead of the BN
         # backward writing it out, conv1's data-gradient epilogue adds dout under the bit mask
         masked_sc = s_down is None and s3.mode == 3 and s1.g.is_pointwise
-        d3c, dsc = bn_backward(b.c3, s3, dout, want_dres=not masked_sc)
+        # downsample shortcut: its BN's input gradient is dout under bn3's ReLU mask.  bn3's dx sweep also
+        # writes that BN's reduce partials (it reads dout and the mask anyway; + a read of the shortcut's
+        # pre-BN tensor), and the shortcut BN's dx sweep re-applies the mask to dout — so the masked
+        # gradient is never written, and the shortcut BN runs no reduce sweep
+        fuse_down = _FUSE_DOWN and s_down is not None and s3.mode == 3 and s_down.mode == 0
+        ws_d = None
+        if fuse_down:
+            Cd = s_down.yc.shape[-1]
+            ws_d = partials_workspace(s_down.yc.numel() // Cd, Cd, dout.device)
+            d3c, dsc = bn_backward(b.c3, s3, dout, False, red2=(s_down.yc, s_down.mean, ws_d))
+        else:
+            d3c, dsc = bn_backward(b.c3, s3, dout, want_dres=not masked_sc)
         # the data-gradients of conv3 and conv2 produce bn2's / bn1's output gradients: their epilogues also
         # accumulate those BNs' backward partial sums (ReLU mask recomputed from yc), so bn_backward skips the
         # reduce sweep wherever the kernel that ran could take it (bnr["done"])
@@ -203,7 +232,10 @@ class _BottleneckFn(torch.autograd.Function):
         d1c, _ = bn_backward(b.c1, s1, d1, False)
         rsub = None
         if s_down is not None:
-            ddc, _ = bn_backward(b.down, s_down, dsc, False)
+            if fuse_down:
+                ddc, _ = bn_backward(b.down, s_down, dout, False, dy_mask=s3.mask, reduced=ws_d)
+            else:
+                ddc, _ = bn_backward(b.down, s_down, dsc, False)
             gd = s_down.g
             if (_HALF_RES_SC and ctx.needs_dx and s1.g.is_pointwise and gd.KH == 1 and gd.KW == 1
                     and (gd.sh, gd.sw) == (2, 2) and (gd.ph, gd.pw) == (0, 0)):
@@ -240,6 +272,11 @@ _FUSE_BNR = _os.environ.get("DDL_FUSE_BN_REDUCE", "1") != "0"
 # bn1 / bn2 of every bottleneck: reduce fused into the conv2 / conv3 data-gradient epilogues
 _FUSE_BNR_INNER = _os.environ.get("DDL_FUSE_BN_REDUCE_INNER", "1") != "0"
 _HALF_RES_SC = _os.environ.get("DDL_HALF_RES_SHORTCUT", "1") != "0"
+# downsample BN backward fed by bn3's dx sweep (bn_bwd_dx_red): no masked-gradient tensor, no reduce sweep
+_FUSE_DOWN = _os.environ.get("DDL_FUSE_DOWN_BN", "1") != "0"
+# stem: BN backward through the max pool without materialising the pool's gradient (pool3s2_bn_bwd)
+_FUSE_STEM_BWD = _os.environ.get("DDL_FUSE_STEM_BWD", "1") != "0"
+_STEM_PARTIALS = int(_os.environ.get("DDL_STEM_PARTIALS", "2048"))  # workgroups (= partial rows) of its reduce
 # Normalise-on-load is opt-in (DDL_NORM_ON_LOAD=1): it removes bn2's apply sweep (-0.27 ms/step on
 # ResNet-50 b256) but the per-fragment scale/shift/ReLU VALU in the RC x RC weight gradient (+0.22 ms)
 # and the LDS transform pass + narrower panels of the streaming forward (+0.20 ms) cost more
@@ -340,9 +377,27 @@ class _StemPoolFn(torch.autograd.Function):
         xs, am = ctx.saved_tensors
         unit, st = ctx.unit, ctx.st
         k, s, p = ctx.pool
-        d = torch.empty_like(st.yc)
-        C().maxpool_bwd(dy.contiguous(), am, d, k, k, s, s, p, p)
-        dyc, _ = bn_backward(unit, st, d, False)
+        dy = dy.contiguous()
+        N, H, W, Co = st.yc.shape
+        if _FUSE_STEM_BWD and (k, s, p) == (3, 2, 1) and C().pool3s2_bn_bwd_ok(N, H, W, Co, dy.shape[1], dy.shape[2]):
+            # the BN output gradient (the pool's gather) is recomputed from dy + argmax by the reduce and the dx
+            # sweeps instead of being written (411 MB at batch 256) and read back by both
+            bn = unit.bn
+            M = N * H * W
+            ws = torch.empty((_STEM_PARTIALS, 2, Co), dtype=torch.float32, device=dy.device)  # one row per workgroup
+            C().pool3s2_bn_bwd(dy, am, st.yc, st.scale, st.shift, st.mean, ws, None)
+            coef = torch.empty(3 * Co, dtype=torch.float32, device=dy.device)
+            C().bn_bwd_finalize(ws, M, Co, None if bn.gamma is None else bn.gamma.master, st.mean, st.invstd,
+                                None if bn.gamma is None else bn.gamma.grad, None if bn.beta is None else bn.beta.grad,
+                                coef)
+            dyc = torch.empty_like(st.yc)
+            C().pool3s2_bn_bwd(dy, am, st.yc, st.scale, st.shift, st.mean, coef, dyc)
+            if bn.grad_hook is not None:
+                bn.grad_hook()
+        else:
+            d = torch.empty_like(st.yc)
+            C().maxpool_bwd(dy, am, d, k, k, s, s, p, p)
+            dyc, _ = bn_backward(unit, st, d, False)
         conv = unit.conv
         g = st.g
         with on_grad_stream(dy.device, dyc, xs, default=False):

@@ -285,8 +285,7 @@ def linear_dgrad(dy, w, out=None, resid=None, gelu_pre=None, stats=None, resid_m
     "shift", "mean", "ws"} (mode 2: ReLU recomputed from x): the GEMM's epilogue also accumulates the
     BatchNorm-backward partial sums of the output (``GemmParams.bnr_*``) into ``ws`` and
     ``bnr["done"]`` is set — the consumer BN then skips its reduce sweep.  Where no kernel can
-    (a residual on a non-streaming tile, mode 2 on the streaming kernel, split-K) ``bnr`` is left
-    untouched.  ``rsub = (H, W)``: the rows are an
+    (mode 2 with a residual on the streaming kernel, split-K) ``bnr`` is left untouched.  ``rsub = (H, W)``: the rows are an
     [N][H][W] grid and ``resid`` lives on its stride-2 subgrid (``GemmParams.rsub_h``)."""
     M, N = dy.shape
     K = w.shape[1]
@@ -320,7 +319,7 @@ def linear_dgrad(dy, w, out=None, resid=None, gelu_pre=None, stats=None, resid_m
         if fb:
             bnr["done"] = True
         return out
-    if (bnr is not None and stats is None and "scale" not in bnr
+    if (bnr is not None and stats is None and ("scale" not in bnr or (resid is None and rsub is None))
             and use_stream(M, K, N, KC, RC, EPI_BF16, dy.stride(0), out.stride(0), aux=gelu_pre, relu=act,
                            resid=resid, ldr=ldr)):
         gemm(dy, w, out, M, K, N, KC, RC, dy.stride(0), w.stride(0), out.stride(0), EPI_BF16, resid=resid, ldr=ldr,
@@ -337,9 +336,10 @@ def linear_dgrad(dy, w, out=None, resid=None, gelu_pre=None, stats=None, resid_m
 
 
 def _bnr_plain_ok(bnr, stats, resid, gelu_pre, ncols) -> bool:
-    """The LDS-DMA GEMM's EPI_BF16_BNR epilogue can take this data-gradient's BN-backward reduce."""
-    return (bnr is not None and stats is None and resid is None and gelu_pre is None and ncols % 8 == 0
-            and bnr["x"].is_contiguous())
+    """The LDS-DMA GEMM's EPI_BF16_BNR epilogue can take this data-gradient's BN-backward reduce (a residual
+    included: 8-B aligned rows of 4-element multiples, as its 4-column fragment loads read it)."""
+    return (bnr is not None and stats is None and gelu_pre is None and ncols % 8 == 0 and bnr["x"].is_contiguous()
+            and (resid is None or (resid.stride(0) % 4 == 0 and resid.data_ptr() % 8 == 0)))
 
 
 def transpose(w):

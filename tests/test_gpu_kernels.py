@@ -685,11 +685,14 @@ def test_conv3x3_halo_kernel(N, H, W, Ci, Co, bias_relu, monkeypatch):
     close(y, y2, rtol=1e-2, atol=1e-2, what="halo vs implicit GEMM")
 
 
-@pytest.mark.parametrize("M,N,K,resid", [(16384, 256, 64, True), (20000, 512, 128, True), (16384, 1024, 256, False)])
-def test_stream_dgrad_fused_bn_backward_reduce(M, N, K, resid):
+@pytest.mark.parametrize("M,N,K,resid,mode", [(16384, 256, 64, True, 3), (20000, 512, 128, True, 3),
+                                              (16384, 1024, 256, False, 3), (32768, 64, 256, False, 2),
+                                              (16384, 256, 64, False, 2), (16384, 128, 128, False, 2)])
+def test_stream_dgrad_fused_bn_backward_reduce(M, N, K, resid, mode):
     """linear_dgrad on the streaming kernel with ``bnr``: the output equals the plain launch, and the
     workspace holds sum_m d*relu and sum_m d*relu*(x - mean) of the STORED output (fp64 reference),
-    with relu the mode-3 bit mask — the partial sums bn_bwd_reduce would have produced."""
+    with relu the mode-3 bit mask or (mode 2) x * scale + shift > 0 — the partial sums bn_bwd_reduce
+    would have produced.  (32768, 64, 256): ResNet-50 stage 1's conv3 data-gradient feeding bn2."""
     from distributeddeeplearningspark_amd.ops import gemm as G
     from distributeddeeplearningspark_amd.ops.norm import SHARDS
 
@@ -705,6 +708,11 @@ def test_stream_dgrad_fused_bn_backward_reduce(M, N, K, resid):
     assert G.use_stream(M, N, K, G.KC, G.RC, G.EPI_BF16, K, N, resid=r, ldr=N if resid else 0)
     ws = torch.zeros((SHARDS, 2, N), dtype=torch.float32, device=DEV)
     bnr = {"x": x, "mask": mask, "mean": mean, "ws": ws}
+    if mode == 2:
+        scale = (torch.rand(N, generator=gen) + 0.5).to(DEV)
+        shift = torch.randn(N, generator=gen).to(DEV) * 0.5
+        bnr = {"x": x, "scale": scale, "shift": shift, "mean": mean, "ws": ws}
+        keep = (x.float() * scale + shift > 0).cpu()
     out = G.linear_dgrad(dy, w, resid=r, bnr=bnr)
     assert bnr.get("done")
     ref_out = G.linear_dgrad(dy, w, resid=r)
@@ -816,8 +824,183 @@ def test_bottleneck_inner_fused_bn_reduce_matches_unfused(monkeypatch):
         out.append((float(loss.detach()), m.arena.grad.float().cpu().clone(), n_reduce))
     (l0, g0, r0), (l1, g1, r1), (l0b, g0b, _) = out
     assert r1 <= r0 - 2, (r1, r0)
-    assert_scalar_within_noise(l1, l0, l0b, floor=2e-5)
+    # the loss is the FORWARD's (both variants run the same forward kernels): its spread is the forward's own
+    # BN-statistics noise, amplified by bf16 through the blocks (measured up to 5.6e-3 relative after four
+    # blocks, tests/noise.py) — two reference runs under-sample it, hence the 1e-3 relative floor
+    assert_scalar_within_noise(l1, l0, l0b, floor=1e-3)
     assert_within_noise(g1, g0, g0b, floor=2e-3, what="arena gradients")
+
+
+@pytest.mark.parametrize("N,H,C,Co", [(64, 56, 128, 128), (64, 28, 256, 256), (32, 14, 512, 512)])
+def test_strided_conv_dgrad_fused_bn_backward_reduce(monkeypatch, N, H, C, Co):
+    """3x3 / stride-2 data-gradient (four parity classes scattered through the OutMap) with a mode-2 ``bnr``:
+    every class's EPI_BF16_BNR epilogue adds the partial sums of the pixels it writes — the same dx as
+    without, and the reduce of the whole dx (ResNet-50's stride-2 conv2 feeding bn1)."""
+    from distributeddeeplearningspark_amd.ops import conv as CV
+    from distributeddeeplearningspark_amd.ops.norm import SHARDS
+
+    monkeypatch.setattr(CV, "_STRIDED_BNR", True)  # opt-in path (DDL_STRIDED_BNR=1)
+    g = CV.geometry(N, H, H, C, Co, 3, 3, (2, 2), (1, 1), (1, 1))
+    gen = torch.Generator().manual_seed(H * C + 1)
+    dy = torch.randn(N, g.Ho, g.Wo, Co, generator=gen).to(DEV, torch.bfloat16)
+    w = (torch.randn(Co, 3, 3, C, generator=gen) * 0.05).to(DEV, torch.bfloat16)
+    x = torch.randn(N, H, H, C, generator=gen).to(DEV, torch.bfloat16)
+    mean = torch.randn(C, generator=gen).to(DEV) * 0.1
+    scale = (torch.rand(C, generator=gen) + 0.5).to(DEV)
+    shift = torch.randn(C, generator=gen).to(DEV) * 0.5
+    ws = torch.zeros((SHARDS, 2, C), dtype=torch.float32, device=DEV)
+    bnr = {"x": x, "scale": scale, "shift": shift, "mean": mean, "ws": ws}
+    dx = CV.conv_dgrad_native(dy, w, g, bnr=bnr)
+    assert bnr.get("done")
+    assert torch.equal(dx, CV.conv_dgrad_native(dy, w, g))
+    keep = (x.float() * scale + shift > 0).cpu().reshape(-1, C)
+    s1, s2 = _bnr_reference(dx, x, mean, keep)
+    got = ws.double().cpu().sum(0)
+    close(got[0], s1, rtol=1e-4, atol=1e-2 * s1.abs().mean().item(), what="sum d")
+    close(got[1], s2, rtol=1e-4, atol=1e-2 * s2.abs().mean().item(), what="sum d (x - mean)")
+
+
+@pytest.mark.parametrize("M,N,K,rsub", [(12544, 512, 2048, False), (8192, 256, 1024, True)])
+def test_dma_dgrad_fused_bn_reduce_with_residual(M, N, K, rsub):
+    """linear_dgrad on the LDS-DMA GEMM with a residual AND ``bnr`` (mode 3): the identity shortcut's masked
+    gradient (resid + resid_mask) or the stride-2 shortcut's half-resolution gradient (rsub) added in the
+    EPI_BF16_BNR epilogue — the same output as the full epilogue, and the reduce of the stored sum
+    (ResNet-50 stage 4's conv1 data-gradients and the stage-3 -> 4 boundary)."""
+    from distributeddeeplearningspark_amd.ops import gemm as G
+    from distributeddeeplearningspark_amd.ops.norm import SHARDS
+
+    gen = torch.Generator().manual_seed(M + K)
+    dy = torch.randn(M, N, generator=gen).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, K, generator=gen) / N ** 0.5).to(DEV, torch.bfloat16)
+    x = torch.randn(M, K, generator=gen).to(DEV, torch.bfloat16)
+    mean = torch.randn(K, generator=gen).to(DEV)
+    keep = torch.rand(M, K, generator=gen) > 0.4
+    mbits = (keep.reshape(-1, 8).to(torch.uint8) << torch.arange(8, dtype=torch.uint8)).sum(1, dtype=torch.uint8)
+    if rsub:  # rows = [M / 64][8][8] grid, residual on its [4][4] even subgrid
+        hw = 8
+        r = torch.randn(M // 4, K, generator=gen).to(DEV, torch.bfloat16)
+        kw = dict(resid=r, rsub=(hw, hw))
+    else:
+        r = torch.randn(M, K, generator=gen).to(DEV, torch.bfloat16)
+        rk = torch.rand(M, K, generator=gen) > 0.5
+        rmask = (rk.reshape(-1, 8).to(torch.uint8) << torch.arange(8, dtype=torch.uint8)).sum(1, dtype=torch.uint8)
+        kw = dict(resid=r, resid_mask=rmask.to(DEV))
+    assert not G.use_stream(M, K, N, G.KC, G.RC, G.EPI_BF16, N, K, resid=r, ldr=K)
+    ws = torch.zeros((SHARDS, 2, K), dtype=torch.float32, device=DEV)
+    bnr = {"x": x, "mask": mbits.to(DEV), "mean": mean, "ws": ws}
+    out = G.linear_dgrad(dy, w, bnr=bnr, **kw)
+    assert bnr.get("done")
+    assert torch.equal(out, G.linear_dgrad(dy, w, **kw))
+    s1, s2 = _bnr_reference(out, x, mean, keep)
+    got = ws.double().cpu().sum(0)
+    close(got[0], s1, rtol=1e-4, atol=1e-2 * s1.abs().mean().item(), what="sum d")
+    close(got[1], s2, rtol=1e-4, atol=1e-2 * s2.abs().mean().item(), what="sum d (x - mean)")
+
+
+@pytest.mark.parametrize("N,H,C", [(16, 112, 64), (8, 57, 32)])
+def test_stem_pool_bn_backward_fused(N, H, C):
+    """pool3s2_bn_bwd: the stem BN's reduce and dx sweeps computed through the 3x3 / 2 / pad-1 max pool's
+    gather (pooled gradient + argmax bytes) match maxpool_bwd -> bn_bwd_reduce -> bn_bwd_dx (mode 2) on the
+    materialised pool gradient: partial sums to fp32 rounding, dx to bf16 rounding."""
+    from distributeddeeplearningspark_amd.ops._native import C as NC
+    from distributeddeeplearningspark_amd.ops.norm import partials_workspace
+
+    gen = torch.Generator().manual_seed(N * H + C)
+    x = torch.randn(N, H, H, C, generator=gen).to(DEV, torch.bfloat16)
+    scale = (torch.rand(C, generator=gen) + 0.5).to(DEV)
+    shift = (torch.randn(C, generator=gen) * 0.5).to(DEV)
+    mean = (torch.randn(C, generator=gen) * 0.1).to(DEV)
+    Ho = (H - 1) // 2 + 1
+    y = torch.empty(N, Ho, Ho, C, dtype=torch.bfloat16, device=DEV)
+    am = torch.empty(N, Ho, Ho, C, dtype=torch.uint8, device=DEV)
+    NC().maxpool_fwd(x, y, am, 3, 3, 2, 2, 1, 1, scale, shift)
+    dy = torch.randn(N, Ho, Ho, C, generator=gen).to(DEV, torch.bfloat16)
+    d = torch.empty_like(x)
+    NC().maxpool_bwd(dy, am, d, 3, 3, 2, 2, 1, 1)
+    M = N * H * H
+    ws_ref = partials_workspace(M, C, DEV)
+    NC().bn_bwd_reduce(d, x, None, scale, shift, mean, ws_ref, C, 2)
+    ws = torch.empty((1024, 2, C), dtype=torch.float32, device=DEV)
+    assert NC().pool3s2_bn_bwd_ok(N, H, H, C, Ho, Ho)
+    NC().pool3s2_bn_bwd(dy, am, x, scale, shift, mean, ws, None)
+    ref, got = ws_ref.double().sum(0).cpu(), ws.double().sum(0).cpu()
+    close(got[0], ref[0], rtol=1e-4, atol=1e-4 * ref[0].abs().mean().item(), what="sum d'")
+    close(got[1], ref[1], rtol=1e-4, atol=1e-4 * ref[1].abs().mean().item(), what="sum d' (x - mean)")
+    coef = torch.randn(3 * C, generator=gen).to(DEV)
+    dx_ref = torch.empty_like(x)
+    NC().bn_bwd_dx(d, x, None, scale, shift, coef, dx_ref, None, C, 2)
+    dx = torch.empty_like(x)
+    NC().pool3s2_bn_bwd(dy, am, x, scale, shift, mean, coef, dx)
+    close(dx.float(), dx_ref.float(), rtol=1e-2, atol=1e-2, what="dx")
+
+
+def test_bn_bwd_dx_fused_second_reduce():
+    """bn_bwd_dx_red: the dx sweep of a mode-3 BN (bit mask) also writes the reduce partials of a second
+    BN fed by the masked gradient (ResNet downsample BN): dx equals bn_bwd_dx's, and the partial rows sum
+    to bn_bwd_reduce's result on (dy, x2, mask) — the fp64 reference of sum d, sum d (x2 - mean2)."""
+    from distributeddeeplearningspark_amd.ops._native import C as NC
+    from distributeddeeplearningspark_amd.ops.norm import partials_workspace
+
+    for M, Cc in ((50176, 256), (12544, 2048), (4000, 192)):
+        gen = torch.Generator().manual_seed(M + Cc)
+        dy = torch.randn(M, Cc, generator=gen).to(DEV, torch.bfloat16)
+        x = torch.randn(M, Cc, generator=gen).to(DEV, torch.bfloat16)
+        x2 = torch.randn(M, Cc, generator=gen).to(DEV, torch.bfloat16)
+        keep = torch.rand(M, Cc, generator=gen) > 0.4
+        mask = (keep.reshape(-1, 8).to(torch.uint8) << torch.arange(8, dtype=torch.uint8)).sum(
+            1, dtype=torch.uint8).to(DEV)
+        coef = torch.randn(3 * Cc, generator=gen).to(DEV)
+        mean2 = (torch.randn(Cc, generator=gen) * 0.1).to(DEV)
+        dx_ref = torch.empty_like(dy)
+        dres = torch.empty_like(dy)
+        NC().bn_bwd_dx(dy, x, mask, None, None, coef, dx_ref, dres, Cc, 3)
+        dx = torch.empty_like(dy)
+        ws2 = partials_workspace(M, Cc, DEV)
+        NC().bn_bwd_dx_red(dy, x, mask, None, None, coef, dx, Cc, 3, x2, mean2, ws2)
+        assert torch.equal(dx, dx_ref)
+        s1, s2 = _bnr_reference(dres, x2, mean2, torch.ones(M, Cc, dtype=torch.bool))
+        got = ws2.double().cpu().sum(0)
+        close(got[0], s1, rtol=1e-4, atol=1e-3 * s1.abs().mean().item(), what="sum d")
+        close(got[1], s2, rtol=1e-4, atol=1e-3 * s2.abs().mean().item(), what="sum d (x2 - mean2)")
+
+
+def test_bottleneck_downsample_bn_fused_matches_unfused(monkeypatch):
+    """Downsample blocks: bn3's dx sweep writes the shortcut BN's reduce partials and the shortcut BN reads
+    dout under bn3's mask (no masked-gradient tensor, no reduce sweep for that BN): two fewer reduce sweeps
+    on a two-stage ResNet.  Run in the deterministic mode (fixed-order statistics), so the reference path
+    is bitwise reproducible: the forward loss is identical, and the gradients differ only by the shortcut
+    BN's reduce summation order (partial rows of the dx sweep vs the reduce sweep's), then bf16 rounding."""
+    from noise import rel
+
+    from distributeddeeplearningspark_amd.models.resnet import ResNet
+    from distributeddeeplearningspark_amd.ops import fused_blocks as FB
+    from distributeddeeplearningspark_amd.ops.determinism import deterministic
+
+    torch.manual_seed(6)
+    x = torch.randn(64, 64, 64, 3)
+    y = torch.randint(0, 10, (64,))
+    out = []
+    with deterministic(True):
+        for fuse in (False, True, False):
+            monkeypatch.setattr(FB, "_FUSE_DOWN", fuse)
+            m = ResNet(blocks=(1, 1), input_shape=(64, 64, 3), num_classes=10)
+            m.compile("sgd", "sparse_categorical_crossentropy")
+            m.place(DEV, seed=7)
+            xd, yd = m.to_input(x), m.to_target(y)
+            m.backward_step(xd, yd)
+            from torch.profiler import ProfilerActivity, profile
+
+            torch.cuda.synchronize()
+            with profile(activities=[ProfilerActivity.CUDA]) as prof:
+                loss = m.backward_step(xd, yd)
+                torch.cuda.synchronize()
+            n_reduce = sum(1 for e in prof.events() if "bn_bwd_reduce" in e.name)
+            out.append((float(loss.detach()), m.arena.grad.float().cpu().clone(), n_reduce))
+    (l0, g0, r0), (l1, g1, r1), (l0b, g0b, _) = out
+    assert r1 == r0 - 2, (r1, r0)
+    assert l0 == l0b and torch.equal(g0, g0b)  # the reference is reproducible in this mode
+    assert l1 == l0, (l1, l0)
+    assert rel(g1, g0) < 2e-2, rel(g1, g0)
 
 
 def test_bottleneck_chain_fused_bn_reduce_matches_unfused(monkeypatch):
@@ -851,7 +1034,10 @@ def test_bottleneck_chain_fused_bn_reduce_matches_unfused(monkeypatch):
         out.append((float(loss.detach()), m.arena.grad.float().cpu().clone(), n_reduce))
     (l0, g0, r0), (l1, g1, r1), (l0b, g0b, _) = out
     assert r1 == r0 - 1, (r1, r0)  # block 1's bn3 reduce sweep was absorbed by block 2's conv1 dgrad
-    assert_scalar_within_noise(l1, l0, l0b, floor=2e-5)
+    # the loss is the FORWARD's (both variants run the same forward kernels): its spread is the forward's own
+    # BN-statistics noise, amplified by bf16 through the blocks (measured up to 5.6e-3 relative after four
+    # blocks, tests/noise.py) — two reference runs under-sample it, hence the 1e-3 relative floor
+    assert_scalar_within_noise(l1, l0, l0b, floor=1e-3)
     assert_within_noise(g1, g0, g0b, floor=2e-3, what="arena gradients")
 
 
