@@ -361,6 +361,52 @@ constexpr bool epi_dt(int epi) {
 template <int RN>
 constexpr int row_epi_bytes() { return 16 * (RN * 16 + 4) * 4; }
 
+// Per-column statistics of a wave's D^T fragments (lane: row lane & 15 of 16, columns nb + 16 j + 4 (lane >> 4)
+// + e) summed over the 16 rows and added to st[0][n] / st[N][n] (s1 / s2).  A butterfly reduce-scatter:
+// at each of the four xor levels a lane keeps one half of its values and trades the other half with its
+// partner (NV/2 + NV/4 + NV/8 + NV/16 shuffles instead of 4 NV), leaving every lane NV/16 DIFFERENT column
+// totals — so the adds go out as NV/16 whole-wave atomic instructions (64 lanes each) instead of NV/2
+// instructions with 4 lanes active: the atomic issue rate (~50 ns per wave-instruction per CU) was the
+// epilogue's bottleneck (a BN-reducing epilogue made a short GEMM 39 -> 71 us).
+template <int H, int NV>
+__device__ __forceinline__ void bfly_level(float (&v)[NV], const int mrow) {
+  constexpr int M = (H * 16) / NV;  // xor mask of this level: 8, 4, 2, 1
+  const bool up = (mrow & M) != 0;
+#pragma unroll
+  for (int i = 0; i < H; ++i) {
+    const float send = up ? v[i] : v[i + H];
+    const float keep = up ? v[i + H] : v[i];
+    v[i] = keep + __shfl_xor(send, M, 64);
+  }
+}
+template <int RN>
+__device__ __forceinline__ void col_stats_atomics(const float (&s1)[RN][4], const float (&s2)[RN][4], float* st,
+                                                  const int N, const int nb, const int lane) {
+  constexpr int RP = RN < 4 ? 4 : RN;  // column groups padded so every lane ends with >= 2 values
+  constexpr int NV = 8 * RP;
+  float v[NV];
+#pragma unroll
+  for (int j = 0; j < RP; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[4 * j + e] = j < RN ? s1[j < RN ? j : 0][e] : 0.f;
+      v[NV / 2 + 4 * j + e] = j < RN ? s2[j < RN ? j : 0][e] : 0.f;
+    }
+  const int mrow = lane & 15;
+  bfly_level<NV / 2, NV>(v, mrow);
+  bfly_level<NV / 4, NV>(v, mrow);
+  bfly_level<NV / 8, NV>(v, mrow);
+  bfly_level<NV / 16, NV>(v, mrow);
+  constexpr int PL = NV / 16;  // lane mrow now holds original values PL * mrow .. PL * mrow + PL - 1
+#pragma unroll
+  for (int q = 0; q < PL; ++q) {
+    const int idx = PL * mrow + q;
+    const int stt = idx / (NV / 2), rem = idx - stt * (NV / 2), j = rem >> 2, e = rem & 3;
+    const int n = nb + 16 * j + 4 * (lane >> 4) + e;
+    if (j < RN && n < N) atomicAdd(st + (long)stt * N + n, v[q]);
+  }
+}
+
 // EPI_BF16_BNR: bf16 store of alpha*acc (+ the residual: optional ReLU bit mask / stride-2 subgrid, as the
 // full epilogue adds it) + the BatchNorm-backward partial sums of the stored gradient (GemmParams::bnr_*),
 // accumulated like the forward statistics (16-lane shuffle, one atomic per column and shard).  Output rows
@@ -373,6 +419,11 @@ __device__ __forceinline__ void gemm_epilogue_bnr(const GemmParams& p, f32x4 (&a
   const int ncol = 4 * (lane >> 4);
   const bf16_t* X = reinterpret_cast<const bf16_t*>(p.bnr_x);
   float* st = p.stats + (long)(bid % kStatShards) * 2 * p.N;
+  float s1[RN][4], s2[RN][4];
+#pragma unroll
+  for (int j = 0; j < RN; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s1[j][e] = s2[j][e] = 0.f;
   // per-row destination and residual row offsets, once per row (the loops below are column-outer; the
   // OutMap / stride-2 subgrid decompositions are two integer divisions each)
   long rowoff[RM], resoff[RM];
@@ -413,7 +464,6 @@ __device__ __forceinline__ void gemm_epilogue_bnr(const GemmParams& p, f32x4 (&a
         sh[0] = c.x; sh[1] = c.y; sh[2] = c.z; sh[3] = c.w;
       }
     }
-    float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < RM; ++i) {
       const int m = mb + 16 * i + mrow;
@@ -450,26 +500,14 @@ __device__ __forceinline__ void gemm_epilogue_bnr(const GemmParams& p, f32x4 (&a
         bool keep = (mbits >> e) & 1u;
         if (p.bnr_scale) keep = (x[e] * sc[e] + sh[e]) > 0.f;
         const float d = keep ? bf2f(o[e]) : 0.f;
-        s1[e] += d;
-        s2[e] += d * (x[e] - mu[e]);
+        s1[j][e] += d;
+        s2[j][e] += d * (x[e] - mu[e]);
       }
       *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.c) + off) =
           make_uint2((uint32_t)o[0] | ((uint32_t)o[1] << 16), (uint32_t)o[2] | ((uint32_t)o[3] << 16));
     }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float a = s1[e], b = s2[e];
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        a += __shfl_xor(a, o, 64);
-        b += __shfl_xor(b, o, 64);
-      }
-      if (mrow == 0 && nok) {
-        atomicAdd(st + n + e, a);
-        atomicAdd(st + p.N + n + e, b);
-      }
-    }
   }
+  col_stats_atomics<RN>(s1, s2, st, p.N, nb, lane);
 }
 
 // normalise-on-load of a fragment whose 8 values share one channel (row-contiguous B operand)
@@ -929,26 +967,8 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
     }
   }
   if constexpr (BF) {
-    if (p.stats) {  // reduce over the 16 rows held by lanes sharing (lane>>4), then one atomic per column
-      float* st = p.stats + (long)(bid % kStatShards) * 2 * p.N;
-#pragma unroll
-      for (int j = 0; j < RN; ++j) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float a = s1[j][e], b = s2[j][e];
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) {
-            a += __shfl_xor(a, o, 64);
-            b += __shfl_xor(b, o, 64);
-          }
-          const int n = nb + 16 * j + ncol + e;
-          if (mrow == 0 && n < p.N) {
-            atomicAdd(st + n, a);
-            atomicAdd(st + p.N + n, b);
-          }
-        }
-      }
-    }
+    if (p.stats)  // reduce over the 16 rows held by lanes sharing (lane>>4), whole-wave atomics
+      col_stats_atomics<RN>(s1, s2, p.stats + (long)(bid % kStatShards) * 2 * p.N, p.N, nb, lane);
   }
 }
 

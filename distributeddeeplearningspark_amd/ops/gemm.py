@@ -77,6 +77,25 @@ def use_stream(M, N, K, a_mode, b_mode, epi, lda, ldc, *, outmap=None, aux=None,
     return True
 
 
+def bnr_stream_panels(N: int, K: int, resid: bool) -> int:
+    """Panels (re-reads of A) the streaming kernel takes for an (N, K) data-gradient WITH the fused BN reduce:
+    gemm_stream.hip narrows the panel to 128 columns (64 at K = 256) for those variants."""
+    nb = stream_panel(N, K)
+    if not nb:
+        return 0
+    if resid and K == 128 and nb == 256:
+        nb = 128
+    nb = min(nb, 64 if K >= 256 else 128)
+    return N // nb
+
+
+# a BN-reducing data-gradient goes to the LDS-DMA GEMM (EPI_BF16_BNR, residual included) instead of the
+# streaming kernel when the latter would re-read A over more panels than this.  Measured: the streaming
+# kernel wins even at 16 panels (ResNet-50 stage 3's conv1 data-gradient): 12,000-12,075 img/s vs
+# 11,767-11,812 (limit 4) and 11,469-11,485 (limit 2), interleaved (profiles/r4/fuse_bn/ab_bnr_panels.txt)
+_BNR_STREAM_MAX_PANELS = int(_os.environ.get("DDL_BNR_STREAM_MAX_PANELS", "1000"))
+
+
 def use_tile256(M: int, N: int, K: int, a_mode: int, b_mode: int, epi: int) -> bool:
     """The 256x256 kernel pays off when its tiles (times split-K for fp32 outputs) fill the chip."""
     if _USE256 == "0" or a_mode > RC or b_mode > RC or K % 64 or M < 128 or N < 128:
@@ -308,14 +327,18 @@ def linear_dgrad(dy, w, out=None, resid=None, gelu_pre=None, stats=None, resid_m
         else:
             C().splitk_finalize(ws, out, K, None, False, stats)
         return out
-    if M >= _WT_MIN_M and not use_stream(M, K, N, KC, RC, EPI_BF16, dy.stride(0), out.stride(0), aux=gelu_pre,
-                                          relu=act, resid=resid, ldr=ldr):
+    bnr_wide = (bnr is not None and stats is None
+                and bnr_stream_panels(K, N, resid is not None) > _BNR_STREAM_MAX_PANELS
+                and _bnr_plain_ok(bnr, stats, resid, gelu_pre, K))
+    if M >= _WT_MIN_M and (bnr_wide or not use_stream(M, K, N, KC, RC, EPI_BF16, dy.stride(0), out.stride(0),
+                                                       aux=gelu_pre, relu=act, resid=resid, ldr=ldr)):
         # transpose the (small) weight once so the GEMM reads B K-contiguous with ds_read_b128 instead
         # of paired transposed LDS reads: the BERT-size data-gradients run ~1.4x faster this way
         wt = transpose(w)
         fb = _bnr_plain_ok(bnr, stats, resid, gelu_pre, K)
         gemm(dy, wt, out, M, K, N, KC, KC, dy.stride(0), wt.stride(0), out.stride(0), EPI_BF16, resid=resid,
-             ldr=ldr, relu=act, aux=gelu_pre, stats=stats, resid_mask=resid_mask, rsub=rsub, bnr=bnr if fb else None)
+             ldr=ldr, relu=act, aux=gelu_pre, stats=stats, resid_mask=resid_mask, rsub=rsub, bnr=bnr if fb else None,
+             tile=choose_tile(M, K) if bnr_wide else None)  # (not the streaming kernel: see bnr_wide)
         if fb:
             bnr["done"] = True
         return out
