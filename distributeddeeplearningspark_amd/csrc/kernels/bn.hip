@@ -380,11 +380,25 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint4* __restrict__
   }
 }
 
+// workgroup cap of a streaming sweep (DDL_BN_GRID: A/B knob).  Default: no cap — one workgroup per 2 x RT rows,
+// every lane's loads issued at once and never a second grid-stride trip.  The former 4,096-workgroup cap
+// (grid-stride loops) measured slower at every value: ResNet-50 11,914-11,928 (4,096) -> 12,018-12,049 (8,192)
+// -> 12,106-12,144 (16,384) -> 12,166-12,195 (32,768) -> 12,203-12,217 img/s (65,536 = uncapped at ResNet-50's
+// shapes), interleaved (profiles/r4/fuse_bn/ab_bn_grid.txt)
+static long bn_grid_cap() {
+  static const long cap = [] {
+    const char* e = getenv("DDL_BN_GRID");
+    const long v = e ? atol(e) : (1L << 24);
+    return v >= 256 && v <= (1L << 24) ? v : (1L << 24);
+  }();
+  return cap;
+}
+
 static dim3 stream_grid(long M, int C, int rows = 2) {
   const int CV = C >> 3, CT = CV < 256 ? CV : 256, RT = 256 / CT;
   const int gy = (CV + CT - 1) / CT;
   long gx = (M + rows * RT - 1) / (rows * RT);
-  const long cap = 4096 / gy > 1 ? 4096 / gy : 1;
+  const long cap = bn_grid_cap() / gy > 1 ? bn_grid_cap() / gy : 1;
   if (gx > cap) gx = cap;
   return dim3((unsigned)(gx > 0 ? gx : 1), (unsigned)gy);
 }
@@ -749,8 +763,7 @@ int pool3s2_bn_bwd(const void* dy, const uint8_t* am, const void* x, const float
   const int CV = C / 8, CT = CV, RT = 256 / CT;
   const long nq = (long)N * ((H + 1) / 2) * ((W + 1) / 2);
   if (dx) {
-    long gx = (nq + RT - 1) / RT;
-    if (gx > 4096) gx = 4096;
+    const long gx = (nq + RT - 1) / RT;  // one 2 x 2 block per lane, no grid-stride trips (see bn_grid_cap)
     hipLaunchKernelGGL(pool3s2_bn_bwd_kernel<true>, dim3((unsigned)gx), dim3(256), 0, s, (const uint4*)dy,
                        (const uint2*)am, (const uint4*)x, scale, shift, mean, coef, ws, (uint4*)dx, N, H, W, Ho, Wo, C);
   } else {  // one partial row per block: S blocks (the caller's workspace rows; more than a reduce sweep's 512:
