@@ -4,6 +4,7 @@
 // (uint8 NHWC images -> bf16, channel padded) that runs right after the H2D copy.
 #include "ddl_common.h"
 #include "ddl_ops.h"
+#include <stdlib.h>
 
 namespace ddl {
 
@@ -12,9 +13,18 @@ static int g_deterministic = 0;
 void set_deterministic(int on) { g_deterministic = on ? 1 : 0; }
 int deterministic() { return g_deterministic; }
 
+// one element group per lane (DDL_MISC_GRID caps the workgroups for A/B; the former cap was 8,192)
+static long misc_grid_cap() {
+  static const long cap = [] {
+    const char* e = getenv("DDL_MISC_GRID");
+    const long v = e ? atol(e) : (1L << 24);
+    return v >= 256 ? v : (1L << 24);
+  }();
+  return cap;
+}
 static unsigned mgrid(long n) {
   long g = (n + 255) / 256;
-  if (g > 8192) g = 8192;
+  if (g > misc_grid_cap()) g = misc_grid_cap();
   return (unsigned)(g > 0 ? g : 1);
 }
 
@@ -210,7 +220,7 @@ int slab_reduce(const float* ws, int splits, float* c, long M, int N, long ldc, 
   const int vec = (N % 4 == 0 && ldc % 4 == 0 && ((uintptr_t)c & 15) == 0 && ((uintptr_t)ws & 15) == 0) ? 1 : 0;
   long work = vec ? (M * N) >> 2 : M * N;
   long blocks = (work + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
+  if (blocks > misc_grid_cap()) blocks = misc_grid_cap();
   hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)(blocks > 0 ? blocks : 1)), dim3(256), 0, s, ws, splits, c, M, N,
                      ldc, beta, vec);
   return (int)hipGetLastError();

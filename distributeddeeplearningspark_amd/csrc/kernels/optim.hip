@@ -5,12 +5,20 @@
 // into the update instead of a separate pass over the gradients.
 #include "ddl_common.h"
 #include "ddl_ops.h"
+#include <stdlib.h>
 
 namespace ddl {
 
+// one float4 per lane, no grid-stride trips (DDL_OPT_GRID caps the workgroups for A/B; the former cap was 4,096:
+// see bn.hip bn_grid_cap for the measured cost of grid-stride sweeps)
 static unsigned ogrid(long n4) {
+  static const long cap = [] {
+    const char* e = getenv("DDL_OPT_GRID");
+    const long v = e ? atol(e) : (1L << 24);
+    return v >= 256 ? v : (1L << 24);
+  }();
   long g = (n4 + 255) / 256;
-  if (g > 4096) g = 4096;
+  if (g > cap) g = cap;
   return (unsigned)(g > 0 ? g : 1);
 }
 
