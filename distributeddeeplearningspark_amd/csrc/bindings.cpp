@@ -59,8 +59,7 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
           c10::optional<at::Tensor> resid_mask, c10::optional<at::Tensor> bnr_x, c10::optional<at::Tensor> bnr_mask,
           c10::optional<at::Tensor> bnr_mean, int64_t rsub_h, int64_t rsub_w, c10::optional<at::Tensor> a_scale,
           c10::optional<at::Tensor> a_shift, c10::optional<at::Tensor> b_scale, c10::optional<at::Tensor> b_shift,
-          c10::optional<at::Tensor> bnr_scale, c10::optional<at::Tensor> bnr_shift, int64_t split_stride,
-          c10::optional<py::dict> fin) {
+          c10::optional<at::Tensor> bnr_scale, c10::optional<at::Tensor> bnr_shift, int64_t split_stride) {
   CHECK_CUDA(a);
   CHECK_CUDA(b);
   CHECK_CUDA(c);
@@ -250,37 +249,6 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
                 "gemm: split-K slabs need EPI_F32, beta = 0 and a workspace of splits x split_stride floats");
     p.split_stride = split_stride;
   }
-  if (fin) {  // fused BN finalize of the statistics (GemmParams::fin_*): counter, gamma, beta, rmean, rvar, mean,
-              // invstd, scale, shift (fp32 [N]; gamma / beta / rmean / rvar may be None), eps, momentum, M
-    TORCH_CHECK(stats.has_value() && epi == EPI_BF16, "gemm: fin needs the statistics workspace and a bf16 epilogue");
-    const py::dict& f = *fin;
-    auto ten = [&](const char* k, bool required) -> float* {
-      if (!f.contains(k) || f[k].is_none()) {
-        TORCH_CHECK(!required, "gemm fin: missing ", k);
-        return nullptr;
-      }
-      at::Tensor t = f[k].cast<at::Tensor>();
-      CHECK_CUDA(t);
-      CHECK_F32(t);
-      TORCH_CHECK(t.is_contiguous() && t.numel() >= N, "gemm fin: ", k, " must be fp32 [N]");
-      return t.data_ptr<float>();
-    };
-    at::Tensor cnt = f["counter"].cast<at::Tensor>();
-    CHECK_CUDA(cnt);
-    TORCH_CHECK(cnt.scalar_type() == at::kInt && cnt.numel() >= 1, "gemm fin: counter must be int32 (zeroed once)");
-    p.fin_counter = reinterpret_cast<unsigned*>(cnt.data_ptr<int>());
-    p.fin_gamma = ten("gamma", false);
-    p.fin_beta = ten("beta", false);
-    p.fin_rmean = ten("rmean", false);
-    p.fin_rvar = ten("rvar", false);
-    p.fin_mean = ten("mean", true);
-    p.fin_invstd = ten("invstd", true);
-    p.fin_scale = ten("scale", true);
-    p.fin_shift = ten("shift", true);
-    p.fin_eps = f["eps"].cast<float>();
-    p.fin_momentum = f["momentum"].cast<float>();
-    p.fin_M = f["M"].cast<long>();
-  }
   at::DeviceGuard guard(a.device());
   HIP_OK(launch_gemm_bf16(p, (int)epi, (int)tile, cur_stream()));
 }
@@ -348,7 +316,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("bnr_mean") = py::none(), py::arg("rsub_h") = 0, py::arg("rsub_w") = 0,
         py::arg("a_scale") = py::none(), py::arg("a_shift") = py::none(), py::arg("b_scale") = py::none(),
         py::arg("b_shift") = py::none(), py::arg("bnr_scale") = py::none(), py::arg("bnr_shift") = py::none(),
-        py::arg("split_stride") = 0, py::arg("fin") = py::none());
+        py::arg("split_stride") = 0);
   m.def("conv3x3_wgrad", &conv3x3_wgrad, "3x3 stride-1 weight gradient (halo kernel): gw += dW", py::arg("dy"),
         py::arg("x"), py::arg("gw"), py::arg("ws"), py::arg("splits"), py::arg("tpb"), py::arg("pp") = false);
   m.def("conv3x3_wgrad_plan", &conv3x3_wgrad_plan_py,

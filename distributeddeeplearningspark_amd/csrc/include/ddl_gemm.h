@@ -134,21 +134,6 @@ struct GemmParams {
   // c + s * split_stride (elements, ldc unchanged); a reduce pass sums the slabs in split order
   // (slab_reduce: deterministic, and ~4x the store rate of the fp32 atomics it replaces).  0 = off.
   long split_stride;
-  // fused BatchNorm finalize of the statistics this GEMM accumulates into ``stats``: the workgroup that finishes
-  // last (device-scope counter, reset by that workgroup) sums the kStatShards shards and writes what bn_finalize
-  // writes (mean, inverse std, scale / shift, running statistics) — no separate finalize launch.  The dispatcher
-  // (launch_gemm_bf16) keeps it only for kernels that run the tail and launches bn_finalize otherwise.
-  unsigned* fin_counter;  // null: off
-  const float* fin_gamma;
-  const float* fin_beta;
-  float* fin_rmean;
-  float* fin_rvar;
-  float* fin_mean;
-  float* fin_invstd;
-  float* fin_scale;
-  float* fin_shift;
-  float fin_eps, fin_momentum;
-  long fin_M;
 };
 
 enum Activation : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_GELU_BWD = 3 };

@@ -510,52 +510,6 @@ __device__ __forceinline__ void gemm_epilogue_bnr(const GemmParams& p, f32x4 (&a
   col_stats_atomics<RN>(s1, s2, st, p.N, nb, lane);
 }
 
-// GemmParams::fin_counter: the fused BatchNorm finalize.  Every workgroup calls this once, after its
-// statistics atomics; the last one to arrive sums the shards and writes bn_finalize's outputs, then rearms the
-// counter for the next launch (graph replay included).  No __threadfence: an agent-scope release writes the
-// XCD's L2 back (measured: every workgroup fencing cost ResNet-50 a third of its throughput).  The statistics
-// are device-scope atomics, performed at the coherence point once the issuing wave's vmcnt drains; the
-// counter add and the shard loads are device-scope atomics too, so the last arrival reads every shard's sum.
-__device__ __forceinline__ void bn_finalize_tail(const GemmParams& p) {
-  __shared__ unsigned fin_last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's statistics atomics have been performed
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned total = gridDim.x * gridDim.y * gridDim.z;
-    fin_last = __hip_atomic_fetch_add(p.fin_counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1
-                   ? 1u : 0u;
-  }
-  __syncthreads();
-  if (!fin_last) return;
-  const int N = p.N;
-  for (int c = threadIdx.x; c < N; c += blockDim.x) {
-    double s1 = 0.0, s2 = 0.0;
-#pragma unroll 4
-    for (int sh = 0; sh < kStatShards; ++sh) {
-      s1 += (double)__hip_atomic_load(p.stats + (long)sh * 2 * N + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s2 += (double)__hip_atomic_load(p.stats + (long)sh * 2 * N + N + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    const long M = p.fin_M;
-    const double mean = s1 / (double)M;
-    double var = s2 / (double)M - mean * mean;
-    if (var < 0) var = 0;
-    const float inv = (float)(1.0 / sqrt(var + (double)p.fin_eps));
-    const float g = p.fin_gamma ? p.fin_gamma[c] : 1.f;
-    const float b = p.fin_beta ? p.fin_beta[c] : 0.f;
-    const float mom = p.fin_momentum;
-    if (p.fin_mean) p.fin_mean[c] = (float)mean;
-    if (p.fin_invstd) p.fin_invstd[c] = inv;
-    p.fin_scale[c] = g * inv;
-    p.fin_shift[c] = b - (float)mean * g * inv;
-    if (p.fin_rmean) p.fin_rmean[c] = (1.f - mom) * p.fin_rmean[c] + mom * (float)mean;
-    if (p.fin_rvar) {
-      const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
-      p.fin_rvar[c] = (1.f - mom) * p.fin_rvar[c] + mom * (float)unb;
-    }
-  }
-  if (threadIdx.x == 0) __hip_atomic_store(p.fin_counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // normalise-on-load of a fragment whose 8 values share one channel (row-contiguous B operand)
 __device__ __forceinline__ bf16x8 norm_frag(const bf16x8 f, float sc, float sh) {
   const s16x8 v = __builtin_bit_cast(s16x8, f);
@@ -1240,9 +1194,6 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
     if constexpr (EPI == EPI_BF16_ROW) __syncthreads();  // the ring slots become the staging area
     gemm_epilogue<RM, RN, EPI>(p, acc, m0 + wm0, n0 + wn0, lane, bid, -1,
                                reinterpret_cast<float*>(smem + wid * row_epi_bytes<RN>()), (long)split * p.split_stride);
-    if constexpr (epi_dt(EPI)) {
-      if (p.fin_counter) bn_finalize_tail(p);
-    }
     return;
   }
   if (nk > 0) {
@@ -1295,9 +1246,6 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
   // (ST 1 / 2: the loop's closing barrier already freed the stages for the row epilogue's staging area)
   gemm_epilogue<RM, RN, EPI>(p, acc, m0 + wm0, n0 + wn0, lane, bid, -1,
                              reinterpret_cast<float*>(smem + wid * row_epi_bytes<RN>()), (long)split * p.split_stride);
-  if constexpr (epi_dt(EPI)) {
-    if (p.fin_counter) bn_finalize_tail(p);
-  }
 }
 
 // DDL_GEMM_DMA: 0 = register-staged kernel, 1 = LDS-DMA single stage (default), 2 = LDS-DMA double stage

@@ -170,9 +170,6 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv3x3_halo_kernel(const GemmPar
   }
 
   gemm_epilogue<FR, RN, EPI>(p, acc, m0 + wm * (16 * FR), n0 + wn0, lane, bid, mend);
-  if constexpr (EPI != EPI_BF16_BNR) {
-    if (p.fin_counter) bn_finalize_tail(p);  // fused BN finalize (GemmParams::fin_counter)
-  }
 }
 
 // max_px: pixels per tile (256 for the forward / data-gradient kernels; 224 for the weight gradient, whose
@@ -994,12 +991,6 @@ bool conv3x3_halo_ok(const GemmParams& p) {
   return t.rows > 0 && t.P >= 64 && t.hr <= C3_MAX_HALO_ROWS && p.M == g.n * g.hi * g.wi;
 }
 
-// the halo launcher would run the resident-filter 64-channel kernel (no fused BN finalize there)
-bool conv3x3_uses_c64(const GemmParams& p) {
-  static const bool c64pp = env_int("DDL_CONV3X3_C64PP", 1) == 1;
-  return conv3x3_halo_ok(p) && c64pp && c64_variant(p, plan(p)) >= 0;
-}
-
 int launch_conv3x3(const GemmParams& p, int epi, hipStream_t s) {
   if (!conv3x3_halo_ok(p) || epi != EPI_BF16) return (int)hipErrorInvalidValue;
   const Conv3Tiling t = plan(p);
@@ -1012,10 +1003,8 @@ int launch_conv3x3(const GemmParams& p, int epi, hipStream_t s) {
   const bool bn128 = p.N % 128 == 0 && (force_bn ? force_bn == 128 : (long)tiles_px * (p.N / 128) >= 2L * 256);
   static const int nb128 = env_int("DDL_CONV3X3_NB", 2);  // 3: third weight slot (1 workgroup per CU)
   static const bool c64pp = env_int("DDL_CONV3X3_C64PP", 1) == 1;
-  if (c64pp && c64_variant(p, t) >= 0) {
-    if (p.fin_counter) return (int)hipErrorInvalidValue;  // no finalize tail there (the dispatcher routes it away)
+  if (c64pp && c64_variant(p, t) >= 0)
     return p.bnr_x ? launch_c64<EPI_BF16_BNR>(p, t, s) : launch_c64<EPI_BF16_LITE>(p, t, s);
-  }
   if (p.bnr_x) return bn128 ? launch<128, EPI_BF16_BNR, 2>(p, t, s) : launch<64, EPI_BF16_BNR, 3>(p, t, s);
   if (bn128) return nb128 == 3 ? launch<128, EPI_BF16_LITE, 3>(p, t, s) : launch<128, EPI_BF16_LITE, 2>(p, t, s);
   return launch<64, EPI_BF16_LITE, 3>(p, t, s);

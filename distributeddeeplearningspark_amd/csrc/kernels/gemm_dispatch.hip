@@ -1,10 +1,8 @@
 // Host-side dispatch of the implicit-GEMM kernel family.
 #include "ddl_gemm.h"
-#include "ddl_ops.h"
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 namespace ddl {
-bool conv3x3_uses_c64(const GemmParams& p);
 int launch_gemm_plain_akc(const GemmParams& p, int epi, int tile, hipStream_t s);
 int launch_gemm_plain_arc(const GemmParams& p, int epi, int tile, hipStream_t s);
 int launch_gemm_conv(const GemmParams& p, int epi, int tile, hipStream_t s);
@@ -13,35 +11,8 @@ int launch_gemm_w4(const GemmParams& p, int epi, int tile, hipStream_t s);
 int launch_gemm_stream(const GemmParams& p, int epi, hipStream_t s);
 int launch_conv3x3(const GemmParams& p, int epi, hipStream_t s);
 
-static int launch_gemm_bf16_impl(const GemmParams& p_in, int epi, int tile, hipStream_t s);
-
-// GemmParams::fin_counter (fused BN finalize): kept for the kernels that run bn_finalize_tail — the LDS-DMA GEMM
-// (DDL_GEMM_DMA != 0), the halo conv (not its resident-filter 64-channel variant) and the streaming kernel, all
-// with a bf16 statistics epilogue and no split-K; every other launch runs bn_finalize after the GEMM instead.
-static bool fin_tail_ok(const GemmParams& p, int epi, int tile) {
-  if (!p.stats || p.bnr_x || epi != EPI_BF16 || p.k_split < p.K) return false;
-  if (tile == kTileStream) return true;
-  if (tile == kTileConv3) return !conv3x3_uses_c64(p);
-  if (tile == kTile256 || tile == kTile256P || tile == kTileW4 || tile == kTileW4N) return false;
-  const char* e = getenv("DDL_GEMM_DMA");
-  return !(e && atoi(e) == 0);
-}
-
 int launch_gemm_bf16(const GemmParams& p_in, int epi, int tile, void* stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (!p_in.fin_counter) return launch_gemm_bf16_impl(p_in, epi, tile, s);
-  if (p_in.M <= 0 || p_in.N <= 0) return 0;
-  if (fin_tail_ok(p_in, epi, tile)) return launch_gemm_bf16_impl(p_in, epi, tile, s);
-  GemmParams q = p_in;
-  q.fin_counter = nullptr;
-  const int rc = launch_gemm_bf16_impl(q, epi, tile, s);
-  if (rc) return rc;
-  return bn_finalize(p_in.stats, kStatShards, p_in.fin_M, p_in.N, p_in.fin_gamma, p_in.fin_beta, p_in.fin_eps,
-                     p_in.fin_momentum, p_in.fin_rmean, p_in.fin_rvar, p_in.fin_mean, p_in.fin_invstd, p_in.fin_scale,
-                     p_in.fin_shift, s);
-}
-
-static int launch_gemm_bf16_impl(const GemmParams& p_in, int epi, int tile, hipStream_t s) {
   if (p_in.M <= 0 || p_in.N <= 0) return 0;
   // DDL_GEMM_GROUP_M: grouped tile raster (GemmParams::group_m; 0 = row-major).  8 measured +1-2 % on
   // BERT-base (835K vs 817-824K tok/s), ResNet-50 neutral; 128-tile GEMM 8192^3 810 -> 1089 TF/s

@@ -382,9 +382,6 @@ __global__ __launch_bounds__(gst::THREADS, 2) void gemm_stream_kernel(const Gemm
       atomicAdd(st + p.N + n0 + t, b);
     }
   }
-  if constexpr (BNR == 0) {
-    if (p.fin_counter) bn_finalize_tail(p);  // fused BN finalize (GemmParams::fin_counter)
-  }
 }
 
 namespace {

@@ -171,24 +171,17 @@ def splitk_fwd_ok(g: ConvGeometry) -> bool:
     return math.ceil(g.M / 64) * math.ceil(g.Co / 64) <= _SPLITK_MAX_TILES
 
 
-def conv_fwd_native(x, w, g: ConvGeometry, bias=None, relu=False, stats=None, x_norm=None, bnr=None, fin=None):
+def conv_fwd_native(x, w, g: ConvGeometry, bias=None, relu=False, stats=None, x_norm=None, bnr=None):
     """``x_norm = (scale, shift)``: x is pre-BatchNorm and normalised on load (pointwise convs on the
     streaming kernel: :func:`norm_on_load_ok`).  ``bnr``: fused BN-backward reduce of the output (a
     stride-1 data-gradient run as a forward conv; see ``gemm.linear_dgrad``) — applied on the halo and
-    gathered implicit-GEMM paths, which then set ``bnr["done"]``.  ``fin``: fused BatchNorm finalize of ``stats``
-    (``GemmParams.fin_*``, see ``fused_blocks._bn_forward``); ``fin["done"]`` is set when the GEMM launch took it
-    (the native dispatcher runs either the kernel tail or bn_finalize), left unset on the split-K path."""
+    gathered implicit-GEMM paths, which then set ``bnr["done"]``."""
     y = torch.empty((g.N, g.Ho, g.Wo, g.Co), dtype=torch.bfloat16, device=x.device)
     y2 = y.view(g.M, g.Co)
-    if fin is not None and stats is None:
-        fin = None
     if x_norm is not None:
         if not norm_on_load_ok(g):
             raise ValueError("conv_fwd_native: normalise-on-load not supported for this geometry")
-        G.linear_fwd(x.view(g.M, g.Ci), w.view(g.Co, g.Ci), bias=bias, relu=relu, out=y2, stats=stats, x_norm=x_norm,
-                     fin=fin)
-        if fin is not None:
-            fin["done"] = True
+        G.linear_fwd(x.view(g.M, g.Ci), w.view(g.Co, g.Ci), bias=bias, relu=relu, out=y2, stats=stats, x_norm=x_norm)
         return y
     if splitk_fwd_ok(g):
         ws = G.splitk_workspace(g.M, g.Co, x.device)
@@ -204,25 +197,21 @@ def conv_fwd_native(x, w, g: ConvGeometry, bias=None, relu=False, stats=None, x_
         return y
     fb = (bnr is not None and bias is None and not relu and stats is None and g.Co % 8 == 0
           and bnr["x"].is_contiguous() and not g.is_pointwise and (halo3_ok(g) or g.implicit_fwd))
-    if fb:
-        fin = None  # (a data-gradient with a BN reduce: no forward statistics)
     if halo3_ok(g):
         G.gemm(x, w, y2, g.M, g.Co, g.T * g.Ci, G.KC_GATHER, G.KC, 0, g.T * g.Ci, g.Co, G.EPI_BF16, bias=bias,
-               relu=relu, geom=g.fwd_geom, stats=stats, tile=G.TILE_CONV3, bnr=bnr if fb else None, fin=fin)
+               relu=relu, geom=g.fwd_geom, stats=stats, tile=G.TILE_CONV3, bnr=bnr if fb else None)
     elif g.is_pointwise:
-        G.linear_fwd(x.view(g.M, g.Ci), w.view(g.Co, g.Ci), bias=bias, relu=relu, out=y2, stats=stats, fin=fin)
+        G.linear_fwd(x.view(g.M, g.Ci), w.view(g.Co, g.Ci), bias=bias, relu=relu, out=y2, stats=stats)
     elif g.implicit_fwd or g.gather8_fwd:
         G.gemm(x, w, y2, g.M, g.Co, g.T * g.Ci, G.KC_GATHER if g.implicit_fwd else G.KC_GATHER8, G.KC, 0,
                g.T * g.Ci, g.Co, G.EPI_BF16, bias=bias, relu=relu, geom=g.fwd_geom, stats=stats,
-               bnr=bnr if fb else None, fin=fin)
+               bnr=bnr if fb else None)
     else:
         col = _im2col(x, g, g.taps_h, g.taps_w, g.Ho, g.Wo, g.sh, g.sw, g.kpad)
         w2 = w.reshape(g.Co, g.T * g.Ci)
         if g.kpad != g.T * g.Ci:
             w2 = F.pad(w2, (0, g.kpad - g.T * g.Ci))
-        G.linear_fwd(col, w2.contiguous(), bias=bias, relu=relu, out=y2, stats=stats, fin=fin)
-    if fin is not None:
-        fin["done"] = True
+        G.linear_fwd(col, w2.contiguous(), bias=bias, relu=relu, out=y2, stats=stats)
     if fb:
         bnr["done"] = True
     return y

@@ -63,43 +63,23 @@ def _producer_of(x):
     return None if st is None else (e[1], st)
 
 
-def _fin_request(layer_bn, Cc, M, device):
-    """Fused-finalize request for the conv GEMM producing this BN's input (``GemmParams.fin_*``): the GEMM's last
-    workgroup turns the statistics into scale / shift / mean / inverse std (+ running statistics) — no separate
-    bn_finalize launch.  The per-BN arrival counter is zeroed once and re-armed by the kernel."""
-    bn = layer_bn
-    key = ("_fin_counter", str(device))
-    cnt = bn.__dict__.get(key)
-    if cnt is None:
-        cnt = bn.__dict__[key] = torch.zeros(1, dtype=torch.int32, device=device)
-    scale, shift, mean, invstd = torch.empty(4, Cc, dtype=torch.float32, device=device).unbind(0)
-    return {"counter": cnt, "gamma": None if bn.gamma is None else bn.gamma.master,
-            "beta": None if bn.beta is None else bn.beta.master, "rmean": bn._states["moving_mean"],
-            "rvar": bn._states["moving_variance"], "mean": mean, "invstd": invstd, "scale": scale, "shift": shift,
-            "eps": float(bn.epsilon), "momentum": float(1.0 - bn.momentum), "M": int(M)}
-
-
-def _bn_forward(layer_bn, yc, stats, resid, relu, training, mask=None, apply=True, res_affine=None, fin=None):
+def _bn_forward(layer_bn, yc, stats, resid, relu, training, mask=None, apply=True, res_affine=None):
     """Finalize the fused statistics into scale/shift (+ running stats) and, with ``apply``, write
     ``relu(yc * scale + shift + resid)``; ``res_affine = (scale_r, shift_r)`` normalises a pre-BN
-    residual on the fly (the downsample shortcut's BN rides in its consumer's apply sweep).  ``fin``: a
-    :func:`_fin_request` the producing GEMM already completed (``fin["done"]``): its vectors are used as they are."""
+    residual on the fly (the downsample shortcut's BN rides in its consumer's apply sweep)."""
     Cc = yc.shape[-1]
     M = yc.numel() // Cc
     dev = yc.device
     bn = layer_bn
-    if fin is not None and fin.get("done"):
-        scale, shift, mean, invstd = fin["scale"], fin["shift"], fin["mean"], fin["invstd"]
-    else:
-        gamma = None if bn.gamma is None else bn.gamma.master
-        beta = None if bn.beta is None else bn.beta.master
-        rm, rv = bn._states["moving_mean"], bn._states["moving_variance"]
-        # one allocation for the four per-channel vectors (host cost per BN: VGG-16 runs launch-bound)
-        scale, shift, mean, invstd = torch.empty(4, Cc, dtype=torch.float32, device=dev).unbind(0)
-        if stats is None:  # deterministic mode: no fused (atomic) statistics; fixed-order partial rows instead
-            stats = partials_workspace(M, Cc, dev)
-            C().bn_stats(yc, stats, Cc)
-        C().bn_finalize(stats, M, Cc, gamma, beta, bn.epsilon, 1.0 - bn.momentum, rm, rv, mean, invstd, scale, shift)
+    gamma = None if bn.gamma is None else bn.gamma.master
+    beta = None if bn.beta is None else bn.beta.master
+    rm, rv = bn._states["moving_mean"], bn._states["moving_variance"]
+    # one allocation for the four per-channel vectors (host cost per BN: VGG-16 runs launch-bound)
+    scale, shift, mean, invstd = torch.empty(4, Cc, dtype=torch.float32, device=dev).unbind(0)
+    if stats is None:  # deterministic mode: no fused (atomic) statistics; fixed-order partial rows instead
+        stats = partials_workspace(M, Cc, dev)
+        C().bn_stats(yc, stats, Cc)
+    C().bn_finalize(stats, M, Cc, gamma, beta, bn.epsilon, 1.0 - bn.momentum, rm, rv, mean, invstd, scale, shift)
     if not apply:
         return None, mean, invstd, scale, shift
     y = torch.empty_like(yc)
@@ -118,8 +98,7 @@ def convbn_forward(unit, x, resid=None, relu=True, apply=True, res_affine=None, 
     p = conv.padding if isinstance(conv.padding, tuple) else (kh // 2, kw // 2)
     g = CV.geometry(N, H, W, Ci, conv.filters, kh, kw, conv.strides, p, conv.dilation_rate)
     stats = new_stats_workspace(conv.filters, x.device)
-    fin = _fin_request(bn, conv.filters, g.M, x.device) if (_FUSE_FINALIZE and stats is not None) else None
-    yc = CV.conv_fwd_native(x, conv.kernel.data, g, stats=stats, x_norm=x_norm, fin=fin)
+    yc = CV.conv_fwd_native(x, conv.kernel.data, g, stats=stats, x_norm=x_norm)
     st = _ConvBNState()
     st.g, st.yc = g, yc
     # ReLU after a residual add: the backward mask cannot be recomputed from yc alone, so the
@@ -127,7 +106,7 @@ def convbn_forward(unit, x, resid=None, relu=True, apply=True, res_affine=None, 
     bits = relu and resid is not None
     st.mask = torch.empty(-(-yc.numel() // 32) * 4, dtype=torch.uint8, device=yc.device) if bits else None
     st.y, st.mean, st.invstd, st.scale, st.shift = _bn_forward(bn, yc, stats, resid, relu, True, st.mask, apply,
-                                                               res_affine, fin=fin)
+                                                               res_affine)
     st.mode = 0 if not relu else (2 if resid is None else (3 if bits else 1))
     return st
 
@@ -298,12 +277,6 @@ _FUSE_DOWN = _os.environ.get("DDL_FUSE_DOWN_BN", "1") != "0"
 # stem: BN backward through the max pool without materialising the pool's gradient (pool3s2_bn_bwd)
 _FUSE_STEM_BWD = _os.environ.get("DDL_FUSE_STEM_BWD", "1") != "0"
 _STEM_PARTIALS = int(_os.environ.get("DDL_STEM_PARTIALS", "2048"))  # workgroups (= partial rows) of its reduce
-# BN forward finalize fused into the last workgroup of the conv GEMM that accumulated the statistics: opt-in —
-# correct (tests/test_gpu_kernels.py::test_fused_bn_finalize_tail) but slower: every workgroup must drain its
-# stores and statistics atomics (vmcnt(0)) before counting its arrival, which costs more than the 53 finalize
-# launches it removes (ResNet-50 11,910-11,933 vs 12,210-12,216 img/s interleaved; with an agent-scope
-# __threadfence instead, 8,132-8,142: the fence writes the XCD's L2 back) — profiles/r4/ab_fused_finalize.txt
-_FUSE_FINALIZE = _os.environ.get("DDL_FUSE_BN_FINALIZE", "0") == "1"
 # Normalise-on-load is opt-in (DDL_NORM_ON_LOAD=1): it removes bn2's apply sweep (-0.27 ms/step on
 # ResNet-50 b256) but the per-fragment scale/shift/ReLU VALU in the RC x RC weight gradient (+0.22 ms)
 # and the LDS transform pass + narrower panels of the streaming forward (+0.20 ms) cost more

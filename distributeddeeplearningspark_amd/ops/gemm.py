@@ -161,7 +161,7 @@ def choose_split(M: int, N: int, K: int, tile: int, allow: bool, rounds: float |
 def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, beta=0.0, bias=None, resid=None,
          ldr=0, relu=False, geom=None, outmap=None, b_kdiv=0, b_tap_stride=0, stats=None, tile=None, k_split=None,
          bn_cap=128, aux=None, drop_p=0.0, drop_seed=0, split_rounds=None, resid_mask=None, bnr=None, rsub=None,
-         a_norm=None, b_norm=None, slabs=None, defer_slabs=False, fin=None):
+         a_norm=None, b_norm=None, slabs=None, defer_slabs=False):
     """Raw launcher with automatic tile / split-K choice.  ``slabs``: force (True) or forbid (False) the
     partial-slab split-K path of fp32 outputs (default: deterministic mode or DDL_SPLITK_SLABS);
     ``defer_slabs``: when that path is taken, skip the reduce and return ``(slabs, splits)`` for a
@@ -213,7 +213,7 @@ def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, bet
              None if bnr is None else bnr["x"], None if bnr is None else bnr.get("mask"),
              None if bnr is None else bnr["mean"], *(rsub or (0, 0)), *(a_norm or (None, None)),
              *(b_norm or (None, None)), None if bnr is None else bnr.get("scale"),
-             None if bnr is None else bnr.get("shift"), split_stride, fin)
+             None if bnr is None else bnr.get("shift"), split_stride)
     if split_stride:
         if defer_slabs:
             return out, math.ceil(K / k_split)
@@ -256,7 +256,7 @@ ACT_NONE, ACT_RELU, ACT_GELU, ACT_GELU_BWD = 0, 1, 2, 3
 
 
 def linear_fwd(x2, w, bias=None, relu=False, out=None, resid=None, stats=None, act=None, aux=None, drop_p=0.0,
-               drop_seed=0, x_norm=None, fin=None):
+               drop_seed=0, x_norm=None):
     """y[M,N] = x2[M,K] @ w[N,K]^T (+bias) -> act -> dropout (+resid) -> bf16.
 
     ``act``: ACT_RELU / ACT_GELU (``aux`` receives the bf16 pre-activation).  ``x_norm = (scale,
@@ -269,7 +269,7 @@ def linear_fwd(x2, w, bias=None, relu=False, out=None, resid=None, stats=None, a
     act = (ACT_RELU if relu else ACT_NONE) if act is None else act
     return gemm(x2, w, out, M, N, K, KC, KC, x2.stride(0), w.stride(0), out.stride(0), EPI_BF16, bias=bias, relu=act,
                 resid=resid, ldr=(resid.stride(0) if resid is not None else 0), stats=stats, aux=aux, drop_p=drop_p,
-                drop_seed=drop_seed, a_norm=x_norm, tile=TILE_STREAM if x_norm is not None else None, fin=fin)
+                drop_seed=drop_seed, a_norm=x_norm, tile=TILE_STREAM if x_norm is not None else None)
 
 
 def norm_on_load_fwd_ok(M, N, K, lda, ldc) -> bool:

@@ -1246,48 +1246,3 @@ def test_splitk_slabs_match_atomics(M, N, K, monkeypatch):
     assert torch.equal(outs[True][0], outs[True][1]), "slab split-K must be bitwise reproducible"
     close(outs[True][0], ref, rtol=2e-3, atol=0.5, what="slabs vs fp32")
     close(outs[True][0], outs[False][0], rtol=1e-4, atol=1e-3, what="slabs vs atomics")
-
-
-@pytest.mark.parametrize("case", ["stream_1x1", "dma_1x1", "gather_3x3_c64", "halo_3x3_c128", "stem_gather8"])
-def test_fused_bn_finalize_tail(case):
-    """GemmParams.fin_* (opt-in, DDL_FUSE_BN_FINALIZE=1): the conv GEMM's last workgroup finalizes the BN statistics it accumulated (streaming kernel,
-    LDS-DMA plain / gathered GEMM, halo conv).  The outputs equal bn_finalize's on the same statistics
-    workspace, the running statistics move exactly once per launch, and the re-armed counter finalizes a
-    second launch too."""
-    from distributeddeeplearningspark_amd.ops import conv as CV
-    from distributeddeeplearningspark_amd.ops._native import C as NC
-    from distributeddeeplearningspark_amd.ops.norm import SHARDS
-
-    geo = {"stream_1x1": (64, 56, 256, 64, 1), "dma_1x1": (64, 14, 1024, 256, 1), "gather_3x3_c64": (32, 56, 64, 64, 3),
-           "halo_3x3_c128": (64, 28, 128, 128, 3), "stem_gather8": (16, 115, 16, 64, 4)}[case]
-    N, H, Ci, Co, k = geo
-    pad = (k // 2, k // 2) if k == 3 else (0, 0)
-    g = CV.geometry(N, H, H, Ci, Co, k, k, (1, 1), pad, (1, 1))
-    if case == "halo_3x3_c128":
-        assert CV.halo3_ok(g)
-    assert not CV.splitk_fwd_ok(g)
-    gen = torch.Generator().manual_seed(sum(geo))
-    x = torch.randn(N, H, H, Ci, generator=gen).to(DEV, torch.bfloat16)
-    w = (torch.randn(Co, k, k, Ci, generator=gen) / (k * k * Ci) ** 0.5).to(DEV, torch.bfloat16)
-    gamma = (torch.rand(Co, generator=gen) + 0.5).to(DEV)
-    beta = torch.randn(Co, generator=gen).to(DEV)
-    rm0 = torch.randn(Co, generator=gen).to(DEV)
-    rv0 = (torch.rand(Co, generator=gen) + 0.5).to(DEV)
-    cnt = torch.zeros(1, dtype=torch.int32, device=DEV)
-    for it in range(2):
-        stats = torch.zeros((SHARDS, 2, Co), dtype=torch.float32, device=DEV)
-        rm, rv = rm0.clone(), rv0.clone()
-        vec = torch.empty(4, Co, dtype=torch.float32, device=DEV)
-        fin = {"counter": cnt, "gamma": gamma, "beta": beta, "rmean": rm, "rvar": rv, "mean": vec[0], "invstd": vec[1],
-               "scale": vec[2], "shift": vec[3], "eps": 1e-3, "momentum": 0.01, "M": g.M}
-        CV.conv_fwd_native(x, w, g, stats=stats, fin=fin)
-        assert fin.get("done")
-        ref = torch.empty(4, Co, dtype=torch.float32, device=DEV)
-        rm2, rv2 = rm0.clone(), rv0.clone()
-        NC().bn_finalize(stats, g.M, Co, gamma, beta, 1e-3, 0.01, rm2, rv2, ref[0], ref[1], ref[2], ref[3])
-        torch.cuda.synchronize()
-        assert int(cnt.item()) == 0, "the last workgroup re-arms the counter"
-        for i, nm in enumerate(("mean", "invstd", "scale", "shift")):
-            close(vec[i], ref[i], rtol=1e-6, atol=1e-6, what=f"{case} {nm} (launch {it})")
-        close(rm, rm2, rtol=1e-6, atol=1e-6, what="running mean")
-        close(rv, rv2, rtol=1e-6, atol=1e-6, what="running var")
