@@ -1,6 +1,5 @@
 #!/bin/bash
-# Interleaved A/B against the previous build in ab_prev/ (commit 514c1e2, before the whole-wave statistics
-# atomics): BERT-base and ResNet-50 benches.
+# Interleaved A/B against a previous build in ab_prev/ (see the commit message of the run), BERT-base and ResNet-50.
 set -o pipefail
 R=$GRAFT_REPO_ROOT; cd $R
 O=$R/gpurun_out/r4/ab_prev; mkdir -p $O
