@@ -125,5 +125,8 @@ def test_resnet50_learns_synthetic_task_like_torch_path(monkeypatch):
     # window 0 across runs; hip 0.02-0.41, torch 0.29-0.89 at step 70), so the curves are compared where both
     # have converged, plus a factor-2 band over the first windows
     assert 0.5 * win(t, 0, 10) < win(h, 0, 10) < 2.0 * win(t, 0, 10), summary
-    assert win(h, 140, 150) < 0.1 and win(t, 140, 150) < 0.1, summary
+    # the reference (PyTorch / MIOpen) path's own late spikes reach ~0.13 in its final window on some runs
+    # (measured 0.125 at HEAD with hip 0.001, round 4): the reference is held to having learned (< 0.3, its
+    # held-out accuracy below), the HIP path to having converged
+    assert win(h, 140, 150) < 0.1 and win(t, 140, 150) < 0.3, summary
     assert accs["hip"] >= 0.9 and accs["torch"] >= 0.9, accs
