@@ -254,6 +254,9 @@ __global__ __launch_bounds__(256) void avgpool_fwd_kernel(const uint4* __restric
     float acc[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+    // unrolled: eight independent 16-B loads in flight per lane (the rolled loop waited on each of the 49
+    // pixels of ResNet-50's 7x7 map in turn: 27 us for 51 MB)
+#pragma unroll 8
     for (int p = 0; p < HW; ++p) {
       float f[8];
       unpack8p(x[(n * HW + p) * CV + cv], f);
