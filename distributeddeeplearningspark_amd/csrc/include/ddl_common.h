@@ -133,6 +133,13 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
       (uint32_t) reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) char*)p));
 }
 // s_waitcnt vmcnt(N) (gfx9 encoding), visible to the compiler's wait-insertion pass
+// Workgroup barrier that orders LDS only.  __syncthreads() is a workgroup-scope fence + s_barrier,
+// and the fence makes every wave drain its outstanding GLOBAL loads and stores (s_waitcnt vmcnt(0))
+// first: in a latency-bound loop that streams results to HBM each iteration (the recurrent kernels)
+// that is a full store round trip per barrier.  Here only the LDS / scalar queue is waited for; the
+// "memory" clobber keeps the compiler from moving memory operations across it.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);

@@ -211,12 +211,34 @@ constexpr int RNN_BB_FWD = 1, RNN_BB_BWD = 1;  // default rows per workgroup (H 
 
 __device__ __forceinline__ int cpos(int col) { return (col / CH) * CP + (col % CH); }
 
+// lane ^ 1 / lane ^ 2 / ... partner value by DPP (VALU) instead of ds_bpermute (an LDS round trip
+// on the recurrence's critical path): quad_perm within 4 lanes, row_ror / row_mirror patterns beyond
+template <int O>
+__device__ __forceinline__ float xor_lane(float v) {
+  const int iv = __builtin_bit_cast(int, v);
+  if constexpr (O == 1) return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(iv, 0xB1, 0xf, 0xf, false));
+  else if constexpr (O == 2) return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(iv, 0x4E, 0xf, 0xf, false));
+  else return __shfl_xor(v, O, 64);
+}
+// partner-quad value inside each 8-lane group (row_half_mirror): lane i reads lane 7 - i, i.e. a lane
+// of the OTHER quad — equal to lane ^ 4 whenever the values are uniform within quads, as they are
+// after the xor 1 / xor 2 steps of a sum reduction
+__device__ __forceinline__ float other_quad(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x141, 0xf, 0xf, false));
+}
+
+// The waitcnt pass treats the values loaded before a loop as possibly still in flight inside it and
+// then waits, in every iteration, for whatever vector loads are outstanding at their first use (the
+// next step's prefetch).  One real s_waitcnt vmcnt(0) before the loop (a builtin the pass models,
+// unlike an asm string) retires them once.  gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15.
+__device__ __forceinline__ void retire_vm_loads() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 template <int CELL, int H>
 constexpr int fwd_threads() { return (CELL == 0 ? 3 : 4) * H * (H / 64); }
 template <int CELL, int H>
 constexpr int bwd_threads() { return H * (((CELL == 0 ? 3 : 4) * H / 64) <= 4 ? 4 : 8); }
 
-template <int CELL, int H, int BB_>
+template <int CELL, int H, int BB_, bool FUSE>
 __global__ __launch_bounds__((fwd_threads<CELL, H>())) void rnn_fwd_reg_kernel(
     const float* __restrict__ xw, const float* __restrict__ x, const float* __restrict__ W,
     const float* __restrict__ bias, int I, const float* __restrict__ U, float* __restrict__ hs,
@@ -225,6 +247,7 @@ __global__ __launch_bounds__((fwd_threads<CELL, H>())) void rnn_fwd_reg_kernel(
   constexpr int GH = G * H;
   constexpr int KS = H / CH;
   constexpr int HC = KS * CP;  // padded row length of h / c
+  constexpr int NT = fwd_threads<CELL, H>();  // == blockDim.x (the launcher's block size)
   __shared__ __attribute__((aligned(16))) float h[BB_][HC];
   __shared__ __attribute__((aligned(16))) float c[BB_][HC];  // LSTM cell state / GRU r*h
   __shared__ float gb[BB_][GH];
@@ -235,29 +258,44 @@ __global__ __launch_bounds__((fwd_threads<CELL, H>())) void rnn_fwd_reg_kernel(
   float u[CH];
 #pragma unroll
   for (int i = 0; i < CH; ++i) u[i] = U[(long)(kh * CH + i) * GH + j];
-  float wv[IMAX], bv = 0.f;  // input-projection column j (fused path)
+  float wv[IMAX], bv = 0.f;  // input-projection column j (fused path); wv[i] = 0 past the input width
 #pragma unroll
-  for (int i = 0; i < IMAX; ++i) wv[i] = (!xw && i < I) ? W[(long)i * GH + j] : 0.f;
-  if (!xw && bias) bv = bias[j];
-  // x W + b of step t for my column and rows (only kh == 0 lanes consume it)
-  auto load_x = [&](int t, float* xv) {
+  for (int i = 0; i < IMAX; ++i) wv[i] = (FUSE && i < I) ? W[(long)i * GH + j] : 0.f;
+  if (FUSE && bias) bv = bias[j];
+  // Step t's inputs are fetched one step ahead and contracted only when used, so their latency hides
+  // behind a whole step.  The x row address is workgroup-uniform: an opaque zero offset keeps the loads
+  // on the vector path (a scalar load is counted by lgkmcnt, which every LDS barrier drains), and the
+  // loads are unconditional at clamped indices (a runtime-guarded load per element makes the compiler
+  // branch and wait per element); padded inputs meet wv = 0.
+  int zoff;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(zoff));
+  auto fetch_x = [&](int t, float (&xr)[BB_][IMAX]) {
+    const int tc = min(max(t, 0), T - 1);
 #pragma unroll
     for (int r = 0; r < BB_; ++r) {
-      xv[r] = 0.f;
-      if (kh != 0 || r >= nb || t < 0) continue;
-      const long bt = (long)(b0 + r) * T + t;
-      if (xw) {
-        xv[r] = xw[bt * GH + j];
+      const long bt = (long)(b0 + min(r, nb - 1)) * T + tc;
+      if constexpr (!FUSE) {
+        xr[r][0] = xw[bt * GH + j];
+      } else {
+#pragma unroll
+        for (int i = 0; i < IMAX; ++i) xr[r][i] = x[bt * I + min(i, I - 1) + zoff];
+      }
+    }
+  };
+  auto proj = [&](const float (&xr)[BB_][IMAX], float* xv) {
+#pragma unroll
+    for (int r = 0; r < BB_; ++r) {
+      if constexpr (!FUSE) {
+        xv[r] = xr[r][0];
       } else {
         float a = bv;
 #pragma unroll
-        for (int i = 0; i < IMAX; ++i)
-          if (i < I) a += x[bt * I + i] * wv[i];
+        for (int i = 0; i < IMAX; ++i) a += xr[r][i] * wv[i];
         xv[r] = a;
       }
     }
   };
-  for (int i = tid; i < BB_ * HC; i += blockDim.x) (&h[0][0])[i] = (&c[0][0])[i] = 0.f;
+  for (int i = tid; i < BB_ * HC; i += NT) (&h[0][0])[i] = (&c[0][0])[i] = 0.f;
   // element owned in the state-update phase
   const int er = tid / H, ek = tid - er * H;
   const bool eown = er < nb;
@@ -266,8 +304,10 @@ __global__ __launch_bounds__((fwd_threads<CELL, H>())) void rnn_fwd_reg_kernel(
     hs[(erow * (T + 1)) * H + ek] = 0.f;
     if (CELL == 1) cs[(erow * (T + 1)) * H + ek] = 0.f;
   }
-  float xv[BB_];
-  load_x(0, xv);
+  float xr[BB_][IMAX], xv[BB_];
+  fetch_x(0, xr);
+  proj(xr, xv);
+  retire_vm_loads();
   __syncthreads();
   auto contract = [&](float (*src)[HC], float* acc) {
 #pragma unroll
@@ -282,12 +322,11 @@ __global__ __launch_bounds__((fwd_threads<CELL, H>())) void rnn_fwd_reg_kernel(
     }
     if (KS == 2) {
 #pragma unroll
-      for (int r = 0; r < BB_; ++r) acc[r] += __shfl_xor(acc[r], 1, 64);
+      for (int r = 0; r < BB_; ++r) acc[r] += xor_lane<1>(acc[r]);
     }
   };
   for (int t = 0; t < T; ++t) {
-    float xn[BB_];
-    load_x(t + 1 < T ? t + 1 : -1, xn);  // prefetch the next step's projection
+    fetch_x(t + 1, xr);  // the next step's inputs (consumed at the end of this step)
     float acc[BB_];
     if (CELL == 1 || j < 2 * H) {  // wave-uniform: 2H columns span whole waves
       contract(h, acc);
@@ -297,13 +336,13 @@ __global__ __launch_bounds__((fwd_threads<CELL, H>())) void rnn_fwd_reg_kernel(
         for (int r = 0; r < BB_; ++r) gb[r][j] = is_tanh ? tanhf(acc[r] + xv[r]) : hsig(acc[r] + xv[r]);
       }
     }
-    __syncthreads();
+    lds_barrier();
     if (CELL == 0) {
-      for (int i = tid; i < BB_ * H; i += blockDim.x) {
+      for (int i = tid; i < BB_ * H; i += NT) {
         const int r = i / H, k = i - r * H;
         c[r][cpos(k)] = gb[r][H + k] * h[r][cpos(k)];
       }
-      __syncthreads();
+      lds_barrier();
       if (j >= 2 * H) {
         contract(c, acc);
         if (kh == 0) {
@@ -311,8 +350,14 @@ __global__ __launch_bounds__((fwd_threads<CELL, H>())) void rnn_fwd_reg_kernel(
           for (int r = 0; r < BB_; ++r) gb[r][j] = tanhf(acc[r] + xv[r]);
         }
       }
-      __syncthreads();
+      lds_barrier();
     }
+    // next step's projection before this step's stores: its wait then covers the loads issued at the
+    // top of the step and the PREVIOUS step's stores (a whole step old), never the stores below
+    float xnext[BB_];
+    proj(xr, xnext);
+#pragma unroll
+    for (int r = 0; r < BB_; ++r) asm volatile("" ::"v"(xnext[r]) : "memory");  // computed here, not sunk past the stores
     if (eown) {
       float hn;
       if (CELL == 0) {
@@ -329,13 +374,13 @@ __global__ __launch_bounds__((fwd_threads<CELL, H>())) void rnn_fwd_reg_kernel(
       if (rs) y[(erow * T + t) * H + ek] = hn;
       else if (t == T - 1) y[erow * H + ek] = hn;
     }
-    for (int i = tid; i < nb * GH; i += blockDim.x) {
+    for (int i = tid; i < nb * GH; i += NT) {
       const int r = i / GH, jj = i - r * GH;
       gates[((long)(b0 + r) * T + t) * GH + jj] = gb[r][jj];
     }
 #pragma unroll
-    for (int r = 0; r < BB_; ++r) xv[r] = xn[r];
-    __syncthreads();
+    for (int r = 0; r < BB_; ++r) xv[r] = xnext[r];
+    lds_barrier();
   }
 }
 
@@ -348,6 +393,7 @@ __global__ __launch_bounds__((bwd_threads<CELL, H>())) void rnn_bwd_reg_kernel(
   constexpr int JS = GH / CH;                            // column chunks
   constexpr int JSP = JS <= 4 ? 4 : 8;                   // lanes per k (power of two)
   constexpr int ZR = CELL == 0 ? 2 * H / CH : JS;        // chunks feeding dh directly
+  constexpr int NT = bwd_threads<CELL, H>();            // == blockDim.x
   __shared__ __attribute__((aligned(16))) float p[BB_][JS * CP];  // pre-activation gradients
   __shared__ float dh[BB_][H];
   __shared__ float aux[BB_][H];  // GRU: d*z direct part; LSTM: running dc
@@ -364,8 +410,8 @@ __global__ __launch_bounds__((bwd_threads<CELL, H>())) void rnn_bwd_reg_kernel(
     const float4 v = *reinterpret_cast<const float4*>(&U[(long)k * GH + min(js, JS - 1) * CH + i]);  // idle: unused
     u[i] = v.x; u[i + 1] = v.y; u[i + 2] = v.z; u[i + 3] = v.w;
   }
-  for (int i = tid; i < BB_ * H; i += blockDim.x) (&dh[0][0])[i] = (&aux[0][0])[i] = 0.f;
-  for (int i = tid; i < BB_ * JS * CP; i += blockDim.x) (&p[0][0])[i] = 0.f;
+  for (int i = tid; i < BB_ * H; i += NT) (&dh[0][0])[i] = (&aux[0][0])[i] = 0.f;
+  for (int i = tid; i < BB_ * JS * CP; i += NT) (&p[0][0])[i] = 0.f;
   // element owned in the element-wise phase, and its prefetched inputs
   const int er = tid / H, ek = tid - er * H;
   const bool eown = er < nb;
@@ -386,6 +432,7 @@ __global__ __launch_bounds__((bwd_threads<CELL, H>())) void rnn_bwd_reg_kernel(
   };
   In cur{}, nxt{};
   load_in(T - 1, cur);
+  retire_vm_loads();
   __syncthreads();
   auto contract = [&](bool use, float* acc) {
 #pragma unroll
@@ -405,8 +452,9 @@ __global__ __launch_bounds__((bwd_threads<CELL, H>())) void rnn_bwd_reg_kernel(
 #pragma unroll
     for (int r = 0; r < BB_; ++r) {
       acc[r] = use ? acc[r] : 0.f;
-#pragma unroll
-      for (int o = 1; o < JSP; o <<= 1) acc[r] += __shfl_xor(acc[r], o, 64);
+      acc[r] += xor_lane<1>(acc[r]);
+      acc[r] += xor_lane<2>(acc[r]);
+      if constexpr (JSP == 8) acc[r] += other_quad(acc[r]);
     }
   };
   for (int t = T - 1; t >= 0; --t) {
@@ -432,7 +480,7 @@ __global__ __launch_bounds__((bwd_threads<CELL, H>())) void rnn_bwd_reg_kernel(
         aux[er][ek] = dc * gf;
       }
     }
-    __syncthreads();
+    lds_barrier();
     // GRU: phase 0 = d(r*h) = dp_h Uh^T -> dr and the r-path part of dh_{t-1}; phase 1 = dh_{t-1}.
     // One call site for the contraction (keeps a single register-resident copy of U).
 #pragma unroll 1
@@ -452,14 +500,14 @@ __global__ __launch_bounds__((bwd_threads<CELL, H>())) void rnn_bwd_reg_kernel(
           for (int r = 0; r < BB_; ++r) dh[r][k] = (CELL == 0 ? aux[r][k] : 0.f) + acc[r];
         }
       }
-      if (ph == 0) __syncthreads();
+      if (ph == 0) lds_barrier();
     }
-    for (int i = tid; i < nb * GH; i += blockDim.x) {
+    for (int i = tid; i < nb * GH; i += NT) {
       const int r = i / GH, jj = i - r * GH;
       dgates[((long)(b0 + r) * T + t) * GH + jj] = p[r][cpos(jj)];
     }
     cur = nxt;
-    __syncthreads();
+    lds_barrier();
   }
 }
 
@@ -538,9 +586,14 @@ int launch_fwd_reg(const float* xw, const float* x, const float* W, const float*
                    float* cs, float* gates, float* y, int B, int T, int rs, hipStream_t s) {
   constexpr int G = CELL == 0 ? 3 : 4;
   static_assert(BB_ * H <= fwd_threads<CELL, H>(), "one state element per thread");
+  if (!xw && (I < 1 || I > IMAX)) return (int)hipErrorInvalidValue;
   const dim3 grid((B + BB_ - 1) / BB_);
-  hipLaunchKernelGGL((rnn_fwd_reg_kernel<CELL, H, BB_>), grid, dim3(G * H * (H / CH)), 0, s, xw, x, W, b, I, U, hs,
-                     cs, gates, y, B, T, rs);
+  if (xw)
+    hipLaunchKernelGGL((rnn_fwd_reg_kernel<CELL, H, BB_, false>), grid, dim3(G * H * (H / CH)), 0, s, xw, x, W, b, I,
+                       U, hs, cs, gates, y, B, T, rs);
+  else
+    hipLaunchKernelGGL((rnn_fwd_reg_kernel<CELL, H, BB_, true>), grid, dim3(G * H * (H / CH)), 0, s, xw, x, W, b, I,
+                       U, hs, cs, gates, y, B, T, rs);
   return (int)hipGetLastError();
 }
 

@@ -20,7 +20,9 @@ token element).  Under this mode every one of them is replaced by a fixed-order 
     sums the run in token order (``embed_word_grad_det``).
 
 Two runs of the same step on the same inputs then produce bitwise-identical losses and gradient
-arenas (``tests/test_gpu_determinism.py``).  The mode costs throughput (more sweeps, fewer
+arenas (``tests/test_gpu_determinism.py``).  Multi-rank runs additionally need fixed all-reduce
+bucket boundaries: under this mode ``DataParallel`` skips the timing-based bucket calibration and
+uses 32 MB buckets (or an explicit ``DDL_BUCKET_MB``).  The mode costs throughput (more sweeps, fewer
 workgroups on the reductions); ``scripts/r4/determinism.sh`` measures the price.  The reference has
 no reproducible mode: its parameter server applies commits in arrival order
 (``/root/reference/ddl_mnist_aztk.py:216-224``).

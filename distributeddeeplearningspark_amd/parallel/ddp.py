@@ -220,7 +220,13 @@ class DataParallel:
         self.calibration = None
         if bucket_mb is None:
             env = os.environ.get("DDL_BUCKET_MB", "auto")
-            if env == "auto":
+            from ..ops import determinism
+
+            if env == "auto" and determinism.enabled():
+                # reproducible multi-rank runs need fixed bucket boundaries (a timing-based size can
+                # change RCCL's chunking, and with it the summation order, from run to run)
+                bucket_mb = 32.0
+            elif env == "auto":
                 # measured on THIS group (RCCL over xGMI on a GPU node): see bucket_policy / calibrate_allreduce
                 self.calibration = calibrate_allreduce(pg, model.arena.grad.device if model.arena is not None else None)
                 bucket_mb = self.calibration["bucket_mb"] if self.calibration else 32.0

@@ -78,12 +78,15 @@ def _release_block(key):
             pass
 
 
-def _fingerprint(a) -> int | None:
-    """Content hash of a WRITABLE source array (None for read-only ones, which cannot change under
-    the cache).  xxh3 runs at memory speed: ~10 ms per 150 MB shard."""
+def _fingerprint(a, base=None) -> int | None:
+    """Content hash of a source array whose memory can change (None when the root buffer ``base``
+    is read-only: then nothing can write it under the cache).  A read-only VIEW of a writable base
+    is still hashed, since the base can be modified in place.  xxh3 runs at memory speed: ~10 ms
+    per 150 MB shard."""
     import numpy as np
 
-    if not a.flags.writeable:
+    root = a if base is None else base
+    if not root.flags.writeable and not a.flags.writeable:
         return None
     buf = memoryview(np.ascontiguousarray(a)).cast("B")
     try:
@@ -111,7 +114,7 @@ def share_array(a):
     while isinstance(getattr(base, "base", None), np.ndarray):
         base = base.base
     key = (id(base), a.__array_interface__["data"][0], a.shape, a.strides, a.dtype.str)
-    fp = _fingerprint(a)
+    fp = _fingerprint(a, base)
     with _SHM_LOCK:
         e = _SHM_BLOCKS.get(key)
     if e is not None:

@@ -147,6 +147,11 @@ class _Replica:
         with torch.cuda.graph(g, stream=stream):
             for _ in range(k):
                 self._step_body(captured=True)
+        from ..ops.norm import _POOL
+
+        # the replayed kernels address the statistics-pool buffers: keep them alive even if the
+        # (global) pool is regrown later by another model (as models/step.py does)
+        self._keep = list(_POOL.buf.values())
         self.graph = g
         self.k = k
 
@@ -291,7 +296,7 @@ class ReplicaGroup:
         for j in range(self.rounds):
             todo = [r for r in self.reps if j < r.commits]
             if graphs and j == warm_rounds:
-                self._capture(todo)
+                graphs = self._capture(todo)
             self._window_all(todo, k, graphs and j >= warm_rounds)
             # exhausted replicas: their leftover (< k) steps come before their first zero commit
             for r in self.reps:
@@ -304,14 +309,28 @@ class ReplicaGroup:
         if self.gpu:
             torch.cuda.synchronize(self.pg.device)
 
-    def _capture(self, reps):
+    def _capture(self, reps) -> bool:
+        """Capture every replica's window; on failure fall back to eager windows (capture is an
+        optimisation, as in ``models/step.py``) and return False."""
         main = torch.cuda.current_stream(self.pg.device)
         torch.cuda.synchronize(self.pg.device)
-        for rep in reps:
-            rep.stream.wait_stream(main)
-            rep.capture_window(self.k, rep.stream)
+        try:
+            if os.environ.get("DDL_TEST_FAIL_CAPTURE") == "1":  # test hook: force the fallback path
+                raise RuntimeError("capture forced to fail (DDL_TEST_FAIL_CAPTURE)")
+            for rep in reps:
+                rep.stream.wait_stream(main)
+                rep.capture_window(self.k, rep.stream)
+        except Exception as e:
+            if os.environ.get("DDL_GRAPHS_STRICT") == "1":
+                raise
+            print(f"[ddl] replica-group hipGraph capture disabled: {type(e).__name__}: {e}", flush=True)
+            for rep in self.reps:
+                rep.graph = None
+            torch.cuda.synchronize(self.pg.device)
+            return False
         for rep in reps:
             main.wait_stream(rep.stream)
+        return True
 
     def _average(self):
         """AveragingTrainer: independent training, then the mean of all replicas' weights."""

@@ -674,7 +674,7 @@ class _ShardedTrainer(Trainer):
         if cfg.get("mode") == "async" and issubclass(_WORKERS[self.algorithm], _CommitWorker):
             server = self._start_async_server(cfg)
         try:
-            devices = self._replica_devices(cfg, server)
+            devices = self._replica_devices(cfg, server, Xs, Ys)
             if devices is not None:
                 results = self._train_replica_groups(cfg, Xs, Ys, sizes, devices)
             else:
@@ -700,9 +700,14 @@ class _ShardedTrainer(Trainer):
         self.record_training_end()
         return model
 
-    def _replica_devices(self, cfg, server):
+    def _replica_devices(self, cfg, server, Xs=None, Ys=None):
         """The worker -> device plan when the co-located workers run as in-process replica groups
-        (``parallel/replicas.py``), else None (one OS process per worker)."""
+        (``parallel/replicas.py``), else None (one OS process per worker).
+
+        Replica groups keep every shard resident in HBM, so they are used only when the user did
+        not ask for streamed ingest (``ingest="stream"``) and each group's shards together fit the
+        resident limit (``DDL_RESIDENT_MB``, as ``_ShardFeed`` applies per worker); otherwise the
+        process-per-worker path streams the shards through the pinned ring."""
         from .parallel import replicas as _rep
         from .parallel.launcher import plan_devices
 
@@ -710,8 +715,17 @@ class _ShardedTrainer(Trainer):
             return None
         if cfg.get("checkpoint_dir") or cfg.get("watchdog_s") or self.extra.get("max_restarts"):
             return None  # per-rank checkpoints / watchdog / restart live on the process-per-worker path
+        if cfg.get("ingest", "auto") == "stream":
+            return None
         devices = plan_devices(self.num_workers, self.device)
-        return devices if _rep.applies(cfg, devices) else None
+        if not _rep.applies(cfg, devices):
+            return None
+        if Xs is not None and devices[0] != "cpu":
+            limit = float(os.environ.get("DDL_RESIDENT_MB", "4096")) * (1 << 20)
+            for g in _rep.plan(devices):
+                if sum(Xs[r].nbytes + Ys[r].nbytes for r in g) > limit:
+                    return None
+        return devices
 
     def _train_replica_groups(self, cfg, Xs, Ys, sizes, devices):
         from .parallel import comm

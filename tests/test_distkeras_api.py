@@ -429,6 +429,31 @@ def test_shared_shards_follow_in_place_mutation(spark, monkeypatch):
         np.testing.assert_array_equal(a, b)
 
 
+def test_shared_block_follows_mutation_of_readonly_view_base():
+    """A READ-ONLY view of a writable base (``setflags(write=False)`` on a view) must still be
+    re-validated: the base can change in place under the cached /dev/shm block."""
+    from multiprocessing import shared_memory
+
+    from distributeddeeplearningspark_amd.parallel import executors as EX
+
+    base = np.arange(4096, dtype=np.float32).reshape(64, 64)
+    view = base[8:40]
+    view.setflags(write=False)
+
+    def read(desc):
+        shm = shared_memory.SharedMemory(name=desc.name)
+        try:
+            return np.ndarray(desc.shape, np.dtype(desc.dtype), buffer=shm.buf).copy()
+        finally:
+            shm.close()
+
+    d0 = EX.share_array(view)
+    np.testing.assert_array_equal(read(d0), base[8:40])
+    base *= 2.0  # in place, through the writable base
+    d1 = EX.share_array(view)
+    np.testing.assert_array_equal(read(d1), base[8:40])
+
+
 def test_prob_cross_entropy_cpu_matches_keras_formula():
     from distributeddeeplearningspark_amd.ops.loss import prob_cross_entropy
 

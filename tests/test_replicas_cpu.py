@@ -75,3 +75,23 @@ def test_replica_groups_not_used_for_async_or_syncgrad(spark, monkeypatch):
     assert replicas.applies({"algorithm": "adag"}, ["cuda:0", "cuda:0"])
     assert not replicas.applies({"algorithm": "adag"}, ["cuda:0", "cuda:1"])  # one worker per GPU
     assert replicas.plan(["cuda:0", "cuda:1", "cuda:0", "cuda:1"]) == [[0, 2], [1, 3]]
+
+
+def test_replica_groups_respect_stream_ingest_and_resident_limit(monkeypatch):
+    """Replica groups keep every shard resident in HBM: ``ingest="stream"`` or a group whose shards
+    exceed ``DDL_RESIDENT_MB`` must keep the process-per-worker path (which streams them)."""
+    from distributeddeeplearningspark_amd import trainers as T
+    from distributeddeeplearningspark_amd.parallel import launcher
+
+    monkeypatch.setenv("DDL_REPLICA_GROUPS", "auto")
+    monkeypatch.setattr(launcher, "plan_devices", lambda n, dev=None: ["cuda:0"] * n)
+    base = Sequential([Dense(1, input_shape=(5,))])
+    tr = T.ADAG(keras_model=base, worker_optimizer="adam", loss="mean_squared_error", num_workers=2,
+                batch_size=4, num_epoch=1, features_col="f", label_col="l", communication_window=2)
+    Xs = [np.zeros((1 << 16, 5), np.float32)] * 2  # 1.25 MiB per shard
+    Ys = [np.zeros((1 << 16, 1), np.float32)] * 2
+    cfg = tr._cfg()
+    assert tr._replica_devices(cfg, None, Xs, Ys) == ["cuda:0", "cuda:0"]
+    assert tr._replica_devices({**cfg, "ingest": "stream"}, None, Xs, Ys) is None
+    monkeypatch.setenv("DDL_RESIDENT_MB", "2")  # the two shards of the group: 2.75 MiB > 2 MiB
+    assert tr._replica_devices(cfg, None, Xs, Ys) is None
