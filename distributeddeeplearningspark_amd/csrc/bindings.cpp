@@ -57,9 +57,7 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
           c10::optional<py::dict> outmap, int64_t b_kdiv, int64_t b_tap_stride,
           c10::optional<at::Tensor> stats, c10::optional<at::Tensor> aux, double drop_p, int64_t drop_seed,
           c10::optional<at::Tensor> resid_mask, c10::optional<at::Tensor> bnr_x, c10::optional<at::Tensor> bnr_mask,
-          c10::optional<at::Tensor> bnr_mean, int64_t rsub_h, int64_t rsub_w, c10::optional<at::Tensor> a_scale,
-          c10::optional<at::Tensor> a_shift, c10::optional<at::Tensor> b_scale, c10::optional<at::Tensor> b_shift,
-          c10::optional<at::Tensor> bnr_scale, c10::optional<at::Tensor> bnr_shift, int64_t split_stride) {
+          c10::optional<at::Tensor> bnr_mean, int64_t rsub_h, int64_t rsub_w, c10::optional<at::Tensor> bnr_scale, c10::optional<at::Tensor> bnr_shift, int64_t split_stride) {
   CHECK_CUDA(a);
   CHECK_CUDA(b);
   CHECK_CUDA(c);
@@ -74,7 +72,7 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
   if (b_mode == OP_RC || b_mode == OP_RC_TAPS) TORCH_CHECK(ldb % 8 == 0, "gemm: ldb must be a multiple of 8");
   TORCH_CHECK(((uintptr_t)a.data_ptr() % 16) == 0 && ((uintptr_t)b.data_ptr() % 16) == 0, "gemm: operands must be 16-B aligned");
   TORCH_CHECK(k_split > 0 && k_split % 64 == 0, "gemm: k_split must be a positive multiple of 64");
-  TORCH_CHECK(tile >= 0 && tile <= kTile256P, "gemm: bad tile id");
+  TORCH_CHECK(tile >= 0 && tile <= kTileConv3, "gemm: bad tile id");
   if (tile == kTileStream) {
     TORCH_CHECK(a_mode == OP_KC && (b_mode == OP_KC || b_mode == OP_RC) && epi == EPI_BF16 && !outmap.has_value() &&
                     relu <= ACT_RELU && drop_p == 0.0 && beta == 0.0 && k_split >= K,
@@ -83,7 +81,7 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
     TORCH_CHECK(ldc % 8 == 0 && ((uintptr_t)c.data_ptr() % 16) == 0, "gemm stream: 16-B aligned output rows");
     TORCH_CHECK(!resid || (ldr % 4 == 0 && ((uintptr_t)resid->data_ptr() % 8) == 0), "gemm stream: resid alignment");
   }
-  if (tile == kTile256 || tile == kTile256P || tile == kTileW4 || tile == kTileW4N) {
+  if (tile == kTile256) {
     TORCH_CHECK(a_mode <= OP_RC && b_mode <= OP_RC && !outmap.has_value(), "gemm256: plain KC/RC operands only");
     TORCH_CHECK(K % 64 == 0 && k_split % 64 == 0, "gemm256: K and k_split must be multiples of 64");
     TORCH_CHECK(M >= 8 && N >= 8, "gemm256: M, N >= 8");
@@ -189,7 +187,7 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
     p.stats = stats->data_ptr<float>();
   }
   if (bnr_x) {
-    TORCH_CHECK(stats.has_value() && bnr_mean.has_value() && epi == EPI_BF16 && tile != kTile256 && tile != kTile256P && tile != kTileW4 && tile != kTileW4N,
+    TORCH_CHECK(stats.has_value() && bnr_mean.has_value() && epi == EPI_BF16 && tile != kTile256,
                 "gemm: the fused BN-backward reduction needs a stats workspace, the mean and a bf16 epilogue");
     TORCH_CHECK(tile == kTileStream || (N % 4 == 0 && ldc % 8 == 0 && !bias && relu == 0 && !aux &&
                                         drop_p == 0.0 && (a_mode == OP_KC || (a_mode == OP_KC_GATHER && b_mode == OP_KC))),
@@ -221,24 +219,6 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
       p.bnr_shift = bnr_shift->data_ptr<float>();
     }
   }
-  auto norm_pair = [&](const c10::optional<at::Tensor>& sc, const c10::optional<at::Tensor>& sh, int64_t n,
-                       const char* what) -> std::pair<const float*, const float*> {
-    if (!sc && !sh) return {nullptr, nullptr};
-    TORCH_CHECK(sc && sh, "gemm: ", what, " scale and shift together");
-    CHECK_CUDA(*sc);
-    CHECK_F32(*sc);
-    CHECK_F32(*sh);
-    TORCH_CHECK(sc->numel() >= n && sh->numel() >= n && ((uintptr_t)sc->data_ptr() % 16) == 0 &&
-                    ((uintptr_t)sh->data_ptr() % 16) == 0,
-                "gemm: ", what, " scale / shift must cover the channels and be 16-B aligned");
-    return {sc->data_ptr<float>(), sh->data_ptr<float>()};
-  };
-  std::tie(p.a_scale, p.a_shift) = norm_pair(a_scale, a_shift, K, "A normalise-on-load");
-  std::tie(p.b_scale, p.b_shift) = norm_pair(b_scale, b_shift, N, "B normalise-on-load");
-  if (p.a_scale) TORCH_CHECK(tile == kTileStream && a_mode == OP_KC, "gemm: A normalise-on-load needs the streaming kernel");
-  if (p.b_scale)
-    TORCH_CHECK(a_mode == OP_RC && b_mode == OP_RC && epi != EPI_BF16 && K % 64 == 0 && k_split % 64 == 0,
-                "gemm: B normalise-on-load needs a plain RC x RC fp32 GEMM over whole K-tiles");
   (void)bm;
   if (tile == kTileConv3)
     TORCH_CHECK(conv3x3_halo_ok(p) && epi == EPI_BF16, "gemm conv3x3: needs a 3x3 / stride-1 / pad-1 KC_GATHER x KC "
@@ -314,8 +294,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("aux") = py::none(), py::arg("drop_p") = 0.0, py::arg("drop_seed") = 0,
         py::arg("resid_mask") = py::none(), py::arg("bnr_x") = py::none(), py::arg("bnr_mask") = py::none(),
         py::arg("bnr_mean") = py::none(), py::arg("rsub_h") = 0, py::arg("rsub_w") = 0,
-        py::arg("a_scale") = py::none(), py::arg("a_shift") = py::none(), py::arg("b_scale") = py::none(),
-        py::arg("b_shift") = py::none(), py::arg("bnr_scale") = py::none(), py::arg("bnr_shift") = py::none(),
+        py::arg("bnr_scale") = py::none(), py::arg("bnr_shift") = py::none(),
         py::arg("split_stride") = 0);
   m.def("conv3x3_wgrad", &conv3x3_wgrad, "3x3 stride-1 weight gradient (halo kernel): gw += dW", py::arg("dy"),
         py::arg("x"), py::arg("gw"), py::arg("ws"), py::arg("splits"), py::arg("tpb"), py::arg("pp") = false);

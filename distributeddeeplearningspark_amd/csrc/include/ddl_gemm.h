@@ -37,11 +37,6 @@ enum EpilogueMode : int {
   // (GemmParams::bnr_*) — the LDS-DMA GEMM and halo-conv kernels' form of the streaming kernel's BNR
   // read-out (selected by the launchers when bnr_x is set on a non-streaming tile)
   EPI_BF16_BNR = 4,
-  // EPI_BF16 (every feature) through a per-wave LDS staging area: the accumulators are written to LDS
-  // once, then a ROLLED loop walks the wave's rows with each lane owning 8 consecutive columns —
-  // 16-B bias / residual loads and 16-B bf16 stores, and a code size that does not scale with the
-  // fragment count (the unrolled EPI_BF16 epilogue is ~12-25K instructions per kernel)
-  EPI_BF16_ROW = 5,
 };
 
 constexpr int kMaxTaps = 64;
@@ -117,15 +112,6 @@ struct GemmParams {
   // data-gradient of a ResNet stride-2 1x1 downsample shortcut, added at half resolution instead of
   // being scattered (with zeros) to full resolution first
   int rsub_h, rsub_w;
-  // normalise-on-load (BatchNorm + ReLU of the PRODUCER folded into this GEMM's operand read):
-  // an operand element of channel c becomes relu(v * scale[c] + shift[c]) before the MFMA.  The channel
-  // is k for a K-contiguous A operand (a_scale: streaming kernel, A tiles transformed in LDS) and the
-  // operand row for a row-contiguous B operand (b_scale: LDS-DMA kernel, transformed in the fragment).
-  // The pre-BN tensor is then the only copy: the producer's BN-apply sweep is not run.
-  const float* a_scale;
-  const float* a_shift;
-  const float* b_scale;
-  const float* b_shift;
   // tile raster of the LDS-DMA GEMM kernel: > 1 walks groups of group_m M-tiles across all N-tiles
   // (M fastest inside a group) so the tiles resident on one XCD share fewer A rows and B columns
   // (set by launch_gemm_bf16 from DDL_GEMM_GROUP_M; 0 = row-major over the tiles)
@@ -142,9 +128,6 @@ constexpr int kStatShards = 32;
 constexpr int kTile256 = 4;     // tile id of the 256x256 ping-pong kernel (ddl_gemm256.h)
 constexpr int kTileStream = 5;  // tile id of the weight-stationary streaming kernel (gemm_stream.hip)
 constexpr int kTileConv3 = 6;   // tile id of the 3x3 stride-1 halo convolution kernel (conv3x3.hip)
-constexpr int kTileW4 = 7;      // four-wave 256x256 kernel, 128x128 per wave (ddl_gemm_w4.h)
-constexpr int kTileW4N = 8;     // four-wave 256x128 kernel, 128x64 per wave
-constexpr int kTile256P = 9;    // the 256x256 ping-pong kernel in its persistent form (one workgroup per CU)
 
 // the halo kernel applies to this (KC_GATHER x KC, 3x3 / stride 1 / pad 1) GEMM
 bool conv3x3_halo_ok(const GemmParams& p);

@@ -191,248 +191,17 @@ __global__ __launch_bounds__(g256::THREADS, 1) void gemm256_kernel(const GemmPar
 #undef DDL_G256_MMA
   if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
 
-  // (after the re-alignment every wave has issued its last fragment read: the ring is free for the row
-  // epilogue's wave-private staging areas)
-  float* wl = reinterpret_cast<float*>(smem + wid * row_epi_bytes<2>());
-  if constexpr (EPI == EPI_BF16_ROW) {  // the four quadrants through ONE rolled row epilogue
-    const int mbs[4] = {m0 + ra, m0 + ra, m0 + 128 + ra, m0 + 128 + ra};
-    const int nbs[4] = {n0 + rb, n0 + 128 + rb, n0 + rb, n0 + 128 + rb};
-    gemm_epilogue_rows<4, 4, 2>(p, reinterpret_cast<f32x4(&)[4][4][2]>(acc), mbs, nbs, lane, bid, p.M, wl);
-    return;
-  }
-  gemm_epilogue<4, 2, EPI>(p, acc[0][0], m0 + ra, n0 + rb, lane, bid, -1, wl, (long)split * p.split_stride);
-  gemm_epilogue<4, 2, EPI>(p, acc[0][1], m0 + ra, n0 + 128 + rb, lane, bid, -1, wl, (long)split * p.split_stride);
-  gemm_epilogue<4, 2, EPI>(p, acc[1][0], m0 + 128 + ra, n0 + rb, lane, bid, -1, wl, (long)split * p.split_stride);
-  gemm_epilogue<4, 2, EPI>(p, acc[1][1], m0 + 128 + ra, n0 + 128 + rb, lane, bid, -1, wl, (long)split * p.split_stride);
-}
-
-// ------------------------------------------------------------------------------------------------
-// Persistent form (tile id kTile256P): one workgroup per CU walks its output tiles bid, bid + grid, ...
-// as ONE stream of K-tiles through the same ping-pong ring, so the next tile's first K-tiles load while
-// this tile's last one computes and its epilogue stores drain (a 256x256 tile over K = 768 is 12
-// K-tiles: with one workgroup per CU the plain form exposes a prologue and an epilogue per tile).
-//   * staging sources: per-lane 32-bit byte offsets of each half computed once per tile (the plain form
-//     lets the compiler hoist them out of its K loop; here the tile changes inside the loop) over a
-//     uniform K-tile base, so each LDS-DMA costs one address add;
-//   * vmcnt counts stores too, in issue order: a tile's epilogue stores sit in the counter in front of
-//     every load issued after them.  So the next-next K-tile's B0 half is staged BEFORE the epilogue
-//     (its slot's last reads retired at the phase-4 barrier), and the following K-tile waits with
-//     vmcnt(6 + kEpiVm) — the epilogue's store count — instead of draining the stores.
-// No split-K (one K range per tile); not with the row epilogue (it stages through the ring).
-namespace g256 {
-template <int MODE>
-__device__ __forceinline__ void half_offs(long ld, int rows, int r0, int wid, int lane, uint32_t (&o)[2]) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int blk = i * 8 + wid;
-    if constexpr (MODE == OP_KC) {
-      const int row = blk * 8 + (lane >> 3);
-      const int ch = (lane & 7) ^ ((row >> 1) & 7);
-      const int gr = min(r0 + row, rows - 1);
-      o[i] = (uint32_t)(((long)gr * ld + ch * 8) * 2);
-    } else {
-      const int k = blk * 4 + (lane >> 4);
-      const int ch = (lane & 15) ^ rc_sw(k);
-      const int gc = min(r0 + ch * 8, rows - 8);
-      o[i] = (uint32_t)(((long)k * ld + gc) * 2);
-    }
-  }
-}
-template <int MODE>
-__device__ __forceinline__ const char* kbase(const bf16_t* ptr, long ld, int k0) {
-  return MODE == OP_KC ? reinterpret_cast<const char*>(ptr + k0) : reinterpret_cast<const char*>(ptr + (long)k0 * ld);
-}
-__device__ __forceinline__ void stage_o(const char* base, const uint32_t (&o)[2], char* slot, int wid) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-    __builtin_amdgcn_global_load_lds((const void*)(base + o[i]), (lds_t*)(slot + (i * 8 + wid) * 1024), 16, 0, 0);
-}
-// vector-memory instructions a full tile's epilogue issues per wave, at least: 4 quadrants x 4 x 2 fragment
-// stores (bf16x4 per lane; fp32 outputs store per element, more)
-constexpr int kEpiVm = 32;
-}  // namespace g256
-
-template <int AMODE, int BMODE, int EPI>
-__global__ __launch_bounds__(g256::THREADS, 1) void gemm256p_kernel(const GemmParams p) {
-  using namespace g256;
-  static_assert(EPI != EPI_BF16_ROW, "g256 persistent: the row epilogue stages through the ring");
-  __shared__ __attribute__((aligned(16))) char smem[8 * HALF];  // ring: [K-tile parity][A0, A1, B0, B1]
-
-  const int tiles_n = (p.N + 255) >> 8;
-  const int ntiles = ((p.M + 255) >> 8) * tiles_n;
-  int bid, split;
-  grid_tile(bid, split);
-  const int G = (int)gridDim.x;
-  const int nk = p.K >> 6;
-  const int total = (bid < ntiles ? (ntiles - 1 - bid) / G + 1 : 0) * nk;  // K-tiles of this stream
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wr = wid >> 2, wc = wid & 3;
-  const bf16_t* A = reinterpret_cast<const bf16_t*>(p.a);
-  const bf16_t* B = reinterpret_cast<const bf16_t*>(p.b);
-  auto slot = [&](int par, int h) -> char* { return smem + (par * 4 + h) * HALF; };
-
-  struct Tile {
-    int m0, n0;
-    uint32_t oa[2][2], ob[2][2];  // per-lane source offsets of the halves A0, A1, B0, B1
-  };
-  auto load_tile = [&](int i, Tile& T) {
-    int tm, tn;
-    tile_raster<256>(p, bid + i * G, tiles_n, tm, tn);
-    T.m0 = tm * 256;
-    T.n0 = tn * 256;
-    half_offs<AMODE>(p.lda, p.M, T.m0, wid, lane, T.oa[0]);
-    half_offs<AMODE>(p.lda, p.M, T.m0 + 128, wid, lane, T.oa[1]);
-    half_offs<BMODE>(p.ldb, p.N, T.n0, wid, lane, T.ob[0]);
-    half_offs<BMODE>(p.ldb, p.N, T.n0 + 128, wid, lane, T.ob[1]);
-  };
-  auto sa = [&](int kt, const uint32_t (&o)[2], char* dst) { stage_o(kbase<AMODE>(A, p.lda, kt * 64), o, dst, wid); };
-  auto sb = [&](int kt, const uint32_t (&o)[2], char* dst) { stage_o(kbase<BMODE>(B, p.ldb, kt * 64), o, dst, wid); };
-
-  f32x4 acc[2][2][4][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 ar[4][2], br[2][2];
-
-  // stream cursor of K-tile t + 2 (tile ordinal i2, its offsets T2); t and t + 1 keep what they need
-  Tile T2;
-  int kt2 = 0, i2 = 0;
-  load_tile(0, T2);
-  auto adv = [&]() {
-    if (++kt2 == nk) {
-      kt2 = 0;
-      ++i2;
-      load_tile(i2, T2);
-    }
-  };
-  if (total > 0) {  // K-tile 0 complete
-    sa(kt2, T2.oa[0], slot(0, 0));
-    sb(kt2, T2.ob[0], slot(0, 2));
-    sb(kt2, T2.ob[1], slot(0, 3));
-    sa(kt2, T2.oa[1], slot(0, 1));
-  }
-  int kt0 = kt2, mc = T2.m0, nc = T2.n0;  // K-tile t: its k index and output tile origin
-  adv();
-  if (total > 1) {  // K-tile 1's A0, B1, A1 (its B0 is staged in phase 1 of K-tile 0)
-    sa(kt2, T2.oa[0], slot(1, 0));
-    sb(kt2, T2.ob[1], slot(1, 3));
-    sa(kt2, T2.oa[1], slot(1, 1));
-    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  int kt1 = kt2, m1 = T2.m0, n1 = T2.n0;  // K-tile t + 1
-  uint32_t ob1[2] = {T2.ob[0][0], T2.ob[0][1]};
-  adv();
-  __syncthreads();
-  if (wr == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind
-
-  const int ra = wr * 64;  // this wave's first row inside an A half
-  const int rb = wc * 32;  // this wave's first column inside a B half
-
-#define DDL_G256_LOAD_A(par, h)                                                  \
-  _Pragma("unroll") for (int i = 0; i < 4; ++i)                                  \
-      _Pragma("unroll") for (int kk = 0; kk < 2; ++kk) ar[i][kk] =               \
-          frag<AMODE>(slot(par, h), ra + 16 * i, kk, lane);
-#define DDL_G256_LOAD_B(par, h)                                                  \
-  _Pragma("unroll") for (int j = 0; j < 2; ++j)                                  \
-      _Pragma("unroll") for (int kk = 0; kk < 2; ++kk) br[j][kk] =               \
-          frag<BMODE>(slot(par, h), rb + 16 * j, kk, lane);
-#define DDL_G256_MMA(QM, QN)                                                                     \
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                             \
-  __builtin_amdgcn_sched_barrier(0);                                                             \
-  __builtin_amdgcn_s_barrier();                                                                  \
-  __builtin_amdgcn_sched_barrier(0);                                                             \
-  __builtin_amdgcn_s_setprio(1);                                                                 \
-  _Pragma("unroll") for (int kk = 0; kk < 2; ++kk) _Pragma("unroll") for (int i = 0; i < 4; ++i) \
-      _Pragma("unroll") for (int j = 0; j < 2; ++j) {                                            \
-    if constexpr (epi_dt(EPI))                                                                   \
-      acc[QM][QN][i][j] = mfma16x16x32(br[j][kk], ar[i][kk], acc[QM][QN][i][j]);                 \
-    else                                                                                         \
-      acc[QM][QN][i][j] = mfma16x16x32(ar[i][kk], br[j][kk], acc[QM][QN][i][j]);                 \
-  }                                                                                              \
-  __builtin_amdgcn_s_setprio(0);                                                                 \
-  __builtin_amdgcn_sched_barrier(0);                                                             \
-  __builtin_amdgcn_s_barrier();
-
-  bool early = false;  // B0 of K-tile t + 1 was staged before the last epilogue (and vmcnt holds its stores)
-  for (int t = 0; t < total; ++t) {
-    const int par = t & 1;
-    const bool s1 = t + 1 < total, s2 = t + 2 < total;
-    // phase 1: quadrant (0,0) — reads A0, B0
-    DDL_G256_LOAD_A(par, 0)
-    DDL_G256_LOAD_B(par, 2)
-    if (s1 && !early) sb(kt1, ob1, slot(par ^ 1, 2));
-    DDL_G256_MMA(0, 0)
-    // phase 2: quadrant (0,1) — reads B1; A0 is free
-    DDL_G256_LOAD_B(par, 3)
-    if (s2) sa(kt2, T2.oa[0], slot(par, 0));
-    DDL_G256_MMA(0, 1)
-    // phase 3: quadrant (1,1) — reads A1; B1 is free
-    DDL_G256_LOAD_A(par, 1)
-    if (s2) sb(kt2, T2.ob[1], slot(par, 3));
-    DDL_G256_MMA(1, 1)
-    // phase 4: quadrant (1,0) — reads B0; A1 is free; retire K-tile t + 1
-    DDL_G256_LOAD_B(par, 2)
-    if (s2) {
-      sa(kt2, T2.oa[1], slot(par, 1));
-      if (early) asm volatile("s_waitcnt vmcnt(38)" ::: "memory");  // 6 + kEpiVm
-      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    DDL_G256_MMA(1, 0)
-    early = false;
-    if (kt0 == nk - 1) {  // the tile's last K-tile
-      if (s2) {  // B0 of K-tile t + 2 ahead of the stores (every wave's phase-4 reads of its slot retired)
-        sb(kt2, T2.ob[0], slot(par, 2));
-        early = true;
-        if (mc + 256 > p.M || nc + 256 > p.N)  // partial tile: fewer than kEpiVm stores follow
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      gemm_epilogue<4, 2, EPI>(p, acc[0][0], mc + ra, nc + rb, lane, bid);
-      gemm_epilogue<4, 2, EPI>(p, acc[0][1], mc + ra, nc + 128 + rb, lane, bid);
-      gemm_epilogue<4, 2, EPI>(p, acc[1][0], mc + 128 + ra, nc + rb, lane, bid);
-      gemm_epilogue<4, 2, EPI>(p, acc[1][1], mc + 128 + ra, nc + 128 + rb, lane, bid);
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    kt0 = kt1, mc = m1, nc = n1;
-    kt1 = kt2, m1 = T2.m0, n1 = T2.n0;
-    ob1[0] = T2.ob[0][0], ob1[1] = T2.ob[0][1];
-    adv();
-  }
-#undef DDL_G256_LOAD_A
-#undef DDL_G256_LOAD_B
-#undef DDL_G256_MMA
-  if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
+  const long coff = (long)split * p.split_stride;
+  gemm_epilogue<4, 2, EPI>(p, acc[0][0], m0 + ra, n0 + rb, lane, bid, -1, coff);
+  gemm_epilogue<4, 2, EPI>(p, acc[0][1], m0 + ra, n0 + 128 + rb, lane, bid, -1, coff);
+  gemm_epilogue<4, 2, EPI>(p, acc[1][0], m0 + 128 + ra, n0 + rb, lane, bid, -1, coff);
+  gemm_epilogue<4, 2, EPI>(p, acc[1][1], m0 + 128 + ra, n0 + 128 + rb, lane, bid, -1, coff);
 }
 
 template <int AMODE, int BMODE, int EPI>
-inline int launch_g256(const GemmParams& p, hipStream_t s, bool persist = false) {
+inline int launch_g256(const GemmParams& p, hipStream_t s) {
   const int tiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
   const int splits = (p.K + p.k_split - 1) / p.k_split;
-  if constexpr (EPI != EPI_BF16_ROW) {
-    // persistent form: un-split GEMMs with more tiles than CUs whose KC operands fit 32-bit byte offsets
-    const bool fits = (AMODE != OP_KC || (long)p.M * p.lda * 2 < (1L << 32)) &&
-                      (BMODE != OP_KC || (long)p.N * p.ldb * 2 < (1L << 32)) &&
-                      (AMODE != OP_RC || 64L * p.lda * 2 < (1L << 32)) && (BMODE != OP_RC || 64L * p.ldb * 2 < (1L << 32));
-    if (persist && splits == 1 && tiles > device_cus() && fits) {
-      hipLaunchKernelGGL((gemm256p_kernel<AMODE, BMODE, EPI>), dim3(device_cus(), 1), dim3(g256::THREADS), 0, s, p);
-      return (int)hipGetLastError();
-    }
-  }
   hipLaunchKernelGGL((gemm256_kernel<AMODE, BMODE, EPI>), dim3(tiles, splits), dim3(g256::THREADS), 0, s, p);
   return (int)hipGetLastError();
 }

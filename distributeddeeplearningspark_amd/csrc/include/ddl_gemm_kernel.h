@@ -355,11 +355,8 @@ struct Operand {
 
 // bf16-output epilogues take D^T fragments (a lane owns 4 consecutive columns of one row)
 constexpr bool epi_dt(int epi) {
-  return epi == EPI_BF16 || epi == EPI_BF16_LITE || epi == EPI_BF16_BNR || epi == EPI_BF16_ROW;
+  return epi == EPI_BF16 || epi == EPI_BF16_LITE || epi == EPI_BF16_BNR;
 }
-// per-wave LDS bytes the row epilogue stages through (16 rows of RN*16 columns, padded rows)
-template <int RN>
-constexpr int row_epi_bytes() { return 16 * (RN * 16 + 4) * 4; }
 
 // Per-column statistics of a wave's D^T fragments (lane: row lane & 15 of 16, columns nb + 16 j + 4 (lane >> 4)
 // + e) summed over the 16 rows and added to st[0][n] / st[N][n] (s1 / s2).  A butterfly reduce-scatter:
@@ -407,6 +404,31 @@ __device__ __forceinline__ void col_stats_atomics(const float (&s1)[RN][4], cons
   }
 }
 
+// Paired D^T fragments (j, j + 1) of one row <-> 16-B memory accesses.  In the D^T layout lane group
+// g = lane >> 4 holds columns 4g .. 4g + 3 of each fragment (8 B); v_permlane16_swap (odd 16-lane rows of
+// its first operand <-> even rows of its second, an involution) regroups a pair so that group g holds the
+// 8 consecutive columns 16 (g & 1) + 8 (g >> 1) .. + 7 of the 32: one 16-B access per lane instead of two
+// 8-B ones.  `base` points at the pair's first column (16-B aligned).
+__device__ __forceinline__ int pair_col(const int lane) { return 16 * ((lane >> 4) & 1) + 8 * (lane >> 5); }
+__device__ __forceinline__ void pair_store(bf16_t* base, const uint2 a, const uint2 b, const int lane) {
+  const auto sx = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
+  const auto sy = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
+  *reinterpret_cast<uint4*>(base + pair_col(lane)) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+}
+__device__ __forceinline__ void pair_load(const bf16_t* base, uint2& a, uint2& b, const int lane) {
+  const uint4 v = *reinterpret_cast<const uint4*>(base + pair_col(lane));
+  const auto sx = __builtin_amdgcn_permlane16_swap(v.x, v.z, false, false);
+  const auto sy = __builtin_amdgcn_permlane16_swap(v.y, v.w, false, false);
+  a = make_uint2(sx[0], sy[0]);
+  b = make_uint2(sx[1], sy[1]);
+}
+__device__ __forceinline__ void unpack4(const uint2 v, float (&f)[4]) {
+  f[0] = __uint_as_float(v.x << 16);
+  f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16);
+  f[3] = __uint_as_float(v.y & 0xffff0000u);
+}
+
 // EPI_BF16_BNR: bf16 store of alpha*acc (+ the residual: optional ReLU bit mask / stride-2 subgrid, as the
 // full epilogue adds it) + the BatchNorm-backward partial sums of the stored gradient (GemmParams::bnr_*),
 // accumulated like the forward statistics (16-lane shuffle, one atomic per column and shard).  Output rows
@@ -449,316 +471,138 @@ __device__ __forceinline__ void gemm_epilogue_bnr(const GemmParams& p, f32x4 (&a
       resoff[i] = rrow < 0 ? -1L : rrow * p.ldr;
     }
   }
+  // fragment pairs whose 32 columns are in range (wave-uniform) go through 16-B loads / stores
+  const bool wide = (p.ldc % 8) == 0 && (!p.resid || (p.ldr % 8) == 0) &&
+                    ((reinterpret_cast<uintptr_t>(p.c) | reinterpret_cast<uintptr_t>(p.bnr_x) |
+                      reinterpret_cast<uintptr_t>(p.resid)) & 15) == 0;
 #pragma unroll
-  for (int j = 0; j < RN; ++j) {
-    const int n = nb + 16 * j + ncol;  // host check: N % 4 == 0, so n < N covers n .. n+3
-    const bool nok = n < p.N;
-    float mu[4] = {0.f, 0.f, 0.f, 0.f}, sc[4] = {0.f, 0.f, 0.f, 0.f}, sh[4] = {0.f, 0.f, 0.f, 0.f};
-    if (nok) {
-      const float4 a = *reinterpret_cast<const float4*>(p.bnr_mean + n);
-      mu[0] = a.x; mu[1] = a.y; mu[2] = a.z; mu[3] = a.w;
-      if (p.bnr_scale) {
-        const float4 b = *reinterpret_cast<const float4*>(p.bnr_scale + n);
-        const float4 c = *reinterpret_cast<const float4*>(p.bnr_shift + n);
-        sc[0] = b.x; sc[1] = b.y; sc[2] = b.z; sc[3] = b.w;
-        sh[0] = c.x; sh[1] = c.y; sh[2] = c.z; sh[3] = c.w;
+  for (int jp = 0; jp < RN; jp += 2) {
+    if (wide && jp + 1 < RN && nb + 16 * jp + 32 <= p.N) {  // wave-uniform
+      const int j = jp;
+      float mu[2][4], sc[2][4], sh[2][4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int n = nb + 16 * (j + h) + ncol;
+        const float4 a = *reinterpret_cast<const float4*>(p.bnr_mean + n);
+        mu[h][0] = a.x; mu[h][1] = a.y; mu[h][2] = a.z; mu[h][3] = a.w;
+        if (p.bnr_scale) {
+          const float4 b = *reinterpret_cast<const float4*>(p.bnr_scale + n);
+          const float4 c = *reinterpret_cast<const float4*>(p.bnr_shift + n);
+          sc[h][0] = b.x; sc[h][1] = b.y; sc[h][2] = b.z; sc[h][3] = b.w;
+          sh[h][0] = c.x; sh[h][1] = c.y; sh[h][2] = c.z; sh[h][3] = c.w;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) sc[h][e] = sh[h][e] = 0.f;
+        }
       }
-    }
 #pragma unroll
-    for (int i = 0; i < RM; ++i) {
-      const int m = mb + 16 * i + mrow;
-      if (!nok || m >= mlim) continue;
-      const long off = rowoff[i] + n;
-      const uint2 xv = *reinterpret_cast<const uint2*>(X + off);
-      uint32_t mbits = 0xfu;
-      if (p.bnr_mask) mbits = (uint32_t)p.bnr_mask[off >> 3] >> (off & 7);
-      float rv[4] = {0.f, 0.f, 0.f, 0.f};
-      if (p.resid) {
-        if (resoff[i] >= 0) {
-          const uint2 r2 = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(p.resid) + resoff[i] + n);
-          rv[0] = __uint_as_float(r2.x << 16);
-          rv[1] = __uint_as_float(r2.x & 0xffff0000u);
-          rv[2] = __uint_as_float(r2.y << 16);
-          rv[3] = __uint_as_float(r2.y & 0xffff0000u);
-          if (p.resid_mask) {
+      for (int i = 0; i < RM; ++i) {
+        const int m = mb + 16 * i + mrow;
+        if (m >= mlim) continue;  // (partner lanes of the swaps share m)
+        const long off0 = rowoff[i] + nb + 16 * j;  // the pair's first column
+        uint2 xv[2], rr[2] = {make_uint2(0, 0), make_uint2(0, 0)};
+        pair_load(X + off0, xv[0], xv[1], lane);
+        if (p.resid && resoff[i] >= 0)
+          pair_load(reinterpret_cast<const bf16_t*>(p.resid) + resoff[i] + nb + 16 * j, rr[0], rr[1], lane);
+        uint2 ov[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int n = nb + 16 * (j + h) + ncol;
+          const long off = rowoff[i] + n;
+          uint32_t mbits = 0xfu;
+          if (p.bnr_mask) mbits = (uint32_t)p.bnr_mask[off >> 3] >> (off & 7);
+          float rv[4], x[4];
+          unpack4(rr[h], rv);
+          unpack4(xv[h], x);
+          if (p.resid && p.resid_mask && resoff[i] >= 0) {
             const long bit = (long)m * p.ldr + n;
             const uint32_t rb = (uint32_t)p.resid_mask[bit >> 3] >> (bit & 7);
 #pragma unroll
             for (int e = 0; e < 4; ++e) rv[e] = ((rb >> e) & 1u) ? rv[e] : 0.f;
           }
+          bf16_t o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            o[e] = f2bf(__fmul_rn(acc[i][j + h][e], p.alpha) + rv[e]);
+            bool keep = (mbits >> e) & 1u;
+            if (p.bnr_scale) keep = (x[e] * sc[h][e] + sh[h][e]) > 0.f;
+            const float d = keep ? bf2f(o[e]) : 0.f;
+            s1[j + h][e] += d;
+            s2[j + h][e] += d * (x[e] - mu[h][e]);
+          }
+          ov[h] = make_uint2((uint32_t)o[0] | ((uint32_t)o[1] << 16), (uint32_t)o[2] | ((uint32_t)o[3] << 16));
+        }
+        pair_store(reinterpret_cast<bf16_t*>(p.c) + off0, ov[0], ov[1], lane);
+      }
+    } else {
+#pragma unroll
+      for (int h = 0; h < 2 && jp + h < RN; ++h) {
+        const int j = jp + h;
+        const int n = nb + 16 * j + ncol;  // host check: N % 4 == 0, so n < N covers n .. n+3
+        const bool nok = n < p.N;
+        float mu[4] = {0.f, 0.f, 0.f, 0.f}, sc[4] = {0.f, 0.f, 0.f, 0.f}, sh[4] = {0.f, 0.f, 0.f, 0.f};
+        if (nok) {
+          const float4 a = *reinterpret_cast<const float4*>(p.bnr_mean + n);
+          mu[0] = a.x; mu[1] = a.y; mu[2] = a.z; mu[3] = a.w;
+          if (p.bnr_scale) {
+            const float4 b = *reinterpret_cast<const float4*>(p.bnr_scale + n);
+            const float4 c = *reinterpret_cast<const float4*>(p.bnr_shift + n);
+            sc[0] = b.x; sc[1] = b.y; sc[2] = b.z; sc[3] = b.w;
+            sh[0] = c.x; sh[1] = c.y; sh[2] = c.z; sh[3] = c.w;
+          }
+        }
+    #pragma unroll
+        for (int i = 0; i < RM; ++i) {
+          const int m = mb + 16 * i + mrow;
+          if (!nok || m >= mlim) continue;
+          const long off = rowoff[i] + n;
+          const uint2 xv = *reinterpret_cast<const uint2*>(X + off);
+          uint32_t mbits = 0xfu;
+          if (p.bnr_mask) mbits = (uint32_t)p.bnr_mask[off >> 3] >> (off & 7);
+          float rv[4] = {0.f, 0.f, 0.f, 0.f};
+          if (p.resid) {
+            if (resoff[i] >= 0) {
+              const uint2 r2 = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(p.resid) + resoff[i] + n);
+              rv[0] = __uint_as_float(r2.x << 16);
+              rv[1] = __uint_as_float(r2.x & 0xffff0000u);
+              rv[2] = __uint_as_float(r2.y << 16);
+              rv[3] = __uint_as_float(r2.y & 0xffff0000u);
+              if (p.resid_mask) {
+                const long bit = (long)m * p.ldr + n;
+                const uint32_t rb = (uint32_t)p.resid_mask[bit >> 3] >> (bit & 7);
+    #pragma unroll
+                for (int e = 0; e < 4; ++e) rv[e] = ((rb >> e) & 1u) ? rv[e] : 0.f;
+              }
+            }
+          }
+          float x[4];
+          x[0] = __uint_as_float(xv.x << 16);
+          x[1] = __uint_as_float(xv.x & 0xffff0000u);
+          x[2] = __uint_as_float(xv.y << 16);
+          x[3] = __uint_as_float(xv.y & 0xffff0000u);
+          bf16_t o[4];
+    #pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            o[e] = f2bf(__fmul_rn(acc[i][j][e], p.alpha) + rv[e]);  // (no fma contraction: the full epilogue's rounding)
+            bool keep = (mbits >> e) & 1u;
+            if (p.bnr_scale) keep = (x[e] * sc[e] + sh[e]) > 0.f;
+            const float d = keep ? bf2f(o[e]) : 0.f;
+            s1[j][e] += d;
+            s2[j][e] += d * (x[e] - mu[e]);
+          }
+          *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.c) + off) =
+              make_uint2((uint32_t)o[0] | ((uint32_t)o[1] << 16), (uint32_t)o[2] | ((uint32_t)o[3] << 16));
         }
       }
-      float x[4];
-      x[0] = __uint_as_float(xv.x << 16);
-      x[1] = __uint_as_float(xv.x & 0xffff0000u);
-      x[2] = __uint_as_float(xv.y << 16);
-      x[3] = __uint_as_float(xv.y & 0xffff0000u);
-      bf16_t o[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        o[e] = f2bf(__fmul_rn(acc[i][j][e], p.alpha) + rv[e]);  // (no fma contraction: the full epilogue's rounding)
-        bool keep = (mbits >> e) & 1u;
-        if (p.bnr_scale) keep = (x[e] * sc[e] + sh[e]) > 0.f;
-        const float d = keep ? bf2f(o[e]) : 0.f;
-        s1[j][e] += d;
-        s2[j][e] += d * (x[e] - mu[e]);
-      }
-      *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.c) + off) =
-          make_uint2((uint32_t)o[0] | ((uint32_t)o[1] << 16), (uint32_t)o[2] | ((uint32_t)o[3] << 16));
     }
   }
   col_stats_atomics<RN>(s1, s2, st, p.N, nb, lane);
 }
 
-// normalise-on-load of a fragment whose 8 values share one channel (row-contiguous B operand)
-__device__ __forceinline__ bf16x8 norm_frag(const bf16x8 f, float sc, float sh) {
-  const s16x8 v = __builtin_bit_cast(s16x8, f);
-  s16x8 o;
-#pragma unroll
-  for (int j = 0; j < 8; j += 2) {
-    const float a = fmaxf(__uint_as_float((uint32_t)(uint16_t)v[j] << 16) * sc + sh, 0.f);
-    const float b = fmaxf(__uint_as_float((uint32_t)(uint16_t)v[j + 1] << 16) * sc + sh, 0.f);
-    const uint32_t pk = pack_bf16x2(a, b);
-    o[j] = (short)(pk & 0xffffu);
-    o[j + 1] = (short)(pk >> 16);
-  }
-  return __builtin_bit_cast(bf16x8, o);
-}
-
-
-__device__ __forceinline__ void epi_unpack8(const uint4& u, float* f) {
-  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    f[2 * k] = __uint_as_float(w[k] << 16);
-    f[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
-  }
-}
-__device__ __forceinline__ uint4 epi_pack8(const float* f) {
-  return make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]), pack_bf16x2(f[6], f[7]));
-}
-
-// EPI_BF16_ROW: the full bf16 epilogue (bias / GELU fwd+bwd / dropout / residual (masked, stride-2
-// subgrid) / ReLU / statistics / output map) with the accumulators staged through a per-wave LDS area
-// (``wlds``, row_epi_bytes<RN>() bytes, wave-private).  NQ output blocks (the 256x256 kernel's four
-// quadrants; 1 elsewhere), each RM fragment rows x RN fragment columns at (mbs[q], nbs[q]).  Per block and
-// fragment row: the 16 x RN*16 accumulators go to LDS, then lane l owns the 8 columns 8 (l % LPR) of rows
-// l / LPR + k (64 / LPR): 16-B bias / residual / aux loads and 16-B bf16 stores.  The block, pass and row
-// loops are ROLLED (only the LDS writes are selected per compile-time fragment), so the code size does not
-// scale with the fragment count; element arithmetic and rounding points are those of EPI_BF16.
-template <int NQ, int RM, int RN>
-__device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, f32x4 (&acc)[NQ][RM][RN], const int (&mbs)[NQ],
-                                                   const int (&nbs)[NQ], const int lane, const int bid, const int mlim,
-                                                   float* __restrict__ wlds) {
-  constexpr int CW = RN * 16;   // columns of a block
-  constexpr int LD = CW + 4;    // padded LDS row (floats): the 16 rows of a fragment hit different banks
-  constexpr int LPR = CW / 8;   // lanes per row
-  constexpr int RPI = 64 / LPR; // rows per iteration
-  const int cl = lane % LPR, rl = lane / LPR;
-  const bool vstride_c = (p.ldc % 8) == 0;
-  const bool vstride_r = !p.resid || (p.ldr % 8) == 0;
-#pragma unroll 1
-  for (int qd = 0; qd < NQ; ++qd) {
-    int mb = mbs[0], nb = nbs[0];
-#pragma unroll
-    for (int q = 1; q < NQ; ++q)
-      if (q == qd) {
-        mb = mbs[q];
-        nb = nbs[q];
-      }
-    const int n = nb + 8 * cl;
-    const bool colfull = n + 7 < p.N;
-    const bool vec_c = colfull && vstride_c, vec_r = colfull && vstride_r;
-    float bias[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) bias[e] = 0.f;
-    if (p.bias) {
-      if (colfull && (n % 4) == 0) {
-        const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n);
-        const float4 b1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
-        bias[0] = b0.x; bias[1] = b0.y; bias[2] = b0.z; bias[3] = b0.w;
-        bias[4] = b1.x; bias[5] = b1.y; bias[6] = b1.z; bias[7] = b1.w;
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) bias[e] = (n + e < p.N) ? p.bias[n + e] : 0.f;
-      }
-    }
-    float s1[8], s2[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
-#pragma unroll 1
-    for (int pass = 0; pass < RM; ++pass) {
-      // fragment row `pass` of block qd -> LDS (D^T: the lane holds 4 consecutive columns of row lane & 15)
-#pragma unroll
-      for (int q = 0; q < NQ; ++q)
-#pragma unroll
-        for (int i = 0; i < RM; ++i)
-          if (q == qd && i == pass) {
-#pragma unroll
-            for (int j = 0; j < RN; ++j) {
-              const f32x4 a = acc[q][i][j];
-              *reinterpret_cast<float4*>(wlds + (lane & 15) * LD + 16 * j + 4 * (lane >> 4)) =
-                  make_float4(a[0] * p.alpha, a[1] * p.alpha, a[2] * p.alpha, a[3] * p.alpha);
-            }
-          }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll 1
-      for (int r = rl; r < 16; r += RPI) {
-        const int m = mb + 16 * pass + r;
-        float v[8];
-        {
-          const float4 x0 = *reinterpret_cast<const float4*>(wlds + r * LD + 8 * cl);
-          const float4 x1 = *reinterpret_cast<const float4*>(wlds + r * LD + 8 * cl + 4);
-          v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w;
-          v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
-        }
-        if (m >= mlim || n >= p.N) continue;
-        long rowoff;
-        int nn = 0, ii = 0, jj = 0;
-        if (p.om.enabled) {
-          pix_decompose((uint32_t)m, p.om.gh, p.om.gw, nn, ii, jj);
-          rowoff = ((long)(nn * p.om.hy + ii * p.om.so + p.om.oh) * p.om.wy + jj * p.om.so + p.om.ow) * p.ldc;
-        } else {
-          rowoff = (long)m * p.ldc;
-        }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += bias[e];
-        if (p.relu >= ACT_GELU) {
-          bf16_t* ax = reinterpret_cast<bf16_t*>(p.aux) + (long)m * p.ldc + n;
-          if (p.relu == ACT_GELU) {
-            float pa[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              pa[e] = bf2f(f2bf(v[e]));
-              v[e] = gelu_f(pa[e]);
-            }
-            if (vec_c) {
-              *reinterpret_cast<uint4*>(ax) = epi_pack8(pa);
-            } else {
-              for (int e = 0; e < 8; ++e)
-                if (n + e < p.N) ax[e] = f2bf(pa[e]);
-            }
-          } else {
-            float pre[8];
-            if (vec_c) {
-              epi_unpack8(*reinterpret_cast<const uint4*>(ax), pre);
-            } else {
-#pragma unroll
-              for (int e = 0; e < 8; ++e) pre[e] = (n + e < p.N) ? bf2f(ax[e]) : 0.f;
-            }
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] *= (n + e < p.N) ? gelu_grad_f(pre[e]) : 0.f;
-          }
-        }
-        if (p.drop_thresh) {
-          const unsigned long long base = (unsigned long long)m * (unsigned long long)p.N + (unsigned long long)n;
-          const uint32_t kb = drop_bits8(p.drop_seed, base, p.drop_thresh);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = ((kb >> e) & 1u) ? v[e] * p.drop_scale : 0.f;
-        }
-        if (p.resid) {
-          long rrow = m;
-          if (p.rsub_h) {
-            int rn_, ri_, rj_;
-            pix_decompose((uint32_t)m, p.rsub_h, p.rsub_w, rn_, ri_, rj_);
-            rrow = ((ri_ | rj_) & 1)
-                       ? -1L
-                       : ((long)rn_ * ((p.rsub_h + 1) >> 1) + (ri_ >> 1)) * ((p.rsub_w + 1) >> 1) + (rj_ >> 1);
-          }
-          if (rrow >= 0) {
-            const bf16_t* rp = reinterpret_cast<const bf16_t*>(p.resid) + rrow * p.ldr + n;
-            float rv[8];
-            if (vec_r) {
-              epi_unpack8(*reinterpret_cast<const uint4*>(rp), rv);
-            } else {
-#pragma unroll
-              for (int e = 0; e < 8; ++e) rv[e] = (n + e < p.N) ? bf2f(rp[e]) : 0.f;
-            }
-            if (p.resid_mask) {  // bits n .. n+7 of the row's mask (n % 8 == 0: one byte)
-              const long bit = (long)m * p.ldr + n;
-              const uint32_t mbits = (uint32_t)p.resid_mask[bit >> 3] >> (bit & 7);
-#pragma unroll
-              for (int e = 0; e < 8; ++e) rv[e] = ((mbits >> e) & 1u) ? rv[e] : 0.f;
-            }
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] += rv[e];
-          }
-        }
-        if (p.relu == ACT_RELU) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-        }
-        float o[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          o[e] = bf2f(f2bf(v[e]));
-          const float rr = (n + e < p.N) ? o[e] : 0.f;
-          s1[e] += rr;
-          s2[e] += rr * rr;
-        }
-        bf16_t* c = reinterpret_cast<bf16_t*>(p.c) + rowoff + n;
-        if (vec_c) {
-          *reinterpret_cast<uint4*>(c) = epi_pack8(o);
-        } else {
-          for (int e = 0; e < 8; ++e)
-            if (n + e < p.N) c[e] = f2bf(o[e]);
-        }
-        if (p.om.enabled && p.om.zero_siblings) {  // this class is the only one with taps: zero the rest
-          bf16_t* cb = reinterpret_cast<bf16_t*>(p.c);
-          for (int a = 0; a < p.om.so; ++a) {
-            const int hy = ii * p.om.so + a;
-            if (hy >= p.om.hy) break;
-            for (int b = 0; b < p.om.so; ++b) {
-              const int wy = jj * p.om.so + b;
-              if (wy >= p.om.wy || (a == p.om.oh && b == p.om.ow)) continue;
-              bf16_t* z = cb + ((long)(nn * p.om.hy + hy) * p.om.wy + wy) * p.ldc + n;
-              if (vec_c) {
-                *reinterpret_cast<uint4*>(z) = make_uint4(0, 0, 0, 0);
-              } else {
-                for (int e = 0; e < 8; ++e)
-                  if (n + e < p.N) z[e] = 0;
-              }
-            }
-          }
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_wave_barrier();  // every lane read this pass before the next overwrites the area
-    }
-    if (p.stats) {  // lanes sharing cl hold the same 8 columns: reduce over the row lanes, one atomic per column
-      float* st = p.stats + (long)(bid % kStatShards) * 2 * p.N;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float a = s1[e], b = s2[e];
-#pragma unroll
-        for (int o = LPR; o < 64; o <<= 1) {
-          a += __shfl_xor(a, o, 64);
-          b += __shfl_xor(b, o, 64);
-        }
-        if (rl == 0 && n + e < p.N) {
-          atomicAdd(st + n + e, a);
-          atomicAdd(st + p.N + n + e, b);
-        }
-      }
-    }
-  }
-}
-
-// Epilogue shared by the GEMM kernels.  mb / nb: first row / column of this wave's
-// RM x RN fragment block; rows >= mend (default p.M) are not stored (tile-local row limits of
-// the halo conv kernel).  bf16 epilogue: acc holds D^T fragments (lane owns 4 consecutive
-// columns of one row); fp32 epilogues: D fragments (16 consecutive columns per row).
 template <int RM, int RN, int EPI>
 __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[RM][RN], const int mb, const int nb,
-                                              const int lane, const int bid, int mend = -1, float* wlds = nullptr,
-                                              long coff = 0) {
+                                              const int lane, const int bid, int mend = -1, long coff = 0) {
   const int mlim = mend < 0 ? p.M : mend;
-  if constexpr (EPI == EPI_BF16_ROW) {
-    const int mbs[1] = {mb}, nbs[1] = {nb};
-    gemm_epilogue_rows<1, RM, RN>(p, reinterpret_cast<f32x4(&)[1][RM][RN]>(acc), mbs, nbs, lane, bid, mlim, wlds);
-    return;
-  }
   if constexpr (EPI == EPI_BF16_BNR) {
     gemm_epilogue_bnr<RM, RN>(p, acc, mb, nb, lane, bid, mlim);
     return;
@@ -798,6 +642,10 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
 #pragma unroll
     for (int e = 0; e < 4; ++e) s1[j][e] = s2[j][e] = 0.f;
   const bool vec_ok = (p.ldc % 4) == 0 && (LITE || !p.resid || (p.ldr % 4) == 0);
+  // bf16 outputs: fragment pairs (j, j + 1) whose 32 columns are all in range leave as ONE 16-B store per
+  // lane (8 consecutive columns) after a v_permlane16_swap: the epilogue's store tail is bound by store
+  // INSTRUCTIONS issued (the same bytes in half the instructions)
+  const bool wide_ok = BF && (p.ldc % 8) == 0 && (reinterpret_cast<uintptr_t>(p.c) & 15) == 0;
   // bias of this lane's columns, loaded once: inside the row loop the compiler must re-load it
   // after every output store (p.bias may alias p.c), 4 * RM * RN dependent loads per lane
   // (one 16-B load per fragment column group where the 4 columns are in range: n % 4 == 0 and the
@@ -821,6 +669,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
   for (int i = 0; i < RM; ++i) {
     const int m = mb + 16 * i + mrow;
     if (m >= mlim) continue;
+    uint2 pk[RN];  // this row's packed bf16x4 per fragment (BF), stored after the column loop
     long rowoff;
     int nn = 0, ii = 0, jj = 0;
     if (!LITE && p.om.enabled) {
@@ -919,9 +768,14 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
           s2[j][e] += rr * rr;
         }
         bf16_t* c = reinterpret_cast<bf16_t*>(p.c) + rowoff + n;
-        if (full) {
-          *reinterpret_cast<uint2*>(c) = make_uint2((uint32_t)o[0] | ((uint32_t)o[1] << 16),
-                                                    (uint32_t)o[2] | ((uint32_t)o[3] << 16));
+        pk[j] = make_uint2((uint32_t)o[0] | ((uint32_t)o[1] << 16), (uint32_t)o[2] | ((uint32_t)o[3] << 16));
+        if (wide_ok && (j & 1) == 0 && j + 1 < RN && nb + 16 * j + 32 <= p.N) {
+          // stored with fragment j + 1 below
+        } else if (wide_ok && (j & 1) == 1 && nb + 16 * j + 16 <= p.N) {
+          // pair (j - 1, j), wave-uniform condition (pair_store)
+          pair_store(reinterpret_cast<bf16_t*>(p.c) + rowoff + nb + 16 * (j - 1), pk[j - 1], pk[j], lane);
+        } else if (full) {
+          *reinterpret_cast<uint2*>(c) = pk[j];
         } else {
 #pragma unroll
           for (int e = 0; e < 4; ++e)
@@ -991,104 +845,12 @@ __device__ __forceinline__ void tile_raster(const GemmParams& p, int bid, int ti
   }
 }
 
-template <int BM, int BN, int AMODE, int BMODE, int EPI>
-__global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const GemmParams p) {
-  constexpr int WTM = BM / 2, WTN = BN / 2;
-  constexpr int RM = WTM / 16, RN = WTN / 16;
-  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  constexpr int TAPB = tap_table_bytes<AMODE, BMODE>();
-  char* smem = smem_raw + TAPB;
-  const bool one_stage = p.k_split <= BK;  // must match launch_tile's LDS allocation
-  char* lds_a0 = smem;
-  char* lds_a1 = smem + A_BYTES;
-  char* lds_b0 = smem + (one_stage ? A_BYTES : 2 * A_BYTES);
-  char* lds_b1 = smem + 2 * A_BYTES + B_BYTES;
-
-  const int tiles_n = (p.N + BN - 1) / BN;
-  int bid, split;
-  grid_tile(bid, split);
-  int tm, tn;
-  tile_raster<BM>(p, bid, tiles_n, tm, tn);
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int kbeg = split * p.k_split;
-  const int kend = min(p.K, kbeg + p.k_split);
-  const int nk = (kend - kbeg + BK - 1) / BK;
-
-  const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
-  const int wm0 = (wid >> 1) * WTM, wn0 = (wid & 1) * WTN;
-
-  Operand<BM, AMODE> A;
-  Operand<BN, BMODE> B;
-  if constexpr (TAPB > 0) {
-    load_tap_table(reinterpret_cast<int*>(smem_raw), p.g);
-    A.tt = (const DDL_LDS int*)(smem_raw);
-    B.tt = (const DDL_LDS int*)(smem_raw);
-  }
-  A.init(p.a, p.lda, p.M, m0, p.K, p.g, kbeg);
-  B.init(p.b, p.ldb, p.N, n0, p.K, p.g, kbeg);
-
-  f32x4 acc[RM][RN];
-#pragma unroll
-  for (int i = 0; i < RM; ++i)
-#pragma unroll
-    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  if (nk > 0) {
-    A.load(kbeg, p.g, p.b_kdiv, p.b_tap_stride);
-    B.load(kbeg, p.g, p.b_kdiv, p.b_tap_stride);
-    A.store(lds_a0);
-    B.store(lds_b0);
-    __syncthreads();
-  }
-  for (int t = 0; t < nk; ++t) {
-    const bool odd = t & 1;
-    const char* la = odd ? lds_a1 : lds_a0;
-    const char* lb = odd ? lds_b1 : lds_b0;
-    const bool more = t + 1 < nk;
-    if (more) {
-      A.load(kbeg + (t + 1) * BK, p.g, p.b_kdiv, p.b_tap_stride);
-      B.load(kbeg + (t + 1) * BK, p.g, p.b_kdiv, p.b_tap_stride);
-    }
-#pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk) {
-      bf16x8 af[RM], bf[RN];
-#pragma unroll
-      for (int i = 0; i < RM; ++i) af[i] = A.frag(la, kk, i, wm0, lane);
-#pragma unroll
-      for (int j = 0; j < RN; ++j) bf[j] = B.frag(lb, kk, j, wn0, lane);
-#pragma unroll
-      for (int i = 0; i < RM; ++i)
-#pragma unroll
-        for (int j = 0; j < RN; ++j) {
-          if constexpr (epi_dt(EPI))
-            acc[i][j] = mfma16x16x32(bf[j], af[i], acc[i][j]);  // D^T: 4 consecutive n per lane (vector stores)
-          else
-            acc[i][j] = mfma16x16x32(af[i], bf[j], acc[i][j]);  // D: 16 consecutive n per row (coalesced atomics)
-        }
-    }
-    if (more) {
-      A.store(odd ? lds_a0 : lds_a1);
-      B.store(odd ? lds_b0 : lds_b1);
-    }
-    __syncthreads();
-  }
-
-  gemm_epilogue<RM, RN, EPI>(p, acc, m0 + wm0, n0 + wn0, lane, bid, -1,
-                             reinterpret_cast<float*>(smem + wid * row_epi_bytes<RN>()), (long)split * p.split_stride);
-}
-
-// LDS-DMA variant of the same kernel: identical tiles, operand modes, fragments and epilogue,
-// but the K-tiles are staged with global_load_lds (Operand::dma: no VGPR round trip, no VALU
-// pack, the LDS swizzle moved to the source address; padding and out-of-range vectors read
-// ddl_zero_page).  ST = 1: one LDS stage per block (32 KB at 128x128, so 4 blocks share a CU
-// and each block's load latency hides under the others' MFMAs); ST = 2: two stages, the next
-// K-tile's DMA in flight under the current tile's MFMAs (counted vmcnt, raw barriers).
-// BNORM (row-contiguous B only): GemmParams::b_scale / b_shift normalise every B fragment (one channel
-// per lane and fragment: 2 registers per fragment column, loaded once) — a weight gradient reading the
-// pre-BatchNorm output of the layer below instead of its applied copy.
-template <int BM, int BN, int AMODE, int BMODE, int EPI, int ST, bool BNORM = false>
+// The K-tiles are staged with global_load_lds (Operand::dma: no VGPR round trip, no VALU pack, the LDS
+// swizzle moved to the source address; padding and out-of-range vectors read ddl_zero_page).
+// ST = 1: one LDS stage per block (32 KB at 128x128, so 4 blocks share a CU and each block's load
+// latency hides under the others' MFMAs); ST = 3: a 3-slot ring with one barrier per K-tile (the plain
+// fp32 weight gradients at 2 workgroups per CU, too few for co-resident blocks alone to hide the DMA).
+template <int BM, int BN, int AMODE, int BMODE, int EPI, int ST>
 __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_kernel(const GemmParams p) {
   constexpr int WTM = BM / 2, WTN = BN / 2;
   constexpr int RM = WTM / 16, RN = WTN / 16;
@@ -1121,21 +883,8 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
   }
   A.init(p.a, p.lda, p.M, m0, p.K, p.g, kbeg);
   B.init(p.b, p.ldb, p.N, n0, p.K, p.g, kbeg);
-  static_assert(!BNORM || BMODE == OP_RC, "normalise-on-load: row-contiguous B only");
-  float bsc[BNORM ? RN : 1], bsh[BNORM ? RN : 1];
-  if constexpr (BNORM) {
-#pragma unroll
-    for (int j = 0; j < RN; ++j) {
-      const int n = min(n0 + wn0 + 16 * j + (lane & 15), p.N - 1);
-      bsc[j] = p.b_scale[n];
-      bsh[j] = p.b_shift[n];
-    }
-  }
-  auto bfrag = [&](const char* lb, int kk, int j) {
-    const bf16x8 f = B.frag(lb, kk, j, wn0, lane);
-    if constexpr (BNORM) return norm_frag(f, bsc[j], bsh[j]);
-    else return f;
-  };
+  static_assert(ST == 1 || ST == 3, "stages: 1 or a 3-slot ring");
+  auto bfrag = [&](const char* lb, int kk, int j) { return B.frag(lb, kk, j, wn0, lane); };
 
   f32x4 acc[RM][RN];
 #pragma unroll
@@ -1191,9 +940,7 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
       }
       slot = slot + 1 == ST ? 0 : slot + 1;
     }
-    if constexpr (EPI == EPI_BF16_ROW) __syncthreads();  // the ring slots become the staging area
-    gemm_epilogue<RM, RN, EPI>(p, acc, m0 + wm0, n0 + wn0, lane, bid, -1,
-                               reinterpret_cast<float*>(smem + wid * row_epi_bytes<RN>()), (long)split * p.split_stride);
+    gemm_epilogue<RM, RN, EPI>(p, acc, m0 + wm0, n0 + wn0, lane, bid, -1, (long)split * p.split_stride);
     return;
   }
   if (nk > 0) {
@@ -1201,20 +948,9 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
     B.dma(stage(0) + A_BYTES, kbeg, p.g, p.b_kdiv, p.b_tap_stride, wid);
   }
   for (int t = 0; t < nk; ++t) {
-    const char* la = stage(ST == 2 ? (t & 1) : 0);
+    const char* la = stage(0);
     const char* lb = la + A_BYTES;
-    if constexpr (ST == 2) {
-      if (t + 1 < nk) {  // refill the stage read in iteration t - 1 (freed by its closing barrier)
-        char* nx = stage((t + 1) & 1);
-        A.dma(nx, kbeg + (t + 1) * BK, p.g, p.b_kdiv, p.b_tap_stride, wid);
-        B.dma(nx + A_BYTES, kbeg + (t + 1) * BK, p.g, p.b_kdiv, p.b_tap_stride, wid);
-        wait_vmcnt<VA + VB>();  // this wave's tile-t DMAs done, tile t+1 still in flight
-      } else {
-        wait_vmcnt<0>();
-      }
-    } else {
-      wait_vmcnt<0>();
-    }
+    wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();  // every wave's tile-t DMAs have landed
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
@@ -1235,50 +971,13 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every wave is done reading this stage
-    if constexpr (ST == 1) {
-      if (t + 1 < nk) {
-        A.dma(smem, kbeg + (t + 1) * BK, p.g, p.b_kdiv, p.b_tap_stride, wid);
-        B.dma(smem + A_BYTES, kbeg + (t + 1) * BK, p.g, p.b_kdiv, p.b_tap_stride, wid);
-      }
+    if (t + 1 < nk) {
+      A.dma(smem, kbeg + (t + 1) * BK, p.g, p.b_kdiv, p.b_tap_stride, wid);
+      B.dma(smem + A_BYTES, kbeg + (t + 1) * BK, p.g, p.b_kdiv, p.b_tap_stride, wid);
     }
   }
 
-  // (ST 1 / 2: the loop's closing barrier already freed the stages for the row epilogue's staging area)
-  gemm_epilogue<RM, RN, EPI>(p, acc, m0 + wm0, n0 + wn0, lane, bid, -1,
-                             reinterpret_cast<float*>(smem + wid * row_epi_bytes<RN>()), (long)split * p.split_stride);
-}
-
-// DDL_GEMM_DMA: 0 = register-staged kernel, 1 = LDS-DMA single stage (default), 2 = LDS-DMA double stage
-inline int gemm_dma_mode() {
-  static int mode = -1;
-  if (mode < 0) {
-    const char* e = getenv("DDL_GEMM_DMA");
-    mode = e ? atoi(e) : 1;
-  }
-  return mode;
-}
-
-// LDS ring depth of the fp32-output (weight-gradient) kernels, forced by DDL_WGRAD_STAGES: 1 = the
-// single-stage kernel, 3 / 4 = the one-barrier ring with 2 / 3 K-tiles in flight; unset = default.  These kernels run at 2
-// blocks per CU, too few for co-resident blocks alone to hide the LDS-DMA latency.
-inline int stages_env(const char* name) {
-  const char* e = getenv(name);
-  int st = e ? atoi(e) : 0;  // 0: per-operand-mode default (launch_tile)
-  return (st == 1 || st == 3 || st == 4) ? st : 0;
-}
-inline int wgrad_stages() {
-  static const int st = stages_env("DDL_WGRAD_STAGES");
-  return st;
-}
-// the same for the plain bf16-output kernels (default 1: single stage, 4 workgroups per CU)
-inline int gemm_stages() {
-  static const int st = stages_env("DDL_GEMM_STAGES");
-  return st;
-}
-// the same for the gathered fp32 kernels only (conv weight gradients, split-K small-grid forward)
-inline int gather_stages() {
-  static const int st = stages_env("DDL_GATHER_STAGES");
-  return st;
+  gemm_epilogue<RM, RN, EPI>(p, acc, m0 + wm0, n0 + wn0, lane, bid, -1, (long)split * p.split_stride);
 }
 
 inline int device_cus() {
@@ -1291,89 +990,46 @@ inline int device_cus() {
   return cus;
 }
 
-template <int BM, int BN, int AMODE, int BMODE, int EPI, int ST, bool BNORM = false>
-inline int launch_ring(const dim3 grid, const GemmParams& p, hipStream_t s) {
-  constexpr int lds = ST * (BM + BN) * BK * 2 + tap_table_bytes<AMODE, BMODE>();
-  static bool attr = [] {  // dynamic LDS above 64 KB must be allowed explicitly
-    return lds <= 65536 ||
-           hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_dma_kernel<BM, BN, AMODE, BMODE, EPI, ST, BNORM>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
-  }();
-  (void)attr;
-  hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, AMODE, BMODE, EPI, ST, BNORM>), grid, dim3(NTHREADS), lds, s, p);
-  return (int)hipGetLastError();
-}
-
-template <int BM, int BN, int AMODE, int BMODE, int EPI, bool BNORM = false>
+template <int BM, int BN, int AMODE, int BMODE, int EPI>
 inline int launch_tile(const GemmParams& p, hipStream_t s) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
   const int splits = (p.K + p.k_split - 1) / p.k_split;
-  // single K-tile (1x1 convs with K <= 64): one LDS stage -> twice the resident blocks per CU
-  const bool one_stage = p.k_split <= BK;
   const dim3 grid(tiles, splits > 0 ? splits : 1);
-  const int dm = gemm_dma_mode();
-  if constexpr (EPI == EPI_F32 || EPI == EPI_F32_ATOMIC) {
-    // default: the 3-slot ring for plain (1x1 / Linear) weight gradients on 64x128 / 128x64 tiles
-    // (72 KB: still 2 workgroups per CU), measured 10-25 % faster on the ResNet-50 1x1 layers; not on
-    // 128x128 tiles (96 KB -> 1 workgroup per CU: BERT-base 664K -> 630K tokens/s) nor on the
-    // gathered (3x3 / strided) weight gradients (ring 30 % slower there)
-    constexpr bool plain_tile = AMODE == OP_RC && BMODE == OP_RC && BM * BN < 128 * 128;
-    // ... and only when the grid is one round at 2 workgroups per CU (the ring's 72 KB of LDS): a
-    // longer grid (BERT's weight gradients: 576 workgroups) runs 4 single-stage workgroups per CU
-    const bool plain = plain_tile && (long)grid.x * grid.y <= 2L * device_cus();
-    const int st = one_stage ? 1
-                             : (wgrad_stages() ? wgrad_stages()
-                                               : (plain ? 3 : (gather_stages() ? gather_stages() : 1)));
-    if (dm == 1 && st == 3) return launch_ring<BM, BN, AMODE, BMODE, EPI, 3, BNORM>(grid, p, s);
-    if (dm == 1 && st == 4) return launch_ring<BM, BN, AMODE, BMODE, EPI, 4, BNORM>(grid, p, s);
-  } else if constexpr (AMODE == OP_KC || AMODE == OP_RC) {
-    // DDL_GEMM_STAGES=3/4: the one-barrier LDS ring for the plain bf16-output GEMMs too (A/B)
-    const int st = one_stage ? 1 : gemm_stages();
-    if (dm == 1 && st == 3) return launch_ring<BM, BN, AMODE, BMODE, EPI, 3, BNORM>(grid, p, s);
-    if (dm == 1 && st == 4) return launch_ring<BM, BN, AMODE, BMODE, EPI, 4, BNORM>(grid, p, s);
-  }
   constexpr int TAPB = tap_table_bytes<AMODE, BMODE>();
-  if (dm == 1 || (dm == 2 && one_stage)) {
-    hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, AMODE, BMODE, EPI, 1, BNORM>), grid, dim3(NTHREADS),
-                       (BM + BN) * BK * 2 + TAPB, s, p);
-  } else if (dm == 2) {
-    hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, AMODE, BMODE, EPI, 2, BNORM>), grid, dim3(NTHREADS),
-                       2 * (BM + BN) * BK * 2 + TAPB, s, p);
-  } else if (BNORM) {
-    return (int)hipErrorInvalidValue;  // the register-staged kernel has no normalise-on-load
-  } else {
-    const size_t lds = (one_stage ? 1 : 2) * (BM + BN) * BK * 2 + TAPB;
-    hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, AMODE, BMODE, EPI>), grid, dim3(NTHREADS), lds, s, p);
+  if constexpr (AMODE == OP_RC && BMODE == OP_RC && BM * BN < 128 * 128 && (EPI == EPI_F32 || EPI == EPI_F32_ATOMIC)) {
+    // the 3-slot ring for plain (1x1 / Linear) weight gradients on 64x128 / 128x64 tiles (72 KB: 2 workgroups
+    // per CU), measured 10-25 % faster on the ResNet-50 1x1 layers; only when the grid is one round at 2
+    // workgroups per CU and there is more than one K-tile (BERT's longer weight-gradient grids run 4
+    // single-stage workgroups per CU; 128x128 tiles would drop to 1 workgroup per CU with the ring)
+    if (p.k_split > BK && (long)grid.x * grid.y <= 2L * device_cus()) {
+      constexpr int lds = 3 * (BM + BN) * BK * 2 + TAPB;
+      static bool attr = [] {  // dynamic LDS above 64 KB must be allowed explicitly
+        return lds <= 65536 ||
+               hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_dma_kernel<BM, BN, AMODE, BMODE, EPI, 3>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
+      }();
+      (void)attr;
+      hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, AMODE, BMODE, EPI, 3>), grid, dim3(NTHREADS), lds, s, p);
+      return (int)hipGetLastError();
+    }
   }
+  hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, AMODE, BMODE, EPI, 1>), grid, dim3(NTHREADS), (BM + BN) * BK * 2 + TAPB,
+                     s, p);
   return (int)hipGetLastError();
 }
 
-// DDL_GEMM_ROW_EPI=1: the full bf16 epilogue runs as the LDS-staged row epilogue (EPI_BF16_ROW)
-inline bool row_epilogue() {
-  static const bool on = [] {
-    const char* e = getenv("DDL_GEMM_ROW_EPI");
-    return e && atoi(e) == 1;
-  }();
-  return on;
-}
-
 // The bf16 epilogue features a call uses beyond bias / ReLU / statistics.
-// DDL_GEMM_FULL_EPI=1 forces the full instantiation (A/B of the epilogue's code size on plain GEMMs).
 inline bool needs_full_epilogue(const GemmParams& p) {
-  static const bool force = [] {
-    const char* e = getenv("DDL_GEMM_FULL_EPI");
-    return e && atoi(e) == 1;
-  }();
-  return force || p.om.enabled || p.resid || p.aux || p.drop_thresh || p.relu > ACT_RELU;
+  return p.om.enabled || p.resid || p.aux || p.drop_thresh || p.relu > ACT_RELU;
 }
 
-template <int AMODE, int BMODE, int EPI, bool BNORM = false>
+template <int AMODE, int BMODE, int EPI>
 inline int launch_modes(const GemmParams& p, int tile, hipStream_t s) {
   switch (tile) {
-    case 0: return launch_tile<128, 128, AMODE, BMODE, EPI, BNORM>(p, s);
-    case 1: return launch_tile<128, 64, AMODE, BMODE, EPI, BNORM>(p, s);
-    case 2: return launch_tile<64, 128, AMODE, BMODE, EPI, BNORM>(p, s);
-    default: return launch_tile<64, 64, AMODE, BMODE, EPI, BNORM>(p, s);
+    case 0: return launch_tile<128, 128, AMODE, BMODE, EPI>(p, s);
+    case 1: return launch_tile<128, 64, AMODE, BMODE, EPI>(p, s);
+    case 2: return launch_tile<64, 128, AMODE, BMODE, EPI>(p, s);
+    default: return launch_tile<64, 64, AMODE, BMODE, EPI>(p, s);
   }
 }
 

@@ -172,6 +172,44 @@ int embed_bwd(const int64_t* ids, const int64_t* types, const void* ds, float* g
 // xw: [B][T][G*H] input projections (incl. bias) or nullptr: then the fast path (H = 64/128,
 // I <= 8) computes x W + b in-kernel from x [B][T][I], W [I][G*H], b (nullable);
 // hs/cs: [B][T+1][H]; gates: [B][T][G*H] post-activation
+// Replica-batched recurrent step (parallel/replica_batch.py): R co-located dist-keras workers whose models
+// are RNN(H) -> Dense(K) with an MSE loss step as ONE launch per phase.  Replica r owns global batch
+// rows [r B, (r+1) B) of every activation buffer; parameters, gradients, optimizer state and the resident
+// shard are its own (pointer tables).  The replicas step in lockstep: one device step counter.
+constexpr int kMaxRnnRep = 8;
+struct RnnRep {
+  const float* x[kMaxRnnRep];  // resident input shard [nb B][T][I]
+  const float* y[kMaxRnnRep];  // resident target shard [nb B][K]
+  const float* W[kMaxRnnRep];  // [I][GH]
+  const float* U[kMaxRnnRep];  // [H][GH]
+  const float* b[kMaxRnnRep];  // [GH] or null
+  const float* Wd[kMaxRnnRep]; // Dense kernel [K][H]
+  const float* bd[kMaxRnnRep]; // Dense bias [K] or null
+  float* gW[kMaxRnnRep];
+  float* gU[kMaxRnnRep];
+  float* gb[kMaxRnnRep];
+  float* gWd[kMaxRnnRep];
+  float* gbd[kMaxRnnRep];
+  float* hist[kMaxRnnRep];     // per-replica loss history [cap]
+  int* ctr;                    // device step counter (batch index = ctr % nb, history slot = ctr)
+  int nb, B, K, cap;
+};
+struct OptRep {
+  float* w[kMaxRnnRep];
+  const float* g[kMaxRnnRep];
+  float* s1[kMaxRnnRep];       // adagrad accumulator / adam m / sgd momentum (or null)
+  float* s2[kMaxRnnRep];       // adam v
+  float* t[kMaxRnnRep];        // adam device step counters
+};
+// one training step of the R replicas: rnn forward, Dense + MSE forward / backward (+ loss record, Adam
+// step tick), rnn backward, recurrent parameter gradients, optimizer (+ step counter advance); buffers:
+// hs / cs / gates / dgates [R B][T(+1)][..], h_last / dh [R B][H].  opt: 0 sgd, 1 adagrad, 2 adam (mode bits
+// of adam_step in amode).
+int rnn_replica_step(int cell, const RnnRep& rp, int R, int T, int H, int I, float* hs, float* cs, float* gates,
+                     float* hlast, float* dh, float* dgates, const OptRep& op, long n, int opt, float lr, float p1,
+                     float p2, float eps, float wd, int amode, hipStream_t s);
+bool rnn_replica_ok(int cell, int H, int I, int K, int B);
+
 bool rnn_fast_path(int H);
 bool rnn_fuses_input(int H, int I);
 // the register-resident kernels apply for this (cell, H, activations)

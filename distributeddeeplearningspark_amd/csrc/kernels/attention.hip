@@ -637,10 +637,8 @@ __global__ __launch_bounds__(THREADS, MINB) void attn_bwd_dq_kernel(const AttnPa
 
 }  // namespace
 
-static int attn_xcd() {
-  static const int v = getenv("DDL_ATTN_XCD") ? atoi(getenv("DDL_ATTN_XCD")) : 1;
-  return v;
-}
+// XCD-aware block remap (attn_block): the S / 128 blocks of one sequence-head share an XCD's L2
+static int attn_xcd() { return 1; }
 
 #define DDL_ATTN_LAUNCH(KERNEL, grid, MINB, drop, s, p)                                   \
   do {                                                                                   \
@@ -654,10 +652,7 @@ int attn_fwd(const AttnParams& p_in, hipStream_t s) {
   p.xcd_remap = attn_xcd();
   const dim3 grid(p.S / BLOCK_ROWS, p.H, p.B);
   const bool drop = p.drop_t8 != 0;
-  static const int occ = getenv("DDL_ATTN_FWD_OCC") ? atoi(getenv("DDL_ATTN_FWD_OCC")) : 2;
-  if (occ == 2) DDL_ATTN_LAUNCH(attn_fwd_kernel, grid, 2, drop, s, p);
-  else if (occ == 4) DDL_ATTN_LAUNCH(attn_fwd_kernel, grid, 4, drop, s, p);
-  else DDL_ATTN_LAUNCH(attn_fwd_kernel, grid, 3, drop, s, p);
+  DDL_ATTN_LAUNCH(attn_fwd_kernel, grid, 2, drop, s, p);  // 2 workgroups per CU (measured vs 3 / 4)
   return (int)hipGetLastError();
 }
 
@@ -669,12 +664,8 @@ int attn_bwd(const AttnParams& p_in, hipStream_t s) {
   const dim3 grid(p.S / BLOCK_ROWS, p.H, p.B);
   const bool drop = p.drop_t8 != 0;
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s, p, rows);
-  static const int dkdv_occ = getenv("DDL_ATTN_DKDV_OCC") ? atoi(getenv("DDL_ATTN_DKDV_OCC")) : 2;
-  if (dkdv_occ == 1) DDL_ATTN_LAUNCH(attn_bwd_dkdv_kernel, grid, 1, drop, s, p);
-  else DDL_ATTN_LAUNCH(attn_bwd_dkdv_kernel, grid, 2, drop, s, p);
-  static const int dq_occ = getenv("DDL_ATTN_DQ_OCC") ? atoi(getenv("DDL_ATTN_DQ_OCC")) : 2;
-  if (dq_occ == 3) DDL_ATTN_LAUNCH(attn_bwd_dq_kernel, grid, 3, drop, s, p);
-  else DDL_ATTN_LAUNCH(attn_bwd_dq_kernel, grid, 2, drop, s, p);
+  DDL_ATTN_LAUNCH(attn_bwd_dkdv_kernel, grid, 2, drop, s, p);
+  DDL_ATTN_LAUNCH(attn_bwd_dq_kernel, grid, 2, drop, s, p);
   return (int)hipGetLastError();
 }
 

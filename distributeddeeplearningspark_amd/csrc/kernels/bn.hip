@@ -197,12 +197,7 @@ static dim3 col_grid(long M, int C) {
   const int CV = C >> 3, CT = CV < 256 ? CV : 256, RT = 256 / CT;
   const int gy = (CV + CT - 1) / CT;
   long gx = M / (16L * RT);
-  static const int cap = [] {  // DDL_BN_PARTIALS: experiments (<= kMaxPartials * 8)
-    const char* e = getenv("DDL_BN_PARTIALS");
-    const int v = e ? atoi(e) : kMaxPartials;
-    return v >= 16 && v <= 8 * kMaxPartials ? v : kMaxPartials;
-  }();
-  if (gx > cap) gx = cap;
+  if (gx > kMaxPartials) gx = kMaxPartials;
   if (gx < 1) gx = 1;
   return dim3((unsigned)gx, (unsigned)gy);
 }
@@ -380,19 +375,12 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint4* __restrict__
   }
 }
 
-// workgroup cap of a streaming sweep (DDL_BN_GRID: A/B knob).  Default: no cap — one workgroup per 2 x RT rows,
+// workgroup cap of a streaming sweep: effectively none — one workgroup per 2 x RT rows,
 // every lane's loads issued at once and never a second grid-stride trip.  The former 4,096-workgroup cap
 // (grid-stride loops) measured slower at every value: ResNet-50 11,914-11,928 (4,096) -> 12,018-12,049 (8,192)
 // -> 12,106-12,144 (16,384) -> 12,166-12,195 (32,768) -> 12,203-12,217 img/s (65,536 = uncapped at ResNet-50's
 // shapes), interleaved (profiles/r4/fuse_bn/ab_bn_grid.txt)
-static long bn_grid_cap() {
-  static const long cap = [] {
-    const char* e = getenv("DDL_BN_GRID");
-    const long v = e ? atol(e) : (1L << 24);
-    return v >= 256 && v <= (1L << 24) ? v : (1L << 24);
-  }();
-  return cap;
-}
+static long bn_grid_cap() { return 1L << 24; }
 
 static dim3 stream_grid(long M, int C, int rows = 2) {
   const int CV = C >> 3, CT = CV < 256 ? CV : 256, RT = 256 / CT;
@@ -403,24 +391,15 @@ static dim3 stream_grid(long M, int C, int rows = 2) {
   return dim3((unsigned)(gx > 0 ? gx : 1), (unsigned)gy);
 }
 
-// rows in flight per lane of the apply / dx sweeps: DDL_BN_ROWS = 2 (default) or 4 (A/B knob, read per
-// launch so a test can switch it)
-static int bn_rows() {
-  const char* e = getenv("DDL_BN_ROWS");
-  return e && atoi(e) == 4 ? 4 : 2;
-}
-// nontemporal output stores in those sweeps (default; DDL_BN_NT=0: plain stores, read per launch):
-// ResNet-50 11,785 / 11,805 vs 11,703 / 11,688 img/s interleaved (profiles/r3/bn_sweeps/ab_bnnt.jsonl)
-static bool bn_nt() {
-  const char* e = getenv("DDL_BN_NT");
-  return !(e && atoi(e) == 0);
-}
+// 2 rows in flight per lane of the apply / dx sweeps (4 measured within noise or slower:
+// profiles/r4/ab_bn_rows_stem_partials.txt) and nontemporal output stores (plain stores: ResNet-50
+// 11,703 / 11,688 vs 11,785 / 11,805 img/s interleaved, profiles/r3/bn_sweeps/ab_bnnt.jsonl)
+constexpr int kBnRows = 2;
 
 int bn_apply(const void* x, const float* scale, const float* shift, const void* resid, void* y, void* mask, long M,
              int C, int relu, hipStream_t s, const float* res_scale, const float* res_shift) {
-  const int rows = bn_rows();
-  auto k = rows == 4 ? (bn_nt() ? bn_apply_kernel<4, true> : bn_apply_kernel<4, false>)
-                     : (bn_nt() ? bn_apply_kernel<2, true> : bn_apply_kernel<2, false>);
+  const int rows = kBnRows;
+  auto k = bn_apply_kernel<kBnRows, true>;
   hipLaunchKernelGGL(k, stream_grid(M, C, rows), dim3(256), 0, s, (const uint4*)x, scale, shift, (const uint4*)resid,
                      (uint4*)y, (uint8_t*)mask, M, C, relu, res_scale, res_shift);
   return (int)hipGetLastError();
@@ -625,16 +604,14 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const uint4* __restrict_
 int bn_bwd_dx(const void* dy, const void* x, const void* y, const float* scale, const float* shift, const float* coef,
               void* dx, void* dres, long M, int C, int mode, hipStream_t s, const void* x2, const float* mean2,
               float* ws2) {
-  const int rows = bn_rows();
+  const int rows = kBnRows;
   if (x2) {  // fused second-BN reduce: partial row per block, so the reduction's grid (S = bn_partial_rows)
-    auto k = rows == 4 ? (bn_nt() ? bn_bwd_dx_kernel<4, true, true> : bn_bwd_dx_kernel<4, false, true>)
-                       : (bn_nt() ? bn_bwd_dx_kernel<2, true, true> : bn_bwd_dx_kernel<2, false, true>);
+    auto k = bn_bwd_dx_kernel<kBnRows, true, true>;
     hipLaunchKernelGGL(k, col_grid(M, C), dim3(256), 0, s, (const uint4*)dy, (const uint4*)x, (const uint4*)y, scale,
                        shift, coef, (uint4*)dx, (uint4*)dres, M, C, mode, (const uint4*)x2, mean2, ws2);
     return (int)hipGetLastError();
   }
-  auto k = rows == 4 ? (bn_nt() ? bn_bwd_dx_kernel<4, true, false> : bn_bwd_dx_kernel<4, false, false>)
-                     : (bn_nt() ? bn_bwd_dx_kernel<2, true, false> : bn_bwd_dx_kernel<2, false, false>);
+  auto k = bn_bwd_dx_kernel<kBnRows, true, false>;
   hipLaunchKernelGGL(k, stream_grid(M, C, rows), dim3(256), 0, s, (const uint4*)dy, (const uint4*)x, (const uint4*)y,
                      scale, shift, coef, (uint4*)dx, (uint4*)dres, M, C, mode, (const uint4*)nullptr,
                      (const float*)nullptr, (float*)nullptr);

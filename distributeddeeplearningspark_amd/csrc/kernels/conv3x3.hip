@@ -48,7 +48,7 @@ struct Conv3Tiling {
 // FR * 16): 8 covers a full 256-pixel tile; 7 serves the 196-pixel tiles every ResNet-50 stage
 // plans (7 rows of 28, one 14x14 image, four 7x7 images) — with 8 the second pixel wave spent 3 of
 // its 8 fragments on rows past the tile, so every tap paid 16 MFMA blocks for 12.25 of work.
-template <int BN, int EPI, int NB, int FR = 8, bool PRIO = false>
+template <int BN, int EPI, int NB, int FR = 8>
 __global__ __launch_bounds__(NTHREADS, 2) void conv3x3_halo_kernel(const GemmParams p, const Conv3Tiling t) {
   constexpr int RN = BN / 32;  // channel fragments per wave (2 waves along N)
   constexpr int B_BYTES = BN * BK * 2;
@@ -155,12 +155,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv3x3_halo_kernel(const GemmPar
         const int ch = kk * 4 + (lane >> 4);
         af[i] = *reinterpret_cast<const bf16x8*>(halo + row * 128 + ((ch ^ (row & 6)) << 4));
       }
-      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < FR; ++i)
 #pragma unroll
         for (int j = 0; j < RN; ++j) acc[i][j] = mfma16x16x32(bfr[j], af[i], acc[i][j]);  // D^T (bf16 epilogue)
-      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     }
     if (NB == 2 || tap == 8) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -198,248 +196,24 @@ Conv3Tiling plan(const GemmParams& p, int max_px = 256) {
   return t;
 }
 
-// ------------------------------------------------------------------------------------------------
-// 64 -> 64 channel 3x3 / stride-1 convolution (the forward, and the data-gradient through the flipped
-// filter: ResNet-50 stage 1, VGG-16's first block) — the halo kernel above re-stages the weights per
-// tap and, with a single 64-channel chunk, cannot amortise its halo prologue, so these layers ran on the
-// gathered implicit GEMM at ~0.25 of roofline (123 / 141 us per forward / data-gradient at 56 x 56 x 256).
-// Here the WHOLE filter (9 taps x 64 x 64 bf16 = 72 KB) stays resident in LDS, loaded once per
-// workgroup, and one 512-thread workgroup per CU ping-pongs two halo buffers over pixel tiles: half A
-// computes a tile (9 taps x 2 k-steps x 7-8 x 2 MFMAs per wave, no barrier inside) while half B's halo
-// DMA lands, then the roles swap — one workgroup barrier per tile.  Each half stores its own tile
-// through the GEMM epilogue (bias / ReLU / BN statistics, or the fused BN-backward reduce).
-// Halo image chunk-major [8 chunks][SC rows][16 B], SC = hr rounded up to 16: a fragment's ds_read_b128
-// serves 16 consecutive rows of one chunk per lane group (256 contiguous bytes), conflict-free with no
-// swizzle, so a tap shift is a ds_read immediate (WW is a template parameter).  The LDS-DMA fills 64
-// rows of one chunk per wave-instruction; lanes past SC are masked off (EXEC) so a chunk's last group
-// never writes into the next chunk's image.  LDS: 72 KB + 2 x 8 x SC x 16 B = 160 KB at SC = 352.
-constexpr int C64_W_BYTES = 9 * 64 * 128;
-
-template <int WW, int FR, int EPI>
-__global__ __launch_bounds__(512, 1) void conv3x3_c64_pp_kernel(const GemmParams p, const Conv3Tiling t, int tpb) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int SC = (t.hr + 15) & ~15;
-  const int HB = 8 * SC * 16;
-  const ConvGeom& g = p.g;
-  const int H = g.hi, W = g.wi, C = g.c, N = g.n;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int grp = __builtin_amdgcn_readfirstlane(wid >> 2), w4 = wid & 3;
-  const int wm = w4 >> 1, wn0 = (w4 & 1) * 32;
-  char* wl = smem;
-  char* halo = smem + C64_W_BYTES + grp * HB;
-  const int ntiles = t.tiles_img * t.tiles_row;
-  const int tp_beg = blockIdx.x * tpb, nt = max(0, min(ntiles, tp_beg + tpb) - tp_beg);
-
-  // the filter, once: tap image = 64 co rows x 128 B (the Operand<64, OP_KC> image: chunk ^ (row >> 1) & 7)
-  {
-    const bf16_t* w = reinterpret_cast<const bf16_t*>(p.b);
-    const int row = threadIdx.x >> 3;
-    const int kc = (threadIdx.x & 7) ^ ((row >> 1) & 7);
-    const uint32_t wl_lds = lds_addr(wl) + (uint32_t)__builtin_amdgcn_readfirstlane(wid) * 1024u;
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap) dma16(w + (long)row * p.ldb + tap * C + kc * 8, wl_lds + (uint32_t)(tap * 8192));
-  }
-  // tile-independent halo-row decode of this lane's DMA rows (64 rows of one chunk per instruction)
-  constexpr int MAXG = 6;  // SC <= 384
-  const int ngrp = (SC + 63) / 64;
-  int hcode[MAXG];
-#pragma unroll
-  for (int gi = 0; gi < MAXG; ++gi) {
-    const int hrow = gi * 64 + lane;
-    hcode[gi] = -1;
-    if (gi < ngrp && hrow < t.hr) {
-      const int im = hrow / (t.hh * WW);
-      const int rem = hrow - im * t.hh * WW;
-      const int hy = rem / WW, hx = rem - hy * WW;
-      hcode[gi] = (im << 20) | (hy << 10) | hx;
-    }
-  }
-  const uint32_t halo_lds = lds_addr(halo);
-  auto stage = [&](int tp) {  // this half's 4 waves: chunks w4 and w4 + 4
-    const int timg = tp / t.tiles_row, trow = tp - timg * t.tiles_row;
-    const int img0 = timg * t.img, oy0 = trow * t.rows;
-    const bf16_t* x = reinterpret_cast<const bf16_t*>(p.a);
-#pragma unroll
-    for (int gi = 0; gi < MAXG; ++gi) {
-      if (gi < ngrp) {
-        const int code = hcode[gi];
-        const int n = img0 + (code >> 20), iy = oy0 + ((code >> 10) & 1023) - 1, ix = (code & 1023) - 1;
-        const bool ok = code >= 0 && n < N && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
-        const bf16_t* src = x + ((n * H + iy) * W + ix) * C;
-        if (gi * 64 + lane < SC) {  // EXEC-masked: never past this chunk's image
-#pragma unroll
-          for (int h2 = 0; h2 < 2; ++h2) {
-            const int c = w4 + 4 * h2;
-            dma16(ok ? (const void*)(src + c * 8) : (const void*)ddl_zero_page,
-                  halo_lds + (uint32_t)__builtin_amdgcn_readfirstlane(c * SC * 16 + gi * 1024));
-          }
-        }
-      }
-    }
-  };
-
-  // per-lane fragment offsets: A = 16 consecutive pixel rows of chunk kk*4 + (lane >> 4); B = the KC frag
-  int abase[FR];
-#pragma unroll
-  for (int i = 0; i < FR; ++i) {
-    const int px = wm * (16 * FR) + 16 * i + (lane & 15);
-    int r = 0;  // beyond the tile: row 0, never stored (mend)
-    if (px < t.P) {
-      const int im = px / (t.rows * t.w);
-      const int rem = px - im * t.rows * t.w;
-      const int oy = rem / t.w, ox = rem - oy * t.w;
-      r = im * t.hh * WW + oy * WW + ox;
-    }
-    abase[i] = (lane >> 4) * SC * 16 + r * 16;
-  }
-  int boffs[2][2];
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int row = wn0 + 16 * j + (lane & 15);
-      const int chunk = kk * 4 + (lane >> 4);
-      boffs[kk][j] = row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
-    }
-
-  f32x4 acc[FR][2];
-  auto zero = [&] {
-#pragma unroll
-    for (int i = 0; i < FR; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  };
-  zero();
-  // one tile: 18 (tap, k-step) steps, software-pipelined — step s+1's A / B fragments are read before step
-  // s's MFMAs (a wave is alone on its SIMD in the computing half, so nothing else hides LDS latency)
-  auto load = [&](int st, bf16x8 (&af)[FR], bf16x8 (&bfr)[2]) {
-    const int tap = st >> 1, kk = st & 1;
-    const int toff = ((tap / 3) * WW + (tap % 3)) * 16;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(wl + tap * 8192 + boffs[kk][j]);
-#pragma unroll
-    for (int i = 0; i < FR; ++i) af[i] = *reinterpret_cast<const bf16x8*>(halo + abase[i] + kk * 4 * SC * 16 + toff);
-  };
-  auto mma = [&](const bf16x8 (&af)[FR], const bf16x8 (&bfr)[2]) {
-#pragma unroll
-    for (int i = 0; i < FR; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = mfma16x16x32(bfr[j], af[i], acc[i][j]);  // D^T (bf16 epilogue)
-  };
-  auto compute = [&] {
-    bf16x8 a0[FR], b0[2], a1[FR], b1[2];
-    load(0, a0, b0);
-#pragma unroll
-    for (int st = 0; st < 18; st += 2) {
-      load(st + 1, a1, b1);
-      mma(a0, b0);
-      __builtin_amdgcn_sched_barrier(0);
-      if (st + 2 < 18) load(st + 2, a0, b0);
-      mma(a1, b1);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  auto epilogue = [&](int tp) {
-    const int timg = tp / t.tiles_row, trow = tp - timg * t.tiles_row;
-    const long m0 = ((long)timg * t.img * H + (long)trow * t.rows) * W;
-    const int mend = (int)min((long)p.M, m0 + t.P);
-    gemm_epilogue<FR, 2, EPI>(p, acc, (int)m0 + wm * (16 * FR), wn0, lane, blockIdx.x, mend);
-    zero();
-  };
-
-  // phase ph: half (ph & 1) computes tile ph; the other half stores tile ph - 1 (its epilogue deferred
-  // off the MFMA critical path) and waits for its tile ph + 1, staged right after the previous barrier
-  if (grp < nt) stage(tp_beg + grp);
-  wait_vmcnt<0>();  // the filter (every wave's share) and each half's first tile
-  __syncthreads();
-  for (int ph = 0; ph <= nt; ++ph) {
-    const bool mine = (ph & 1) == grp;
-    if (mine) {
-      if (ph < nt) compute();
-    } else {
-      if (ph >= 1) epilogue(tp_beg + ph - 1);
-      wait_vmcnt<0>();
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (mine && ph + 2 < nt) stage(tp_beg + ph + 2);  // this half's halo buffer is free again
-  }
-}
-
-template <int WW, int FR, int EPI>
-int launch_c64_v(const GemmParams& p, const Conv3Tiling& t, int tpb, int blocks, hipStream_t s) {
-  const int SC = (t.hr + 15) & ~15;
-  const size_t lds = C64_W_BYTES + 2 * 8 * SC * 16;
-  static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_c64_pp_kernel<WW, FR, EPI>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
-  }();
-  (void)attr;
-  hipLaunchKernelGGL((conv3x3_c64_pp_kernel<WW, FR, EPI>), dim3(blocks), dim3(512), lds, s, p, t, tpb);
-  return (int)hipGetLastError();
-}
-
-// instantiated: 56 x 56 (ResNet-50 stage 1, FR 7) and 32 x 32 (VGG-16 CIFAR block 1, FR 8)
-int c64_variant(const GemmParams& p, const Conv3Tiling& t) {
-  const ConvGeom& g = p.g;
-  if (g.c != 64 || p.N != 64 || (C64_W_BYTES + 2 * 8 * ((t.hr + 15) & ~15) * 16) > 160 * 1024) return -1;
-  if (t.ww == 58 && t.P <= 224 && t.P > 192) return 0;
-  if (t.ww == 34 && t.P <= 256 && t.P > 224) return 1;
-  return -1;
-}
-
-template <int EPI>
-int launch_c64(const GemmParams& p, const Conv3Tiling& t, hipStream_t s) {
-  const int ntiles = t.tiles_img * t.tiles_row;
-  static const int cus = [] {
-    int dev = 0, n = 256;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    return n;
-  }();
-  const int tpb = (ntiles + cus - 1) / cus;
-  const int blocks = (ntiles + tpb - 1) / tpb;
-  switch (c64_variant(p, t)) {
-    case 0: return launch_c64_v<58, 7, EPI>(p, t, tpb, blocks, s);
-    case 1: return launch_c64_v<34, 8, EPI>(p, t, tpb, blocks, s);
-    default: return (int)hipErrorInvalidValue;
-  }
-}
-
-template <int BN, int EPI, int NB, int FR, bool PRIO>
-int launch_fr_p(const GemmParams& p, const Conv3Tiling& t, hipStream_t s) {
+template <int BN, int EPI, int NB, int FR>
+int launch_fr(const GemmParams& p, const Conv3Tiling& t, hipStream_t s) {
   const int blocks = t.tiles_img * t.tiles_row * ((p.N + BN - 1) / BN);
   const size_t lds = (size_t)t.hr_pad * 128 + NB * BN * BK * 2;
   static bool attr = [] {  // dynamic LDS above 64 KB must be allowed explicitly (at most 96 KB here)
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_halo_kernel<BN, EPI, NB, FR, PRIO>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_halo_kernel<BN, EPI, NB, FR>),
                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                C3_MAX_HALO_ROWS * 128 + NB * BN * BK * 2) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL((conv3x3_halo_kernel<BN, EPI, NB, FR, PRIO>), dim3(blocks), dim3(NTHREADS), lds, s, p, t);
+  hipLaunchKernelGGL((conv3x3_halo_kernel<BN, EPI, NB, FR>), dim3(blocks), dim3(NTHREADS), lds, s, p, t);
   return (int)hipGetLastError();
-}
-
-int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e && e[0] ? atoi(e) : dflt;
-}
-
-// DDL_CONV3X3_PRIO=1: raise the wave priority over the MFMA block (experiment knob)
-template <int BN, int EPI, int NB, int FR>
-int launch_fr(const GemmParams& p, const Conv3Tiling& t, hipStream_t s) {
-  static const bool prio = env_int("DDL_CONV3X3_PRIO", 0) == 1;
-  return prio ? launch_fr_p<BN, EPI, NB, FR, true>(p, t, s) : launch_fr_p<BN, EPI, NB, FR, false>(p, t, s);
 }
 
 // fragments per pixel wave: the fewest that cover half the tile (7 for the 196-pixel ResNet tiles)
 template <int BN, int EPI, int NB>
 int launch(const GemmParams& p, const Conv3Tiling& t, hipStream_t s) {
-  static const bool fr_off = [] {  // DDL_CONV3X3_FR8=1: always 8 fragments (A/B knob)
-    const char* e = getenv("DDL_CONV3X3_FR8");
-    return e && e[0] == '1';
-  }();
-  if (!fr_off && t.P <= 2 * 16 * 7) return launch_fr<BN, EPI, NB, 7>(p, t, s);
+  if (t.P <= 2 * 16 * 7) return launch_fr<BN, EPI, NB, 7>(p, t, s);
   return launch_fr<BN, EPI, NB, 8>(p, t, s);
 }
 
@@ -996,17 +770,9 @@ int launch_conv3x3(const GemmParams& p, int epi, hipStream_t s) {
   const Conv3Tiling t = plan(p);
   // 64-channel tiles when 128 would leave the chip under-filled or the output has 64 channels
   const int tiles_px = t.tiles_img * t.tiles_row;
-  static const int force_bn = [] {  // DDL_CONV3X3_BN=64|128: experiments
-    const char* e = getenv("DDL_CONV3X3_BN");
-    return e ? atoi(e) : 0;
-  }();
-  const bool bn128 = p.N % 128 == 0 && (force_bn ? force_bn == 128 : (long)tiles_px * (p.N / 128) >= 2L * 256);
-  static const int nb128 = env_int("DDL_CONV3X3_NB", 2);  // 3: third weight slot (1 workgroup per CU)
-  static const bool c64pp = env_int("DDL_CONV3X3_C64PP", 1) == 1;
-  if (c64pp && c64_variant(p, t) >= 0)
-    return p.bnr_x ? launch_c64<EPI_BF16_BNR>(p, t, s) : launch_c64<EPI_BF16_LITE>(p, t, s);
+  const bool bn128 = p.N % 128 == 0 && (long)tiles_px * (p.N / 128) >= 2L * 256;
   if (p.bnr_x) return bn128 ? launch<128, EPI_BF16_BNR, 2>(p, t, s) : launch<64, EPI_BF16_BNR, 3>(p, t, s);
-  if (bn128) return nb128 == 3 ? launch<128, EPI_BF16_LITE, 3>(p, t, s) : launch<128, EPI_BF16_LITE, 2>(p, t, s);
+  if (bn128) return launch<128, EPI_BF16_LITE, 2>(p, t, s);
   return launch<64, EPI_BF16_LITE, 3>(p, t, s);
 }
 

@@ -8,15 +8,13 @@ int launch_gemm_plain_akc(const GemmParams& p, int epi, int tile, hipStream_t s)
   if (p.b_mode == OP_KC) {
     if (epi == EPI_BF16)
       return !needs_full_epilogue(p) ? launch_modes<OP_KC, OP_KC, EPI_BF16_LITE>(p, tile, s)
-                                     : (row_epilogue() ? launch_modes<OP_KC, OP_KC, EPI_BF16_ROW>(p, tile, s)
-                                                       : launch_modes<OP_KC, OP_KC, EPI_BF16>(p, tile, s));
+                                     : launch_modes<OP_KC, OP_KC, EPI_BF16>(p, tile, s);
     if (epi == EPI_F32) return launch_modes<OP_KC, OP_KC, EPI_F32>(p, tile, s);
     return launch_modes<OP_KC, OP_KC, EPI_F32_ATOMIC>(p, tile, s);
   }
   if (epi == EPI_BF16)
     return !needs_full_epilogue(p) ? launch_modes<OP_KC, OP_RC, EPI_BF16_LITE>(p, tile, s)
-                                   : (row_epilogue() ? launch_modes<OP_KC, OP_RC, EPI_BF16_ROW>(p, tile, s)
-                                                     : launch_modes<OP_KC, OP_RC, EPI_BF16>(p, tile, s));
+                                   : launch_modes<OP_KC, OP_RC, EPI_BF16>(p, tile, s);
   if (epi == EPI_F32) return launch_modes<OP_KC, OP_RC, EPI_F32>(p, tile, s);
   return launch_modes<OP_KC, OP_RC, EPI_F32_ATOMIC>(p, tile, s);
 }

@@ -7,11 +7,6 @@ int launch_gemm_plain_arc(const GemmParams& p, int epi, int tile, hipStream_t s)
     if (epi == EPI_F32) return launch_modes<OP_RC, OP_KC, EPI_F32>(p, tile, s);
     return launch_modes<OP_RC, OP_KC, EPI_F32_ATOMIC>(p, tile, s);
   }
-  if (p.b_scale) {  // weight gradient reading a pre-BN activation (normalise-on-load of B)
-    if (epi == EPI_F32) return launch_modes<OP_RC, OP_RC, EPI_F32, true>(p, tile, s);
-    if (epi == EPI_F32_ATOMIC) return launch_modes<OP_RC, OP_RC, EPI_F32_ATOMIC, true>(p, tile, s);
-    return (int)hipErrorInvalidValue;
-  }
   if (epi == EPI_BF16) return launch_modes<OP_RC, OP_RC, EPI_BF16>(p, tile, s);
   if (epi == EPI_F32) return launch_modes<OP_RC, OP_RC, EPI_F32>(p, tile, s);
   return launch_modes<OP_RC, OP_RC, EPI_F32_ATOMIC>(p, tile, s);

@@ -102,12 +102,9 @@ __device__ __forceinline__ void stage_a(const bf16_t* __restrict__ A, long lda, 
 
 }  // namespace gst
 
-// ANORM: GemmParams::a_scale / a_shift — each landed A tile is normalised in place in LDS (BN affine +
-// ReLU of the layer that produced A) before any wave reads its fragments: thread t owns logical 16-B
-// chunk t % CPR (8 channels, parameters in registers) of rows t / CPR, t / CPR + 256 / CPR, ...
 // BNR: 0 off; 1 the ReLU mask of the BN-backward reduce from GemmParams::bnr_mask (bits, or all ones);
 // 2 recomputed from the BN input as x * bnr_scale + bnr_shift > 0 (a BN without residual: mode 2)
-template <int WN, int K, int BMODE, bool RES, int BNR = 0, bool ANORM = false>
+template <int WN, int K, int BMODE, bool RES, int BNR = 0>
 __global__ __launch_bounds__(gst::THREADS, 2) void gemm_stream_kernel(const GemmParams p) {
   using namespace gst;
   using CF = Cfg<WN, K>;
@@ -150,14 +147,6 @@ __global__ __launch_bounds__(gst::THREADS, 2) void gemm_stream_kernel(const Gemm
     bias_r[rn][1] = bv.y;
     bias_r[rn][2] = bv.z;
     bias_r[rn][3] = bv.w;
-  }
-  float nsc[8], nsh[8];
-  if constexpr (ANORM) {  // this thread's 8 channels of A (fixed logical chunk)
-    const int c8 = (threadIdx.x % CF::CPR) * 8;
-    const float4 a0 = *reinterpret_cast<const float4*>(p.a_scale + c8), a1 = *reinterpret_cast<const float4*>(p.a_scale + c8 + 4);
-    const float4 b0 = *reinterpret_cast<const float4*>(p.a_shift + c8), b1 = *reinterpret_cast<const float4*>(p.a_shift + c8 + 4);
-    nsc[0] = a0.x; nsc[1] = a0.y; nsc[2] = a0.z; nsc[3] = a0.w; nsc[4] = a1.x; nsc[5] = a1.y; nsc[6] = a1.z; nsc[7] = a1.w;
-    nsh[0] = b0.x; nsh[1] = b0.y; nsh[2] = b0.z; nsh[3] = b0.w; nsh[4] = b1.x; nsh[5] = b1.y; nsh[6] = b1.z; nsh[7] = b1.w;
   }
   wait_vm<0>();  // B fragments and bias in registers before the LDS-DMA ring starts
   auto tile_m0 = [&](int i) { return min((int)blockIdx.x + i * (int)gridDim.x, mt - 1) * BM; };
@@ -244,26 +233,6 @@ __global__ __launch_bounds__(gst::THREADS, 2) void gemm_stream_kernel(const Gemm
     __builtin_amdgcn_s_barrier();  // tile i visible to every wave; previous read-out finished
 
     const char* abuf = smem + (i % CF::NBUF) * CF::TILE;
-    if constexpr (ANORM) {
-      char* ab = smem + (i % CF::NBUF) * CF::TILE;
-      const int lc = threadIdx.x % CF::CPR;
-#pragma unroll
-      for (int rr = threadIdx.x / CF::CPR; rr < BM; rr += THREADS / CF::CPR) {
-        uint4* q = reinterpret_cast<uint4*>(ab + rr * (K * 2) + ((lc ^ sw<CF::CPR>(rr)) << 4));
-        const uint4 v = *q;
-        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-        uint32_t o[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float lo = fmaxf(__uint_as_float(w4[e] << 16) * nsc[2 * e] + nsh[2 * e], 0.f);
-          const float hi = fmaxf(__uint_as_float(w4[e] & 0xffff0000u) * nsc[2 * e + 1] + nsh[2 * e + 1], 0.f);
-          o[e] = pack_bf16x2(lo, hi);
-        }
-        *q = make_uint4(o[0], o[1], o[2], o[3]);
-      }
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the normalised tile is in LDS
-      __builtin_amdgcn_s_barrier();
-    }
     f32x4 acc[BM / 16][CF::RN];
 #pragma unroll
     for (int mb = 0; mb < BM / 16; ++mb)
@@ -402,11 +371,7 @@ int launch_ws(const GemmParams& p, hipStream_t s) {
   const int panels = p.N / CF::NB;
   const int mt = (p.M + gst::BM - 1) / gst::BM;
   const int gx = std::max(1, std::min(mt, 2 * num_cus() / std::max(1, panels)));
-  if (p.a_scale) {  // normalise-on-load of A (no residual / BN-reduce variants: a forward conv)
-    if (p.resid || p.bnr_x) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL((gemm_stream_kernel<WN, K, BMODE, false, 0, true>), dim3(gx, panels), dim3(gst::THREADS), 0, s,
-                       p);
-  } else if (p.bnr_x && p.bnr_scale) {  // mode 2 (no residual: a BN + ReLU without a shortcut)
+  if (p.bnr_x && p.bnr_scale) {  // mode 2 (no residual: a BN + ReLU without a shortcut)
     if (p.resid) return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL((gemm_stream_kernel<WN, K, BMODE, false, 2>), dim3(gx, panels), dim3(gst::THREADS), 0, s, p);
   } else if (p.bnr_x) {
@@ -459,7 +424,6 @@ int launch_gemm_stream(const GemmParams& p, int epi, hipStream_t s) {
   // the fused BN-backward reduction prefetches x and the mask per read-out vector: narrower panels keep
   // those variants spill-free (128 wide up to K = 128, 64 at K = 256; A is re-read once more per panel)
   if (p.bnr_x && nb > (p.K >= 256 ? 64 : 128)) nb = p.K >= 256 ? 64 : 128;
-  if (p.a_scale && p.K >= 128 && nb > 128) nb = 128;  // normalise-on-load parameters: the 256 x 128 variant spills
   const bool ok = nb && epi == EPI_BF16 && p.a_mode == OP_KC && (p.b_mode == OP_KC || p.b_mode == OP_RC) &&
                   !p.om.enabled && !p.aux && !p.drop_thresh && (p.relu == ACT_NONE || p.relu == ACT_RELU) &&
                   p.beta == 0.f && p.k_split >= p.K && p.lda % 8 == 0 && p.ldc % 8 == 0 &&
@@ -468,8 +432,7 @@ int launch_gemm_stream(const GemmParams& p, int epi, hipStream_t s) {
                   (p.b_mode == OP_RC || (uintptr_t)p.b % 16 == 0) && (!p.resid || (uintptr_t)p.resid % 8 == 0) &&
                   (!p.bnr_x || (p.stats && (uintptr_t)p.bnr_x % 16 == 0 && (uintptr_t)p.bnr_mean % 16 == 0)) &&
                   (!p.bnr_scale || (p.bnr_shift && !p.resid && (uintptr_t)p.bnr_scale % 16 == 0 &&
-                                    (uintptr_t)p.bnr_shift % 16 == 0)) &&
-                  (!p.a_scale || (p.a_shift && (uintptr_t)p.a_scale % 16 == 0 && (uintptr_t)p.a_shift % 16 == 0));
+                                    (uintptr_t)p.bnr_shift % 16 == 0));
   if (!ok) return (int)hipErrorInvalidValue;
   return p.b_mode == OP_KC ? launch_panel<OP_KC>(p, nb, s) : launch_panel<OP_RC>(p, nb, s);
 }

@@ -555,49 +555,27 @@ constexpr int kLnBwdBlocks = 512;  // 2 waves/SIMD: LN bwd 48 -> 37 us per BERT 
 
 }  // namespace
 
-// DDL_LN_PREFETCH=0 selects the row-serial LayerNorm sweeps (A/B knob; read once per process)
-static bool ln_prefetch() {
-  static const bool on = [] {
-    const char* e = std::getenv("DDL_LN_PREFETCH");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 int layernorm_fwd(const void* x, const float* gamma, const float* beta, void* y, float* mean, float* rstd, long M,
                   int H, float eps, float drop_p, unsigned long long seed, hipStream_t s) {
   if (M <= 0) return 0;
   const uint32_t th = drop_t8(drop_p);
   const float ds = drop_scale8(th);
   const int nv = H / 8;
-  const bool PF = ln_prefetch();
-  // grid-stride: gamma / beta loaded once per wave (DDL_LN_FWD_BLOCKS: experiment knob, read once)
-  static const long cap = [] {
-    const char* e = std::getenv("DDL_LN_FWD_BLOCKS");
-    const long v = e ? std::atol(e) : 0;
-    return v > 0 ? v : 2048L;
-  }();
-  const dim3 grid((unsigned)std::min<long>((M + 3) / 4, cap));
+  // grid-stride: gamma / beta loaded once per wave
+  const dim3 grid((unsigned)std::min<long>((M + 3) / 4, 2048L));
   auto X = reinterpret_cast<const bf16_t*>(x);
   auto Y = reinterpret_cast<bf16_t*>(y);
-  if (nv <= 64) { if (PF) hipLaunchKernelGGL((ln_fwd_kernel<1, true>), grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed); else hipLaunchKernelGGL((ln_fwd_kernel<1, false>), grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed); }
-  else if (nv <= 128) { if (PF) hipLaunchKernelGGL((ln_fwd_kernel<2, true>), grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed); else hipLaunchKernelGGL((ln_fwd_kernel<2, false>), grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed); }
-  else if (nv <= 256) { if (PF) hipLaunchKernelGGL((ln_fwd_kernel<4, true>), grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed); else hipLaunchKernelGGL((ln_fwd_kernel<4, false>), grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed); }
+  if (nv <= 64) hipLaunchKernelGGL((ln_fwd_kernel<1, true>), grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed);
+  else if (nv <= 128) hipLaunchKernelGGL((ln_fwd_kernel<2, true>), grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed);
+  else if (nv <= 256) hipLaunchKernelGGL((ln_fwd_kernel<4, true>), grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed);
   else hipLaunchKernelGGL((ln_fwd_kernel<8, false>), grid, dim3(256), 0, s, X, gamma, beta, Y, mean, rstd, M, H, eps, th, ds, seed);
   return (int)hipGetLastError();
 }
 
 int ln_partial_rows(long M) {
-  // workgroups of the row-per-wave backward sweeps (4 waves each); DDL_LN_BWD_BLOCKS overrides.
-  // The override is read ONCE per process (function-local static: setting it after the first
-  // LayerNorm / embedding backward has no effect) and also sizes embed_bwd's grid and its
-  // token-type partial-row workspace, which share this partial-row count.
-  static const long cap = [] {
-    const char* e = std::getenv("DDL_LN_BWD_BLOCKS");
-    const long v = e ? std::atol(e) : 0;
-    return v > 0 ? v : (long)kLnBwdBlocks;
-  }();
-  const long blocks = std::min<long>(cap, (M + 3) / 4);
+  // workgroups of the row-per-wave backward sweeps (4 waves each); also sizes embed_bwd's grid and its
+  // token-type partial-row workspace, which share this partial-row count
+  const long blocks = std::min<long>((long)kLnBwdBlocks, (M + 3) / 4);
   return (int)std::max<long>(1, blocks) * 4;
 }
 
@@ -608,7 +586,6 @@ int layernorm_bwd(const void* dy, const void* x, const float* mean, const float*
   const uint32_t ith = drop_t8(in_drop_p);
   const float iscale = drop_scale8(ith);
   const int nv = H / 8;
-  const bool PF = ln_prefetch();
   const dim3 grid((unsigned)(P / 4));
   const uint32_t thresh = drop_t8(drop_p);
   const float dscale = drop_scale8(thresh);
@@ -616,8 +593,8 @@ int layernorm_bwd(const void* dy, const void* x, const float* mean, const float*
   auto X = reinterpret_cast<const bf16_t*>(x);
   auto DX = reinterpret_cast<bf16_t*>(dx);
   auto DD = reinterpret_cast<bf16_t*>(dx_drop);
-  if (nv <= 64) { if (PF) hipLaunchKernelGGL((ln_bwd_kernel<1, true>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts); else hipLaunchKernelGGL((ln_bwd_kernel<1, false>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts); }
-  else if (nv <= 128) { if (PF) hipLaunchKernelGGL((ln_bwd_kernel<2, true>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts); else hipLaunchKernelGGL((ln_bwd_kernel<2, false>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts); }
+  if (nv <= 64) hipLaunchKernelGGL((ln_bwd_kernel<1, true>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts);
+  else if (nv <= 128) hipLaunchKernelGGL((ln_bwd_kernel<2, true>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts);
   else if (nv <= 256) hipLaunchKernelGGL((ln_bwd_kernel<4, false>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts);
   else hipLaunchKernelGGL((ln_bwd_kernel<8, false>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts);
   return (int)hipGetLastError();

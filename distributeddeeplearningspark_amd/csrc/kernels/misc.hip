@@ -13,15 +13,8 @@ static int g_deterministic = 0;
 void set_deterministic(int on) { g_deterministic = on ? 1 : 0; }
 int deterministic() { return g_deterministic; }
 
-// one element group per lane (DDL_MISC_GRID caps the workgroups for A/B; the former cap was 8,192)
-static long misc_grid_cap() {
-  static const long cap = [] {
-    const char* e = getenv("DDL_MISC_GRID");
-    const long v = e ? atol(e) : (1L << 24);
-    return v >= 256 ? v : (1L << 24);
-  }();
-  return cap;
-}
+// one element group per lane (a former cap of 8,192 workgroups cost the sweeps 2-3 %: bn.hip bn_grid_cap)
+static long misc_grid_cap() { return 1L << 24; }
 static unsigned mgrid(long n) {
   long g = (n + 255) / 256;
   if (g > misc_grid_cap()) g = misc_grid_cap();

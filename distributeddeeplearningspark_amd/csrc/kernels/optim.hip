@@ -9,16 +9,10 @@
 
 namespace ddl {
 
-// one float4 per lane, no grid-stride trips (DDL_OPT_GRID caps the workgroups for A/B; the former cap was 4,096:
-// see bn.hip bn_grid_cap for the measured cost of grid-stride sweeps)
+// one float4 per lane, no grid-stride trips (a 4,096-workgroup cap cost the sweeps 2-3 %: bn.hip bn_grid_cap)
 static unsigned ogrid(long n4) {
-  static const long cap = [] {
-    const char* e = getenv("DDL_OPT_GRID");
-    const long v = e ? atol(e) : (1L << 24);
-    return v >= 256 ? v : (1L << 24);
-  }();
   long g = (n4 + 255) / 256;
-  if (g > cap) g = cap;
+  if (g > (1L << 24)) g = 1L << 24;
   return (unsigned)(g > 0 ? g : 1);
 }
 

@@ -83,16 +83,10 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint4* __restric
   }
 }
 
-// one vector per lane (the grid-stride cap of 8,192 workgroups cost the BN sweeps 2-3 %: bn.hip bn_grid_cap);
-// DDL_POOL_GRID caps it for A/B
+// one vector per lane (the grid-stride cap of 8,192 workgroups cost the BN sweeps 2-3 %: bn.hip bn_grid_cap)
 static unsigned pgrid(long n) {
-  static const long cap = [] {
-    const char* e = getenv("DDL_POOL_GRID");
-    const long v = e ? atol(e) : (1L << 24);
-    return v >= 256 ? v : (1L << 24);
-  }();
   long g = (n + 255) / 256;
-  if (g > cap) g = cap;
+  if (g > (1L << 24)) g = 1L << 24;
   return (unsigned)(g > 0 ? g : 1);
 }
 

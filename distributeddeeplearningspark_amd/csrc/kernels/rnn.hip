@@ -238,11 +238,13 @@ constexpr int fwd_threads() { return (CELL == 0 ? 3 : 4) * H * (H / 64); }
 template <int CELL, int H>
 constexpr int bwd_threads() { return H * (((CELL == 0 ? 3 : 4) * H / 64) <= 4 ? 4 : 8); }
 
-template <int CELL, int H, int BB_, bool FUSE>
+// REP: replica-batched (RnnRep): the workgroup's replica is b0 / rp.B; W / U / bias come from its table
+// entries and x from its resident shard at mini-batch (*rp.ctr % rp.nb) — outputs stay global-row indexed.
+template <int CELL, int H, int BB_, bool FUSE, bool REP = false>
 __global__ __launch_bounds__((fwd_threads<CELL, H>())) void rnn_fwd_reg_kernel(
     const float* __restrict__ xw, const float* __restrict__ x, const float* __restrict__ W,
     const float* __restrict__ bias, int I, const float* __restrict__ U, float* __restrict__ hs,
-    float* __restrict__ cs, float* __restrict__ gates, float* __restrict__ y, int B, int T, int rs) {
+    float* __restrict__ cs, float* __restrict__ gates, float* __restrict__ y, int B, int T, int rs, const RnnRep rp) {
   constexpr int G = CELL == 0 ? 3 : 4;
   constexpr int GH = G * H;
   constexpr int KS = H / CH;
@@ -255,6 +257,15 @@ __global__ __launch_bounds__((fwd_threads<CELL, H>())) void rnn_fwd_reg_kernel(
   const int j = tid / KS, kh = tid % KS;
   const int b0 = blockIdx.x * BB_;
   const int nb = min(BB_, B - b0);
+  long xrow0 = b0;  // input row of the workgroup's first batch row
+  if constexpr (REP) {
+    const int r = b0 / rp.B;
+    U = rp.U[r];
+    W = rp.W[r];
+    bias = rp.b[r];
+    x = rp.x[r];
+    xrow0 = (long)(*rp.ctr % rp.nb) * rp.B + (b0 - r * rp.B);
+  }
   float u[CH];
 #pragma unroll
   for (int i = 0; i < CH; ++i) u[i] = U[(long)(kh * CH + i) * GH + j];
@@ -273,7 +284,7 @@ __global__ __launch_bounds__((fwd_threads<CELL, H>())) void rnn_fwd_reg_kernel(
     const int tc = min(max(t, 0), T - 1);
 #pragma unroll
     for (int r = 0; r < BB_; ++r) {
-      const long bt = (long)(b0 + min(r, nb - 1)) * T + tc;
+      const long bt = (xrow0 + min(r, nb - 1)) * T + tc;
       if constexpr (!FUSE) {
         xr[r][0] = xw[bt * GH + j];
       } else {
@@ -384,10 +395,11 @@ __global__ __launch_bounds__((fwd_threads<CELL, H>())) void rnn_fwd_reg_kernel(
   }
 }
 
-template <int CELL, int H, int BB_>
+template <int CELL, int H, int BB_, bool REP = false>
 __global__ __launch_bounds__((bwd_threads<CELL, H>())) void rnn_bwd_reg_kernel(
     const float* __restrict__ dy, const float* __restrict__ U, const float* __restrict__ hs,
-    const float* __restrict__ cs, const float* __restrict__ gates, float* __restrict__ dgates, int B, int T, int rs) {
+    const float* __restrict__ cs, const float* __restrict__ gates, float* __restrict__ dgates, int B, int T, int rs,
+    const RnnRep rp) {
   constexpr int G = CELL == 0 ? 3 : 4;
   constexpr int GH = G * H;
   constexpr int JS = GH / CH;                            // column chunks
@@ -404,6 +416,7 @@ __global__ __launch_bounds__((bwd_threads<CELL, H>())) void rnn_bwd_reg_kernel(
   const bool active = js < JS;
   const int b0 = blockIdx.x * BB_;
   const int nb = min(BB_, B - b0);
+  if constexpr (REP) U = rp.U[b0 / rp.B];
   float u[CH];
 #pragma unroll
   for (int i = 0; i < CH; i += 4) {
@@ -588,12 +601,13 @@ int launch_fwd_reg(const float* xw, const float* x, const float* W, const float*
   static_assert(BB_ * H <= fwd_threads<CELL, H>(), "one state element per thread");
   if (!xw && (I < 1 || I > IMAX)) return (int)hipErrorInvalidValue;
   const dim3 grid((B + BB_ - 1) / BB_);
+  const RnnRep none{};
   if (xw)
     hipLaunchKernelGGL((rnn_fwd_reg_kernel<CELL, H, BB_, false>), grid, dim3(G * H * (H / CH)), 0, s, xw, x, W, b, I,
-                       U, hs, cs, gates, y, B, T, rs);
+                       U, hs, cs, gates, y, B, T, rs, none);
   else
     hipLaunchKernelGGL((rnn_fwd_reg_kernel<CELL, H, BB_, true>), grid, dim3(G * H * (H / CH)), 0, s, xw, x, W, b, I,
-                       U, hs, cs, gates, y, B, T, rs);
+                       U, hs, cs, gates, y, B, T, rs, none);
   return (int)hipGetLastError();
 }
 
@@ -602,8 +616,9 @@ int launch_bwd_reg(const float* dy, const float* U, const float* hs, const float
                    float* dgates, int B, int T, int rs, hipStream_t s) {
   static_assert(BB_ * H <= bwd_threads<CELL, H>(), "one state element per thread");
   const dim3 grid((B + BB_ - 1) / BB_);
+  const RnnRep none{};
   hipLaunchKernelGGL((rnn_bwd_reg_kernel<CELL, H, BB_>), grid, dim3(bwd_threads<CELL, H>()), 0, s, dy, U, hs, cs,
-                     gates, dgates, B, T, rs);
+                     gates, dgates, B, T, rs, none);
   return (int)hipGetLastError();
 }
 
@@ -615,32 +630,14 @@ bool rnn_reg_path(int cell, int H, int act, int ract) {
   return (cell == 0 || cell == 1) && rnn_fast_path(H) && act == ACT_C_TANH && ract == ACT_C_HARD_SIGMOID;
 }
 
-// batch rows per workgroup of the register-resident kernels: fewer rows = more CUs busy and
-// less VALU work per step (the recurrence is latency-bound); DDL_RNN_BB overrides (1/2/4)
-static int rnn_rows_per_wg(int dflt) {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("DDL_RNN_BB");
-    v = e ? atoi(e) : 0;
-    if (v != 1 && v != 2 && v != 4) v = 0;
-  }
-  return v ? v : dflt;
-}
 
 int rnn_fwd(int cell, const float* xw, const float* x, const float* W, const float* b, int I, const float* U,
             float* hs, float* cs, float* gates, float* y, int B, int T, int H, int rs, int act, int ract,
             hipStream_t s) {
   const bool reg = rnn_reg_path(cell, H, act, ract);
-  if (reg && H == 128) {
-    const int bb = rnn_rows_per_wg(RNN_BB_FWD);
-#define DDL_RNN_FWD(BBV)                                                                                    \
-  return cell == 0 ? launch_fwd_reg<0, 128, BBV>(xw, x, W, b, I, U, hs, cs, gates, y, B, T, rs, s)           \
-                   : launch_fwd_reg<1, 128, BBV>(xw, x, W, b, I, U, hs, cs, gates, y, B, T, rs, s)
-    if (bb == 1) DDL_RNN_FWD(1);
-    if (bb == 2) DDL_RNN_FWD(2);
-    DDL_RNN_FWD(4);
-#undef DDL_RNN_FWD
-  }
+  if (reg && H == 128)  // one batch row per workgroup: more CUs busy, less VALU per step (latency-bound)
+    return cell == 0 ? launch_fwd_reg<0, 128, RNN_BB_FWD>(xw, x, W, b, I, U, hs, cs, gates, y, B, T, rs, s)
+                     : launch_fwd_reg<1, 128, RNN_BB_FWD>(xw, x, W, b, I, U, hs, cs, gates, y, B, T, rs, s);
   if (reg && H == 64)
     return cell == 0 ? launch_fwd_reg<0, 64, 2>(xw, x, W, b, I, U, hs, cs, gates, y, B, T, rs, s)
                      : launch_fwd_reg<1, 64, 2>(xw, x, W, b, I, U, hs, cs, gates, y, B, T, rs, s);
@@ -679,16 +676,9 @@ int rnn_param_grad(int cell, const float* dg, const float* hs, const float* gate
 int rnn_bwd(int cell, const float* dy, const float* U, const float* UT, const float* hs, const float* cs,
             const float* gates, float* dgates, int B, int T, int H, int rs, int act, int ract, hipStream_t s) {
   const bool reg = rnn_reg_path(cell, H, act, ract);
-  if (reg && H == 128) {
-    const int bb = rnn_rows_per_wg(RNN_BB_BWD);
-#define DDL_RNN_BWD(BBV)                                                                                    \
-  return cell == 0 ? launch_bwd_reg<0, 128, BBV>(dy, U, hs, cs, gates, dgates, B, T, rs, s)                   \
-                   : launch_bwd_reg<1, 128, BBV>(dy, U, hs, cs, gates, dgates, B, T, rs, s)
-    if (bb == 1) DDL_RNN_BWD(1);
-    if (bb == 4) DDL_RNN_BWD(4);
-    DDL_RNN_BWD(2);
-#undef DDL_RNN_BWD
-  }
+  if (reg && H == 128)
+    return cell == 0 ? launch_bwd_reg<0, 128, RNN_BB_BWD>(dy, U, hs, cs, gates, dgates, B, T, rs, s)
+                     : launch_bwd_reg<1, 128, RNN_BB_BWD>(dy, U, hs, cs, gates, dgates, B, T, rs, s);
   if (reg && H == 64)
     return cell == 0 ? launch_bwd_reg<0, 64, 2>(dy, U, hs, cs, gates, dgates, B, T, rs, s)
                      : launch_bwd_reg<1, 64, 2>(dy, U, hs, cs, gates, dgates, B, T, rs, s);
@@ -706,6 +696,244 @@ int rnn_bwd(int cell, const float* dy, const float* U, const float* UT, const fl
     hipLaunchKernelGGL(rnn_bwd_kernel<2>, grid, dim3(threads), lds, s, dy, UT, hs, cs, gates, dgates, B, T, H, rs, act,
                        ract);
   return (int)hipGetLastError();
+}
+
+// =============================================================================================
+// Replica-batched training step (RnnRep / OptRep, ddl_ops.h; parallel/replica_batch.py).
+// The reference runs its dist-keras workers as separate Keras models, num_processes per executor
+// (ddl_nyiso_aztk.py:51-55, 206-218); on one MI355X the R co-located replicas of RNN(H) -> Dense(K)
+// with an MSE loss are ONE launch per phase: the recurrences of all R x B batch rows run side by side
+// (each workgroup reads its replica's U / W from the pointer table), the Dense head + loss + its
+// backward is one workgroup per replica, and the parameter gradients and optimizer sweep take the
+// replica from blockIdx.z / blockIdx.y.  Gradients are written (not accumulated), so no step zeroes them.
+// =============================================================================================
+namespace {
+
+constexpr int kRepMaxB = 64, kRepMaxK = 8;
+
+// One workgroup per replica: y = h Wd^T + bd, loss = mean (y - t)^2 over B K (Keras / ops.loss.mse),
+// dy = 2 (y - t) / (B K); gWd = dy^T h, gbd = colsum dy, dh = dy Wd; history[ctr] = loss; Adam tick.
+template <int H>
+__global__ __launch_bounds__(256) void dense_mse_rep_kernel(const float* __restrict__ hlast, float* __restrict__ dh,
+                                                            const RnnRep rp, const OptRep op) {
+  const int r = blockIdx.x, B = rp.B, K = rp.K, tid = threadIdx.x;
+  __shared__ float hsm[kRepMaxB][H + 1];
+  __shared__ float dys[kRepMaxB][kRepMaxK];
+  __shared__ float red[256];
+  const float* hb = hlast + (long)r * B * H;
+  for (int i = tid; i < B * H; i += 256) hsm[i / H][i % H] = hb[i];
+  const int ctr = *rp.ctr;
+  const float* tgt = rp.y[r] + (long)(ctr % rp.nb) * B * K;
+  const float* Wd = rp.Wd[r];
+  const float* bd = rp.bd[r];
+  __syncthreads();
+  const float sc = 2.f / (float)(B * K);
+  float se = 0.f;
+  for (int q = tid; q < B * K; q += 256) {
+    const int b = q / K, o = q - b * K;
+    float a = bd ? bd[o] : 0.f;
+    const float* w = Wd + (long)o * H;
+#pragma unroll 8
+    for (int i = 0; i < H; ++i) a += hsm[b][i] * w[i];
+    const float e = a - tgt[q];
+    se += e * e;
+    dys[b][o] = sc * e;
+  }
+  red[tid] = se;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) red[tid] += red[tid + o];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    if (ctr < rp.cap) rp.hist[r][ctr] = red[0] / (float)(B * K);
+    if (op.t[r]) op.t[r][0] += 1.f;  // Adam's device step counter (read by the optimizer sweep below)
+  }
+  // gWd[o][i] = sum_b dy[b][o] h[b][i];  gbd[o] = sum_b dy[b][o]
+  for (int q = tid; q < K * H; q += 256) {
+    const int o = q / H, i = q - o * H;
+    float a = 0.f;
+    for (int b = 0; b < B; ++b) a += dys[b][o] * hsm[b][i];
+    rp.gWd[r][q] = a;
+  }
+  if (rp.gbd[r] && tid < K) {
+    float a = 0.f;
+    for (int b = 0; b < B; ++b) a += dys[b][tid];
+    rp.gbd[r][tid] = a;
+  }
+  // dh[b][i] = sum_o dy[b][o] Wd[o][i]  (the recurrent backward's dy at the last step)
+  float* dhb = dh + (long)r * B * H;
+  for (int q = tid; q < B * H; q += 256) {
+    const int b = q / H, i = q - b * H;
+    float a = 0.f;
+    for (int o = 0; o < K; ++o) a += dys[b][o] * Wd[(long)o * H + i];
+    dhb[q] = a;
+  }
+}
+
+// Recurrent parameter gradients of replica blockIdx.z over ALL its B T rows (chunks of PG_BT staged in
+// LDS), written with plain stores: rows m < H gU, H <= m < H + I gW, m = H + I gb (as rnn_param_grad).
+template <int CELL>
+__global__ __launch_bounds__(256) void rnn_param_grad_rep_kernel(const float* __restrict__ dg, const float* __restrict__ hs,
+                                                                 const float* __restrict__ gates, const RnnRep rp,
+                                                                 int T, int H, int I) {
+  constexpr int G = CELL == 0 ? 3 : (CELL == 1 ? 4 : 1);
+  const int GH = G * H, r = blockIdx.z, B = rp.B;
+  const bool has_b = rp.gb[r] != nullptr;
+  const int M = H + I + (has_b ? 1 : 0);
+  const long BT = (long)B * T, row0 = (long)r * B;  // global batch row of the replica's row 0
+  const long xrow0 = (long)(*rp.ctr % rp.nb) * B;   // shard row of its mini-batch
+  const float* x = rp.x[r];
+  const int m0 = blockIdx.x * 64, j0 = blockIdx.y * 64;
+  __shared__ float As[PG_BT][64 + 1];
+  __shared__ float Ds[PG_BT][64 + 1];
+  const bool cand = CELL == 0 && j0 >= 2 * H;
+  const int c = threadIdx.x & 63, q0 = threadIdx.x >> 6;
+  const int tm = (threadIdx.x / 16) * 4, tj = (threadIdx.x % 16) * 4;
+  float acc[4][4] = {};
+  for (long bt0 = 0; bt0 < BT; bt0 += PG_BT) {
+    const int nbt = (int)min((long)PG_BT, BT - bt0);
+    long b = (bt0 + q0) / T, t = (bt0 + q0) - b * T;
+    for (int q = q0; q < nbt; q += 4, t += 4) {
+      while (t >= T) { t -= T; ++b; }
+      const long gbt = (row0 + b) * T + t;  // global (row, step)
+      const int m = m0 + c;
+      float a = 0.f;
+      if (m < H) {
+        a = hs[((row0 + b) * (T + 1) + t) * H + m];
+        if (cand) a *= gates[gbt * GH + H + m];
+      } else if (m < H + I) {
+        a = x[((xrow0 + b) * T + t) * I + (m - H)];
+      } else if (m < M) {
+        a = 1.f;
+      }
+      As[q][c] = a;
+      const int jj = j0 + c;
+      Ds[q][c] = jj < GH ? dg[gbt * GH + jj] : 0.f;
+    }
+    __syncthreads();
+    for (int q = 0; q < nbt; ++q) {
+      float a[4], d[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { a[i] = As[q][tm + i]; d[i] = Ds[q][tj + i]; }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int l = 0; l < 4; ++l) acc[i][l] += a[i] * d[l];
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + tm + i;
+    if (m >= M) continue;
+    float* dst = m < H ? rp.gU[r] + (long)m * GH : (m < H + I ? rp.gW[r] + (long)(m - H) * GH : rp.gb[r]);
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      const int jj = j0 + tj + l;
+      if (jj < GH) dst[jj] = acc[i][l];
+    }
+  }
+}
+
+// Optimizer sweep over the R replica arenas (blockIdx.y = replica), Keras semantics as the per-replica
+// kernels (optim.hip): OPT 0 SGD (+momentum p1), 1 Adagrad, 2 Adam (b1 = p1, b2 = p2, amode as adam_step).
+// Block (0, 0) advances the shared step counter (no block of this kernel reads it).
+template <int OPT>
+__global__ __launch_bounds__(256) void opt_rep_kernel(const OptRep op, long n4, float lr, float p1, float p2, float eps,
+                                                      float wd, int amode, int* ctr) {
+  const int r = blockIdx.y;
+  float4* w = reinterpret_cast<float4*>(op.w[r]);
+  const float4* g = reinterpret_cast<const float4*>(op.g[r]);
+  float4* s1 = reinterpret_cast<float4*>(op.s1[r]);
+  float4* s2 = reinterpret_cast<float4*>(op.s2[r]);
+  float bc1 = 1.f, bc2 = 1.f;
+  if constexpr (OPT == 2) {
+    const float t = op.t[r][0];
+    bc1 = 1.f - powf(p1, t);
+    bc2 = 1.f - powf(p2, t);
+  }
+  const float sbc2 = sqrtf(bc2);
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    float4 p = w[i], d = g[i];
+    float4 a = s1 ? s1[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 v = (OPT == 2) ? s2[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float *pp = &p.x, *dd = &d.x, *aa = &a.x, *vv = &v.x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if constexpr (OPT == 0) {
+        float gg = dd[k] + wd * pp[k];
+        if (s1) {
+          aa[k] = p1 * aa[k] + gg;
+          gg = aa[k];
+        }
+        pp[k] -= lr * gg;
+      } else if constexpr (OPT == 1) {
+        const float gg = dd[k] + wd * pp[k];
+        aa[k] += gg * gg;
+        pp[k] -= lr * gg / (sqrtf(aa[k]) + eps);
+      } else {
+        float gg = dd[k];
+        if (amode & 1) pp[k] *= (1.f - lr * wd);
+        else gg += wd * pp[k];
+        aa[k] = p1 * aa[k] + (1.f - p1) * gg;
+        vv[k] = p2 * vv[k] + (1.f - p2) * gg * gg;
+        if (amode & 2) pp[k] -= lr * (sbc2 / bc1) * aa[k] / (sqrtf(vv[k]) + eps);
+        else pp[k] -= lr * (aa[k] / bc1) / (sqrtf(vv[k]) / sbc2 + eps);
+      }
+    }
+    w[i] = p;
+    if (s1) s1[i] = a;
+    if constexpr (OPT == 2) s2[i] = v;
+  }
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *ctr += 1;
+}
+
+template <int CELL, int H>
+int rep_step(const RnnRep& rp, int R, int T, int I, float* hs, float* cs, float* gates, float* hlast, float* dh,
+             float* dgates, const OptRep& op, long n, int opt, float lr, float p1, float p2, float eps, float wd,
+             int amode, hipStream_t s) {
+  constexpr int G = CELL == 0 ? 3 : 4;
+  constexpr int BBF = H == 128 ? RNN_BB_FWD : 2, BBB = H == 128 ? RNN_BB_BWD : 2;
+  const int RB = R * rp.B;
+  hipLaunchKernelGGL((rnn_fwd_reg_kernel<CELL, H, BBF, true, true>), dim3((RB + BBF - 1) / BBF),
+                     dim3(fwd_threads<CELL, H>()), 0, s, (const float*)nullptr, (const float*)nullptr,
+                     (const float*)nullptr, (const float*)nullptr, I, (const float*)nullptr, hs, cs, gates, hlast, RB,
+                     T, 0, rp);
+  hipLaunchKernelGGL((dense_mse_rep_kernel<H>), dim3(R), dim3(256), 0, s, hlast, dh, rp, op);
+  hipLaunchKernelGGL((rnn_bwd_reg_kernel<CELL, H, BBB, true>), dim3((RB + BBB - 1) / BBB), dim3(bwd_threads<CELL, H>()),
+                     0, s, dh, (const float*)nullptr, hs, cs, gates, dgates, RB, T, 0, rp);
+  const int M = H + I + 1;
+  hipLaunchKernelGGL((rnn_param_grad_rep_kernel<CELL>), dim3((M + 63) / 64, (G * H + 63) / 64, R), dim3(256), 0, s,
+                     dgates, hs, gates, rp, T, H, I);
+  const long n4 = n / 4;
+  const dim3 og((unsigned)std::min<long>((n4 + 255) / 256, 1024), R);
+  if (opt == 0)
+    hipLaunchKernelGGL(opt_rep_kernel<0>, og, dim3(256), 0, s, op, n4, lr, p1, p2, eps, wd, amode, rp.ctr);
+  else if (opt == 1)
+    hipLaunchKernelGGL(opt_rep_kernel<1>, og, dim3(256), 0, s, op, n4, lr, p1, p2, eps, wd, amode, rp.ctr);
+  else
+    hipLaunchKernelGGL(opt_rep_kernel<2>, og, dim3(256), 0, s, op, n4, lr, p1, p2, eps, wd, amode, rp.ctr);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+bool rnn_replica_ok(int cell, int H, int I, int K, int B) {
+  return (cell == 0 || cell == 1) && (H == 128 || (H == 64 && B % 2 == 0)) && I >= 1 && I <= IMAX && K >= 1 &&
+         K <= kRepMaxK && B >= 1 && B <= kRepMaxB;
+}
+
+int rnn_replica_step(int cell, const RnnRep& rp, int R, int T, int H, int I, float* hs, float* cs, float* gates,
+                     float* hlast, float* dh, float* dgates, const OptRep& op, long n, int opt, float lr, float p1,
+                     float p2, float eps, float wd, int amode, hipStream_t s) {
+  if (!rnn_replica_ok(cell, H, I, rp.K, rp.B) || R < 1 || R > kMaxRnnRep || n % 4 || opt < 0 || opt > 2 || rp.nb < 1)
+    return (int)hipErrorInvalidValue;
+  if (cell == 0)
+    return H == 128 ? rep_step<0, 128>(rp, R, T, I, hs, cs, gates, hlast, dh, dgates, op, n, opt, lr, p1, p2, eps, wd, amode, s)
+                    : rep_step<0, 64>(rp, R, T, I, hs, cs, gates, hlast, dh, dgates, op, n, opt, lr, p1, p2, eps, wd, amode, s);
+  return H == 128 ? rep_step<1, 128>(rp, R, T, I, hs, cs, gates, hlast, dh, dgates, op, n, opt, lr, p1, p2, eps, wd, amode, s)
+                  : rep_step<1, 64>(rp, R, T, I, hs, cs, gates, hlast, dh, dgates, op, n, opt, lr, p1, p2, eps, wd, amode, s);
 }
 
 }  // namespace ddl

@@ -142,6 +142,85 @@ py::tuple rnn_bwd_(const std::string& cell, const at::Tensor& dy, const at::Tens
   return py::make_tuple(dx, dW, dU, db.defined() ? py::cast(db) : py::none());
 }
 
+// Replica-batched training step of R co-located RNN(H) -> Dense(K) / MSE replicas (kernels/rnn.hip,
+// rnn_replica_step): every list holds one entry per replica; None entries of the optional lists are
+// absent biases / optimizer states.  All tensors fp32, contiguous, on one device.
+float* fptr(const py::handle& o, const char* what, int64_t numel = -1) {
+  if (o.is_none()) return nullptr;
+  at::Tensor t = o.cast<at::Tensor>();
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous(), "rnn_replica_step: ", what,
+              " must be a contiguous fp32 GPU tensor");
+  TORCH_CHECK(numel < 0 || t.numel() >= numel, "rnn_replica_step: ", what, " too small");
+  return t.data_ptr<float>();
+}
+
+void rnn_replica_step_(const std::string& cell, py::list xs, py::list ys, py::list Ws, py::list Us, py::list bs,
+                       py::list Wds, py::list bds, py::list gWs, py::list gUs, py::list gbs, py::list gWds,
+                       py::list gbds, py::list hists, at::Tensor ctr, int64_t nb, int64_t B, at::Tensor hs,
+                       at::Tensor cs, at::Tensor gates, at::Tensor hlast, at::Tensor dh, at::Tensor dgates,
+                       py::list ws, py::list gs, py::list s1s, py::list s2s, py::list ts, int64_t opt, double lr,
+                       double p1, double p2, double eps, double wd, int64_t amode) {
+  const int c = cell_id(cell);
+  TORCH_CHECK(c == 0 || c == 1, "rnn_replica_step: GRU or LSTM");
+  const int G = gates_of(c);
+  const int R = (int)xs.size();
+  TORCH_CHECK(R >= 1 && R <= kMaxRnnRep, "rnn_replica_step: 1..", kMaxRnnRep, " replicas");
+  for (py::list* l : {&ys, &Ws, &Us, &bs, &Wds, &bds, &gWs, &gUs, &gbs, &gWds, &gbds, &hists, &ws, &gs, &s1s, &s2s, &ts})
+    TORCH_CHECK((int)l->size() == R, "rnn_replica_step: one entry per replica in every list");
+  at::Tensor x0 = xs[0].cast<at::Tensor>(), U0 = Us[0].cast<at::Tensor>(), Wd0 = Wds[0].cast<at::Tensor>();
+  TORCH_CHECK(x0.dim() == 3, "rnn_replica_step: x shards [rows, T, I]");
+  const int64_t T = x0.size(1), I = x0.size(2), H = U0.size(0), K = Wd0.size(0);
+  TORCH_CHECK(U0.size(1) == G * H && Wd0.size(1) == H, "rnn_replica_step: U [H, GH], Dense kernel [K, H]");
+  TORCH_CHECK(rnn_replica_ok(c, (int)H, (int)I, (int)K, (int)B), "rnn_replica_step: unsupported H / I / K / B");
+  TORCH_CHECK(ctr.is_cuda() && ctr.scalar_type() == at::kInt && ctr.numel() >= 1, "rnn_replica_step: int32 ctr");
+  const int64_t RB = R * B;
+  const int64_t n = ws[0].cast<at::Tensor>().numel();
+  RnnRep rp{};
+  OptRep op{};
+  for (int r = 0; r < R; ++r) {
+    rp.x[r] = fptr(xs[r], "x shard", nb * B * T * I);
+    rp.y[r] = fptr(ys[r], "y shard", nb * B * K);
+    rp.W[r] = fptr(Ws[r], "W", I * G * H);
+    rp.U[r] = fptr(Us[r], "U", H * G * H);
+    rp.b[r] = fptr(bs[r], "b", G * H);
+    rp.Wd[r] = fptr(Wds[r], "Dense kernel", K * H);
+    rp.bd[r] = fptr(bds[r], "Dense bias", K);
+    rp.gW[r] = fptr(gWs[r], "gW", I * G * H);
+    rp.gU[r] = fptr(gUs[r], "gU", H * G * H);
+    rp.gb[r] = fptr(gbs[r], "gb", G * H);
+    rp.gWd[r] = fptr(gWds[r], "gWd", K * H);
+    rp.gbd[r] = fptr(gbds[r], "gbd", K);
+    TORCH_CHECK(!bs[r].is_none() && !gbs[r].is_none(), "rnn_replica_step: recurrent bias required");
+    TORCH_CHECK(bds[r].is_none() == gbds[r].is_none(), "rnn_replica_step: Dense bias and its gradient together");
+    at::Tensor h = hists[r].cast<at::Tensor>();
+    rp.hist[r] = fptr(hists[r], "history");
+    if (r == 0) rp.cap = (int)h.numel();
+    TORCH_CHECK(h.numel() == rp.cap, "rnn_replica_step: equal history capacities");
+    op.w[r] = fptr(ws[r], "weights", n);
+    op.g[r] = fptr(gs[r], "grads", n);
+    op.s1[r] = fptr(s1s[r], "optimizer state", n);
+    op.s2[r] = fptr(s2s[r], "optimizer state 2", n);
+    op.t[r] = fptr(ts[r], "step counter", 1);
+    TORCH_CHECK(ws[r].cast<at::Tensor>().numel() == n, "rnn_replica_step: equal arena sizes");
+    if (opt == 2) TORCH_CHECK(op.s1[r] && op.s2[r] && op.t[r], "rnn_replica_step: Adam needs m, v and t");
+    if (opt == 1) TORCH_CHECK(op.s1[r], "rnn_replica_step: Adagrad needs its accumulator");
+  }
+  rp.ctr = ctr.data_ptr<int>();
+  rp.nb = (int)nb;
+  rp.B = (int)B;
+  rp.K = (int)K;
+  float* hsp = fptr(py::cast(hs), "hs", RB * (T + 1) * H);
+  float* csp = c == 1 ? fptr(py::cast(cs), "cs", RB * (T + 1) * H) : nullptr;
+  float* gp = fptr(py::cast(gates), "gates", RB * T * G * H);
+  float* hl = fptr(py::cast(hlast), "h_last", RB * H);
+  float* dhp = fptr(py::cast(dh), "dh", RB * H);
+  float* dgp = fptr(py::cast(dgates), "dgates", RB * T * G * H);
+  at::DeviceGuard g(x0.device());
+  const int e = rnn_replica_step(c, rp, R, (int)T, (int)H, (int)I, hsp, csp, gp, hl, dhp, dgp, op, n, (int)opt,
+                                 (float)lr, (float)p1, (float)p2, (float)eps, (float)wd, (int)amode, cur_stream());
+  TORCH_CHECK(e == 0, "rnn_replica_step launch failed: ", hipGetErrorString((hipError_t)e));
+}
+
 }  // namespace
 
 void register_rnn(py::module& m) {
@@ -152,4 +231,8 @@ void register_rnn(py::module& m) {
         py::arg("W"), py::arg("U"), py::arg("b"), py::arg("rs"), py::arg("saved"), py::arg("gW") = py::none(),
         py::arg("gU") = py::none(), py::arg("gb") = py::none(), py::arg("need_dx") = true,
         py::arg("act") = (int64_t)ACT_C_TANH, py::arg("ract") = (int64_t)ACT_C_HARD_SIGMOID);
+  m.def("rnn_replica_step", &rnn_replica_step_, "one training step of R co-located RNN -> Dense / MSE replicas");
+  m.def("rnn_replica_ok", [](const std::string& cell, int64_t H, int64_t I, int64_t K, int64_t B) {
+    return rnn_replica_ok(cell_id(cell), (int)H, (int)I, (int)K, (int)B);
+  });
 }

@@ -27,6 +27,9 @@ _LAYER_TYPES: dict[str, type] = {}
 _NAME_COUNTS: dict[str, int] = {}
 
 
+FUSE_CONVBN = True  # Sequential Conv2D -> BN (-> ReLU) as one fused training node (tests compare with False)
+
+
 def _auto_name(prefix: str) -> str:
     n = _NAME_COUNTS.get(prefix, 0) + 1
     _NAME_COUNTS[prefix] = n
@@ -588,10 +591,8 @@ class Sequential(Model):
     def _convbn_unit(self, conv, bn, x):
         """The (conv, BN) pair as a ``fused_blocks`` unit when the fused training node applies: no conv
         bias, stride 1 or an even split of "same" padding (no explicit pre-pad), dilation 1, both
-        trainable; ``DDL_FUSE_CONVBN=0`` keeps the two-node path."""
-        import os
-
-        if os.environ.get("DDL_FUSE_CONVBN", "1") == "0" or conv.bias is not None or conv.dilation_rate != (1, 1):
+        trainable; ``FUSE_CONVBN = False`` keeps the two-node path."""
+        if not FUSE_CONVBN or conv.bias is not None or conv.dilation_rate != (1, 1):
             return None
         if not (conv.trainable and bn.trainable and bn.gamma is not None and bn.beta is not None):
             return None

@@ -18,10 +18,11 @@ from .layers import BatchNormalization, Conv2D, Dense, Flatten, MaxPooling2D
 from ..ops import pool as pool_ops
 
 
-def _fused() -> bool:
-    import os
+FUSED_BLOCKS = True  # bottlenecks as fused training nodes (ops/fused_blocks.py); tests compare with False
 
-    return os.environ.get("DDL_FUSED_BLOCKS", "1") != "0"
+
+def _fused() -> bool:
+    return FUSED_BLOCKS
 
 
 class ConvBN(Layer):

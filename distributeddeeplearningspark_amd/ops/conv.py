@@ -18,7 +18,6 @@ Decomposition (``ConvGeometry``):
 from __future__ import annotations
 
 import math
-import os as _os
 from functools import lru_cache
 
 import torch
@@ -103,8 +102,7 @@ def _im2col(x, g: ConvGeometry, taps_h, taps_w, ho, wo, sh, sw, kpad):
     return col
 
 
-_HALO3 = _os.environ.get("DDL_CONV3X3", "1") != "0"
-_C64PP = _os.environ.get("DDL_CONV3X3_C64PP", "0") == "1"  # opt-in until it beats the implicit GEMM
+_HALO3 = True  # the 3x3 stride-1 halo kernel (tests switch it off to compare with the implicit GEMM)
 
 
 def halo3_ok(g: ConvGeometry) -> bool:
@@ -114,12 +112,10 @@ def halo3_ok(g: ConvGeometry) -> bool:
     if not (_HALO3 and g.KH == 3 and g.KW == 3 and (g.sh, g.sw) == (1, 1) and (g.ph, g.pw) == (1, 1)
             and (g.dh, g.dw) == (1, 1) and g.Ci % 64 == 0 and g.Co % 64 == 0 and g.implicit_fwd):
         return False
-    if g.Ci == 64 and g.Co == 64 and _os.environ.get("DDL_CONV3X3_C64", "0") != "1":
+    if g.Ci == 64 and g.Co == 64:
         # one 64-channel chunk: the per-tap halo kernel cannot amortise its halo prologue (measured 0.128 vs
-        # 0.120 ms for the implicit GEMM at 56x56); the resident-filter ping-pong kernel (conv3x3.hip,
-        # conv3x3_c64_pp_kernel) takes the 56x56 and 32x32 row tilings it is instantiated for
-        if not (_C64PP and g.H == g.W and g.H in (56, 32)):
-            return False
+        # 0.120 ms for the implicit GEMM at 56x56; a resident-filter variant lost too, profiles/r4/ab_c64_after_atomics.txt)
+        return False
     H, W = g.H, g.W
     if H * W <= 256:
         return H * W * max(1, min(256 // (H * W), 384 // ((H + 2) * (W + 2)))) >= 64
@@ -129,10 +125,10 @@ def halo3_ok(g: ConvGeometry) -> bool:
     return False
 
 
-_WG3 = _os.environ.get("DDL_WGRAD3X3", "1") != "0"
-_WG3_BPC = int(_os.environ.get("DDL_WGRAD3X3_BPC", "2"))  # workgroups per CU the pixel split aims for
-_WG3_SLAB = _os.environ.get("DDL_WGRAD3X3_SLAB", "1") == "1"  # partial slabs + reduce instead of atomics
-_WG3_PP = _os.environ.get("DDL_WGRAD3X3_PP", "1") == "1"  # 512-thread ping-pong form (one workgroup per CU)
+_WG3 = True  # 3x3 stride-1 weight gradients on the halo kernel
+_WG3_BPC = 2  # workgroups per CU the pixel split aims for
+_WG3_SLAB = True  # partial slabs + reduce instead of atomics
+_WG3_PP = True  # 512-thread ping-pong form (one workgroup per CU)
 
 
 @lru_cache(maxsize=None)
@@ -155,9 +151,9 @@ def wgrad3_plan(g: ConvGeometry, device=None):
     return _wgrad3_plan(g.N, g.H, g.W, g.Ci, g.Co, 1 if _WG3_PP else _WG3_BPC, _device_cus(idx))
 
 
-_SPLITK_FWD = _os.environ.get("DDL_CONV_SPLITK", "1") != "0"
-_SPLITK_MAX_TILES = int(_os.environ.get("DDL_CONV_SPLITK_TILES", "512"))
-_SPLITK_WG = int(_os.environ.get("DDL_CONV_SPLITK_WG", "1024"))  # workgroups the split aims for
+_SPLITK_FWD = True
+_SPLITK_MAX_TILES = 512
+_SPLITK_WG = 1024  # workgroups the split aims for
 
 
 def splitk_fwd_ok(g: ConvGeometry) -> bool:
@@ -171,18 +167,12 @@ def splitk_fwd_ok(g: ConvGeometry) -> bool:
     return math.ceil(g.M / 64) * math.ceil(g.Co / 64) <= _SPLITK_MAX_TILES
 
 
-def conv_fwd_native(x, w, g: ConvGeometry, bias=None, relu=False, stats=None, x_norm=None, bnr=None):
-    """``x_norm = (scale, shift)``: x is pre-BatchNorm and normalised on load (pointwise convs on the
-    streaming kernel: :func:`norm_on_load_ok`).  ``bnr``: fused BN-backward reduce of the output (a
+def conv_fwd_native(x, w, g: ConvGeometry, bias=None, relu=False, stats=None, bnr=None):
+    """``bnr``: fused BN-backward reduce of the output (a
     stride-1 data-gradient run as a forward conv; see ``gemm.linear_dgrad``) — applied on the halo and
     gathered implicit-GEMM paths, which then set ``bnr["done"]``."""
     y = torch.empty((g.N, g.Ho, g.Wo, g.Co), dtype=torch.bfloat16, device=x.device)
     y2 = y.view(g.M, g.Co)
-    if x_norm is not None:
-        if not norm_on_load_ok(g):
-            raise ValueError("conv_fwd_native: normalise-on-load not supported for this geometry")
-        G.linear_fwd(x.view(g.M, g.Ci), w.view(g.Co, g.Ci), bias=bias, relu=relu, out=y2, stats=stats, x_norm=x_norm)
-        return y
     if splitk_fwd_ok(g):
         ws = G.splitk_workspace(g.M, g.Co, x.device)
         K = g.T * g.Ci
@@ -232,7 +222,7 @@ def _dgrad_as_forward(g: ConvGeometry):
     filter (padding d*(k-1) - p), which runs on the forward implicit-GEMM path (K-contiguous
     weights, no transposed LDS reads) — measured 1.3-1.7x faster than the RC_TAPS data-gradient
     on the ResNet-50 3x3 layers.  Returns the forward geometry, or None when not applicable."""
-    if g.sh != 1 or g.sw != 1 or g.is_pointwise or _os.environ.get("DDL_DGRAD_AS_FWD", "1") == "0":
+    if g.sh != 1 or g.sw != 1 or g.is_pointwise:
         return None
     ph, pw = g.dh * (g.KH - 1) - g.ph, g.dw * (g.KW - 1) - g.pw
     if ph < 0 or pw < 0 or g.Co % 64 or g.T > 64:
@@ -243,22 +233,12 @@ def _dgrad_as_forward(g: ConvGeometry):
     return g2
 
 
-_KC_DGRAD = _os.environ.get("DDL_DGRAD_KC", "1") != "0"
-# BN-backward reduce fused into the parity-class GEMMs of a strided data-gradient (EPI_BF16_BNR with OutMap):
-# opt-in — correct (tests/test_gpu_kernels.py) but the BNR epilogue costs the short class GEMMs more than the
-# three reduce sweeps it removes (ResNet-50 11,942-11,948 vs 12,029-12,040 img/s interleaved,
-# profiles/r4/fuse_bn/ab_strided_bnr.txt)
-_STRIDED_BNR = _os.environ.get("DDL_STRIDED_BNR", "0") == "1"
-_WIDE_WGRAD = _os.environ.get("DDL_WGRAD_WIDE", "1") != "0"
-# gathered weight gradients: split-K workgroup rounds and tile (experiments: DDL_WGRAD_ROUNDS,
-# DDL_WGRAD_TILE=128 forces 128x128 tiles where M, N >= 128 instead of choose_tile's fill rule)
-_WGRAD_ROUNDS = float(_os.environ.get("DDL_WGRAD_ROUNDS", "4"))
-_WGRAD_TILE = _os.environ.get("DDL_WGRAD_TILE", "auto")
+_KC_DGRAD = True  # strided data-gradients read a K-contiguous per-class filter copy (not RC_TAPS)
+_WIDE_WGRAD = True
+_WGRAD_ROUNDS = 4.0  # gathered weight gradients: split-K workgroup rounds
 
 
 def _wgrad_tile(M, N, bn_cap):
-    if _WGRAD_TILE == "128" and M >= 128 and N >= 128 and bn_cap >= 128:
-        return 0
     return None
 
 
@@ -303,11 +283,6 @@ def conv_dgrad_native(dy, w, g: ConvGeometry, resid=None, resid_mask=None, bnr=N
         return dx
     dx = (torch.zeros if g.dgrad_needs_zero else torch.empty)((g.N, g.H, g.W, g.Ci), dtype=torch.bfloat16, device=dev)
     strided = g.sh > 1 or g.sw > 1
-    # fused BN-backward reduce of dx over the parity classes (each class's EPI_BF16_BNR epilogue adds the partial
-    # sums of the pixels it writes, through the OutMap): every pixel must be written by exactly one class
-    cls_bnr = (bnr if _STRIDED_BNR and bnr is not None and strided and resid is None and g.implicit_dgrad and _KC_DGRAD
-               and not g.dgrad_needs_zero and not g.dgrad_zero_siblings and g.Ci % 8 == 0
-               and bnr["x"].is_contiguous() else None)
     for cl in g.classes:
         nt = len(cl["wt"])
         if nt == 0:
@@ -325,7 +300,7 @@ def conv_dgrad_native(dy, w, g: ConvGeometry, resid=None, resid_mask=None, bnr=N
             geom = dict(n=g.N, hi=g.Ho, wi=g.Wo, c=g.Co, ho=cl["Hc"], wo=cl["Wc"], sh=1, sw=1, tap_c=g.Co,
                         dh=cl["dh"], dw=cl["dw"])
             G.gemm(dy, wkc, dx, Mc, g.Ci, nt * g.Co, G.KC_GATHER, G.KC, 0, nt * g.Co, g.Ci, G.EPI_BF16,
-                   geom=geom, outmap=om, resid=r, ldr=g.Ci if r is not None else 0, bnr=cls_bnr)
+                   geom=geom, outmap=om, resid=r, ldr=g.Ci if r is not None else 0)
         elif g.implicit_dgrad:
             geom = dict(n=g.N, hi=g.Ho, wi=g.Wo, c=g.Co, ho=cl["Hc"], wo=cl["Wc"], sh=1, sw=1, tap_c=g.Co,
                         dh=cl["dh"], dw=cl["dw"], wt=cl["wt"])
@@ -344,26 +319,15 @@ def conv_dgrad_native(dy, w, g: ConvGeometry, resid=None, resid_mask=None, bnr=N
                    ldr=g.Ci if r is not None else 0)
     if resid is not None and strided:
         C().add_bf16(dx, resid, dx)
-    if cls_bnr is not None:
-        cls_bnr["done"] = True
     return dx
 
 
-def norm_on_load_ok(g: ConvGeometry) -> bool:
-    """A pointwise conv can read a pre-BatchNorm input and normalise it on load in BOTH its forward
-    (streaming kernel) and its weight gradient (RC x RC GEMM over whole 64-pixel K-tiles)."""
-    return (g.is_pointwise and g.M % 64 == 0
-            and G.norm_on_load_fwd_ok(g.M, g.Co, g.Ci, g.Ci, g.Co))
-
-
-def conv_wgrad_native(dy, x, g: ConvGeometry, gw, x_norm=None):
-    """gw[Co, KH, KW, Ci] (fp32) += dW.  ``x_norm``: x is pre-BatchNorm (pointwise convs only)."""
+def conv_wgrad_native(dy, x, g: ConvGeometry, gw):
+    """gw[Co, KH, KW, Ci] (fp32) += dW."""
     gw2 = gw.view(g.Co, g.T * g.Ci)
-    if x_norm is not None and not g.is_pointwise:
-        raise ValueError("conv_wgrad_native: normalise-on-load for pointwise convs only")
     plan = None if g.is_pointwise else wgrad3_plan(g, dy.device)
     if g.is_pointwise:
-        G.linear_wgrad(dy.view(g.M, g.Co), x.view(g.M, g.Ci), gw2, x_norm=x_norm)
+        G.linear_wgrad(dy.view(g.M, g.Co), x.view(g.M, g.Ci), gw2)
     elif plan is not None:
         # 3x3 / stride 1: halo kernel (csrc/kernels/conv3x3.hip), 64 co x 64 ci x 9 taps per workgroup
         splits, tpb = plan

@@ -26,11 +26,6 @@ from .norm import new_stats_workspace, partials_workspace
 from .streams import on_grad_stream
 
 
-def _norm_of(st):
-    """(scale, shift) when the unit's BN output was NOT materialised (its consumer normalises on load)."""
-    return None if st.y is not None else (st.scale, st.shift)
-
-
 class _ConvBNState:
     """Per-(conv,BN) forward results needed by the backward.  ``pre_reduced``: the BN-backward
     partial sums [32, 2, C] already accumulated by the producer of this BN's output gradient
@@ -88,17 +83,16 @@ def _bn_forward(layer_bn, yc, stats, resid, relu, training, mask=None, apply=Tru
     return y, mean, invstd, scale, shift
 
 
-def convbn_forward(unit, x, resid=None, relu=True, apply=True, res_affine=None, x_norm=None):
+def convbn_forward(unit, x, resid=None, relu=True, apply=True, res_affine=None):
     """conv (fused statistics) + BN (+resid)(+relu) for a ``models.resnet.ConvBN`` unit.
-    ``apply=False``: statistics and scale/shift only (``st.y`` is None: the consumer applies them).
-    ``x_norm``: x is the pre-BN output of the previous unit, normalised on load by this conv."""
+    ``apply=False``: statistics and scale/shift only (``st.y`` is None: the consumer applies them)."""
     conv, bn = unit.conv, unit.bn
     N, H, W, Ci = x.shape
     kh, kw = conv.kernel_size
     p = conv.padding if isinstance(conv.padding, tuple) else (kh // 2, kw // 2)
     g = CV.geometry(N, H, W, Ci, conv.filters, kh, kw, conv.strides, p, conv.dilation_rate)
     stats = new_stats_workspace(conv.filters, x.device)
-    yc = CV.conv_fwd_native(x, conv.kernel.data, g, stats=stats, x_norm=x_norm)
+    yc = CV.conv_fwd_native(x, conv.kernel.data, g, stats=stats)
     st = _ConvBNState()
     st.g, st.yc = g, yc
     # ReLU after a residual add: the backward mask cannot be recomputed from yc alone, so the
@@ -154,14 +148,14 @@ def bn_backward(unit, st, dy, want_dres, red2=None, dy_mask=None, reduced=None):
     return dyc, dres
 
 
-def conv_backward(unit, st, dyc, x, need_dx, resid=None, resid_mask=None, bnr=None, rsub=None, x_norm=None):
+def conv_backward(unit, st, dyc, x, need_dx, resid=None, resid_mask=None, bnr=None, rsub=None):
     conv = unit.conv
     # the weight gradient only feeds the optimizer / all-reduce: it runs on the side stream
     # (ops/streams.py) beside the data-gradient and BatchNorm sweeps of the layers below
-    # (every tensor the side-stream kernel reads is recorded on that stream, the normalise-on-load
-    # scale / shift included: the main stream may drop them before the side stream has run)
-    with on_grad_stream(dyc.device, dyc, x, *(x_norm or ()), default=False):
-        CV.conv_wgrad_native(dyc, x, st.g, conv.kernel.grad, x_norm=x_norm)
+    # (every tensor the side-stream kernel reads is recorded on that stream: the main stream may
+    # drop them before the side stream has run)
+    with on_grad_stream(dyc.device, dyc, x, default=False):
+        CV.conv_wgrad_native(dyc, x, st.g, conv.kernel.grad)
     if conv.grad_hook is not None:
         conv.grad_hook()
     if not need_dx:
@@ -179,19 +173,9 @@ class _BottleneckFn(torch.autograd.Function):
         s_down = convbn_forward(block.down, x, relu=False, apply=False) if block.down is not None else None
         sc = s_down.yc if s_down is not None else x
         s1 = convbn_forward(block.c1, x, relu=True)
-        # normalise-on-load: conv3 (1x1) reads bn2's PRE-BN input and applies bn2 + ReLU as it loads it, in
-        # its forward (streaming kernel) and its weight gradient — bn2's apply sweep (a write and a re-read
-        # of the block's width-channel tensor) is not run
-        c2 = block.c2.conv
-        kh2, kw2 = c2.kernel_size
-        p2 = c2.padding if isinstance(c2.padding, tuple) else (kh2 // 2, kw2 // 2)
-        g2 = CV.geometry(x.shape[0], s1.g.Ho, s1.g.Wo, s1.g.Co, c2.filters, kh2, kw2, c2.strides, p2, c2.dilation_rate)
-        n3 = _NORM_ON_LOAD and CV.norm_on_load_ok(CV.geometry(x.shape[0], g2.Ho, g2.Wo, c2.filters,
-                                                              block.c3.conv.filters, 1, 1, (1, 1), (0, 0), (1, 1)))
-        s2 = convbn_forward(block.c2, s1.y, relu=True, apply=not n3)
-        s3 = convbn_forward(block.c3, s2.yc if n3 else s2.y, resid=sc, relu=True,
-                            res_affine=None if s_down is None else (s_down.scale, s_down.shift),
-                            x_norm=(s2.scale, s2.shift) if n3 else None)
+        s2 = convbn_forward(block.c2, s1.y, relu=True)
+        s3 = convbn_forward(block.c3, s2.y, resid=sc, relu=True,
+                            res_affine=None if s_down is None else (s_down.scale, s_down.shift))
         ctx.block, ctx.states = block, (s_down, s1, s2, s3)
         ctx.save_for_backward(x)
         ctx.needs_dx = ctx.needs_input_grad[0]
@@ -223,7 +207,7 @@ class _BottleneckFn(torch.autograd.Function):
         # accumulate those BNs' backward partial sums (ReLU mask recomputed from yc), so bn_backward skips the
         # reduce sweep wherever the kernel that ran could take it (bnr["done"])
         bnr2 = _bnr_mode2(s2, dout.device)
-        d2 = conv_backward(b.c3, s3, d3c, s2.yc if s2.y is None else s2.y, True, x_norm=_norm_of(s2), bnr=bnr2)
+        d2 = conv_backward(b.c3, s3, d3c, s2.y, True, bnr=bnr2)
         _take_reduced(s2, bnr2, d2)
         d2c, _ = bn_backward(b.c2, s2, d2, False)
         bnr1 = _bnr_mode2(s1, dout.device)
@@ -256,6 +240,9 @@ class _BottleneckFn(torch.autograd.Function):
             pst = ctx.prev[1]
             bnr = {"x": pst.yc, "mask": pst.mask, "mean": pst.mean,
                    "ws": new_stats_workspace(pst.yc.shape[-1], dout.device)}
+        if _TEST_MUTATION is not None and _TEST_MUTATION[0] == "drop_shortcut" and _TEST_MUTATION[1] in (None, b.name):
+            # test-only fault (tests/test_gpu_determinism.py): the block's input gradient loses its shortcut term
+            masked_sc, dsc, rsub = False, None, None
         if masked_sc:
             dx = conv_backward(b.c1, s1, d1c, x, ctx.needs_dx, resid=dout, resid_mask=s3.mask, bnr=bnr)
         else:
@@ -266,22 +253,18 @@ class _BottleneckFn(torch.autograd.Function):
         return dx, None, None
 
 
-import os as _os
 
-_FUSE_BNR = _os.environ.get("DDL_FUSE_BN_REDUCE", "1") != "0"
+_FUSE_BNR = True
+# test-only fault injection for the discriminating gradient checks: ("drop_shortcut", block name or None)
+_TEST_MUTATION = None
 # bn1 / bn2 of every bottleneck: reduce fused into the conv2 / conv3 data-gradient epilogues
-_FUSE_BNR_INNER = _os.environ.get("DDL_FUSE_BN_REDUCE_INNER", "1") != "0"
-_HALF_RES_SC = _os.environ.get("DDL_HALF_RES_SHORTCUT", "1") != "0"
+_FUSE_BNR_INNER = True
+_HALF_RES_SC = True
 # downsample BN backward fed by bn3's dx sweep (bn_bwd_dx_red): no masked-gradient tensor, no reduce sweep
-_FUSE_DOWN = _os.environ.get("DDL_FUSE_DOWN_BN", "1") != "0"
+_FUSE_DOWN = True
 # stem: BN backward through the max pool without materialising the pool's gradient (pool3s2_bn_bwd)
-_FUSE_STEM_BWD = _os.environ.get("DDL_FUSE_STEM_BWD", "1") != "0"
-_STEM_PARTIALS = int(_os.environ.get("DDL_STEM_PARTIALS", "2048"))  # workgroups (= partial rows) of its reduce
-# Normalise-on-load is opt-in (DDL_NORM_ON_LOAD=1): it removes bn2's apply sweep (-0.27 ms/step on
-# ResNet-50 b256) but the per-fragment scale/shift/ReLU VALU in the RC x RC weight gradient (+0.22 ms)
-# and the LDS transform pass + narrower panels of the streaming forward (+0.20 ms) cost more
-# (profiles/r3/ab/norm_on_load_kstats_diff.txt: 23.12 vs 22.91 ms/step).
-_NORM_ON_LOAD = _os.environ.get("DDL_NORM_ON_LOAD", "0") == "1"
+_FUSE_STEM_BWD = True
+_STEM_PARTIALS = 2048  # workgroups (= partial rows) of its reduce
 
 
 def _bnr_mode2(st, device):
@@ -315,12 +298,14 @@ def convbn_relu(unit, x, anchor, relu=True):
     return _ConvBNFn.apply(x, anchor, unit, relu)
 
 
+_STEM_S2D = True  # space-to-depth stem (tests switch it off to compare with the plain 7x7 conv)
+_STEM_POOL = True  # stem conv + BN + ReLU + max pool as one node
+
+
 def _stem_s2d_ok(conv, Ci) -> bool:
     """7x7 / stride 2 / pad 3 stem on <= 4 channels: run as a 4x4 stride-1 conv after a
     block-2 space-to-depth (12 of 16 channels used instead of 3 of 8, K = 256 instead of 392)."""
-    import os
-
-    return (os.environ.get("DDL_STEM_S2D", "1") != "0" and Ci <= 4 and tuple(conv.kernel_size) == (7, 7)
+    return (_STEM_S2D and Ci <= 4 and tuple(conv.kernel_size) == (7, 7)
             and tuple(conv.strides) == (2, 2) and tuple(conv.dilation_rate) == (1, 1)
             and (conv.padding == (3, 3) or conv.padding == 3 or conv.padding == "same"))
 
@@ -412,8 +397,8 @@ class _StemPoolFn(torch.autograd.Function):
 
 def stem_pool(unit, x, anchor, k=3, s=2, p=1):
     """Stem conv+BN+ReLU followed by a k x k / s max pool, fused when the space-to-depth stem applies
-    (``DDL_STEM_POOL=0`` keeps the separate apply + pool); returns None when not applicable."""
-    if (_os.environ.get("DDL_STEM_POOL", "1") == "0" or x.requires_grad or not _stem_s2d_ok(unit.conv, x.shape[-1])
+    (``_STEM_POOL = False`` keeps the separate apply + pool); returns None when not applicable."""
+    if (not _STEM_POOL or x.requires_grad or not _stem_s2d_ok(unit.conv, x.shape[-1])
             or unit.conv.filters % 8):
         return None
     return _StemPoolFn.apply(x, anchor, unit, k, s, p)

@@ -22,12 +22,9 @@ EPI_BF16, EPI_F32, EPI_F32_ATOMIC = 0, 1, 2
 TILE256 = 4  # 256x256 ping-pong kernel (csrc/include/ddl_gemm256.h): plain KC/RC operands, K % 64 == 0
 TILE_STREAM = 5  # weight-stationary streaming kernel (csrc/kernels/gemm_stream.hip): K in {64, 128, 256}
 TILE_CONV3 = 6  # 3x3 stride-1 halo convolution (csrc/kernels/conv3x3.hip): KC_GATHER x KC, no split-K
-TILE_W4 = 7  # four-wave 256x256 kernel, 128x128 wave tiles (csrc/include/ddl_gemm_w4.h): plain KC/RC, K % 64 == 0
-TILE_W4N = 8  # four-wave 256x128 kernel, 128x64 wave tiles
-TILE256P = 9  # the 256x256 ping-pong kernel in its persistent form (un-split GEMMs with more tiles than CUs)
 _TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), TILE256: (256, 256), TILE_STREAM: (64, 256),
-          TILE_CONV3: (224, 128), TILE_W4: (256, 256), TILE_W4N: (256, 128), TILE256P: (256, 256)}
-_ONE_PER_CU = (TILE256, TILE_W4, TILE_W4N, TILE256P)  # kernels running one workgroup per CU
+          TILE_CONV3: (224, 128)}
+_ONE_PER_CU = (TILE256,)  # kernels running one workgroup per CU
 _CU = 256
 import os as _os
 
@@ -35,20 +32,18 @@ import os as _os
 # GEMMs (8192^3: ~1045 vs ~810 TF for the 128-tile kernel) but loses on the BERT / ResNet
 # shapes (K <= 3072 with <= 2.25 workgroup rounds), so it is opt-in (DDL_GEMM256=1) and
 # auto-selected only for GEMMs with many tiles AND a long K loop.
-_USE256 = _os.environ.get("DDL_GEMM256", "auto")
-_USE_W4 = _os.environ.get("DDL_GEMM_W4", "0")  # four-wave 256-row kernel routing (use_w4); opt-in until measured
-_USE_W4_WGRAD = _os.environ.get("DDL_GEMM_W4_WGRAD", "0")  # ... for the fp32 weight gradients: "256" / "128"
+_USE256 = "auto"
 
 
-_USE_STREAM = _os.environ.get("DDL_GEMM_STREAM", "1")
+_USE_STREAM = "1"
 # 128x128 tiles per CU below which choose_tile shrinks the tile (one CU holds up to 4 blocks)
-_TILE_FILL = float(_os.environ.get("DDL_TILE_FILL", "2"))
+_TILE_FILL = 2.0
 # Linear data-gradients with at least this many rows use a transposed weight copy (KC x KC GEMM)
-_WT_MIN_M = int(_os.environ.get("DDL_DGRAD_WT_MIN_M", "4096"))
-_LINEAR_WGRAD_ROUNDS = float(_os.environ.get("DDL_LINEAR_WGRAD_ROUNDS", "1"))
+_WT_MIN_M = 4096
+_LINEAR_WGRAD_ROUNDS = 1.0
 # split-K fp32 GEMMs (weight gradients): workgroup rounds to aim for; every split adds one fp32
 # atomic per output element, so more rounds trade atomics for parallelism
-_SPLIT_ROUNDS = float(_os.environ.get("DDL_SPLIT_ROUNDS", "2"))
+_SPLIT_ROUNDS = 2.0
 
 
 def stream_panel(N: int, K: int) -> int:
@@ -77,25 +72,6 @@ def use_stream(M, N, K, a_mode, b_mode, epi, lda, ldc, *, outmap=None, aux=None,
     return True
 
 
-def bnr_stream_panels(N: int, K: int, resid: bool) -> int:
-    """Panels (re-reads of A) the streaming kernel takes for an (N, K) data-gradient WITH the fused BN reduce:
-    gemm_stream.hip narrows the panel to 128 columns (64 at K = 256) for those variants."""
-    nb = stream_panel(N, K)
-    if not nb:
-        return 0
-    if resid and K == 128 and nb == 256:
-        nb = 128
-    nb = min(nb, 64 if K >= 256 else 128)
-    return N // nb
-
-
-# a BN-reducing data-gradient goes to the LDS-DMA GEMM (EPI_BF16_BNR, residual included) instead of the
-# streaming kernel when the latter would re-read A over more panels than this.  Measured: the streaming
-# kernel wins even at 16 panels (ResNet-50 stage 3's conv1 data-gradient): 12,000-12,075 img/s vs
-# 11,767-11,812 (limit 4) and 11,469-11,485 (limit 2), interleaved (profiles/r4/fuse_bn/ab_bnr_panels.txt)
-_BNR_STREAM_MAX_PANELS = int(_os.environ.get("DDL_BNR_STREAM_MAX_PANELS", "1000"))
-
-
 def use_tile256(M: int, N: int, K: int, a_mode: int, b_mode: int, epi: int) -> bool:
     """The 256x256 kernel pays off when its tiles (times split-K for fp32 outputs) fill the chip."""
     if _USE256 == "0" or a_mode > RC or b_mode > RC or K % 64 or M < 128 or N < 128:
@@ -104,30 +80,6 @@ def use_tile256(M: int, N: int, K: int, a_mode: int, b_mode: int, epi: int) -> b
     if _USE256 == "1":
         return tiles >= _CU // 2
     return epi == EPI_BF16 and tiles >= 4 * _CU and K >= 4096
-
-
-def use_w4(M: int, N: int, K: int, a_mode: int, b_mode: int, epi: int):
-    """Tile id of the four-wave 256-row kernel for this GEMM, or None.  DDL_GEMM_W4: 0 = off, 1 = when its
-    tiles fill whole rounds of the chip (256x256 first, then 256x128), 2 = 256x256 whenever it applies."""
-    if a_mode > RC or b_mode > RC or K % 64 or M < 256 or N < 128:
-        return None
-    if epi == EPI_F32:  # weight gradients (split-K over the long token dimension): DDL_GEMM_W4_WGRAD=256 / 128
-        if _USE_W4_WGRAD == "256" and N >= 256 and K >= 2048:
-            return TILE_W4
-        if _USE_W4_WGRAD == "128" and K >= 2048:
-            return TILE_W4N
-        return None
-    if _USE_W4 == "0" or epi != EPI_BF16:
-        return None
-    t256 = math.ceil(M / 256) * math.ceil(N / 256)
-    if _USE_W4 == "2":
-        return TILE_W4 if N >= 256 else TILE_W4N
-    if N >= 256 and t256 >= _CU and (t256 % _CU == 0 or t256 >= 6 * _CU):
-        return TILE_W4
-    t128 = math.ceil(M / 256) * math.ceil(N / 128)
-    if t128 >= _CU and (t128 % _CU == 0 or t128 >= 6 * _CU):
-        return TILE_W4N
-    return None
 
 
 def choose_tile(M: int, N: int, bn_cap: int = 128) -> int:
@@ -161,7 +113,7 @@ def choose_split(M: int, N: int, K: int, tile: int, allow: bool, rounds: float |
 def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, beta=0.0, bias=None, resid=None,
          ldr=0, relu=False, geom=None, outmap=None, b_kdiv=0, b_tap_stride=0, stats=None, tile=None, k_split=None,
          bn_cap=128, aux=None, drop_p=0.0, drop_seed=0, split_rounds=None, resid_mask=None, bnr=None, rsub=None,
-         a_norm=None, b_norm=None, slabs=None, defer_slabs=False):
+         slabs=None, defer_slabs=False):
     """Raw launcher with automatic tile / split-K choice.  ``slabs``: force (True) or forbid (False) the
     partial-slab split-K path of fp32 outputs (default: deterministic mode or DDL_SPLITK_SLABS);
     ``defer_slabs``: when that path is taken, skip the reduce and return ``(slabs, splits)`` for a
@@ -176,9 +128,6 @@ def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, bet
         if use_stream(M, N, K, a_mode, b_mode, epi, lda, ldc, outmap=outmap, aux=aux, drop_p=drop_p, relu=relu,
                       beta=beta, resid=resid, ldr=ldr):
             tile = TILE_STREAM
-        elif (outmap is None and bnr is None and a_norm is None and b_norm is None
-              and use_w4(M, N, K, a_mode, b_mode, epi) is not None):
-            tile = use_w4(M, N, K, a_mode, b_mode, epi)
         elif outmap is None and bnr is None and use_tile256(M, N, K, a_mode, b_mode, epi):
             tile = TILE256
         elif epi == EPI_F32 and a_mode <= RC and b_mode <= RC and big_wgrad(M, N, K) and _SPLITK_SLABS_MODE != "0":
@@ -211,8 +160,7 @@ def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, bet
     C().gemm(a, b, out, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, tile, k_split, alpha, beta, bias, resid, ldr,
              int(relu), geom, outmap, b_kdiv, b_tap_stride, stats, aux, float(drop_p), int(drop_seed), resid_mask,
              None if bnr is None else bnr["x"], None if bnr is None else bnr.get("mask"),
-             None if bnr is None else bnr["mean"], *(rsub or (0, 0)), *(a_norm or (None, None)),
-             *(b_norm or (None, None)), None if bnr is None else bnr.get("scale"),
+             None if bnr is None else bnr["mean"], *(rsub or (0, 0)), None if bnr is None else bnr.get("scale"),
              None if bnr is None else bnr.get("shift"), split_stride)
     if split_stride:
         if defer_slabs:
@@ -256,12 +204,10 @@ ACT_NONE, ACT_RELU, ACT_GELU, ACT_GELU_BWD = 0, 1, 2, 3
 
 
 def linear_fwd(x2, w, bias=None, relu=False, out=None, resid=None, stats=None, act=None, aux=None, drop_p=0.0,
-               drop_seed=0, x_norm=None):
+               drop_seed=0):
     """y[M,N] = x2[M,K] @ w[N,K]^T (+bias) -> act -> dropout (+resid) -> bf16.
 
-    ``act``: ACT_RELU / ACT_GELU (``aux`` receives the bf16 pre-activation).  ``x_norm = (scale,
-    shift)``: x2 is a pre-BatchNorm tensor, normalised on load as relu(x * scale + shift) per channel
-    (streaming kernel only: check :func:`norm_on_load_fwd_ok` first)."""
+    ``act``: ACT_RELU / ACT_GELU (``aux`` receives the bf16 pre-activation)."""
     M, K = x2.shape
     N = w.shape[0]
     if out is None:
@@ -269,12 +215,7 @@ def linear_fwd(x2, w, bias=None, relu=False, out=None, resid=None, stats=None, a
     act = (ACT_RELU if relu else ACT_NONE) if act is None else act
     return gemm(x2, w, out, M, N, K, KC, KC, x2.stride(0), w.stride(0), out.stride(0), EPI_BF16, bias=bias, relu=act,
                 resid=resid, ldr=(resid.stride(0) if resid is not None else 0), stats=stats, aux=aux, drop_p=drop_p,
-                drop_seed=drop_seed, a_norm=x_norm, tile=TILE_STREAM if x_norm is not None else None)
-
-
-def norm_on_load_fwd_ok(M, N, K, lda, ldc) -> bool:
-    """A forward 1x1 conv / Linear y = x W^T can normalise x on load (the streaming kernel runs it)."""
-    return use_stream(M, N, K, KC, KC, EPI_BF16, lda, ldc)
+                drop_seed=drop_seed)
 
 
 _SPLITK_WS = {}
@@ -292,7 +233,7 @@ def splitk_workspace(M, N, device):
     return ws
 
 
-_SPLITK_DGRAD = _os.environ.get("DDL_DGRAD_SPLITK", "1") != "0"
+_SPLITK_DGRAD = True
 
 
 def linear_dgrad(dy, w, out=None, resid=None, gelu_pre=None, stats=None, resid_mask=None, bnr=None, rsub=None):
@@ -327,18 +268,14 @@ def linear_dgrad(dy, w, out=None, resid=None, gelu_pre=None, stats=None, resid_m
         else:
             C().splitk_finalize(ws, out, K, None, False, stats)
         return out
-    bnr_wide = (bnr is not None and stats is None
-                and bnr_stream_panels(K, N, resid is not None) > _BNR_STREAM_MAX_PANELS
-                and _bnr_plain_ok(bnr, stats, resid, gelu_pre, K))
-    if M >= _WT_MIN_M and (bnr_wide or not use_stream(M, K, N, KC, RC, EPI_BF16, dy.stride(0), out.stride(0),
-                                                       aux=gelu_pre, relu=act, resid=resid, ldr=ldr)):
+    if M >= _WT_MIN_M and not use_stream(M, K, N, KC, RC, EPI_BF16, dy.stride(0), out.stride(0), aux=gelu_pre,
+                                         relu=act, resid=resid, ldr=ldr):
         # transpose the (small) weight once so the GEMM reads B K-contiguous with ds_read_b128 instead
         # of paired transposed LDS reads: the BERT-size data-gradients run ~1.4x faster this way
         wt = transpose(w)
         fb = _bnr_plain_ok(bnr, stats, resid, gelu_pre, K)
         gemm(dy, wt, out, M, K, N, KC, KC, dy.stride(0), wt.stride(0), out.stride(0), EPI_BF16, resid=resid,
-             ldr=ldr, relu=act, aux=gelu_pre, stats=stats, resid_mask=resid_mask, rsub=rsub, bnr=bnr if fb else None,
-             tile=choose_tile(M, K) if bnr_wide else None)  # (not the streaming kernel: see bnr_wide)
+             ldr=ldr, relu=act, aux=gelu_pre, stats=stats, resid_mask=resid_mask, rsub=rsub, bnr=bnr if fb else None)
         if fb:
             bnr["done"] = True
         return out
@@ -376,20 +313,17 @@ def transpose(w):
     return out
 
 
-def linear_wgrad(dy, x2, gw, x_norm=None):
-    """gw[N,K] += dy[M,N]^T @ x2[M,K]  (fp32 accumulation into the gradient arena).  ``x_norm``: x2 is
-    pre-BatchNorm, normalised on load per channel (needs M % 64 == 0: whole K-tiles)."""
+def linear_wgrad(dy, x2, gw):
+    """gw[N,K] += dy[M,N]^T @ x2[M,K]  (fp32 accumulation into the gradient arena)."""
     M, N = dy.shape
     K = x2.shape[1]
-    if x_norm is not None and M % 64:
-        raise ValueError("linear_wgrad: normalise-on-load needs M % 64 == 0")
     # measured on the ResNet-50 1x1 weight gradients: one workgroup round (half the fp32 atomics
     # of two rounds) is 5-15 % faster — these GEMMs are bound by the split-K atomics, not MFMA
     # (the large BERT weight gradients, on 128x128 tiles with partial slabs, take two rounds: 8 splits
     # measured 642-739 TF/s vs 629-689 at one round, profiles/r4/wgrad_slabs_ab.txt)
-    rounds = None if (x_norm is None and big_wgrad(N, K, M) and _SPLITK_SLABS_MODE == "auto") else _LINEAR_WGRAD_ROUNDS
+    rounds = None if (big_wgrad(N, K, M) and _SPLITK_SLABS_MODE == "auto") else _LINEAR_WGRAD_ROUNDS
     return gemm(dy, x2, gw, N, K, M, RC, RC, dy.stride(0), x2.stride(0), gw.stride(0), EPI_F32, beta=1.0,
-                split_rounds=rounds, b_norm=x_norm)
+                split_rounds=rounds)
 
 
 def matmul(a, b, trans_a=False, trans_b=False, out=None, alpha=1.0):

@@ -28,7 +28,6 @@ fork / join through events, so a captured step keeps the overlap.
 """
 from __future__ import annotations
 
-import os
 from contextlib import contextmanager
 
 import torch
@@ -42,8 +41,7 @@ def enabled(default: bool = True) -> bool:
 
     if _scope.tag():  # replica-group steps run on their own streams: no shared side stream
         return False
-    v = os.environ.get("DDL_WGRAD_STREAM", "auto")
-    return default if v == "auto" else v != "0"
+    return default
 
 
 def _key(device) -> int:

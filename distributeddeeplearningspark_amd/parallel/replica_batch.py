@@ -1,0 +1,191 @@
+"""Replica-batched execution of co-located recurrent workers: the R replicas of a ``ReplicaGroup``
+(``parallel/replicas.py``) step as ONE launch per phase instead of R graph replays on R streams.
+
+The reference's NYISO workload (``ddl_nyiso_aztk.py:195-218``; ``ddl_nyiso_hdi.ipynb:577-609``) trains
+GRU(128) -> Dense(1) and LSTM(128) -> Dense(1) regressors with an MSE loss on ADAG workers, two per
+executor.  Co-located on one MI355X, each replica step is a few latency-bound kernels on 32 batch
+rows; run replica by replica, the GPU is mostly idle between them.  Here one step of ALL replicas is
+(``csrc/kernels/rnn.hip``, ``rnn_replica_step``):
+
+  1. the recurrent forward over R x B batch rows, each workgroup reading its replica's U / W / bias
+     and its mini-batch from the replica's resident shard (index = device step counter % batches);
+  2. the Dense head, MSE loss and their backward, one workgroup per replica (loss -> the replica's
+     device history, Adam step tick);
+  3. the recurrent backward over R x B rows;
+  4. the recurrent parameter gradients, one grid slice per replica, written (not accumulated);
+  5. one optimizer sweep over the R flat arenas, which also advances the step counter.
+
+A commit window of ``k`` steps for all replicas is captured into ONE hipGraph and replayed per round;
+the commit itself is the group's ``commit_replicas`` kernel, unchanged.  The update law, histories,
+``num_updates`` and optimizer state are those of the per-replica path (tests/test_gpu_colocated.py
+compares the two to fp32 rounding).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from ..models import optimizers as opt_mod
+
+
+def _layers(model):
+    from ..models.core import Sequential
+    from ..models.layers import GRU, LSTM, Dense
+
+    if not isinstance(model, Sequential) or len(model.layers) != 2:
+        return None
+    rnn, dense = model.layers
+    if type(rnn) not in (GRU, LSTM) or type(dense) is not Dense:
+        return None
+    return rnn, dense
+
+
+def applies(group) -> bool:
+    """The group's replicas are RNN(64|128) -> Dense(K) / MSE fp32 models with a supported worker
+    optimizer, equal shards (the replicas step in lockstep) and at most 8 replicas."""
+    if os.environ.get("DDL_REPLICA_BATCH", "1") == "0" or not group.gpu or group.rule == "averaging":
+        return False
+    reps = group.reps
+    if not (1 < len(reps) <= 8):
+        return False
+    from ..ops._native import C
+
+    if len({(r.nb, r.steps, r.commits) for r in reps}) != 1:
+        return False
+    for r in reps:
+        m = r.model
+        ls = _layers(m)
+        if ls is None or m.loss != "mean_squared_error" or m.arena.compute is not m.arena.master:
+            return False
+        rnn, dense = ls
+        if (rnn.return_sequences or not rnn.use_bias or rnn.activation != "tanh"
+                or rnn.recurrent_activation != "hard_sigmoid" or not rnn.trainable or not dense.trainable):
+            return False
+        if dense.activation_name not in (None, "linear") or dense.kernel.data.shape[1] != rnn.units:
+            return False
+        o = m.optimizer
+        if getattr(o, "clipnorm", None) is not None or m.arena.numel % 4:
+            return False
+        if isinstance(o, opt_mod.SGD):
+            if o.nesterov or o.dampening:
+                return False
+        elif not isinstance(o, (opt_mod.Adagrad, opt_mod.Adam)):
+            return False
+        X = r.X
+        if X.dim() != 3 or X.dtype != torch.float32 or r.Y.dtype != torch.float32:
+            return False
+        if r.Y.numel() != r.Y.shape[0] * dense.units or not (X.is_contiguous() and r.Y.is_contiguous()):
+            return False
+        if not C().rnn_replica_ok(rnn.cell, rnn.units, int(X.shape[2]), dense.units, r.bs):
+            return False
+    return True
+
+
+class BatchedReplicas:
+    """Device state of the batched step for the replicas of one group (see module doc)."""
+
+    def __init__(self, group):
+        self.group = group
+        reps = group.reps
+        r0 = reps[0]
+        rnn0, dense0 = _layers(r0.model)
+        self.cell, self.H, self.K = rnn0.cell, rnn0.units, dense0.units
+        self.T, self.I = int(r0.X.shape[1]), int(r0.X.shape[2])
+        self.B, self.nb, self.R = r0.bs, r0.nb, len(reps)
+        dev = r0.model.device
+        G = 3 if self.cell == "gru" else 4
+        RB, T, H = self.R * self.B, self.T, self.H
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.hs = torch.empty((RB, T + 1, H), **f32)
+        self.cs = torch.empty((RB, T + 1, H) if self.cell == "lstm" else (1,), **f32)
+        self.gates = torch.empty((RB, T, G * H), **f32)
+        self.hlast = torch.empty((RB, H), **f32)
+        self.dh = torch.empty((RB, H), **f32)
+        self.dgates = torch.empty((RB, T, G * H), **f32)
+        self.ctr = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.graph = None
+        o = r0.model.optimizer
+        if isinstance(o, opt_mod.Adam):
+            self.opt, self.p1, self.p2 = 2, o.b1, o.b2
+            self.amode = (1 if o.decoupled else 0) | (2 if o.keras_eps else 0)
+        elif isinstance(o, opt_mod.Adagrad):
+            self.opt, self.p1, self.p2, self.amode = 1, 0.0, 0.0, 0
+        else:
+            self.opt, self.p1, self.p2, self.amode = 0, o.momentum, 0.0, 0
+        self.lr, self.eps, self.wd = o.lr, getattr(o, "eps", 0.0), o.weight_decay
+        lists = {k: [] for k in ("xs", "ys", "Ws", "Us", "bs", "Wds", "bds", "gWs", "gUs", "gbs", "gWds", "gbds",
+                                 "hists", "ws", "gs", "s1s", "s2s", "ts")}
+        for r in reps:
+            m = r.model
+            rnn, dense = _layers(m)
+            if self.opt == 2:
+                m.optimizer.enable_device_step()
+            lists["xs"].append(r.X)
+            lists["ys"].append(r.Y.reshape(r.Y.shape[0], -1))
+            lists["Ws"].append(rnn.kernel.data)
+            lists["Us"].append(rnn.recurrent_kernel.data)
+            lists["bs"].append(rnn.bias.data)
+            lists["Wds"].append(dense.kernel.data)
+            lists["bds"].append(None if dense.bias is None else dense.bias.data)
+            lists["gWs"].append(rnn.kernel.grad)
+            lists["gUs"].append(rnn.recurrent_kernel.grad)
+            lists["gbs"].append(rnn.bias.grad)
+            lists["gWds"].append(dense.kernel.grad)
+            lists["gbds"].append(None if dense.bias is None else dense.bias.grad)
+            lists["hists"].append(r.hist)
+            lists["ws"].append(m.arena.master.detach())
+            lists["gs"].append(m.arena.grad)
+            st = m.optimizer.state
+            lists["s1s"].append(st.get("m", st.get("acc", st.get("momentum"))))
+            lists["s2s"].append(st.get("v"))
+            lists["ts"].append(m.optimizer.device_step if self.opt == 2 else None)
+        self.args = lists
+
+    def _step(self):
+        from ..ops._native import C
+
+        a = self.args
+        C().rnn_replica_step(self.cell, a["xs"], a["ys"], a["Ws"], a["Us"], a["bs"], a["Wds"], a["bds"], a["gWs"],
+                             a["gUs"], a["gbs"], a["gWds"], a["gbds"], a["hists"], self.ctr, self.nb, self.B,
+                             self.hs, self.cs, self.gates, self.hlast, self.dh, self.dgates, a["ws"], a["gs"],
+                             a["s1s"], a["s2s"], a["ts"], self.opt, self.lr, self.p1, self.p2, self.eps, self.wd,
+                             self.amode)
+
+    def run_steps(self, n: int):
+        """n steps of every replica (eager launches on the current stream)."""
+        for _ in range(n):
+            self._step()
+        self._advance(n)
+
+    def capture(self, k: int) -> bool:
+        """Capture a k-step window of all replicas into one hipGraph (False: capture failed, stay eager)."""
+        dev = self.group.pg.device
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        g = torch.cuda.CUDAGraph()
+        try:
+            if os.environ.get("DDL_TEST_FAIL_CAPTURE") == "1":  # test hook: force the eager fallback
+                raise RuntimeError("capture forced to fail (DDL_TEST_FAIL_CAPTURE)")
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, stream=s):
+                    for _ in range(k):
+                        self._step()
+        except Exception as e:
+            if os.environ.get("DDL_GRAPHS_STRICT") == "1":
+                raise
+            print(f"[ddl] batched replica hipGraph capture disabled: {type(e).__name__}: {e}", flush=True)
+            torch.cuda.synchronize(dev)
+            return False
+        torch.cuda.current_stream(dev).wait_stream(s)
+        self.graph, self.k = g, k
+        return True
+
+    def replay(self):
+        self.graph.replay()
+        self._advance(self.k)
+
+    def _advance(self, n: int):
+        for r in self.group.reps:  # host mirrors of the device counters
+            r.done += n
+            r.model.optimizer.iterations += n

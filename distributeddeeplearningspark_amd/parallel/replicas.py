@@ -202,6 +202,7 @@ class ReplicaGroup:
         self.sum = torch.zeros_like(self.center) if (pg.distributed and self.gpu) else None
         self.commit_s = 0.0
         self.graph_rounds = 0
+        self.batched = None  # replica_batch.BatchedReplicas when the replicas step as one launch per phase
 
     @staticmethod
     def _resident(a, model, labels=False):
@@ -293,6 +294,12 @@ class ReplicaGroup:
                 self._window_all([rep], rep.steps, False)
             self._average()
             return
+        from . import replica_batch
+
+        if replica_batch.applies(self):
+            self.batched = replica_batch.BatchedReplicas(self)
+            self._run_batched(graphs)
+            return
         for j in range(self.rounds):
             todo = [r for r in self.reps if j < r.commits]
             if graphs and j == warm_rounds:
@@ -308,6 +315,24 @@ class ReplicaGroup:
                 self._window_all([r], r.steps - r.done, False)
         if self.gpu:
             torch.cuda.synchronize(self.pg.device)
+
+    def _run_batched(self, graphs: bool):
+        """Every replica steps in lockstep (equal shards): round j = one k-step window of ALL replicas
+        (one hipGraph replay from round 1 on; round 0 runs eagerly) + the commit kernel."""
+        bat, k = self.batched, self.k
+        for j in range(self.rounds):
+            if graphs and j == 1 and bat.graph is None:
+                graphs = bat.capture(k)
+            if graphs and bat.graph is not None:
+                bat.replay()
+                self.graph_rounds += 1
+            else:
+                bat.run_steps(k)
+            self._commit(j)
+        left = self.reps[0].steps - self.reps[0].done  # steps after the last commit round (history only)
+        if left > 0:
+            bat.run_steps(left)
+        torch.cuda.synchronize(self.pg.device)
 
     def _capture(self, reps) -> bool:
         """Capture every replica's window; on failure fall back to eager windows (capture is an
@@ -361,8 +386,10 @@ def train_group(rank, world, pg, cfg, blob, Xs, Ys, rids, sizes):
     for i, rep in enumerate(grp.reps):
         res = {"rank": rep.rid, "history": rep.losses(), "num_updates": grp.num_updates(), "time": elapsed,
                "commit_s": grp.commit_s, "commit_wait_s": None, "commit_xfer_s": None,
-               "graph": rep.graph is not None, "ingest": "resident", "timed_s": None, "timed_steps": 0,
-               "replica_group": {"group": rank, "groups": world, "replicas": len(grp.reps)}}
+               "graph": (grp.batched.graph is not None) if grp.batched is not None else rep.graph is not None,
+               "ingest": "resident", "timed_s": None, "timed_steps": 0,
+               "replica_group": {"group": rank, "groups": world, "replicas": len(grp.reps),
+                                 "batched": grp.batched is not None}}
         if rep.rid == 0:
             res["flat"] = grp.center.cpu().numpy().copy()
             res["states"] = get_states(rep.model)

@@ -74,16 +74,11 @@ def main():
         out = torch.zeros(M, N, dtype=torch.float32 if f32 else torch.bfloat16, device="cuda")
         ref = (A[:256].float() @ B.float().T)
         runs = {}
-        variants = {"g256": G.TILE256, "g256p": G.TILE256P, "t128": G.choose_tile(M, N)}
+        variants = {"g256": G.TILE256, "t128": G.choose_tile(M, N)}
         if f32:  # weight gradients: the production tile choice (gemm picks tile and split-K) and 128x128
             variants = {"auto": None, "t128": 0}
         elif not (M >= 256 and N >= 256 and K % 64 == 0):
             variants.pop("g256")
-            variants.pop("g256p")
-        if os.environ.get("DDL_BENCH_W4", "1") == "1" and M >= 256 and N >= 128 and K % 64 == 0:  # the four-wave 256-row kernels (ddl_gemm_w4.h)
-            if N >= 256:
-                variants["w4"] = G.TILE_W4
-            variants["w4n"] = G.TILE_W4N
         def run(tile):
             if f32 and tile is None:  # the production call (tile, split-K rounds, slabs / atomics)
                 return G.linear_wgrad(a_t, b_t, out)

@@ -73,3 +73,57 @@ def test_replica_group_matches_process_workers(algo, monkeypatch):
     for a, b in zip(res_grp, res_ipc):
         assert len(a["history"]) == len(b["history"])
         np.testing.assert_allclose(a["history"], b["history"], rtol=1e-3, atol=1e-5)
+
+
+def _seq_frame(n=1024, T=25, seed=1):
+    from distributeddeeplearningspark_amd.sql.dataframe import from_columns
+
+    rng = np.random.default_rng(seed)
+    x = np.cumsum(rng.normal(size=(n, T, 1)) * 0.1, axis=1).astype(np.float32)
+    y = (x[:, -1:, 0] * 0.8 + 0.1).astype(np.float32)
+    return from_columns({"features": x, "label": y}, num_partitions=4)
+
+
+def _train_rnn(cell, opt, batched, monkeypatch):
+    from distributeddeeplearningspark_amd import trainers as T
+    from distributeddeeplearningspark_amd.models.zoo import gru_regressor, lstm_regressor
+
+    monkeypatch.setenv("DDL_WORKERS_PER_GPU", "4")
+    monkeypatch.setenv("DDL_REPLICA_GROUPS", "1")
+    monkeypatch.setenv("DDL_REPLICA_BATCH", "1" if batched else "0")
+    m = (gru_regressor if cell == "gru" else lstm_regressor)(128)
+    tr = T.ADAG(keras_model=m, worker_optimizer=opt, loss="mean_squared_error", num_workers=4, batch_size=32,
+                num_epoch=3, features_col="features", label_col="label", communication_window=5)
+    out = tr.train(_seq_frame())
+    return out.arena.master.detach().cpu().clone(), tr.parameter_server.num_updates, tr._results
+
+
+@pytest.mark.parametrize("cell,opt", [("gru", "adagrad"), ("lstm", "adam"), ("gru", "sgd")])
+def test_batched_replicas_match_stream_replicas(cell, opt, monkeypatch):
+    """Replica-batched recurrent step (parallel/replica_batch.py, rnn.hip rnn_replica_step: one launch
+    per phase for all four replicas, one hipGraph per commit window) vs the per-replica path (each
+    replica's window graph-replayed on its own stream): same update count, the same per-replica loss
+    histories and the same trained center to fp32 rounding (the parameter-gradient reduction order
+    differs: chunked rows summed in order vs fp32 atomics per chunk)."""
+    w_b, n_b, res_b = _train_rnn(cell, opt, True, monkeypatch)
+    w_s, n_s, res_s = _train_rnn(cell, opt, False, monkeypatch)
+    assert all(r["replica_group"]["batched"] for r in res_b), "batched path not used"
+    assert not any(r["replica_group"]["batched"] for r in res_s)
+    assert all(r["graph"] for r in res_b)
+    assert n_b == n_s > 0
+    for a, b in zip(res_b, res_s):
+        assert len(a["history"]) == len(b["history"]) > 0
+        np.testing.assert_allclose(a["history"], b["history"], rtol=2e-3, atol=1e-5)
+    torch.testing.assert_close(w_b, w_s, rtol=2e-3, atol=2e-4)
+
+
+@pytest.mark.parametrize("batched", [False, True])
+def test_replica_capture_failure_falls_back_to_eager(batched, monkeypatch):
+    """A replica group whose hipGraph capture fails keeps training eagerly: same updates and
+    the same trained center as the graph-replayed run."""
+    w_g, n_g, res_g = _train_rnn("gru", "adagrad", batched, monkeypatch)
+    monkeypatch.setenv("DDL_TEST_FAIL_CAPTURE", "1")
+    w_e, n_e, res_e = _train_rnn("gru", "adagrad", batched, monkeypatch)
+    assert all(r["graph"] for r in res_g) and not any(r["graph"] for r in res_e)
+    assert n_g == n_e > 0
+    torch.testing.assert_close(w_e, w_g, rtol=1e-5, atol=1e-6)

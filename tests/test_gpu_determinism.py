@@ -137,3 +137,80 @@ def test_resnet50_full_depth_gradient_direction_per_stage():
     for k in cos:
         assert cos[k] > base[k], (k, cos[k], base[k])
     assert cos["head"] > 0.9, cos
+
+
+def _resnet50_conditioned(dev, noise=0.0, gamma3=0.2, mutation=None):
+    """One deterministic full-depth ResNet-50 step at a WELL-CONDITIONED point: every bottleneck's last
+    BN scale (gamma3) set to ``gamma3`` so each residual branch is a small perturbation of its shortcut
+    (the zero-init-residual idea without zeroing the branch gradients).  Returns (model, loss, grads)."""
+    from distributeddeeplearningspark_amd.models import ResNet50
+    from distributeddeeplearningspark_amd.ops import fused_blocks as FB
+    from distributeddeeplearningspark_amd.ops.determinism import deterministic
+
+    torch.manual_seed(0)
+    x = torch.randn(16, 64, 64, 3)
+    y = torch.randint(0, 10, (16,))
+    if noise:
+        x = x * (1 + noise * torch.randn(x.shape, generator=torch.Generator().manual_seed(101)))
+    old = FB._TEST_MUTATION
+    FB._TEST_MUTATION = mutation
+    try:
+        with deterministic(dev != "cpu"):
+            m = ResNet50(input_shape=(64, 64, 3), num_classes=10)
+            m.compile("sgd", "sparse_categorical_crossentropy")
+            m.place(dev, seed=3)
+            with torch.no_grad():
+                for blk in m.stages:
+                    blk.c3.bn.gamma.master.fill_(gamma3)
+            m.arena.sync_compute()
+            loss = m.backward_step(m.to_input(x), m.to_target(y))
+            if dev != "cpu":
+                torch.cuda.synchronize()
+    finally:
+        FB._TEST_MUTATION = old
+    return m, float(loss.detach()), m.arena.grad.detach().float().cpu().clone()
+
+
+def _stage_cosines(m, ga, gb):
+    stages: dict = {}
+    for p in m.arena.params:
+        if not p.trainable:
+            continue
+        sl = slice(p.offset, p.offset + p.numel)
+        st = stages.setdefault(_stage_of(p.name), ([], []))
+        st[0].append(ga[sl])
+        st[1].append(gb[sl])
+    return {k: torch.nn.functional.cosine_similarity(torch.cat(a), torch.cat(b), dim=0).item()
+            for k, (a, b) in stages.items()}
+
+
+def test_resnet50_gradient_per_stage_well_conditioned():
+    """SURVEY §7.6 oracle at a point where it can discriminate: with gamma3 = 0.2 the
+    fp32 CPU gradient is stable under a 2^-7 input perturbation (asserted: >= 0.95 per stage), and the
+    deterministic HIP gradient must match it per stage to >= 0.95 cosine.  The mutation test below shows
+    the same assertion failing when one block's shortcut gradient is dropped."""
+    m, lc, gc = _resnet50_conditioned("cpu")
+    _, _, gp = _resnet50_conditioned("cpu", noise=2.0**-7)
+    _, lg, gg = _resnet50_conditioned(DEV)
+    base = _stage_cosines(m, gc, gp)
+    cos = _stage_cosines(m, gc, gg)
+    print("well-conditioned per-stage cosine, fp32 CPU vs 2^-7 perturbed:", {k: round(v, 4) for k, v in base.items()})
+    print("well-conditioned per-stage cosine, det GPU vs fp32 CPU:", {k: round(v, 4) for k, v in cos.items()})
+    assert set(cos) >= {"stem", "stage1", "stage2", "stage3", "stage4", "head"}, cos
+    assert abs(lg - lc) < 0.02 * max(1.0, abs(lc)), (lg, lc)
+    for k in cos:
+        assert base[k] >= 0.95, ("the check point is not well conditioned", k, base[k])
+        assert cos[k] >= 0.95, (k, cos[k])
+
+
+def test_resnet50_gradient_check_catches_dropped_shortcut_term():
+    """Mutation test of the per-stage oracle: the HIP backward with ONE block's shortcut gradient dropped
+    (fused_blocks._TEST_MUTATION, stage 3's last block) must fail the >= 0.95 per-stage assertion in every
+    stage below that block, while the stages above it (stage 4, head) still pass."""
+    m, _, gc = _resnet50_conditioned("cpu")
+    _, _, gbad = _resnet50_conditioned(DEV, mutation=("drop_shortcut", "resnet50/s3b6"))
+    cos = _stage_cosines(m, gc, gbad)
+    print("per-stage cosine with stage 3 block 6's shortcut gradient dropped:", {k: round(v, 4) for k, v in cos.items()})
+    for k in ("stem", "stage1", "stage2"):
+        assert cos[k] < 0.95, (k, cos[k])
+    assert cos["stage4"] >= 0.95 and cos["head"] >= 0.95, cos

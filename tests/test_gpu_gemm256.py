@@ -1,7 +1,5 @@
-"""The 256-row GEMM kernels against fp32 references: the 256x256 ping-pong kernel
-(csrc/include/ddl_gemm256.h), in its persistent form too, and the four-wave 256x256 / 256x128 kernels
-(ddl_gemm_w4.h) — every operand layout, every epilogue, tails in M and N, split-K (atomics and partial
-slabs).  The persistent form engages with more tiles than CUs: the shapes marked below have 272-289 tiles."""
+"""The 256x256 ping-pong GEMM kernel (csrc/include/ddl_gemm256.h) against fp32 references: every operand
+layout, every epilogue, tails in M and N, split-K (atomics and partial slabs)."""
 import pytest
 import torch
 
@@ -9,7 +7,7 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-TILES = [4, 7, 8, 9]  # G.TILE256, G.TILE_W4, G.TILE_W4N, G.TILE256P
+TILES = [4]  # G.TILE256
 
 
 def rnd(*shape, seed=0, scale=1.0):
@@ -101,19 +99,3 @@ def test_gemm256_auto_selected_for_bert_shapes():
     assert not G.use_tile256(16384, 3072, 100, G.KC, G.KC, G.EPI_BF16)
 
 
-def test_w4_routing():
-    from distributeddeeplearningspark_amd.ops import gemm as G
-
-    old = G._USE_W4
-    try:
-        G._USE_W4 = "1"
-        assert G.use_w4(16384, 3072, 768, G.KC, G.KC, G.EPI_BF16) == G.TILE_W4  # 768 tiles: 3 rounds
-        assert G.use_w4(16384, 2304, 768, G.KC, G.KC, G.EPI_BF16) is None  # 576 / 1152 tiles: partial rounds
-        assert G.use_w4(65536, 768, 768, G.KC, G.KC, G.EPI_BF16) == G.TILE_W4  # 768 256x256 tiles: 3 rounds
-        assert G.use_w4(65536, 128, 768, G.KC, G.KC, G.EPI_BF16) == G.TILE_W4N  # 256 256x128 tiles: one round
-        assert G.use_w4(16384, 768, 768, G.KC, G.KC, G.EPI_BF16) is None  # 384 tiles: 1.5 rounds
-        assert G.use_w4(16384, 3072, 100, G.KC, G.KC, G.EPI_BF16) is None  # K % 64
-        G._USE_W4 = "0"
-        assert G.use_w4(16384, 3072, 768, G.KC, G.KC, G.EPI_BF16) is None
-    finally:
-        G._USE_W4 = old

@@ -290,14 +290,10 @@ def test_bn_apply_dual(Cc):
     assert (bits != ref).float().mean().item() < 1e-3
 
 
-@pytest.mark.parametrize("rows", ["2", "4", "4nt"])
 @pytest.mark.parametrize("M,Cc", [(300007, 64), (100003, 512), (4099, 2048)])
-def test_bn_sweeps_grid_stride(monkeypatch, M, Cc, rows):
+def test_bn_sweeps_grid_stride(monkeypatch, M, Cc):
     """bn_apply (residual + bit mask) and bn_bwd_dx (modes 2 and 3, residual-gradient output) on row
-    counts where the capped grid walks several R-row groups per lane with a ragged last group, vs
-    fp32 torch on the same bf16 inputs; every sweep form (DDL_BN_ROWS: rows in flight per lane, DDL_BN_NT: nontemporal stores)."""
-    monkeypatch.setenv("DDL_BN_ROWS", rows[0])
-    monkeypatch.setenv("DDL_BN_NT", "1" if rows.endswith("nt") else "0")
+    counts with a ragged last 2-row group per lane, vs fp32 torch on the same bf16 inputs."""
     x = rnd(M, Cc, seed=23)
     r = rnd(M, Cc, seed=24)
     dy = rnd(M, Cc, seed=25)
@@ -548,6 +544,7 @@ def test_fused_bottleneck_matches_composed_ops():
     where it is well conditioned."""
     import os
 
+    from distributeddeeplearningspark_amd.models import resnet as RN
     from distributeddeeplearningspark_amd.models.resnet import ResNet
 
     torch.manual_seed(1)
@@ -555,7 +552,8 @@ def test_fused_bottleneck_matches_composed_ops():
     y = torch.randint(0, 10, (16,))
     res = {}
     for fused, dev in (("1", DEV), ("0", DEV), ("0", "cpu")):
-        os.environ["DDL_FUSED_BLOCKS"] = fused
+        old = RN.FUSED_BLOCKS
+        RN.FUSED_BLOCKS = fused == "1"
         try:
             m = ResNet(blocks=(2,), input_shape=(32, 32, 3), num_classes=10)
             m.compile("sgd", "sparse_categorical_crossentropy")
@@ -563,7 +561,7 @@ def test_fused_bottleneck_matches_composed_ops():
             loss = m.backward_step(m.to_input(x), m.to_target(y))
             res[fused + dev] = (float(loss.detach()), m.arena.grad.float().cpu().clone())
         finally:
-            os.environ.pop("DDL_FUSED_BLOCKS", None)
+            RN.FUSED_BLOCKS = old
     l1, l0, lc = res["1" + DEV][0], res["0" + DEV][0], res["0cpu"][0]
     assert abs(l1 - l0) < 1e-2 * max(1.0, abs(l0)), (l1, l0)
     # the fused node applies the downsample BN inside the block-output sweep (the shortcut is never
@@ -667,9 +665,11 @@ def test_conv3x3_halo_kernel(N, H, W, Ci, Co, bias_relu, monkeypatch):
     from distributeddeeplearningspark_amd.ops import conv as CV
     from distributeddeeplearningspark_amd.ops import gemm as G
 
-    monkeypatch.setenv("DDL_CONV3X3_C64", "1")  # also the 64 -> 64 channel case (off by default)
     g = CV.geometry(N, H, W, Ci, Co, 3, 3, (1, 1), (1, 1), (1, 1))
-    assert CV.halo3_ok(g)
+    if Ci == 64 and Co == 64:  # one 64-channel chunk: conv.halo3_ok routes it to the implicit GEMM
+        assert not CV.halo3_ok(g)
+    else:
+        assert CV.halo3_ok(g)
     x = rnd(N, H, W, Ci, seed=1)
     w = rnd(Co, 3, 3, Ci, scale=0.05, seed=2)
     b = torch.randn(Co, device=DEV) * 0.1 if bias_relu else None
@@ -831,35 +831,6 @@ def test_bottleneck_inner_fused_bn_reduce_matches_unfused(monkeypatch):
     # blocks, tests/noise.py) — two reference runs under-sample it, hence the 1e-3 relative floor
     assert_scalar_within_noise(l1, l0, l0b, floor=1e-3)
     assert_within_noise(g1, g0, g0b, floor=2e-3, what="arena gradients")
-
-
-@pytest.mark.parametrize("N,H,C,Co", [(64, 56, 128, 128), (64, 28, 256, 256), (32, 14, 512, 512)])
-def test_strided_conv_dgrad_fused_bn_backward_reduce(monkeypatch, N, H, C, Co):
-    """3x3 / stride-2 data-gradient (four parity classes scattered through the OutMap) with a mode-2 ``bnr``:
-    every class's EPI_BF16_BNR epilogue adds the partial sums of the pixels it writes — the same dx as
-    without, and the reduce of the whole dx (ResNet-50's stride-2 conv2 feeding bn1)."""
-    from distributeddeeplearningspark_amd.ops import conv as CV
-    from distributeddeeplearningspark_amd.ops.norm import SHARDS
-
-    monkeypatch.setattr(CV, "_STRIDED_BNR", True)  # opt-in path (DDL_STRIDED_BNR=1)
-    g = CV.geometry(N, H, H, C, Co, 3, 3, (2, 2), (1, 1), (1, 1))
-    gen = torch.Generator().manual_seed(H * C + 1)
-    dy = torch.randn(N, g.Ho, g.Wo, Co, generator=gen).to(DEV, torch.bfloat16)
-    w = (torch.randn(Co, 3, 3, C, generator=gen) * 0.05).to(DEV, torch.bfloat16)
-    x = torch.randn(N, H, H, C, generator=gen).to(DEV, torch.bfloat16)
-    mean = torch.randn(C, generator=gen).to(DEV) * 0.1
-    scale = (torch.rand(C, generator=gen) + 0.5).to(DEV)
-    shift = torch.randn(C, generator=gen).to(DEV) * 0.5
-    ws = torch.zeros((SHARDS, 2, C), dtype=torch.float32, device=DEV)
-    bnr = {"x": x, "scale": scale, "shift": shift, "mean": mean, "ws": ws}
-    dx = CV.conv_dgrad_native(dy, w, g, bnr=bnr)
-    assert bnr.get("done")
-    assert torch.equal(dx, CV.conv_dgrad_native(dy, w, g))
-    keep = (x.float() * scale + shift > 0).cpu().reshape(-1, C)
-    s1, s2 = _bnr_reference(dx, x, mean, keep)
-    got = ws.double().cpu().sum(0)
-    close(got[0], s1, rtol=1e-4, atol=1e-2 * s1.abs().mean().item(), what="sum d")
-    close(got[1], s2, rtol=1e-4, atol=1e-2 * s2.abs().mean().item(), what="sum d (x - mean)")
 
 
 @pytest.mark.parametrize("M,N,K,rsub", [(12544, 512, 2048, False), (8192, 256, 1024, True)])
@@ -1054,7 +1025,9 @@ def test_stem_pool_fusion_matches_separate_apply_and_pool(monkeypatch):
     y = torch.randint(0, 10, (8,))
     out = {}
     for fused in ("1", "0"):
-        monkeypatch.setenv("DDL_STEM_POOL", fused)
+        from distributeddeeplearningspark_amd.ops import fused_blocks as FB
+
+        monkeypatch.setattr(FB, "_STEM_POOL", fused == "1")
         m = ResNet(blocks=(1,), input_shape=(64, 64, 3), num_classes=10)
         m.compile("sgd", "sparse_categorical_crossentropy")
         m.place(DEV, seed=4)
@@ -1085,144 +1058,6 @@ def test_dgrad_stride2_subgrid_residual(N, H, W, K, C):
     ref = G.linear_dgrad(dy, w, resid=full.view(M, C))
     close(out, ref, rtol=1e-2, atol=1e-2, what="stride-2 residual")
     assert torch.equal(out.view(N, H, W, C)[:, 1::2], ref.view(N, H, W, C)[:, 1::2])
-
-
-@pytest.mark.parametrize("M,K,N", [(16384, 64, 256), (20480, 128, 512), (16384, 256, 1024)])
-def test_normalise_on_load_fwd_and_wgrad(M, K, N):
-    """A pre-BatchNorm input normalised on load — relu(x * scale + shift) per channel — in the forward
-    1x1 GEMM (streaming kernel, A tile transformed in LDS) and in the weight gradient (RC x RC, B fragment
-    transformed): both equal the same GEMMs on the materialised bf16 activation (the transform rounds to
-    bf16 exactly as the BN-apply sweep does, so the operands are bit-identical)."""
-    from distributeddeeplearningspark_amd.ops import gemm as G
-    from distributeddeeplearningspark_amd.ops._native import C as _C
-
-    x = rnd(M, K, seed=41)
-    w = rnd(N, K, seed=42, scale=K ** -0.5)
-    sc = (torch.rand(K, generator=torch.Generator().manual_seed(43)) + 0.5).to(DEV)
-    sh = (torch.randn(K, generator=torch.Generator().manual_seed(44)) * 0.5).to(DEV)
-    xa = torch.empty_like(x)
-    _C().bn_apply(x, sc, sh, None, xa, K, True, None, None, None)
-    assert G.norm_on_load_fwd_ok(M, N, K, K, N)
-    y = G.linear_fwd(x, w, x_norm=(sc, sh))
-    y_ref = G.linear_fwd(xa, w)
-    close(y, y_ref, rtol=1e-2, atol=1e-2, what="fwd normalise-on-load")
-    dy = rnd(M, N, seed=45)
-    gw = torch.zeros(N, K, device=DEV)
-    gw_ref = torch.zeros(N, K, device=DEV)
-    G.linear_wgrad(dy, x, gw, x_norm=(sc, sh))
-    G.linear_wgrad(dy, xa, gw_ref)
-    close(gw, gw_ref, rtol=1e-3, atol=1e-3, what="wgrad normalise-on-load")
-
-
-def test_bottleneck_norm_on_load_matches_applied(monkeypatch):
-    """Stage-1 bottlenecks (M = 64 x 16 x 16 rows): conv3 reading bn2's pre-BN tensor with the apply
-    folded into its loads gives the same loss and gradients as the applied path, up to the applied
-    path's own run-to-run spread (tests/noise.py; the fused path also skips one bf16 rounding)."""
-    from noise import assert_scalar_within_noise, assert_within_noise
-
-    from distributeddeeplearningspark_amd.models.resnet import ResNet
-    from distributeddeeplearningspark_amd.ops import fused_blocks as FB
-
-    torch.manual_seed(6)
-    x = torch.randn(64, 64, 64, 3)
-    y = torch.randint(0, 10, (64,))
-    out = []
-    for on in (False, True, False):
-        monkeypatch.setattr(FB, "_NORM_ON_LOAD", on)
-        m = ResNet(blocks=(2,), input_shape=(64, 64, 3), num_classes=10)
-        m.compile("sgd", "sparse_categorical_crossentropy")
-        m.place(DEV, seed=8)
-        xd, yd = m.to_input(x), m.to_target(y)
-        from torch.profiler import ProfilerActivity, profile
-
-        torch.cuda.synchronize()
-        with profile(activities=[ProfilerActivity.CUDA]) as prof:
-            loss = m.backward_step(xd, yd)
-            torch.cuda.synchronize()
-        n_apply = sum(1 for e in prof.events() if "bn_apply" in e.name)
-        out.append((float(loss.detach()), m.arena.grad.float().cpu().clone(), n_apply))
-    (l0, g0, a0), (l1, g1, a1), (l0b, g0b, _) = out
-    assert a1 == a0 - 2, (a1, a0)  # both blocks' bn2 apply sweeps are gone
-    assert_scalar_within_noise(l1, l0, l0b, floor=1e-4)
-    assert_within_noise(g1, g0, g0b, floor=3e-3, what="arena gradients")
-
-@pytest.mark.parametrize("N,H,W,Ci,Co", [(2, 56, 56, 64, 64), (3, 28, 28, 128, 64), (2, 14, 14, 64, 128),
-                                         (9, 7, 7, 128, 128), (1, 14, 14, 256, 192),
-                                         (7, 8, 8, 128, 64), (13, 4, 4, 64, 128), (30, 2, 2, 128, 64),
-                                         (2, 32, 32, 64, 64), (3, 16, 16, 64, 128)])
-@pytest.mark.parametrize("slab,pp", [(False, False), (True, False), (True, True), (False, True)])
-def test_conv3x3_wgrad_halo_kernel(N, H, W, Ci, Co, slab, pp, monkeypatch):
-    """3x3 stride-1 weight-gradient halo kernel (csrc/kernels/conv3x3.hip) vs the fp32 PyTorch weight
-    gradient of the same bf16 operands: every ResNet-50 row tiling (56/28/14/7 wide), the VGG-16 CIFAR
-    whole-image tilings (8x8 / 4x4 / 2x2: 3 / 10 / 24 images per tile) and 128-pixel row tilings (32x32 / 16x16), a partial last group of images
-    (N = 9 at 7x7, N = 7 / 13 / 30 at the VGG sizes), several 64-channel tiles each way, atomics and partial slabs, and
-    accumulation into a non-zero gradient; the two-workgroups-per-CU form and the 512-thread ping-pong form
-    (two halves accumulating the same block, merged through LDS)."""
-    from distributeddeeplearningspark_amd.ops import conv as CV
-
-    monkeypatch.setattr(CV, "_WG3_SLAB", slab)
-    monkeypatch.setattr(CV, "_WG3_PP", pp)
-    g = CV.geometry(N, H, W, Ci, Co, 3, 3, (1, 1), (1, 1), (1, 1))
-    plan = CV.wgrad3_plan(g)
-    assert plan is not None
-    x = rnd(N, H, W, Ci, seed=3)
-    dy = rnd(N, H, W, Co, scale=0.5, seed=4)
-    gw0 = torch.randn(Co, 3, 3, Ci, device=DEV)
-    gw = gw0.clone()
-    CV.conv_wgrad_native(dy, x, g, gw)
-    ref = torch.nn.grad.conv2d_weight(x.float().cpu().permute(0, 3, 1, 2), (Co, Ci, 3, 3),
-                                      dy.float().cpu().permute(0, 3, 1, 2), stride=1, padding=1)
-    ref = ref.permute(0, 2, 3, 1) + gw0.cpu()
-    close(gw, ref, rtol=1e-3, atol=1e-2, what=f"wgrad3 halo slab={slab} pp={pp}")
-    # the gathered implicit GEMM agrees on the same problem
-    monkeypatch.setattr(CV, "_WG3", False)
-    gw2 = gw0.clone()
-    CV.conv_wgrad_native(dy, x, g, gw2)
-    close(gw, gw2, rtol=1e-3, atol=1e-2, what="wgrad3 halo vs gathered GEMM")
-
-
-@pytest.mark.parametrize("N,H", [(40, 56), (3, 56), (160, 32)])
-def test_conv3x3_c64_resident_filter_kernel(N, H, monkeypatch):
-    """64 -> 64 channel 3x3 stride-1 convolution on the resident-filter ping-pong kernel (conv3x3.hip,
-    conv3x3_c64_pp_kernel) vs fp32 PyTorch: the forward with bias + ReLU + fused BN statistics, and the
-    data-gradient (run as a forward conv through the flipped filter) with the fused mode-2 BN-backward
-    reduce.  N = 40 at 56x56 gives 3 pixel tiles per workgroup (both halves of the ping-pong), N = 3 one."""
-    from distributeddeeplearningspark_amd.ops import conv as CV
-    from distributeddeeplearningspark_amd.ops.norm import SHARDS
-
-    monkeypatch.setattr(CV, "_C64PP", True)
-    C = 64
-    g = CV.geometry(N, H, H, C, C, 3, 3, (1, 1), (1, 1), (1, 1))
-    assert CV.halo3_ok(g)
-    x = rnd(N, H, H, C, seed=5)
-    w = rnd(C, 3, 3, C, scale=0.05, seed=6)
-    b = torch.randn(C, device=DEV) * 0.1
-    st = torch.zeros((32, 2, C), dtype=torch.float32, device=DEV)
-    y = CV.conv_fwd_native(x, w, g, bias=b, relu=True, stats=st)
-    ref = CV.conv_ref(x.float(), w.float(), b, (1, 1), (1, 1), (1, 1), relu=True)
-    close(y, ref, what="c64 conv")
-    yf = y.float().reshape(-1, C)
-    close(st.sum(0)[0], yf.sum(0), rtol=1e-3, atol=1e-1, what="c64 stats sum")
-    close(st.sum(0)[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-1, what="c64 stats sumsq")
-    # data-gradient with the fused BN-backward reduce (mode 2)
-    gen = torch.Generator().manual_seed(H)
-    dy = torch.randn(N, H, H, C, generator=gen).to(DEV, torch.bfloat16)
-    xb = torch.randn(N, H, H, C, generator=gen).to(DEV, torch.bfloat16)
-    mean = torch.randn(C, generator=gen).to(DEV) * 0.1
-    scale = (torch.rand(C, generator=gen) + 0.5).to(DEV)
-    shift = torch.randn(C, generator=gen).to(DEV) * 0.5
-    ws = torch.zeros((SHARDS, 2, C), dtype=torch.float32, device=DEV)
-    bnr = {"x": xb, "scale": scale, "shift": shift, "mean": mean, "ws": ws}
-    dx = CV.conv_dgrad_native(dy, w, g, bnr=bnr)
-    assert bnr.get("done")
-    dref = torch.nn.grad.conv2d_input((N, C, H, H), w.float().cpu().permute(0, 3, 1, 2),
-                                      dy.float().cpu().permute(0, 3, 1, 2), stride=1, padding=1).permute(0, 2, 3, 1)
-    close(dx, dref, what="c64 dgrad")
-    keep = (xb.float() * scale + shift > 0).cpu().reshape(-1, C)
-    s1, s2 = _bnr_reference(dx, xb, mean, keep)
-    got = ws.double().cpu().sum(0)
-    close(got[0], s1, rtol=1e-4, atol=1e-2 * s1.abs().mean().item(), what="c64 sum d")
-    close(got[1], s2, rtol=1e-4, atol=1e-2 * s2.abs().mean().item(), what="c64 sum d (x - mean)")
 
 
 @pytest.mark.parametrize("M,N,K", [(768, 2304, 16384), (256, 64, 200704), (104, 72, 5000)])

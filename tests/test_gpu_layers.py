@@ -296,7 +296,9 @@ def test_sequential_fused_convbn_matches_two_node_path(monkeypatch):
     x, y = torch.randn(8, 16, 16, 3, generator=g), torch.randint(0, 10, (8,), generator=g)
     res = {}
     for fuse in ("1", "0"):
-        monkeypatch.setenv("DDL_FUSE_CONVBN", fuse)
+        from distributeddeeplearningspark_amd.models import core as _core
+
+        monkeypatch.setattr(_core, "FUSE_CONVBN", fuse == "1")
         m = build()
         xd, yd = m.to_input(x), m.to_target(y)
         loss = float(m.backward_step(xd, yd))

@@ -1,7 +1,5 @@
 """Space-to-depth ResNet stem (7x7 s2 conv as a 4x4 s1 conv on a block-2 s2d input) vs the
 channel-padded implicit-GEMM stem: same forward and the same parameter gradients."""
-import os
-
 import pytest
 import torch
 
@@ -10,8 +8,10 @@ pytestmark = pytest.mark.gpu
 
 def _run(s2d):
     from distributeddeeplearningspark_amd.models.resnet import ResNet
+    from distributeddeeplearningspark_amd.ops import fused_blocks as FB
 
-    os.environ["DDL_STEM_S2D"] = "1" if s2d else "0"
+    old = FB._STEM_S2D
+    FB._STEM_S2D = s2d
     try:
         torch.manual_seed(0)
         x = torch.randn(8, 96, 96, 3)
@@ -23,7 +23,7 @@ def _run(s2d):
         stem = m.stem.conv.kernel.grad.detach().clone()
         return loss, stem, m.arena.grad.detach().clone()
     finally:
-        os.environ.pop("DDL_STEM_S2D", None)
+        FB._STEM_S2D = old
 
 
 def test_stem_s2d_matches_padded_path():

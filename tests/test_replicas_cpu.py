@@ -48,7 +48,8 @@ def test_replica_group_matches_process_workers(spark, monkeypatch, algo, groups)
     tr_p, w_p = _train(spark, monkeypatch, algo, "0")
     tr_g, w_g = _train(spark, monkeypatch, algo, groups)
     ng = int(groups)
-    assert tr_g._results[0].get("replica_group") == {"group": 0, "groups": ng, "replicas": 3 if ng == 1 else 2}
+    assert tr_g._results[0].get("replica_group") == {"group": 0, "groups": ng, "replicas": 3 if ng == 1 else 2,
+                                                     "batched": False}
     assert "replica_group" not in tr_p._results[0]
     assert tr_g.parameter_server.num_updates == tr_p.parameter_server.num_updates
     if algo != "AveragingTrainer":
