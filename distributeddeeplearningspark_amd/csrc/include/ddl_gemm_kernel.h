@@ -471,10 +471,10 @@ __device__ __forceinline__ void gemm_epilogue_bnr(const GemmParams& p, f32x4 (&a
       resoff[i] = rrow < 0 ? -1L : rrow * p.ldr;
     }
   }
-  // fragment pairs whose 32 columns are in range (wave-uniform) go through 16-B loads / stores
-  const bool wide = (p.ldc % 8) == 0 && (!p.resid || (p.ldr % 8) == 0) &&
-                    ((reinterpret_cast<uintptr_t>(p.c) | reinterpret_cast<uintptr_t>(p.bnr_x) |
-                      reinterpret_cast<uintptr_t>(p.resid)) & 15) == 0;
+  // Fragment pairs whose 32 columns are in range could go through 16-B loads / stores (pair_load /
+  // pair_store), but the extra live registers spill in the 128-VGPR 128x128 kernel (0 -> 92 B scratch,
+  // ResNet-50 BNR GEMMs 7.80 -> 8.65 ms per 5 steps, profiles/r5/ab_epilogue_kernels.txt): off.
+  constexpr bool wide = false;
 #pragma unroll
   for (int jp = 0; jp < RN; jp += 2) {
     if (wide && jp + 1 < RN && nb + 16 * jp + 32 <= p.N) {  // wave-uniform
@@ -599,7 +599,9 @@ __device__ __forceinline__ void gemm_epilogue_bnr(const GemmParams& p, f32x4 (&a
   col_stats_atomics<RN>(s1, s2, st, p.N, nb, lane);
 }
 
-template <int RM, int RN, int EPI>
+// WIDE: the LITE epilogue's paired 16-B stores (off for the gathered-A LDS-DMA kernels: their address state
+// leaves no registers for the pair, 0 -> 24 B scratch and +0.03 ms/step on ResNet-50)
+template <int RM, int RN, int EPI, bool WIDE = true>
 __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[RM][RN], const int mb, const int nb,
                                               const int lane, const int bid, int mend = -1, long coff = 0) {
   const int mlim = mend < 0 ? p.M : mend;
@@ -645,7 +647,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
   // bf16 outputs: fragment pairs (j, j + 1) whose 32 columns are all in range leave as ONE 16-B store per
   // lane (8 consecutive columns) after a v_permlane16_swap: the epilogue's store tail is bound by store
   // INSTRUCTIONS issued (the same bytes in half the instructions)
-  const bool wide_ok = BF && (p.ldc % 8) == 0 && (reinterpret_cast<uintptr_t>(p.c) & 15) == 0;
+  // (the full epilogue keeps 8-B stores: its GELU / residual / dropout values leave no registers for the pair
+  // in the 128-VGPR 128x128 kernel — 8 -> 36 B scratch, BERT-base -1.2 % — profiles/r5/ab_epilogue_kernels.txt)
+  const bool wide_ok = WIDE && LITE && (p.ldc % 8) == 0 && (reinterpret_cast<uintptr_t>(p.c) & 15) == 0;
   // bias of this lane's columns, loaded once: inside the row loop the compiler must re-load it
   // after every output store (p.bias may alias p.c), 4 * RM * RN dependent loads per lane
   // (one 16-B load per fragment column group where the 4 columns are in range: n % 4 == 0 and the
@@ -940,7 +944,8 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
       }
       slot = slot + 1 == ST ? 0 : slot + 1;
     }
-    gemm_epilogue<RM, RN, EPI>(p, acc, m0 + wm0, n0 + wn0, lane, bid, -1, (long)split * p.split_stride);
+    gemm_epilogue<RM, RN, EPI, (AMODE == OP_KC || AMODE == OP_RC)>(p, acc, m0 + wm0, n0 + wn0, lane, bid, -1,
+                                                                  (long)split * p.split_stride);
     return;
   }
   if (nk > 0) {
@@ -977,7 +982,8 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
     }
   }
 
-  gemm_epilogue<RM, RN, EPI>(p, acc, m0 + wm0, n0 + wn0, lane, bid, -1, (long)split * p.split_stride);
+  gemm_epilogue<RM, RN, EPI, (AMODE == OP_KC || AMODE == OP_RC)>(p, acc, m0 + wm0, n0 + wn0, lane, bid, -1,
+                                                                  (long)split * p.split_stride);
 }
 
 inline int device_cus() {

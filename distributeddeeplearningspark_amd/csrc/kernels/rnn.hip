@@ -771,14 +771,16 @@ __global__ __launch_bounds__(256) void dense_mse_rep_kernel(const float* __restr
   }
 }
 
-// Recurrent parameter gradients of replica blockIdx.z over ALL its B T rows (chunks of PG_BT staged in
-// LDS), written with plain stores: rows m < H gU, H <= m < H + I gW, m = H + I gb (as rnn_param_grad).
+// Recurrent parameter gradients: rows m < H gU, H <= m < H + I gW, m = H + I gb (as rnn_param_grad).
+// blockIdx.z = replica * S + slice: a workgroup sums PG_BT-row chunks [slice, slice + S, ...) of its
+// replica's B T rows.  S = 1 (deterministic mode): one writer per output, plain stores in row order;
+// S > 1: fp32 atomics into gradients the optimizer sweep of the previous step left zeroed.
 template <int CELL>
 __global__ __launch_bounds__(256) void rnn_param_grad_rep_kernel(const float* __restrict__ dg, const float* __restrict__ hs,
                                                                  const float* __restrict__ gates, const RnnRep rp,
-                                                                 int T, int H, int I) {
+                                                                 int T, int H, int I, int S) {
   constexpr int G = CELL == 0 ? 3 : (CELL == 1 ? 4 : 1);
-  const int GH = G * H, r = blockIdx.z, B = rp.B;
+  const int GH = G * H, r = blockIdx.z / S, slice = blockIdx.z - r * S, B = rp.B;
   const bool has_b = rp.gb[r] != nullptr;
   const int M = H + I + (has_b ? 1 : 0);
   const long BT = (long)B * T, row0 = (long)r * B;  // global batch row of the replica's row 0
@@ -791,7 +793,7 @@ __global__ __launch_bounds__(256) void rnn_param_grad_rep_kernel(const float* __
   const int c = threadIdx.x & 63, q0 = threadIdx.x >> 6;
   const int tm = (threadIdx.x / 16) * 4, tj = (threadIdx.x % 16) * 4;
   float acc[4][4] = {};
-  for (long bt0 = 0; bt0 < BT; bt0 += PG_BT) {
+  for (long bt0 = (long)slice * PG_BT; bt0 < BT; bt0 += (long)S * PG_BT) {
     const int nbt = (int)min((long)PG_BT, BT - bt0);
     long b = (bt0 + q0) / T, t = (bt0 + q0) - b * T;
     for (int q = q0; q < nbt; q += 4, t += 4) {
@@ -831,20 +833,24 @@ __global__ __launch_bounds__(256) void rnn_param_grad_rep_kernel(const float* __
 #pragma unroll
     for (int l = 0; l < 4; ++l) {
       const int jj = j0 + tj + l;
-      if (jj < GH) dst[jj] = acc[i][l];
+      if (jj < GH) {
+        if (S == 1) dst[jj] = acc[i][l];
+        else atomicAdd(dst + jj, acc[i][l]);
+      }
     }
   }
 }
 
 // Optimizer sweep over the R replica arenas (blockIdx.y = replica), Keras semantics as the per-replica
 // kernels (optim.hip): OPT 0 SGD (+momentum p1), 1 Adagrad, 2 Adam (b1 = p1, b2 = p2, amode as adam_step).
-// Block (0, 0) advances the shared step counter (no block of this kernel reads it).
+// zero_g: leave the gradients zeroed for the next step's atomic parameter-gradient slices.  Block (0, 0)
+// advances the shared step counter (no block of this kernel reads it).
 template <int OPT>
 __global__ __launch_bounds__(256) void opt_rep_kernel(const OptRep op, long n4, float lr, float p1, float p2, float eps,
-                                                      float wd, int amode, int* ctr) {
+                                                      float wd, int amode, int* ctr, int zero_g) {
   const int r = blockIdx.y;
   float4* w = reinterpret_cast<float4*>(op.w[r]);
-  const float4* g = reinterpret_cast<const float4*>(op.g[r]);
+  float4* g = const_cast<float4*>(reinterpret_cast<const float4*>(op.g[r]));
   float4* s1 = reinterpret_cast<float4*>(op.s1[r]);
   float4* s2 = reinterpret_cast<float4*>(op.s2[r]);
   float bc1 = 1.f, bc2 = 1.f;
@@ -885,6 +891,7 @@ __global__ __launch_bounds__(256) void opt_rep_kernel(const OptRep op, long n4, 
     w[i] = p;
     if (s1) s1[i] = a;
     if constexpr (OPT == 2) s2[i] = v;
+    if (zero_g) g[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *ctr += 1;
 }
@@ -904,16 +911,19 @@ int rep_step(const RnnRep& rp, int R, int T, int I, float* hs, float* cs, float*
   hipLaunchKernelGGL((rnn_bwd_reg_kernel<CELL, H, BBB, true>), dim3((RB + BBB - 1) / BBB), dim3(bwd_threads<CELL, H>()),
                      0, s, dh, (const float*)nullptr, hs, cs, gates, dgates, RB, T, 0, rp);
   const int M = H + I + 1;
-  hipLaunchKernelGGL((rnn_param_grad_rep_kernel<CELL>), dim3((M + 63) / 64, (G * H + 63) / 64, R), dim3(256), 0, s,
-                     dgates, hs, gates, rp, T, H, I);
+  // row slices of the parameter gradients (atomics); deterministic mode: one ordered writer per output
+  const int S = deterministic() ? 1 : (int)std::max<long>(1, ((long)rp.B * T + PG_BT - 1) / PG_BT);
+  hipLaunchKernelGGL((rnn_param_grad_rep_kernel<CELL>), dim3((M + 63) / 64, (G * H + 63) / 64, R * S), dim3(256), 0,
+                     s, dgates, hs, gates, rp, T, H, I, S);
   const long n4 = n / 4;
   const dim3 og((unsigned)std::min<long>((n4 + 255) / 256, 1024), R);
+  const int zg = S > 1;
   if (opt == 0)
-    hipLaunchKernelGGL(opt_rep_kernel<0>, og, dim3(256), 0, s, op, n4, lr, p1, p2, eps, wd, amode, rp.ctr);
+    hipLaunchKernelGGL(opt_rep_kernel<0>, og, dim3(256), 0, s, op, n4, lr, p1, p2, eps, wd, amode, rp.ctr, zg);
   else if (opt == 1)
-    hipLaunchKernelGGL(opt_rep_kernel<1>, og, dim3(256), 0, s, op, n4, lr, p1, p2, eps, wd, amode, rp.ctr);
+    hipLaunchKernelGGL(opt_rep_kernel<1>, og, dim3(256), 0, s, op, n4, lr, p1, p2, eps, wd, amode, rp.ctr, zg);
   else
-    hipLaunchKernelGGL(opt_rep_kernel<2>, og, dim3(256), 0, s, op, n4, lr, p1, p2, eps, wd, amode, rp.ctr);
+    hipLaunchKernelGGL(opt_rep_kernel<2>, og, dim3(256), 0, s, op, n4, lr, p1, p2, eps, wd, amode, rp.ctr, zg);
   return (int)hipGetLastError();
 }
 

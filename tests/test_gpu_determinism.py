@@ -139,7 +139,7 @@ def test_resnet50_full_depth_gradient_direction_per_stage():
     assert cos["head"] > 0.9, cos
 
 
-def _resnet50_conditioned(dev, noise=0.0, gamma3=0.2, mutation=None):
+def _resnet50_conditioned(dev, noise=0.0, gamma3=0.1, mutation=None):
     """One deterministic full-depth ResNet-50 step at a WELL-CONDITIONED point: every bottleneck's last
     BN scale (gamma3) set to ``gamma3`` so each residual branch is a small perturbation of its shortcut
     (the zero-init-residual idea without zeroing the branch gradients).  Returns (model, loss, grads)."""
@@ -185,10 +185,12 @@ def _stage_cosines(m, ga, gb):
 
 
 def test_resnet50_gradient_per_stage_well_conditioned():
-    """SURVEY §7.6 oracle at a point where it can discriminate: with gamma3 = 0.2 the
-    fp32 CPU gradient is stable under a 2^-7 input perturbation (asserted: >= 0.95 per stage), and the
-    deterministic HIP gradient must match it per stage to >= 0.95 cosine.  The mutation test below shows
-    the same assertion failing when one block's shortcut gradient is dropped."""
+    """SURVEY §7.6 oracle at a point where it can discriminate: with gamma3 = 0.1 the
+    fp32 CPU gradient is stable under a 2^-7 input perturbation (asserted: >= 0.95 per stage; measured
+    0.957 / 0.963 / 0.968 / 0.974 / 0.990 / 0.9998 stem..head, profiles/r5/gradient_oracle.txt), and the
+    deterministic HIP gradient must match it per stage to >= 0.95 cosine (measured 0.969 / 0.972 / 0.974 /
+    0.979 / 0.992 / 0.9999: closer to fp32 than fp32 is to itself under the perturbation).  The mutation
+    test below shows the same assertion failing when one block's shortcut gradient is dropped."""
     m, lc, gc = _resnet50_conditioned("cpu")
     _, _, gp = _resnet50_conditioned("cpu", noise=2.0**-7)
     _, lg, gg = _resnet50_conditioned(DEV)
@@ -206,11 +208,12 @@ def test_resnet50_gradient_per_stage_well_conditioned():
 def test_resnet50_gradient_check_catches_dropped_shortcut_term():
     """Mutation test of the per-stage oracle: the HIP backward with ONE block's shortcut gradient dropped
     (fused_blocks._TEST_MUTATION, stage 3's last block) must fail the >= 0.95 per-stage assertion in every
-    stage below that block, while the stages above it (stage 4, head) still pass."""
+    stage at or below that block (measured 0.23 / 0.21 / 0.20 / 0.35 stem..stage3), while the stages above
+    it (stage 4, head) still pass."""
     m, _, gc = _resnet50_conditioned("cpu")
     _, _, gbad = _resnet50_conditioned(DEV, mutation=("drop_shortcut", "resnet50/s3b6"))
     cos = _stage_cosines(m, gc, gbad)
     print("per-stage cosine with stage 3 block 6's shortcut gradient dropped:", {k: round(v, 4) for k, v in cos.items()})
-    for k in ("stem", "stage1", "stage2"):
+    for k in ("stem", "stage1", "stage2", "stage3"):
         assert cos[k] < 0.95, (k, cos[k])
     assert cos["stage4"] >= 0.95 and cos["head"] >= 0.95, cos
