@@ -71,7 +71,8 @@ int avgpool_global_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream
 // loss_rows[b] = CE; dlogits = (softmax - target) * grad_scale  (same dtype as logits)
 int softmax_xent(const void* logits, int logits_bf16, const int64_t* labels, const float* target_probs,
                  float* loss_rows, void* dlogits, int B, int K, long ld, float grad_scale, float label_smoothing,
-                 int ignore_index, hipStream_t s, const float* grad_scale_dev = nullptr);
+                 int ignore_index, hipStream_t s, const float* grad_scale_dev = nullptr, float* loss_out = nullptr,
+                 float out_scale = 1.f);
 int label_count_inv(const int64_t* labels, long n, int ignore_index, float* inv, hipStream_t s);
 int rows_sum_scaled(const float* rows, long n, float scale, const float* dev, float* out, hipStream_t s);
 int scale_bf16_dev(void* x, long n, const float* s_dev, hipStream_t s);
@@ -89,7 +90,10 @@ int relu_bwd(const void* dy, const void* y, void* dx, long n, hipStream_t s);
 int add_bf16(const void* a, const void* b, void* y, long n, hipStream_t s);
 // db[n] (+)= sum_m dy[m][n]; deterministic mode: det_ws (bias_grad_rows(M) x N floats) holds per-workgroup
 // partial rows summed in order by colsum_partials (without it: one workgroup per column block)
-int bias_grad(const void* dy, float* db, long M, int N, int accumulate, hipStream_t s, float* det_ws = nullptr);
+int bias_grad(const void* dy, float* db, long M, int N, int accumulate, hipStream_t s, float* det_ws = nullptr,
+              const void* relu_y = nullptr, void* relu_dx = nullptr);
+// zero-padded [R][Kp] copy of a row-strided [R][K] bf16 view
+int pad_cols_bf16(const void* x, long ldx, void* out, long R, int K, int Kp, hipStream_t s);
 int bias_grad_rows(long M);
 // c = beta * c + sum over split-K partial slabs ws[splits][M][N] (split order, one writer per element)
 int slab_reduce(const float* ws, int splits, float* c, long M, int N, long ldc, float beta, hipStream_t s);
@@ -108,8 +112,8 @@ int normalize_u8(const uint8_t* x, void* y, long npix, int c, int cpad, const fl
 int sgd_step(float* w, const float* g, float* mom, void* w16, long n, float lr, float momentum, float dampening,
              float wd, int nesterov, float gscale, hipStream_t s);
 int adam_step(float* w, const float* g, float* m, float* v, void* w16, long n, float lr, float b1, float b2,
-              float eps, float wd, int adamw, float bc1, float bc2, float gscale, const float* tstep,
-              hipStream_t s);
+              float eps, float wd, int adamw, float bc1, float bc2, float gscale, float* tstep,
+              hipStream_t s, unsigned* tick_ctr = nullptr);
 int step_tick(float* t, hipStream_t s);
 int adagrad_step(float* w, const float* g, float* acc, void* w16, long n, float lr, float eps, float wd, float gscale,
                  hipStream_t s);

@@ -27,16 +27,22 @@ __device__ __forceinline__ float ld_logit(const void* p, long i) {
   else return reinterpret_cast<const float*>(p)[i];
 }
 
+// Rows b = blockIdx.x, blockIdx.x + gridDim.x, ...: grid B for wide rows (one workgroup each), or ONE
+// workgroup for a small batch (the reference's MNIST head: 16 rows of 10 classes), which then also reduces
+// the batch loss itself: loss_out[0] = out_scale * (out_dev ? out_dev[0] : 1) * sum of the row losses (no
+// second launch for the mean).
 template <bool BF16>
 __global__ __launch_bounds__(256) void softmax_xent_kernel(const void* __restrict__ logits,
                                                             const int64_t* __restrict__ labels,
                                                             const float* __restrict__ tprob, float* loss_rows,
                                                             void* dlogits, int K, long ld, float gscale, float smooth,
-                                                            int ignore_index, const float* __restrict__ gscale_dev) {
-  const int b = blockIdx.x;
+                                                            int ignore_index, const float* __restrict__ gscale_dev,
+                                                            int B, float* __restrict__ loss_out, float out_scale) {
   if (gscale_dev) gscale *= gscale_dev[0];  // device-resident factor (e.g. 1 / #valid labels: no host sync)
-  const long base = (long)b * ld;  // row stride ld >= K (padded vocabularies); tprob rows are dense [B][K]
   __shared__ float sm[2][4];
+  float total = 0.f;
+  for (int b = blockIdx.x; b < B; b += gridDim.x) {
+  const long base = (long)b * ld;  // row stride ld >= K (padded vocabularies); tprob rows are dense [B][K]
   // vec: bf16 logits with 16-B aligned rows and class labels (the MLM decoder: 30,522-wide rows):
   // both passes read 8 logits per lane per 16-B load (2-B loads before) and the gradient row is
   // written as 16-B vectors; the last K % 8 columns take the scalar loop
@@ -126,19 +132,28 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const void* __restric
   __syncthreads();
   if (lane == 0) sm[0][wid] = lpart;
   __syncthreads();
-  if (threadIdx.x == 0) loss_rows[b] = sm[0][0] + sm[0][1] + sm[0][2] + sm[0][3];
+  const float row = sm[0][0] + sm[0][1] + sm[0][2] + sm[0][3];
+  if (threadIdx.x == 0) {
+    if (loss_rows) loss_rows[b] = row;
+    total += row;
+  }
+  __syncthreads();  // sm is rewritten by the next row
+  }
+  if (loss_out && threadIdx.x == 0) loss_out[0] = total * out_scale * (gscale_dev ? gscale_dev[0] : 1.f);
 }
 
 int softmax_xent(const void* logits, int logits_bf16, const int64_t* labels, const float* target_probs,
                  float* loss_rows, void* dlogits, int B, int K, long ld, float grad_scale, float label_smoothing,
-                 int ignore_index, hipStream_t s, const float* grad_scale_dev) {
+                 int ignore_index, hipStream_t s, const float* grad_scale_dev, float* loss_out, float out_scale) {
   if (B <= 0) return 0;
+  // loss_out: one workgroup walks every row and writes the reduced loss (small batches only)
+  const dim3 grid(loss_out ? 1 : B);
   if (logits_bf16)
-    hipLaunchKernelGGL(softmax_xent_kernel<true>, dim3(B), dim3(256), 0, s, logits, labels, target_probs, loss_rows,
-                       dlogits, K, ld, grad_scale, label_smoothing, ignore_index, grad_scale_dev);
+    hipLaunchKernelGGL(softmax_xent_kernel<true>, grid, dim3(256), 0, s, logits, labels, target_probs, loss_rows,
+                       dlogits, K, ld, grad_scale, label_smoothing, ignore_index, grad_scale_dev, B, loss_out, out_scale);
   else
-    hipLaunchKernelGGL(softmax_xent_kernel<false>, dim3(B), dim3(256), 0, s, logits, labels, target_probs, loss_rows,
-                       dlogits, K, ld, grad_scale, label_smoothing, ignore_index, grad_scale_dev);
+    hipLaunchKernelGGL(softmax_xent_kernel<false>, grid, dim3(256), 0, s, logits, labels, target_probs, loss_rows,
+                       dlogits, K, ld, grad_scale, label_smoothing, ignore_index, grad_scale_dev, B, loss_out, out_scale);
   return (int)hipGetLastError();
 }
 

@@ -118,6 +118,30 @@ int add_bf16(const void* a, const void* b, void* y, long n, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// out[r][k] = k < K ? x[r * ldx + k] : 0 for r < R, k < Kp: a zero-padded [R][Kp] copy of a row-strided
+// [R][K] view (the 16-B-vector width of the GEMM operands; params.py keeps weights padded, this pads
+// activations that arrive unpadded).  One lane per output pair of columns.
+__global__ __launch_bounds__(256) void pad_cols_bf16_kernel(const bf16_t* __restrict__ x, long ldx,
+                                                            bf16_t* __restrict__ out, long R, int K, int Kp) {
+  const int kh = Kp >> 1;
+  GRID_LOOP(i, R * kh) {
+    const long r = i / kh;
+    const int k = (int)(i - r * kh) * 2;
+    const bf16_t* xr = x + r * ldx;
+    const unsigned lo = k < K ? (unsigned)xr[k] : 0u;
+    const unsigned hi = k + 1 < K ? (unsigned)xr[k + 1] : 0u;
+    reinterpret_cast<unsigned*>(out)[i] = lo | (hi << 16);
+  }
+}
+
+int pad_cols_bf16(const void* x, long ldx, void* out, long R, int K, int Kp, hipStream_t s) {
+  if (Kp % 2 || K > Kp || ldx < K) return (int)hipErrorInvalidValue;
+  if (R <= 0) return 0;
+  hipLaunchKernelGGL(pad_cols_bf16_kernel, dim3(mgrid(R * (Kp / 2))), dim3(256), 0, s, (const bf16_t*)x, ldx,
+                     (bf16_t*)out, R, K, Kp);
+  return (int)hipGetLastError();
+}
+
 // db[n] += sum_m dy[m][n]; grid (col blocks, row splits) with one atomic per column per block
 __global__ void bias_grad_kernel(const bf16_t* dy, float* db, long M, int N) {
   const int n = blockIdx.x * 256 + threadIdx.x;
@@ -132,7 +156,11 @@ __global__ void bias_grad_kernel(const bf16_t* dy, float* db, long M, int N) {
 // atomic per column per block.  The scalar form above moved 2 bytes per lane per load.
 // pout != nullptr (deterministic mode): each workgroup stores its column totals to pout[blockIdx.y][n]
 // instead of adding them into db; colsum_partials then sums the rows in index order, one writer per column
-__global__ __launch_bounds__(256) void bias_grad_vec_kernel(const bf16_t* dy, float* db, long M, int N, float* pout) {
+// ry != nullptr: the ReLU backward is fused in: dy is masked by ry > 0, the masked rows are stored to rdx
+// and summed (a Dense / Conv2D with a fused ReLU: one sweep instead of relu_bwd + bias_grad)
+__global__ __launch_bounds__(256) void bias_grad_vec_kernel(const bf16_t* dy, float* db, long M, int N, float* pout,
+                                                            const bf16_t* __restrict__ ry = nullptr,
+                                                            bf16_t* __restrict__ rdx = nullptr) {
   __shared__ float part[8][257];
   const int cg = threadIdx.x & 31, rl = threadIdx.x >> 5;
   const int n0 = blockIdx.x * 256 + cg * 8;
@@ -141,7 +169,18 @@ __global__ __launch_bounds__(256) void bias_grad_vec_kernel(const bf16_t* dy, fl
   for (int k = 0; k < 8; ++k) acc[k] = 0.f;
   if (n0 < N) {
     for (long m = (long)blockIdx.y * 8 + rl; m < M; m += (long)gridDim.y * 8) {
-      const uint4 q = *reinterpret_cast<const uint4*>(dy + m * N + n0);
+      uint4 q = *reinterpret_cast<const uint4*>(dy + m * N + n0);
+      if (ry) {
+        const uint4 yv = *reinterpret_cast<const uint4*>(ry + m * N + n0);
+        // bf16 > 0: sign bit clear and any other bit set, per 16-bit half
+        auto msk = [](unsigned d, unsigned y) {
+          const unsigned lo = ((y & 0x8000u) == 0 && (y & 0x7fffu) != 0) ? 0xffffu : 0u;
+          const unsigned hi = ((y & 0x80000000u) == 0 && (y & 0x7fff0000u) != 0) ? 0xffff0000u : 0u;
+          return d & (lo | hi);
+        };
+        q = make_uint4(msk(q.x, yv.x), msk(q.y, yv.y), msk(q.z, yv.z), msk(q.w, yv.w));
+        *reinterpret_cast<uint4*>(rdx + m * N + n0) = q;
+      }
       const unsigned u[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -226,14 +265,19 @@ int bias_grad_rows(long M) {
   return (int)ys;
 }
 
-int bias_grad(const void* dy, float* db, long M, int N, int accumulate, hipStream_t s, float* det_ws) {
+int bias_grad(const void* dy, float* db, long M, int N, int accumulate, hipStream_t s, float* det_ws, const void* ry,
+              void* rdx) {
   if (!accumulate) hipMemsetAsync(db, 0, sizeof(float) * N, s);
   long ys = bias_grad_rows(M);
   const bool vec = N % 8 == 0 && (reinterpret_cast<uintptr_t>(dy) & 15) == 0;
+  if (ry && (!vec || (reinterpret_cast<uintptr_t>(ry) & 15) || (reinterpret_cast<uintptr_t>(rdx) & 15)))
+    return (int)hipErrorInvalidValue;  // the fused ReLU form is the vector kernel only
+  const bf16_t* ryb = reinterpret_cast<const bf16_t*>(ry);
+  bf16_t* rdxb = reinterpret_cast<bf16_t*>(rdx);
   if (deterministic()) {
     if (vec && det_ws) {  // per-workgroup partial rows, then an in-order column sum (one writer per column)
       hipLaunchKernelGGL(bias_grad_vec_kernel, dim3((N + 255) / 256, (unsigned)ys), dim3(256), 0, s,
-                         (const bf16_t*)dy, db, M, N, det_ws);
+                         (const bf16_t*)dy, db, M, N, det_ws, ryb, rdxb);
       const int e = (int)hipGetLastError();
       return e ? e : colsum_partials(det_ws, (int)ys, N, db, 1, s);
     }
@@ -241,7 +285,7 @@ int bias_grad(const void* dy, float* db, long M, int N, int accumulate, hipStrea
   }
   if (vec) {
     hipLaunchKernelGGL(bias_grad_vec_kernel, dim3((N + 255) / 256, (unsigned)ys), dim3(256), 0, s,
-                       (const bf16_t*)dy, db, M, N, (float*)nullptr);
+                       (const bf16_t*)dy, db, M, N, (float*)nullptr, ryb, rdxb);
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(bias_grad_kernel, dim3((N + 255) / 256, (unsigned)ys), dim3(256), 0, s, (const bf16_t*)dy, db, M,

@@ -61,14 +61,23 @@ int sgd_step(float* w, const float* g, float* mom, void* w16, long n, float lr, 
 // mode bit0: decoupled weight decay (AdamW); bit1: Keras epsilon placement
 //   PyTorch: w -= lr * (m/bc1) / (sqrt(v/bc2) + eps)
 //   Keras 2: w -= lr * sqrt(bc2)/bc1 * m / (sqrt(v) + eps)
+// bit2 (kAdamTick): this launch also advances the device step counter: every workgroup uses t + 1 and the
+//   last workgroup to finish (tick_ctr, an atomicInc that wraps back to 0) stores it — every other
+//   workgroup has read the counter by then, so no separate step_tick launch precedes the update.
+// bit3 (kAdamZeroGrad): the gradients are zeroed as they are consumed (the next step's zero_grad fill is
+//   skipped: models/optimizers.py captured_update(zero_grads=True)).
+constexpr int kAdamTick = 4, kAdamZeroGrad = 8;
 __global__ __launch_bounds__(256) void adam_kernel(float4* w, const float4* g, float4* m, float4* v, void* w16, long n,
                                                     float lr, float b1, float b2, float eps, float wd, int mode,
-                                                    float bc1, float bc2, float gs, const float* tstep) {
+                                                    float bc1, float bc2, float gs, float* tstep,
+                                                    unsigned* __restrict__ tick_ctr) {
+  float t = 0.f;
   if (tstep) {  // graph-replayed step: bias corrections from the device step counter
-    const float t = *tstep;
+    t = *tstep + ((mode & kAdamTick) ? 1.f : 0.f);
     bc1 = 1.f - powf(b1, t);
     bc2 = 1.f - powf(b2, t);
   }
+  const bool zg = mode & kAdamZeroGrad;
   const float sbc2 = sqrtf(bc2);
   auto upd = [&](float4& p, const float4& d, float4& mm, float4& vv) {
     float *pp = &p.x, *m_ = &mm.x, *v_ = &vv.x;
@@ -97,20 +106,30 @@ __global__ __launch_bounds__(256) void adam_kernel(float4* w, const float4* g, f
     w[i] = p0; m[i] = m0; v[i] = v0;
     w[j] = p1; m[j] = m1; v[j] = v1;
     if (w16) { store_bf16x4(w16, i, p0); store_bf16x4(w16, j, p1); }
+    if (zg) { const_cast<float4*>(g)[i] = make_float4(0, 0, 0, 0); const_cast<float4*>(g)[j] = make_float4(0, 0, 0, 0); }
   }
   if (i < n4) {
     float4 p0 = w[i], d0 = g[i], m0 = m[i], v0 = v[i];
     upd(p0, d0, m0, v0);
     w[i] = p0; m[i] = m0; v[i] = v0;
     if (w16) store_bf16x4(w16, i, p0);
+    if (zg) const_cast<float4*>(g)[i] = make_float4(0, 0, 0, 0);
+  }
+  if ((mode & kAdamTick) && tstep) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __threadfence();
+      if (atomicInc(tick_ctr, gridDim.x - 1) == gridDim.x - 1) *tstep = t;  // last workgroup: publish t
+    }
   }
 }
 
 int adam_step(float* w, const float* g, float* m, float* v, void* w16, long n, float lr, float b1, float b2, float eps,
-              float wd, int adamw, float bc1, float bc2, float gscale, const float* tstep, hipStream_t s) {
+              float wd, int adamw, float bc1, float bc2, float gscale, float* tstep, hipStream_t s, unsigned* tick_ctr) {
   if (n % 4) return (int)hipErrorInvalidValue;
+  if ((adamw & kAdamTick) && (!tstep || !tick_ctr)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(adam_kernel, dim3(ogrid(n / 4)), dim3(256), 0, s, (float4*)w, (const float4*)g, (float4*)m,
-                     (float4*)v, w16, n, lr, b1, b2, eps, wd, adamw, bc1, bc2, gscale, tstep);
+                     (float4*)v, w16, n, lr, b1, b2, eps, wd, adamw, bc1, bc2, gscale, tstep, tick_ctr);
   return (int)hipGetLastError();
 }
 

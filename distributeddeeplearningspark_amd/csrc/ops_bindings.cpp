@@ -237,16 +237,18 @@ void avgpool_bwd_(const at::Tensor& dy, const at::Tensor& dx) {
 
 // ---------------------------------------------------------------- loss
 void softmax_xent_(const at::Tensor& logits, c10::optional<at::Tensor> labels, c10::optional<at::Tensor> probs,
-                   const at::Tensor& loss_rows, c10::optional<at::Tensor> dlogits, double grad_scale, double smoothing,
-                   int64_t ignore_index, c10::optional<at::Tensor> grad_scale_dev) {
+                   c10::optional<at::Tensor> loss_rows, c10::optional<at::Tensor> dlogits, double grad_scale, double smoothing,
+                   int64_t ignore_index, c10::optional<at::Tensor> grad_scale_dev, c10::optional<at::Tensor> loss_out,
+                   double out_scale) {
   GPU(logits);
   CK(logits.dim() == 2 && logits.stride(1) == 1 && logits.stride(0) >= logits.size(1),
      "softmax_xent: logits [B,K] with unit column stride");
   const bool bf = logits.scalar_type() == at::kBFloat16;
   CK(bf || logits.scalar_type() == at::kFloat, "softmax_xent: logits bf16/fp32");
   const int B = logits.size(0), K = logits.size(1);
-  F32(loss_rows);
-  CK(loss_rows.numel() == B, "loss_rows size");
+  CK(loss_rows.has_value() || loss_out.has_value(), "softmax_xent: loss_rows and/or loss_out");
+  if (loss_rows) { F32(*loss_rows); CK(loss_rows->numel() == B, "loss_rows size"); }
+  if (loss_out) { F32(*loss_out); CK(loss_out->numel() == 1 && B <= 4096, "softmax_xent: loss_out [1], B <= 4096 (one workgroup)"); }
   CK((labels.has_value()) != (probs.has_value()), "exactly one of labels/probs");
   if (labels) CK(labels->scalar_type() == at::kLong && labels->numel() == B, "labels int64 [B]");
   if (probs) { F32(*probs); CK(probs->numel() == (int64_t)B * K, "probs [B,K]"); }
@@ -258,8 +260,9 @@ void softmax_xent_(const at::Tensor& logits, c10::optional<at::Tensor> labels, c
   if (grad_scale_dev) { F32(*grad_scale_dev); CK(grad_scale_dev->numel() == 1 && grad_scale_dev->is_cuda(), "grad_scale_dev: one fp32 on the GPU"); }
   at::DeviceGuard g(logits.device());
   HIP_OK(softmax_xent(logits.data_ptr(), bf ? 1 : 0, optr<const int64_t>(labels), optr<const float>(probs),
-                      loss_rows.data_ptr<float>(), optr<void>(dlogits), B, K, ld, (float)grad_scale, (float)smoothing,
-                      (int)ignore_index, cur_stream(), optr<const float>(grad_scale_dev)));
+                      optr<float>(loss_rows), optr<void>(dlogits), B, K, ld, (float)grad_scale, (float)smoothing,
+                      (int)ignore_index, cur_stream(), optr<const float>(grad_scale_dev), optr<float>(loss_out),
+                      (float)out_scale));
 }
 
 void label_count_inv_(const at::Tensor& labels, int64_t ignore_index, const at::Tensor& inv) {
@@ -327,17 +330,37 @@ void transpose_bf16_(const at::Tensor& x, const at::Tensor& y) {
   at::DeviceGuard g(x.device());
   HIP_OK(transpose_bf16(x.data_ptr(), y.data_ptr(), (int)x.size(0), (int)x.size(1), x.stride(0), cur_stream()));
 }
-void bias_grad_(const at::Tensor& dy, const at::Tensor& db, int64_t N, bool accumulate) {
+// relu_y / relu_dx: fused ReLU backward (relu_dx = dy * (relu_y > 0), and db sums relu_dx); N % 8 == 0 only
+void bias_grad_(const at::Tensor& dy, const at::Tensor& db, int64_t N, bool accumulate, c10::optional<at::Tensor> relu_y,
+                c10::optional<at::Tensor> relu_dx) {
   GPU(dy); BF16(dy); F32(db);
   CK(dy.numel() % N == 0 && db.numel() >= N, "bias_grad: shapes");
   // the kernels read dy as a dense [M][N] array (row stride N, 16-B vectors): no strided views
   CK(dy.is_contiguous() && db.is_contiguous(), "bias_grad: dy and db must be contiguous");
+  CK(relu_y.has_value() == relu_dx.has_value(), "bias_grad: relu_y and relu_dx together");
+  if (relu_y) {
+    BF16(*relu_y); BF16(*relu_dx);
+    CK(N % 8 == 0 && relu_y->is_contiguous() && relu_dx->is_contiguous() && relu_y->numel() == dy.numel() &&
+           relu_dx->numel() == dy.numel(), "bias_grad: fused ReLU needs N % 8 == 0 and dense y / dx like dy");
+  }
   at::DeviceGuard g(dy.device());
   const long M = dy.numel() / N;
   at::Tensor ws;  // deterministic mode: partial rows from the caching allocator (stream-ordered)
   if (deterministic()) ws = at::empty({(int64_t)bias_grad_rows(M) * N}, dy.options().dtype(at::kFloat));
   HIP_OK(bias_grad(dy.data_ptr(), db.data_ptr<float>(), M, (int)N, accumulate ? 1 : 0, cur_stream(),
-                   ws.defined() ? ws.data_ptr<float>() : nullptr));
+                   ws.defined() ? ws.data_ptr<float>() : nullptr, relu_y ? relu_y->data_ptr() : nullptr,
+                   relu_dx ? relu_dx->data_ptr() : nullptr));
+}
+void pad_cols_bf16_(const at::Tensor& x, const at::Tensor& out) {
+  GPU(x); BF16(x); BF16(out);
+  CK(x.dim() >= 1 && x.stride(-1) == 1 && out.is_contiguous() && out.dim() == x.dim(), "pad_cols: unit column stride");
+  const long K = x.size(-1), Kp = out.size(-1), R = K ? x.numel() / K : 0;
+  CK(out.numel() == R * Kp && Kp >= K && Kp % 2 == 0, "pad_cols: out [..., Kp >= K], Kp even");
+  // rows of x: every leading dimension must collapse to one row stride
+  long ldx = x.dim() >= 2 ? x.stride(-2) : K;
+  for (int d = x.dim() - 3; d >= 0; --d) CK(x.stride(d) == x.stride(d + 1) * x.size(d + 1), "pad_cols: x rows must have one stride");
+  at::DeviceGuard g(x.device());
+  HIP_OK(pad_cols_bf16(x.data_ptr(), ldx, out.data_ptr(), R, (int)K, (int)Kp, cur_stream()));
 }
 void im2col_(const at::Tensor& x, const at::Tensor& col, int64_t ho, int64_t wo, int64_t sh, int64_t sw,
              std::vector<int> dh, std::vector<int> dw, int64_t kpad) {
@@ -388,16 +411,21 @@ void sgd_step_(const at::Tensor& w, const at::Tensor& g, c10::optional<at::Tenso
 }
 void adam_step_(const at::Tensor& w, const at::Tensor& g, const at::Tensor& m, const at::Tensor& v,
                 c10::optional<at::Tensor> w16, double lr, double b1, double b2, double eps, double wd, int64_t mode,
-                double bc1, double bc2, double gscale, c10::optional<at::Tensor> tstep) {
+                double bc1, double bc2, double gscale, c10::optional<at::Tensor> tstep,
+                c10::optional<at::Tensor> tick_ctr) {
   OPT_CHECK(w, g);
   F32(m); F32(v);
   if (tstep) { F32(*tstep); CK(tstep->numel() == 1 && tstep->device() == w.device(), "adam: step counter"); }
+  if (mode & 4)
+    CK(tstep && tick_ctr && tick_ctr->scalar_type() == at::kInt && tick_ctr->numel() == 1 &&
+           tick_ctr->device() == w.device(), "adam: the fused tick needs the step counter and an int32 [1] tick_ctr");
   CK(m.numel() == w.numel() && v.numel() == w.numel(), "adam: state sizes");
   if (w16) { BF16(*w16); CK(w16->numel() == w.numel(), "w16 size"); }
   at::DeviceGuard gd(w.device());
   HIP_OK(adam_step(w.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), optr<void>(w16),
                    w.numel(), (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (int)mode, (float)bc1,
-                   (float)bc2, (float)gscale, optr<float>(tstep), cur_stream()));
+                   (float)bc2, (float)gscale, optr<float>(tstep), cur_stream(),
+                   tick_ctr ? reinterpret_cast<unsigned*>(tick_ctr->data_ptr<int>()) : nullptr));
 }
 void commit_delta_(const at::Tensor& W, const at::Tensor& center, const at::Tensor& X, c10::optional<at::Tensor> w16,
                    double scale, bool elastic) {
@@ -597,16 +625,19 @@ void register_ops(py::module& m) {
   m.def("avgpool_bwd", &avgpool_bwd_);
   m.def("softmax_xent", &softmax_xent_, "fused softmax cross-entropy", py::arg("logits"), py::arg("labels"),
         py::arg("probs"), py::arg("loss_rows"), py::arg("dlogits"), py::arg("grad_scale"), py::arg("smoothing"),
-        py::arg("ignore_index"), py::arg("grad_scale_dev") = py::none());
+        py::arg("ignore_index"), py::arg("grad_scale_dev") = py::none(), py::arg("loss_out") = py::none(),
+        py::arg("out_scale") = 1.0);
   m.def("label_count_inv", &label_count_inv_);
   m.def("rows_sum_scaled", &rows_sum_scaled_);
+  m.def("pad_cols_bf16", &pad_cols_bf16_, "zero-padded copy of a row-strided bf16 view");
   m.def("scale_bf16_dev", &scale_bf16_dev_);
   m.def("cast_f32_bf16", &cast_f32_bf16_);
   m.def("sum_rows_bf16", &sum_rows_bf16_);
   m.def("cast_bf16_f32", &cast_bf16_f32_);
   m.def("relu_bwd", &relu_bwd_);
   m.def("add_bf16", &add_bf16_);
-  m.def("bias_grad", &bias_grad_);
+  m.def("bias_grad", &bias_grad_, py::arg("dy"), py::arg("db"), py::arg("N"), py::arg("accumulate"),
+        py::arg("relu_y") = py::none(), py::arg("relu_dx") = py::none());
   m.def("transpose_bf16", &transpose_bf16_);
   m.def("im2col", &im2col_);
   m.def("normalize_u8", &normalize_u8_);
@@ -614,7 +645,8 @@ void register_ops(py::module& m) {
   m.def("sgd_step", &sgd_step_);
   m.def("adam_step", &adam_step_, "fused Adam/AdamW", py::arg("w"), py::arg("g"), py::arg("m"), py::arg("v"),
         py::arg("w16"), py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("mode"),
-        py::arg("bc1"), py::arg("bc2"), py::arg("gscale"), py::arg("tstep") = py::none());
+        py::arg("bc1"), py::arg("bc2"), py::arg("gscale"), py::arg("tstep") = py::none(),
+        py::arg("tick_ctr") = py::none());
   m.def("step_tick", &step_tick_);
   m.def("mse_fwd_bwd", &mse_fwd_bwd_);
   m.def("prob_xent", &prob_xent_);

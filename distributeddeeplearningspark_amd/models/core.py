@@ -24,6 +24,7 @@ from . import optimizers as optim_mod
 from .params import Param, ParamArena, to_numpy
 
 _LAYER_TYPES: dict[str, type] = {}
+_UNIT_SEEDS: dict = {}  # (device, dtype, shape) -> ones: the backward seed of training steps
 _NAME_COUNTS: dict[str, int] = {}
 
 
@@ -75,8 +76,8 @@ class Layer:
         self._initial_weights = kwargs.get("weights")
 
     # ------------------------------------------------------------------ params
-    def add_weight(self, name: str, shape, init, trainable: bool = True) -> Param:
-        p = Param(f"{self.name}/{name}", shape, init, trainable)
+    def add_weight(self, name: str, shape, init, trainable: bool = True, pad=None) -> Param:
+        p = Param(f"{self.name}/{name}", shape, init, trainable, pad=pad)
         self._params.append(p)
         return p
 
@@ -227,10 +228,10 @@ class Model(Layer):
             dtype = torch.bfloat16 if device.type == "cuda" and not self._keeps_fp32() else torch.float32
         old = None
         if self.arena is not None:
-            old = self.arena.master.detach().cpu()
+            old = self.arena.get_flat().detach().cpu()  # canonical: the new arena may pad differently
         params = self.all_params()
         self.arena = ParamArena(params, device, dtype, seed=self.seed if seed is None else seed)
-        if old is not None and old.numel() == self.arena.master.numel():
+        if old is not None and old.numel() == self.arena.canon_numel:
             self.arena.set_flat(old)
         self.states_to(device)
         self.device, self.compute_dtype = device, dtype
@@ -372,15 +373,23 @@ class Model(Layer):
         return loss
 
     def backward_unit(self, loss):
-        """``loss.backward()`` with the model told that the seed gradient is exactly 1 (loss nodes
-        may then skip applying it, with no device -> host read of the seed)."""
+        """``loss.backward()`` with the model (and the loss nodes, ``ops.loss.unit_seed``) told that the
+        seed gradient is exactly 1: they hand out their stored gradients without applying it, and the
+        seed itself is a cached device constant (no fill launch per step)."""
+        from ..ops import loss as loss_ops
         from ..ops.streams import join
 
+        key = (loss.device, loss.dtype, loss.shape)
+        one = _UNIT_SEEDS.get(key)
+        if one is None:
+            one = _UNIT_SEEDS[key] = torch.ones(loss.shape, dtype=loss.dtype, device=loss.device)
         self._unit_loss_grad = True
+        loss_ops._UNIT_SEED[0] = loss.grad_fn
         try:
-            loss.backward()
+            loss.backward(one)
         finally:
             self._unit_loss_grad = False
+            loss_ops._UNIT_SEED[0] = None
         join(self.device)  # side-stream weight gradients (ops/streams.py) land before anyone reads them
 
     def train_on_batch(self, x, y, grad_sync=None, grad_scale: float = 1.0) -> float:
@@ -467,7 +476,7 @@ class Model(Layer):
 
     def get_flat_weights(self) -> torch.Tensor:
         self._ensure_placed()
-        return self.arena.master
+        return self.arena.get_flat()
 
     def to_json(self) -> str:
         d = {"class_name": type(self).__name__, "config": self.get_config(),

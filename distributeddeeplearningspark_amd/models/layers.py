@@ -46,6 +46,11 @@ def _pair(v):
     return (int(v), int(v)) if isinstance(v, (int, np.integer)) else tuple(int(t) for t in v)
 
 
+def _r8(n: int) -> int:
+    """Storage width of a GEMM operand dimension: whole 16-B bf16 vectors (``params.Param(pad=)``)."""
+    return -(-int(n) // 8) * 8
+
+
 class Activation(Layer):
     def __init__(self, activation, **kw):
         super().__init__(**kw)
@@ -74,10 +79,10 @@ class Dense(Layer):
     def build(self, input_shape):
         fin = int(input_shape[-1])
         init = P.he_normal(fin) if self.kernel_initializer == "he_normal" else P.glorot_uniform(fin, self.units)
-        self.kernel = self.add_weight("kernel", (self.units, fin), init)
+        self.kernel = self.add_weight("kernel", (self.units, fin), init, pad=(_r8(self.units), _r8(fin)))
         self.kernel.to_keras = lambda a: a.T.copy()
         self.kernel.from_keras = lambda a: a.T.copy()
-        self.bias = self.add_weight("bias", (self.units,), P.zeros) if self.use_bias else None
+        self.bias = self.add_weight("bias", (self.units,), P.zeros, pad=(_r8(self.units),)) if self.use_bias else None
 
     def compute_output_shape(self, s):
         return (*s[:-1], self.units)
@@ -88,10 +93,19 @@ class Dense(Layer):
         y = linear_ops.linear(x, self.kernel.data, None if self.bias is None else self.bias.master,
                               relu=fused, grad_w=self.kernel.grad if self.trainable else None,
                               grad_b=None if (self.bias is None or not self.trainable) else self.bias.grad,
-                              on_grad=self.grad_hook)
+                              on_grad=self.grad_hook, padded=self._padded())
         if not fused and not skip_activation:
             y = apply_activation(act, y)
         return y
+
+    def _padded(self):
+        """(kernel, bias master, kernel grad, bias grad) padded storage views when the arena pads
+        this layer (``ops.linear.linear(padded=)``), else None."""
+        k, b = self.kernel, self.bias
+        if not k.padded and (b is None or not b.padded):
+            return None
+        return (k.pdata, None if b is None else b.pmaster, k.pgrad if self.trainable else None,
+                None if (b is None or not self.trainable) else b.pgrad)
 
     def get_config(self):
         return {**super().get_config(), "units": self.units, "activation": self.activation_name,
@@ -138,10 +152,11 @@ class Conv2D(Layer):
         kh, kw = self.kernel_size
         fan_in, fan_out = kh * kw * cin, kh * kw * self.filters
         init = P.he_normal(fan_in) if self.kernel_initializer == "he_normal" else P.glorot_uniform(fan_in, fan_out)
-        self.kernel = self.add_weight("kernel", (self.filters, kh, kw, cin), init)
+        self.kernel = self.add_weight("kernel", (self.filters, kh, kw, cin), init,
+                                      pad=(_r8(self.filters), kh, kw, _r8(cin)))
         self.kernel.to_keras = lambda a: np.ascontiguousarray(a.transpose(1, 2, 3, 0))
         self.kernel.from_keras = lambda a: np.ascontiguousarray(a.transpose(3, 0, 1, 2))
-        self.bias = self.add_weight("bias", (self.filters,), P.zeros) if self.use_bias else None
+        self.bias = self.add_weight("bias", (self.filters,), P.zeros, pad=(_r8(self.filters),)) if self.use_bias else None
 
     def compute_output_shape(self, s):
         H, W, _ = s
@@ -162,7 +177,7 @@ class Conv2D(Layer):
                             stride=self.strides, padding=(ph, pw), dilation=self.dilation_rate, relu=fused,
                             grad_w=self.kernel.grad if self.trainable else None,
                             grad_b=None if (self.bias is None or not self.trainable) else self.bias.grad,
-                            stats=stats, on_grad=self.grad_hook)
+                            stats=stats, on_grad=self.grad_hook, padded=Dense._padded(self))
         if not fused and not skip_activation:
             y = apply_activation(self.activation_name, y)
         return y

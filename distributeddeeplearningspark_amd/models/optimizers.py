@@ -23,6 +23,7 @@ class Optimizer:
         self.arena = None
         self.state: dict[str, torch.Tensor] = {}
         self.device_step: torch.Tensor | None = None  # set for graph capture (models/step.py)
+        self.tick_ctr: torch.Tensor | None = None  # int32 workgroup counter of the fused tick (Adam)
 
     def bind(self, arena):
         self.arena = arena
@@ -41,13 +42,18 @@ class Optimizer:
         return {"name": self.name, "lr": self.lr, "weight_decay": self.weight_decay}
 
     def state_dict(self):
-        return {"iterations": self.iterations, **{k: v.detach().cpu() for k, v in self.state.items()}}
+        """Iterations + the flat state slots in the arena's canonical layout (params.py)."""
+        conv = self.arena.to_canonical if self.arena is not None else (lambda t: t)
+        return {"iterations": self.iterations, **{k: conv(v.detach()).cpu() for k, v in self.state.items()}}
 
     def load_state_dict(self, sd):
         self.iterations = int(sd.get("iterations", 0))
         for k, v in sd.items():
             if k in self.state:
-                self.state[k].copy_(v.to(self.state[k].device))
+                v = v.to(self.state[k].device)
+                if self.arena is not None and v.numel() != self.state[k].numel():
+                    v = self.arena.from_canonical(v)
+                self.state[k].copy_(v)
         if self.device_step is not None:
             self.device_step.fill_(float(self.iterations))
 
@@ -58,6 +64,7 @@ class Optimizer:
         if self.device_step is None and self.arena is not None and self.arena.master.is_cuda:
             self.device_step = torch.full((1,), float(self.iterations), dtype=torch.float32,
                                           device=self.arena.master.device)
+            self.tick_ctr = torch.zeros(1, dtype=torch.int32, device=self.arena.master.device)
 
     def _grad_scale(self, grad_scale):
         if self.clipnorm is None:
@@ -93,12 +100,24 @@ class Optimizer:
         w16 = None if a.compute is a.master else a.compute[sl]
         self._apply(a.master[sl], a.grad[sl], w16, gs, {k: v[sl] for k, v in self.state.items()})
 
-    def captured_update(self, gs: float = 1.0):
+    def captured_update(self, gs: float = 1.0, zero_grads: bool = False):
         """The device-side part of one step (step-counter tick + full update) for a hipGraph
-        capture; the host counter is advanced per replay by the caller (models/step.py)."""
+        capture; the host counter is advanced per replay by the caller (models/step.py).
+
+        ``zero_grads``: the caller captures another step right after this one — optimizers that can
+        zero the gradients as they consume them do so, and the arena skips that step's zero_grad fill
+        (``ParamArena.grads_zeroed``).  Adam also advances the device step counter inside its own
+        launch (no step_tick)."""
+        a = self.arena
+        if self._fused_update(gs, zero_grads):
+            a.grads_zeroed = zero_grads
+            return
         if self.device_step is not None and self._device_tick:
             K.step_tick(self.device_step)
-        self.apply_range(0, self.arena.numel, gs)
+        self.apply_range(0, a.numel, gs)
+
+    def _fused_update(self, gs: float, zero_grads: bool) -> bool:
+        return False
 
     @property
     def ranged_ok(self) -> bool:
@@ -145,10 +164,20 @@ class Adam(Optimizer):
 
     _device_tick = True
 
-    def _apply(self, w, g, w16, gs, st):
+    def _apply(self, w, g, w16, gs, st, tick_ctr=None, zero_grad=False):
         K.adam_(w, g, st["m"], st["v"], w16, lr=self.lr, beta1=self.b1, beta2=self.b2, eps=self.eps,
                 weight_decay=self.weight_decay, decoupled=self.decoupled, keras_eps=self.keras_eps,
-                step=self.iterations, grad_scale=gs, device_step=self.device_step)
+                step=self.iterations, grad_scale=gs, device_step=self.device_step, tick_ctr=tick_ctr,
+                zero_grad=zero_grad)
+
+    def _fused_update(self, gs, zero_grads):
+        """One launch: tick + update (+ gradient zeroing) over the whole arena."""
+        a = self.arena
+        if self.device_step is None or self.tick_ctr is None or not a.master.is_cuda:
+            return False
+        self._apply(a.master, a.grad, None if a.compute is a.master else a.compute, gs, self.state,
+                    tick_ctr=self.tick_ctr, zero_grad=zero_grads)
+        return True
 
     def get_config(self):
         return {**super().get_config(), "beta_1": self.b1, "beta_2": self.b2, "epsilon": self.eps}

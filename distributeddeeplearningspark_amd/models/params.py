@@ -10,6 +10,20 @@ checkpoints / the reference's ``get_weights()`` are slices of one buffer.
 Parameters are laid out in registration order (forward order); backward produces
 gradients roughly in reverse, so gradient buckets are formed from the END of the
 buffer (``parallel/ddp.py``).
+
+Padded storage: a layer may ask for a parameter's storage to be wider than its shape
+(``Param(pad=...)``, e.g. a Dense(225) kernel [225, 4608] kept as [232, 4608], a
+Conv2D(1 -> 32) filter [32, 3, 3, 1] as [32, 3, 3, 8]) so the MFMA GEMMs, whose operand rows are
+read as 16-B vectors, use the arena storage directly instead of padded copies made every step.
+Bf16 arenas honour the request (fp32 arenas: the fp32 GEMM takes element strides); the padding
+is zero in the master, compute and gradient buffers and stays zero (its gradients are zero, so
+every optimizer leaves it at zero).  ``p.master / p.data / p.grad`` are the logical views (the
+Keras surface); ``p.pmaster / p.pdata / p.pgrad`` the padded storage views.
+
+Flat weights that leave the arena (``get_flat`` / ``set_flat``: serialised models, worker results,
+checkpoints, parameter-server traffic) use the CANONICAL layout — the unpadded one an fp32 arena has —
+so a bf16 GPU worker, the fp32 CPU driver and a checkpoint all agree; ``master`` / ``grad`` and the
+device-side exchanges between workers of one layout stay in the storage layout.
 """
 from __future__ import annotations
 
@@ -26,11 +40,15 @@ class Param:
     """Handle of one trainable tensor living in a :class:`ParamArena`."""
 
     __slots__ = ("name", "shape", "init", "master", "data", "grad", "offset", "trainable", "keras_shape",
-                 "to_keras", "from_keras", "_initial")
+                 "to_keras", "from_keras", "_initial", "pad", "pshape", "pmaster", "pdata", "pgrad")
 
-    def __init__(self, name: str, shape: Sequence[int], init: Callable, trainable: bool = True):
+    def __init__(self, name: str, shape: Sequence[int], init: Callable, trainable: bool = True, pad=None):
         self.name = name
         self.shape = tuple(int(s) for s in shape)
+        # requested storage shape (>= shape per dim); pshape: the one the arena chose
+        self.pad = None if pad is None else tuple(max(int(a), int(b)) for a, b in zip(pad, self.shape))
+        self.pshape = self.shape
+        self.pmaster = self.pdata = self.pgrad = None
         self.init = init
         self.master = None
         self.data = None
@@ -46,6 +64,20 @@ class Param:
     def numel(self) -> int:
         return int(math.prod(self.shape))
 
+    @property
+    def snumel(self) -> int:
+        """Elements of the arena storage (the padded shape)."""
+        return int(math.prod(self.pshape))
+
+    @property
+    def padded(self) -> bool:
+        return self.pshape != self.shape
+
+    @property
+    def logical(self) -> tuple:
+        """Index of the logical region inside the padded storage."""
+        return tuple(slice(0, n) for n in self.shape)
+
     def __repr__(self):
         return f"Param({self.name}, {self.shape})"
 
@@ -57,9 +89,17 @@ class ParamArena:
         self.compute_dtype = compute_dtype
         off = 0
         for p in self.params:
+            p.pshape = p.pad if (p.pad is not None and compute_dtype != torch.float32) else p.shape
             p.offset = off
-            off += math.ceil(p.numel / ALIGN) * ALIGN
+            off += math.ceil(p.snumel / ALIGN) * ALIGN
         self.numel = max(off, ALIGN)
+        self.padded = any(p.padded for p in self.params)
+        # canonical (unpadded) layout: offsets of an fp32 arena over the same parameters
+        self.canon_offsets, coff = [], 0
+        for p in self.params:
+            self.canon_offsets.append(coff)
+            coff += math.ceil(p.numel / ALIGN) * ALIGN
+        self.canon_numel = max(coff, ALIGN)
         self.master = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
         self.grad = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
         if compute_dtype == torch.float32:
@@ -73,13 +113,20 @@ class ParamArena:
                 v = torch.as_tensor(p._initial, dtype=torch.float32).reshape(p.shape)
             else:
                 v = p.init(p.shape, gen).to(torch.float32)
-            host[p.offset : p.offset + p.numel] = v.reshape(-1)
+            if p.padded:
+                host[p.offset : p.offset + p.snumel].view(p.pshape)[p.logical] = v
+            else:
+                host[p.offset : p.offset + p.numel] = v.reshape(-1)
         self.master.copy_(host)
         for p in self.params:
-            sl = slice(p.offset, p.offset + p.numel)
-            p.master = self.master[sl].view(p.shape)
-            p.grad = self.grad[sl].view(p.shape)
-            p.data = self.compute[sl].view(p.shape)
+            sl = slice(p.offset, p.offset + p.snumel)
+            p.pmaster = self.master[sl].view(p.pshape)
+            p.pgrad = self.grad[sl].view(p.pshape)
+            p.pdata = self.compute[sl].view(p.pshape)
+            if p.padded:
+                p.master, p.grad, p.data = p.pmaster[p.logical], p.pgrad[p.logical], p.pdata[p.logical]
+            else:
+                p.master, p.grad, p.data = p.pmaster, p.pgrad, p.pdata
             # Graph anchors: ops take these views and return None for them in backward
             # (their gradients go out of band into ``p.grad``), but marking them makes
             # autograd record every op even when the network input needs no gradient.
@@ -89,7 +136,12 @@ class ParamArena:
         self.sync_compute()
 
     # -------------------------------------------------------------------------
+    grads_zeroed = False  # set by a captured optimizer update that zeroed the gradients it consumed
+
     def zero_grad(self):
+        if self.grads_zeroed:  # the previous (captured) update left them zero: no fill launch
+            self.grads_zeroed = False
+            return
         self.grad.zero_()
 
     def sync_compute(self):
@@ -97,11 +149,34 @@ class ParamArena:
 
         cast_master_to_compute(self.master, None if self.compute is self.master else self.compute)
 
+    def to_canonical(self, t: torch.Tensor) -> torch.Tensor:
+        """A storage-layout flat (``master``, a worker's final weights, a delta) in the canonical layout."""
+        if not self.padded:
+            return t
+        out = t.new_zeros(self.canon_numel)
+        for p, co in zip(self.params, self.canon_offsets):
+            out[co:co + p.numel].view(p.shape).copy_(t[p.offset:p.offset + p.snumel].view(p.pshape)[p.logical])
+        return out
+
+    def from_canonical(self, c: torch.Tensor) -> torch.Tensor:
+        """A canonical flat in the storage layout (zero padding)."""
+        if not self.padded:
+            return c
+        out = c.new_zeros(self.numel)
+        for p, co in zip(self.params, self.canon_offsets):
+            out[p.offset:p.offset + p.snumel].view(p.pshape)[p.logical].copy_(c[co:co + p.numel].view(p.shape))
+        return out
+
     def get_flat(self) -> torch.Tensor:
-        return self.master
+        """The fp32 weights as a canonical flat (``master`` itself when nothing is padded)."""
+        return self.to_canonical(self.master)
 
     def set_flat(self, flat: torch.Tensor):
-        self.master.copy_(flat.to(self.master.device, torch.float32))
+        """Load a canonical flat (``get_flat`` of any arena over the same parameters)."""
+        if flat.numel() != self.canon_numel:
+            raise ValueError(f"set_flat: {flat.numel()} elements, the canonical layout has {self.canon_numel}")
+        with torch.no_grad():
+            self.master.copy_(self.from_canonical(flat.to(self.master.device, torch.float32)))
         self.sync_compute()
 
     def nbytes(self) -> int:

@@ -25,6 +25,7 @@ import torch.nn.functional as F
 
 from . import determinism as _det
 from . import gemm as G
+from . import zpad as ZP
 from ._native import C, use_native
 from ._ref import accumulate, ref_grads
 from .streams import on_grad_stream
@@ -225,10 +226,12 @@ def _dgrad_as_forward(g: ConvGeometry):
     if g.sh != 1 or g.sw != 1 or g.is_pointwise:
         return None
     ph, pw = g.dh * (g.KH - 1) - g.ph, g.dw * (g.KW - 1) - g.pw
-    if ph < 0 or pw < 0 or g.Co % 64 or g.T > 64:
+    if ph < 0 or pw < 0 or g.Co % 8 or g.Ci % 8 or g.T > 64:
         return None
     g2 = geometry(g.N, g.Ho, g.Wo, g.Co, g.Ci, g.KH, g.KW, (1, 1), (ph, pw), (g.dh, g.dw))
-    if (g2.Ho, g2.Wo) != (g.H, g.W) or not g2.implicit_fwd:
+    # narrow channel counts (Co % 64 != 0: MNIST's 32-filter convs) run the per-vector-gathered forward
+    # (KC_GATHER8) — two launches (filter flip + conv) where the im2col form took four
+    if (g2.Ho, g2.Wo) != (g.H, g.W) or not (g2.implicit_fwd or g2.gather8_fwd):
         return None
     return g2
 
@@ -370,7 +373,7 @@ def conv_ref(x, w, bias, stride, pad, dil, relu=False):
 class _Conv2dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, gw, gb, cfg):
-        stride, pad, dil, relu, stats, hook = cfg
+        stride, pad, dil, relu, stats, hook, pads = cfg
         N, H, W, Ci = x.shape
         Co, KH, KW, _ = w.shape
         ctx.cfg = cfg
@@ -378,71 +381,66 @@ class _Conv2dFn(torch.autograd.Function):
         ctx.ci = Ci
         ctx.co = Co
         if ctx.native:
-            x = x.contiguous()
-            if Ci % 8:  # 16-B vector granularity: pad channels (stem: 3 -> 8) with zeros
-                cp = -(-Ci // 8) * 8
-                x = F.pad(x, (0, cp - Ci))
-                w = F.pad(w.detach(), (0, cp - Ci))
-                Ci = cp
-            if Co % 8:  # same for the output channels (extra filters are zero, sliced off below)
-                cop = -(-Co // 8) * 8
-                w = F.pad(w.detach(), (0, 0, 0, 0, 0, 0, 0, cop - Co))
-                b = None if b is None else F.pad(b.detach(), (0, cop - Co))
-                Co = cop
-            g = geometry(N, H, W, Ci, Co, KH, KW, stride, pad, dil)
+            # 16-B vector granularity: channel counts padded to multiples of 8 with zeros (stem: 3 -> 8,
+            # MNIST: 1 -> 8) — the weights in the arena (params.py, ``pads``) or per call, the input by its
+            # producer (ops/zpad.py) or one pad pass here
+            Cip, Cop = ZP.r8(Ci), ZP.r8(Co)
+            if pads is not None:
+                w, b, gw, gb = pads
+            elif Cip != Ci or Cop != Co:
+                w = F.pad(w.detach(), (0, Cip - Ci, 0, 0, 0, 0, 0, Cop - Co))
+                b = None if b is None else F.pad(b.detach(), (0, Cop - Co))
+                ctx.grad_tmp = True
+            x = ZP.padded(x, Cip) if Cip != Ci else x.contiguous()
+            g = geometry(N, H, W, Cip, Cop, KH, KW, stride, pad, dil)
             st = stats
-            if stats is not None and Co != ctx.co:  # statistics of the padded filters land in a wider workspace
-                st = torch.zeros((stats.shape[0], 2, Co), dtype=torch.float32, device=x.device)
+            if stats is not None and Cop != Co:  # statistics of the padded filters land in a wider workspace
+                st = torch.zeros((stats.shape[0], 2, Cop), dtype=torch.float32, device=x.device)
             y = conv_fwd_native(x, w, g, bias=b, relu=relu, stats=st)
             if st is not stats:
-                stats.copy_(st[:, :, : ctx.co])
+                stats.copy_(st[:, :, :Co])
             ctx.g = g
         else:
             y = conv_ref(x, w.to(x.dtype), None if b is None else b.to(x.dtype), stride, pad, dil, relu)
         ctx.gw, ctx.gb = gw, gb
         ctx.save_for_backward(x, w, b, y if relu else None)
         ctx.needs_dx = ctx.needs_input_grad[0]
-        if y.shape[-1] != ctx.co:
-            y = y[..., : ctx.co].contiguous()
-        return y
+        return ZP.logical(y, Co) if ctx.native else y
 
     @staticmethod
     def backward(ctx, dy):
         x, w, b, y = ctx.saved_tensors
         gw, gb = ctx.gw, ctx.gb
-        stride, pad, dil, relu, _, hook = ctx.cfg
-        dy = dy.contiguous()
+        stride, pad, dil, relu, _, hook, _ = ctx.cfg
         dx = None
         if ctx.native:
             g = ctx.g
-            pad_co = g.Co != ctx.co
-            if pad_co:
-                dy = F.pad(dy, (0, g.Co - ctx.co))
-            if relu:
-                d2 = torch.empty_like(dy)
-                C().relu_bwd(dy, y, d2)
-                dy = d2
-            padded = g.Ci != ctx.ci or pad_co
+            dy = ZP.padded(dy, g.Co) if g.Co != ctx.co else dy.contiguous()
+            if getattr(ctx, "grad_tmp", False):  # logical-shape gradient buffers: padded temporaries
+                tgw = None if gw is None else torch.zeros((g.Co, g.KH, g.KW, g.Ci), dtype=torch.float32, device=dy.device)
+                tgb = None if gb is None else torch.zeros(g.Co, dtype=torch.float32, device=dy.device)
+            else:
+                tgw, tgb = gw, gb
             with on_grad_stream(dy.device, dy, x, default=False):  # parameter gradients beside the data-gradient
-                if gb is not None:
-                    if pad_co:
-                        tb = torch.zeros(g.Co, dtype=torch.float32, device=dy.device)
-                        C().bias_grad(dy, tb, g.Co, True)
-                        gb.add_(tb[: ctx.co])
+                if relu:
+                    d2 = torch.empty_like(dy)
+                    if tgb is not None:  # ReLU backward fused into the bias-gradient sweep
+                        C().bias_grad(dy, tgb, g.Co, True, y, d2)
                     else:
-                        C().bias_grad(dy, gb, g.Co, True)
-                if gw is not None:
-                    if padded:
-                        tmp = torch.zeros((g.Co, g.KH, g.KW, g.Ci), dtype=torch.float32, device=dy.device)
-                        conv_wgrad_native(dy, x, g, tmp)
-                        gw.add_(tmp[: ctx.co, ..., : ctx.ci])
-                    else:
-                        conv_wgrad_native(dy, x, g, gw)
+                        C().relu_bwd(dy, y, d2)
+                    dy = d2
+                elif tgb is not None:
+                    C().bias_grad(dy, tgb, g.Co, True)
+                if tgw is not None:
+                    conv_wgrad_native(dy, x, g, tgw)
+            if tgw is not gw and gw is not None:
+                gw.add_(tgw[: ctx.co, ..., : ctx.ci])
+            if tgb is not gb and gb is not None:
+                gb.add_(tgb[: ctx.co])
             if ctx.needs_dx:
-                dx = conv_dgrad_native(dy, w, g)
-                if g.Ci != ctx.ci:
-                    dx = dx[..., : ctx.ci].contiguous()
+                dx = ZP.logical(conv_dgrad_native(dy, w, g), ctx.ci)
         else:
+            dy = dy.contiguous()
             fn = lambda xx, ww, bb: conv_ref(xx, ww, bb, stride, pad, dil, relu)
             bb = None if b is None else b.to(x.dtype)
             gx, gww, gbb = ref_grads(fn, [x, w.to(x.dtype), bb], dy)
@@ -455,10 +453,12 @@ class _Conv2dFn(torch.autograd.Function):
 
 
 def conv2d(x, w, bias=None, *, stride=1, padding=0, dilation=1, relu=False, grad_w=None, grad_b=None, stats=None,
-           on_grad=None):
+           on_grad=None, padded=None):
     """NHWC conv.  ``w``: [Co, KH, KW, Ci] compute-dtype weights; ``grad_w``/``grad_b``:
     fp32 buffers that receive ``+= dW``/``+= db`` in backward; ``stats``: optional
     [32, 2, Co] fp32 workspace receiving fused per-channel sum / sum-of-squares
-    (GPU); ``on_grad``: callback fired once the parameter gradients are final."""
-    cfg = (_pair(stride), _pair(padding), _pair(dilation), bool(relu), stats, on_grad)
+    (GPU); ``on_grad``: callback fired once the parameter gradients are final; ``padded``:
+    (weight, bias, weight grad, bias grad) zero-padded arena storage (channels rounded up to multiples
+    of 8, ``models/params.py``) that the GPU path uses in place of the logical tensors."""
+    cfg = (_pair(stride), _pair(padding), _pair(dilation), bool(relu), stats, on_grad, padded)
     return _Conv2dFn.apply(x, w, bias, grad_w, grad_b, cfg)

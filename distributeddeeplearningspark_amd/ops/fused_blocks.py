@@ -21,6 +21,7 @@ import torch
 from . import conv as CV
 from . import determinism as _det
 from . import gemm as G
+from . import zpad as ZP
 from ._native import C
 from .norm import new_stats_workspace, partials_workspace
 from .streams import on_grad_stream
@@ -450,12 +451,14 @@ class _ConvBNFn(torch.autograd.Function):
         x = x.contiguous()
         Ci = x.shape[-1]
         ctx.ci = Ci
-        if Ci % 8:  # stem: pad 3 -> 8 channels (16-B vectors)
+        kp = unit.conv.kernel
+        if Ci % 8:  # stem: pad 3 -> 8 channels (16-B vectors); the arena keeps the filter padded (params.py)
             cp = -(-Ci // 8) * 8
-            x = torch.nn.functional.pad(x, (0, cp - Ci))
-            w = torch.nn.functional.pad(unit.conv.kernel.data.detach(), (0, cp - Ci))
+            x = ZP.padded(x, cp)
+            w = kp.pdata if kp.pshape[1:] == (*kp.shape[1:3], cp) and kp.pshape[0] == kp.shape[0] \
+                else torch.nn.functional.pad(kp.data.detach(), (0, cp - Ci))
         else:
-            w = unit.conv.kernel.data
+            w = kp.data
         conv = unit.conv
         N, H, W, Cp = x.shape
         kh, kw = conv.kernel_size
@@ -480,17 +483,17 @@ class _ConvBNFn(torch.autograd.Function):
         conv = unit.conv
         g = st.g
         with on_grad_stream(dy.device, dyc, x, default=False):
-            if g.Ci != ctx.ci:
+            if g.Ci != ctx.ci and ctx.w is not conv.kernel.pdata:
                 tmp = torch.zeros((g.Co, g.KH, g.KW, g.Ci), dtype=torch.float32, device=dy.device)
                 CV.conv_wgrad_native(dyc, x, g, tmp)
                 conv.kernel.grad.add_(tmp[..., : ctx.ci])
-            else:
-                CV.conv_wgrad_native(dyc, x, g, conv.kernel.grad)
+            else:  # padded storage: it takes the zero-padded channels' (zero) gradients as is
+                CV.conv_wgrad_native(dyc, x, g, conv.kernel.pgrad if ctx.w is conv.kernel.pdata else conv.kernel.grad)
         if conv.grad_hook is not None:
             conv.grad_hook()
         dx = None
         if ctx.needs_dx:
-            dx = CV.conv_dgrad_native(dyc, ctx.w, g)[..., : ctx.ci].contiguous()
+            dx = ZP.logical(CV.conv_dgrad_native(dyc, ctx.w, g), ctx.ci)
         ctx.st = None
         return dx, None, None, None
 

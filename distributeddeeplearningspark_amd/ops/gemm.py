@@ -213,12 +213,28 @@ def linear_fwd(x2, w, bias=None, relu=False, out=None, resid=None, stats=None, a
     if out is None:
         out = torch.empty((M, N), dtype=torch.bfloat16, device=x2.device)
     act = (ACT_RELU if relu else ACT_NONE) if act is None else act
+    tiles = math.ceil(M / 64) * math.ceil(N / 64)
+    if (K >= 1024 and tiles <= _SKINNY_FWD_TILES and act <= ACT_RELU and resid is None and stats is None and aux is None
+            and not drop_p and N % 8 == 0 and out.is_contiguous() and x2.device.type == "cuda" and not _det.enabled()):
+        # a few output tiles over a long reduction (a Dense on a flattened feature map at a small batch:
+        # MNIST's [16, 4608] x [4608, 232] is 4 tiles of 72 K-steps): the reduction is split over
+        # workgroups into an fp32 workspace, and one finalize pass adds the bias / ReLU and rounds
+        ws = splitk_workspace(M, N, x2.device)
+        splits = max(2, min(math.ceil(256 / tiles), K // 256))
+        r = gemm(x2, w, ws, M, N, K, KC, KC, x2.stride(0), w.stride(0), N, EPI_F32, tile=3,
+                 k_split=math.ceil(K / splits / 64) * 64, defer_slabs=True)
+        if isinstance(r, tuple):
+            C().splitk_finalize(r[0], out, N, bias, act == ACT_RELU, None, r[1])
+        else:
+            C().splitk_finalize(ws, out, N, bias, act == ACT_RELU, None)
+        return out
     return gemm(x2, w, out, M, N, K, KC, KC, x2.stride(0), w.stride(0), out.stride(0), EPI_BF16, bias=bias, relu=act,
                 resid=resid, ldr=(resid.stride(0) if resid is not None else 0), stats=stats, aux=aux, drop_p=drop_p,
                 drop_seed=drop_seed)
 
 
 _SPLITK_WS = {}
+_SKINNY_FWD_TILES = 16  # 64x64 output tiles at or below which a long-K bf16 Linear forward splits K
 
 
 def splitk_workspace(M, N, device):

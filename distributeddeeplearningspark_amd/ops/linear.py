@@ -12,6 +12,7 @@ import torch
 import torch.nn.functional as F
 
 from . import gemm as G
+from . import zpad as ZP
 from ._native import C, use_native
 from .streams import on_grad_stream
 from ._ref import accumulate, ref_grads
@@ -25,7 +26,7 @@ def linear_ref(x, w, b, relu=False):
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, gw, gb, cfg):
-        relu, hook = cfg
+        relu, hook, pads = cfg
         ctx.cfg = cfg
         ctx.native = use_native(x)
         ctx.xshape = x.shape
@@ -42,20 +43,23 @@ class _LinearFn(torch.autograd.Function):
             ctx.save_for_backward(x2, w, y if relu else None)
             return y.view(*x.shape[:-1], w.shape[0])
         if ctx.native:
-            x2 = x.reshape(-1, x.shape[-1]).contiguous()
-            K, N = x2.shape[1], w.shape[0]
-            Kp, Np = -(-K // 8) * 8, -(-N // 8) * 8
+            K, N = x.shape[-1], w.shape[0]
+            Kp, Np = ZP.r8(K), ZP.r8(N)
             ctx.pad = (K, N, Kp, Np)
-            if Kp != K or Np != N:  # 16-B vector alignment of every GEMM operand row
-                x2 = F.pad(x2, (0, Kp - K))
+            if pads is not None:
+                # padded arena storage (params.py): the GEMMs read / accumulate into it directly
+                w, b, gw, gb = pads
+            elif Kp != K or Np != N:  # 16-B vector alignment of every GEMM operand row
                 w = F.pad(w.detach(), (0, Kp - K, 0, Np - N))
                 b = None if b is None else F.pad(b.detach(), (0, Np - N))
-            y = G.linear_fwd(x2, w, bias=b, relu=relu)
+                ctx.grad_tmp = True  # logical-shape gradient buffers: padded temporaries in backward
+            lead = x.shape[:-1]
+            x2 = ZP.padded(x, Kp).view(-1, Kp) if Kp != K else x.reshape(-1, K).contiguous()
+            y = torch.empty((*lead, Np), dtype=torch.bfloat16, device=x.device)
+            G.linear_fwd(x2, w, bias=b, relu=relu, out=y.view(-1, Np))
             ctx.gw, ctx.gb = gw, gb
-            ctx.save_for_backward(x2, w, y if relu else None)
-            if Np != N:
-                y = y[:, :N].contiguous()
-            return y.view(*x.shape[:-1], N)
+            ctx.save_for_backward(x2, w, y.view(-1, Np) if relu else None)
+            return ZP.logical(y, N)  # zero-padded storage: the next Dense reads it as is
         y = linear_ref(x, w.to(x.dtype), None if b is None else b.to(x.dtype), relu)
         ctx.gw, ctx.gb = gw, gb
         ctx.save_for_backward(x, w, b)
@@ -63,7 +67,7 @@ class _LinearFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        relu, hook = ctx.cfg
+        relu, hook, _ = ctx.cfg
         dx = None
         if ctx.fp32:
             x2, w, y = ctx.saved_tensors
@@ -85,26 +89,33 @@ class _LinearFn(torch.autograd.Function):
             x2, w, y = ctx.saved_tensors
             gw, gb = ctx.gw, ctx.gb
             K, N, Kp, Np = ctx.pad
-            d2 = dy.reshape(-1, N).contiguous()
-            if Np != N:
-                d2 = F.pad(d2, (0, Np - N))
-            if relu:
-                t = torch.empty_like(d2)
-                C().relu_bwd(d2, y, t)
-                d2 = t
+            lead = ctx.xshape[:-1]
+            d2 = (ZP.padded(dy, Np) if Np != N else dy.contiguous()).view(-1, Np)
+            if getattr(ctx, "grad_tmp", False):  # logical-shape gradient buffers: padded temporaries
+                tgw = None if gw is None else torch.zeros((Np, Kp), dtype=torch.float32, device=d2.device)
+                tgb = None if gb is None else torch.zeros(Np, dtype=torch.float32, device=d2.device)
+            else:
+                tgw, tgb = gw, gb
             with on_grad_stream(d2.device, d2, x2, default=False):  # parameter gradients beside the data-gradient
-                if gb is not None:
-                    C().bias_grad(d2, gb, N, True) if Np == N else gb.add_(d2[:, :N].float().sum(0))
-                if gw is not None:
-                    if Np == N and Kp == K:
-                        G.linear_wgrad(d2, x2, gw)
+                if relu:
+                    t = torch.empty_like(d2)
+                    if tgb is not None:  # ReLU backward fused into the bias-gradient sweep
+                        C().bias_grad(d2, tgb, Np, True, y, t)
                     else:
-                        tmp = torch.zeros((Np, Kp), dtype=torch.float32, device=d2.device)
-                        G.linear_wgrad(d2, x2, tmp)
-                        gw.add_(tmp[:N, :K])
+                        C().relu_bwd(d2, y, t)
+                    d2 = t
+                elif tgb is not None:
+                    C().bias_grad(d2, tgb, Np, True)
+                if tgw is not None:
+                    G.linear_wgrad(d2, x2, tgw)
+            if tgw is not gw and gw is not None:
+                gw.add_(tgw[:N, :K])
+            if tgb is not gb and gb is not None:
+                gb.add_(tgb[:N])
             if ctx.needs_dx:
-                dxp = G.linear_dgrad(d2, w)
-                dx = (dxp[:, :K].contiguous() if Kp != K else dxp).view(ctx.xshape)
+                dxp = torch.empty((*lead, Kp), dtype=torch.bfloat16, device=d2.device)
+                G.linear_dgrad(d2, w, out=dxp.view(-1, Kp))
+                dx = ZP.logical(dxp, K)  # zero columns past K (the padded weight columns are zero)
         else:
             x, w, b = ctx.saved_tensors
             gw, gb = ctx.gw, ctx.gb
@@ -118,5 +129,8 @@ class _LinearFn(torch.autograd.Function):
         return dx, None, None, None, None, None
 
 
-def linear(x, w, bias=None, *, relu=False, grad_w=None, grad_b=None, on_grad=None):
-    return _LinearFn.apply(x, w, bias, grad_w, grad_b, (bool(relu), on_grad))
+def linear(x, w, bias=None, *, relu=False, grad_w=None, grad_b=None, on_grad=None, padded=None):
+    """``padded``: (weight, bias, weight grad, bias grad) zero-padded arena storage ([Np, Kp], [Np], N and K
+    rounded up to multiples of 8; ``models/params.py``) used by the GPU GEMMs in place of the logical
+    ``w`` / ``bias`` / ``grad_w`` / ``grad_b``."""
+    return _LinearFn.apply(x, w, bias, grad_w, grad_b, (bool(relu), on_grad, padded))

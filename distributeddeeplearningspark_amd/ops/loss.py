@@ -5,7 +5,21 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
+from . import zpad as ZP
 from ._native import C, use_native
+
+
+# The root node of a ``loss.backward()`` a training step runs from a unit seed (models/core.py
+# backward_unit): that loss node hands out its stored gradient as is — no scaling launch.  Only the
+# root qualifies: a loss node inside a user's composite loss receives a non-unit gradient.
+_UNIT_SEED = [None]
+
+
+def unit_seed(ctx) -> bool:
+    return ctx is _UNIT_SEED[0]
+
+
+_SMALL_ROWS = 512  # batches up to this many rows: one workgroup computes every row AND the batch loss
 
 
 class _SoftmaxXentFn(torch.autograd.Function):
@@ -13,19 +27,32 @@ class _SoftmaxXentFn(torch.autograd.Function):
     def forward(ctx, logits, labels, probs, smoothing, ignore_index):
         B, K = logits.shape
         if use_native(logits):
-            logits = logits.contiguous()
-            loss_rows = torch.empty(B, dtype=torch.float32, device=logits.device)
-            dl = torch.empty_like(logits)
+            if logits.stride(1) != 1:
+                logits = logits.contiguous()
+            ld = logits.stride(0)
+            # dlogits in the logits' layout; the kernel zeroes the columns past K, so a padded logits row
+            # (ops/zpad.py: a Dense(10) head writes [B, 16]) gives zero-padded dlogits the Dense reads as is
+            dfull = torch.empty((B, ld), dtype=logits.dtype, device=logits.device)
+            dl = ZP.logical(dfull, K)
+            loss = torch.empty(1, dtype=torch.float32, device=logits.device)
+            small = B <= _SMALL_ROWS
+            rows = None if small else torch.empty(B, dtype=torch.float32, device=logits.device)
             if labels is not None:
-                valid = (labels != ignore_index).sum().clamp_min(1).to(torch.float32)
-                # grad scale 1/valid is data-dependent: use 1/B in-kernel, rescale below on host-free path
-                C().softmax_xent(logits, labels.to(torch.int64).contiguous(), None, loss_rows, dl, 1.0, smoothing,
-                                 ignore_index)
-                ctx.save_for_backward(dl, valid)
-                return loss_rows.sum() / valid
-            C().softmax_xent(logits, None, probs.to(torch.float32).contiguous(), loss_rows, dl, 1.0 / B, 0.0, -100)
-            ctx.save_for_backward(dl, None)
-            return loss_rows.mean()
+                # 1 / #valid labels on the device (no host sync): the gradient scale and the loss normaliser
+                inv = torch.empty(1, dtype=torch.float32, device=logits.device)
+                lab = labels.to(torch.int64).contiguous()
+                C().label_count_inv(lab, ignore_index, inv)
+                C().softmax_xent(logits, lab, None, rows, dl, 1.0, smoothing, ignore_index, inv,
+                                 loss if small else None, 1.0)
+                if not small:
+                    C().rows_sum_scaled(rows, 1.0, inv, loss)
+            else:
+                C().softmax_xent(logits, None, probs.to(torch.float32).contiguous(), rows, dl, 1.0 / B, 0.0, -100,
+                                 None, loss if small else None, 1.0 / B)
+                if not small:
+                    C().rows_sum_scaled(rows, 1.0 / B, None, loss)
+            ctx.save_for_backward(dl)
+            return loss.view(())
         with torch.enable_grad():
             lg = logits.detach().requires_grad_(True)
             lp = F.log_softmax(lg.float(), dim=-1)
@@ -39,14 +66,15 @@ class _SoftmaxXentFn(torch.autograd.Function):
             else:
                 out = -(probs.float() * lp).sum(-1).mean()
             (dl,) = torch.autograd.grad(out, [lg])
-        ctx.save_for_backward(dl, None)
+        ctx.save_for_backward(dl)
         return out.detach()
 
     @staticmethod
     def backward(ctx, g):
-        dl, valid = ctx.saved_tensors
-        scale = g if valid is None else g / valid
-        return (dl * scale.to(dl.dtype)).to(dl.dtype), None, None, None, None
+        (dl,) = ctx.saved_tensors
+        if unit_seed(ctx):
+            return dl, None, None, None, None
+        return (dl * g.to(dl.dtype)).to(dl.dtype), None, None, None, None
 
 
 def softmax_cross_entropy(logits, labels=None, probs=None, label_smoothing=0.0, ignore_index=-100):
@@ -71,7 +99,7 @@ class _MSEFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         (grad,) = ctx.saved_tensors
-        return grad * g, None
+        return (grad if unit_seed(ctx) else grad * g), None
 
 
 def mean_squared_error(pred, target):
@@ -113,6 +141,8 @@ class _ProbXentFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         (dp,) = ctx.saved_tensors
+        if unit_seed(ctx) and dp.dtype == ctx.in_dtype:
+            return dp, None, None, None, None
         return (dp * g).to(ctx.in_dtype), None, None, None, None
 
 

@@ -26,15 +26,19 @@ def sgd_(w, g, mom, w16, *, lr, momentum=0.0, dampening=0.0, weight_decay=0.0, n
 
 
 def adam_(w, g, m, v, w16, *, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0, decoupled=False,
-          keras_eps=False, step=1, grad_scale=1.0, device_step=None):
+          keras_eps=False, step=1, grad_scale=1.0, device_step=None, tick_ctr=None, zero_grad=False):
     """``device_step``: optional fp32 GPU scalar holding the step count, already advanced for
     this step by :func:`step_tick` (the optimizer does it once per step, before the first
-    ranged update); the bias corrections are computed from it on the device (graph-replay safe)."""
+    ranged update); the bias corrections are computed from it on the device (graph-replay safe).
+    ``tick_ctr`` (int32 [1], zeroed once): the launch advances ``device_step`` itself (no step_tick
+    launch); ``zero_grad``: ``g`` is zeroed as it is consumed.  Both GPU only (captured steps)."""
     bc1 = 1.0 - beta1 ** step
     bc2 = 1.0 - beta2 ** step
     if use_native(w):
-        mode = (1 if decoupled else 0) | (2 if keras_eps else 0)
-        C().adam_step(w, g, m, v, w16, lr, beta1, beta2, eps, weight_decay, mode, bc1, bc2, grad_scale, device_step)
+        mode = (1 if decoupled else 0) | (2 if keras_eps else 0) | (4 if tick_ctr is not None else 0) \
+            | (8 if zero_grad else 0)
+        C().adam_step(w, g, m, v, w16, lr, beta1, beta2, eps, weight_decay, mode, bc1, bc2, grad_scale, device_step,
+                      tick_ctr)
         return
     d = g * grad_scale
     if decoupled:

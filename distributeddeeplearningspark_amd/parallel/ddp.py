@@ -274,7 +274,7 @@ class DataParallel:
         buckets = []  # built front -> back, reversed below: index 0 = end of the arena
         cur = None
         for p in params:
-            end = p.offset + (-(-p.numel // 64) * 64)
+            end = p.offset + (-(-p.snumel // 64) * 64)
             if cur is None:
                 cur = {"start": p.offset, "end": end, "params": [p]}
             else:

@@ -106,7 +106,7 @@ class _Replica:
         self.graph = None
 
     # one step: fetch batch (ctr % nb) -> loss / backward -> optimizer -> record loss, ctr += 1
-    def _step_body(self, captured: bool):
+    def _step_body(self, captured: bool, more: bool = False):
         from ..ops._native import C
         from ..ops.scope import replica_scope
 
@@ -114,8 +114,8 @@ class _Replica:
         with replica_scope(self.rid):
             C().batch_fetch([self.X, self.Y], [self.sx, self.sy], self.ctr, self.nb)
             loss = m.backward_step(m.to_input(self.sx), m.to_target(self.sy))
-            if captured:
-                m.optimizer.captured_update(1.0)
+            if captured:  # ``more``: another captured step follows (it skips its zero_grad fill)
+                m.optimizer.captured_update(1.0, zero_grads=more)
             else:
                 m.optimizer.step(1.0)
             C().step_record(loss.detach().float().reshape(1), self.hist, self.ctr)
@@ -145,8 +145,8 @@ class _Replica:
         m.optimizer.enable_device_step()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=stream):
-            for _ in range(k):
-                self._step_body(captured=True)
+            for i in range(k):
+                self._step_body(captured=True, more=i + 1 < k)
         from ..ops.norm import _POOL
 
         # the replayed kernels address the statistics-pool buffers: keep them alive even if the
@@ -351,6 +351,7 @@ class ReplicaGroup:
             print(f"[ddl] replica-group hipGraph capture disabled: {type(e).__name__}: {e}", flush=True)
             for rep in self.reps:
                 rep.graph = None
+                rep.model.arena.grads_zeroed = False  # a capture cut short must not skip an eager fill
             torch.cuda.synchronize(self.pg.device)
             return False
         for rep in reps:
@@ -391,7 +392,7 @@ def train_group(rank, world, pg, cfg, blob, Xs, Ys, rids, sizes):
                "replica_group": {"group": rank, "groups": world, "replicas": len(grp.reps),
                                  "batched": grp.batched is not None}}
         if rep.rid == 0:
-            res["flat"] = grp.center.cpu().numpy().copy()
+            res["flat"] = grp.reps[0].model.arena.to_canonical(grp.center).cpu().numpy().copy()
             res["states"] = get_states(rep.model)
         out.append(res)
     return out

@@ -374,13 +374,13 @@ class _AsyncPSWorker(_Worker):
 
         a, algo, k = self.arena, self.cfg["algorithm"], self.k
         W = a.master.detach()
-        cli = ParameterServerClient(self.cfg["ps_port"], self.pg.rank, W.numel())
+        # the server holds the driver's canonical flat (params.py); the arena may be padded
+        cli = ParameterServerClient(self.cfg["ps_port"], self.pg.rank, a.canon_numel)
         self._n = 0
         try:
             def pull():
                 with torch.no_grad():
-                    W.copy_(cli.pull().to(W.device))
-                    a.sync_compute()
+                    a.set_flat(cli.pull())
                 return W.clone()
 
             anchor = pull()
@@ -394,15 +394,15 @@ class _AsyncPSWorker(_Worker):
                     if algo in ("easgd", "aeasgd", "eamsgd"):
                         e = (W - anchor) * self.cfg["alpha"]
                         W.sub_(e)
-                        cli.commit(e)
+                        cli.commit(a.to_canonical(e))
                     else:
                         r = W - anchor
                         if algo == "adag":
                             r.div_(k)
-                        cli.commit(r)
+                        cli.commit(a.to_canonical(r))
                 self._n += 1
                 if algo in ("easgd", "aeasgd", "eamsgd"):
-                    anchor = cli.pull().to(W.device).clone()  # elastic: keep local weights, refresh center
+                    anchor = a.from_canonical(cli.pull().to(W.device)).clone()  # elastic: keep local weights, refresh center
                     a.sync_compute()
                 else:
                     anchor = pull()
@@ -551,7 +551,7 @@ def _train_worker(rank, world, pg, cfg, blob, X, Y, sizes):
            "ingest": "stream" if feed.streaming else "resident", "timed_s": getattr(w, "timed_s", None),
            "timed_steps": getattr(w, "timed_steps", 0)}
     if rank == 0 or cfg["algorithm"] == "ensemble":
-        out["flat"] = final.cpu().numpy().copy()
+        out["flat"] = model.arena.to_canonical(final).cpu().numpy().copy()
         out["states"] = get_states(model)
     return out
 

@@ -27,7 +27,7 @@ def serialize_keras_model(model) -> dict:
     model.build_model()
     d = {"model": model.to_json(), "weights": model.get_weights()}
     if model.arena is not None:
-        d["flat"] = model.arena.master.detach().cpu().numpy().copy()
+        d["flat"] = model.arena.get_flat().detach().cpu().numpy().copy()  # canonical layout (params.py)
     d["states"] = {f"{l.name}/{k}": v.detach().cpu().numpy().copy()
                    for l in model.all_layers() for k, v in l._states.items()}
     if model.optimizer is not None:

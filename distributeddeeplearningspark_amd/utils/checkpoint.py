@@ -53,7 +53,7 @@ def save_checkpoint(directory: str, model, step: int = 0, optimizer=None, extra:
             f.write(model.to_json())
         ws = model.get_weights()
         np.savez(os.path.join(tmp, "weights.npz"), **{f"w_{i:03d}": np.asarray(w) for i, w in enumerate(ws)})
-        tensors = {"arena.master": model.arena.master.detach().float().cpu().contiguous()}
+        tensors = {"arena.master": model.arena.get_flat().detach().float().cpu().contiguous()}
         for i, s in enumerate(_states_in_order(model)):
             tensors[f"layer_state.{i:04d}"] = s.detach().float().cpu().contiguous()
         opt = optimizer if optimizer is not None else model.optimizer
@@ -108,7 +108,7 @@ def save_rank_state(directory: str, model, step: int, rank: int, extra: dict | N
     ``latest`` never names a step whose rank files are missing."""
     path = _rank_file(directory, step, rank)
     os.makedirs(os.path.dirname(path), exist_ok=True)
-    tensors = {"arena.master": model.arena.master.detach().float().cpu().contiguous()}
+    tensors = {"arena.master": model.arena.get_flat().detach().float().cpu().contiguous()}
     for i, st in enumerate(_states_in_order(model)):
         tensors[f"layer_state.{i:04d}"] = st.detach().float().cpu().contiguous()
     opt = model.optimizer

@@ -312,3 +312,52 @@ def test_sequential_fused_convbn_matches_two_node_path(monkeypatch):
     assert rel < 1e-2, rel
     for a, b in zip(s1, s0):
         assert torch.allclose(a, b, rtol=1e-3, atol=1e-4)
+
+
+def test_mnist_cnn_padded_arena_matches_fp32_cpu():
+    """The reference's MNIST CNN (``ddl_mnist_aztk.py:180-192``: 1-channel input, Dense(225), Dense(10))
+    on the GPU keeps its odd-width weights in zero-padded arena storage (params.py) and passes padded
+    activations / gradients between layers (ops/zpad.py): same loss and parameter gradients as the fp32 CPU
+    model, padding that stays exactly zero through an Adam step, and a training step that launches no
+    ATen kernel besides the eager step's gradient zero-fill and the loss read-back."""
+    from distributeddeeplearningspark_amd.models.zoo import mnist_cnn
+
+    def build(dev):
+        m = mnist_cnn()
+        m.compile("adam", "categorical_crossentropy")
+        m.place(dev, seed=0)
+        return m
+
+    mg, mc = build(DEV), build("cpu")
+    padded = [p for p in mg.arena.params if p.padded]
+    assert len(padded) == 5, padded  # conv1 kernel (1 -> 8 channels), both Dense kernels and biases
+    g = torch.Generator().manual_seed(3)
+    x = torch.rand(16, 28, 28, 1, generator=g)
+    y = F.one_hot(torch.randint(0, 10, (16,), generator=g), 10).float()
+    lg = float(mg.backward_step(mg.to_input(x), mg.to_target(y)))
+    lc = float(mc.backward_step(mc.to_input(x), mc.to_target(y)))
+    assert abs(lg - lc) < 0.02 * abs(lc) + 1e-3, (lg, lc)
+    errs = {}
+    for pg, pc in zip(mg.arena.params, mc.arena.params):
+        a, b = pg.grad.float().cpu(), pc.grad.float()
+        errs[pg.name] = (a - b).norm().item() / max(b.norm().item(), 1e-6)
+    print("relative gradient error vs fp32 CPU:", {k: round(v, 4) for k, v in errs.items()})
+    # bf16 activations / gradients: the first conv's weight gradient sits under the longest bf16 chain (~7 %);
+    # a layout error (a tap or channel misread) would be O(1)
+    assert max(errs.values()) < 0.1, errs
+
+    def pad_max(p, t):
+        m = torch.ones(p.pshape, dtype=torch.bool)
+        m[p.logical] = False
+        return t.detach().float().cpu()[m].abs().max().item()
+
+    for p in padded:
+        assert pad_max(p, p.pgrad) == 0.0 and pad_max(p, p.pmaster) == 0.0, p.name
+    mg.optimizer.step(1.0)
+    for p in padded:
+        assert pad_max(p, p.pmaster) == 0.0 and pad_max(p, p.pdata) == 0.0, p.name
+    xd, yd = mg.to_input(x), mg.to_target(y)
+    mg.train_on_batch(xd, yd)
+    names = _kernel_names(lambda: mg.train_on_batch(xd, yd))
+    aten = sorted(n for n in names if "ddl::" not in n and "Memcpy" not in n and "FillFunctor<float>" not in n)
+    assert not aten, f"ATen kernels in the MNIST step: {aten}"

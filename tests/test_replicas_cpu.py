@@ -5,6 +5,7 @@ steps, then ONE commit over all replicas) must reproduce the multi-process gloo 
 dist-keras trainer: same center to fp32 rounding, same num_updates and per-worker loss histories.
 Shards of unequal size make the last rounds have fewer contributors (zero commits)."""
 import numpy as np
+import torch
 import pytest
 
 from distributeddeeplearningspark_amd.context import SparkSession
@@ -96,3 +97,57 @@ def test_replica_groups_respect_stream_ingest_and_resident_limit(monkeypatch):
     assert tr._replica_devices({**cfg, "ingest": "stream"}, None, Xs, Ys) is None
     monkeypatch.setenv("DDL_RESIDENT_MB", "2")  # the two shards of the group: 2.75 MiB > 2 MiB
     assert tr._replica_devices(cfg, None, Xs, Ys) is None
+
+
+def test_padded_param_storage_bf16_arena():
+    """Bf16 arenas keep odd-width weights in zero-padded storage (params.py): logical views carry the
+    Keras values, the padding is zero in every buffer, and fp32 arenas ignore the request."""
+    import numpy as np
+
+    from distributeddeeplearningspark_amd.models import params as P
+
+    def mk():
+        return [P.Param("d/kernel", (225, 20), P.uniform(0.5), pad=(232, 24)), P.Param("d/bias", (225,), P.ones, pad=(232,)),
+                P.Param("c/kernel", (32, 3, 3, 1), P.uniform(0.5), pad=(32, 3, 3, 8))]
+
+    a16 = P.ParamArena(mk(), "cpu", torch.bfloat16, seed=1)
+    a32 = P.ParamArena(mk(), "cpu", torch.float32, seed=1)
+    for p16, p32 in zip(a16.params, a32.params):
+        assert p16.padded and not p32.padded and p16.pshape == p16.pad and p32.pshape == p32.shape
+        assert p16.master.shape == p16.shape and p16.grad.shape == p16.shape
+        np.testing.assert_array_equal(p16.master.detach().numpy(), p32.master.detach().numpy())
+        m = torch.ones(p16.pshape, dtype=torch.bool)
+        m[p16.logical] = False
+        assert p16.pmaster.detach()[m].abs().max() == 0 and p16.pdata.detach().float()[m].abs().max() == 0
+        assert p16.offset % P.ALIGN == 0
+    assert a16.numel >= sum(p.snumel for p in a16.params) > a32.numel - 3 * P.ALIGN
+
+
+def test_canonical_flat_roundtrip_between_layouts():
+    """get_flat / set_flat speak the canonical (unpadded) layout, so a padded bf16 arena and an fp32 arena
+    exchange weights and optimizer state exactly (worker results, checkpoints, parameter-server traffic)."""
+    from distributeddeeplearningspark_amd.models import optimizers as O
+    from distributeddeeplearningspark_amd.models import params as P
+
+    def mk():
+        return [P.Param("d/kernel", (225, 20), P.uniform(0.5), pad=(232, 24)), P.Param("d/bias", (225,), P.ones, pad=(232,)),
+                P.Param("e/kernel", (10, 225), P.uniform(0.5), pad=(16, 232))]
+
+    a16, a32 = P.ParamArena(mk(), "cpu", torch.bfloat16, seed=1), P.ParamArena(mk(), "cpu", torch.float32, seed=2)
+    assert a16.padded and not a32.padded and a16.canon_numel == a32.numel != a16.numel
+    a32.set_flat(a16.get_flat())
+    torch.testing.assert_close(a32.master, a16.get_flat(), rtol=0, atol=0)
+    a32.master.add_(0.25)
+    a16.set_flat(a32.get_flat())
+    for p16, p32 in zip(a16.params, a32.params):
+        torch.testing.assert_close(p16.master, p32.master, rtol=0, atol=0)
+        m = torch.ones(p16.pshape, dtype=torch.bool)
+        m[p16.logical] = False
+        assert p16.pmaster.detach()[m].abs().max() == 0
+    o16, o32 = O.Adam().bind(a16), O.Adam().bind(a32)
+    for p, co in zip(a32.params, a32.canon_offsets):  # parameter regions (the alignment gaps stay zero)
+        o32.state["m"][co:co + p.numel].uniform_()
+    o16.load_state_dict(o32.state_dict())
+    torch.testing.assert_close(o16.state_dict()["m"], o32.state_dict()["m"], rtol=0, atol=0)
+    with pytest.raises(ValueError):
+        a16.set_flat(a16.master)  # storage layout is not a canonical flat
