@@ -34,7 +34,7 @@ def _resnet50_step(dev, seed=3, det=True, batch=16, noise=0.0):
             loss = m.backward_step(m.to_input(x), m.to_target(y))
             if dev != "cpu":
                 torch.cuda.synchronize()
-            out.append((loss.detach().float().cpu().clone(), m.arena.grad.detach().float().cpu().clone()))
+            out.append((loss.detach().float().cpu().clone(), m.arena.to_canonical(m.arena.grad.detach()).float().cpu().clone()))
     return m, out
 
 
@@ -60,7 +60,7 @@ def _bert_tiny_step(det):
             m._step = 0  # the dropout hashes are seeded from the step counter: same masks both times
             loss = m.backward_step(m.to_input(x), m.to_target(y))
             torch.cuda.synchronize()
-            out.append((loss.detach().float().cpu().clone(), m.arena.grad.detach().float().cpu().clone()))
+            out.append((loss.detach().float().cpu().clone(), m.arena.to_canonical(m.arena.grad.detach()).float().cpu().clone()))
     return out
 
 
@@ -117,10 +117,10 @@ def test_resnet50_full_depth_gradient_direction_per_stage():
     assert torch.equal(gg, gg2)
     assert abs(lg.item() - lc.item()) < 0.04 * max(1.0, abs(lc.item())), (lg, lc)
     stages: dict = {}
-    for p in m_cpu.arena.params:
+    for p, co in zip(m_cpu.arena.params, m_cpu.arena.canon_offsets):  # canonical layout (params.py)
         if not p.trainable:
             continue
-        sl = slice(p.offset, p.offset + p.numel)
+        sl = slice(co, co + p.numel)
         st = stages.setdefault(_stage_of(p.name), ([], [], []))
         st[0].append(gc[sl])
         st[1].append(gg[sl])
@@ -168,15 +168,15 @@ def _resnet50_conditioned(dev, noise=0.0, gamma3=0.1, mutation=None):
                 torch.cuda.synchronize()
     finally:
         FB._TEST_MUTATION = old
-    return m, float(loss.detach()), m.arena.grad.detach().float().cpu().clone()
+    return m, float(loss.detach()), m.arena.to_canonical(m.arena.grad.detach()).float().cpu().clone()
 
 
 def _stage_cosines(m, ga, gb):
     stages: dict = {}
-    for p in m.arena.params:
+    for p, co in zip(m.arena.params, m.arena.canon_offsets):  # canonical layout (params.py)
         if not p.trainable:
             continue
-        sl = slice(p.offset, p.offset + p.numel)
+        sl = slice(co, co + p.numel)
         st = stages.setdefault(_stage_of(p.name), ([], []))
         st[0].append(ga[sl])
         st[1].append(gb[sl])

@@ -559,7 +559,7 @@ def test_fused_bottleneck_matches_composed_ops():
             m.compile("sgd", "sparse_categorical_crossentropy")
             m.place(dev, seed=5)
             loss = m.backward_step(m.to_input(x), m.to_target(y))
-            res[fused + dev] = (float(loss.detach()), m.arena.grad.float().cpu().clone())
+            res[fused + dev] = (float(loss.detach()), m.arena.to_canonical(m.arena.grad.detach()).float().cpu().clone())
         finally:
             RN.FUSED_BLOCKS = old
     l1, l0, lc = res["1" + DEV][0], res["0" + DEV][0], res["0cpu"][0]
@@ -823,7 +823,7 @@ def test_bottleneck_inner_fused_bn_reduce_matches_unfused(monkeypatch):
             loss = m.backward_step(xd, yd)
             torch.cuda.synchronize()
         n_reduce = sum(1 for e in prof.events() if "bn_bwd_reduce" in e.name)
-        out.append((float(loss.detach()), m.arena.grad.float().cpu().clone(), n_reduce))
+        out.append((float(loss.detach()), m.arena.to_canonical(m.arena.grad.detach()).float().cpu().clone(), n_reduce))
     (l0, g0, r0), (l1, g1, r1), (l0b, g0b, _) = out
     assert r1 <= r0 - 2, (r1, r0)
     # the loss is the FORWARD's (both variants run the same forward kernels): its spread is the forward's own
@@ -968,7 +968,7 @@ def test_bottleneck_downsample_bn_fused_matches_unfused(monkeypatch):
                 loss = m.backward_step(xd, yd)
                 torch.cuda.synchronize()
             n_reduce = sum(1 for e in prof.events() if "bn_bwd_reduce" in e.name)
-            out.append((float(loss.detach()), m.arena.grad.float().cpu().clone(), n_reduce))
+            out.append((float(loss.detach()), m.arena.to_canonical(m.arena.grad.detach()).float().cpu().clone(), n_reduce))
     (l0, g0, r0), (l1, g1, r1), (l0b, g0b, _) = out
     assert r1 == r0 - 2, (r1, r0)
     assert l0 == l0b and torch.equal(g0, g0b)  # the reference is reproducible in this mode
@@ -1004,7 +1004,7 @@ def test_bottleneck_chain_fused_bn_reduce_matches_unfused(monkeypatch):
             loss = m.backward_step(xd, yd)
             torch.cuda.synchronize()
         n_reduce = sum(1 for e in prof.events() if "bn_bwd_reduce" in e.name)
-        out.append((float(loss.detach()), m.arena.grad.float().cpu().clone(), n_reduce))
+        out.append((float(loss.detach()), m.arena.to_canonical(m.arena.grad.detach()).float().cpu().clone(), n_reduce))
     (l0, g0, r0), (l1, g1, r1), (l0b, g0b, _) = out
     assert r1 == r0 - 1, (r1, r0)  # block 1's bn3 reduce sweep was absorbed by block 2's conv1 dgrad
     # the loss is the FORWARD's (both variants run the same forward kernels): its spread is the forward's own
@@ -1032,7 +1032,7 @@ def test_stem_pool_fusion_matches_separate_apply_and_pool(monkeypatch):
         m.compile("sgd", "sparse_categorical_crossentropy")
         m.place(DEV, seed=4)
         loss = m.backward_step(m.to_input(x), m.to_target(y))
-        out[fused] = (float(loss), m.arena.grad.float().cpu().clone(),
+        out[fused] = (float(loss), m.arena.to_canonical(m.arena.grad.detach()).float().cpu().clone(),
                       m.stem.bn._states["moving_mean"].float().cpu().clone())
     (l1, g1, r1), (l0, g0, r0) = out["1"], out["0"]
     assert abs(l1 - l0) < 2e-3 * max(1.0, abs(l0)), (l1, l0)

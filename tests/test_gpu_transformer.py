@@ -226,7 +226,7 @@ def test_bert_tiny_gpu_matches_cpu():
         x = m.to_input({"input_ids": ids, "lens": torch.tensor([S, 100], dtype=torch.int32)})
         y = m.to_target({"positions": pos, "labels": labels})
         loss = m.backward_step(x, y)
-        res[dev] = (float(loss), m.arena.grad.detach().float().cpu().clone())
+        res[dev] = (float(loss), m.arena.to_canonical(m.arena.grad.detach()).float().cpu().clone())
     (lc, gc), (lg, gg) = res["cpu"], res[DEV]
     assert abs(lc - lg) < 2e-2 * abs(lc), (lc, lg)
     rel = ((gg - gc).norm() / gc.norm()).item()
@@ -254,7 +254,7 @@ def test_bert_base_layer_shapes_match_fp32_cpu():
         x = m.to_input({"input_ids": ids})
         y = m.to_target({"positions": pos, "labels": labels, "num_masked": B * Pm})
         loss = m.backward_step(x, y)
-        res[dev] = (float(loss.detach()), m.arena.grad.detach().float().cpu().clone(),
+        res[dev] = (float(loss.detach()), m.arena.to_canonical(m.arena.grad.detach()).float().cpu().clone(),
                     {p.name: p.grad.detach().float().cpu().reshape(-1).clone() for p in m.arena.params
                      if p.trainable and len(p.shape) == 2})
     (lc, gc, pc), (lg, gg, pg) = res["cpu"], res[DEV]
