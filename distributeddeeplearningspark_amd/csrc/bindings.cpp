@@ -57,7 +57,8 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
           c10::optional<py::dict> outmap, int64_t b_kdiv, int64_t b_tap_stride,
           c10::optional<at::Tensor> stats, c10::optional<at::Tensor> aux, double drop_p, int64_t drop_seed,
           c10::optional<at::Tensor> resid_mask, c10::optional<at::Tensor> bnr_x, c10::optional<at::Tensor> bnr_mask,
-          c10::optional<at::Tensor> bnr_mean, int64_t rsub_h, int64_t rsub_w, c10::optional<at::Tensor> bnr_scale, c10::optional<at::Tensor> bnr_shift, int64_t split_stride) {
+          c10::optional<at::Tensor> bnr_mean, int64_t rsub_h, int64_t rsub_w, c10::optional<at::Tensor> bnr_scale, c10::optional<at::Tensor> bnr_shift, int64_t split_stride,
+          int64_t zcount, int64_t za, int64_t zb, int64_t zc, int64_t zbias) {
   CHECK_CUDA(a);
   CHECK_CUDA(b);
   CHECK_CUDA(c);
@@ -229,6 +230,20 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
                 "gemm: split-K slabs need EPI_F32, beta = 0 and a workspace of splits x split_stride floats");
     p.split_stride = split_stride;
   }
+  if (zcount > 1) {  // replica batching: z-th operands / output / bias at element offsets z * (za, zb, zc, zbias)
+    TORCH_CHECK(tile >= 0 && tile <= 3 && !stats && !bnr_x && !outmap && !resid && !aux && drop_p == 0.0 &&
+                    split_stride == 0 && relu <= ACT_RELU && za >= 0 && zb >= 0 && zc >= 0 && zbias >= 0,
+                "gemm: replica batching (zcount > 1) runs the 64/128 tiles with at most bias / ReLU / split-K atomics");
+    TORCH_CHECK(za % 8 == 0 && zb % 8 == 0 && (epi == EPI_BF16 ? zc % 8 : zc % 4) == 0 && zbias % 4 == 0,
+                "gemm: replica strides must keep 16-B alignment");
+    TORCH_CHECK(c.numel() >= (zcount - 1) * zc + (M - 1) * ldc + N, "gemm: output too small for zcount replicas");
+    TORCH_CHECK(!bias || bias->numel() >= (zcount - 1) * zbias + N, "gemm: bias too short for zcount replicas");
+    p.zcount = (int)zcount;
+    p.za = za;
+    p.zb = zb;
+    p.zc = zc;
+    p.zbias = zbias;
+  }
   at::DeviceGuard guard(a.device());
   HIP_OK(launch_gemm_bf16(p, (int)epi, (int)tile, cur_stream()));
 }
@@ -295,7 +310,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("resid_mask") = py::none(), py::arg("bnr_x") = py::none(), py::arg("bnr_mask") = py::none(),
         py::arg("bnr_mean") = py::none(), py::arg("rsub_h") = 0, py::arg("rsub_w") = 0,
         py::arg("bnr_scale") = py::none(), py::arg("bnr_shift") = py::none(),
-        py::arg("split_stride") = 0);
+        py::arg("split_stride") = 0, py::arg("zcount") = 1, py::arg("za") = 0, py::arg("zb") = 0, py::arg("zc") = 0,
+        py::arg("zbias") = 0);
   m.def("conv3x3_wgrad", &conv3x3_wgrad, "3x3 stride-1 weight gradient (halo kernel): gw += dW", py::arg("dy"),
         py::arg("x"), py::arg("gw"), py::arg("ws"), py::arg("splits"), py::arg("tpb"), py::arg("pp") = false);
   m.def("conv3x3_wgrad_plan", &conv3x3_wgrad_plan_py,

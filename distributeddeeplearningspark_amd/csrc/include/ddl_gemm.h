@@ -120,6 +120,11 @@ struct GemmParams {
   // c + s * split_stride (elements, ldc unchanged); a reduce pass sums the slabs in split order
   // (slab_reduce: deterministic, and ~4x the store rate of the fp32 atomics it replaces).  0 = off.
   long split_stride;
+  // replica batching (gemm_dma_kernel only): blockIdx.z = z selects operands a + z*za, b + z*zb (bf16
+  // elements), output c + z*zc and bias + z*zbias (elements) — the co-located replicas of one model, each
+  // with its own weights, as ONE launch (parallel/replica_seq.py).  0 / unused when gridDim.z == 1.
+  int zcount;
+  long za, zb, zc, zbias;
 };
 
 enum Activation : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_GELU_BWD = 3 };

@@ -603,7 +603,8 @@ __device__ __forceinline__ void gemm_epilogue_bnr(const GemmParams& p, f32x4 (&a
 // leaves no registers for the pair, 0 -> 24 B scratch and +0.03 ms/step on ResNet-50)
 template <int RM, int RN, int EPI, bool WIDE = true>
 __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[RM][RN], const int mb, const int nb,
-                                              const int lane, const int bid, int mend = -1, long coff = 0) {
+                                              const int lane, const int bid, int mend = -1, long coff = 0,
+                                              long boff = 0) {
   const int mlim = mend < 0 ? p.M : mend;
   if constexpr (EPI == EPI_BF16_BNR) {
     gemm_epilogue_bnr<RM, RN>(p, acc, mb, nb, lane, bid, mlim);
@@ -659,14 +660,14 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
   for (int j = 0; j < RN; ++j) {
     const int n = nb + 16 * j + ncol;
     if (p.bias && n + 3 < p.N) {
-      const float4 bv = *reinterpret_cast<const float4*>(p.bias + n);
+      const float4 bv = *reinterpret_cast<const float4*>(p.bias + boff + n);
       bias_r[j][0] = bv.x;
       bias_r[j][1] = bv.y;
       bias_r[j][2] = bv.z;
       bias_r[j][3] = bv.w;
     } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) bias_r[j][e] = (p.bias && n + e < p.N) ? p.bias[n + e] : 0.f;
+      for (int e = 0; e < 4; ++e) bias_r[j][e] = (p.bias && n + e < p.N) ? p.bias[boff + n + e] : 0.f;
     }
   }
 #pragma unroll
@@ -771,13 +772,13 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
           s1[j][e] += rr;
           s2[j][e] += rr * rr;
         }
-        bf16_t* c = reinterpret_cast<bf16_t*>(p.c) + rowoff + n;
+        bf16_t* c = reinterpret_cast<bf16_t*>(p.c) + coff + rowoff + n;
         pk[j] = make_uint2((uint32_t)o[0] | ((uint32_t)o[1] << 16), (uint32_t)o[2] | ((uint32_t)o[3] << 16));
         if (wide_ok && (j & 1) == 0 && j + 1 < RN && nb + 16 * j + 32 <= p.N) {
           // stored with fragment j + 1 below
         } else if (wide_ok && (j & 1) == 1 && nb + 16 * j + 16 <= p.N) {
           // pair (j - 1, j), wave-uniform condition (pair_store)
-          pair_store(reinterpret_cast<bf16_t*>(p.c) + rowoff + nb + 16 * (j - 1), pk[j - 1], pk[j], lane);
+          pair_store(reinterpret_cast<bf16_t*>(p.c) + coff + rowoff + nb + 16 * (j - 1), pk[j - 1], pk[j], lane);
         } else if (full) {
           *reinterpret_cast<uint2*>(c) = pk[j];
         } else {
@@ -786,7 +787,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
             if (n + e < p.N) c[e] = o[e];
         }
       } else if constexpr (EPI == EPI_F32) {
-        float* c = reinterpret_cast<float*>(p.c) + rowoff + n;
+        float* c = reinterpret_cast<float*>(p.c) + coff + rowoff + n;
         if (full && p.beta == 0.f) {
           *reinterpret_cast<float4*>(c) = make_float4(v[0], v[1], v[2], v[3]);
         } else {
@@ -795,7 +796,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
             if (n + e < p.N) c[e] = (p.beta != 0.f) ? v[e] + p.beta * c[e] : v[e];
         }
       } else {
-        float* c = reinterpret_cast<float*>(p.c) + rowoff + n;
+        float* c = reinterpret_cast<float*>(p.c) + coff + rowoff + n;
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           if (n + e < p.N) atomicAdd(c + e, v[e]);
@@ -885,8 +886,10 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
     A.tt = (const DDL_LDS int*)(smem_raw);
     B.tt = (const DDL_LDS int*)(smem_raw);
   }
-  A.init(p.a, p.lda, p.M, m0, p.K, p.g, kbeg);
-  B.init(p.b, p.ldb, p.N, n0, p.K, p.g, kbeg);
+  const long zi = blockIdx.z;  // replica of a batched launch (GemmParams::zcount), 0 otherwise
+  A.init(reinterpret_cast<const bf16_t*>(p.a) + zi * p.za, p.lda, p.M, m0, p.K, p.g, kbeg);
+  B.init(reinterpret_cast<const bf16_t*>(p.b) + zi * p.zb, p.ldb, p.N, n0, p.K, p.g, kbeg);
+  const long zc = (long)split * p.split_stride + zi * p.zc, zb = zi * p.zbias;
   static_assert(ST == 1 || ST == 3, "stages: 1 or a 3-slot ring");
   auto bfrag = [&](const char* lb, int kk, int j) { return B.frag(lb, kk, j, wn0, lane); };
 
@@ -944,8 +947,7 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
       }
       slot = slot + 1 == ST ? 0 : slot + 1;
     }
-    gemm_epilogue<RM, RN, EPI, (AMODE == OP_KC || AMODE == OP_RC)>(p, acc, m0 + wm0, n0 + wn0, lane, bid, -1,
-                                                                  (long)split * p.split_stride);
+    gemm_epilogue<RM, RN, EPI, (AMODE == OP_KC || AMODE == OP_RC)>(p, acc, m0 + wm0, n0 + wn0, lane, bid, -1, zc, zb);
     return;
   }
   if (nk > 0) {
@@ -982,8 +984,7 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
     }
   }
 
-  gemm_epilogue<RM, RN, EPI, (AMODE == OP_KC || AMODE == OP_RC)>(p, acc, m0 + wm0, n0 + wn0, lane, bid, -1,
-                                                                  (long)split * p.split_stride);
+  gemm_epilogue<RM, RN, EPI, (AMODE == OP_KC || AMODE == OP_RC)>(p, acc, m0 + wm0, n0 + wn0, lane, bid, -1, zc, zb);
 }
 
 inline int device_cus() {
@@ -1000,7 +1001,7 @@ template <int BM, int BN, int AMODE, int BMODE, int EPI>
 inline int launch_tile(const GemmParams& p, hipStream_t s) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
   const int splits = (p.K + p.k_split - 1) / p.k_split;
-  const dim3 grid(tiles, splits > 0 ? splits : 1);
+  const dim3 grid(tiles, splits > 0 ? splits : 1, p.zcount > 1 ? p.zcount : 1);
   constexpr int TAPB = tap_table_bytes<AMODE, BMODE>();
   if constexpr (AMODE == OP_RC && BMODE == OP_RC && BM * BN < 128 * 128 && (EPI == EPI_F32 || EPI == EPI_F32_ATOMIC)) {
     // the 3-slot ring for plain (1x1 / Linear) weight gradients on 64x128 / 128x64 tiles (72 KB: 2 workgroups

@@ -26,7 +26,8 @@ constexpr int kMaxPartials = 512;  // partial rows of a column-reduction sweep
 //   * bn_stats / bn_bwd_reduce sweeps: S = bn_partial_rows(M, C), every row written (no zeroing).
 int bn_partial_rows(long M, int C);
 int splitk_finalize(float* ws, void* y, const float* bias, float* stats, long M, int C, int relu, int splits,
-                    long slab_stride, hipStream_t s);  // splits > 0: ws = `splits` slabs slab_stride floats apart
+                    long slab_stride, hipStream_t s, long brows = 0,
+                    long zbias = 0);  // splits > 0: ws = `splits` slabs slab_stride floats apart
 int bn_stats(const void* x, float* ws, long M, int C, hipStream_t s);
 // ws -> mean/invstd (saved for backward), scale/shift for apply, running stats update
 int bn_finalize(const float* ws, int S, long M, int C, const float* gamma, const float* beta, float eps,
@@ -72,7 +73,7 @@ int avgpool_global_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream
 int softmax_xent(const void* logits, int logits_bf16, const int64_t* labels, const float* target_probs,
                  float* loss_rows, void* dlogits, int B, int K, long ld, float grad_scale, float label_smoothing,
                  int ignore_index, hipStream_t s, const float* grad_scale_dev = nullptr, float* loss_out = nullptr,
-                 float out_scale = 1.f);
+                 float out_scale = 1.f, int zrows = 0);
 int label_count_inv(const int64_t* labels, long n, int ignore_index, float* inv, hipStream_t s);
 int rows_sum_scaled(const float* rows, long n, float scale, const float* dev, float* out, hipStream_t s);
 int scale_bf16_dev(void* x, long n, const float* s_dev, hipStream_t s);
@@ -90,8 +91,9 @@ int relu_bwd(const void* dy, const void* y, void* dx, long n, hipStream_t s);
 int add_bf16(const void* a, const void* b, void* y, long n, hipStream_t s);
 // db[n] (+)= sum_m dy[m][n]; deterministic mode: det_ws (bias_grad_rows(M) x N floats) holds per-workgroup
 // partial rows summed in order by colsum_partials (without it: one workgroup per column block)
+// zcount > 1: replica-batched, dy = zcount stacked [M][N] blocks, db of block z at db + z * zdb
 int bias_grad(const void* dy, float* db, long M, int N, int accumulate, hipStream_t s, float* det_ws = nullptr,
-              const void* relu_y = nullptr, void* relu_dx = nullptr);
+              const void* relu_y = nullptr, void* relu_dx = nullptr, int zcount = 1, long zdb = 0);
 // zero-padded [R][Kp] copy of a row-strided [R][K] bf16 view
 int pad_cols_bf16(const void* x, long ldx, void* out, long R, int K, int Kp, hipStream_t s);
 int bias_grad_rows(long M);
@@ -260,7 +262,7 @@ int embedding_scatter(const int64_t* ids, const void* dy, float* gw, long n, int
 constexpr int kMaxFilterTaps = 64;
 struct FilterTaps { int16_t t[kMaxFilterTaps]; };
 int filter_taps_transpose(const void* w, void* out, int Co, int T, int Ci, const FilterTaps& taps, int nt,
-                          hipStream_t s);
+                          hipStream_t s, int zcount = 1, long zw = 0, long zo = 0);
 // y[C][R] = x[R][C] (fp32)
 int transpose_f32(const float* x, float* y, int R, int C, hipStream_t s);
 // db[n] += sum_m dy[m][n] (fp32, dense rows of N)
@@ -303,7 +305,7 @@ struct ReplicaPtrs {
 };
 int commit_replicas(const ReplicaPtrs& rp, int nr, float* center, float* sum, long n, int elastic, int mode,
                     hipStream_t s);
-constexpr int kMaxBatchCopies = 4;
+constexpr int kMaxBatchCopies = 16;  // 2 per replica of a batched group (parallel/replica_seq.py)
 struct BatchCopy {
   const void* src[kMaxBatchCopies];
   void* dst[kMaxBatchCopies];
@@ -311,6 +313,6 @@ struct BatchCopy {
   long nbatch;                  // mini-batches per epoch
 };
 int batch_fetch(const BatchCopy& bc, int ncopy, const int* ctr, hipStream_t s);
-int step_record(const float* loss, float* hist, int cap, int* ctr, hipStream_t s);
+int step_record(const float* loss, float* hist, int cap, int* ctr, hipStream_t s, int nrep = 1);
 
 }  // namespace ddl

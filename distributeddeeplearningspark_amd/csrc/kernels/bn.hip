@@ -112,9 +112,11 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const uint4* __restrict__
 // block % kStatShards).  Convolutions whose output tiles cannot fill the chip (VGG / ResNet layers
 // at 2x2-4x4 spatial) run their K loop split over workgroups into an fp32 workspace; this pass
 // completes them with the epilogue the un-split GEMM would have applied.
+// brows > 0: replica-batched rows — row r adds bias + (r / brows) * zbias (each replica's own bias)
 __global__ __launch_bounds__(256) void splitk_finalize_kernel(float4* __restrict__ ws, uint4* __restrict__ y,
                                                               const float* __restrict__ bias, float* stats, long M,
-                                                              int C, int relu, int splits, long slab_stride) {
+                                                              int C, int relu, int splits, long slab_stride,
+                                                              long brows, long zbias) {
   ColGeom g(C);
   float acc[16];
 #pragma unroll
@@ -128,6 +130,12 @@ __global__ __launch_bounds__(256) void splitk_finalize_kernel(float4* __restrict
     const long step = (long)gridDim.x * g.RT;
     for (long r = (long)blockIdx.x * g.RT + g.rt; r < M; r += step) {
       const long idx = r * g.CV + g.cv;
+      if (brows > 0 && bias) {
+        const float4* bz = reinterpret_cast<const float4*>(bias + (r / brows) * zbias);
+        const float4 c0 = bz[2 * g.cv], c1 = bz[2 * g.cv + 1];
+        b[0] = c0.x; b[1] = c0.y; b[2] = c0.z; b[3] = c0.w;
+        b[4] = c1.x; b[5] = c1.y; b[6] = c1.z; b[7] = c1.w;
+      }
       float4 u = ws[2 * idx], v = ws[2 * idx + 1];
       if (splits > 0) {
         const long st4 = slab_stride >> 2;
@@ -182,13 +190,14 @@ __global__ __launch_bounds__(256) void splitk_finalize_kernel(float4* __restrict
 }
 
 int splitk_finalize(float* ws, void* y, const float* bias, float* stats, long M, int C, int relu, int splits,
-                    long slab_stride, hipStream_t s) {
+                    long slab_stride, hipStream_t s, long brows, long zbias) {
+  if (brows > 0 && (stats || zbias % 4)) return (int)hipErrorInvalidValue;
   const int CV = C >> 3, CT = CV < 256 ? CV : 256, RT = 256 / CT;
   const int gy = (CV + CT - 1) / CT;
   long gx = (M + 4 * RT - 1) / (4 * RT);  // >= 4 rows per lane
   if (gx > 1024) gx = 1024;
   hipLaunchKernelGGL(splitk_finalize_kernel, dim3((unsigned)(gx > 0 ? gx : 1), (unsigned)gy), dim3(256), 0, s,
-                     (float4*)ws, (uint4*)y, bias, stats, M, C, relu, splits, slab_stride);
+                     (float4*)ws, (uint4*)y, bias, stats, M, C, relu, splits, slab_stride, brows, zbias);
   return (int)hipGetLastError();
 }
 

@@ -169,11 +169,14 @@ __global__ __launch_bounds__(256) void embedding_scatter_kernel(const int64_t* _
 // in ONE pass (replaces flip + permute-copy / index_select + permute-copy: 2-3 ATen launches per
 // conv per step).  32x32 (co, ci) tiles through LDS so both the read (ci) and the write (co) are
 // contiguous; blockIdx.z = output tap.
+// blockIdx.z = replica * nt + tap (replica batching: filters every zw, outputs every zo elements)
 __global__ __launch_bounds__(256) void filter_taps_transpose_kernel(const bf16_t* __restrict__ w,
                                                                     bf16_t* __restrict__ out, int Co, int T,
-                                                                    int Ci, int nt, FilterTaps taps) {
+                                                                    int Ci, int nt, FilterTaps taps, long zw, long zo) {
   __shared__ bf16_t tile[32][33];
-  const int t = blockIdx.z, src_t = taps.t[t];
+  const int zr = blockIdx.z / nt, t = blockIdx.z - zr * nt, src_t = taps.t[t];
+  w += zr * zw;
+  out += zr * zo;
   const int co0 = blockIdx.y * 32, ci0 = blockIdx.x * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   for (int i = ty; i < 32; i += 8) {
@@ -286,11 +289,11 @@ int avgpool2d_bwd(const void* dy, void* dx, int N, int H, int W, int C, int Ho, 
 }
 
 int filter_taps_transpose(const void* w, void* out, int Co, int T, int Ci, const FilterTaps& taps, int nt,
-                          hipStream_t s) {
-  if (nt <= 0 || nt > kMaxFilterTaps || Co <= 0 || Ci <= 0) return (int)hipErrorInvalidValue;
-  const dim3 grid((Ci + 31) / 32, (Co + 31) / 32, nt);
+                          hipStream_t s, int zcount, long zw, long zo) {
+  if (nt <= 0 || nt > kMaxFilterTaps || Co <= 0 || Ci <= 0 || zcount < 1) return (int)hipErrorInvalidValue;
+  const dim3 grid((Ci + 31) / 32, (Co + 31) / 32, nt * zcount);
   hipLaunchKernelGGL(filter_taps_transpose_kernel, grid, dim3(256), 0, s, (const bf16_t*)w, (bf16_t*)out, Co, T, Ci,
-                     nt, taps);
+                     nt, taps, zw, zo);
   return (int)hipGetLastError();
 }
 

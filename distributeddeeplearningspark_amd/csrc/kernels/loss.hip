@@ -140,10 +140,16 @@ __global__ __launch_bounds__(1024) void softmax_xent_small_kernel(const void* __
                                                                    void* dlogits, int K, long ld, float gscale,
                                                                    float smooth, int ignore_index,
                                                                    const float* __restrict__ gscale_dev, int B,
-                                                                   float* __restrict__ loss_out, float out_scale) {
+                                                                   float* __restrict__ loss_out, float out_scale,
+                                                                   int zrows) {
+  // zrows > 0 (replica batching): rows [z * zrows, (z + 1) * zrows) belong to replica z, whose loss goes
+  // to loss_out[z] (B / zrows <= 64 replicas)
   if (gscale_dev) gscale *= gscale_dev[0];
   __shared__ float part[16];
+  __shared__ float rep[64];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (zrows > 0 && threadIdx.x < 64) rep[threadIdx.x] = 0.f;
+  if (zrows > 0) __syncthreads();
   float total = 0.f;
   const float off = smooth / (float)K;
   for (int b = wid; b < B; b += 16) {
@@ -178,8 +184,15 @@ __global__ __launch_bounds__(1024) void softmax_xent_small_kernel(const void* __
     lpart = warp_sum(lpart);
     if (lane == 0) {
       if (loss_rows) loss_rows[b] = lpart;
+      if (zrows > 0) atomicAdd(&rep[b / zrows], lpart);
       total += lpart;
     }
+  }
+  if (zrows > 0) {
+    __syncthreads();
+    const int nz = (B + zrows - 1) / zrows;
+    if (threadIdx.x < nz) loss_out[threadIdx.x] = rep[threadIdx.x] * out_scale * (gscale_dev ? gscale_dev[0] : 1.f);
+    return;
   }
   if (lane == 0) part[wid] = total;
   __syncthreads();
@@ -192,17 +205,19 @@ __global__ __launch_bounds__(1024) void softmax_xent_small_kernel(const void* __
 
 int softmax_xent(const void* logits, int logits_bf16, const int64_t* labels, const float* target_probs,
                  float* loss_rows, void* dlogits, int B, int K, long ld, float grad_scale, float label_smoothing,
-                 int ignore_index, hipStream_t s, const float* grad_scale_dev, float* loss_out, float out_scale) {
+                 int ignore_index, hipStream_t s, const float* grad_scale_dev, float* loss_out, float out_scale,
+                 int zrows) {
   if (B <= 0) return 0;
+  if (zrows > 0 && (!loss_out || (B + zrows - 1) / zrows > 64)) return (int)hipErrorInvalidValue;
   if (loss_out) {  // small batch: one workgroup, a wave per row, the reduced loss written in place
     if (logits_bf16)
       hipLaunchKernelGGL(softmax_xent_small_kernel<true>, dim3(1), dim3(1024), 0, s, logits, labels, target_probs,
                          loss_rows, dlogits, K, ld, grad_scale, label_smoothing, ignore_index, grad_scale_dev, B,
-                         loss_out, out_scale);
+                         loss_out, out_scale, zrows);
     else
       hipLaunchKernelGGL(softmax_xent_small_kernel<false>, dim3(1), dim3(1024), 0, s, logits, labels, target_probs,
                          loss_rows, dlogits, K, ld, grad_scale, label_smoothing, ignore_index, grad_scale_dev, B,
-                         loss_out, out_scale);
+                         loss_out, out_scale, zrows);
     return (int)hipGetLastError();
   }
   if (!loss_rows) return (int)hipErrorInvalidValue;

@@ -158,10 +158,20 @@ __global__ void bias_grad_kernel(const bf16_t* dy, float* db, long M, int N) {
 // instead of adding them into db; colsum_partials then sums the rows in index order, one writer per column
 // ry != nullptr: the ReLU backward is fused in: dy is masked by ry > 0, the masked rows are stored to rdx
 // and summed (a Dense / Conv2D with a fused ReLU: one sweep instead of relu_bwd + bias_grad)
+// blockIdx.z = replica z of a batched launch: rows z*M.. of dy / ry / rdx, db + z * zdb
 __global__ __launch_bounds__(256) void bias_grad_vec_kernel(const bf16_t* dy, float* db, long M, int N, float* pout,
                                                             const bf16_t* __restrict__ ry = nullptr,
-                                                            bf16_t* __restrict__ rdx = nullptr) {
+                                                            bf16_t* __restrict__ rdx = nullptr, long zdb = 0) {
   __shared__ float part[8][257];
+  if (blockIdx.z) {
+    const long zr = (long)blockIdx.z * M * N;
+    dy += zr;
+    db += (long)blockIdx.z * zdb;
+    if (ry) {
+      ry += zr;
+      rdx += zr;
+    }
+  }
   const int cg = threadIdx.x & 31, rl = threadIdx.x >> 5;
   const int n0 = blockIdx.x * 256 + cg * 8;
   float acc[8];
@@ -266,7 +276,15 @@ int bias_grad_rows(long M) {
 }
 
 int bias_grad(const void* dy, float* db, long M, int N, int accumulate, hipStream_t s, float* det_ws, const void* ry,
-              void* rdx) {
+              void* rdx, int zcount, long zdb) {
+  if (zcount > 1) {  // replica-batched: the vector kernel, accumulate, non-deterministic form only
+    if (!accumulate || det_ws || deterministic() || N % 8 || (reinterpret_cast<uintptr_t>(dy) & 15) || zdb % 4)
+      return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(bias_grad_vec_kernel, dim3((N + 255) / 256, (unsigned)bias_grad_rows(M), (unsigned)zcount),
+                       dim3(256), 0, s, (const bf16_t*)dy, db, M, N, (float*)nullptr, (const bf16_t*)ry, (bf16_t*)rdx,
+                       zdb);
+    return (int)hipGetLastError();
+  }
   if (!accumulate) hipMemsetAsync(db, 0, sizeof(float) * N, s);
   long ys = bias_grad_rows(M);
   const bool vec = N % 8 == 0 && (reinterpret_cast<uintptr_t>(dy) & 15) == 0;

@@ -102,10 +102,13 @@ __global__ __launch_bounds__(256) void batch_fetch_kernel(BatchCopy bc, int ncop
 }
 
 // hist[ctr] = loss (while ctr < cap); ctr += 1 — one lane, vector memory only
-__global__ void step_record_kernel(const float* __restrict__ loss, float* __restrict__ hist, int cap, int* ctr) {
+// nrep replicas (replica batching): loss[r] -> hist[r * cap + step], one shared step counter
+__global__ void step_record_kernel(const float* __restrict__ loss, float* __restrict__ hist, int cap, int* ctr,
+                                   int nrep) {
   if (threadIdx.x == 0) {
     const int c = *ctr;
-    if (hist && c < cap) hist[c] = *loss;
+    if (hist && c < cap)
+      for (int r = 0; r < nrep; ++r) hist[(long)r * cap + c] = loss[r];
     *ctr = c + 1;
   }
 }
@@ -131,8 +134,9 @@ int batch_fetch(const BatchCopy& bc, int ncopy, const int* ctr, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-int step_record(const float* loss, float* hist, int cap, int* ctr, hipStream_t s) {
-  hipLaunchKernelGGL(step_record_kernel, dim3(1), dim3(64), 0, s, loss, hist, cap, ctr);
+int step_record(const float* loss, float* hist, int cap, int* ctr, hipStream_t s, int nrep) {
+  if (nrep < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(step_record_kernel, dim3(1), dim3(64), 0, s, loss, hist, cap, ctr, nrep);
   return (int)hipGetLastError();
 }
 

@@ -164,20 +164,26 @@ void embedding_bwd_(const at::Tensor& ids, const at::Tensor& dy, const at::Tenso
 }
 
 // out [Ci][nt][Co] = w [Co][T][Ci] gathered at the given taps
-void filter_taps_transpose_(const at::Tensor& w, const at::Tensor& out, std::vector<int64_t> taps) {
+// zcount > 1 (replica batching): zcount filters every zw elements from w's storage, outputs [zcount][Ci][nt][Co]
+void filter_taps_transpose_(const at::Tensor& w, const at::Tensor& out, std::vector<int64_t> taps, int64_t zcount,
+                            int64_t zw) {
   CK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.dim() == 4,
      "filter_taps_transpose: w [Co][KH][KW][Ci] contiguous bf16");
   const int64_t Co = w.size(0), T = w.size(1) * w.size(2), Ci = w.size(3), nt = (int64_t)taps.size();
   CK(nt >= 1 && nt <= kMaxFilterTaps, "filter_taps_transpose: 1..64 taps");
-  CK(out.is_cuda() && out.scalar_type() == at::kBFloat16 && out.is_contiguous() && out.numel() == Ci * nt * Co,
-     "filter_taps_transpose: out [Ci][nt][Co] contiguous bf16");
+  CK(out.is_cuda() && out.scalar_type() == at::kBFloat16 && out.is_contiguous() && out.numel() == zcount * Ci * nt * Co,
+     "filter_taps_transpose: out [zcount][Ci][nt][Co] contiguous bf16");
+  CK(zcount == 1 || (zw >= Co * T * Ci && w.storage_offset() * 2 + (zcount - 1) * zw * 2 + Co * T * Ci * 2 <=
+                                              (int64_t)w.storage().nbytes()),
+     "filter_taps_transpose: zcount filters every zw elements must lie inside w's storage");
   FilterTaps ft{};
   for (int64_t i = 0; i < nt; ++i) {
     CK(taps[i] >= 0 && taps[i] < T, "filter_taps_transpose: tap out of range");
     ft.t[i] = (int16_t)taps[i];
   }
   at::DeviceGuard g(w.device());
-  HIP_OK(filter_taps_transpose(w.data_ptr(), out.data_ptr(), (int)Co, (int)T, (int)Ci, ft, (int)nt, cur_stream()));
+  HIP_OK(filter_taps_transpose(w.data_ptr(), out.data_ptr(), (int)Co, (int)T, (int)Ci, ft, (int)nt, cur_stream(),
+                               (int)zcount, (long)zw, (long)(Ci * nt * Co)));
 }
 
 }  // namespace
@@ -196,7 +202,8 @@ void register_layer_ops(py::module& m) {
         py::arg("K"), py::arg("alpha") = 1.0, py::arg("beta") = 0.0, py::arg("bias") = py::none(),
         py::arg("relu") = false);
   m.def("transpose_f32", &transpose_f32_, "y = x^T (fp32)");
-  m.def("filter_taps_transpose", &filter_taps_transpose_, "conv dgrad filter: out[ci][t][co] = w[co][taps[t]][ci]");
+  m.def("filter_taps_transpose", &filter_taps_transpose_, "conv dgrad filter: out[ci][t][co] = w[co][taps[t]][ci]",
+        py::arg("w"), py::arg("out"), py::arg("taps"), py::arg("zcount") = 1, py::arg("zw") = 0);
   m.def("embedding_fwd", &embedding_fwd_, "Keras Embedding gather (bf16/fp32 table)");
   m.def("embedding_bwd", &embedding_bwd_, "Keras Embedding gradient scatter-add into fp32");
   m.attr("ACT_CODES") = py::dict(py::arg("linear") = (int)ACT_C_LINEAR, py::arg("relu") = (int)ACT_C_RELU,

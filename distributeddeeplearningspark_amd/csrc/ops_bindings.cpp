@@ -38,17 +38,22 @@ void bn_stats_(const at::Tensor& x, const at::Tensor& ws, int64_t C) {
 }
 
 void splitk_finalize_(const at::Tensor& ws, const at::Tensor& y, int64_t C, c10::optional<at::Tensor> bias, bool relu,
-                      c10::optional<at::Tensor> stats, int64_t splits) {
+                      c10::optional<at::Tensor> stats, int64_t splits, int64_t brows, int64_t zbias) {
   GPU(ws); F32(ws); BF16(y);
   CK(C % 8 == 0 && y.numel() % C == 0 && y.is_contiguous() && ws.is_contiguous(), "splitk_finalize: shapes");
   // splits == 0: ws is the [M, C] atomic accumulator (zeroed again); splits > 0: `splits` [M, C] slabs
   CK(splits >= 0 && ws.numel() >= std::max<int64_t>(splits, 1) * y.numel() && (splits > 0 || ws.numel() == y.numel()),
      "splitk_finalize: workspace size");
-  if (bias) { F32(*bias); CK(bias->numel() == C, "splitk_finalize: bias [C]"); }
+  // brows > 0 (replica batching): rows r use bias + (r / brows) * zbias
+  if (bias) {
+    F32(*bias);
+    CK(brows > 0 ? (zbias % 4 == 0 && bias->numel() >= ((y.numel() / C - 1) / brows) * zbias + C) : bias->numel() == C,
+       "splitk_finalize: bias [C] (or per-replica biases every zbias elements)");
+  }
   if (stats) { F32(*stats); CK(stats->numel() == (int64_t)kBnShards * 2 * C, "splitk_finalize: stats [32, 2, C]"); }
   at::DeviceGuard g(ws.device());
   HIP_OK(splitk_finalize(ws.data_ptr<float>(), y.data_ptr(), optr<const float>(bias), optr<float>(stats), y.numel() / C,
-                         (int)C, relu ? 1 : 0, (int)splits, (long)y.numel(), cur_stream()));
+                         (int)C, relu ? 1 : 0, (int)splits, (long)y.numel(), cur_stream(), (long)brows, (long)zbias));
 }
 
 int64_t bn_partial_rows_(int64_t M, int64_t C) { return bn_partial_rows(M, (int)C); }
@@ -239,7 +244,7 @@ void avgpool_bwd_(const at::Tensor& dy, const at::Tensor& dx) {
 void softmax_xent_(const at::Tensor& logits, c10::optional<at::Tensor> labels, c10::optional<at::Tensor> probs,
                    c10::optional<at::Tensor> loss_rows, c10::optional<at::Tensor> dlogits, double grad_scale, double smoothing,
                    int64_t ignore_index, c10::optional<at::Tensor> grad_scale_dev, c10::optional<at::Tensor> loss_out,
-                   double out_scale) {
+                   double out_scale, int64_t zrows) {
   GPU(logits);
   CK(logits.dim() == 2 && logits.stride(1) == 1 && logits.stride(0) >= logits.size(1),
      "softmax_xent: logits [B,K] with unit column stride");
@@ -248,7 +253,10 @@ void softmax_xent_(const at::Tensor& logits, c10::optional<at::Tensor> labels, c
   const int B = logits.size(0), K = logits.size(1);
   CK(loss_rows.has_value() || loss_out.has_value(), "softmax_xent: loss_rows and/or loss_out");
   if (loss_rows) { F32(*loss_rows); CK(loss_rows->numel() == B, "loss_rows size"); }
-  if (loss_out) { F32(*loss_out); CK(loss_out->numel() == 1 && B <= 4096, "softmax_xent: loss_out [1], B <= 4096 (one workgroup)"); }
+  // zrows > 0 (replica batching): loss_out[z] = the loss of rows [z * zrows, (z + 1) * zrows)
+  const int64_t nz = zrows > 0 ? (B + zrows - 1) / zrows : 1;
+  if (loss_out) { F32(*loss_out); CK(loss_out->numel() == nz && nz <= 64 && B <= 4096, "softmax_xent: loss_out [B / zrows <= 64], B <= 4096 (one workgroup)"); }
+  CK(zrows == 0 || loss_out.has_value(), "softmax_xent: zrows needs loss_out");
   CK((labels.has_value()) != (probs.has_value()), "exactly one of labels/probs");
   if (labels) CK(labels->scalar_type() == at::kLong && labels->numel() == B, "labels int64 [B]");
   if (probs) { F32(*probs); CK(probs->numel() == (int64_t)B * K, "probs [B,K]"); }
@@ -262,7 +270,7 @@ void softmax_xent_(const at::Tensor& logits, c10::optional<at::Tensor> labels, c
   HIP_OK(softmax_xent(logits.data_ptr(), bf ? 1 : 0, optr<const int64_t>(labels), optr<const float>(probs),
                       optr<float>(loss_rows), optr<void>(dlogits), B, K, ld, (float)grad_scale, (float)smoothing,
                       (int)ignore_index, cur_stream(), optr<const float>(grad_scale_dev), optr<float>(loss_out),
-                      (float)out_scale));
+                      (float)out_scale, (int)zrows));
 }
 
 void label_count_inv_(const at::Tensor& labels, int64_t ignore_index, const at::Tensor& inv) {
@@ -332,9 +340,9 @@ void transpose_bf16_(const at::Tensor& x, const at::Tensor& y) {
 }
 // relu_y / relu_dx: fused ReLU backward (relu_dx = dy * (relu_y > 0), and db sums relu_dx); N % 8 == 0 only
 void bias_grad_(const at::Tensor& dy, const at::Tensor& db, int64_t N, bool accumulate, c10::optional<at::Tensor> relu_y,
-                c10::optional<at::Tensor> relu_dx) {
+                c10::optional<at::Tensor> relu_dx, int64_t zcount, int64_t zdb) {
   GPU(dy); BF16(dy); F32(db);
-  CK(dy.numel() % N == 0 && db.numel() >= N, "bias_grad: shapes");
+  CK(zcount >= 1 && dy.numel() % (N * zcount) == 0 && db.numel() >= (zcount - 1) * zdb + N, "bias_grad: shapes");
   // the kernels read dy as a dense [M][N] array (row stride N, 16-B vectors): no strided views
   CK(dy.is_contiguous() && db.is_contiguous(), "bias_grad: dy and db must be contiguous");
   CK(relu_y.has_value() == relu_dx.has_value(), "bias_grad: relu_y and relu_dx together");
@@ -344,12 +352,12 @@ void bias_grad_(const at::Tensor& dy, const at::Tensor& db, int64_t N, bool accu
            relu_dx->numel() == dy.numel(), "bias_grad: fused ReLU needs N % 8 == 0 and dense y / dx like dy");
   }
   at::DeviceGuard g(dy.device());
-  const long M = dy.numel() / N;
+  const long M = dy.numel() / N / zcount;
   at::Tensor ws;  // deterministic mode: partial rows from the caching allocator (stream-ordered)
-  if (deterministic()) ws = at::empty({(int64_t)bias_grad_rows(M) * N}, dy.options().dtype(at::kFloat));
+  if (deterministic() && zcount == 1) ws = at::empty({(int64_t)bias_grad_rows(M) * N}, dy.options().dtype(at::kFloat));
   HIP_OK(bias_grad(dy.data_ptr(), db.data_ptr<float>(), M, (int)N, accumulate ? 1 : 0, cur_stream(),
                    ws.defined() ? ws.data_ptr<float>() : nullptr, relu_y ? relu_y->data_ptr() : nullptr,
-                   relu_dx ? relu_dx->data_ptr() : nullptr));
+                   relu_dx ? relu_dx->data_ptr() : nullptr, (int)zcount, (long)zdb));
 }
 void pad_cols_bf16_(const at::Tensor& x, const at::Tensor& out) {
   GPU(x); BF16(x); BF16(out);
@@ -483,7 +491,7 @@ void commit_replicas_(const std::vector<at::Tensor>& ws, const std::vector<c10::
 // copies mini-batch (ctr % nbatch) of each resident shard srcs[q] ([nbatch * rows, ...]) into dsts[q]
 void batch_fetch_(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts, const at::Tensor& ctr,
                   int64_t nbatch) {
-  CK(!srcs.empty() && srcs.size() <= (size_t)kMaxBatchCopies && dsts.size() == srcs.size(), "batch_fetch: 1..4 copies");
+  CK(!srcs.empty() && srcs.size() <= (size_t)kMaxBatchCopies && dsts.size() == srcs.size(), "batch_fetch: 1..16 copies");
   CK(ctr.is_cuda() && ctr.scalar_type() == at::kInt && ctr.numel() == 1, "batch_fetch: int32 step counter");
   CK(nbatch >= 1, "batch_fetch: nbatch >= 1");
   BatchCopy bc{};
@@ -502,15 +510,21 @@ void batch_fetch_(const std::vector<at::Tensor>& srcs, const std::vector<at::Ten
   at::DeviceGuard g(ctr.device());
   HIP_OK(batch_fetch(bc, (int)srcs.size(), ctr.data_ptr<int>(), cur_stream()));
 }
+// loss [R] with hist [R, cap] (replica batching: one shared counter) or loss [1] with hist [cap]
 void step_record_(const at::Tensor& loss, c10::optional<at::Tensor> hist, const at::Tensor& ctr) {
   F32(loss);
-  CK(loss.is_cuda() && loss.numel() == 1, "step_record: one fp32 loss on the GPU");
+  const int64_t R = loss.numel();
+  CK(loss.is_cuda() && loss.is_contiguous() && R >= 1 && R <= 64, "step_record: 1..64 fp32 losses on the GPU");
   CK(ctr.is_cuda() && ctr.scalar_type() == at::kInt && ctr.numel() == 1 && ctr.device() == loss.device(),
      "step_record: int32 step counter on the loss device");
-  if (hist) { F32(*hist); CK(hist->device() == loss.device(), "step_record: history device"); }
+  if (hist) {
+    F32(*hist);
+    CK(hist->device() == loss.device() && hist->is_contiguous() && (R == 1 || (hist->dim() == 2 && hist->size(0) == R)),
+       "step_record: history [cap] (or [R, cap] for R losses) on the loss device");
+  }
   at::DeviceGuard g(loss.device());
-  HIP_OK(step_record(loss.data_ptr<float>(), optr<float>(hist), hist ? (int)hist->numel() : 0, ctr.data_ptr<int>(),
-                     cur_stream()));
+  HIP_OK(step_record(loss.data_ptr<float>(), optr<float>(hist), hist ? (int)(hist->numel() / R) : 0, ctr.data_ptr<int>(),
+                     cur_stream(), (int)R));
 }
 void prob_xent_(const at::Tensor& p, c10::optional<at::Tensor> labels, c10::optional<at::Tensor> target,
                 const at::Tensor& loss_rows, const at::Tensor& dp, double eps, double scale, int64_t ignore_index) {
@@ -603,7 +617,7 @@ void register_ops(py::module& m) {
   m.attr("BN_SHARDS") = (int)kBnShards;
   m.def("bn_stats", &bn_stats_);
   m.def("splitk_finalize", &splitk_finalize_, py::arg("ws"), py::arg("y"), py::arg("C"), py::arg("bias"), py::arg("relu"),
-        py::arg("stats"), py::arg("splits") = 0);
+        py::arg("stats"), py::arg("splits") = 0, py::arg("brows") = 0, py::arg("zbias") = 0);
   m.def("bn_partial_rows", &bn_partial_rows_);
   m.def("bn_finalize", &bn_finalize_);
   m.def("bn_apply", &bn_apply_, py::arg("x"), py::arg("scale"), py::arg("shift"), py::arg("resid"), py::arg("y"),
@@ -626,7 +640,7 @@ void register_ops(py::module& m) {
   m.def("softmax_xent", &softmax_xent_, "fused softmax cross-entropy", py::arg("logits"), py::arg("labels"),
         py::arg("probs"), py::arg("loss_rows"), py::arg("dlogits"), py::arg("grad_scale"), py::arg("smoothing"),
         py::arg("ignore_index"), py::arg("grad_scale_dev") = py::none(), py::arg("loss_out") = py::none(),
-        py::arg("out_scale") = 1.0);
+        py::arg("out_scale") = 1.0, py::arg("zrows") = 0);
   m.def("label_count_inv", &label_count_inv_);
   m.def("rows_sum_scaled", &rows_sum_scaled_);
   m.def("pad_cols_bf16", &pad_cols_bf16_, "zero-padded copy of a row-strided bf16 view");
@@ -637,7 +651,7 @@ void register_ops(py::module& m) {
   m.def("relu_bwd", &relu_bwd_);
   m.def("add_bf16", &add_bf16_);
   m.def("bias_grad", &bias_grad_, py::arg("dy"), py::arg("db"), py::arg("N"), py::arg("accumulate"),
-        py::arg("relu_y") = py::none(), py::arg("relu_dx") = py::none());
+        py::arg("relu_y") = py::none(), py::arg("relu_dx") = py::none(), py::arg("zcount") = 1, py::arg("zdb") = 0);
   m.def("transpose_bf16", &transpose_bf16_);
   m.def("im2col", &im2col_);
   m.def("normalize_u8", &normalize_u8_);

@@ -118,6 +118,10 @@ class ParamArena:
             else:
                 host[p.offset : p.offset + p.numel] = v.reshape(-1)
         self.master.copy_(host)
+        self._bind_views()
+        self.sync_compute()
+
+    def _bind_views(self):
         for p in self.params:
             sl = slice(p.offset, p.offset + p.snumel)
             p.pmaster = self.master[sl].view(p.pshape)
@@ -133,7 +137,16 @@ class ParamArena:
             p.data.requires_grad_(True)
             if p.master is not p.data:
                 p.master.requires_grad_(True)
-        self.sync_compute()
+
+    def rebind(self, master: torch.Tensor, grad: torch.Tensor, compute: torch.Tensor):
+        """Move the arena into caller-provided flat buffers (same layout; their current contents are kept):
+        a replica group stacks its replicas' arenas in one [R, numel] allocation so that one launch can
+        address every replica's weights at a fixed stride (parallel/replica_seq.py).  Layers read the new
+        views from their Params at the next call."""
+        assert master.numel() == grad.numel() == compute.numel() == self.numel
+        self.master, self.grad = master, grad
+        self.compute = master if self.compute_dtype == torch.float32 else compute
+        self._bind_views()
 
     # -------------------------------------------------------------------------
     grads_zeroed = False  # set by a captured optimizer update that zeroed the gradients it consumed

@@ -294,10 +294,14 @@ class ReplicaGroup:
                 self._window_all([rep], rep.steps, False)
             self._average()
             return
-        from . import replica_batch
+        from . import replica_batch, replica_seq
 
-        if replica_batch.applies(self):
+        if replica_batch.applies(self):  # recurrent regressors (NYISO)
             self.batched = replica_batch.BatchedReplicas(self)
+            self._run_batched(graphs)
+            return
+        if replica_seq.applies(self):  # Sequential CNN / MLP classifiers (MNIST)
+            self.batched = replica_seq.SeqReplicas(self)
             self._run_batched(graphs)
             return
         for j in range(self.rounds):

@@ -127,3 +127,46 @@ def test_replica_capture_failure_falls_back_to_eager(batched, monkeypatch):
     assert all(r["graph"] for r in res_g) and not any(r["graph"] for r in res_e)
     assert n_g == n_e > 0
     torch.testing.assert_close(w_e, w_g, rtol=1e-5, atol=1e-6)
+
+
+def _img_frame(n=1024, seed=3):
+    from distributeddeeplearningspark_amd.sql.dataframe import from_columns
+
+    rng = np.random.default_rng(seed)
+    lab = rng.integers(0, 10, n)
+    tmpl = rng.random((10, 28, 28, 1)).astype(np.float32)
+    x = (tmpl[lab] + 0.3 * rng.random((n, 28, 28, 1))).astype(np.float32)
+    return from_columns({"features": x, "label": np.eye(10, dtype=np.float32)[lab]}, num_partitions=4)
+
+
+def _train_cnn(batched, monkeypatch, epochs=2):
+    from distributeddeeplearningspark_amd import trainers as T
+    from distributeddeeplearningspark_amd.models.zoo import mnist_cnn
+
+    monkeypatch.setenv("DDL_WORKERS_PER_GPU", "4")
+    monkeypatch.setenv("DDL_REPLICA_GROUPS", "1")
+    monkeypatch.setenv("DDL_REPLICA_BATCH", "1" if batched else "0")
+    tr = T.ADAG(keras_model=mnist_cnn(), worker_optimizer="adam", loss="categorical_crossentropy", num_workers=4,
+                batch_size=16, num_epoch=epochs, features_col="features", label_col="label", communication_window=5)
+    out = tr.train(_img_frame())
+    return out.arena.get_flat().detach().cpu().clone(), tr.parameter_server.num_updates, tr._results
+
+
+def test_batched_cnn_replicas_match_stream_replicas(monkeypatch):
+    """Replica-batched Sequential CNN step (parallel/replica_seq.py: the reference's MNIST network, four
+    co-located ADAG workers; every GEMM / conv / bias-gradient / loss launch covers all replicas through
+    its replica grid dimension, one optimizer launch over the stacked arenas) vs the per-replica path
+    (one graph per replica on its own stream): same update count and, to bf16 / split-K atomic-order
+    noise, the same loss histories and trained center."""
+    w_b, n_b, res_b = _train_cnn(True, monkeypatch)
+    w_s, n_s, res_s = _train_cnn(False, monkeypatch)
+    assert all(r["replica_group"]["batched"] for r in res_b), "batched path not used"
+    assert not any(r["replica_group"]["batched"] for r in res_s)
+    assert all(r["graph"] for r in res_b)
+    assert n_b == n_s > 0
+    for a, b in zip(res_b, res_s):
+        assert len(a["history"]) == len(b["history"]) > 0
+        np.testing.assert_allclose(a["history"][:5], b["history"][:5], rtol=2e-2, atol=2e-3)
+        assert abs(np.mean(a["history"][-5:]) - np.mean(b["history"][-5:])) < 0.05 * max(1.0, np.mean(b["history"][-5:]))
+    err = ((w_b - w_s).norm() / w_s.norm()).item()
+    assert err < 2e-2, err
