@@ -89,44 +89,53 @@ def _batch(tmpl, n, g):
     return x, y
 
 
-def test_resnet50_learns_synthetic_task_like_torch_path(monkeypatch):
+def _hip_curve():
     from distributeddeeplearningspark_amd.models import ResNet50
     from distributeddeeplearningspark_amd.models.optimizers import SGD
 
     tmpl = _templates()
-    curves, accs = {}, {}
-    for name, backend in (("hip", None), ("torch", "torch")):
-        if backend:
-            monkeypatch.setenv("DDL_BACKEND", backend)
-        else:
-            monkeypatch.delenv("DDL_BACKEND", raising=False)
-        torch.manual_seed(0)
-        m = ResNet50(input_shape=(64, 64, 3), num_classes=10)
-        # lr 0.05 diverged on both paths (loss 17-33 in the first windows, round 4); at 0.01 the fp32 CPU
-        # path reads loss windows 4.0 / 0.11 / 0.11 / 0.00 and held-out accuracy 1.0
-        m.compile(SGD(lr=0.01, momentum=0.9), "sparse_categorical_crossentropy")
-        m.place(DEV, seed=1)
-        g = torch.Generator().manual_seed(2)
-        losses = []
-        for _ in range(150):
-            x, y = _batch(tmpl, 32, g)
-            losses.append(float(m.train_on_batch(m.to_input(x), m.to_target(y))))
-        xt, yt = _batch(tmpl, 512, torch.Generator().manual_seed(99))
-        pred = m.predict(xt.numpy(), batch_size=128).argmax(1)
-        curves[name] = np.array(losses)
-        accs[name] = float((pred == yt.numpy()).mean())
+    torch.manual_seed(0)
+    m = ResNet50(input_shape=(64, 64, 3), num_classes=10)
+    m.compile(SGD(lr=0.01, momentum=0.9), "sparse_categorical_crossentropy")
+    m.place(DEV, seed=1)
+    g = torch.Generator().manual_seed(2)
+    losses = []
+    for _ in range(150):
+        x, y = _batch(tmpl, 32, g)
+        losses.append(float(m.train_on_batch(m.to_input(x), m.to_target(y))))
+    xt, yt = _batch(tmpl, 512, torch.Generator().manual_seed(99))
+    acc = float((m.predict(xt.numpy(), batch_size=128).argmax(1) == yt.numpy()).mean())
+    return np.array(losses), acc
+
+
+def test_resnet50_deterministic_convergence_vs_fp32_curve():
+    """ResNet-50 (64x64) trained 150 SGD-momentum steps on the synthetic template task in deterministic mode
+    (DDL_DETERMINISTIC semantics: fixed-order reductions): two GPU runs give the SAME curve bit for bit, and the
+    curve is pinned against the stored fp32 CPU curve of the same run (tests/fixtures/
+    resnet50_synthetic_fp32_curve.json, scripts/r5/make_convergence_fixture.py: loss windows 4.03 / 0.114 / 0.106
+    / 0.000, held-out accuracy 1.0) instead of a second, itself noisy, PyTorch / MIOpen run (round 4's flaky
+    form).  The early windows of this random-init network are chaotic under any perturbation (bf16 noise
+    included), so they are held to a factor-2 band; the run must converge like the fp32 one."""
+    import json
+    import os
+
+    from distributeddeeplearningspark_amd.ops import determinism as D
+
+    ref = json.load(open(os.path.join(os.path.dirname(__file__), "fixtures", "resnet50_synthetic_fp32_curve.json")))
+    r = np.array(ref["losses"])
+    D.set_enabled(True)
+    try:
+        h, acc = _hip_curve()
+        h2, acc2 = _hip_curve()
+    finally:
+        D.set_enabled(False)
     win = lambda c, a, b: float(c[a:b].mean())
-    summary = {k: [round(win(c, a, a + 10), 3) for a in (0, 30, 70, 140)] for k, c in curves.items()}
-    print("ResNet-50 64x64 synthetic task: loss windows", summary, "held-out accuracy", accs)
-    h, t = curves["hip"], curves["torch"]
+    summary = {k: [round(win(c, a, a + 10), 3) for a in (0, 30, 70, 140)] for k, c in (("hip", h), ("fp32", r))}
+    print("ResNet-50 64x64 synthetic task (deterministic): loss windows", summary, "held-out accuracy", acc,
+          "fp32", ref["heldout_accuracy"])
+    assert np.array_equal(h, h2) and acc == acc2, "deterministic mode: two runs differ"
     assert np.isfinite(h).all()
-    assert win(h, 140, 150) < 0.1 * win(h, 0, 10), summary  # it learns
-    # the first windows carry run-to-run loss spikes on both paths (measured: hip 3.3 / 4.1, torch 3.2 / 2.7 in
-    # window 0 across runs; hip 0.02-0.41, torch 0.29-0.89 at step 70), so the curves are compared where both
-    # have converged, plus a factor-2 band over the first windows
-    assert 0.5 * win(t, 0, 10) < win(h, 0, 10) < 2.0 * win(t, 0, 10), summary
-    # the reference (PyTorch / MIOpen) path's own late spikes reach ~0.13 in its final window on some runs
-    # (measured 0.125 at HEAD with hip 0.001, round 4): the reference is held to having learned (< 0.3, its
-    # held-out accuracy below), the HIP path to having converged
-    assert win(h, 140, 150) < 0.1 and win(t, 140, 150) < 0.3, summary
-    assert accs["hip"] >= 0.9 and accs["torch"] >= 0.9, accs
+    assert 0.5 * win(r, 0, 10) < win(h, 0, 10) < 2.0 * win(r, 0, 10), summary
+    assert win(h, 140, 150) < 0.1 and win(r, 140, 150) < 0.1, summary  # both converged
+    assert win(h, 140, 150) < 0.05 * win(h, 0, 10), summary
+    assert acc >= 0.95 and ref["heldout_accuracy"] >= 0.95, (acc, ref["heldout_accuracy"])
