@@ -261,6 +261,15 @@ int embedding_scatter(const int64_t* ids, const void* dy, float* gw, long n, int
 // conv data-gradient filter layouts: out[ci][t][co] = w[co][taps.t[t]][ci] (bf16, nt <= 64 taps)
 constexpr int kMaxFilterTaps = 64;
 struct FilterTaps { int16_t t[kMaxFilterTaps]; };
+// one job of taps_batch: dst[ci][t][co] = src[co][taps[t]][ci], t < nt (blk0: its first block in the grid)
+struct TapsJob {
+  const uint16_t* src;
+  uint16_t* dst;
+  int Co, T, Ci, nt, blk0, pad_;
+  int16_t taps[kMaxFilterTaps];
+};
+int taps_batch(const TapsJob* jobs, int njobs, int blocks, hipStream_t s);
+int taps_job_blocks(int Co, int Ci, int nt);
 int filter_taps_transpose(const void* w, void* out, int Co, int T, int Ci, const FilterTaps& taps, int nt,
                           hipStream_t s, int zcount = 1, long zw = 0, long zo = 0);
 // y[C][R] = x[R][C] (fp32)

@@ -190,6 +190,36 @@ __global__ __launch_bounds__(256) void filter_taps_transpose_kernel(const bf16_t
   }
 }
 
+// Every weight-derived filter of a training step in ONE launch (ops/derived.py): job j transposes
+// src [Co][T][Ci] into dst [Ci][nt][Co] over the taps taps[0..nt) (a flipped stride-1 dgrad filter, a strided
+// dgrad class filter, or — T = nt = 1 — a plain [N][K] -> [K][N] weight transpose for a Linear dgrad).  The
+// blocks of all jobs form one grid; a block finds its job in the (device-resident, per-model) table.
+__global__ __launch_bounds__(256) void taps_batch_kernel(const TapsJob* __restrict__ jobs, int njobs) {
+  __shared__ bf16_t tile[32][33];
+  const int blk = blockIdx.x;
+  int j = 0;
+  while (j + 1 < njobs && jobs[j + 1].blk0 <= blk) ++j;
+  const TapsJob& jb = jobs[j];
+  const int Co = jb.Co, Ci = jb.Ci, T = jb.T, nt = jb.nt;
+  const int nbi = (Ci + 31) >> 5, nbo = (Co + 31) >> 5;
+  const int local = blk - jb.blk0;
+  const int t = local / (nbi * nbo), rem = local - t * nbi * nbo;
+  const int co0 = (rem / nbi) * 32, ci0 = (rem % nbi) * 32;
+  const int src_t = jb.taps[t];
+  const bf16_t* w = jb.src;
+  bf16_t* out = jb.dst;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int i = ty; i < 32; i += 8) {
+    const int co = co0 + i, ci = ci0 + tx;
+    tile[i][tx] = (co < Co && ci < Ci) ? w[((long)co * T + src_t) * Ci + ci] : (bf16_t)0;
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    const int ci = ci0 + i, co = co0 + tx;
+    if (ci < Ci && co < Co) out[((long)ci * nt + t) * Co + co] = tile[tx][i];
+  }
+}
+
 // y[C][R] = x[R][C] (fp32) through a padded 32x32 LDS tile
 __global__ __launch_bounds__(256) void transpose_f32_kernel(const float* __restrict__ x, float* __restrict__ y, int R,
                                                             int C) {
@@ -296,6 +326,14 @@ int filter_taps_transpose(const void* w, void* out, int Co, int T, int Ci, const
                      nt, taps, zw, zo);
   return (int)hipGetLastError();
 }
+
+int taps_batch(const TapsJob* jobs, int njobs, int blocks, hipStream_t s) {
+  if (njobs < 1 || blocks < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(taps_batch_kernel, dim3(blocks), dim3(256), 0, s, jobs, njobs);
+  return (int)hipGetLastError();
+}
+
+int taps_job_blocks(int Co, int Ci, int nt) { return ((Ci + 31) / 32) * ((Co + 31) / 32) * nt; }
 
 int transpose_f32(const float* x, float* y, int R, int C, hipStream_t s) {
   if (R <= 0 || C <= 0) return 0;

@@ -164,6 +164,46 @@ void embedding_bwd_(const at::Tensor& ids, const at::Tensor& dy, const at::Tenso
 }
 
 // out [Ci][nt][Co] = w [Co][T][Ci] gathered at the given taps
+// Job table of taps_batch (host uint8 tensor of TapsJob records; the caller keeps it on the device): every
+// src [Co][KH][KW][Ci] (or [N][K]) contiguous bf16, dst [Ci][nt][Co] (or [K][N]).  Returns (table, total blocks).
+py::tuple taps_batch_table(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts,
+                           const std::vector<std::vector<int64_t>>& taps) {
+  CK(!srcs.empty() && srcs.size() == dsts.size() && taps.size() == srcs.size(), "taps_batch_table: one dst / taps per src");
+  const int64_t n = (int64_t)srcs.size();
+  at::Tensor table = at::zeros({n * (int64_t)sizeof(TapsJob)}, at::TensorOptions().dtype(at::kByte));
+  TapsJob* jb = reinterpret_cast<TapsJob*>(table.data_ptr());
+  int64_t blocks = 0;
+  for (int64_t j = 0; j < n; ++j) {
+    const at::Tensor &w = srcs[j], &o = dsts[j];
+    CK(w.is_cuda() && o.is_cuda() && w.scalar_type() == at::kBFloat16 && o.scalar_type() == at::kBFloat16 &&
+           w.is_contiguous() && o.is_contiguous() && (w.dim() == 4 || w.dim() == 2) && o.device() == w.device(),
+       "taps_batch_table: contiguous bf16 GPU tensors, src [Co][KH][KW][Ci] or [N][K]");
+    const int64_t Co = w.size(0), Ci = w.size(-1), T = w.dim() == 4 ? w.size(1) * w.size(2) : 1;
+    const int64_t nt = (int64_t)taps[j].size();
+    CK(nt >= 1 && nt <= kMaxFilterTaps && o.numel() == Ci * nt * Co, "taps_batch_table: dst [Ci][nt][Co]");
+    jb[j].src = reinterpret_cast<const uint16_t*>(w.data_ptr());
+    jb[j].dst = reinterpret_cast<uint16_t*>(o.data_ptr());
+    jb[j].Co = (int)Co;
+    jb[j].T = (int)T;
+    jb[j].Ci = (int)Ci;
+    jb[j].nt = (int)nt;
+    jb[j].blk0 = (int)blocks;
+    for (int64_t i = 0; i < nt; ++i) {
+      CK(taps[j][i] >= 0 && taps[j][i] < T, "taps_batch_table: tap out of range");
+      jb[j].taps[i] = (int16_t)taps[j][i];
+    }
+    blocks += taps_job_blocks((int)Co, (int)Ci, (int)nt);
+    CK(blocks < (int64_t(1) << 31), "taps_batch_table: grid too large");
+  }
+  return py::make_tuple(table, blocks);
+}
+void taps_batch_(const at::Tensor& table, int64_t njobs, int64_t blocks) {
+  CK(table.is_cuda() && table.scalar_type() == at::kByte && table.numel() == njobs * (int64_t)sizeof(TapsJob),
+     "taps_batch: the device copy of taps_batch_table's table");
+  at::DeviceGuard g(table.device());
+  HIP_OK(taps_batch(reinterpret_cast<const TapsJob*>(table.data_ptr()), (int)njobs, (int)blocks, cur_stream()));
+}
+
 // zcount > 1 (replica batching): zcount filters every zw elements from w's storage, outputs [zcount][Ci][nt][Co]
 void filter_taps_transpose_(const at::Tensor& w, const at::Tensor& out, std::vector<int64_t> taps, int64_t zcount,
                             int64_t zw) {
@@ -202,6 +242,8 @@ void register_layer_ops(py::module& m) {
         py::arg("K"), py::arg("alpha") = 1.0, py::arg("beta") = 0.0, py::arg("bias") = py::none(),
         py::arg("relu") = false);
   m.def("transpose_f32", &transpose_f32_, "y = x^T (fp32)");
+  m.def("taps_batch_table", &taps_batch_table);
+  m.def("taps_batch", &taps_batch_);
   m.def("filter_taps_transpose", &filter_taps_transpose_, "conv dgrad filter: out[ci][t][co] = w[co][taps[t]][ci]",
         py::arg("w"), py::arg("out"), py::arg("taps"), py::arg("zcount") = 1, py::arg("zw") = 0);
   m.def("embedding_fwd", &embedding_fwd_, "Keras Embedding gather (bf16/fp32 table)");

@@ -365,11 +365,17 @@ class Model(Layer):
         """zero grads -> forward -> loss -> backward (grads land in the arena). Returns loss tensor."""
         from ..ops.norm import reset_workspaces
 
+        from ..ops import derived
+
         self._ensure_placed()
         reset_workspaces(self.device)
         self.arena.zero_grad()
-        loss = self.compute_loss(x, y, training=True)
-        self.backward_unit(loss)
+        derived.begin_step(self)  # weight-derived filters: one launch per step (ops/derived.py)
+        try:
+            loss = self.compute_loss(x, y, training=True)
+            self.backward_unit(loss)
+        finally:
+            derived.end_step()
         return loss
 
     def backward_unit(self, loss):

@@ -24,6 +24,7 @@ import torch
 import torch.nn.functional as F
 
 from . import determinism as _det
+from . import derived
 from . import gemm as G
 from . import zpad as ZP
 from ._native import C, use_native
@@ -249,19 +250,15 @@ def flip_filter(w):
     """[Co, KH, KW, Ci] -> [Ci, KH, KW, Co] with the taps reversed (the transposed conv's filter):
     one HIP pass on the GPU (``filter_taps_transpose``), flip + permute on the CPU."""
     Co, KH, KW, Ci = w.shape
-    if use_native(w) and w.dtype == torch.bfloat16:
-        out = torch.empty((Ci, KH, KW, Co), dtype=w.dtype, device=w.device)
-        C().filter_taps_transpose(w.contiguous(), out, list(range(KH * KW - 1, -1, -1)))
-        return out
+    if use_native(w) and w.dtype == torch.bfloat16:  # batched with the step's other derived filters (ops/derived.py)
+        return derived.taps_transpose(w.contiguous(), range(KH * KW - 1, -1, -1), (Ci, KH, KW, Co))
     return w.flip(1, 2).permute(3, 1, 2, 0).contiguous()
 
 
 def class_filter(w, g: ConvGeometry, cl):
     """K-contiguous filter of one strided data-gradient class: [Ci][taps of the class][Co]."""
     if use_native(w) and w.dtype == torch.bfloat16:
-        out = torch.empty((g.Ci, len(cl["wt"]), g.Co), dtype=w.dtype, device=w.device)
-        C().filter_taps_transpose(w.contiguous(), out, list(cl["wt"]))
-        return out
+        return derived.taps_transpose(w.contiguous(), cl["wt"], (g.Ci, len(cl["wt"]), g.Co))
     return w.reshape(g.Co, g.T, g.Ci).index_select(1, _tap_index(cl, w.device)).permute(2, 1, 0).contiguous()
 
 

@@ -324,6 +324,10 @@ def transpose(w):
     R, Cc = w.shape
     if w.stride(1) != 1 or R % 8 or Cc % 8 or w.stride(0) % 8:
         return w.t().contiguous()
+    if w.is_contiguous():  # batched with the step's other derived weights (ops/derived.py)
+        from . import derived
+
+        return derived.taps_transpose(w, (0,), (Cc, R))
     out = torch.empty((Cc, R), dtype=w.dtype, device=w.device)
     C().transpose_bf16(w, out)
     return out

@@ -425,10 +425,16 @@ class DataParallel:
             m.arena.zero_grad()
             if self.overlap:
                 self._begin()
-            with phase("forward"):
-                loss = m.compute_loss(x, y, training=True)
-            with phase("backward"):
-                m.backward_unit(loss)
+            from ..ops import derived
+
+            derived.begin_step(m)  # weight-derived filters: one launch per step (ops/derived.py)
+            try:
+                with phase("forward"):
+                    loss = m.compute_loss(x, y, training=True)
+                with phase("backward"):
+                    m.backward_unit(loss)
+            finally:
+                derived.end_step()
             ev = None
             if self.timing and self.pg.distributed:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))

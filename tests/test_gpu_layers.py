@@ -361,3 +361,35 @@ def test_mnist_cnn_padded_arena_matches_fp32_cpu():
     names = _kernel_names(lambda: mg.train_on_batch(xd, yd))
     aten = sorted(n for n in names if "ddl::" not in n and "Memcpy" not in n and "FillFunctor<float>" not in n)
     assert not aten, f"ATen kernels in the MNIST step: {aten}"
+
+
+def test_derived_filters_one_launch_matches_per_copy():
+    """ops/derived.py: the step's flipped / class / transposed weight copies come from ONE taps_batch launch
+    (from the second step on) and give bit-identical gradients to the one-launch-per-copy path (deterministic
+    mode), for a ResNet stage with stride-2 and 3x3 convs and a Dense head over 4096+ rows."""
+    from distributeddeeplearningspark_amd.models.resnet import ResNet
+    from distributeddeeplearningspark_amd.ops import derived
+    from distributeddeeplearningspark_amd.ops import determinism as D
+
+    torch.manual_seed(0)
+    x = torch.randn(8, 32, 32, 3)
+    y = torch.randint(0, 10, (8,))
+    grads = {}
+    D.set_enabled(True)
+    try:
+        for on in (True, False):
+            derived.ENABLED = on
+            m = ResNet(blocks=(1, 1), input_shape=(32, 32, 3), num_classes=10)
+            m.compile("sgd", "sparse_categorical_crossentropy")
+            m.place(DEV, seed=5)
+            xd, yd = m.to_input(x), m.to_target(y)
+            m.train_on_batch(xd, yd)  # step 1 registers the copies, one launch each
+            names = _kernel_names(lambda: m.backward_step(xd, yd))
+            grads[on] = m.arena.grad.detach().float().cpu().clone()
+            if on:
+                assert any("taps_batch_kernel" in n for n in names), sorted(names)
+                assert not any("filter_taps_transpose" in n or "transpose_bf16" in n for n in names), sorted(names)
+    finally:
+        derived.ENABLED = True
+        D.set_enabled(False)
+    assert torch.equal(grads[True], grads[False])
