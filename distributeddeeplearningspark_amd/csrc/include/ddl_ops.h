@@ -153,6 +153,8 @@ int layernorm_fwd(const void* x, const float* gamma, const float* beta, void* y,
 // dx = LN'(dy); dx_drop = dx * dropout-mask(seed, m*H+n) * 1/(1-p) (the gradient entering the
 // dropout of the residual branch, nullable); per-wave partial rows ws[P][2][H] of dgamma/dbeta
 int ln_partial_rows(long M);
+// partial rows [P][parts][H] that layernorm_bwd writes (its ws and colsum size)
+int ln_bwd_rows(long M, int H);
 // in_drop_p/in_seed: dy is first masked by the forward's output dropout
 // parts = 2: ws[P][2][H] = (dgamma, dbeta); parts = 3: ws[P][3][H] = (dbias, dgamma, dbeta) where
 // dbias = column sums of dx_drop, the bias gradient of the GEMM whose dropped output fed the residual sum
@@ -269,7 +271,7 @@ struct TapsJob {
   int16_t taps[kMaxFilterTaps];
 };
 int taps_batch(const TapsJob* jobs, int njobs, int blocks, hipStream_t s);
-int taps_job_blocks(int Co, int Ci, int nt);
+int taps_job_blocks(int Co, int Ci, int nt, int T);
 int filter_taps_transpose(const void* w, void* out, int Co, int T, int Ci, const FilterTaps& taps, int nt,
                           hipStream_t s, int zcount = 1, long zw = 0, long zo = 0);
 // y[C][R] = x[R][C] (fp32)

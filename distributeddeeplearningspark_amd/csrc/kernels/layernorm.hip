@@ -123,7 +123,10 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
   }
 }
 
-template <int VPL, bool PF>
+// BR: the 4 waves of a workgroup sum their parameter-gradient partials through LDS and write ONE partial row
+// per workgroup (H <= 1024): twice the waves of the per-wave form at the same partial-row count (so the same
+// column-sum cost), 4 rows per wave instead of 8 — the sweep was latency-bound at 2 waves per SIMD.
+template <int VPL, bool PF, bool BR = false>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const float* __restrict__ gamma, bf16_t* __restrict__ dx,
@@ -239,10 +242,50 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
       }
     }
   }
+  if constexpr (BR) {
+  if (ws) {
+    // block reduce: waves 1..3 park [dbias | dgamma | dbeta] in LDS, wave 0 adds them and writes the row
+    __shared__ float red[3][3 * 8 * 64 * VPL];
+    const int w = threadIdx.x >> 6;
+    constexpr int CW = 8 * 64 * VPL;  // columns of one part held by a wave (>= H)
+    if (w > 0) {
+      float* r = red[w - 1];
+#pragma unroll
+      for (int u = 0; u < VPL; ++u) {
+        const int c = lane + 64 * u;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          r[c * 8 + e] = dd[u][e];
+          r[CW + c * 8 + e] = dg[u][e];
+          r[2 * CW + c * 8 + e] = db[u][e];
+        }
+      }
+    }
+    __syncthreads();
+    if (w == 0) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const float* r = red[q];
+#pragma unroll
+        for (int u = 0; u < VPL; ++u) {
+          const int c = lane + 64 * u;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            dd[u][e] += r[c * 8 + e];
+            dg[u][e] += r[CW + c * 8 + e];
+            db[u][e] += r[2 * CW + c * 8 + e];
+          }
+        }
+      }
+    } else {
+      return;
+    }
+  }
+  }
   if (ws) {
     // parts == 2: [dgamma | dbeta]; parts == 3: [dbias | dgamma | dbeta] (the arena order of a
     // sublayer's output bias followed by the LayerNorm's gamma and beta)
-    float* wb = ws + (long)wave * parts * H;
+    float* wb = ws + (long)(BR ? blockIdx.x : wave) * parts * H;
     float* w0 = parts == 3 ? wb + H : wb;
     if (parts == 3) {
 #pragma unroll
@@ -572,6 +615,14 @@ int layernorm_fwd(const void* x, const float* gamma, const float* beta, void* y,
   return (int)hipGetLastError();
 }
 
+constexpr int kLnBwdBlocksBR = 1024;  // block-reduced form: 4,096 waves (4 per SIMD), one partial row per workgroup
+
+// partial rows [P][parts][H] layernorm_bwd writes for M rows of width H
+int ln_bwd_rows(long M, int H) {
+  if (H / 8 <= 128) return (int)std::max<long>(1, std::min<long>((long)kLnBwdBlocksBR, (M + 3) / 4));
+  return ln_partial_rows(M);
+}
+
 int ln_partial_rows(long M) {
   // workgroups of the row-per-wave backward sweeps (4 waves each); also sizes embed_bwd's grid and its
   // token-type partial-row workspace, which share this partial-row count
@@ -586,15 +637,16 @@ int layernorm_bwd(const void* dy, const void* x, const float* mean, const float*
   const uint32_t ith = drop_t8(in_drop_p);
   const float iscale = drop_scale8(ith);
   const int nv = H / 8;
-  const dim3 grid((unsigned)(P / 4));
+  if (P != ln_bwd_rows(M, H)) return (int)hipErrorInvalidValue;
+  const dim3 grid((unsigned)(nv <= 128 ? P : P / 4));
   const uint32_t thresh = drop_t8(drop_p);
   const float dscale = drop_scale8(thresh);
   auto DY = reinterpret_cast<const bf16_t*>(dy);
   auto X = reinterpret_cast<const bf16_t*>(x);
   auto DX = reinterpret_cast<bf16_t*>(dx);
   auto DD = reinterpret_cast<bf16_t*>(dx_drop);
-  if (nv <= 64) hipLaunchKernelGGL((ln_bwd_kernel<1, true>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts);
-  else if (nv <= 128) hipLaunchKernelGGL((ln_bwd_kernel<2, true>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts);
+  if (nv <= 64) hipLaunchKernelGGL((ln_bwd_kernel<1, true, true>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts);
+  else if (nv <= 128) hipLaunchKernelGGL((ln_bwd_kernel<2, true, true>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts);
   else if (nv <= 256) hipLaunchKernelGGL((ln_bwd_kernel<4, false>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts);
   else hipLaunchKernelGGL((ln_bwd_kernel<8, false>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts);
   return (int)hipGetLastError();

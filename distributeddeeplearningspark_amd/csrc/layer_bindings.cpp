@@ -192,7 +192,7 @@ py::tuple taps_batch_table(const std::vector<at::Tensor>& srcs, const std::vecto
       CK(taps[j][i] >= 0 && taps[j][i] < T, "taps_batch_table: tap out of range");
       jb[j].taps[i] = (int16_t)taps[j][i];
     }
-    blocks += taps_job_blocks((int)Co, (int)Ci, (int)nt);
+    blocks += taps_job_blocks((int)Co, (int)Ci, (int)nt, (int)T);
     CK(blocks < (int64_t(1) << 31), "taps_batch_table: grid too large");
   }
   return py::make_tuple(table, blocks);

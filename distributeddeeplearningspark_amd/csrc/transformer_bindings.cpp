@@ -121,6 +121,7 @@ void layernorm_fwd_(const at::Tensor& x, c10::optional<at::Tensor> gamma, c10::o
 }
 
 int64_t ln_partial_rows_(int64_t M) { return ln_partial_rows(M); }
+int64_t ln_bwd_rows_(int64_t M, int64_t H) { return ln_bwd_rows(M, (int)H); }
 
 void layernorm_bwd_(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& mean, const at::Tensor& rstd,
                     c10::optional<at::Tensor> gamma, const at::Tensor& dx, c10::optional<at::Tensor> dx_drop,
@@ -132,7 +133,7 @@ void layernorm_bwd_(const at::Tensor& dy, const at::Tensor& x, const at::Tensor&
   CK(dy.numel() == x.numel() && dx.numel() == x.numel() && mean.numel() == M && rstd.numel() == M, "shapes");
   if (gamma) { F32(*gamma); CK(gamma->numel() == H && (uintptr_t)gamma->data_ptr() % 16 == 0, "gamma [H], 16-B aligned"); }
   if (dx_drop) { BF16(*dx_drop); CK(dx_drop->numel() == x.numel(), "dx_drop shape"); }
-  const int P = ln_partial_rows(M);
+  const int P = ln_bwd_rows(M, (int)H);
   CK(parts == 2 || parts == 3, "layernorm_bwd: parts must be 2 or 3");
   if (ws) { F32(*ws); CK(ws->numel() >= (int64_t)P * parts * H, "layernorm_bwd: ws must hold [P][parts][H]"); }
   at::DeviceGuard g(x.device());
@@ -236,6 +237,7 @@ void register_transformer(py::module& m) {
   m.def("layernorm_fwd", &layernorm_fwd_, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("y"),
         py::arg("mean"), py::arg("rstd"), py::arg("eps"), py::arg("drop_p") = 0.0, py::arg("seed") = 0);
   m.def("ln_partial_rows", &ln_partial_rows_);
+  m.def("ln_bwd_rows", &ln_bwd_rows_, "partial rows written by layernorm_bwd for M rows of width H");
   m.def("layernorm_bwd", &layernorm_bwd_, py::arg("dy"), py::arg("x"), py::arg("mean"), py::arg("rstd"),
         py::arg("gamma"), py::arg("dx"), py::arg("dx_drop"), py::arg("drop_p"), py::arg("seed"), py::arg("ws"),
         py::arg("in_drop_p") = 0.0, py::arg("in_seed") = 0, py::arg("parts") = 2);

@@ -257,7 +257,7 @@ class _EmbeddingsFn(torch.autograd.Function):
             ids, types, e, mean, rstd = ctx.saved_tensors
             T_ = e.shape[0]
             de = torch.empty_like(e)
-            ws = torch.empty((C().ln_partial_rows(T_), 2, H), dtype=torch.float32, device=e.device)
+            ws = torch.empty((C().ln_bwd_rows(T_, H), 2, H), dtype=torch.float32, device=e.device)
             C().layernorm_bwd(dy.contiguous(), e, mean, rstd, layer.ln_g.master, de, None, 0.0, 0, ws, ctx.p, ctx.seed)
             _ln_param_grads(ws, H, layer.ln_g, layer.ln_b)
             # word rows: no-return fp32 atomics straight into the arena (no id sort); positions: sum over batch
@@ -347,7 +347,7 @@ class _BertLayerFn(torch.autograd.Function):
         T_ = h.shape[0]
         dev = h.device
         dout = dout.contiguous()
-        P_ = C().ln_partial_rows(T_)
+        P_ = C().ln_bwd_rows(T_, H)
         ws = torch.empty((P_, 3, H), dtype=torch.float32, device=dev)
         red = torch.empty(3 * H, dtype=torch.float32, device=dev)
 
@@ -471,7 +471,7 @@ class _MLMHeadFn(torch.autograd.Function):
         _bias_grad(dlogits, head.dec_b.grad)
         dt2 = _dgrad(dlogits, emb.word.data)
         dt = torch.empty_like(t)
-        P_ = C().ln_partial_rows(M)
+        P_ = C().ln_bwd_rows(M, H)
         ws = torch.empty((P_, 2, H), dtype=torch.float32, device=hm.device)
         C().layernorm_bwd(dt2, t, mt, rt, head.ln_g.master, dt, None, 0.0, 0, ws)
         _ln_param_grads(ws, H, head.ln_g, head.ln_b)

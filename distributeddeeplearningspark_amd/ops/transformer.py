@@ -208,7 +208,7 @@ class _LayerNormFn(torch.autograd.Function):
             dx = torch.empty_like(x2)
             ws = None
             if ctx.gg is not None or ctx.gb is not None:
-                P = C().ln_partial_rows(M)
+                P = C().ln_bwd_rows(M, H)
                 ws = torch.empty((P, 2, H), dtype=torch.float32, device=x2.device)
             C().layernorm_bwd(dy.reshape(-1, H).contiguous(), x2, mean, rstd, ctx.gamma, dx, None, 0.0, 0, ws)
             if ws is not None:

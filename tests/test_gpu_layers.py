@@ -393,3 +393,27 @@ def test_derived_filters_one_launch_matches_per_copy():
         derived.ENABLED = True
         D.set_enabled(False)
     assert torch.equal(grads[True], grads[False])
+
+
+def test_taps_batch_mixed_jobs_match_reference():
+    """csrc/kernels/layer_ops.hip taps_batch: one launch over a job table mixing 64-multiple plain transposes
+    (the 16-B vector path: BERT-base weight shapes), odd-sized transposes and tap-reordered conv filters."""
+    c = _C()
+    g = torch.Generator(device=DEV).manual_seed(7)
+    srcs, dsts, taps, refs = [], [], [], []
+    for R, Cc in ((768, 3072), (2304, 768), (1000, 2048), (40, 24)):
+        w = torch.randn(R, Cc, device=DEV, generator=g).to(torch.bfloat16)
+        srcs.append(w)
+        dsts.append(torch.empty(Cc, R, dtype=torch.bfloat16, device=DEV))
+        taps.append([0])
+        refs.append(w.t())
+    for Co, Ci, tp in ((64, 32, list(range(8, -1, -1))), (24, 16, [0, 2, 6, 8])):
+        w = torch.randn(Co, 3, 3, Ci, device=DEV, generator=g).to(torch.bfloat16)
+        srcs.append(w)
+        dsts.append(torch.empty(Ci, len(tp), Co, dtype=torch.bfloat16, device=DEV))
+        taps.append(tp)
+        refs.append(w.reshape(Co, 9, Ci)[:, tp, :].permute(2, 1, 0))
+    table, blocks = c.taps_batch_table(srcs, dsts, taps)
+    c.taps_batch(table.to(DEV), len(srcs), int(blocks))
+    for d, r in zip(dsts, refs):
+        assert torch.equal(d, r.reshape(d.shape)), d.shape

@@ -384,7 +384,7 @@ def _ln_bwd_case(M, H, parts, seed=0):
     y = torch.empty_like(x)
     mean, rstd = torch.empty(M, device=DEV), torch.empty(M, device=DEV)
     C().layernorm_fwd(x, g, None, y, mean, rstd, 1e-12, 0.0, 0)
-    P = C().ln_partial_rows(M)
+    P = C().ln_bwd_rows(M, H)  # partial rows the sweep writes (block-reduced: one per workgroup at H <= 1024)
     ws = torch.full((P, parts, H), float("nan"), device=DEV)
     dx = torch.empty_like(x)
     dxd = torch.empty_like(x) if parts == 3 else None
@@ -407,18 +407,3 @@ def test_layernorm_bwd_many_rows_per_wave(parts):
     """M = 9001 (> 4 x the 512-workgroup cap, not a multiple of 4): every wave accumulates its
     dgamma / dbeta (/ dbias) partial row over several LayerNorm rows."""
     _ln_bwd_case(9001, 768, parts)
-
-
-def test_layernorm_bwd_blocks_override_child():
-    """DDL_LN_BWD_BLOCKS is read once per process (function-local static): check a small
-    override (3 workgroups) in a fresh child process."""
-    import os
-    import subprocess
-    import sys
-
-    code = ("import sys; sys.path.insert(0, 'tests'); import test_gpu_transformer as t; "
-            "t._ln_bwd_case(9001, 256, 2); t._ln_bwd_case(1000, 768, 3); print('ok')")
-    env = dict(os.environ, DDL_LN_BWD_BLOCKS="3")
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=180)
-    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
