@@ -28,8 +28,15 @@ class _StatsPool:
     def __init__(self):
         self.buf, self.used, self.demand = {}, {}, {}
 
+    @staticmethod
+    def _key(device):
+        d = torch.device(device)
+        if d.type == "cuda" and d.index is None:  # "cuda" and "cuda:0" must share one pool entry
+            d = torch.device("cuda", torch.cuda.current_device())
+        return str(d) + _scope.tag()
+
     def get(self, C_, device):
-        key = str(device) + _scope.tag()
+        key = self._key(device)
         n = -(-SHARDS * 2 * C_ // 64) * 64
         self.demand[key] = self.demand.get(key, 0) + n
         buf, used = self.buf.get(key), self.used.get(key, 0)
@@ -39,7 +46,7 @@ class _StatsPool:
         return buf[used : used + SHARDS * 2 * C_].view(SHARDS, 2, C_)
 
     def reset(self, device):
-        key = str(device) + _scope.tag()
+        key = self._key(device)
         want = self.demand.get(key, 0)
         buf = self.buf.get(key)
         if want and (buf is None or buf.numel() < want):
