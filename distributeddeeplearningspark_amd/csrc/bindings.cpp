@@ -58,7 +58,8 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
           c10::optional<at::Tensor> stats, c10::optional<at::Tensor> aux, double drop_p, int64_t drop_seed,
           c10::optional<at::Tensor> resid_mask, c10::optional<at::Tensor> bnr_x, c10::optional<at::Tensor> bnr_mask,
           c10::optional<at::Tensor> bnr_mean, int64_t rsub_h, int64_t rsub_w, c10::optional<at::Tensor> bnr_scale, c10::optional<at::Tensor> bnr_shift, int64_t split_stride,
-          int64_t zcount, int64_t za, int64_t zb, int64_t zc, int64_t zbias) {
+          int64_t zcount, int64_t za, int64_t zb, int64_t zc, int64_t zbias, std::vector<int64_t> cls_tap0,
+          std::vector<int64_t> cls_nt, std::vector<int64_t> cls_coff) {
   CHECK_CUDA(a);
   CHECK_CUDA(b);
   CHECK_CUDA(c);
@@ -159,7 +160,9 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
     // the gathering operand modes compute element offsets in 32 bits (ddl_gemm_kernel.h)
     TORCH_CHECK((int64_t)p.g.n * p.g.hi * p.g.wi * p.g.c < (int64_t(1) << 31),
                 "gemm: a gathered tensor must have fewer than 2^31 elements");
-    if (a_mode == OP_KC_GATHER) TORCH_CHECK(p.g.tap_c % 64 == 0 && K == (int64_t)p.g.ntaps * p.g.tap_c, "conv A gather: tap_c % 64 and K = taps*C");
+    if (a_mode == OP_KC_GATHER)  // (parity classes: each class's K = its taps * C, checked below)
+      TORCH_CHECK(p.g.tap_c % 64 == 0 && (cls_nt.empty() ? K == (int64_t)p.g.ntaps * p.g.tap_c : K <= (int64_t)p.g.ntaps * p.g.tap_c),
+                  "conv A gather: tap_c % 64 and K = taps*C");
     if (b_mode == OP_RC_GATHER) TORCH_CHECK(p.g.tap_c % bn == 0 && N == (int64_t)p.g.ntaps * p.g.tap_c, "conv B gather: tap_c % BN and N = taps*C");
     if (b_mode == OP_RC_TAPS) TORCH_CHECK(b_kdiv % 64 == 0 && K == (int64_t)p.g.ntaps * b_kdiv, "conv B taps: kdiv % 64 and K = taps*kdiv");
     if (a_mode == OP_KC_GATHER8) TORCH_CHECK(p.g.tap_c % 8 == 0 && K == (int64_t)p.g.ntaps * p.g.tap_c, "conv A gather8: tap_c % 8 and K = taps*C");
@@ -230,7 +233,7 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
                 "gemm: split-K slabs need EPI_F32, beta = 0 and a workspace of splits x split_stride floats");
     p.split_stride = split_stride;
   }
-  if (zcount > 1) {  // replica batching: z-th operands / output / bias at element offsets z * (za, zb, zc, zbias)
+  if (zcount > 1 && cls_nt.empty()) {  // replica batching: z-th operands / output / bias at element offsets z * (za, zb, zc, zbias)
     TORCH_CHECK(tile >= 0 && tile <= 3 && !stats && !bnr_x && !outmap && !resid && !aux && drop_p == 0.0 &&
                     split_stride == 0 && relu <= ACT_RELU && za >= 0 && zb >= 0 && zc >= 0 && zbias >= 0,
                 "gemm: replica batching (zcount > 1) runs the 64/128 tiles with at most bias / ReLU / split-K atomics");
@@ -243,6 +246,32 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
     p.zb = zb;
     p.zc = zc;
     p.zbias = zbias;
+  }
+  if (!cls_nt.empty()) {  // parity classes of a strided data-gradient in one launch (GemmParams::zcls)
+    const int64_t nc = (int64_t)cls_nt.size();
+    TORCH_CHECK(nc <= kMaxZCls && (int64_t)cls_tap0.size() == nc && (int64_t)cls_coff.size() == nc && zcount == nc,
+                "gemm: parity classes need cls_tap0 / cls_nt / cls_coff of zcount <= ", kMaxZCls, " entries");
+    TORCH_CHECK(tile >= 0 && tile <= 3 && a_mode == OP_KC_GATHER && b_mode == OP_KC && epi == EPI_BF16 && outmap &&
+                    p.om.oh == 0 && p.om.ow == 0 && !p.om.zero_siblings && !stats && !bnr_x && !resid && !aux && !bias &&
+                    drop_p == 0.0 && relu == 0 && split_stride == 0 && za == 0 && zb == 0 && zc == 0 && zbias == 0,
+                "gemm: parity classes run KC_GATHER x KC on the 64/128 tiles with a plain bf16 output map");
+    TORCH_CHECK(p.om.gh > 0 && p.om.gw > 0 && M % ((int64_t)p.om.gh * p.om.gw) == 0, "gemm: classes need M = n * gh * gw");
+    const int64_t nimg = M / ((int64_t)p.om.gh * p.om.gw);
+    const int64_t last_row = ((nimg - 1) * p.om.hy + (int64_t)(p.om.gh - 1) * p.om.so) * p.om.wy + (int64_t)(p.om.gw - 1) * p.om.so;
+    int64_t kmax = 0;
+    for (int64_t z = 0; z < nc; ++z) {
+      TORCH_CHECK(cls_nt[z] > 0 && cls_tap0[z] >= 0 && cls_tap0[z] + cls_nt[z] <= p.g.ntaps, "gemm: class taps out of range");
+      TORCH_CHECK(cls_coff[z] >= 0 && cls_coff[z] % 8 == 0 && cls_coff[z] + last_row * ldc + N <= c.numel(),
+                  "gemm: class output offset out of range");
+      TORCH_CHECK((cls_tap0[z] + cls_nt[z]) * (int64_t)p.g.tap_c <= ldb, "gemm: class filter columns past ldb");
+      kmax = std::max(kmax, cls_nt[z] * (int64_t)p.g.tap_c);
+      p.cls_tap0[z] = (int)cls_tap0[z];
+      p.cls_nt[z] = (int)cls_nt[z];
+      p.cls_coff[z] = cls_coff[z];
+    }
+    TORCH_CHECK(K == kmax && k_split >= K, "gemm: classes need K = the largest class's K and no split-K");
+    p.zcls = 1;
+    p.zcount = (int)nc;
   }
   at::DeviceGuard guard(a.device());
   HIP_OK(launch_gemm_bf16(p, (int)epi, (int)tile, cur_stream()));
@@ -311,7 +340,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("bnr_mean") = py::none(), py::arg("rsub_h") = 0, py::arg("rsub_w") = 0,
         py::arg("bnr_scale") = py::none(), py::arg("bnr_shift") = py::none(),
         py::arg("split_stride") = 0, py::arg("zcount") = 1, py::arg("za") = 0, py::arg("zb") = 0, py::arg("zc") = 0,
-        py::arg("zbias") = 0);
+        py::arg("zbias") = 0, py::arg("cls_tap0") = std::vector<int64_t>{}, py::arg("cls_nt") = std::vector<int64_t>{},
+        py::arg("cls_coff") = std::vector<int64_t>{});
   m.def("conv3x3_wgrad", &conv3x3_wgrad, "3x3 stride-1 weight gradient (halo kernel): gw += dW", py::arg("dy"),
         py::arg("x"), py::arg("gw"), py::arg("ws"), py::arg("splits"), py::arg("tpb"), py::arg("pp") = false);
   m.def("conv3x3_wgrad_plan", &conv3x3_wgrad_plan_py,

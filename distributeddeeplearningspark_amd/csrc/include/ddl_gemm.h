@@ -40,6 +40,7 @@ enum EpilogueMode : int {
 };
 
 constexpr int kMaxTaps = 64;
+constexpr int kMaxZCls = 4;  // parity classes per batched data-gradient launch (stride 2)
 
 struct ConvGeom {
   int n, hi, wi, c;   // gathered NHWC tensor
@@ -125,6 +126,14 @@ struct GemmParams {
   // with its own weights, as ONE launch (parallel/replica_seq.py).  0 / unused when gridDim.z == 1.
   int zcount;
   long za, zb, zc, zbias;
+  // parity classes of a strided data-gradient as ONE launch (gemm_dma_kernel, KC_GATHER x KC; zcls = 1,
+  // zcount = classes): class z = blockIdx.z reduces K = cls_nt[z] * g.tap_c over taps [cls_tap0[z],
+  // cls_tap0[z] + cls_nt[z]) of the tap table, reads B from column cls_tap0[z] * g.tap_c of the shared
+  // [N][taps * tap_c] class-ordered filter and writes C at element offset cls_coff[z] (the class's
+  // (oh, ow) cell offset in the OutMap grid, whose own oh / ow stay 0).  ops/conv.py:conv_dgrad_native.
+  int zcls;
+  int cls_tap0[kMaxZCls], cls_nt[kMaxZCls];
+  long cls_coff[kMaxZCls];
 };
 
 enum Activation : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_GELU_BWD = 3 };

@@ -871,8 +871,17 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
   int tm, tn;
   tile_raster<BM>(p, bid, tiles_n, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
+  const long zi = blockIdx.z;  // replica of a batched launch (GemmParams::zcount) / parity class (zcls), else 0
+  int kz = p.K, tap0 = 0;
+  long bz = zi * p.zb, cz = zi * p.zc;
+  if (p.zcls) {  // parity class zi of a strided data-gradient (GemmParams::zcls)
+    tap0 = p.cls_tap0[zi];
+    kz = p.cls_nt[zi] * p.g.tap_c;
+    bz = (long)tap0 * p.g.tap_c;
+    cz = p.cls_coff[zi];
+  }
   const int kbeg = split * p.k_split;
-  const int kend = min(p.K, kbeg + p.k_split);
+  const int kend = min(kz, kbeg + p.k_split);
   const int nk = (kend - kbeg + BK - 1) / BK;
 
   const int lane = threadIdx.x & 63;
@@ -883,13 +892,12 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
   Operand<BN, BMODE> B;
   if constexpr (TAPB > 0) {
     load_tap_table(reinterpret_cast<int*>(smem_raw), p.g);
-    A.tt = (const DDL_LDS int*)(smem_raw);
+    A.tt = (const DDL_LDS int*)(smem_raw) + tap0;
     B.tt = (const DDL_LDS int*)(smem_raw);
   }
-  const long zi = blockIdx.z;  // replica of a batched launch (GemmParams::zcount), 0 otherwise
-  A.init(reinterpret_cast<const bf16_t*>(p.a) + zi * p.za, p.lda, p.M, m0, p.K, p.g, kbeg);
-  B.init(reinterpret_cast<const bf16_t*>(p.b) + zi * p.zb, p.ldb, p.N, n0, p.K, p.g, kbeg);
-  const long zc = (long)split * p.split_stride + zi * p.zc, zb = zi * p.zbias;
+  A.init(reinterpret_cast<const bf16_t*>(p.a) + zi * p.za, p.lda, p.M, m0, kz, p.g, kbeg);
+  B.init(reinterpret_cast<const bf16_t*>(p.b) + bz, p.ldb, p.N, n0, kz, p.g, kbeg);
+  const long zc = (long)split * p.split_stride + cz, zb = zi * p.zbias;
   static_assert(ST == 1 || ST == 3, "stages: 1 or a 3-slot ring");
   auto bfrag = [&](const char* lb, int kk, int j) { return B.frag(lb, kk, j, wn0, lane); };
 

@@ -262,6 +262,47 @@ def class_filter(w, g: ConvGeometry, cl):
     return w.reshape(g.Co, g.T, g.Ci).index_select(1, _tap_index(cl, w.device)).permute(2, 1, 0).contiguous()
 
 
+_CLASS_BATCH = True  # strided data-gradients: every parity class in one launch (GemmParams::zcls)
+
+
+def _class_batch(g: ConvGeometry):
+    """The z order of the parity classes of a strided data-gradient run as ONE launch (heaviest class
+    first, so its workgroups are dispatched first), or None: every class must have taps and the same
+    (Hc, Wc) grid (even H, W at stride 2: ResNet-50's three 3x3 / stride-2 layers), at most 4 classes."""
+    cached = getattr(g, "_zcls", False)
+    if cached is not False:
+        return cached
+    cls = g.classes
+    ok = (_KC_DGRAD and g.implicit_dgrad and (g.sh > 1 or g.sw > 1) and 1 < len(cls) == g.sh * g.sw <= 4
+          and all(c["wt"] for c in cls) and len({(c["Hc"], c["Wc"]) for c in cls}) == 1
+          and cls[0]["Hc"] * g.sh == g.H and cls[0]["Wc"] * g.sw == g.W)
+    order = sorted(cls, key=lambda c: -len(c["wt"])) if ok else None
+    g._zcls = order
+    return order
+
+
+def _dgrad_classes_one_launch(dy, w, g: ConvGeometry, order, dx):
+    """All parity classes of a strided data-gradient in one launch: blockIdx.z = class, the class's taps
+    of one [Ci][taps of all classes][Co] filter copy, its rows scattered to its (oh, ow) cell of dx."""
+    taps, dh, dw, tap0, nt, coff = [], [], [], [], [], []
+    for c in order:
+        tap0.append(len(taps))
+        nt.append(len(c["wt"]))
+        taps += c["wt"]
+        dh += c["dh"]
+        dw += c["dw"]
+        coff.append((c["ph"] * g.W + c["pw"]) * g.Ci)
+    wkc = derived.taps_transpose(w.contiguous(), taps, (g.Ci, len(taps), g.Co))
+    Hc, Wc = order[0]["Hc"], order[0]["Wc"]
+    Mc = g.N * Hc * Wc
+    K = max(nt) * g.Co
+    geom = dict(n=g.N, hi=g.Ho, wi=g.Wo, c=g.Co, ho=Hc, wo=Wc, sh=1, sw=1, tap_c=g.Co, dh=dh, dw=dw)
+    om = dict(gh=Hc, gw=Wc, hy=g.H, wy=g.W, so=g.sh, oh=0, ow=0, zero=0)
+    tile = G.choose_tile(Mc * len(order), g.Ci)
+    C().gemm(dy, wkc, dx, Mc, g.Ci, K, G.KC_GATHER, G.KC, 0, len(taps) * g.Co, g.Ci, G.EPI_BF16, tile, K,
+             geom=geom, outmap=om, zcount=len(order), cls_tap0=tap0, cls_nt=nt, cls_coff=coff)
+
+
 def conv_dgrad_native(dy, w, g: ConvGeometry, resid=None, resid_mask=None, bnr=None, rsub=None):
     """dx = conv^T(dy, w) (+ resid, fused into the epilogue when the layout allows; with
     ``resid_mask`` (1x1 / stride 1 only) only where the residual's ReLU bit is set).  ``bnr``:
@@ -283,7 +324,8 @@ def conv_dgrad_native(dy, w, g: ConvGeometry, resid=None, resid_mask=None, bnr=N
         return dx
     dx = (torch.zeros if g.dgrad_needs_zero else torch.empty)((g.N, g.H, g.W, g.Ci), dtype=torch.bfloat16, device=dev)
     strided = g.sh > 1 or g.sw > 1
-    for cl in g.classes:
+    order = _class_batch(g) if (_CLASS_BATCH and dy.is_contiguous() and w.dtype == torch.bfloat16) else None
+    for cl in (() if order else g.classes):
         nt = len(cl["wt"])
         if nt == 0:
             continue
@@ -317,6 +359,8 @@ def conv_dgrad_native(dy, w, g: ConvGeometry, resid=None, resid_mask=None, bnr=N
             wperm = wperm.contiguous()
             G.gemm(col, wperm, dx, Mc, g.Ci, kp, G.KC, G.KC, kp, kp, g.Ci, G.EPI_BF16, outmap=om, resid=r,
                    ldr=g.Ci if r is not None else 0)
+    if order:
+        _dgrad_classes_one_launch(dy, w, g, order, dx)
     if resid is not None and strided:
         C().add_bf16(dx, resid, dx)
     return dx

@@ -11,6 +11,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 
 from distributeddeeplearningspark_amd.ops import conv as CV
+from distributeddeeplearningspark_amd.ops import derived
+from distributeddeeplearningspark_amd.ops import gemm as G
 
 PEAK_FLOPS = 2.3e15
 PEAK_BW = 6.0e12
@@ -47,6 +49,25 @@ def timeit(fn, reps=10):
     return ts[len(ts) // 2] * 1e-3
 
 
+class _Weights:
+    """Stand-in for a model whose arena holds ``w``: the derived filter copies (flipped / class / transposed
+    weights) then come from one batched launch per call (ops/derived.py), as in a training step, where that
+    one launch serves every layer of the model."""
+
+    def __init__(self, w):
+        self.arena = type("A", (), {"compute": w})()
+
+
+def _in_step(m, fn):
+    def run():
+        derived.begin_step(m)
+        try:
+            return fn()
+        finally:
+            derived.end_step()
+    return run
+
+
 def main():
     N = int(os.environ.get("BATCH", "256"))
     rows, total = [], {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0, "bound": 0.0}
@@ -61,8 +82,18 @@ def main():
         flops = 2.0 * N * Ho * Ho * Co * Ci * k * k
         b_io = 2.0 * x.numel() + 2.0 * dy.numel()
         row = {"H": H, "Ci": Ci, "Co": Co, "k": k, "stride": s, "count": cnt}
+        m = _Weights(w)
+        dgrad = _in_step(m, lambda: CV.conv_dgrad_native(dy, w, g))
+        dg_io = b_io + 2 * w.numel()
+        if k == 1 and s == 2:
+            # ResNet-50's stride-2 1x1 shortcut (ops/fused_blocks.py, _HALF_RES_SC): the data-gradient is a dense GEMM
+            # at half resolution, added at the even pixels by conv1's data-gradient epilogue (rsub) -- no
+            # full-resolution tensor of 3/4 zeros is written
+            row["dgrad_path"] = "half-resolution GEMM (model path)"
+            dgrad = _in_step(m, lambda: G.linear_dgrad(dy.view(-1, Co), w.view(Co, Ci)))
+            dg_io = 2.0 * dy.numel() * (1 + Ci / Co) + 2 * w.numel()
         cases = (("fwd", lambda: CV.conv_fwd_native(x, w, g), b_io + 2 * w.numel()),
-                 ("dgrad", lambda: CV.conv_dgrad_native(dy, w, g), b_io + 2 * w.numel()),
+                 ("dgrad", dgrad, dg_io),
                  ("wgrad", lambda: CV.conv_wgrad_native(dy, x, g, gw), b_io + 4 * w.numel()))
         for name, fn, byts in cases:
             t = timeit(fn)

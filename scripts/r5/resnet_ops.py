@@ -1,5 +1,5 @@
-"""Call sites of the ATen fills / copies inside one ResNet-50 training step (bench.py's DataParallel step,
-batch 256): torch.zeros / zeros_like / full / Tensor.zero_ / fill_ / copy_ / clone on CUDA tensors are
+"""Call sites of the ATen fills / copies inside one ResNet-50 (MODEL=vgg16: VGG-16 CIFAR-shape) training step
+(bench.py's DataParallel step, batch 256): torch.zeros / zeros_like / full / Tensor.zero_ / fill_ / copy_ / clone on CUDA tensors are
 wrapped and counted by the package frame that called them."""
 import collections
 import os
@@ -15,11 +15,17 @@ from distributeddeeplearningspark_amd.parallel import comm
 from distributeddeeplearningspark_amd.parallel.ddp import DataParallel
 
 B = int(os.environ.get("BATCH", "256"))
-m = ResNet50(input_shape=(224, 224, 3), num_classes=1000)
-m.compile(SGD(lr=0.1, momentum=0.9), "sparse_categorical_crossentropy")
+if os.environ.get("MODEL") == "vgg16":
+    from distributeddeeplearningspark_amd.models.zoo import vgg16
+    IMG, NCLS = 32, 10
+    m = vgg16(nb_classes=NCLS, input_shape=(IMG, IMG, 3))
+else:
+    IMG, NCLS = 224, 1000
+    m = ResNet50(input_shape=(IMG, IMG, 3), num_classes=NCLS)
+m.compile(SGD(lr=0.1, momentum=0.9, weight_decay=5e-5), "sparse_categorical_crossentropy")
 m.place("cuda:0", seed=0)  # as bench.py (LOCAL_RANK device)
-x = torch.randint(0, 255, (B, 224, 224, 3), dtype=torch.uint8).pin_memory()
-y = torch.randint(0, 1000, (B,))
+x = torch.randint(0, 255, (B, IMG, IMG, 3), dtype=torch.uint8).pin_memory()
+y = torch.randint(0, NCLS, (B,))
 eng = DataParallel(m, comm.init_from_env(prefer_gpu=True), bucket_mb=32.0)
 step = lambda: eng.train_step(m.to_input(x), m.to_target(y))
 for _ in range(3):

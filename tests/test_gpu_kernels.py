@@ -108,6 +108,7 @@ CONV_CASES = [
     # N, H, W, Ci, Co, k, stride, pad
     (2, 14, 14, 64, 64, 3, 1, 1),
     (2, 15, 15, 64, 128, 3, 2, 1),
+    (2, 14, 14, 128, 64, 3, 2, 1),  # even grid: the four parity classes in one launch (GemmParams::zcls)
     (2, 14, 14, 256, 512, 1, 2, 0),
     (2, 7, 7, 128, 64, 1, 1, 0),
     (2, 32, 32, 3, 64, 7, 2, 3),   # stem: im2col path
@@ -144,6 +145,29 @@ def test_conv_fwd_bwd(case):
     close(xg.grad, xr.grad.permute(0, 2, 3, 1), what=f"conv dgrad {case}")
     close(gw, wr.grad.permute(0, 2, 3, 1), rtol=1e-2, atol=1e-2, what=f"conv wgrad {case}")
     close(gb, br.grad, rtol=1e-2, atol=1e-2, what=f"conv bgrad {case}")
+
+
+@pytest.mark.parametrize("N,H,Ci,Co", [(2, 14, 128, 64), (4, 28, 64, 128), (3, 8, 256, 512)])
+def test_strided_dgrad_classes_one_launch(N, H, Ci, Co, monkeypatch):
+    """3x3 / stride-2 data-gradient: the four parity classes as ONE launch (blockIdx.z = class, heaviest
+    class first) equal the one-launch-per-class path bit for bit, and the fp32 reference; with and
+    without a residual."""
+    from distributeddeeplearningspark_amd.ops import conv as CV
+
+    g = CV.geometry(N, H, H, Ci, Co, 3, 3, (2, 2), (1, 1), (1, 1))
+    assert CV._class_batch(g) is not None and [len(c["wt"]) for c in CV._class_batch(g)] == [4, 2, 2, 1]
+    w = rnd(Co, 3, 3, Ci, scale=1.0 / math.sqrt(9 * Ci), seed=60)
+    dy = rnd(N, g.Ho, g.Wo, Co, seed=61)
+    r = rnd(N, H, H, Ci, seed=62)
+    one = CV.conv_dgrad_native(dy, w, g)
+    one_r = CV.conv_dgrad_native(dy, w, g, resid=r)
+    monkeypatch.setattr(CV, "_CLASS_BATCH", False)
+    per = CV.conv_dgrad_native(dy, w, g)
+    assert torch.equal(one, per)
+    assert torch.equal(one_r, CV.conv_dgrad_native(dy, w, g, resid=r))
+    wr = w.float().permute(0, 3, 1, 2)
+    ref = torch.nn.grad.conv2d_input((N, Ci, H, H), wr, dy.float().permute(0, 3, 1, 2), stride=2, padding=1)
+    close(one, ref.permute(0, 2, 3, 1), what=f"one-launch strided dgrad {N}x{H}x{Ci}->{Co}")
 
 
 @pytest.mark.parametrize("M,N,K", [(20000, 256, 64), (600, 512, 128), (4096, 2048, 512)])
