@@ -96,6 +96,16 @@ int bias_grad(const void* dy, float* db, long M, int N, int accumulate, hipStrea
               const void* relu_y = nullptr, void* relu_dx = nullptr, int zcount = 1, long zdb = 0);
 // zero-padded [R][Kp] copy of a row-strided [R][K] bf16 view
 int pad_cols_bf16(const void* x, long ldx, void* out, long R, int K, int Kp, hipStream_t s);
+constexpr int kMaxZeroRanges = 8;
+struct ZeroRanges {                    // buffers zeroed by one launch: p[k] (16-B aligned), pre[k + 1] - pre[k]
+  void* p[kMaxZeroRanges];             // 16-B vectors followed by tail_words[k] (< 4) 4-B words
+  long pre[kMaxZeroRanges + 1];
+  int tail_words[kMaxZeroRanges];
+  int count;
+};
+int zero_ranges(const ZeroRanges& r, hipStream_t s);
+int gather_bf16(const void* src, const int* idx, void* out, long n, hipStream_t s);
+int scatter_add_f32(const float* src, const int* idx, float* dst, long n, hipStream_t s);
 int bias_grad_rows(long M);
 // c = beta * c + sum over split-K partial slabs ws[splits][M][N] (split order, one writer per element)
 int slab_reduce(const float* ws, int splits, float* c, long M, int N, long ldc, float beta, hipStream_t s);

@@ -134,6 +134,53 @@ __global__ __launch_bounds__(256) void pad_cols_bf16_kernel(const bf16_t* __rest
   }
 }
 
+// Several buffers zeroed by ONE launch (a training step's statistics workspaces and gradient arena):
+// 16-B vector stores over the concatenated ranges, each range's < 16-B tail by the first workgroup.
+__global__ __launch_bounds__(256) void zero_ranges_kernel(const ZeroRanges r) {
+  GRID_LOOP(i, r.pre[r.count]) {
+    int k = 0;
+    while (k + 1 < r.count && i >= r.pre[k + 1]) ++k;
+    reinterpret_cast<uint4*>(r.p[k])[i - r.pre[k]] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  if (blockIdx.x == 0 && (int)threadIdx.x < r.count * 3) {
+    const int k = threadIdx.x / 3, w = threadIdx.x % 3;
+    if (w < r.tail_words[k])
+      reinterpret_cast<uint32_t*>(r.p[k])[(r.pre[k + 1] - r.pre[k]) * 4 + w] = 0u;
+  }
+}
+
+int zero_ranges(const ZeroRanges& r, hipStream_t s) {
+  if (r.count <= 0 || r.count > kMaxZeroRanges) return r.count == 0 ? 0 : (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(zero_ranges_kernel, dim3(mgrid(r.pre[r.count] > 0 ? r.pre[r.count] : 1)), dim3(256), 0, s, r);
+  return (int)hipGetLastError();
+}
+
+// Table-driven re-layout of a small weight: out[i] = idx[i] >= 0 ? src[idx[i]] : 0 (bf16), and its
+// adjoint for the gradient, dst[idx[i]] += src[i] (fp32; idx injective, so no atomics) — the ResNet stem's
+// space-to-depth filter (ops/fused_blocks.py) without the torch pad / permute / add kernels.
+__global__ void gather_bf16_kernel(const bf16_t* __restrict__ src, const int* __restrict__ idx, bf16_t* __restrict__ out, long n) {
+  GRID_LOOP(i, n) {
+    const int j = idx[i];
+    out[i] = j >= 0 ? src[j] : (bf16_t)0;
+  }
+}
+__global__ void scatter_add_f32_kernel(const float* __restrict__ src, const int* __restrict__ idx, float* __restrict__ dst, long n) {
+  GRID_LOOP(i, n) {
+    const int j = idx[i];
+    if (j >= 0) dst[j] += src[i];
+  }
+}
+int gather_bf16(const void* src, const int* idx, void* out, long n, hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(gather_bf16_kernel, dim3(mgrid(n)), dim3(256), 0, s, (const bf16_t*)src, idx, (bf16_t*)out, n);
+  return (int)hipGetLastError();
+}
+int scatter_add_f32(const float* src, const int* idx, float* dst, long n, hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(scatter_add_f32_kernel, dim3(mgrid(n)), dim3(256), 0, s, src, idx, dst, n);
+  return (int)hipGetLastError();
+}
+
 int pad_cols_bf16(const void* x, long ldx, void* out, long R, int K, int Kp, hipStream_t s) {
   if (Kp % 2 || K > Kp || ldx < K) return (int)hipErrorInvalidValue;
   if (R <= 0) return 0;

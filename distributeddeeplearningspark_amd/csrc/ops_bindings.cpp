@@ -359,6 +359,54 @@ void bias_grad_(const at::Tensor& dy, const at::Tensor& db, int64_t N, bool accu
                    ws.defined() ? ws.data_ptr<float>() : nullptr, relu_y ? relu_y->data_ptr() : nullptr,
                    relu_dx ? relu_dx->data_ptr() : nullptr, (int)zcount, (long)zdb));
 }
+// zero several contiguous device buffers (4-B multiples, 16-B aligned, one device) in one launch
+void zero_ranges_(const std::vector<at::Tensor>& ts) {
+  ZeroRanges r{};
+  TORCH_CHECK(ts.size() <= (size_t)kMaxZeroRanges, "zero_ranges: at most ", kMaxZeroRanges, " buffers");
+  for (const auto& t : ts) {
+    GPU(t);
+    TORCH_CHECK(t.is_contiguous() && t.device() == ts[0].device(), "zero_ranges: contiguous buffers on one device");
+    const long bytes = (long)t.numel() * (long)t.element_size();
+    if (bytes == 0) continue;
+    TORCH_CHECK(bytes % 4 == 0 && (uintptr_t)t.data_ptr() % 16 == 0, "zero_ranges: 16-B aligned, 4-B multiple buffers");
+    const int k = r.count++;
+    r.p[k] = t.data_ptr();
+    r.pre[k + 1] = r.pre[k] + bytes / 16;
+    r.tail_words[k] = (int)((bytes % 16) / 4);
+  }
+  if (r.count == 0) return;
+  at::DeviceGuard guard(ts[0].device());
+  HIP_OK(zero_ranges(r, cur_stream()));
+}
+
+// out[i] = src_storage[idx[i]] (0 where idx < 0); idx holds element offsets from src.data_ptr() that the
+// caller derived from src's own strides (ops/fused_blocks.py:_s2d_tables), all inside src's storage
+void gather_bf16_(const at::Tensor& src, const at::Tensor& idx, const at::Tensor& out, int64_t src_extent) {
+  GPU(src);
+  GPU(idx);
+  GPU(out);
+  CK(src.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kBFloat16 && out.is_contiguous(), "gather_bf16: bf16");
+  CK(idx.scalar_type() == at::kInt && idx.is_contiguous() && idx.numel() == out.numel(), "gather_bf16: int32 idx per output");
+  CK(src_extent >= 0 && (int64_t)src.storage().nbytes() / 2 - src.storage_offset() >= src_extent,
+     "gather_bf16: src_extent past src's storage");
+  at::DeviceGuard guard(out.device());
+  HIP_OK(gather_bf16(src.data_ptr(), idx.data_ptr<int>(), out.data_ptr(), out.numel(), cur_stream()));
+}
+
+// dst_storage[idx[i]] += src[i] for idx[i] >= 0 (idx injective: each destination from one source)
+void scatter_add_f32_(const at::Tensor& src, const at::Tensor& idx, const at::Tensor& dst, int64_t dst_extent) {
+  GPU(src);
+  GPU(idx);
+  GPU(dst);
+  F32(src);
+  CK(dst.scalar_type() == at::kFloat, "scatter_add_f32: fp32 destination");
+  CK(idx.scalar_type() == at::kInt && idx.is_contiguous() && idx.numel() == src.numel(), "scatter_add_f32: int32 idx per source");
+  CK(dst_extent >= 0 && (int64_t)dst.storage().nbytes() / 4 - dst.storage_offset() >= dst_extent,
+     "scatter_add_f32: dst_extent past dst's storage");
+  at::DeviceGuard guard(dst.device());
+  HIP_OK(scatter_add_f32(src.data_ptr<float>(), idx.data_ptr<int>(), dst.data_ptr<float>(), src.numel(), cur_stream()));
+}
+
 void pad_cols_bf16_(const at::Tensor& x, const at::Tensor& out) {
   GPU(x); BF16(x); BF16(out);
   CK(x.dim() >= 1 && x.stride(-1) == 1 && out.is_contiguous() && out.dim() == x.dim(), "pad_cols: unit column stride");
@@ -644,6 +692,11 @@ void register_ops(py::module& m) {
   m.def("label_count_inv", &label_count_inv_);
   m.def("rows_sum_scaled", &rows_sum_scaled_);
   m.def("pad_cols_bf16", &pad_cols_bf16_, "zero-padded copy of a row-strided bf16 view");
+  m.def("zero_ranges", &zero_ranges_, "zero up to 8 contiguous device buffers in one launch", py::arg("buffers"));
+  m.def("gather_bf16", &gather_bf16_, "out[i] = src[idx[i]] (0 where idx < 0)", py::arg("src"), py::arg("idx"),
+        py::arg("out"), py::arg("src_extent"));
+  m.def("scatter_add_f32", &scatter_add_f32_, "dst[idx[i]] += src[i] (idx injective, < 0 skipped)", py::arg("src"),
+        py::arg("idx"), py::arg("dst"), py::arg("dst_extent"));
   m.def("scale_bf16_dev", &scale_bf16_dev_);
   m.def("cast_f32_bf16", &cast_f32_bf16_);
   m.def("sum_rows_bf16", &sum_rows_bf16_);

@@ -40,6 +40,7 @@ from ..ops import determinism as _det
 from ..ops import gemm as G
 from ..ops import transformer as T
 from ..ops._native import C, use_native
+from ..ops.norm import new_stats_workspace
 from ..ops._ref import ref_grads
 from ..ops.streams import on_grad_stream
 from . import params as P
@@ -377,7 +378,7 @@ class _BertLayerFn(torch.autograd.Function):
             _wgrad(dpre, a, L.i_w.grad)
             _bias_grad(dpre, L.i_b.grad)
         else:
-            st = torch.zeros((32, 2, c.intermediate_size), dtype=torch.float32, device=dev)
+            st = new_stats_workspace(c.intermediate_size, dev)  # pooled, zeroed with the step's other workspaces
             # d(pre) = (ds2d W2) * gelu'(pre); its column sums (bias grad of W1) come from the epilogue statistics
             dpre = G.linear_dgrad(ds2d, L.out_w.data, gelu_pre=pre, stats=st)
             _wgrad(dpre, a, L.i_w.grad)

@@ -368,8 +368,7 @@ class Model(Layer):
         from ..ops import derived
 
         self._ensure_placed()
-        reset_workspaces(self.device)
-        self.arena.zero_grad()
+        reset_workspaces(self.device, extra=self.arena.zero_grad(defer=True))  # one zeroing launch
         derived.begin_step(self)  # weight-derived filters: one launch per step (ops/derived.py)
         try:
             loss = self.compute_loss(x, y, training=True)

@@ -151,11 +151,16 @@ class ParamArena:
     # -------------------------------------------------------------------------
     grads_zeroed = False  # set by a captured optimizer update that zeroed the gradients it consumed
 
-    def zero_grad(self):
+    def zero_grad(self, defer: bool = False):
+        """Zero the gradient arena; ``defer``: return the arena for the caller to zero (with the step's
+        other workspaces in one launch, ``ops.norm.reset_workspaces``) instead."""
         if self.grads_zeroed:  # the previous (captured) update left them zero: no fill launch
             self.grads_zeroed = False
-            return
+            return None
+        if defer:
+            return self.grad
         self.grad.zero_()
+        return None
 
     def sync_compute(self):
         from ..ops.optim import cast_master_to_compute

@@ -326,6 +326,53 @@ def _s2d_weight_grad(g4, Cc):
     return g[:, :7, :7, :]
 
 
+_S2D_TABLES: dict = {}
+
+
+def _s2d_table(t):
+    """(int32 [Co, 4, 4, 16] table, extent): entry i of the space-to-depth filter is element table[i] of
+    ``t``'s storage from ``t.data_ptr()`` (its own strides: the arena's padded views work), -1 = zero.
+    The same table gathers the bf16 filter (forward) and scatters the fp32 gradient back (backward)."""
+    key = (tuple(t.shape), tuple(t.stride()), str(t.device))
+    hit = _S2D_TABLES.get(key)
+    if hit is None:
+        offs = torch.zeros((), dtype=torch.int64)
+        for d, (n, st) in enumerate(zip(t.shape, t.stride())):
+            offs = offs.unsqueeze(-1) + torch.arange(n, dtype=torch.int64) * st
+        Co, _, _, Cc = t.shape
+        o8 = torch.nn.functional.pad(offs, (0, 0, 0, 1, 0, 1), value=-1)
+        o4 = o8.view(Co, 4, 2, 4, 2, Cc).permute(0, 1, 3, 2, 4, 5).reshape(Co, 4, 4, 4 * Cc)
+        tab = torch.nn.functional.pad(o4, (0, 16 - 4 * Cc), value=-1).contiguous()
+        hit = _S2D_TABLES[key] = (tab.to(torch.int32).to(t.device), int(offs.max()) + 1)
+    return hit
+
+
+def _s2d_weight_dev(w):
+    """``_s2d_weight`` as one table-driven HIP gather (no pad / permute / copy kernels per step)."""
+    if not (w.is_cuda and w.dtype == torch.bfloat16):
+        return _s2d_weight(w)
+    tab, ext = _s2d_table(w)
+    out = torch.empty(tab.shape, dtype=w.dtype, device=w.device)
+    C().gather_bf16(w, tab, out, ext)
+    return out
+
+
+def _s2d_weight_grad_into(conv, g, dyc, xs, Cc):
+    """Stem weight gradient: the 4x4 conv's gradient into a zeroed scratch, scattered (added) into the
+    7x7 filter's gradient by the gather table's adjoint — HIP launches only."""
+    gw = conv.kernel.grad
+    tmp = torch.empty((g.Co, 4, 4, 16), dtype=torch.float32, device=dyc.device)
+    if not gw.is_cuda:
+        tmp.zero_()
+        CV.conv_wgrad_native(dyc, xs, g, tmp)
+        gw.add_(_s2d_weight_grad(tmp, Cc))
+        return
+    C().zero_ranges([tmp])
+    CV.conv_wgrad_native(dyc, xs, g, tmp)
+    tab, ext = _s2d_table(gw)
+    C().scatter_add_f32(tmp, tab, gw, ext)
+
+
 class _StemPoolFn(torch.autograd.Function):
     """ResNet stem conv (7x7 s2 p3 through space-to-depth) + BN + ReLU + 3x3/2 max pool as ONE node:
     the BN affine and ReLU are applied by the pool as it loads the conv output (maxpool_fwd with
@@ -341,7 +388,7 @@ class _StemPoolFn(torch.autograd.Function):
         Ho, Wo = (H + 6 + 1) // 2, (W + 6 + 1) // 2
         xs = torch.empty((N, Ho, Wo, 16), dtype=x.dtype, device=x.device)
         C().s2d_pad(x, xs, 3)
-        w4 = _s2d_weight(conv.kernel.data.detach())
+        w4 = _s2d_weight_dev(conv.kernel.data.detach())
         g = CV.geometry(N, Ho, Wo, 16, conv.filters, 4, 4, (1, 1), (0, 0), (1, 1))
         stats = new_stats_workspace(conv.filters, x.device)
         yc = CV.conv_fwd_native(xs, w4, g, stats=stats)
@@ -387,9 +434,7 @@ class _StemPoolFn(torch.autograd.Function):
         conv = unit.conv
         g = st.g
         with on_grad_stream(dy.device, dyc, xs, default=False):
-            tmp = torch.zeros((g.Co, 4, 4, 16), dtype=torch.float32, device=dy.device)
-            CV.conv_wgrad_native(dyc, xs, g, tmp)
-            conv.kernel.grad.add_(_s2d_weight_grad(tmp, ctx.cc))
+            _s2d_weight_grad_into(conv, g, dyc, xs, ctx.cc)
         if conv.grad_hook is not None:
             conv.grad_hook()
         ctx.st = None
@@ -416,7 +461,7 @@ class _StemS2DFn(torch.autograd.Function):
         Ho, Wo = (H + 6 + 1) // 2, (W + 6 + 1) // 2
         xs = torch.empty((N, Ho, Wo, 16), dtype=x.dtype, device=x.device)
         C().s2d_pad(x, xs, 3)
-        w4 = _s2d_weight(conv.kernel.data.detach())
+        w4 = _s2d_weight_dev(conv.kernel.data.detach())
         g = CV.geometry(N, Ho, Wo, 16, conv.filters, 4, 4, (1, 1), (0, 0), (1, 1))
         stats = new_stats_workspace(conv.filters, x.device)
         yc = CV.conv_fwd_native(xs, w4, g, stats=stats)
@@ -436,9 +481,7 @@ class _StemS2DFn(torch.autograd.Function):
         conv = unit.conv
         g = st.g
         with on_grad_stream(dy.device, dyc, xs, default=False):
-            tmp = torch.zeros((g.Co, 4, 4, 16), dtype=torch.float32, device=dy.device)
-            CV.conv_wgrad_native(dyc, xs, g, tmp)
-            conv.kernel.grad.add_(_s2d_weight_grad(tmp, ctx.cc))
+            _s2d_weight_grad_into(conv, g, dyc, xs, ctx.cc)
         if conv.grad_hook is not None:
             conv.grad_hook()
         ctx.st = None

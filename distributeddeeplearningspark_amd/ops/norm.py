@@ -46,15 +46,19 @@ class _StatsPool:
         return buf[used : used + SHARDS * 2 * C_].view(SHARDS, 2, C_)
 
     def reset(self, device):
+        """Start a new step: returns the part of the pool the last step used (to be zeroed by the caller),
+        or None (nothing used, or a freshly zero-allocated pool sized to the last step's demand)."""
         key = self._key(device)
         want = self.demand.get(key, 0)
         buf = self.buf.get(key)
+        dirty = None
         if want and (buf is None or buf.numel() < want):
             self.buf[key] = torch.zeros(want, dtype=torch.float32, device=device)
         elif buf is not None and self.used.get(key, 0):
-            buf[: self.used[key]].zero_()
+            dirty = buf[: self.used[key]]
         self.used[key] = 0
         self.demand[key] = 0
+        return dirty
 
 
 _POOL = _StatsPool()
@@ -75,10 +79,18 @@ def partials_workspace(M, C_, device):
     return torch.empty((C().bn_partial_rows(M, C_), 2, C_), dtype=torch.float32, device=device)
 
 
-def reset_workspaces(device):
-    """Call once per training step before the forward (zeroes all statistics workspaces)."""
-    if torch.device(device).type == "cuda":
-        _POOL.reset(device)
+def reset_workspaces(device, extra=None):
+    """Call once per training step before the forward: zeroes the statistics workspaces and ``extra``
+    (the gradient arena, when the step needs it zeroed) in ONE launch (``zero_ranges``)."""
+    dirty = _POOL.reset(device) if torch.device(device).type == "cuda" else None
+    bufs = [t for t in (dirty, extra) if t is not None and t.numel()]
+    if not bufs:
+        return
+    if bufs[0].is_cuda:
+        C().zero_ranges(bufs)
+    else:
+        for t in bufs:
+            t.zero_()
 
 
 def bn_ref(x, gamma, beta, mean, var, eps, resid=None, relu=False):

@@ -421,8 +421,7 @@ class DataParallel:
         m = self.model
         phase = timer.phase if timer is not None else (lambda name: trace_range(name))
         with trace_range("train_step"):
-            reset_workspaces(m.device)
-            m.arena.zero_grad()
+            reset_workspaces(m.device, extra=m.arena.zero_grad(defer=True))  # one zeroing launch
             if self.overlap:
                 self._begin()
             from ..ops import derived

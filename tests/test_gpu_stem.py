@@ -38,3 +38,39 @@ def test_stem_s2d_matches_padded_path():
     assert abs(l1 - l0) < 1e-2 * max(1.0, abs(l0)), (l1, l0)
     assert_within_noise(s1, s0, s0b, floor=1e-2, what="stem kernel gradient")
     assert_within_noise(g1, g0, g0b, floor=1e-2, what="arena gradients")
+
+
+def test_s2d_filter_tables_match_torch_relayout():
+    """The table-driven HIP gather (forward filter) and scatter-add (gradient) equal the torch pad / permute
+    forms bit for bit, on a channel-padded arena view ([64, 7, 7, 8] storage, 3 logical channels)."""
+    from distributeddeeplearningspark_amd.ops import fused_blocks as FB
+    from distributeddeeplearningspark_amd.ops._native import C
+
+    torch.manual_seed(3)
+    store = torch.randn(64, 7, 7, 8, device="cuda").to(torch.bfloat16)
+    w = store[..., :3]
+    assert not w.is_contiguous()
+    assert torch.equal(FB._s2d_weight_dev(w), FB._s2d_weight(w))
+    gstore = torch.randn(64, 7, 7, 8, device="cuda")
+    gw = gstore[..., :3]
+    before = gstore.clone()
+    tmp = torch.randn(64, 4, 4, 16, device="cuda")
+    tab, ext = FB._s2d_table(gw)
+    C().scatter_add_f32(tmp, tab, gw, ext)
+    ref = before[..., :3] + FB._s2d_weight_grad(tmp, 3)
+    assert torch.equal(gw, ref)
+    assert torch.equal(gstore[..., 3:], before[..., 3:])  # the pad channels untouched
+
+
+def test_zero_ranges_one_launch():
+    """zero_ranges zeroes several buffers (16-B vectors + 4-B tails) and nothing around them."""
+    from distributeddeeplearningspark_amd.ops._native import C
+
+    big = torch.randn(10_000, device="cuda")
+    a, b, c = big[0:1001], big[1004:3004], big[3008:3013]  # 1001 / 2000 / 5 floats, 16-B aligned starts
+    keep = big.clone()
+    C().zero_ranges([a, b, c, torch.empty(0, device="cuda")])
+    zero = torch.zeros_like(big, dtype=torch.bool)
+    zero[0:1001] = zero[1004:3004] = zero[3008:3013] = True
+    assert (big[zero] == 0).all()
+    assert torch.equal(big[~zero], keep[~zero])
