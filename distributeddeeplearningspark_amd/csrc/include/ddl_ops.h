@@ -54,10 +54,10 @@ int bn_bwd_dx(const void* dy, const void* x, const void* y, const float* scale, 
 // ResNet stem: BN backward through the fused 3x3 / 2 / pad-1 max pool (pooled gradient dy + argmax bytes, the
 // BN output gradient recomputed per pixel, never stored): dx == nullptr -> reduce partials into ws
 // [S][2][C] (one row per workgroup); else dx = A d' + B x + K (coef) — bn.hip
-bool pool3s2_bn_bwd_ok(int N, int H, int W, int C, int Ho, int Wo);
+bool pool3s2_bn_bwd_ok(int N, int H, int W, int C, int Ho, int Wo, int k = 3);  // k: 3 = 3x3/2/p1, 2 = 2x2/2
 int pool3s2_bn_bwd(const void* dy, const uint8_t* am, const void* x, const float* scale, const float* shift,
                    const float* mean, const float* coef, float* ws, int S, void* dx, int N, int H, int W, int C, int Ho,
-                   int Wo, hipStream_t s);
+                   int Wo, hipStream_t s, int k = 3);
 
 // ---------------- pooling (NHWC) ----------------
 int maxpool_fwd(const void* x, void* y, uint8_t* argmax, int N, int H, int W, int C, int Ho, int Wo, int kh, int kw,

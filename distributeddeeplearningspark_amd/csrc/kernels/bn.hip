@@ -640,7 +640,9 @@ namespace ddl {
 //   DX = true : dx = A d' + B x + K with the finalize's coefficients — the dx sweep.
 // A thread owns a 2 x 2 pixel block of one 8-channel vector (the four pooled outputs that can cover it are
 // loaded once); the ColGeom mapping keeps that vector fixed per thread for the column reduction.
-template <bool DX>
+// PK = 2: the same for a 2 x 2 / stride-2 pool (VGG block tails, ops/fused_blocks.py:_ConvBNPoolFn), whose
+// window (bi, bj) is exactly the thread's pixel block.
+template <bool DX, int PK>
 __global__ __launch_bounds__(256) void pool3s2_bn_bwd_kernel(const uint4* __restrict__ dy, const uint2* __restrict__ am,
                                                               const uint4* __restrict__ x, const float* __restrict__ scale,
                                                               const float* __restrict__ shift, const float* __restrict__ mean,
@@ -672,6 +674,7 @@ __global__ __launch_bounds__(256) void pool3s2_bn_bwd_kernel(const uint4* __rest
       const int bj = (int)(q - q2 * (uint32_t)WB);
       const int bi = (int)(q2 % (uint32_t)HB);
       const int n = (int)(q2 / (uint32_t)HB);
+      constexpr int NW = PK == 3 ? 2 : 1;  // pooled windows that can cover a pixel of the block, per axis
       uint2 a[2][2];
       uint4 gv[2][2], xv[2][2];
 #pragma unroll
@@ -679,7 +682,7 @@ __global__ __launch_bounds__(256) void pool3s2_bn_bwd_kernel(const uint4* __rest
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const int oh = bi + i, ow = bj + j;
-          if (oh < Ho && ow < Wo) {
+          if (i < NW && j < NW && oh < Ho && ow < Wo) {
             const uint32_t o = (((uint32_t)n * Ho + oh) * Wo + ow) * (uint32_t)CV + cv;
             a[i][j] = am[o];
             gv[i][j] = dy[o];
@@ -700,12 +703,14 @@ __global__ __launch_bounds__(256) void pool3s2_bn_bwd_kernel(const uint4* __rest
 #pragma unroll
           for (int e = 0; e < 8; ++e) d[e] = 0.f;
 #pragma unroll
-          for (int i = 0; i < 2; ++i)
+          for (int i = 0; i < NW; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-              const int dr = h + 1 - 2 * (bi + i), dc = w + 1 - 2 * (bj + j);  // position inside window
-              if (dr < 0 || dr > 2 || dc < 0 || dc > 2) continue;             // compile-time after unrolling
-              const uint32_t idx = (uint32_t)(dr * 3 + dc);
+            for (int j = 0; j < NW; ++j) {
+              // position inside window (bi + i, bj + j): 3x3 / 2 / pad 1 windows start one row / column before
+              // the block, 2x2 / 2 windows at it
+              const int dr = PK == 3 ? h + 1 - 2 * (bi + i) : pa, dc = PK == 3 ? w + 1 - 2 * (bj + j) : pb;
+              if (dr < 0 || dr >= PK || dc < 0 || dc >= PK) continue;  // compile-time after unrolling
+              const uint32_t idx = (uint32_t)(dr * PK + dc);
               float gf[8];
               unpack8(gv[i][j], gf);
 #pragma unroll
@@ -737,27 +742,37 @@ __global__ __launch_bounds__(256) void pool3s2_bn_bwd_kernel(const uint4* __rest
   if constexpr (!DX) col_reduce_store(acc, g, ws, C);
 }
 
-bool pool3s2_bn_bwd_ok(int N, int H, int W, int C, int Ho, int Wo) {
-  return C % 8 == 0 && C / 8 <= 256 && Ho == (H - 1) / 2 + 1 && Wo == (W - 1) / 2 + 1 &&
+bool pool3s2_bn_bwd_ok(int N, int H, int W, int C, int Ho, int Wo, int k) {
+  const bool shape = k == 3 ? (Ho == (H - 1) / 2 + 1 && Wo == (W - 1) / 2 + 1) : (k == 2 && Ho == H / 2 && Wo == W / 2);
+  return shape && C % 8 == 0 && C / 8 <= 256 &&
          (long)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8) < (1L << 31) && (long)N * H * W * (C / 8) < (1L << 31);
 }
 
 int pool3s2_bn_bwd(const void* dy, const uint8_t* am, const void* x, const float* scale, const float* shift,
                    const float* mean, const float* coef, float* ws, int S, void* dx, int N, int H, int W, int C, int Ho,
-                   int Wo, hipStream_t s) {
-  if (!pool3s2_bn_bwd_ok(N, H, W, C, Ho, Wo)) return (int)hipErrorInvalidValue;
+                   int Wo, hipStream_t s, int k) {
+  if (!pool3s2_bn_bwd_ok(N, H, W, C, Ho, Wo, k)) return (int)hipErrorInvalidValue;
   const int CV = C / 8, CT = CV, RT = 256 / CT;
   const long nq = (long)N * ((H + 1) / 2) * ((W + 1) / 2);
   if (dx) {
     const long gx = (nq + RT - 1) / RT;  // one 2 x 2 block per lane, no grid-stride trips (see bn_grid_cap)
-    hipLaunchKernelGGL(pool3s2_bn_bwd_kernel<true>, dim3((unsigned)gx), dim3(256), 0, s, (const uint4*)dy,
-                       (const uint2*)am, (const uint4*)x, scale, shift, mean, coef, ws, (uint4*)dx, N, H, W, Ho, Wo, C);
+    if (k == 3)
+      hipLaunchKernelGGL((pool3s2_bn_bwd_kernel<true, 3>), dim3((unsigned)gx), dim3(256), 0, s, (const uint4*)dy,
+                         (const uint2*)am, (const uint4*)x, scale, shift, mean, coef, ws, (uint4*)dx, N, H, W, Ho, Wo, C);
+    else
+      hipLaunchKernelGGL((pool3s2_bn_bwd_kernel<true, 2>), dim3((unsigned)gx), dim3(256), 0, s, (const uint4*)dy,
+                         (const uint2*)am, (const uint4*)x, scale, shift, mean, coef, ws, (uint4*)dx, N, H, W, Ho, Wo, C);
   } else {  // one partial row per block: S blocks (the caller's workspace rows; more than a reduce sweep's 512:
             // each thread's 2 x 2 gather is latency-bound, so the sweep needs the extra waves in flight)
     if (S < 1) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(pool3s2_bn_bwd_kernel<false>, dim3((unsigned)S), dim3(256), 0,
-                       s, (const uint4*)dy, (const uint2*)am, (const uint4*)x, scale, shift, mean, coef, ws,
-                       (uint4*)nullptr, N, H, W, Ho, Wo, C);
+    if (k == 3)
+      hipLaunchKernelGGL((pool3s2_bn_bwd_kernel<false, 3>), dim3((unsigned)S), dim3(256), 0, s, (const uint4*)dy,
+                         (const uint2*)am, (const uint4*)x, scale, shift, mean, coef, ws, (uint4*)nullptr, N, H, W, Ho,
+                         Wo, C);
+    else
+      hipLaunchKernelGGL((pool3s2_bn_bwd_kernel<false, 2>), dim3((unsigned)S), dim3(256), 0, s, (const uint4*)dy,
+                         (const uint2*)am, (const uint4*)x, scale, shift, mean, coef, ws, (uint4*)nullptr, N, H, W, Ho,
+                         Wo, C);
   }
   (void)CT;
   return (int)hipGetLastError();

@@ -94,10 +94,14 @@ int maxpool_fwd(const void* x, void* y, uint8_t* argmax, int N, int H, int W, in
                 int sh, int sw, int ph, int pw, hipStream_t s, const float* scale, const float* shift) {
   const long total = (long)N * Ho * Wo * (C / 8);
   if (total >= (1L << 31) || (long)N * H * W * (C / 8) >= (1L << 31)) return (int)hipErrorInvalidValue;
-  if (scale) {  // fused BN + ReLU on load (generic window loop)
+  if (scale) {  // fused BN + ReLU on load (the VGG block tails' 2x2 / 2 unrolled, else the generic window loop)
     if (!shift || kh > 16 || kw > 16) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL((maxpool_fwd_kernel<0, 0, 0, 0, true>), dim3(pgrid(total)), dim3(256), 0, s, (const uint4*)x,
-                       (uint4*)y, (uint2*)argmax, N, H, W, C / 8, Ho, Wo, kh, kw, sh, sw, ph, pw, scale, shift);
+    if (kh == 2 && kw == 2 && sh == 2 && sw == 2)
+      hipLaunchKernelGGL((maxpool_fwd_kernel<2, 2, 2, 2, true>), dim3(pgrid(total)), dim3(256), 0, s, (const uint4*)x,
+                         (uint4*)y, (uint2*)argmax, N, H, W, C / 8, Ho, Wo, kh, kw, sh, sw, ph, pw, scale, shift);
+    else
+      hipLaunchKernelGGL((maxpool_fwd_kernel<0, 0, 0, 0, true>), dim3(pgrid(total)), dim3(256), 0, s, (const uint4*)x,
+                         (uint4*)y, (uint2*)argmax, N, H, W, C / 8, Ho, Wo, kh, kw, sh, sw, ph, pw, scale, shift);
     return (int)hipGetLastError();
   }
 #define DDL_POOL_FWD(A, B, C_, D)                                                                          \

@@ -169,14 +169,15 @@ void bn_bwd_dx_red_(const at::Tensor& dy, const at::Tensor& x, c10::optional<at:
 // bytes, x [N, H, W, C] the pre-BN conv output; phase 0: reduce partials into ws; phase 1: dx with coef
 void pool3s2_bn_bwd_(const at::Tensor& dy, const at::Tensor& am, const at::Tensor& x, const at::Tensor& scale,
                      const at::Tensor& shift, const at::Tensor& mean, const at::Tensor& coef_or_ws,
-                     c10::optional<at::Tensor> dx) {
+                     c10::optional<at::Tensor> dx, int64_t k) {
   GPU(dy); BF16(dy); BF16(x); F32(scale); F32(shift); F32(mean); F32(coef_or_ws);
   CK(dy.dim() == 4 && x.dim() == 4 && dy.size(0) == x.size(0) && dy.size(3) == x.size(3) && dy.is_contiguous() &&
      x.is_contiguous(), "pool3s2_bn_bwd: NHWC dy / x");
   CK(am.scalar_type() == at::kByte && am.numel() == dy.numel() && am.is_contiguous(), "pool3s2_bn_bwd: argmax bytes");
   const int N = (int)x.size(0), H = (int)x.size(1), W = (int)x.size(2), C = (int)x.size(3);
   const int Ho = (int)dy.size(1), Wo = (int)dy.size(2);
-  CK(pool3s2_bn_bwd_ok(N, H, W, C, Ho, Wo), "pool3s2_bn_bwd: 3x3 / 2 / pad-1 pool, C % 8 == 0, C <= 2048");
+  CK(pool3s2_bn_bwd_ok(N, H, W, C, Ho, Wo, (int)k), "pool3s2_bn_bwd: 3x3 / 2 / pad-1 (k = 3) or 2x2 / 2 (k = 2) pool, ",
+     "C % 8 == 0, C <= 2048");
   CK(scale.numel() >= C && shift.numel() >= C && mean.numel() >= C, "pool3s2_bn_bwd: per-channel vectors");
   if (dx) {
     BF16(*dx);
@@ -189,7 +190,7 @@ void pool3s2_bn_bwd_(const at::Tensor& dy, const at::Tensor& am, const at::Tenso
                         shift.data_ptr<float>(), mean.data_ptr<float>(), dx ? coef_or_ws.data_ptr<float>() : nullptr,
                         dx ? nullptr : coef_or_ws.data_ptr<float>(), (int)(coef_or_ws.numel() / (2 * C)),
                         dx ? dx->data_ptr() : nullptr, N, H, W, C, Ho, Wo,
-                        cur_stream()));
+                        cur_stream(), (int)k));
 }
 
 // ---------------------------------------------------------------- pooling
@@ -675,9 +676,10 @@ void register_ops(py::module& m) {
   m.def("bn_bwd_finalize", &bn_bwd_finalize_);
   m.def("bn_bwd_dx", &bn_bwd_dx_);
   m.def("bn_bwd_dx_red", &bn_bwd_dx_red_);
-  m.def("pool3s2_bn_bwd", &pool3s2_bn_bwd_);
-  m.def("pool3s2_bn_bwd_ok", [](int64_t N, int64_t H, int64_t W, int64_t C, int64_t Ho, int64_t Wo) {
-    return pool3s2_bn_bwd_ok((int)N, (int)H, (int)W, (int)C, (int)Ho, (int)Wo);
+  m.def("pool3s2_bn_bwd", &pool3s2_bn_bwd_, py::arg("dy"), py::arg("am"), py::arg("x"), py::arg("scale"),
+        py::arg("shift"), py::arg("mean"), py::arg("coef_or_ws"), py::arg("dx"), py::arg("k") = 3);
+  m.def("pool3s2_bn_bwd_ok", [](int64_t N, int64_t H, int64_t W, int64_t C, int64_t Ho, int64_t Wo, int64_t k) {
+    return pool3s2_bn_bwd_ok((int)N, (int)H, (int)W, (int)C, (int)Ho, (int)Wo, (int)k);
   });
   m.def("maxpool_fwd", &maxpool_fwd_, "NHWC max pool (byte argmax); optional fused BN affine + ReLU on load",
         py::arg("x"), py::arg("y"), py::arg("am"), py::arg("kh"), py::arg("kw"), py::arg("sh"), py::arg("sw"),

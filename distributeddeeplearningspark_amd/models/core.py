@@ -559,7 +559,7 @@ class Sequential(Model):
         loss is the fused softmax-cross-entropy (``logits=True``)."""
         from ..ops._native import use_native
         from ..ops.norm import new_stats_workspace
-        from .layers import Activation, BatchNormalization, Conv2D, Dense
+        from .layers import Activation, BatchNormalization, Conv2D, Dense, MaxPooling2D
 
         L = self.layers
         n = len(L)
@@ -579,8 +579,17 @@ class Sequential(Model):
                 if unit is not None:
                     # conv + BN (+ReLU) as ONE autograd node with a hand-scheduled backward
                     # (ops/fused_blocks.py: half the Python / autograd work per layer)
-                    from ..ops.fused_blocks import convbn_relu
+                    from ..ops.fused_blocks import convbn_relu, convbn_relu_pool
 
+                    nxt3 = L[i + 3] if i + 3 < n else None
+                    if (relu2 and isinstance(nxt3, MaxPooling2D) and nxt3.pool_size == (2, 2)
+                            and nxt3.strides == (2, 2) and nxt3.padding == "valid"):
+                        # ... and the 2x2 max pool behind it: the pool applies BN + ReLU as it loads
+                        y = convbn_relu_pool(unit, x, l.kernel.data)
+                        if y is not None:
+                            x = y
+                            i += 4
+                            continue
                     x = convbn_relu(unit, x, l.kernel.data, relu=relu2)
                     i += 3 if relu2 else 2
                     continue

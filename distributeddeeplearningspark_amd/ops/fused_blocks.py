@@ -412,7 +412,7 @@ class _StemPoolFn(torch.autograd.Function):
         k, s, p = ctx.pool
         dy = dy.contiguous()
         N, H, W, Co = st.yc.shape
-        if _FUSE_STEM_BWD and (k, s, p) == (3, 2, 1) and C().pool3s2_bn_bwd_ok(N, H, W, Co, dy.shape[1], dy.shape[2]):
+        if _FUSE_STEM_BWD and (k, s, p) == (3, 2, 1) and C().pool3s2_bn_bwd_ok(N, H, W, Co, dy.shape[1], dy.shape[2], 3):
             # the BN output gradient (the pool's gather) is recomputed from dy + argmax by the reduce and the dx
             # sweeps instead of being written (411 MB at batch 256) and read back by both
             bn = unit.bn
@@ -488,57 +488,127 @@ class _StemS2DFn(torch.autograd.Function):
         return None, None, None, None  # the stem input is data: no gradient
 
 
+def _seq_conv_forward(ctx, x, unit):
+    """Conv half of a Sequential conv -> BN node (``_ConvBNFn`` / ``_ConvBNPoolFn``): the conv output with
+    its BN statistics fused into the epilogue; records on ``ctx`` what the backward needs."""
+    # a conv -> BN -> ReLU chain (VGG): this conv's data-gradient epilogue accumulates the backward
+    # partial sums of the BN that produced x (mode 2), whose backward then skips its reduce sweep
+    ctx.prev = _producer_of(x) if _FUSE_BNR else None
+    x = x.contiguous()
+    Ci = x.shape[-1]
+    ctx.ci = Ci
+    kp = unit.conv.kernel
+    if Ci % 8:  # stem: pad 3 -> 8 channels (16-B vectors); the arena keeps the filter padded (params.py)
+        cp = -(-Ci // 8) * 8
+        x = ZP.padded(x, cp)
+        w = kp.pdata if kp.pshape[1:] == (*kp.shape[1:3], cp) and kp.pshape[0] == kp.shape[0] \
+            else torch.nn.functional.pad(kp.data.detach(), (0, cp - Ci))
+    else:
+        w = kp.data
+    conv = unit.conv
+    N, H, W, Cp = x.shape
+    kh, kw = conv.kernel_size
+    p = conv.padding if isinstance(conv.padding, tuple) else (kh // 2, kw // 2)
+    g = CV.geometry(N, H, W, Cp, conv.filters, kh, kw, conv.strides, p, conv.dilation_rate)
+    stats = new_stats_workspace(conv.filters, x.device)
+    yc = CV.conv_fwd_native(x, w, g, stats=stats)
+    st = _ConvBNState()
+    st.g, st.yc = g, yc
+    ctx.unit, ctx.st, ctx.w, ctx.x = unit, st, w, x
+    ctx.needs_dx = ctx.needs_input_grad[0]
+    return st, stats
+
+
+def _seq_conv_backward(ctx, dyc):
+    """Weight gradient (side stream) and data gradient of the conv half, given the conv output's gradient."""
+    unit, x = ctx.unit, ctx.x
+    conv = unit.conv
+    g = ctx.st.g
+    with on_grad_stream(dyc.device, dyc, x, default=False):
+        if g.Ci != ctx.ci and ctx.w is not conv.kernel.pdata:
+            tmp = torch.zeros((g.Co, g.KH, g.KW, g.Ci), dtype=torch.float32, device=dyc.device)
+            CV.conv_wgrad_native(dyc, x, g, tmp)
+            conv.kernel.grad.add_(tmp[..., : ctx.ci])
+        else:  # padded storage: it takes the zero-padded channels' (zero) gradients as is
+            CV.conv_wgrad_native(dyc, x, g, conv.kernel.pgrad if ctx.w is conv.kernel.pdata else conv.kernel.grad)
+    if conv.grad_hook is not None:
+        conv.grad_hook()
+    dx = None
+    if ctx.needs_dx:
+        bnr = None if ctx.prev is None else _bnr_mode2(ctx.prev[1], dyc.device)
+        dx = CV.conv_dgrad_native(dyc, ctx.w, g, bnr=bnr)
+        if bnr is not None:
+            _take_reduced(ctx.prev[1], bnr, dx)
+        dx = ZP.logical(dx, ctx.ci)
+    ctx.st = ctx.prev = ctx.x = None
+    return dx
+
+
 class _ConvBNFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, anchor, unit, relu):
-        x = x.contiguous()
-        Ci = x.shape[-1]
-        ctx.ci = Ci
-        kp = unit.conv.kernel
-        if Ci % 8:  # stem: pad 3 -> 8 channels (16-B vectors); the arena keeps the filter padded (params.py)
-            cp = -(-Ci // 8) * 8
-            x = ZP.padded(x, cp)
-            w = kp.pdata if kp.pshape[1:] == (*kp.shape[1:3], cp) and kp.pshape[0] == kp.shape[0] \
-                else torch.nn.functional.pad(kp.data.detach(), (0, cp - Ci))
-        else:
-            w = kp.data
-        conv = unit.conv
-        N, H, W, Cp = x.shape
-        kh, kw = conv.kernel_size
-        p = conv.padding if isinstance(conv.padding, tuple) else (kh // 2, kw // 2)
-        g = CV.geometry(N, H, W, Cp, conv.filters, kh, kw, conv.strides, p, conv.dilation_rate)
-        stats = new_stats_workspace(conv.filters, x.device)
-        yc = CV.conv_fwd_native(x, w, g, stats=stats)
-        st = _ConvBNState()
-        st.g, st.yc = g, yc
-        st.y, st.mean, st.invstd, st.scale, st.shift = _bn_forward(unit.bn, yc, stats, None, relu, True)
+        st, stats = _seq_conv_forward(ctx, x, unit)
+        st.y, st.mean, st.invstd, st.scale, st.shift = _bn_forward(unit.bn, st.yc, stats, None, relu, True)
         st.mode = 2 if relu else 0
-        ctx.unit, ctx.st, ctx.w = unit, st, w
-        ctx.save_for_backward(x)
-        ctx.needs_dx = ctx.needs_input_grad[0]
+        _register_output(st.y, unit, st)
         return st.y
 
     @staticmethod
     def backward(ctx, dy):
-        (x,) = ctx.saved_tensors
-        unit, st = ctx.unit, ctx.st
-        dyc, _ = bn_backward(unit, st, dy.contiguous(), False)
-        conv = unit.conv
-        g = st.g
-        with on_grad_stream(dy.device, dyc, x, default=False):
-            if g.Ci != ctx.ci and ctx.w is not conv.kernel.pdata:
-                tmp = torch.zeros((g.Co, g.KH, g.KW, g.Ci), dtype=torch.float32, device=dy.device)
-                CV.conv_wgrad_native(dyc, x, g, tmp)
-                conv.kernel.grad.add_(tmp[..., : ctx.ci])
-            else:  # padded storage: it takes the zero-padded channels' (zero) gradients as is
-                CV.conv_wgrad_native(dyc, x, g, conv.kernel.pgrad if ctx.w is conv.kernel.pdata else conv.kernel.grad)
-        if conv.grad_hook is not None:
-            conv.grad_hook()
-        dx = None
-        if ctx.needs_dx:
-            dx = ZP.logical(CV.conv_dgrad_native(dyc, ctx.w, g), ctx.ci)
-        ctx.st = None
-        return dx, None, None, None
+        dyc, _ = bn_backward(ctx.unit, ctx.st, dy.contiguous(), False)
+        return _seq_conv_backward(ctx, dyc), None, None, None
+
+
+_SEQ_POOL = True  # Sequential conv -> BN -> ReLU -> 2x2 / 2 max pool as one node (tests compare with False)
+
+
+class _ConvBNPoolFn(torch.autograd.Function):
+    """VGG block tail conv -> BN -> ReLU -> 2x2 / stride-2 max pool as ONE node: the pool applies the BN
+    affine + ReLU as it loads the conv output (no BN-apply sweep, the full-resolution activation is never
+    written); backward: the BN's output gradient is the pool's scatter of the pooled gradient by the argmax
+    bytes, recomputed inside the reduce and dx sweeps (``pool_bn_bwd``, k = 2) instead of written by a pool
+    backward and read twice."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, unit):
+        st, stats = _seq_conv_forward(ctx, x, unit)
+        st.y, st.mean, st.invstd, st.scale, st.shift = _bn_forward(unit.bn, st.yc, stats, None, True, True,
+                                                                    apply=False)
+        st.mode = 2
+        N, Hc, Wc, Co = st.yc.shape
+        y = torch.empty((N, Hc // 2, Wc // 2, Co), dtype=st.yc.dtype, device=st.yc.device)
+        ctx.am = torch.empty(y.shape, dtype=torch.uint8, device=y.device)
+        C().maxpool_fwd(st.yc, y, ctx.am, 2, 2, 2, 2, 0, 0, st.scale, st.shift)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        st, bn = ctx.st, ctx.unit.bn
+        dy = dy.contiguous()
+        N, H, W, Co = st.yc.shape
+        M = N * H * W
+        # one partial row per workgroup, each workgroup one pass over its 256 / (C / 8) rows of 2x2 blocks
+        rows = -(-(N * (H // 2) * (W // 2)) // max(1, 256 // (Co // 8)))
+        ws = torch.empty((min(_STEM_PARTIALS, rows), 2, Co), dtype=torch.float32, device=dy.device)
+        C().pool3s2_bn_bwd(dy, ctx.am, st.yc, st.scale, st.shift, st.mean, ws, None, 2)
+        coef = torch.empty(3 * Co, dtype=torch.float32, device=dy.device)
+        C().bn_bwd_finalize(ws, M, Co, bn.gamma.master, st.mean, st.invstd, bn.gamma.grad, bn.beta.grad, coef)
+        dyc = torch.empty_like(st.yc)
+        C().pool3s2_bn_bwd(dy, ctx.am, st.yc, st.scale, st.shift, st.mean, coef, dyc, 2)
+        if bn.grad_hook is not None:
+            bn.grad_hook()
+        ctx.am = None
+        return _seq_conv_backward(ctx, dyc), None, None
+
+
+def convbn_relu_pool(unit, x, anchor):
+    """Sequential conv -> BN -> ReLU -> MaxPooling2D(2, 2) as one node, or None when it does not apply."""
+    conv = unit.conv
+    if not _SEQ_POOL or conv.filters % 8 or conv.filters > 2048 or tuple(conv.strides) != (1, 1):
+        return None
+    if not (x.is_cuda and x.dtype == torch.bfloat16) or x.shape[1] % 2 or x.shape[2] % 2:
+        return None
+    return _ConvBNPoolFn.apply(x, anchor, unit)
 
 
 _ = G

@@ -911,11 +911,12 @@ def test_dma_dgrad_fused_bn_reduce_with_residual(M, N, K, rsub):
     close(got[1], s2, rtol=1e-4, atol=1e-2 * s2.abs().mean().item(), what="sum d (x - mean)")
 
 
-@pytest.mark.parametrize("N,H,C", [(16, 112, 64), (8, 57, 32)])
-def test_stem_pool_bn_backward_fused(N, H, C):
-    """pool3s2_bn_bwd: the stem BN's reduce and dx sweeps computed through the 3x3 / 2 / pad-1 max pool's
-    gather (pooled gradient + argmax bytes) match maxpool_bwd -> bn_bwd_reduce -> bn_bwd_dx (mode 2) on the
-    materialised pool gradient: partial sums to fp32 rounding, dx to bf16 rounding."""
+@pytest.mark.parametrize("N,H,C,k", [(16, 112, 64, 3), (8, 57, 32, 3), (32, 32, 64, 2), (64, 4, 512, 2), (8, 16, 128, 2)])
+def test_stem_pool_bn_backward_fused(N, H, C, k):
+    """pool3s2_bn_bwd: the BN's reduce and dx sweeps computed through the max pool's gather (pooled gradient
+    + argmax bytes) — the stem's 3x3 / 2 / pad-1 pool (k = 3) or a VGG block's 2x2 / 2 pool (k = 2) — match
+    maxpool_bwd -> bn_bwd_reduce -> bn_bwd_dx (mode 2) on the materialised pool gradient: partial sums to
+    fp32 rounding, dx to bf16 rounding."""
     from distributeddeeplearningspark_amd.ops._native import C as NC
     from distributeddeeplearningspark_amd.ops.norm import partials_workspace
 
@@ -924,19 +925,20 @@ def test_stem_pool_bn_backward_fused(N, H, C):
     scale = (torch.rand(C, generator=gen) + 0.5).to(DEV)
     shift = (torch.randn(C, generator=gen) * 0.5).to(DEV)
     mean = (torch.randn(C, generator=gen) * 0.1).to(DEV)
-    Ho = (H - 1) // 2 + 1
+    p = 1 if k == 3 else 0
+    Ho = (H + 2 * p - k) // 2 + 1
     y = torch.empty(N, Ho, Ho, C, dtype=torch.bfloat16, device=DEV)
     am = torch.empty(N, Ho, Ho, C, dtype=torch.uint8, device=DEV)
-    NC().maxpool_fwd(x, y, am, 3, 3, 2, 2, 1, 1, scale, shift)
+    NC().maxpool_fwd(x, y, am, k, k, 2, 2, p, p, scale, shift)
     dy = torch.randn(N, Ho, Ho, C, generator=gen).to(DEV, torch.bfloat16)
     d = torch.empty_like(x)
-    NC().maxpool_bwd(dy, am, d, 3, 3, 2, 2, 1, 1)
+    NC().maxpool_bwd(dy, am, d, k, k, 2, 2, p, p)
     M = N * H * H
     ws_ref = partials_workspace(M, C, DEV)
     NC().bn_bwd_reduce(d, x, None, scale, shift, mean, ws_ref, C, 2)
     ws = torch.empty((1024, 2, C), dtype=torch.float32, device=DEV)
-    assert NC().pool3s2_bn_bwd_ok(N, H, H, C, Ho, Ho)
-    NC().pool3s2_bn_bwd(dy, am, x, scale, shift, mean, ws, None)
+    assert NC().pool3s2_bn_bwd_ok(N, H, H, C, Ho, Ho, k)
+    NC().pool3s2_bn_bwd(dy, am, x, scale, shift, mean, ws, None, k)
     ref, got = ws_ref.double().sum(0).cpu(), ws.double().sum(0).cpu()
     close(got[0], ref[0], rtol=1e-4, atol=1e-4 * ref[0].abs().mean().item(), what="sum d'")
     close(got[1], ref[1], rtol=1e-4, atol=1e-4 * ref[1].abs().mean().item(), what="sum d' (x - mean)")
@@ -944,7 +946,7 @@ def test_stem_pool_bn_backward_fused(N, H, C):
     dx_ref = torch.empty_like(x)
     NC().bn_bwd_dx(d, x, None, scale, shift, coef, dx_ref, None, C, 2)
     dx = torch.empty_like(x)
-    NC().pool3s2_bn_bwd(dy, am, x, scale, shift, mean, coef, dx)
+    NC().pool3s2_bn_bwd(dy, am, x, scale, shift, mean, coef, dx, k)
     close(dx.float(), dx_ref.float(), rtol=1e-2, atol=1e-2, what="dx")
 
 
