@@ -874,7 +874,9 @@ __global__ __launch_bounds__(NTHREADS, (dma_min_blocks<EPI>())) void gemm_dma_ke
   const long zi = blockIdx.z;  // replica of a batched launch (GemmParams::zcount) / parity class (zcls), else 0
   int kz = p.K, tap0 = 0;
   long bz = zi * p.zb, cz = zi * p.zc;
-  if (p.zcls) {  // parity class zi of a strided data-gradient (GemmParams::zcls)
+  // parity class zi of a strided data-gradient (GemmParams::zcls; only the gathered bf16 conv instantiation: the
+  // extra live values cost the plain 128x128 full-epilogue kernels 16 B/lane of VGPR spills)
+  if (AMODE == OP_KC_GATHER && BMODE == OP_KC && EPI == EPI_BF16 && p.zcls) {
     tap0 = p.cls_tap0[zi];
     kz = p.cls_nt[zi] * p.g.tap_c;
     bz = (long)tap0 * p.g.tap_c;
