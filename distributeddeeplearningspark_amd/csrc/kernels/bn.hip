@@ -259,8 +259,9 @@ __device__ __forceinline__ bool sum_partials(const float* ws, int S, int C, int&
   return true;
 }
 
-// threads of a finalize block: 16 row-lanes for long partial-row lists, 4 for the shard rows
-static int finalize_threads(int S) { return S > 64 ? 1024 : 256; }
+// threads of a finalize block: 16 row-lanes for long partial-row lists, 8 for the 32 shard rows (each lane's
+// four rows loaded in one round: the kernel is a chain of memory latencies)
+static int finalize_threads(int S) { return S > 64 ? 1024 : 512; }
 
 __global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* ws, int S, long M, int C, const float* gamma,
                                                           const float* beta, float eps, float momentum, float* rmean,
