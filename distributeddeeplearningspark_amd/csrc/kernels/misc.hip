@@ -448,8 +448,12 @@ int normalize_u8(const uint8_t* x, void* y, long npix, int c, int cpad, const fl
 // y [N][Ho][Wo][16], y[n][I][J][(2a + b) * C + ch] = x[n][2I + a - pad][2J + b - pad][ch] (0 outside),
 // channels 4C..15 zero.  A 7x7 stride-2 conv on x equals a 4x4 stride-1 conv on y, with 12 of 16
 // channels used instead of 3 of 8 after the 16-B channel padding (see ops/conv.py stem path).
-__global__ void s2d_pad_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int N, int H, int W, int C,
+// CC: the channel count as a compile-time constant (3: the RGB stem, every source load of a pixel block issued
+// back to back), 0 = the runtime C
+template <int CC>
+__global__ void s2d_pad_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int N, int H, int W, int C_,
                                int Ho, int Wo, int pad) {
+  const int C = CC ? CC : C_;
   const long pix = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (pix >= (long)N * Ho * Wo) return;
   const int J = (int)(pix % Wo);
@@ -466,7 +470,9 @@ __global__ void s2d_pad_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict_
       const int r = 2 * I + a - pad, c = 2 * J + b - pad;
       if ((unsigned)r < (unsigned)H && (unsigned)c < (unsigned)W) {
         const bf16_t* src = x + (((long)n * H + r) * W + c) * C;
-        for (int ch = 0; ch < C; ++ch) v[(2 * a + b) * C + ch] = src[ch];
+#pragma unroll
+        for (int ch = 0; ch < (CC ? CC : 4); ++ch)
+          if (CC || ch < C) v[(2 * a + b) * C + ch] = src[ch];
       }
     }
   uint4* dst = reinterpret_cast<uint4*>(y + pix * 16);
@@ -476,8 +482,13 @@ __global__ void s2d_pad_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict_
 
 int s2d_pad(const void* x, void* y, int N, int H, int W, int C, int Ho, int Wo, int pad, hipStream_t s) {
   const long n = (long)N * Ho * Wo;
-  hipLaunchKernelGGL(s2d_pad_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
-                     reinterpret_cast<const bf16_t*>(x), reinterpret_cast<bf16_t*>(y), N, H, W, C, Ho, Wo, pad);
+  if (C > 4) return (int)hipErrorInvalidValue;
+  if (C == 3)
+    hipLaunchKernelGGL(s2d_pad_kernel<3>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                       reinterpret_cast<const bf16_t*>(x), reinterpret_cast<bf16_t*>(y), N, H, W, C, Ho, Wo, pad);
+  else
+    hipLaunchKernelGGL(s2d_pad_kernel<0>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                       reinterpret_cast<const bf16_t*>(x), reinterpret_cast<bf16_t*>(y), N, H, W, C, Ho, Wo, pad);
   return (int)hipGetLastError();
 }
 
