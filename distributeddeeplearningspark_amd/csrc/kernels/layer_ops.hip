@@ -194,10 +194,12 @@ __global__ __launch_bounds__(256) void filter_taps_transpose_kernel(const bf16_t
 // src [Co][T][Ci] into dst [Ci][nt][Co] over the taps taps[0..nt) (a flipped stride-1 dgrad filter, a strided
 // dgrad class filter, or — T = nt = 1 — a plain [N][K] -> [K][N] weight transpose for a Linear dgrad).  The
 // blocks of all jobs form one grid; a block finds its job in the (device-resident, per-model) table.
-// plain [N][K] -> [K][N] transposes in 64-multiples (a BERT weight): 64x64 tiles moved as 16-B vectors both
-// ways (the 2-B element tiles ran ~330 us for BERT-base's 85 M parameters per step)
+// jobs with Co, Ci in 64-multiples (BERT weights, every ResNet-50 filter but the stem's): 64x64 tiles of one tap
+// moved as 16-B vectors both ways (the 2-B element tiles ran ~330 us for BERT-base's 85 M parameters per step)
 __device__ __forceinline__ bool taps_job_vec(int Co, int Ci, int T, int nt) {
-  return T == 1 && nt == 1 && Co % 64 == 0 && Ci % 64 == 0;
+  (void)T;
+  (void)nt;
+  return Co % 64 == 0 && Ci % 64 == 0;  // any tap count: one 64 x 64 tile of one tap per block
 }
 
 __global__ __launch_bounds__(256) void taps_batch_kernel(const TapsJob* __restrict__ jobs, int njobs) {
@@ -209,13 +211,16 @@ __global__ __launch_bounds__(256) void taps_batch_kernel(const TapsJob* __restri
   const TapsJob& jb = jobs[j];
   const int Co = jb.Co, Ci = jb.Ci, T = jb.T, nt = jb.nt;
   if (taps_job_vec(Co, Ci, T, nt)) {
-    const int local = blk - jb.blk0, nbi = Ci >> 6;
-    const int co0 = (local / nbi) * 64, ci0 = (local % nbi) * 64;
+    const int nbi = Ci >> 6, nbo = Co >> 6;
+    const int local = blk - jb.blk0;
+    const int t = local / (nbi * nbo), rem = local - t * nbi * nbo;
+    const int co0 = (rem / nbi) * 64, ci0 = (rem % nbi) * 64;
+    const int src_t = jb.taps[t];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {  // 64 rows (co) x 8 vectors (ci)
+    for (int i = 0; i < 2; ++i) {  // 64 rows (co) x 8 vectors (ci) of source tap src_t
       const int idx = threadIdx.x + 256 * i, r = idx >> 3, cv = idx & 7;
       *reinterpret_cast<uint4*>(&vt[r][cv * 8]) =
-          *reinterpret_cast<const uint4*>(jb.src + (long)(co0 + r) * Ci + ci0 + cv * 8);
+          *reinterpret_cast<const uint4*>(jb.src + ((long)(co0 + r) * T + src_t) * Ci + ci0 + cv * 8);
     }
     __syncthreads();
 #pragma unroll
@@ -225,7 +230,7 @@ __global__ __launch_bounds__(256) void taps_batch_kernel(const TapsJob* __restri
 #pragma unroll
       for (int k = 0; k < 4; ++k)
         w[k] = (uint32_t)vt[cv * 8 + 2 * k][r] | ((uint32_t)vt[cv * 8 + 2 * k + 1][r] << 16);
-      *reinterpret_cast<uint4*>(jb.dst + (long)(ci0 + r) * Co + co0 + cv * 8) = make_uint4(w[0], w[1], w[2], w[3]);
+      *reinterpret_cast<uint4*>(jb.dst + ((long)(ci0 + r) * nt + t) * Co + co0 + cv * 8) = make_uint4(w[0], w[1], w[2], w[3]);
     }
     return;
   }
@@ -362,7 +367,7 @@ int taps_batch(const TapsJob* jobs, int njobs, int blocks, hipStream_t s) {
 }
 
 int taps_job_blocks(int Co, int Ci, int nt, int T) {
-  if (T == 1 && nt == 1 && Co % 64 == 0 && Ci % 64 == 0) return (Ci / 64) * (Co / 64);  // = taps_job_vec
+  if (Co % 64 == 0 && Ci % 64 == 0) return (Ci / 64) * (Co / 64) * nt;  // = taps_job_vec
   return ((Ci + 31) / 32) * ((Co + 31) / 32) * nt;
 }
 

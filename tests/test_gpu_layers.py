@@ -453,7 +453,8 @@ def test_taps_batch_mixed_jobs_match_reference():
         dsts.append(torch.empty(Cc, R, dtype=torch.bfloat16, device=DEV))
         taps.append([0])
         refs.append(w.t())
-    for Co, Ci, tp in ((64, 32, list(range(8, -1, -1))), (24, 16, [0, 2, 6, 8])):
+    for Co, Ci, tp in ((64, 32, list(range(8, -1, -1))), (24, 16, [0, 2, 6, 8]), (128, 64, list(range(8, -1, -1))),
+                       (64, 128, [4, 3, 5, 1, 7, 0, 2, 6, 8]), (128, 128, [4, 1, 7])):
         w = torch.randn(Co, 3, 3, Ci, device=DEV, generator=g).to(torch.bfloat16)
         srcs.append(w)
         dsts.append(torch.empty(Ci, len(tp), Co, dtype=torch.bfloat16, device=DEV))
