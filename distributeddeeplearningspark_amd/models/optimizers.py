@@ -51,7 +51,12 @@ class Optimizer:
         for k, v in sd.items():
             if k in self.state:
                 v = v.to(self.state[k].device)
-                if self.arena is not None and v.numel() != self.state[k].numel():
+                if self.arena is not None and self.arena.padded:
+                    # state_dict() always saves the canonical layout; the two layouts can have the same
+                    # numel (padding inside the ALIGN rounding) while placing values differently
+                    if v.numel() != self.arena.canon_numel:
+                        raise ValueError(f"optimizer slot {k!r}: {v.numel()} elements, the canonical layout "
+                                         f"has {self.arena.canon_numel}")
                     v = self.arena.from_canonical(v)
                 self.state[k].copy_(v)
         if self.device_step is not None:

@@ -153,6 +153,34 @@ def test_canonical_flat_roundtrip_between_layouts():
         a16.set_flat(a16.master)  # storage layout is not a canonical flat
 
 
+def test_optimizer_state_roundtrip_when_layouts_have_equal_numel():
+    """A Dense(3) on 5 features: the padded (8, 8) kernel and the canonical (5, 3) one both round up to one
+    64-element ALIGN block, so the storage and canonical flats have the SAME numel with different placement.
+    Loading saved optimizer state must still convert it (values landed in the padding)."""
+    from distributeddeeplearningspark_amd.models import optimizers as O
+    from distributeddeeplearningspark_amd.models import params as P
+
+    def mk():
+        return [P.Param("d/kernel", (5, 3), P.uniform(0.5), pad=(8, 8)), P.Param("d/bias", (3,), P.ones, pad=(8,))]
+
+    a16, a32 = P.ParamArena(mk(), "cpu", torch.bfloat16, seed=1), P.ParamArena(mk(), "cpu", torch.float32, seed=1)
+    assert a16.padded and a16.canon_numel == a16.numel == a32.numel
+    for opt in (O.Adam, lambda: O.SGD(momentum=0.9)):
+        o16, o32 = opt().bind(a16), opt().bind(a32)
+        for k in o32.state:
+            for p, co in zip(a32.params, a32.canon_offsets):
+                o32.state[k][co:co + p.numel].uniform_(0.5, 1.5)
+        o16.load_state_dict(o32.state_dict())
+        for k in o32.state:
+            torch.testing.assert_close(o16.state_dict()[k], o32.state_dict()[k], rtol=0, atol=0)
+            for p in a16.params:  # the padding slots of the storage layout stay zero
+                pad = torch.ones(p.pshape, dtype=torch.bool)
+                pad[p.logical] = False
+                assert o16.state[k][p.offset:p.offset + p.snumel].view(p.pshape)[pad].abs().max() == 0
+        with pytest.raises(ValueError):
+            o16.load_state_dict({k: torch.zeros(a16.canon_numel + 64) for k in o32.state})
+
+
 def test_replica_seq_plan_parses_the_mnist_network():
     """parallel/replica_seq.py's launch plan of the reference's MNIST CNN: conv(+ReLU) x2, pool, flatten,
     Dense(+ReLU), softmax head; unsupported layers (strided conv, Dropout, BatchNormalization) refuse the
