@@ -193,8 +193,11 @@ int embed_bwd(const int64_t* ids, const int64_t* types, const void* ds, float* g
 // Replica-batched recurrent step (parallel/replica_batch.py): R co-located dist-keras workers whose models
 // are RNN(H) -> Dense(K) with an MSE loss step as ONE launch per phase.  Replica r owns global batch
 // rows [r B, (r+1) B) of every activation buffer; parameters, gradients, optimizer state and the resident
-// shard are its own (pointer tables).  The replicas step in lockstep: one device step counter.
-constexpr int kMaxRnnRep = 8;
+// shard are its own (pointer tables).  The replicas step in lockstep on one device step counter; shards may
+// be ragged (the reference's repartition(num_workers) shards differ by a row, ddl_nyiso_aztk.py:193): replica r
+// fetches mini-batch ctr % nbr[r] and is live while ctr < steps[r] — past that it neither records, ticks nor
+// updates its parameters (the per-replica path's exhausted worker), while the others keep stepping.
+constexpr int kMaxRnnRep = 16;
 struct RnnRep {
   const float* x[kMaxRnnRep];  // resident input shard [nb B][T][I]
   const float* y[kMaxRnnRep];  // resident target shard [nb B][K]
@@ -208,9 +211,12 @@ struct RnnRep {
   float* gb[kMaxRnnRep];
   float* gWd[kMaxRnnRep];
   float* gbd[kMaxRnnRep];
-  float* hist[kMaxRnnRep];     // per-replica loss history [cap]
-  int* ctr;                    // device step counter (batch index = ctr % nb, history slot = ctr)
-  int nb, B, K, cap;
+  float* hist[kMaxRnnRep];     // per-replica loss history [>= steps[r]]
+  int nbr[kMaxRnnRep];         // mini-batches per epoch of replica r's shard
+  int steps[kMaxRnnRep];       // steps replica r takes in total (live while ctr < steps[r])
+  int* ctr;                    // device step counter (batch index = ctr % nbr[r], history slot = ctr)
+  int* live;                   // [R] live flags of the current step (written by the head kernel)
+  int B, K;
 };
 struct OptRep {
   float* w[kMaxRnnRep];
@@ -326,14 +332,24 @@ struct ReplicaPtrs {
 };
 int commit_replicas(const ReplicaPtrs& rp, int nr, float* center, float* sum, long n, int elastic, int mode,
                     hipStream_t s);
-constexpr int kMaxBatchCopies = 16;  // 2 per replica of a batched group (parallel/replica_seq.py)
+constexpr int kMaxBatchCopies = 32;  // 2 per replica of a batched group (parallel/replica_seq.py)
 struct BatchCopy {
   const void* src[kMaxBatchCopies];
   void* dst[kMaxBatchCopies];
-  long bytes[kMaxBatchCopies];  // bytes of ONE mini-batch of copy q
-  long nbatch;                  // mini-batches per epoch
+  long bytes[kMaxBatchCopies];   // bytes of ONE mini-batch of copy q
+  long nbatch[kMaxBatchCopies];  // mini-batches per epoch of copy q's shard (ragged shards differ)
 };
 int batch_fetch(const BatchCopy& bc, int ncopy, const int* ctr, hipStream_t s);
-int step_record(const float* loss, float* hist, int cap, int* ctr, hipStream_t s, int nrep = 1);
+// steps (nullable, int32 [nrep]): replica r records only while ctr < steps[r]; ts (nullable, fp32 [nrep]): the
+// live replicas' Adam step counters advance by one (after the stacked optimizer below has read them)
+int step_record(const float* loss, float* hist, int cap, int* ctr, hipStream_t s, int nrep = 1,
+                const int* steps = nullptr, float* ts = nullptr);
+// Optimizer sweep over R stacked replica arenas [R][n] (parallel/replica_seq.py): replica r is live while
+// *ctr < steps[r] (ragged shards), a dead replica keeps its parameters and state; gradients are zeroed either
+// way.  opt 0: SGD (+ momentum mu, s1), 2: Adam (s1 = m, s2 = v, t = ts[r] + 1, amode bit0 AdamW, bit1 Keras
+// epsilon).  w16 (nullable): bf16 compute copy [R][n].
+int opt_stack_step(int opt, float* w, float* g, float* s1, float* s2, void* w16, long n, int R, const int* ctr,
+                   const int* steps, const float* ts, float lr, float mu, float b1, float b2, float eps, float wd,
+                   int amode, hipStream_t s);
 
 }  // namespace ddl

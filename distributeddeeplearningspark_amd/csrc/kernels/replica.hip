@@ -85,7 +85,7 @@ __global__ __launch_bounds__(256) void commit_replicas_kernel(ReplicaPtrs rp, in
 __global__ __launch_bounds__(256) void batch_fetch_kernel(BatchCopy bc, int ncopy, const int* __restrict__ ctr) {
   const int q = blockIdx.y;
   if (q >= ncopy) return;
-  const long nb = bc.nbatch;
+  const long nb = bc.nbatch[q];
   const long b = (long)(*ctr) % nb;
   const long bytes = bc.bytes[q];
   const char* src = reinterpret_cast<const char*>(bc.src[q]) + b * bytes;
@@ -102,14 +102,72 @@ __global__ __launch_bounds__(256) void batch_fetch_kernel(BatchCopy bc, int ncop
 }
 
 // hist[ctr] = loss (while ctr < cap); ctr += 1 — one lane, vector memory only
-// nrep replicas (replica batching): loss[r] -> hist[r * cap + step], one shared step counter
+// nrep replicas (replica batching): loss[r] -> hist[r * cap + step], one shared step counter; with steps,
+// replica r records (and ticks its Adam counter ts[r]) only while it is live (ctr < steps[r])
 __global__ void step_record_kernel(const float* __restrict__ loss, float* __restrict__ hist, int cap, int* ctr,
-                                   int nrep) {
+                                   int nrep, const int* __restrict__ steps, float* __restrict__ ts) {
   if (threadIdx.x == 0) {
     const int c = *ctr;
-    if (hist && c < cap)
-      for (int r = 0; r < nrep; ++r) hist[(long)r * cap + c] = loss[r];
+    for (int r = 0; r < nrep; ++r) {
+      if (steps && c >= steps[r]) continue;
+      if (hist && c < cap) hist[(long)r * cap + c] = loss[r];
+      if (ts) ts[r] += 1.f;
+    }
     *ctr = c + 1;
+  }
+}
+
+// stacked replica optimizer (opt_stack_step): blockIdx.y = replica; no block writes ctr or ts (step_record
+// advances both after this launch), so every block reads the same step
+template <int OPT>
+__global__ __launch_bounds__(256) void opt_stack_kernel(float4* __restrict__ w, float4* __restrict__ g,
+                                                        float4* __restrict__ s1, float4* __restrict__ s2, void* w16,
+                                                        long n4, const int* __restrict__ ctr,
+                                                        const int* __restrict__ steps, const float* __restrict__ ts,
+                                                        float lr, float mu, float b1, float b2, float eps, float wd,
+                                                        int amode) {
+  const long r = blockIdx.y;
+  const bool live = *ctr < steps[r];
+  const long base = r * n4;
+  float bc1 = 1.f, bc2 = 1.f;
+  if constexpr (OPT == 2) {
+    const float t = ts[r] + 1.f;
+    bc1 = 1.f - powf(b1, t);
+    bc2 = 1.f - powf(b2, t);
+  }
+  const float sbc2 = sqrtf(bc2);
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    const long k4 = base + i;
+    if (live) {
+      float4 p = w[k4], d = g[k4];
+      float4 a = s1 ? s1[k4] : make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 v = OPT == 2 ? s2[k4] : make_float4(0.f, 0.f, 0.f, 0.f);
+      float *pp = &p.x, *dd = &d.x, *aa = &a.x, *vv = &v.x;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if constexpr (OPT == 0) {
+          float gg = dd[k] + wd * pp[k];
+          if (s1) {
+            aa[k] = mu * aa[k] + gg;
+            gg = aa[k];
+          }
+          pp[k] -= lr * gg;
+        } else {
+          float gg = dd[k];
+          if (amode & 1) pp[k] *= (1.f - lr * wd);
+          else gg += wd * pp[k];
+          aa[k] = b1 * aa[k] + (1.f - b1) * gg;
+          vv[k] = b2 * vv[k] + (1.f - b2) * gg * gg;
+          if (amode & 2) pp[k] -= lr * (sbc2 / bc1) * aa[k] / (sqrtf(vv[k]) + eps);
+          else pp[k] -= lr * (aa[k] / bc1) / (sqrtf(vv[k]) / sbc2 + eps);
+        }
+      }
+      w[k4] = p;
+      if (s1) s1[k4] = a;
+      if constexpr (OPT == 2) s2[k4] = v;
+      if (w16) st_bf16x4(w16, k4, p);
+    }
+    g[k4] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
 
@@ -124,7 +182,9 @@ int commit_replicas(const ReplicaPtrs& rp, int nr, float* center, float* sum, lo
 }
 
 int batch_fetch(const BatchCopy& bc, int ncopy, const int* ctr, hipStream_t s) {
-  if (ncopy < 1 || ncopy > kMaxBatchCopies || bc.nbatch < 1) return (int)hipErrorInvalidValue;
+  if (ncopy < 1 || ncopy > kMaxBatchCopies) return (int)hipErrorInvalidValue;
+  for (int q = 0; q < ncopy; ++q)
+    if (bc.nbatch[q] < 1) return (int)hipErrorInvalidValue;
   long most = 0;
   for (int q = 0; q < ncopy; ++q) most = bc.bytes[q] > most ? bc.bytes[q] : most;
   long blocks = (most / 16 + 255) / 256;
@@ -134,9 +194,26 @@ int batch_fetch(const BatchCopy& bc, int ncopy, const int* ctr, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-int step_record(const float* loss, float* hist, int cap, int* ctr, hipStream_t s, int nrep) {
+int step_record(const float* loss, float* hist, int cap, int* ctr, hipStream_t s, int nrep, const int* steps,
+                float* ts) {
   if (nrep < 1) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(step_record_kernel, dim3(1), dim3(64), 0, s, loss, hist, cap, ctr, nrep);
+  hipLaunchKernelGGL(step_record_kernel, dim3(1), dim3(64), 0, s, loss, hist, cap, ctr, nrep, steps, ts);
+  return (int)hipGetLastError();
+}
+
+int opt_stack_step(int opt, float* w, float* g, float* s1, float* s2, void* w16, long n, int R, const int* ctr,
+                   const int* steps, const float* ts, float lr, float mu, float b1, float b2, float eps, float wd,
+                   int amode, hipStream_t s) {
+  if (n % 4 || R < 1 || !ctr || !steps || (opt != 0 && opt != 2) || (opt == 2 && (!s1 || !s2 || !ts)))
+    return (int)hipErrorInvalidValue;
+  const long n4 = n / 4;
+  const dim3 grid((unsigned)std::min<long>((n4 + 255) / 256, 1024), (unsigned)R);
+  if (opt == 0)
+    hipLaunchKernelGGL(opt_stack_kernel<0>, grid, dim3(256), 0, s, (float4*)w, (float4*)g, (float4*)s1, (float4*)s2,
+                       w16, n4, ctr, steps, ts, lr, mu, b1, b2, eps, wd, amode);
+  else
+    hipLaunchKernelGGL(opt_stack_kernel<2>, grid, dim3(256), 0, s, (float4*)w, (float4*)g, (float4*)s1, (float4*)s2,
+                       w16, n4, ctr, steps, ts, lr, mu, b1, b2, eps, wd, amode);
   return (int)hipGetLastError();
 }
 

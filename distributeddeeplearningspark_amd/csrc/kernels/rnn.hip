@@ -239,7 +239,7 @@ template <int CELL, int H>
 constexpr int bwd_threads() { return H * (((CELL == 0 ? 3 : 4) * H / 64) <= 4 ? 4 : 8); }
 
 // REP: replica-batched (RnnRep): the workgroup's replica is b0 / rp.B; W / U / bias come from its table
-// entries and x from its resident shard at mini-batch (*rp.ctr % rp.nb) — outputs stay global-row indexed.
+// entries and x from its resident shard at mini-batch (*rp.ctr % rp.nbr[r]) — outputs stay global-row indexed.
 template <int CELL, int H, int BB_, bool FUSE, bool REP = false>
 __global__ __launch_bounds__((fwd_threads<CELL, H>())) void rnn_fwd_reg_kernel(
     const float* __restrict__ xw, const float* __restrict__ x, const float* __restrict__ W,
@@ -264,7 +264,7 @@ __global__ __launch_bounds__((fwd_threads<CELL, H>())) void rnn_fwd_reg_kernel(
     W = rp.W[r];
     bias = rp.b[r];
     x = rp.x[r];
-    xrow0 = (long)(*rp.ctr % rp.nb) * rp.B + (b0 - r * rp.B);
+    xrow0 = (long)(*rp.ctr % rp.nbr[r]) * rp.B + (b0 - r * rp.B);
   }
   float u[CH];
 #pragma unroll
@@ -723,7 +723,8 @@ __global__ __launch_bounds__(256) void dense_mse_rep_kernel(const float* __restr
   const float* hb = hlast + (long)r * B * H;
   for (int i = tid; i < B * H; i += 256) hsm[i / H][i % H] = hb[i];
   const int ctr = *rp.ctr;
-  const float* tgt = rp.y[r] + (long)(ctr % rp.nb) * B * K;
+  const bool live = ctr < rp.steps[r];  // ragged shards: an exhausted replica computes but does not step
+  const float* tgt = rp.y[r] + (long)(ctr % rp.nbr[r]) * B * K;
   const float* Wd = rp.Wd[r];
   const float* bd = rp.bd[r];
   __syncthreads();
@@ -746,8 +747,11 @@ __global__ __launch_bounds__(256) void dense_mse_rep_kernel(const float* __restr
     __syncthreads();
   }
   if (tid == 0) {
-    if (ctr < rp.cap) rp.hist[r][ctr] = red[0] / (float)(B * K);
-    if (op.t[r]) op.t[r][0] += 1.f;  // Adam's device step counter (read by the optimizer sweep below)
+    rp.live[r] = live ? 1 : 0;  // read by the optimizer sweep of this step
+    if (live) {
+      rp.hist[r][ctr] = red[0] / (float)(B * K);
+      if (op.t[r]) op.t[r][0] += 1.f;  // Adam's device step counter (read by the optimizer sweep below)
+    }
   }
   // gWd[o][i] = sum_b dy[b][o] h[b][i];  gbd[o] = sum_b dy[b][o]
   for (int q = tid; q < K * H; q += 256) {
@@ -784,7 +788,7 @@ __global__ __launch_bounds__(256) void rnn_param_grad_rep_kernel(const float* __
   const bool has_b = rp.gb[r] != nullptr;
   const int M = H + I + (has_b ? 1 : 0);
   const long BT = (long)B * T, row0 = (long)r * B;  // global batch row of the replica's row 0
-  const long xrow0 = (long)(*rp.ctr % rp.nb) * B;   // shard row of its mini-batch
+  const long xrow0 = (long)(*rp.ctr % rp.nbr[r]) * B;  // shard row of its mini-batch
   const float* x = rp.x[r];
   const int m0 = blockIdx.x * 64, j0 = blockIdx.y * 64;
   __shared__ float As[PG_BT][64 + 1];
@@ -844,11 +848,22 @@ __global__ __launch_bounds__(256) void rnn_param_grad_rep_kernel(const float* __
 // Optimizer sweep over the R replica arenas (blockIdx.y = replica), Keras semantics as the per-replica
 // kernels (optim.hip): OPT 0 SGD (+momentum p1), 1 Adagrad, 2 Adam (b1 = p1, b2 = p2, amode as adam_step).
 // zero_g: leave the gradients zeroed for the next step's atomic parameter-gradient slices.  Block (0, 0)
-// advances the shared step counter (no block of this kernel reads it).
+// advances the shared step counter (no block of this kernel reads it: the live flags come from the head kernel).
+// A dead replica (ragged shard exhausted) keeps its parameters and state; its gradients are still zeroed.
 template <int OPT>
 __global__ __launch_bounds__(256) void opt_rep_kernel(const OptRep op, long n4, float lr, float p1, float p2, float eps,
-                                                      float wd, int amode, int* ctr, int zero_g) {
+                                                      float wd, int amode, int* ctr, const int* __restrict__ live,
+                                                      int zero_g) {
   const int r = blockIdx.y;
+  if (!live[r]) {
+    if (zero_g) {
+      float4* g = const_cast<float4*>(reinterpret_cast<const float4*>(op.g[r]));
+      for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256)
+        g[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *ctr += 1;
+    return;
+  }
   float4* w = reinterpret_cast<float4*>(op.w[r]);
   float4* g = const_cast<float4*>(reinterpret_cast<const float4*>(op.g[r]));
   float4* s1 = reinterpret_cast<float4*>(op.s1[r]);
@@ -919,11 +934,14 @@ int rep_step(const RnnRep& rp, int R, int T, int I, float* hs, float* cs, float*
   const dim3 og((unsigned)std::min<long>((n4 + 255) / 256, 1024), R);
   const int zg = S > 1;
   if (opt == 0)
-    hipLaunchKernelGGL(opt_rep_kernel<0>, og, dim3(256), 0, s, op, n4, lr, p1, p2, eps, wd, amode, rp.ctr, zg);
+    hipLaunchKernelGGL(opt_rep_kernel<0>, og, dim3(256), 0, s, op, n4, lr, p1, p2, eps, wd, amode, rp.ctr, rp.live,
+                       zg);
   else if (opt == 1)
-    hipLaunchKernelGGL(opt_rep_kernel<1>, og, dim3(256), 0, s, op, n4, lr, p1, p2, eps, wd, amode, rp.ctr, zg);
+    hipLaunchKernelGGL(opt_rep_kernel<1>, og, dim3(256), 0, s, op, n4, lr, p1, p2, eps, wd, amode, rp.ctr, rp.live,
+                       zg);
   else
-    hipLaunchKernelGGL(opt_rep_kernel<2>, og, dim3(256), 0, s, op, n4, lr, p1, p2, eps, wd, amode, rp.ctr, zg);
+    hipLaunchKernelGGL(opt_rep_kernel<2>, og, dim3(256), 0, s, op, n4, lr, p1, p2, eps, wd, amode, rp.ctr, rp.live,
+                       zg);
   return (int)hipGetLastError();
 }
 
@@ -937,8 +955,10 @@ bool rnn_replica_ok(int cell, int H, int I, int K, int B) {
 int rnn_replica_step(int cell, const RnnRep& rp, int R, int T, int H, int I, float* hs, float* cs, float* gates,
                      float* hlast, float* dh, float* dgates, const OptRep& op, long n, int opt, float lr, float p1,
                      float p2, float eps, float wd, int amode, hipStream_t s) {
-  if (!rnn_replica_ok(cell, H, I, rp.K, rp.B) || R < 1 || R > kMaxRnnRep || n % 4 || opt < 0 || opt > 2 || rp.nb < 1)
+  if (!rnn_replica_ok(cell, H, I, rp.K, rp.B) || R < 1 || R > kMaxRnnRep || n % 4 || opt < 0 || opt > 2 || !rp.live)
     return (int)hipErrorInvalidValue;
+  for (int r = 0; r < R; ++r)
+    if (rp.nbr[r] < 1) return (int)hipErrorInvalidValue;
   if (cell == 0)
     return H == 128 ? rep_step<0, 128>(rp, R, T, I, hs, cs, gates, hlast, dh, dgates, op, n, opt, lr, p1, p2, eps, wd, amode, s)
                     : rep_step<0, 64>(rp, R, T, I, hs, cs, gates, hlast, dh, dgates, op, n, opt, lr, p1, p2, eps, wd, amode, s);

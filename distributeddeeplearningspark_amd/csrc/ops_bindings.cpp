@@ -537,30 +537,38 @@ void commit_replicas_(const std::vector<at::Tensor>& ws, const std::vector<c10::
   HIP_OK(commit_replicas(rp, (int)ws.size(), center.data_ptr<float>(), optr<float>(sum), center.numel(),
                          elastic ? 1 : 0, (int)mode, cur_stream()));
 }
-// copies mini-batch (ctr % nbatch) of each resident shard srcs[q] ([nbatch * rows, ...]) into dsts[q]
+// copies mini-batch (ctr % nbatch[q]) of each resident shard srcs[q] ([nbatch[q] * rows, ...]) into dsts[q];
+// nbatch: one count for every copy, or one per copy (ragged replica shards)
 void batch_fetch_(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts, const at::Tensor& ctr,
-                  int64_t nbatch) {
-  CK(!srcs.empty() && srcs.size() <= (size_t)kMaxBatchCopies && dsts.size() == srcs.size(), "batch_fetch: 1..16 copies");
+                  py::object nbatch) {
+  CK(!srcs.empty() && srcs.size() <= (size_t)kMaxBatchCopies && dsts.size() == srcs.size(), "batch_fetch: 1..",
+     kMaxBatchCopies, " copies");
   CK(ctr.is_cuda() && ctr.scalar_type() == at::kInt && ctr.numel() == 1, "batch_fetch: int32 step counter");
-  CK(nbatch >= 1, "batch_fetch: nbatch >= 1");
+  std::vector<int64_t> nbs;
+  if (py::isinstance<py::int_>(nbatch)) nbs.assign(srcs.size(), nbatch.cast<int64_t>());
+  else nbs = nbatch.cast<std::vector<int64_t>>();
+  CK(nbs.size() == srcs.size(), "batch_fetch: one batch count, or one per copy");
   BatchCopy bc{};
-  bc.nbatch = nbatch;
   for (size_t q = 0; q < srcs.size(); ++q) {
     const at::Tensor &s = srcs[q], &d = dsts[q];
     CK(s.is_cuda() && d.is_cuda() && s.is_contiguous() && d.is_contiguous() && s.scalar_type() == d.scalar_type() &&
            s.device() == ctr.device() && d.device() == ctr.device(),
        "batch_fetch: contiguous GPU tensors of one dtype on the counter's device");
+    CK(nbs[q] >= 1, "batch_fetch: nbatch >= 1");
     const long bytes = (long)d.numel() * (long)d.element_size();
-    CK((long)s.numel() * (long)s.element_size() >= bytes * nbatch, "batch_fetch: shard smaller than nbatch batches");
+    CK((long)s.numel() * (long)s.element_size() >= bytes * nbs[q], "batch_fetch: shard smaller than nbatch batches");
     bc.src[q] = s.data_ptr();
     bc.dst[q] = d.data_ptr();
     bc.bytes[q] = bytes;
+    bc.nbatch[q] = nbs[q];
   }
   at::DeviceGuard g(ctr.device());
   HIP_OK(batch_fetch(bc, (int)srcs.size(), ctr.data_ptr<int>(), cur_stream()));
 }
-// loss [R] with hist [R, cap] (replica batching: one shared counter) or loss [1] with hist [cap]
-void step_record_(const at::Tensor& loss, c10::optional<at::Tensor> hist, const at::Tensor& ctr) {
+// loss [R] with hist [R, cap] (replica batching: one shared counter) or loss [1] with hist [cap];
+// steps (int32 [R]): ragged replicas record only while live; ts (fp32 [R]): their Adam counters tick
+void step_record_(const at::Tensor& loss, c10::optional<at::Tensor> hist, const at::Tensor& ctr,
+                  c10::optional<at::Tensor> steps, c10::optional<at::Tensor> ts) {
   F32(loss);
   const int64_t R = loss.numel();
   CK(loss.is_cuda() && loss.is_contiguous() && R >= 1 && R <= 64, "step_record: 1..64 fp32 losses on the GPU");
@@ -571,9 +579,36 @@ void step_record_(const at::Tensor& loss, c10::optional<at::Tensor> hist, const 
     CK(hist->device() == loss.device() && hist->is_contiguous() && (R == 1 || (hist->dim() == 2 && hist->size(0) == R)),
        "step_record: history [cap] (or [R, cap] for R losses) on the loss device");
   }
+  if (steps) CK(steps->is_cuda() && steps->scalar_type() == at::kInt && steps->numel() == R &&
+                    steps->device() == loss.device(), "step_record: int32 steps [R] on the loss device");
+  if (ts) { F32(*ts); CK(ts->is_cuda() && ts->numel() == R && ts->device() == loss.device(), "step_record: ts [R]"); }
   at::DeviceGuard g(loss.device());
   HIP_OK(step_record(loss.data_ptr<float>(), optr<float>(hist), hist ? (int)(hist->numel() / R) : 0, ctr.data_ptr<int>(),
-                     cur_stream(), (int)R));
+                     cur_stream(), (int)R, steps ? steps->data_ptr<int>() : nullptr, optr<float>(ts)));
+}
+// stacked replica optimizer (replica.hip opt_stack_step): w / g / s1 / s2 fp32 [R, n], w16 bf16 [R, n] or None
+void opt_stack_step_(int64_t opt, const at::Tensor& w, const at::Tensor& g, c10::optional<at::Tensor> s1,
+                     c10::optional<at::Tensor> s2, c10::optional<at::Tensor> w16, const at::Tensor& ctr,
+                     const at::Tensor& steps, c10::optional<at::Tensor> ts, double lr, double mu, double b1, double b2,
+                     double eps, double wd, int64_t amode) {
+  F32(w); F32(g);
+  CK(w.is_cuda() && w.dim() == 2 && w.is_contiguous() && g.sizes() == w.sizes() && g.is_contiguous() &&
+         g.device() == w.device(), "opt_stack_step: w, g [R, n] contiguous on one GPU");
+  const int64_t R = w.size(0), n = w.size(1);
+  for (auto* t : {&s1, &s2}) if (*t) { F32(**t); CK((*t)->sizes() == w.sizes() && (*t)->is_contiguous() &&
+                                                       (*t)->device() == w.device(), "opt_stack_step: state [R, n]"); }
+  if (w16) CK(w16->scalar_type() == at::kBFloat16 && w16->sizes() == w.sizes() && w16->is_contiguous() &&
+                  w16->device() == w.device(), "opt_stack_step: bf16 copy [R, n]");
+  CK(ctr.is_cuda() && ctr.scalar_type() == at::kInt && ctr.numel() == 1 && ctr.device() == w.device(),
+     "opt_stack_step: int32 step counter");
+  CK(steps.is_cuda() && steps.scalar_type() == at::kInt && steps.numel() == R && steps.device() == w.device(),
+     "opt_stack_step: int32 steps [R]");
+  if (ts) { F32(*ts); CK(ts->numel() == R && ts->device() == w.device(), "opt_stack_step: ts [R]"); }
+  at::DeviceGuard dg(w.device());
+  HIP_OK(opt_stack_step((int)opt, w.data_ptr<float>(), g.data_ptr<float>(), optr<float>(s1), optr<float>(s2),
+                        w16 ? w16->data_ptr() : nullptr, n, (int)R, ctr.data_ptr<int>(), steps.data_ptr<int>(),
+                        optr<float>(ts), (float)lr, (float)mu, (float)b1, (float)b2, (float)eps, (float)wd, (int)amode,
+                        cur_stream()));
 }
 void prob_xent_(const at::Tensor& p, c10::optional<at::Tensor> labels, c10::optional<at::Tensor> target,
                 const at::Tensor& loss_rows, const at::Tensor& dp, double eps, double scale, int64_t ignore_index) {
@@ -726,7 +761,9 @@ void register_ops(py::module& m) {
         py::arg("w16s"), py::arg("scales"), py::arg("center"), py::arg("sum") = py::none(), py::arg("elastic") = false,
         py::arg("mode") = 0);
   m.def("batch_fetch", &batch_fetch_);
-  m.def("step_record", &step_record_);
+  m.def("step_record", &step_record_, py::arg("loss"), py::arg("hist"), py::arg("ctr"), py::arg("steps") = py::none(),
+        py::arg("ts") = py::none());
+  m.def("opt_stack_step", &opt_stack_step_);
   m.def("etl_minmax", &etl_minmax_);
   m.def("etl_one_hot", &etl_one_hot_);
   m.def("etl_argmax", &etl_argmax_);

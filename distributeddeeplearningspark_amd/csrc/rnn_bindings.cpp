@@ -156,7 +156,8 @@ float* fptr(const py::handle& o, const char* what, int64_t numel = -1) {
 
 void rnn_replica_step_(const std::string& cell, py::list xs, py::list ys, py::list Ws, py::list Us, py::list bs,
                        py::list Wds, py::list bds, py::list gWs, py::list gUs, py::list gbs, py::list gWds,
-                       py::list gbds, py::list hists, at::Tensor ctr, int64_t nb, int64_t B, at::Tensor hs,
+                       py::list gbds, py::list hists, at::Tensor ctr, std::vector<int64_t> nbs,
+                       std::vector<int64_t> steps, at::Tensor live, int64_t B, at::Tensor hs,
                        at::Tensor cs, at::Tensor gates, at::Tensor hlast, at::Tensor dh, at::Tensor dgates,
                        py::list ws, py::list gs, py::list s1s, py::list s2s, py::list ts, int64_t opt, double lr,
                        double p1, double p2, double eps, double wd, int64_t amode) {
@@ -173,11 +174,18 @@ void rnn_replica_step_(const std::string& cell, py::list xs, py::list ys, py::li
   TORCH_CHECK(U0.size(1) == G * H && Wd0.size(1) == H, "rnn_replica_step: U [H, GH], Dense kernel [K, H]");
   TORCH_CHECK(rnn_replica_ok(c, (int)H, (int)I, (int)K, (int)B), "rnn_replica_step: unsupported H / I / K / B");
   TORCH_CHECK(ctr.is_cuda() && ctr.scalar_type() == at::kInt && ctr.numel() >= 1, "rnn_replica_step: int32 ctr");
+  TORCH_CHECK(live.is_cuda() && live.scalar_type() == at::kInt && live.numel() >= R && live.device() == ctr.device(),
+              "rnn_replica_step: int32 live flags [R] on the counter's device");
+  TORCH_CHECK((int)nbs.size() == R && (int)steps.size() == R, "rnn_replica_step: batches and steps per replica");
   const int64_t RB = R * B;
   const int64_t n = ws[0].cast<at::Tensor>().numel();
   RnnRep rp{};
   OptRep op{};
   for (int r = 0; r < R; ++r) {
+    const int64_t nb = nbs[r];
+    TORCH_CHECK(nb >= 1 && steps[r] >= 0 && steps[r] < (1LL << 31), "rnn_replica_step: batches >= 1, steps >= 0");
+    rp.nbr[r] = (int)nb;
+    rp.steps[r] = (int)steps[r];
     rp.x[r] = fptr(xs[r], "x shard", nb * B * T * I);
     rp.y[r] = fptr(ys[r], "y shard", nb * B * K);
     rp.W[r] = fptr(Ws[r], "W", I * G * H);
@@ -192,10 +200,8 @@ void rnn_replica_step_(const std::string& cell, py::list xs, py::list ys, py::li
     rp.gbd[r] = fptr(gbds[r], "gbd", K);
     TORCH_CHECK(!bs[r].is_none() && !gbs[r].is_none(), "rnn_replica_step: recurrent bias required");
     TORCH_CHECK(bds[r].is_none() == gbds[r].is_none(), "rnn_replica_step: Dense bias and its gradient together");
-    at::Tensor h = hists[r].cast<at::Tensor>();
-    rp.hist[r] = fptr(hists[r], "history");
-    if (r == 0) rp.cap = (int)h.numel();
-    TORCH_CHECK(h.numel() == rp.cap, "rnn_replica_step: equal history capacities");
+    rp.hist[r] = fptr(hists[r], "history", steps[r]);  // one slot per step the replica takes
+    TORCH_CHECK(rp.hist[r], "rnn_replica_step: history required");
     op.w[r] = fptr(ws[r], "weights", n);
     op.g[r] = fptr(gs[r], "grads", n);
     op.s1[r] = fptr(s1s[r], "optimizer state", n);
@@ -206,7 +212,7 @@ void rnn_replica_step_(const std::string& cell, py::list xs, py::list ys, py::li
     if (opt == 1) TORCH_CHECK(op.s1[r], "rnn_replica_step: Adagrad needs its accumulator");
   }
   rp.ctr = ctr.data_ptr<int>();
-  rp.nb = (int)nb;
+  rp.live = live.data_ptr<int>();
   rp.B = (int)B;
   rp.K = (int)K;
   float* hsp = fptr(py::cast(hs), "hs", RB * (T + 1) * H);

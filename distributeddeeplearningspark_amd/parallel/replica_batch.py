@@ -16,7 +16,14 @@ rows; run replica by replica, the GPU is mostly idle between them.  Here one ste
   5. one optimizer sweep over the R flat arenas, which also advances the step counter.
 
 A commit window of ``k`` steps for all replicas is captured into ONE hipGraph and replayed per round;
-the commit itself is the group's ``commit_replicas`` kernel, unchanged.  The update law, histories,
+the commit itself is the group's ``commit_replicas`` kernel, unchanged.
+
+Ragged shards: the reference's ``repartition(num_workers)`` shards differ by a row
+(``ddl_nyiso_aztk.py:193``; its 11,519 training rows give 2,880 / 2,880 / 2,880 / 2,879), so replicas take
+different step counts.  Every replica fetches its own mini-batch (``ctr % nb_r``) and stays live while the
+shared step counter is below its own step count; a replica past it is masked in the kernels (no history
+slot, no Adam tick, no parameter or state update), which is exactly the per-replica schedule: an
+exhausted worker stops stepping while the others finish their windows.  The update law, histories,
 ``num_updates`` and optimizer state are those of the per-replica path (tests/test_gpu_colocated.py
 compares the two to fp32 rounding).
 """
@@ -41,45 +48,56 @@ def _layers(model):
     return rnn, dense
 
 
-def applies(group) -> bool:
-    """The group's replicas are RNN(64|128) -> Dense(K) / MSE fp32 models with a supported worker
-    optimizer, equal shards (the replicas step in lockstep) and at most 8 replicas."""
-    if os.environ.get("DDL_REPLICA_BATCH", "1") == "0" or not group.gpu or group.rule == "averaging":
-        return False
+MAX_R = 16  # kMaxRnnRep (csrc/include/ddl_ops.h): 8 executors x 2 processes
+
+
+def why_not(group) -> str | None:
+    """None when the group's replicas are RNN(64|128) -> Dense(K) / MSE fp32 models with a supported worker
+    optimizer and at most 16 replicas (shards may be ragged); else the reason they are not batched."""
+    if os.environ.get("DDL_REPLICA_BATCH", "1") == "0":
+        return "DDL_REPLICA_BATCH=0"
+    if not group.gpu or group.rule == "averaging":
+        return "CPU group or averaging rule"
     reps = group.reps
-    if not (1 < len(reps) <= 8):
-        return False
+    if not (1 < len(reps) <= MAX_R):
+        return f"{len(reps)} replicas (batched: 2..{MAX_R})"
     from ..ops._native import C
 
-    if len({(r.nb, r.steps, r.commits) for r in reps}) != 1:
-        return False
+    if len({r.bs for r in reps}) != 1:
+        return "unequal batch sizes"
     for r in reps:
         m = r.model
         ls = _layers(m)
-        if ls is None or m.loss != "mean_squared_error" or m.arena.compute is not m.arena.master:
-            return False
+        if ls is None:
+            return "not a GRU/LSTM -> Dense Sequential"
+        if m.loss != "mean_squared_error" or m.arena.compute is not m.arena.master:
+            return "loss is not MSE or compute is not fp32"
         rnn, dense = ls
         if (rnn.return_sequences or not rnn.use_bias or rnn.activation != "tanh"
                 or rnn.recurrent_activation != "hard_sigmoid" or not rnn.trainable or not dense.trainable):
-            return False
+            return "recurrent layer outside the fused cell (return_sequences / no bias / activations / frozen)"
         if dense.activation_name not in (None, "linear") or dense.kernel.data.shape[1] != rnn.units:
-            return False
+            return "Dense head is not linear on the last hidden state"
         o = m.optimizer
         if getattr(o, "clipnorm", None) is not None or m.arena.numel % 4:
-            return False
+            return "clipnorm or arena size not a multiple of 4"
         if isinstance(o, opt_mod.SGD):
             if o.nesterov or o.dampening:
-                return False
+                return "SGD with nesterov / dampening"
         elif not isinstance(o, (opt_mod.Adagrad, opt_mod.Adam)):
-            return False
+            return f"worker optimizer {type(o).__name__}"
         X = r.X
         if X.dim() != 3 or X.dtype != torch.float32 or r.Y.dtype != torch.float32:
-            return False
+            return "inputs are not fp32 [rows, T, I]"
         if r.Y.numel() != r.Y.shape[0] * dense.units or not (X.is_contiguous() and r.Y.is_contiguous()):
-            return False
+            return "targets do not match the Dense head"
         if not C().rnn_replica_ok(rnn.cell, rnn.units, int(X.shape[2]), dense.units, r.bs):
-            return False
-    return True
+            return f"H={rnn.units} / I={int(X.shape[2])} / K={dense.units} / batch={r.bs} outside the fused kernels"
+    return None
+
+
+def applies(group) -> bool:
+    return why_not(group) is None
 
 
 class BatchedReplicas:
@@ -92,7 +110,9 @@ class BatchedReplicas:
         rnn0, dense0 = _layers(r0.model)
         self.cell, self.H, self.K = rnn0.cell, rnn0.units, dense0.units
         self.T, self.I = int(r0.X.shape[1]), int(r0.X.shape[2])
-        self.B, self.nb, self.R = r0.bs, r0.nb, len(reps)
+        self.B, self.R = r0.bs, len(reps)
+        self.nbs = [r.nb for r in reps]
+        self.steps = [r.steps for r in reps]
         dev = r0.model.device
         G = 3 if self.cell == "gru" else 4
         RB, T, H = self.R * self.B, self.T, self.H
@@ -104,6 +124,7 @@ class BatchedReplicas:
         self.dh = torch.empty((RB, H), **f32)
         self.dgates = torch.empty((RB, T, G * H), **f32)
         self.ctr = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.live = torch.ones(self.R, dtype=torch.int32, device=dev)
         self.graph = None
         o = r0.model.optimizer
         if isinstance(o, opt_mod.Adam):
@@ -147,7 +168,8 @@ class BatchedReplicas:
 
         a = self.args
         C().rnn_replica_step(self.cell, a["xs"], a["ys"], a["Ws"], a["Us"], a["bs"], a["Wds"], a["bds"], a["gWs"],
-                             a["gUs"], a["gbs"], a["gWds"], a["gbds"], a["hists"], self.ctr, self.nb, self.B,
+                             a["gUs"], a["gbs"], a["gWds"], a["gbds"], a["hists"], self.ctr, self.nbs, self.steps,
+                             self.live, self.B,
                              self.hs, self.cs, self.gates, self.hlast, self.dh, self.dgates, a["ws"], a["gs"],
                              a["s1s"], a["s2s"], a["ts"], self.opt, self.lr, self.p1, self.p2, self.eps, self.wd,
                              self.amode)
@@ -186,6 +208,7 @@ class BatchedReplicas:
         self._advance(self.k)
 
     def _advance(self, n: int):
-        for r in self.group.reps:  # host mirrors of the device counters
-            r.done += n
-            r.model.optimizer.iterations += n
+        for r in self.group.reps:  # host mirrors of the device counters (a replica stops at its own step count)
+            took = max(0, min(n, r.steps - r.done))
+            r.done += took
+            r.model.optimizer.iterations += took

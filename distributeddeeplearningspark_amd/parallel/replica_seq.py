@@ -17,7 +17,14 @@ so every op addresses replica z's weights at a fixed stride and runs as ONE laun
     lockstep), zeroing the gradients as it goes; one ``batch_fetch`` / ``step_record`` serve all replicas.
 
 A commit window of ``k`` steps for all replicas is one hipGraph, replayed per round; the commit is the
-group's ``commit_replicas`` kernel, unchanged.  Update law, histories, ``num_updates`` and optimizer state are
+group's ``commit_replicas`` kernel, unchanged.
+
+Ragged shards (``repartition(num_workers)`` of 59,999 rows gives shards a row apart,
+``ddl_mnist_aztk.py:156``) and up to 16 replicas (8 executors x 2 processes, ``ddl_mnist_aztk.py:49-53``):
+each replica fetches mini-batch ``ctr % nb_r`` of its own shard, and the stacked optimizer
+(``replica.hip`` ``opt_stack_step``) and ``step_record`` mask a replica once the shared step counter
+reaches its own step count, so an exhausted worker stops while the others finish their windows (the
+per-replica schedule).  Each replica keeps its own Adam step counter.  Update law, histories, ``num_updates`` and optimizer state are
 those of the per-replica path (tests/test_gpu_colocated.py compares the two).
 """
 from __future__ import annotations
@@ -29,7 +36,7 @@ import torch
 
 from ..models import optimizers as opt_mod
 
-_MAX_R = 8
+_MAX_R = 16  # kMaxBatchCopies / 2 (csrc/include/ddl_ops.h)
 
 
 def _plan(model):
@@ -40,6 +47,7 @@ def _plan(model):
     if not isinstance(model, Sequential):
         return None
     L, ops, i = model.layers, [], 0
+    flat = len(tuple(model.input_shape)) == 1  # a Dense reads [rows, features]: 1-D input or after a Flatten
     while i < len(L):
         l = L[i]
         nxt = L[i + 1] if i + 1 < len(L) else None
@@ -47,17 +55,18 @@ def _plan(model):
         if isinstance(l, Conv2D):
             if l.strides != (1, 1) or l.dilation_rate != (1, 1) or not l.trainable:
                 return None
-            if l.activation_name not in ("linear", "relu") or l.filters % 8:
+            if l.activation_name not in ("linear", "relu") or l.filters % 8 or flat:
                 return None
             ops.append(("conv", l, l.activation_name == "relu" or relu_next))
         elif isinstance(l, MaxPooling2D):
-            if l.padding != "valid" or l.pool_size != l.strides:
+            if l.padding != "valid" or l.pool_size != l.strides or flat:
                 return None
             ops.append(("pool", l, False))
         elif isinstance(l, Flatten):
             ops.append(("flatten", l, False))
+            flat = True
         elif isinstance(l, Dense):
-            if not l.trainable:
+            if not l.trainable or not flat:  # a Dense on a 4-D activation is not a [rows, K] GEMM here
                 return None
             last = i == len(L) - 1 or (i == len(L) - 2 and isinstance(nxt, Activation) and nxt.activation_name == "softmax")
             if last:
@@ -77,39 +86,50 @@ def _plan(model):
     return None
 
 
-def applies(group) -> bool:
-    """Co-located Sequential CNN / MLP replicas with a softmax cross-entropy head and Adam / SGD, bf16 compute,
-    equal shards (lockstep) and at most 8 replicas."""
-    if os.environ.get("DDL_REPLICA_BATCH", "1") == "0" or not group.gpu or group.rule == "averaging":
-        return False
+def why_not(group) -> str | None:
+    """None when the group's replicas are co-located Sequential CNN / MLP classifiers with a softmax
+    cross-entropy head, Adam / SGD(+momentum), bf16 compute and at most 16 replicas (shards may be ragged);
+    else the reason they are not batched."""
+    if os.environ.get("DDL_REPLICA_BATCH", "1") == "0":
+        return "DDL_REPLICA_BATCH=0"
+    if not group.gpu or group.rule == "averaging":
+        return "CPU group or averaging rule"
     from ..ops import determinism as _det
 
     reps = group.reps
-    if not (1 < len(reps) <= _MAX_R) or _det.enabled():
-        return False
-    if len({(r.nb, r.steps, r.commits, r.bs) for r in reps}) != 1:
-        return False
+    if not (1 < len(reps) <= _MAX_R):
+        return f"{len(reps)} replicas (batched: 2..{_MAX_R})"
+    if _det.enabled():
+        return "deterministic mode (the batched weight gradients split K with atomics)"
+    if len({r.bs for r in reps}) != 1:
+        return "unequal batch sizes"
     for r in reps:
         m = r.model
-        if _plan(m) is None or m.compute_dtype != torch.bfloat16 or not getattr(m, "graph_capturable", True):
-            return False
+        if _plan(m) is None:
+            return "layer stack outside the batched plan (conv / pool / flatten / dense with a softmax head)"
+        if m.compute_dtype != torch.bfloat16 or not getattr(m, "graph_capturable", True):
+            return "compute dtype is not bf16 or the model is not graph-capturable"
         if m.loss not in ("categorical_crossentropy", "sparse_categorical_crossentropy"):
-            return False
+            return f"loss {m.loss}"
         o = m.optimizer
         if getattr(o, "clipnorm", None) is not None or type(o) not in (opt_mod.Adam, opt_mod.AdamW, opt_mod.SGD):
-            return False
-        if isinstance(o, opt_mod.SGD) and (o.nesterov or o.dampening or o.momentum):
-            return False
+            return f"worker optimizer {type(o).__name__} (or clipnorm)"
+        if isinstance(o, opt_mod.SGD) and (o.nesterov or o.dampening):
+            return "SGD with nesterov / dampening"
         if r.X.dtype != torch.bfloat16 or not r.X.is_contiguous() or not r.Y.is_contiguous():
-            return False
+            return "shard is not contiguous bf16"
         K = m.layers[-1].units if hasattr(m.layers[-1], "units") else m.layers[-2].units
         if r.bs * len(reps) > 4096 or r.bs * K * len(reps) > 65536 or len(reps) * r.bs > 1024:
-            return False
+            return "stacked batch too large for the one-launch loss"
         if m.loss == "categorical_crossentropy" and (r.Y.dtype != torch.float32 or r.Y.numel() != r.Y.shape[0] * K):
-            return False
+            return "one-hot targets are not fp32 [rows, K]"
         if m.loss == "sparse_categorical_crossentropy" and (r.Y.dtype != torch.int64 or r.Y.numel() != r.Y.shape[0]):
-            return False
-    return True
+            return "sparse targets are not int64 [rows]"
+    return None
+
+
+def applies(group) -> bool:
+    return why_not(group) is None
 
 
 class SeqReplicas:
@@ -121,7 +141,8 @@ class SeqReplicas:
 
         self.group = group
         reps = group.reps
-        self.R, self.B, self.nb = len(reps), reps[0].bs, reps[0].nb
+        self.R, self.B = len(reps), reps[0].bs
+        self.nbs = [r.nb for r in reps]
         m0 = reps[0].model
         dev = m0.device
         self.dev = dev
@@ -139,7 +160,7 @@ class SeqReplicas:
             self.W[z].copy_(a.master.detach())
             self.W16[z].copy_(a.compute.detach())
             a.rebind(self.W[z], self.Gr[z], self.W16[z])
-        # ---- optimizer: one launch over the stacked arenas, shared step counter (lockstep replicas)
+        # ---- optimizer: one launch over the stacked arenas; per-replica step counts (ragged shards)
         o0 = m0.optimizer
         self.adam = isinstance(o0, opt_mod.Adam)
         self.state = {}
@@ -149,8 +170,8 @@ class SeqReplicas:
                 st[z].copy_(r.model.optimizer.state[k])
                 r.model.optimizer.state[k] = st[z]
             self.state[k] = st
-        self.tstep = torch.full((1,), float(o0.iterations), dtype=torch.float32, device=dev)
-        self.tick = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.ts = torch.tensor([float(r.model.optimizer.iterations) for r in reps], dtype=torch.float32, device=dev)
+        self.steps_lim = torch.tensor([r.steps for r in reps], dtype=torch.int32, device=dev)
         self.opt = o0
         # ---- data: one fetch for all replicas into the stacked batch
         X0, Y0 = reps[0].X, reps[0].Y
@@ -257,12 +278,11 @@ class SeqReplicas:
     # ------------------------------------------------------------------ one step of every replica
     def _step(self):
         from ..ops import gemm as G
-        from ..ops import optim as K_
         from ..ops._native import C
 
         c = C()
         R, B, NW = self.R, self.B, self.NW
-        c.batch_fetch(self.srcs, self.dsts, self.ctr, self.nb)
+        c.batch_fetch(self.srcs, self.dsts, self.ctr, self.nbs + self.nbs)
         # ---------------- forward
         for st in self.steps:
             kind = st["kind"]
@@ -352,17 +372,17 @@ class SeqReplicas:
                            max(64, math.ceil(g2.T * g2.Ci / 64) * 64), geom=g2.fwd_geom, zcount=R,
                            za=g.M * Cop, zb=g2.T * g2.Ci * g2.Co, zc=g2.M * g2.Co)
                     d = st["dx"]
-        # ---------------- optimizer over the stacked arenas (+ step tick, + gradient zeroing)
+        # ---------------- optimizer over the stacked arenas (live replicas only, + gradient zeroing)
         o = self.opt
-        W, Gr, W16 = self.W.view(-1), self.Gr.view(-1), self.W16.view(-1)
         if self.adam:
-            K_.adam_(W, Gr, self.state["m"].view(-1), self.state["v"].view(-1), W16, lr=o.lr, beta1=o.b1, beta2=o.b2,
-                     eps=o.eps, weight_decay=o.weight_decay, decoupled=o.decoupled, keras_eps=o.keras_eps,
-                     device_step=self.tstep, tick_ctr=self.tick, zero_grad=True)
+            c.opt_stack_step(2, self.W, self.Gr, self.state["m"], self.state["v"], self.W16, self.ctr, self.steps_lim,
+                             self.ts, o.lr, 0.0, o.b1, o.b2, o.eps, o.weight_decay,
+                             (1 if o.decoupled else 0) | (2 if o.keras_eps else 0))
         else:
-            K_.sgd_(W, Gr, None, W16, lr=o.lr, weight_decay=o.weight_decay)
-            Gr.zero_()
-        c.step_record(self.loss, self.hist, self.ctr)
+            mom = self.state.get("momentum") if o.momentum else None
+            c.opt_stack_step(0, self.W, self.Gr, mom, None, self.W16, self.ctr, self.steps_lim, None, o.lr,
+                             float(o.momentum), 0.0, 0.0, 0.0, o.weight_decay, 0)
+        c.step_record(self.loss, self.hist, self.ctr, self.steps_lim, self.ts)
 
     # ------------------------------------------------------------------ schedule (BatchedReplicas interface)
     def run_steps(self, n: int):
@@ -396,6 +416,7 @@ class SeqReplicas:
         self._advance(self.k)
 
     def _advance(self, n: int):
-        for r in self.group.reps:  # host mirrors of the device counters
-            r.done += n
-            r.model.optimizer.iterations += n
+        for r in self.group.reps:  # host mirrors of the device counters (a replica stops at its own step count)
+            took = max(0, min(n, r.steps - r.done))
+            r.done += took
+            r.model.optimizer.iterations += took

@@ -203,6 +203,7 @@ class ReplicaGroup:
         self.commit_s = 0.0
         self.graph_rounds = 0
         self.batched = None  # replica_batch.BatchedReplicas when the replicas step as one launch per phase
+        self.batch_reason = None  # why a GPU group runs per-replica instead (logged once, in the results)
 
     @staticmethod
     def _resident(a, model, labels=False):
@@ -294,14 +295,7 @@ class ReplicaGroup:
                 self._window_all([rep], rep.steps, False)
             self._average()
             return
-        from . import replica_batch, replica_seq
-
-        if replica_batch.applies(self):  # recurrent regressors (NYISO)
-            self.batched = replica_batch.BatchedReplicas(self)
-            self._run_batched(graphs)
-            return
-        if replica_seq.applies(self):  # Sequential CNN / MLP classifiers (MNIST)
-            self.batched = replica_seq.SeqReplicas(self)
+        if self._try_batched():
             self._run_batched(graphs)
             return
         for j in range(self.rounds):
@@ -320,9 +314,38 @@ class ReplicaGroup:
         if self.gpu:
             torch.cuda.synchronize(self.pg.device)
 
+    def _try_batched(self) -> bool:
+        """Pick the one-launch-per-op path for this group's replicas when one applies: recurrent regressors
+        (NYISO, ``replica_batch``) or Sequential CNN / MLP classifiers (MNIST, ``replica_seq``).  When neither
+        does, log one line with the reason (the per-replica path is several times slower on these tiny
+        models) and keep it in ``self.batch_reason`` for the result dicts."""
+        from . import replica_batch, replica_seq
+
+        if not self.gpu:
+            return False
+        why_rnn = replica_batch.why_not(self)
+        if why_rnn is None:
+            self.batched = replica_batch.BatchedReplicas(self)
+            return True
+        why_seq = replica_seq.why_not(self)
+        if why_seq is None:
+            try:
+                self.batched = replica_seq.SeqReplicas(self)
+                return True
+            except ValueError as e:  # a launch-plan shape the batched kernels do not cover: per-replica path
+                why_seq = str(e)
+        is_rnn = replica_batch._layers(self.reps[0].model) is not None
+        self.batch_reason = why_rnn if is_rnn else why_seq
+        if self.batch_reason != "DDL_REPLICA_BATCH=0":
+            print(f"[ddl] replica group of {len(self.reps)} runs per replica (not batched): {self.batch_reason}",
+                  flush=True)
+        return False
+
     def _run_batched(self, graphs: bool):
-        """Every replica steps in lockstep (equal shards): round j = one k-step window of ALL replicas
-        (one hipGraph replay from round 1 on; round 0 runs eagerly) + the commit kernel."""
+        """Every replica steps in lockstep on one device step counter: round j = one k-step window of ALL
+        replicas (one hipGraph replay from round 1 on; round 0 runs eagerly) + the commit kernel.  Ragged
+        shards: a replica whose steps run out is masked on the device (it stops, the others finish their
+        windows), as in the per-replica schedule."""
         bat, k = self.batched, self.k
         for j in range(self.rounds):
             if graphs and j == 1 and bat.graph is None:
@@ -333,7 +356,7 @@ class ReplicaGroup:
             else:
                 bat.run_steps(k)
             self._commit(j)
-        left = self.reps[0].steps - self.reps[0].done  # steps after the last commit round (history only)
+        left = max(r.steps - r.done for r in self.reps)  # steps after the last commit round (history only)
         if left > 0:
             bat.run_steps(left)
         torch.cuda.synchronize(self.pg.device)
@@ -394,7 +417,7 @@ def train_group(rank, world, pg, cfg, blob, Xs, Ys, rids, sizes):
                "graph": (grp.batched.graph is not None) if grp.batched is not None else rep.graph is not None,
                "ingest": "resident", "timed_s": None, "timed_steps": 0,
                "replica_group": {"group": rank, "groups": world, "replicas": len(grp.reps),
-                                 "batched": grp.batched is not None}}
+                                 "batched": grp.batched is not None, "batch_reason": grp.batch_reason}}
         if rep.rid == 0:
             res["flat"] = grp.reps[0].model.arena.to_canonical(grp.center).cpu().numpy().copy()
             res["states"] = get_states(rep.model)

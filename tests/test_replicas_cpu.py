@@ -50,7 +50,7 @@ def test_replica_group_matches_process_workers(spark, monkeypatch, algo, groups)
     tr_g, w_g = _train(spark, monkeypatch, algo, groups)
     ng = int(groups)
     assert tr_g._results[0].get("replica_group") == {"group": 0, "groups": ng, "replicas": 3 if ng == 1 else 2,
-                                                     "batched": False}
+                                                     "batched": False, "batch_reason": None}
     assert "replica_group" not in tr_p._results[0]
     assert tr_g.parameter_server.num_updates == tr_p.parameter_server.num_updates
     if algo != "AveragingTrainer":
@@ -199,3 +199,18 @@ def test_replica_seq_plan_parses_the_mnist_network():
         m2 = Sequential([L.Conv2D(8, 3, input_shape=(12, 12, 1)), bad, L.Flatten(), L.Dense(10, activation="softmax")])
         m2.build_model()
         assert _plan(m2) is None, bad
+
+
+def test_replica_seq_plan_requires_flat_dense_inputs():
+    """a Dense on a 4-D conv activation (Conv -> Dense -> Flatten) is not a [rows, K] GEMM in the
+    batched plan, so the plan refuses it; an MLP on a 1-D input is accepted."""
+    from distributeddeeplearningspark_amd.models import layers as L
+    from distributeddeeplearningspark_amd.models.core import Sequential
+    from distributeddeeplearningspark_amd.parallel.replica_seq import _plan
+
+    m = Sequential([L.Conv2D(8, 3, input_shape=(12, 12, 1)), L.Dense(16), L.Flatten(), L.Dense(10, activation="softmax")])
+    m.build_model()
+    assert _plan(m) is None
+    mlp = Sequential([L.Dense(32, input_shape=(20,), activation="relu"), L.Dense(10, activation="softmax")])
+    mlp.build_model()
+    assert [k for k, _, _ in _plan(mlp)] == ["dense", "head"]
