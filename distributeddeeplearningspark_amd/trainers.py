@@ -239,7 +239,9 @@ class _Worker:
         from .utils.checkpoint import save_checkpoint, save_rank_state
 
         if self.per_rank_state:
-            save_rank_state(d, self.model, it, self.pg.rank, extra=None if center is None else {"center": center})
+            # the center goes to the file in the canonical layout, as the master weights and optimizer slots do
+            extra = None if center is None else {"center": self.model.arena.to_canonical(center.detach())}
+            save_rank_state(d, self.model, it, self.pg.rank, extra=extra)
             self.pg.barrier()  # every rank file exists before rank 0 publishes `latest`
         save_checkpoint(d, self.model, step=it, extra={"round": rnd, "it": it, "algorithm": self.cfg["algorithm"]},
                         rank=self.pg.rank)
@@ -256,7 +258,13 @@ class _CommitWorker(_Worker):
         a = self.arena
         it0, rnd = self._resume()
         ex = self.resumed_extra or {}
-        center = ex["center"].clone() if "center" in ex else a.master.detach().clone()
+        if "center" in ex:  # saved in the canonical layout (_maybe_checkpoint)
+            if ex["center"].numel() != a.canon_numel:
+                raise ValueError(f"checkpointed center: {ex['center'].numel()} elements, the canonical layout has "
+                                 f"{a.canon_numel}")
+            center = a.from_canonical(ex["center"].to(a.master.device, torch.float32)).clone()
+        else:
+            center = a.master.detach().clone()
         self._exchange = None
         if a.master.is_cuda and self.pg.distributed:
             from .parallel.colocated import ColocatedExchange, colocated_ok

@@ -229,3 +229,7 @@ def test_elastic_resume_restores_each_workers_state(spark, tmp_path, monkeypatch
     last = latest_checkpoint(str(tmp_path / "faulty"))
     ranks = os.listdir(os.path.join(str(tmp_path / "faulty"), "ranks", os.path.basename(last)))
     assert sorted(ranks) == ["rank_00000.safetensors", "rank_00001.safetensors"]
+    from safetensors.torch import load_file
+
+    t = load_file(os.path.join(str(tmp_path / "faulty"), "ranks", os.path.basename(last), ranks[0]))
+    assert t["extra.center"].numel() == t["arena.master"].numel()  # both in the canonical layout
