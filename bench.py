@@ -38,6 +38,9 @@ def main():
                          "batch 32, window 5, 20 epochs): training time in seconds, lower is better")
     ap.add_argument("--workers", type=int, default=4, help="nyiso_*: dist-keras workers (reference: 2 x 2 = 4)")
     ap.add_argument("--epochs", type=int, default=20, help="nyiso_*: epochs (reference: 20)")
+    ap.add_argument("--hours", type=int, default=11664,
+                    help="nyiso_*: length of the synthetic hourly series; 11,664 hours give the reference's 11,519 "
+                         "training rows (SURVEY 6.3), i.e. ragged shards of 2,879 / 2,880 / 2,880 / 2,880 rows")
     ap.add_argument("--reduce-dtype", default=None, choices=["fp32", "bf16"],
                     help="gradient all-reduce wire dtype (default DDL_REDUCE_DTYPE or fp32)")
     ap.add_argument("--graph", type=int, default=None,
@@ -204,7 +207,7 @@ def bench_nyiso(args):
     gpus = _gpu_count()
     wpg = max(1, math.ceil(args.workers / max(gpus, 1)))
     argv = ["--workers", str(args.workers), "--epochs", str(args.epochs), "--models", cell,
-            "--device", "auto" if gpus else "cpu", "--workers-per-gpu", str(wpg)]
+            "--device", "auto" if gpus else "cpu", "--workers-per-gpu", str(wpg), "--hours", str(args.hours)]
     with contextlib.redirect_stdout(sys.stderr):  # the workflow's own report goes to stderr
         out = ddl_nyiso.main(argv)
     r = out["results"][cell]
@@ -214,13 +217,15 @@ def bench_nyiso(args):
         "value": round(r["time_s"], 4), "unit": "s", "n_gpus": gpus, "steps": int(r["updates"]), "warmup": 0,
         "ms_per_step": None, "higher_is_better": False, "scaling": "strong",
         "vs_baseline": round(r["time_s"] / ref["time_s"], 5), "dtype": "fp32",
-        "data": "synthetic NYISO-shaped hourly load (11,712 hours)",
+        "data": f"synthetic NYISO-shaped hourly load ({args.hours:,} hours, "
+                f"{sum(out.get('train_rows') or [0]):,} training rows in shards of {out.get('train_rows')})",
         "config": {"model": f"nyiso_{cell.lower()}", "algorithm": "ADAG", "workers": args.workers, "batch": 32,
                    "communication_window": 5, "epochs": args.epochs, "units": 128, "input": [25, 1],
                    "workers_per_gpu": wpg, "num_updates": r["updates"], "mape_pct": round(r["mape"], 4),
                    "wall_incl_executor_start_s": r.get("wall_incl_executor_start_s"),
                    "executor_start_s": r.get("executor_start_s"), "worker_s": r["worker_s"],
-                   "commit_s": r.get("commit_s"), "commit_wait_s": r.get("commit_wait_s"), "reference": ref},
+                   "commit_s": r.get("commit_s"), "commit_wait_s": r.get("commit_wait_s"),
+                   "replicas_batched": r.get("batched"), "reference": ref},
     }), flush=True)
 
 

@@ -677,6 +677,7 @@ class _ShardedTrainer(Trainer):
         self.record_training_start()
         Xs, Ys = self._shards(dataframe, shuffle)
         sizes = [x.shape[0] for x in Xs]
+        self.worker_rows = list(sizes)
         cfg = self._cfg()
         server = None
         if cfg.get("mode") == "async" and issubclass(_WORKERS[self.algorithm], _CommitWorker):

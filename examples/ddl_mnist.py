@@ -154,6 +154,9 @@ def main():
     rs = getattr(trainer, "_results", [])
     print("Workers:", [{k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()
                         if k in ("rank", "time", "commit_s", "commit_wait_s", "commit_xfer_s", "graph", "ingest")} for r in rs])
+    groups = [r["replica_group"] for r in rs if "replica_group" in r]
+    if groups:
+        print("Replica groups: batched", [g["batched"] for g in groups], "shard rows", trainer.worker_rows)
     return trainer, trained_model
 
 

@@ -138,7 +138,8 @@ def main(argv=None):
                      "worker_s": [round(t, 3) for t in tr.worker_times],
                      "commit_s": [round(t, 3) for t in tr.worker_commit_times],
                      "commit_wait_s": [None if r.get("commit_wait_s") is None else round(r["commit_wait_s"], 3)
-                                       for r in rs]}
+                                       for r in rs],
+                     "batched": [r.get("replica_group", {}).get("batched") for r in rs]}
         extra[name] = tr
     print(json.dumps({"workflow": "ddl_nyiso", "workers": a.workers, "epochs": a.epochs, "results": res}))
     return {"results": res, "trainers": extra, "train_rows": [s.stop - s.start for s in df_train.partition_slices()]}

@@ -224,7 +224,7 @@ def test_replica_fallback_reports_reason(monkeypatch, capsys):
     assert "runs per replica (not batched)" in capsys.readouterr().out
 
 
-def _train_cnn_ragged(batched, monkeypatch, workers, n, opt="adam", epochs=2):
+def _train_cnn_ragged(batched, monkeypatch, workers, n, opt="adam", epochs=4):
     from distributeddeeplearningspark_amd import trainers as T
     from distributeddeeplearningspark_amd.models import optimizers as O
     from distributeddeeplearningspark_amd.models.zoo import mnist_cnn
