@@ -157,11 +157,14 @@ def conv_backward(unit, st, dyc, x, need_dx, resid=None, resid_mask=None, bnr=No
     # drop them before the side stream has run)
     with on_grad_stream(dyc.device, dyc, x, default=False):
         CV.conv_wgrad_native(dyc, x, st.g, conv.kernel.grad)
+    dx = None
+    if need_dx:
+        dx = CV.conv_dgrad_native(dyc, conv.kernel.data, st.g, resid=resid, resid_mask=resid_mask, bnr=bnr, rsub=rsub)
+    # the hook comes after the last read of the weights: on one GPU it may start the optimizer on this bucket
+    # (parallel/ddp.py DataParallel.solo), which rewrites them
     if conv.grad_hook is not None:
         conv.grad_hook()
-    if not need_dx:
-        return None
-    return CV.conv_dgrad_native(dyc, conv.kernel.data, st.g, resid=resid, resid_mask=resid_mask, bnr=bnr, rsub=rsub)
+    return dx
 
 
 class _BottleneckFn(torch.autograd.Function):
@@ -227,10 +230,10 @@ class _BottleneckFn(torch.autograd.Function):
                 # stride-2 1x1 shortcut: its data-gradient stays at half resolution ([N, H/2, W/2, Cin], a plain
                 # GEMM) and conv1's dgrad epilogue adds it at the even pixels — instead of a scatter GEMM that
                 # writes a full-resolution tensor of 3/4 zeros which that epilogue then reads back
-                conv_backward(b.down, s_down, ddc, x, False)  # weight gradient only
                 wd = b.down.conv.kernel.data
                 dsc = G.linear_dgrad(ddc.view(gd.M, gd.Co), wd.view(gd.Co, gd.Ci))
                 rsub = (gd.H, gd.W)
+                conv_backward(b.down, s_down, ddc, x, False)  # weight gradient + hook, after the last weight read
             else:
                 dsc = conv_backward(b.down, s_down, ddc, x, ctx.needs_dx)
         # dX = dgrad(conv1) + dShortcut: the residual add rides in the conv1 dgrad epilogue, and so do the
@@ -531,8 +534,6 @@ def _seq_conv_backward(ctx, dyc):
             conv.kernel.grad.add_(tmp[..., : ctx.ci])
         else:  # padded storage: it takes the zero-padded channels' (zero) gradients as is
             CV.conv_wgrad_native(dyc, x, g, conv.kernel.pgrad if ctx.w is conv.kernel.pdata else conv.kernel.grad)
-    if conv.grad_hook is not None:
-        conv.grad_hook()
     dx = None
     if ctx.needs_dx:
         bnr = None if ctx.prev is None else _bnr_mode2(ctx.prev[1], dyc.device)
@@ -540,6 +541,8 @@ def _seq_conv_backward(ctx, dyc):
         if bnr is not None:
             _take_reduced(ctx.prev[1], bnr, dx)
         dx = ZP.logical(dx, ctx.ci)
+    if conv.grad_hook is not None:  # after the last read of the weights (see conv_backward)
+        conv.grad_hook()
     ctx.st = ctx.prev = ctx.x = None
     return dx
 
