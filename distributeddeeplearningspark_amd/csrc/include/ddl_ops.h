@@ -179,6 +179,10 @@ int embed_pos_grad(const void* ds, float* gpos, int B, int S, int H, hipStream_t
 // out[n] (+)= sum_p ws[p][n]
 int colsum_partials(const float* ws, int P, int N, float* out, int accumulate, hipStream_t s, long ld = 0);
 // out[t] = word[ids[t]] + pos[t % S] + type[types[t]]  (bf16 tables, types nullable -> row 0)
+// BERT MLM head rows (layernorm.hip): out[b P + i] = h[b S + pos[b][i]] (bf16 [B S][H] -> [B P][H]) and its
+// backward dh[b S + q] = sum_{i : pos[b][i] == q} dout[b P + i] (every row of dh written, zeros elsewhere)
+int mlm_gather(const void* h, const int64_t* pos, void* out, int B, int S, int P, int H, hipStream_t s);
+int mlm_scatter(const void* dout, const int64_t* pos, void* dh, int B, int S, int P, int H, hipStream_t s);
 int embed_fwd(const int64_t* ids, const int64_t* types, const void* word, const void* pos, const void* type,
               void* out, long T, int S, int H, hipStream_t s);
 // gword[ids[t]] += ds[t] (fp32 atomics), gpos[t % S] += ds[t]; per-wave partial rows of the

@@ -594,9 +594,89 @@ __global__ __launch_bounds__(256) void embed_pos_grad_kernel(const bf16_t* __res
   gpos[col * 2 + 1] += b;
 }
 
+// BERT MLM head input: the hidden rows of the masked positions.  Row r = b P + i of out is row b S + pos[b][i] of
+// h (positions outside [0, S) give a zero row), computed in-kernel from the [B][P] positions (no arange / add /
+// index_select launches).  One wave per row, 16-B vectors.
+__global__ __launch_bounds__(256) void mlm_gather_kernel(const bf16_t* __restrict__ h, const int64_t* __restrict__ pos,
+                                                         bf16_t* __restrict__ out, int B, int S, int P, int H) {
+  const int lane = threadIdx.x & 63;
+  const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= (long)B * P) return;
+  const long b = r / P;
+  const int64_t q = pos[r];
+  const bool ok = q >= 0 && q < S;
+  const uint4* src = reinterpret_cast<const uint4*>(h + (b * S + (ok ? q : 0)) * (long)H);
+  uint4* dst = reinterpret_cast<uint4*>(out + r * (long)H);
+  for (int v = lane; v < (H >> 3); v += 64) dst[v] = ok ? src[v] : make_uint4(0u, 0u, 0u, 0u);
+}
+
+// Its backward: dh[t] = sum of dout[b P + i] over the i with pos[b][i] == t - b S (b = t / S), in increasing i
+// (duplicated padding positions sum in a fixed order: deterministic, no atomics), zero elsewhere — ONE pass that
+// writes every row of dh (no zero fill + index_add).  One wave per row t: the wave ballots its sequence's P
+// positions 64 at a time.
+__global__ __launch_bounds__(256) void mlm_scatter_kernel(const bf16_t* __restrict__ dout,
+                                                          const int64_t* __restrict__ pos, bf16_t* __restrict__ dh,
+                                                          int B, int S, int P, int H) {
+  const int lane = threadIdx.x & 63;
+  const long t = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= (long)B * S) return;
+  const long b = t / S;
+  const int64_t q = t - b * S;
+  const int nv = H >> 3;
+  constexpr int VMAX = 4;  // H <= 2048
+  float acc[VMAX][8];
+#pragma unroll
+  for (int u = 0; u < VMAX; ++u)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[u][e] = 0.f;
+  for (int i0 = 0; i0 < P; i0 += 64) {
+    const int i = i0 + lane;
+    unsigned long long m = __ballot(i < P && pos[b * P + i] == q);
+    while (m) {
+      const int k = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      const uint4* src = reinterpret_cast<const uint4*>(dout + (b * P + i0 + k) * (long)H);
+#pragma unroll
+      for (int u = 0; u < VMAX; ++u) {
+        const int v = lane + 64 * u;
+        if (v < nv) {
+          float f[8];
+          unpack8(src[v], f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[u][e] += f[e];
+        }
+      }
+    }
+  }
+  uint4* dst = reinterpret_cast<uint4*>(dh + t * (long)H);
+#pragma unroll
+  for (int u = 0; u < VMAX; ++u) {
+    const int v = lane + 64 * u;
+    if (v < nv) dst[v] = pack8f(acc[u]);
+  }
+}
+
 constexpr int kLnBwdBlocks = 512;  // 2 waves/SIMD: LN bwd 48 -> 37 us per BERT call (256: 1 wave/SIMD, latency-bound)
 
 }  // namespace
+
+int mlm_gather(const void* h, const int64_t* pos, void* out, int B, int S, int P, int H, hipStream_t s) {
+  if (H % 8 || H > 2048) return (int)hipErrorInvalidValue;
+  const long rows = (long)B * P;
+  if (rows <= 0) return 0;
+  hipLaunchKernelGGL(mlm_gather_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s,
+                     reinterpret_cast<const bf16_t*>(h), pos, reinterpret_cast<bf16_t*>(out), B, S, P, H);
+  return (int)hipGetLastError();
+}
+
+int mlm_scatter(const void* dout, const int64_t* pos, void* dh, int B, int S, int P, int H, hipStream_t s) {
+  if (H % 8 || H > 2048) return (int)hipErrorInvalidValue;
+  const long rows = (long)B * S;
+  if (rows <= 0) return 0;
+  hipLaunchKernelGGL(mlm_scatter_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s,
+                     reinterpret_cast<const bf16_t*>(dout), pos, reinterpret_cast<bf16_t*>(dh), B, S, P, H);
+  return (int)hipGetLastError();
+}
 
 int layernorm_fwd(const void* x, const float* gamma, const float* beta, void* y, float* mean, float* rstd, long M,
                   int H, float eps, float drop_p, unsigned long long seed, hipStream_t s) {

@@ -208,6 +208,28 @@ void embed_fwd_(const at::Tensor& ids, c10::optional<at::Tensor> types, const at
 
 int64_t embed_partial_rows_(int64_t T) { return ln_partial_rows(T); }
 
+// MLM head rows: out [B*P, H] = rows b*S + pos[b][i] of h [B*S, H]; mlm_scatter_: its backward into dh [B*S, H]
+void mlm_gather_(const at::Tensor& h, const at::Tensor& pos, const at::Tensor& out, int64_t S) {
+  GPU(h); BF16(h); I64(pos); BF16(out);
+  CK(pos.is_cuda() && out.is_cuda() && pos.device() == h.device() && out.device() == h.device(), "mlm_gather: one GPU");
+  CK(h.dim() == 2 && pos.dim() == 2 && h.size(0) == pos.size(0) * S && out.size(0) == pos.numel() &&
+         out.size(1) == h.size(1) && h.size(1) % 8 == 0 && h.size(1) <= 2048,
+     "mlm_gather: h [B*S, H], pos [B, P], out [B*P, H], H % 8 == 0, H <= 2048");
+  at::DeviceGuard g(h.device());
+  HIP_OK(mlm_gather(h.data_ptr(), pos.data_ptr<int64_t>(), out.data_ptr(), (int)pos.size(0), (int)S, (int)pos.size(1),
+                    (int)h.size(1), cur_stream()));
+}
+void mlm_scatter_(const at::Tensor& dout, const at::Tensor& pos, const at::Tensor& dh, int64_t S) {
+  GPU(dout); BF16(dout); I64(pos); BF16(dh);
+  CK(pos.is_cuda() && dh.is_cuda() && pos.device() == dout.device() && dh.device() == dout.device(), "mlm_scatter: one GPU");
+  CK(dh.dim() == 2 && pos.dim() == 2 && dh.size(0) == pos.size(0) * S && dout.size(0) == pos.numel() &&
+         dout.size(1) == dh.size(1) && dh.size(1) % 8 == 0 && dh.size(1) <= 2048,
+     "mlm_scatter: dout [B*P, H], pos [B, P], dh [B*S, H], H % 8 == 0, H <= 2048");
+  at::DeviceGuard g(dh.device());
+  HIP_OK(mlm_scatter(dout.data_ptr(), pos.data_ptr<int64_t>(), dh.data_ptr(), (int)pos.size(0), (int)S,
+                     (int)pos.size(1), (int)dh.size(1), cur_stream()));
+}
+
 void embed_bwd_(const at::Tensor& ids, c10::optional<at::Tensor> types, const at::Tensor& ds,
                 c10::optional<at::Tensor> gword, c10::optional<at::Tensor> gpos, c10::optional<at::Tensor> wsT,
                 int64_t ntypes, int64_t S) {
@@ -250,6 +272,8 @@ void register_transformer(py::module& m) {
   m.def("colsum_partials", &colsum_partials_, py::arg("ws"), py::arg("P"), py::arg("N"), py::arg("out"),
         py::arg("accumulate"), py::arg("ld") = 0);
   m.def("embed_fwd", &embed_fwd_);
+  m.def("mlm_gather", &mlm_gather_);
+  m.def("mlm_scatter", &mlm_scatter_);
   m.def("embed_partial_rows", &embed_partial_rows_);
   m.def("embed_bwd", &embed_bwd_);
 }

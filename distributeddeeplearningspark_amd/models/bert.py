@@ -487,6 +487,26 @@ class _MLMHeadFn(torch.autograd.Function):
         return dhm, None, None, None, None, None, None
 
 
+class _MaskedRowsFn(torch.autograd.Function):
+    """hm[b P + i] = h[b S + pos[b, i]] (the MLM head's input rows) and its backward (a sum over duplicated
+    positions), each ONE HIP launch (layernorm.hip mlm_gather / mlm_scatter)."""
+
+    @staticmethod
+    def forward(ctx, h, pos, S):
+        out = torch.empty((pos.numel(), h.shape[1]), dtype=h.dtype, device=h.device)
+        C().mlm_gather(h.contiguous(), pos, out, S)
+        ctx.save_for_backward(pos)
+        ctx.S, ctx.T = S, h.shape[0]
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (pos,) = ctx.saved_tensors
+        dh = torch.empty((ctx.T, dout.shape[1]), dtype=dout.dtype, device=dout.device)
+        C().mlm_scatter(dout.contiguous(), pos, dh, ctx.S)
+        return dh, None, None
+
+
 def _gelu_grad(x):
     return 0.5 * (1.0 + torch.erf(x * 0.7071067811865476)) + x * 0.3989422804014327 * torch.exp(-0.5 * x * x)
 
@@ -559,8 +579,11 @@ class BertForMaskedLM(Model):
         S = x["input_ids"].shape[1]
         pos = y["positions"].long()
         B, Pm = pos.shape
-        flat = (pos + torch.arange(B, device=pos.device).view(B, 1) * S).reshape(-1)
-        hm = h.index_select(0, flat)
+        if use_native(h):  # HIP row gather / scatter-sum (no arange, index_select, zero fill or index_add launches)
+            hm = _MaskedRowsFn.apply(h, pos.contiguous(), S)
+        else:
+            flat = (pos + torch.arange(B, device=pos.device).view(B, 1) * S).reshape(-1)
+            hm = h.index_select(0, flat)
         labels = y["labels"].reshape(-1).long()
         n_valid = y.get("num_masked")
         if n_valid is None and not use_native(hm):
