@@ -310,6 +310,156 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
   }
 }
 
+// 8-byte-vector form for H = 256 NQ (NQ = 1..4; BERT-base H = 768: NQ = 3): one wave per row, each lane owns NQ
+// 4-column quads (64 lanes x 8 B = one contiguous 512-B segment per load instruction), so every lane is busy —
+// the 16-B form leaves a third of the lanes without their second vector at H = 768 — and the per-lane
+// parameter-gradient partials are 3 x 4 NQ registers (the 16-B form holds 3 x 16).  The next row's dy / x /
+// statistics are loaded before this row's math.  Partial rows: one per workgroup (LDS block reduce), the layout
+// of ln_bwd_kernel's BR form, so colsum_partials finishes both.
+__device__ __forceinline__ void unpack4(const uint2& u, float* f) {
+  f[0] = __uint_as_float(u.x << 16);
+  f[1] = __uint_as_float(u.x & 0xffff0000u);
+  f[2] = __uint_as_float(u.y << 16);
+  f[3] = __uint_as_float(u.y & 0xffff0000u);
+}
+__device__ __forceinline__ uint2 pack4f(const float* f) {
+  return make_uint2(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]));
+}
+
+template <int NQ>
+__global__ __launch_bounds__(256) void ln_bwd_q_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                       const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                       const float* __restrict__ gamma, bf16_t* __restrict__ dx,
+                                                       bf16_t* __restrict__ dxd, uint32_t thresh, float dscale,
+                                                       unsigned long long seed, float* __restrict__ ws, long M, int H,
+                                                       uint32_t in_thresh, float in_scale, unsigned long long in_seed,
+                                                       int parts) {
+  const int lane = threadIdx.x & 63;
+  const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const long nwaves = (long)gridDim.x * 4;
+  float dg[NQ][4], db[NQ][4], dd[NQ][4], gmv[NQ][4];
+#pragma unroll
+  for (int u = 0; u < NQ; ++u) {
+    const int c = lane + 64 * u;  // quad index: columns 4c .. 4c + 3
+    const float4 g = gamma ? reinterpret_cast<const float4*>(gamma)[c] : make_float4(1.f, 1.f, 1.f, 1.f);
+    gmv[u][0] = g.x; gmv[u][1] = g.y; gmv[u][2] = g.z; gmv[u][3] = g.w;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dg[u][e] = db[u][e] = dd[u][e] = 0.f;
+  }
+  uint2 ndy[NQ], nx[NQ];
+  float nmu = 0.f, nrs = 0.f;
+  auto fetch = [&](long r) {
+#pragma unroll
+    for (int u = 0; u < NQ; ++u) {
+      ndy[u] = *reinterpret_cast<const uint2*>(dy + r * H + (lane + 64 * u) * 4);
+      nx[u] = *reinterpret_cast<const uint2*>(x + r * H + (lane + 64 * u) * 4);
+    }
+    nmu = mean[r];
+    nrs = rstd[r];
+  };
+  if (wave < M) fetch(wave);
+  for (long row = wave; row < M; row += nwaves) {
+    uint2 cdy[NQ], cx[NQ];
+#pragma unroll
+    for (int u = 0; u < NQ; ++u) {
+      cdy[u] = ndy[u];
+      cx[u] = nx[u];
+    }
+    const float mu = nmu, rs = nrs;
+    if (row + nwaves < M) fetch(row + nwaves);
+    float gy[NQ][4], xh[NQ][4];
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int u = 0; u < NQ; ++u) {
+      const int c = lane + 64 * u;
+      float d[4], xv[4];
+      unpack4(cdy[u], d);
+      unpack4(cx[u], xv);
+      if (in_thresh) {  // dy arrives through the forward's output dropout
+        const uint32_t kb = drop_bits4(in_seed, (unsigned long long)row * (unsigned long long)H + c * 4, in_thresh);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) d[e] = ((kb >> e) & 1u) ? d[e] * in_scale : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float xhat = (xv[e] - mu) * rs;
+        dg[u][e] += d[e] * xhat;
+        db[u][e] += d[e];
+        xh[u][e] = xhat;
+        gy[u][e] = d[e] * gmv[u][e];
+        a += gy[u][e];
+        b += gy[u][e] * xhat;
+      }
+    }
+    a = warp_sum(a) / (float)H;
+    b = warp_sum(b) / (float)H;
+#pragma unroll
+    for (int u = 0; u < NQ; ++u) {
+      const int c = lane + 64 * u;
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = rs * (gy[u][e] - a - xh[u][e] * b);
+      uint2 packed = pack4f(o);
+      *reinterpret_cast<uint2*>(dx + row * H + c * 4) = packed;
+      if (dxd) {
+        const uint32_t kb = drop_bits4(seed, (unsigned long long)row * (unsigned long long)H + c * 4, thresh);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = ((kb >> e) & 1u) ? o[e] * dscale : 0.f;
+        packed = pack4f(o);
+        *reinterpret_cast<uint2*>(dxd + row * H + c * 4) = packed;
+      }
+      if (parts == 3) {  // column sums of the stored gradient (dx_drop, else dx): the sublayer's bias grad
+        float r[4];
+        unpack4(packed, r);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dd[u][e] += r[e];
+      }
+    }
+  }
+  if (!ws) return;
+  constexpr int CW = 4 * 64 * NQ;  // = H
+  __shared__ float red[3][3 * CW];
+  const int w = threadIdx.x >> 6;
+  if (w > 0) {
+    float* r = red[w - 1];
+#pragma unroll
+    for (int u = 0; u < NQ; ++u) {
+      const int c = lane + 64 * u;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        r[c * 4 + e] = dd[u][e];
+        r[CW + c * 4 + e] = dg[u][e];
+        r[2 * CW + c * 4 + e] = db[u][e];
+      }
+    }
+  }
+  __syncthreads();
+  if (w != 0) return;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const float* r = red[q];
+#pragma unroll
+    for (int u = 0; u < NQ; ++u) {
+      const int c = lane + 64 * u;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        dd[u][e] += r[c * 4 + e];
+        dg[u][e] += r[CW + c * 4 + e];
+        db[u][e] += r[2 * CW + c * 4 + e];
+      }
+    }
+  }
+  float* wb = ws + (long)blockIdx.x * parts * H;
+  float* w0 = parts == 3 ? wb + H : wb;
+#pragma unroll
+  for (int u = 0; u < NQ; ++u) {
+    const int c = lane + 64 * u;
+    if (parts == 3) *reinterpret_cast<float4*>(wb + c * 4) = make_float4(dd[u][0], dd[u][1], dd[u][2], dd[u][3]);
+    *reinterpret_cast<float4*>(w0 + c * 4) = make_float4(dg[u][0], dg[u][1], dg[u][2], dg[u][3]);
+    *reinterpret_cast<float4*>(w0 + H + c * 4) = make_float4(db[u][0], db[u][1], db[u][2], db[u][3]);
+  }
+}
+
 // out[n] += sum_p ws[p][n]; block = 64 columns x 16 row-lanes over a chunk of kColsumRows rows,
 // grid.y = row chunks (one fp32 atomic per column per block; out zeroed by the launcher when
 // not accumulating)
@@ -725,7 +875,11 @@ int layernorm_bwd(const void* dy, const void* x, const float* mean, const float*
   auto X = reinterpret_cast<const bf16_t*>(x);
   auto DX = reinterpret_cast<bf16_t*>(dx);
   auto DD = reinterpret_cast<bf16_t*>(dx_drop);
-  if (nv <= 64) hipLaunchKernelGGL((ln_bwd_kernel<1, true, true>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts);
+  // BERT-base: 8-B vectors, three per lane, every lane busy (ln_bwd_q_kernel): 30.3 -> 21.1 us per call,
+  // BERT-base 900-902K -> 916-919K tok/s (profiles/r6/ab_ln_bwd.txt)
+  if (nv == 96)
+    hipLaunchKernelGGL((ln_bwd_q_kernel<3>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts);
+  else if (nv <= 64) hipLaunchKernelGGL((ln_bwd_kernel<1, true, true>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts);
   else if (nv <= 128) hipLaunchKernelGGL((ln_bwd_kernel<2, true, true>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts);
   else if (nv <= 256) hipLaunchKernelGGL((ln_bwd_kernel<4, false>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts);
   else hipLaunchKernelGGL((ln_bwd_kernel<8, false>), grid, dim3(256), 0, s, DY, X, mean, rstd, gamma, DX, DD, thresh, dscale, seed, ws, M, H, ith, iscale, in_seed, parts);
