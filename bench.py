@@ -44,9 +44,10 @@ def main():
     ap.add_argument("--reduce-dtype", default=None, choices=["fp32", "bf16"],
                     help="gradient all-reduce wire dtype (default DDL_REDUCE_DTYPE or fp32)")
     ap.add_argument("--graph", type=int, default=None,
-                    help="1 = replay the whole step from a hipGraph (1-GPU runs without a process group "
-                         "only).  Default off: measured neutral on ResNet-50 (9,532 vs 9,562 img/s) and "
-                         "VGG-16 (74.3K vs 75.1K img/s) — both steps are GPU-bound, not launch-bound")
+                    help="1 = replay the whole step from a hipGraph (1-GPU runs without a process group only; "
+                         "N > 1 steps stay eager: their bucket all-reduces are issued from backward hooks).  "
+                         "Default: on for a 1-GPU run — measured +0.7-0.8 %% on ResNet-50 at 402 launches per step "
+                         "(12,461-12,480 -> 12,550-12,586 img/s interleaved on one box, profiles/r6/ab_graph.txt)")
     ap.add_argument("--via-dataframe", action="store_true",
                     help="ResNet-50 through the DataFrame/trainer API: an ImageNet-shape uint8 frame, one partition "
                          "per rank, SynchronousDataParallel(...).train(df); the timed window is the trainer's own "
@@ -158,8 +159,9 @@ def make_ddp(model, pg, args):
 def make_step(ddp, args):
     """The timed step: ``ddp.train_step`` (eager launches + bucket hooks) or, on a 1-GPU run
     without a process group, the same step replayed from a hipGraph (``models/step.py``)."""
-    use_graph = args.graph if args.graph is not None else 0
-    if not use_graph or ddp.pg.distributed or ddp.model.device.type != "cuda":
+    use_graph = args.graph if args.graph is not None else 1
+    if (not use_graph or ddp.pg.distributed or ddp.model.device.type != "cuda"
+            or not getattr(ddp.model, "graph_capturable", True)):  # BERT: host-seeded dropout, eager steps
         return ddp.train_step
     from distributeddeeplearningspark_amd.models.step import CompiledTrainStep
 
