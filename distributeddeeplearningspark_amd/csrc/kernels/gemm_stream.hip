@@ -368,19 +368,37 @@ int num_cus() {
 template <int WN, int K, int BMODE>
 int launch_ws(const GemmParams& p, hipStream_t s) {
   using CF = gst::Cfg<WN, K>;
+  // variants launch_gemm_stream never routes here are not instantiated (they would spill): a residual on the
+  // 256-wide K = 128 panel, the fused BN-backward reduce on panels wider than 128 (64 at K = 256)
+  constexpr bool kRes = !(WN == 64 && K == 128);
+  constexpr bool kBnr = CF::NB <= (K >= 256 ? 64 : 128);
   const int panels = p.N / CF::NB;
   const int mt = (p.M + gst::BM - 1) / gst::BM;
   const int gx = std::max(1, std::min(mt, 2 * num_cus() / std::max(1, panels)));
   if (p.bnr_x && p.bnr_scale) {  // mode 2 (no residual: a BN + ReLU without a shortcut)
-    if (p.resid) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL((gemm_stream_kernel<WN, K, BMODE, false, 2>), dim3(gx, panels), dim3(gst::THREADS), 0, s, p);
+    if constexpr (kBnr) {
+      if (p.resid) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_stream_kernel<WN, K, BMODE, false, 2>), dim3(gx, panels), dim3(gst::THREADS), 0, s, p);
+    } else {
+      return (int)hipErrorInvalidValue;
+    }
   } else if (p.bnr_x) {
-    if (p.resid)
-      hipLaunchKernelGGL((gemm_stream_kernel<WN, K, BMODE, true, 1>), dim3(gx, panels), dim3(gst::THREADS), 0, s, p);
-    else
+    if constexpr (kBnr && kRes) {
+      if (p.resid)
+        hipLaunchKernelGGL((gemm_stream_kernel<WN, K, BMODE, true, 1>), dim3(gx, panels), dim3(gst::THREADS), 0, s, p);
+      else
+        hipLaunchKernelGGL((gemm_stream_kernel<WN, K, BMODE, false, 1>), dim3(gx, panels), dim3(gst::THREADS), 0, s, p);
+    } else if constexpr (kBnr) {
+      if (p.resid) return (int)hipErrorInvalidValue;
       hipLaunchKernelGGL((gemm_stream_kernel<WN, K, BMODE, false, 1>), dim3(gx, panels), dim3(gst::THREADS), 0, s, p);
+    } else {
+      return (int)hipErrorInvalidValue;
+    }
   } else if (p.resid) {
-    hipLaunchKernelGGL((gemm_stream_kernel<WN, K, BMODE, true>), dim3(gx, panels), dim3(gst::THREADS), 0, s, p);
+    if constexpr (kRes)
+      hipLaunchKernelGGL((gemm_stream_kernel<WN, K, BMODE, true>), dim3(gx, panels), dim3(gst::THREADS), 0, s, p);
+    else
+      return (int)hipErrorInvalidValue;
   } else {
     hipLaunchKernelGGL((gemm_stream_kernel<WN, K, BMODE, false>), dim3(gx, panels), dim3(gst::THREADS), 0, s, p);
   }
