@@ -605,22 +605,49 @@ __device__ __forceinline__ void gemm_epilogue_bnr(const GemmParams& p, f32x4 (&a
   col_stats_atomics<RN>(s1, s2, st, p.N, nb, lane);
 }
 
-// The bf16 epilogue over fragment columns [J0, J0 + RNP) of the wave tile (gemm_epilogue): the full epilogue of
-// the 128x128 kernels runs it in two column halves, so the per-column state (bias, statistics, packed stores)
-// of only half the columns is live at once — the 128-VGPR kernels no longer spill in it.
-template <int RM, int RN, int EPI, bool WIDE, int J0, int RNP>
-__device__ __forceinline__ void gemm_epilogue_cols(const GemmParams& p, f32x4 (&acc)[RM][RN], const int mb,
-                                                   const int nb, const int lane, const int bid, const int mlim,
-                                                   const long coff, const long boff) {
+// WIDE: the LITE epilogue's paired 16-B stores (off for the gathered-A LDS-DMA kernels: their address state
+// leaves no registers for the pair, 0 -> 24 B scratch and +0.03 ms/step on ResNet-50)
+template <int RM, int RN, int EPI, bool WIDE = true>
+__device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[RM][RN], const int mb, const int nb,
+                                              const int lane, const int bid, int mend = -1, long coff = 0,
+                                              long boff = 0) {
+  const int mlim = mend < 0 ? p.M : mend;
+  if constexpr (EPI == EPI_BF16_BNR) {
+    gemm_epilogue_bnr<RM, RN>(p, acc, mb, nb, lane, bid, mlim);
+    return;
+  }
+  // ---------------------------------- epilogue ----------------------------------
   constexpr bool BF = EPI == EPI_BF16 || EPI == EPI_BF16_LITE;
   constexpr bool LITE = EPI == EPI_BF16_LITE;
-  // acc[i][J0 + j][e] = C[m = m0+wm0+16i+(lane&15)][n = n0+wn0+16j+4*(lane>>4)+e]: each lane owns
+  if constexpr (!BF) {
+    // fp32 (weight-gradient) epilogue, D orientation: acc[i][j][e] = C[m0+wm0+16i+4(lane>>4)+e][n0+wn0+16j+(lane&15)]
+    // -> each atomic wave-instruction covers 4 rows x 64 contiguous bytes.
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      const int n = nb + 16 * j + (lane & 15);
+      if (n >= p.N) continue;
+#pragma unroll
+      for (int i = 0; i < RM; ++i) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int m = mb + 16 * i + 4 * (lane >> 4) + e;
+          if (m >= mlim) continue;
+          float* c = reinterpret_cast<float*>(p.c) + coff + (long)m * p.ldc + n;
+          const float v = acc[i][j][e] * p.alpha;
+          if constexpr (EPI == EPI_F32) *c = (p.beta != 0.f) ? v + p.beta * *c : v;
+          else atomicAdd(c, v);
+        }
+      }
+    }
+    return;
+  }
+  // acc[i][j][e] = C[m = m0+wm0+16i+(lane&15)][n = n0+wn0+16j+4*(lane>>4)+e]: each lane owns
   // 4 consecutive columns of one row -> 8-B (bf16x4) / 16-B (f32x4) vector stores.
   const int mrow = lane & 15;
   const int ncol = 4 * (lane >> 4);
-  float s1[RNP][4], s2[RNP][4];
+  float s1[RN][4], s2[RN][4];
 #pragma unroll
-  for (int j = 0; j < RNP; ++j)
+  for (int j = 0; j < RN; ++j)
 #pragma unroll
     for (int e = 0; e < 4; ++e) s1[j][e] = s2[j][e] = 0.f;
   const bool vec_ok = (p.ldc % 4) == 0 && (LITE || !p.resid || (p.ldr % 4) == 0);
@@ -634,10 +661,10 @@ __device__ __forceinline__ void gemm_epilogue_cols(const GemmParams& p, f32x4 (&
   // after every output store (p.bias may alias p.c), 4 * RM * RN dependent loads per lane
   // (one 16-B load per fragment column group where the 4 columns are in range: n % 4 == 0 and the
   // bias is a 16-B aligned fp32 vector — host check)
-  float bias_r[RNP][4];
+  float bias_r[RN][4];
 #pragma unroll
-  for (int j = 0; j < RNP; ++j) {
-    const int n = nb + 16 * (J0 + j) + ncol;
+  for (int j = 0; j < RN; ++j) {
+    const int n = nb + 16 * j + ncol;
     if (p.bias && n + 3 < p.N) {
       const float4 bv = *reinterpret_cast<const float4*>(p.bias + boff + n);
       bias_r[j][0] = bv.x;
@@ -653,7 +680,7 @@ __device__ __forceinline__ void gemm_epilogue_cols(const GemmParams& p, f32x4 (&
   for (int i = 0; i < RM; ++i) {
     const int m = mb + 16 * i + mrow;
     if (m >= mlim) continue;
-    uint2 pk[RNP];  // this row's packed bf16x4 per fragment (BF), stored after the column loop
+    uint2 pk[RN];  // this row's packed bf16x4 per fragment (BF), stored after the column loop
     long rowoff;
     int nn = 0, ii = 0, jj = 0;
     if (!LITE && p.om.enabled) {
@@ -663,13 +690,13 @@ __device__ __forceinline__ void gemm_epilogue_cols(const GemmParams& p, f32x4 (&
       rowoff = (long)m * p.ldc;
     }
 #pragma unroll
-    for (int j = 0; j < RNP; ++j) {
-      const int n = nb + 16 * (J0 + j) + ncol;
+    for (int j = 0; j < RN; ++j) {
+      const int n = nb + 16 * j + ncol;
       if (n >= p.N) continue;
       const bool full = vec_ok && (n + 3 < p.N);
       float v[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = acc[i][J0 + j][e] * p.alpha;
+      for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * p.alpha;
       if constexpr (BF) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] += bias_r[j][e];
@@ -753,11 +780,11 @@ __device__ __forceinline__ void gemm_epilogue_cols(const GemmParams& p, f32x4 (&
         }
         bf16_t* c = reinterpret_cast<bf16_t*>(p.c) + coff + rowoff + n;
         pk[j] = make_uint2((uint32_t)o[0] | ((uint32_t)o[1] << 16), (uint32_t)o[2] | ((uint32_t)o[3] << 16));
-        if (wide_ok && (j & 1) == 0 && j + 1 < RNP && nb + 16 * (J0 + j) + 32 <= p.N) {
+        if (wide_ok && (j & 1) == 0 && j + 1 < RN && nb + 16 * j + 32 <= p.N) {
           // stored with fragment j + 1 below
-        } else if (wide_ok && (j & 1) == 1 && nb + 16 * (J0 + j) + 16 <= p.N) {
+        } else if (wide_ok && (j & 1) == 1 && nb + 16 * j + 16 <= p.N) {
           // pair (j - 1, j), wave-uniform condition (pair_store)
-          pair_store(reinterpret_cast<bf16_t*>(p.c) + coff + rowoff + nb + 16 * (J0 + j - 1), pk[j - 1], pk[j], lane);
+          pair_store(reinterpret_cast<bf16_t*>(p.c) + coff + rowoff + nb + 16 * (j - 1), pk[j - 1], pk[j], lane);
         } else if (full) {
           *reinterpret_cast<uint2*>(c) = pk[j];
         } else {
@@ -792,8 +819,8 @@ __device__ __forceinline__ void gemm_epilogue_cols(const GemmParams& p, f32x4 (&
             if (wy >= p.om.wy || (a == p.om.oh && b == p.om.ow)) continue;
             bf16_t* z = cb + ((long)(nn * p.om.hy + hy) * p.om.wy + wy) * p.ldc;
 #pragma unroll
-            for (int j = 0; j < RNP; ++j) {
-              const int n = nb + 16 * (J0 + j) + ncol;
+            for (int j = 0; j < RN; ++j) {
+              const int n = nb + 16 * j + ncol;
               if (n + 3 < p.N && vec_ok) *reinterpret_cast<uint2*>(z + n) = make_uint2(0, 0);
               else
                 for (int e = 0; e < 4; ++e)
@@ -806,50 +833,7 @@ __device__ __forceinline__ void gemm_epilogue_cols(const GemmParams& p, f32x4 (&
   }
   if constexpr (BF) {
     if (p.stats)  // reduce over the 16 rows held by lanes sharing (lane>>4), whole-wave atomics
-      col_stats_atomics<RNP>(s1, s2, p.stats + (long)(bid % kStatShards) * 2 * p.N, p.N, nb + 16 * J0, lane);
-  }
-}
-
-// WIDE: the LITE epilogue's paired 16-B stores (off for the gathered-A LDS-DMA kernels: their address state
-// leaves no registers for the pair, 0 -> 24 B scratch and +0.03 ms/step on ResNet-50)
-template <int RM, int RN, int EPI, bool WIDE = true>
-__device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[RM][RN], const int mb, const int nb,
-                                              const int lane, const int bid, int mend = -1, long coff = 0,
-                                              long boff = 0) {
-  const int mlim = mend < 0 ? p.M : mend;
-  if constexpr (EPI == EPI_BF16_BNR) {
-    gemm_epilogue_bnr<RM, RN>(p, acc, mb, nb, lane, bid, mlim);
-    return;
-  }
-  // ---------------------------------- epilogue ----------------------------------
-  constexpr bool BF = EPI == EPI_BF16 || EPI == EPI_BF16_LITE;
-  if constexpr (!BF) {
-    // fp32 (weight-gradient) epilogue, D orientation: acc[i][j][e] = C[m0+wm0+16i+4(lane>>4)+e][n0+wn0+16j+(lane&15)]
-    // -> each atomic wave-instruction covers 4 rows x 64 contiguous bytes.
-#pragma unroll
-    for (int j = 0; j < RN; ++j) {
-      const int n = nb + 16 * j + (lane & 15);
-      if (n >= p.N) continue;
-#pragma unroll
-      for (int i = 0; i < RM; ++i) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int m = mb + 16 * i + 4 * (lane >> 4) + e;
-          if (m >= mlim) continue;
-          float* c = reinterpret_cast<float*>(p.c) + coff + (long)m * p.ldc + n;
-          const float v = acc[i][j][e] * p.alpha;
-          if constexpr (EPI == EPI_F32) *c = (p.beta != 0.f) ? v + p.beta * *c : v;
-          else atomicAdd(c, v);
-        }
-      }
-    }
-    return;
-  }
-  if constexpr (EPI == EPI_BF16 && RN == 4) {
-    gemm_epilogue_cols<RM, RN, EPI, WIDE, 0, 2>(p, acc, mb, nb, lane, bid, mlim, coff, boff);
-    gemm_epilogue_cols<RM, RN, EPI, WIDE, 2, 2>(p, acc, mb, nb, lane, bid, mlim, coff, boff);
-  } else {
-    gemm_epilogue_cols<RM, RN, EPI, WIDE, 0, RN>(p, acc, mb, nb, lane, bid, mlim, coff, boff);
+      col_stats_atomics<RN>(s1, s2, p.stats + (long)(bid % kStatShards) * 2 * p.N, p.N, nb, lane);
   }
 }
 

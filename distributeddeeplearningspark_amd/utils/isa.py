@@ -49,9 +49,12 @@ def code_objects(path: str, arch: str = "gfx950") -> list[bytes]:
 _FUNC = re.compile(r"^[0-9a-f]+ <(.+)>:$")
 
 
-def kernel_instruction_counts(path: str, arch: str = "gfx950") -> dict[str, Counter]:
-    """{mangled kernel symbol: Counter(mnemonic)} over all code objects."""
+def kernel_instruction_counts(path: str, arch: str = "gfx950", loop_scratch: dict | None = None) -> dict[str, Counter]:
+    """{mangled kernel symbol: Counter(mnemonic)} over all code objects.  ``loop_scratch`` (optional dict) receives
+    {symbol: scratch instructions placed before the kernel's LAST s_barrier} — for the LDS-staged GEMM / conv
+    kernels, whose K-loop ends at its last barrier, the spills that the main loop can execute."""
     res: dict[str, Counter] = {}
+    order: dict[str, list] = {}
     with tempfile.TemporaryDirectory() as d:
         for i, co in enumerate(code_objects(path, arch)):
             f = os.path.join(d, f"co{i}.o")
@@ -64,11 +67,18 @@ def kernel_instruction_counts(path: str, arch: str = "gfx950") -> dict[str, Coun
                 m = _FUNC.match(line.strip())
                 if m:
                     cur = res.setdefault(m.group(1), Counter())
+                    seq = order.setdefault(m.group(1), [])
                     continue
                 s = line.strip()
                 if cur is None or not s or s.startswith(";") or ":" in s.split()[0]:
                     continue
                 cur[s.split()[0]] += 1
+                if loop_scratch is not None and (s.startswith("scratch_") or s.startswith("s_barrier")):
+                    seq.append(s.split()[0])
+    if loop_scratch is not None:
+        for k, seq in order.items():
+            last = max((i for i, op in enumerate(seq) if op == "s_barrier"), default=-1)
+            loop_scratch[k] = sum(1 for op in seq[:last] if op.startswith("scratch_"))
     return res
 
 
@@ -86,7 +96,8 @@ def demangle(names):
 
 def summary(path: str, arch: str = "gfx950") -> list[dict]:
     """Per-kernel rows: MFMA / LDS-transpose / LDS-DMA / scratch instruction counts."""
-    counts = kernel_instruction_counts(path, arch)
+    loop = {}
+    counts = kernel_instruction_counts(path, arch, loop)
     names = list(counts)
     rows = []
     for name, pretty in zip(names, demangle(names)):
@@ -100,6 +111,7 @@ def summary(path: str, arch: str = "gfx950") -> list[dict]:
             "lds_dma": sum(v for k, v in c.items() if k.startswith(("buffer_load", "global_load_lds"))
                            and "lds" in k),
             "scratch": sum(v for k, v in c.items() if k.startswith("scratch_")),
+            "loop_scratch": loop.get(name, 0),
         })
     rows.sort(key=lambda r: -r["mfma"])
     return rows

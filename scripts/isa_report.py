@@ -11,7 +11,7 @@ from distributeddeeplearningspark_amd.utils.isa import summary  # noqa: E402
 rows = summary(os.path.join(ROOT, "distributeddeeplearningspark_amd", "_C.so"))
 out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "profiles", "isa_summary.csv")
 with open(out, "w", newline="") as f:
-    w = csv.DictWriter(f, fieldnames=["kernel", "instructions", "mfma", "ds_read_tr", "lds_dma", "scratch"])
+    w = csv.DictWriter(f, fieldnames=["kernel", "instructions", "mfma", "ds_read_tr", "lds_dma", "scratch", "loop_scratch"])
     w.writeheader()
     w.writerows(rows)
 print(f"{len(rows)} kernels -> {out}; with MFMA: {sum(r['mfma'] > 0 for r in rows)}; "
