@@ -849,6 +849,8 @@ constexpr int kLnBwdBlocksBR = 1024;  // block-reduced form: 4,096 waves (4 per 
 
 // partial rows [P][parts][H] layernorm_bwd writes for M rows of width H
 int ln_bwd_rows(long M, int H) {
+  static const long cap = std::getenv("DDL_LN_BWD_BLOCKS") ? std::atol(std::getenv("DDL_LN_BWD_BLOCKS")) : 0;  // A/B
+  if (H / 8 == 96 && cap > 0) return (int)std::max<long>(1, std::min<long>(cap, (M + 3) / 4));
   if (H / 8 <= 128) return (int)std::max<long>(1, std::min<long>((long)kLnBwdBlocksBR, (M + 3) / 4));
   return ln_partial_rows(M);
 }
