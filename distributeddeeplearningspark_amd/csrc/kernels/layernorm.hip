@@ -482,6 +482,47 @@ __global__ __launch_bounds__(1024) void colsum_kernel(const float* __restrict__ 
   }
 }
 
+// 16-B form (N, ld % 4 == 0): a workgroup = 64 column quads (256 columns) x 4 row-lanes over a chunk of 32 rows;
+// every lane keeps four row loads in flight (the 4-B form issued one dependent load per row: 7.4 us for BERT's
+// 1024 x 2304 LayerNorm partial rows, 1.3 TB/s).  One fp32 atomic per column per workgroup.
+constexpr int kColsumVecRows = 32;
+__global__ __launch_bounds__(256) void colsum_vec_kernel(const float* __restrict__ ws, int P, int N, long ld,
+                                                         float* __restrict__ out) {
+  __shared__ float4 red[4][64];
+  const int q = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int n = blockIdx.x * 256 + q * 4;
+  const int p0 = blockIdx.y * kColsumVecRows, p1 = min(P, p0 + kColsumVecRows);
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (n < N) {
+    int p = p0 + rl;
+    for (; p + 12 < p1; p += 16) {
+      float4 v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = *reinterpret_cast<const float4*>(ws + (long)(p + 4 * r) * ld + n);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        a.x += v[r].x; a.y += v[r].y; a.z += v[r].z; a.w += v[r].w;
+      }
+    }
+    for (; p < p1; p += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(ws + (long)p * ld + n);
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+  }
+  red[rl][q] = a;
+  __syncthreads();
+  if (rl == 0 && n < N) {
+#pragma unroll
+    for (int r = 1; r < 4; ++r) {
+      a.x += red[r][q].x; a.y += red[r][q].y; a.z += red[r][q].z; a.w += red[r][q].w;
+    }
+    atomicAdd(out + n, a.x);
+    atomicAdd(out + n + 1, a.y);
+    atomicAdd(out + n + 2, a.z);
+    atomicAdd(out + n + 3, a.w);
+  }
+}
+
 // deterministic mode: 16 columns x 64 row-lanes per workgroup (4x the workgroups of colsum_kernel's
 // one-chunk form, a quarter of the serial loop), rows summed in a fixed order, one writer per column
 __global__ __launch_bounds__(1024) void colsum_det_kernel(const float* __restrict__ ws, int P, int N, long ld,
@@ -849,8 +890,9 @@ constexpr int kLnBwdBlocksBR = 1024;  // block-reduced form: 4,096 waves (4 per 
 
 // partial rows [P][parts][H] layernorm_bwd writes for M rows of width H
 int ln_bwd_rows(long M, int H) {
-  static const long cap = std::getenv("DDL_LN_BWD_BLOCKS") ? std::atol(std::getenv("DDL_LN_BWD_BLOCKS")) : 0;  // A/B
-  if (H / 8 == 96 && cap > 0) return (int)std::max<long>(1, std::min<long>(cap, (M + 3) / 4));
+  // H = 768 (ln_bwd_q_kernel, 148 VGPRs: 3 waves per SIMD): one round of 768 workgroups — LN backward + its column
+  // sum 27.1 -> 24.9 us per BERT call vs 1,024 (512: 24.8, 1,536: 28.4; profiles/r6/ln_blocks.txt)
+  if (H / 8 == 96) return (int)std::max<long>(1, std::min<long>(768L, (M + 3) / 4));
   if (H / 8 <= 128) return (int)std::max<long>(1, std::min<long>((long)kLnBwdBlocksBR, (M + 3) / 4));
   return ln_partial_rows(M);
 }
@@ -897,6 +939,12 @@ int colsum_partials(const float* ws, int P, int N, float* out, int accumulate, h
   // deterministic mode: one writer per column, partial rows summed in a fixed order
   if (deterministic()) {
     hipLaunchKernelGGL(colsum_det_kernel, dim3((N + 15) / 16), dim3(1024), 0, s, ws, P, N, ld > 0 ? ld : (long)N, out);
+    return (int)hipGetLastError();
+  }
+  const long ldv = ld > 0 ? ld : (long)N;
+  if (N % 4 == 0 && ldv % 4 == 0 && (reinterpret_cast<uintptr_t>(ws) & 15) == 0) {
+    hipLaunchKernelGGL(colsum_vec_kernel, dim3((N + 255) / 256, (P + kColsumVecRows - 1) / kColsumVecRows), dim3(256), 0,
+                       s, ws, P, N, ldv, out);
     return (int)hipGetLastError();
   }
   const int chunk = kColsumRows;

@@ -217,9 +217,11 @@ def test_resnet50_curve_inside_fp32_envelope():
 
 
 def test_resnet50_envelope_catches_dropped_shortcut_term():
-    """The same check with the shortcut gradient of every bottleneck dropped (fused_blocks._TEST_MUTATION): the
-    network still trains, but the curve leaves the fp32 band."""
-    h = _hard_curve(("drop_shortcut", None))
+    """The same check with ONE bottleneck's shortcut gradient dropped (stage 3's last block,
+    fused_blocks._TEST_MUTATION): the network still trains (loss 3.1 -> 0.63 over 150 steps), but from steps 60-70
+    on the curve leaves the fp32 band (measured 1.42 against a band top of 1.32 there, 1.14 against 0.41 at steps
+    100-110; profiles/r6/convergence_envelope.txt)."""
+    h = _hard_curve(("drop_shortcut", "resnet50/s3b6"))
     bad, _ = _envelope_violations(h)
     print("mutated HIP windows", [round(float(h[a:a + 10].mean()), 3) for a in range(0, len(h), 10)], "violations", bad)
     assert bad, "a dropped shortcut gradient stayed inside the fp32 envelope"

@@ -409,3 +409,18 @@ def test_layernorm_bwd_many_rows_per_wave(parts):
     """M = 9001 (> 4 x the 512-workgroup cap, not a multiple of 4): every wave accumulates its
     dgamma / dbeta (/ dbias) partial row over several LayerNorm rows."""
     _ln_bwd_case(9001, 768, parts)
+
+
+@pytest.mark.parametrize("P,N,ld", [(1024, 2304, 2304), (1001, 772, 776), (37, 96, 96), (513, 10, 10)])
+def test_colsum_partials(P, N, ld):
+    """colsum_partials: out[n] (+)= sum_p ws[p][n] — the 16-B four-rows-in-flight form (N, ld % 4 == 0, partial
+    row chunks) and the 4-B form, against an fp64 column sum."""
+    from distributeddeeplearningspark_amd.ops._native import C
+
+    ws = torch.randn(P, ld, device=DEV)
+    out = torch.full((N,), 0.5, device=DEV)
+    C().colsum_partials(ws, P, N, out, True, ld)
+    ref = ws[:, :N].double().sum(0) + 0.5
+    torch.testing.assert_close(out.double(), ref, rtol=1e-5, atol=1e-4)
+    C().colsum_partials(ws, P, N, out, False, ld)
+    torch.testing.assert_close(out.double(), ref - 0.5, rtol=1e-5, atol=1e-4)
