@@ -269,7 +269,7 @@ int softmax_rows_fwd(const void* x, void* y, long R, int N, int bf16, hipStream_
 int softmax_rows_bwd(const void* dy, const void* y, void* dx, long R, int N, int bf16, hipStream_t s);
 // y = keep(i) ? x * scale : 0 with keep(i) = drop_keep(seed, i, thresh), thresh = drop_t8(p) (also the backward)
 int dropout_apply(const void* x, void* y, long n, unsigned long long seed, uint32_t thresh, float scale, int bf16,
-                  hipStream_t s);
+                  hipStream_t s, const float* dstep = nullptr);
 // NHWC average pooling, padding excluded from the divisor
 int avgpool2d_fwd(const void* x, void* y, int N, int H, int W, int C, int Ho, int Wo, int kh, int kw, int sh, int sw,
                   int ph, int pw, int bf16, hipStream_t s);

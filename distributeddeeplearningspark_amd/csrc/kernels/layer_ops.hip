@@ -64,9 +64,12 @@ __global__ __launch_bounds__(256) void softmax_bwd_kernel(const T* __restrict__ 
   for (int j = lane; j < N; j += 64) stf(dx + o, j, ldf(y + o, j) * (ldf(dy + o, j) - d));
 }
 
+// dstep (nullable): a device step counter (fp32, whole numbers) mixed into the seed, so a hipGraph replaying the
+// step draws a fresh mask every replay (models/step.py ticks it once per step); the backward reads the same value
 template <class T>
 __global__ void dropout_kernel(const T* __restrict__ x, T* __restrict__ y, long n, unsigned long long seed,
-                               uint32_t thresh, float scale) {
+                               uint32_t thresh, float scale, const float* __restrict__ dstep) {
+  if (dstep) seed += (unsigned long long)(*dstep) * 0x9E3779B97F4A7C15ull;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256)
     stf(y, i, drop_keep(seed, (unsigned long long)i, thresh) ? ldf(x, i) * scale : 0.f);
 }
@@ -314,14 +317,14 @@ int softmax_rows_bwd(const void* dy, const void* y, void* dx, long R, int N, int
 }
 
 int dropout_apply(const void* x, void* y, long n, unsigned long long seed, uint32_t thresh, float scale, int bf16,
-                  hipStream_t s) {
+                  hipStream_t s, const float* dstep) {
   if (n <= 0) return 0;
   if (bf16)
     hipLaunchKernelGGL(dropout_kernel<bf16_t>, dim3(blocks_for(n)), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y, n,
-                       seed, thresh, scale);
+                       seed, thresh, scale, dstep);
   else
     hipLaunchKernelGGL(dropout_kernel<float>, dim3(blocks_for(n)), dim3(256), 0, s, (const float*)x, (float*)y, n, seed,
-                       thresh, scale);
+                       thresh, scale, dstep);
   return (int)hipGetLastError();
 }
 

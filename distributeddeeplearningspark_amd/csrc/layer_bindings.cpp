@@ -69,15 +69,18 @@ void softmax_bwd_(const at::Tensor& dy, const at::Tensor& y, const at::Tensor& d
   HIP_OK(softmax_rows_bwd(dy.data_ptr(), y.data_ptr(), dx.data_ptr(), dy.numel() / N, (int)N, bf, cur_stream()));
 }
 
-void dropout_(const at::Tensor& x, const at::Tensor& y, double p, int64_t seed) {
+// dstep (optional fp32 [1] GPU tensor): device step counter mixed into the seed (graph-replayed steps)
+void dropout_(const at::Tensor& x, const at::Tensor& y, double p, int64_t seed, c10::optional<at::Tensor> dstep) {
   const int bf = float_kind(x, "dropout x");
   float_kind(y, "dropout y");
   same(x, y, "dropout");
   CK(p >= 0.0 && p < 1.0, "dropout: rate must be in [0, 1)");
+  if (dstep) CK(dstep->is_cuda() && dstep->scalar_type() == at::kFloat && dstep->numel() == 1 &&
+                    dstep->device() == x.device(), "dropout: dstep must be an fp32 [1] tensor on x's device");
   const uint32_t thresh = drop_t8(p);  // rate quantised to 1/256 (ddl_ops.h)
   at::DeviceGuard g(x.device());
   HIP_OK(dropout_apply(x.data_ptr(), y.data_ptr(), x.numel(), (unsigned long long)seed, thresh, drop_scale8(thresh),
-                       bf, cur_stream()));
+                       bf, cur_stream(), dstep ? dstep->data_ptr<float>() : nullptr));
 }
 
 void avgpool2d_fwd_(const at::Tensor& x, const at::Tensor& y, int64_t kh, int64_t kw, int64_t sh, int64_t sw,
@@ -233,7 +236,8 @@ void register_layer_ops(py::module& m) {
   m.def("act_bwd", &act_bwd_, "dx = dy * act'(ref), ref = y (x for GELU)");
   m.def("softmax_fwd", &softmax_fwd_, "softmax over the last axis");
   m.def("softmax_bwd", &softmax_bwd_, "softmax backward");
-  m.def("dropout", &dropout_, "counter-hash dropout (forward and backward)");
+  m.def("dropout", &dropout_, "counter-hash dropout (forward and backward)", py::arg("x"), py::arg("y"), py::arg("p"),
+        py::arg("seed"), py::arg("dstep") = py::none());
   m.def("avgpool2d_fwd", &avgpool2d_fwd_, "NHWC average pooling");
   m.def("avgpool2d_bwd", &avgpool2d_bwd_, "NHWC average pooling backward");
   m.def("colsum_f32", &colsum_f32_, "db += column sums of dy (fp32)");

@@ -241,13 +241,12 @@ class Model(Layer):
 
     @property
     def graph_capturable(self) -> bool:
-        """False when a layer draws host-seeded per-step state (an active Dropout): a replayed
-        hipGraph would freeze its mask, so ``models/step.py`` trains such a model eagerly."""
+        """False when the model draws host-side per-step state a replayed hipGraph would freeze (BERT's
+        step-seeded dropout sets it).  Dropout layers do not: inside a capture their kernels mix a device step
+        counter into the seed, which every captured step ticks (``ops/act.py dropout_step_counter``)."""
         if "_graph_capturable" in self.__dict__:
             return self.__dict__["_graph_capturable"]
-        from .layers import Dropout
-
-        return not any(isinstance(l, Dropout) and l.rate > 0 for l in self.all_layers())
+        return True
 
     @graph_capturable.setter
     def graph_capturable(self, v: bool):

@@ -15,9 +15,10 @@ Graph-safety of the captured work:
 * statistics workspaces come from a pool whose layout is fixed after the first step;
 * the Adam step counter lives on the device (``Optimizer.enable_device_step``), so the
   bias corrections advance on every replay;
-* ``torch.nn.functional.dropout`` draws from torch's graph-aware Philox state.
-Models that need host-side per-step state (gradient clipping by global norm, models
-with host-seeded dropout hashes) report ``graph_capturable = False`` and run eagerly.
+* Dropout layers' counter-hash kernels mix a device step counter into their capture-time seeds and the
+  captured step ticks it, so every replay draws fresh masks (``ops/act.py dropout_step_counter``).
+Models that need host-side per-step state (gradient clipping by global norm, BERT's step-seeded
+dropout hashes) report ``graph_capturable = False`` and run eagerly.
 
 Used by the dist-keras workers (``trainers.py``) whenever a worker trains on a GPU.
 """
@@ -30,6 +31,12 @@ import torch
 
 def graphs_enabled() -> bool:
     return os.environ.get("DDL_GRAPHS", "1") != "0"
+
+
+def _uses_dropout(model) -> bool:
+    from .layers import Dropout
+
+    return any(isinstance(l, Dropout) and l.rate > 0 for l in model.all_layers())
 
 
 class CompiledTrainStep:
@@ -87,6 +94,10 @@ class CompiledTrainStep:
                 loss = m.backward_step(self.static_x, self.static_y)
                 m.optimizer.captured_update(1.0)
                 self.static_loss = loss.detach().float()
+                if _uses_dropout(m):  # fresh dropout masks on every replay (ops/act.py)
+                    from ..ops.act import tick_dropout_step
+
+                    tick_dropout_step(m.device)
         torch.cuda.current_stream(m.device).wait_stream(s)
         from ..ops.norm import _POOL
 

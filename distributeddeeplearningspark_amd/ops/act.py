@@ -126,19 +126,40 @@ def next_seed(base: int | None = None) -> int:
     return (b * 0x9E3779B97F4A7C15 + next(_SEEDS) * 0xBF58476D1CE4E5B9) & 0x7FFFFFFFFFFFFFFF
 
 
+_DSTEP: dict = {}  # device -> fp32 [1] dropout step counter of graph-replayed steps (models/step.py)
+
+
+def dropout_step_counter(device) -> torch.Tensor:
+    """The device's dropout step counter: a captured step's dropout kernels mix it into their (capture-time) seeds
+    and the replayed graph ticks it once per step (``tick_dropout_step``), so every replay draws fresh masks."""
+    d = torch.device(device)
+    key = (d.type, d.index if d.index is not None else torch.cuda.current_device())
+    t = _DSTEP.get(key)
+    if t is None:
+        t = _DSTEP[key] = torch.zeros(1, dtype=torch.float32, device=d)
+    return t
+
+
+def tick_dropout_step(device):
+    """+1 on the device's dropout step counter (one HIP launch; captured at the end of a graph-replayed step)."""
+    C().step_tick(dropout_step_counter(device))
+
+
 class _DropoutFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, p, seed):
         x = x.contiguous()
         y = torch.empty_like(x)
-        C().dropout(x, y, p, seed)
-        ctx.p, ctx.seed = p, seed
+        # inside a hipGraph capture the seed is fixed at capture time: the device counter varies it per replay
+        ds = dropout_step_counter(x.device) if torch.cuda.is_current_stream_capturing() else None
+        C().dropout(x, y, p, seed, ds)
+        ctx.p, ctx.seed, ctx.ds = p, seed, ds
         return y
 
     @staticmethod
     def backward(ctx, dy):
         dx = torch.empty_like(dy, memory_format=torch.contiguous_format)
-        C().dropout(dy.contiguous(), dx, ctx.p, ctx.seed)  # same counter hash -> same mask
+        C().dropout(dy.contiguous(), dx, ctx.p, ctx.seed, ctx.ds)  # same counter hash -> same mask
         return dx, None, None
 
 

@@ -116,6 +116,12 @@ class _Replica:
             loss = m.backward_step(m.to_input(self.sx), m.to_target(self.sy))
             if captured:  # ``more``: another captured step follows (it skips its zero_grad fill)
                 m.optimizer.captured_update(1.0, zero_grads=more)
+                from ..models.step import _uses_dropout
+
+                if _uses_dropout(m):  # fresh dropout masks on every replayed step (ops/act.py)
+                    from ..ops.act import tick_dropout_step
+
+                    tick_dropout_step(m.device)
             else:
                 m.optimizer.step(1.0)
             C().step_record(loss.detach().float().reshape(1), self.hist, self.ctr)
