@@ -41,4 +41,11 @@ ws = torch.randn(P, 3 * 768, device="cuda")
 red = torch.zeros(3 * 768, device="cuda")
 out["colsum_rows"] = P
 out["colsum_us"] = round(statistics.median(t(lambda: C().colsum_partials(ws, P, 3 * 768, red, True)) for _ in range(5)), 1)
+for splits, M_, N_ in ((8, 3072, 768), (8, 2304, 768), (4, 3072, 768)):
+    ws8 = torch.randn(splits * M_ * N_, device="cuda")
+    c = torch.zeros(M_, N_, device="cuda")
+    us = statistics.median(t(lambda: C().slab_reduce(ws8, splits, c, M_, N_, N_, 1.0)) for _ in range(5))
+    by = (splits + 2) * M_ * N_ * 4
+    out[f"slab_reduce_{splits}x{M_}x{N_}_us"] = round(us, 1)
+    out[f"slab_reduce_{splits}x{M_}x{N_}_TBs"] = round(by / us / 1e6, 2)
 print(json.dumps(out))

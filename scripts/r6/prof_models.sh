@@ -1,0 +1,12 @@
+#!/bin/bash
+# Kernel profiles at HEAD: BERT-base (3 timed + 2 warmup steps) and ResNet-50 (5 + 3), rocprofv3 kernel trace +
+# stats, summarised by scripts/r5/trace_busy.py (per-step = totals / steps in the trace window).
+cd /tmp && export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r6/prof
+mkdir -p $O
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/bert -o bert -- python3 $R/bench.py --model bert --steps 3 --warmup 2 > $O/bert.log 2>&1 || exit 1
+python3 $R/scripts/r5/trace_busy.py $(find $O/bert -name '*kernel_trace.csv') 45 > $O/bert_busy.txt || exit 1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/rn50 -o rn50 -- python3 $R/bench.py --steps 5 --warmup 3 > $O/rn50.log 2>&1 || exit 1
+python3 $R/scripts/r5/trace_busy.py $(find $O/rn50 -name '*kernel_trace.csv') 45 > $O/rn50_busy.txt || exit 1
+find $O -type f -name '*kernel_trace.csv' -delete
