@@ -17,7 +17,9 @@
 //   attn_bwd_dkdv : a workgroup owns 128 keys (32 per wave), streams 64-query tiles of
 //                   Q/dO through LDS: S = Q K^T, dP = dO V^T, dV += P^T dO, dK += dS^T Q;
 //   attn_bwd_dq   : a workgroup owns 128 queries, streams K/V tiles: dQ += dS K.
-// (Two kernels instead of atomics on dQ: deterministic, no fp32 scratch.)
+// (Two kernels instead of atomics on dQ: deterministic, no fp32 scratch.)  dQ runs first and
+// also computes D = rowsum(dO * O) for its queries (it holds their dO already) into the
+// scratch dvec that dK/dV reads — no separate elementwise pass over O and dO.
 // Softmax uses base-2 exponentials with scale*log2(e) folded in; the forward saves the
 // base-2 log-sum-exp per query.  Dropout on the attention probabilities is a stateless
 // hash of (seed, b, h, i, j), regenerated in the backward.  Key padding: lens[b] valid
@@ -302,36 +304,6 @@ __global__ __launch_bounds__(THREADS, MINB) void attn_fwd_kernel(const AttnParam
   }
 }
 
-// ================================================================ backward: D = rowsum(dO * O)
-__global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const AttnParams p, long rows) {
-  // one 16-B vector per thread; 8 threads per (token, head) row of 64
-  const long gid = (long)blockIdx.x * 256 + threadIdx.x;
-  const long r = gid >> 3;
-  float acc = 0.f;
-  if (r < rows) {
-    const long tok = r / p.H;
-    const int h = (int)(r - tok * p.H);
-    const int c = (int)(gid & 7) * 8;
-    const uint4 a = *reinterpret_cast<const uint4*>(p.o + tok * p.ldo + h * HD + c);
-    const uint4 d = *reinterpret_cast<const uint4*>(p.dout + tok * p.lddo + h * HD + c);
-    const uint32_t av[4] = {a.x, a.y, a.z, a.w}, dv[4] = {d.x, d.y, d.z, d.w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      acc += __uint_as_float(av[e] << 16) * __uint_as_float(dv[e] << 16);
-      acc += __uint_as_float(av[e] & 0xffff0000u) * __uint_as_float(dv[e] & 0xffff0000u);
-    }
-  }
-  acc += __shfl_xor(acc, 1, 64);
-  acc += __shfl_xor(acc, 2, 64);
-  acc += __shfl_xor(acc, 4, 64);
-  if (r < rows && (gid & 7) == 0) {
-    const long tok = r / p.H;
-    const int h = (int)(r - tok * p.H);
-    const long b = tok / p.S, i = tok - b * p.S;
-    p.dvec[(b * p.H + h) * p.S + i] = acc;
-  }
-}
-
 // ================================================================ backward: dK, dV
 // MINB = resident blocks per CU the register allocation is capped for: 1 (no spills) or 2 (twice the
 // waves to hide latency); picked at launch by DDL_ATTN_DKDV_OCC (default 2).  Dropout is a template
@@ -547,8 +519,26 @@ __global__ __launch_bounds__(THREADS, MINB) void attn_bwd_dq_kernel(const AttnPa
       df[it][kk] = ldg_frag(dO + (long)i * p.lddo + 32 * kk + 8 * g);
     }
     lq[it] = p.lse[(long)bh * S + i];
-    dq[it] = p.dvec[(long)bh * S + i];
     if constexpr (DROP) hk[it] = row_key(p.drop_seed, bh, S, i) + (uint32_t)g;
+  }
+  // D_i = rowsum(dO * O): this block owns queries q0.., so it computes their D from the dO
+  // fragments it already holds (the four g-lanes of a row cover its 64 columns) and publishes it
+  // for the dK/dV kernel, which runs after this one — no separate pass over O and dO
+  const bf16_t* O = p.o + tok0 * p.ldo + h * HD;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int i = q0 + 16 * it + li;
+    float part = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const bf16x8 of = ldg_frag(O + (long)i * p.ldo + 32 * kk + 8 * g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) part = fmaf((float)of[e], (float)df[it][kk][e], part);
+    }
+    part += __shfl_xor(part, 16, 64);
+    part += __shfl_xor(part, 32, 64);
+    dq[it] = part;
+    if (g == 0) p.dvec[(long)bh * S + i] = part;
   }
   f32x4 acc[2][4];  // dQ[i = 16it + 4g + e][d = 16dt + li]
 #pragma unroll
@@ -660,12 +650,11 @@ int attn_bwd(const AttnParams& p_in, hipStream_t s) {
   if (p_in.B <= 0) return 0;
   AttnParams p = p_in;
   p.xcd_remap = attn_xcd();
-  const long rows = (long)p.B * p.S * p.H;
   const dim3 grid(p.S / BLOCK_ROWS, p.H, p.B);
   const bool drop = p.drop_t8 != 0;
-  hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s, p, rows);
-  DDL_ATTN_LAUNCH(attn_bwd_dkdv_kernel, grid, 2, drop, s, p);
+  // dQ first: it computes D = rowsum(dO * O) for its queries and writes p.dvec, which dK/dV reads
   DDL_ATTN_LAUNCH(attn_bwd_dq_kernel, grid, 2, drop, s, p);
+  DDL_ATTN_LAUNCH(attn_bwd_dkdv_kernel, grid, 2, drop, s, p);
   return (int)hipGetLastError();
 }
 
