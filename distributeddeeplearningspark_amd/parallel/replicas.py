@@ -49,11 +49,11 @@ def mode() -> str:
 def applies(cfg, devices) -> bool:
     if cfg.get("mode", "sync") != "sync" or cfg["algorithm"] not in COMMIT_RULES + ("averaging",):
         return False
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1:  # torchrun SPMD: the ranks are the workers
-        return False
     m = mode()
     if m == "0" or len(devices) < 2:
         return False
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:  # torchrun SPMD: k workers per rank, grouped by rank
+        return len(set(devices)) < len(devices)
     if m == "1" or (m.isdigit() and int(m) > 1):
         return True
     return devices[0] != "cpu" and len(set(devices)) < len(devices)

@@ -720,12 +720,23 @@ class _ShardedTrainer(Trainer):
         from .parallel import replicas as _rep
         from .parallel.launcher import plan_devices
 
-        if server is not None or self.num_workers < 2 or int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        if server is not None or self.num_workers < 2:
             return None
         if cfg.get("checkpoint_dir") or cfg.get("watchdog_s") or self.extra.get("max_restarts"):
             return None  # per-rank checkpoints / watchdog / restart live on the process-per-worker path
         if cfg.get("ingest", "auto") == "stream":
             return None
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        if world > 1:
+            # torchrun SPMD with more workers than ranks (the reference's 2 processes per executor on one
+            # process per GPU): rank r hosts workers r*k .. r*k + k - 1 as one replica group; the groups'
+            # commit sums meet over the job's process group.  num_workers == WORLD_SIZE keeps one worker
+            # per rank (process-per-worker SPMD).
+            if self.num_workers <= world or self.num_workers % world:
+                return None
+            k = self.num_workers // world
+            devices = [f"rank{w // k}" for w in range(self.num_workers)]
+            return devices if _rep.applies(cfg, devices) else None
         devices = plan_devices(self.num_workers, self.device)
         if not _rep.applies(cfg, devices):
             return None
@@ -741,7 +752,15 @@ class _ShardedTrainer(Trainer):
         from .parallel import replicas as _rep
 
         groups = _rep.plan(devices)
-        if len(groups) == 1:  # one device: the replicas train in this process (no executor hop)
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1:  # torchrun: this rank's group, results gathered
+            pg = comm.default_group() or comm.init_from_env()
+            if len(groups) != pg.world_size:
+                raise ValueError(f"{len(groups)} replica groups for torchrun world size {pg.world_size}")
+            g = groups[pg.rank]
+            res = _rep.train_group(pg.rank, pg.world_size, pg, cfg, self.master_model, [Xs[r] for r in g],
+                                   [Ys[r] for r in g], g, sizes)
+            res = [x for grp in pg.all_gather_object(res) for x in grp]
+        elif len(groups) == 1:  # one device: the replicas train in this process (no executor hop)
             g = groups[0]
             dev = torch.device(devices[g[0]])
             if dev.type == "cuda":

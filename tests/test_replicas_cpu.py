@@ -214,3 +214,47 @@ def test_replica_seq_plan_requires_flat_dense_inputs():
     mlp = Sequential([L.Dense(32, input_shape=(20,), activation="relu"), L.Dense(10, activation="softmax")])
     mlp.build_model()
     assert [k for k, _, _ in _plan(mlp)] == ["dense", "head"]
+
+
+@pytest.mark.parametrize("algo", ["ADAG", "AEASGD"])
+def test_replica_groups_under_torchrun(spark, monkeypatch, tmp_path, algo):
+    """torchrun SPMD with 4 workers on 2 ranks: each rank hosts 2 workers as one replica group and the groups'
+    commit sums meet over the job's (gloo) process group — the same center, histories and update count as
+    the 4 process-per-worker run (before, num_workers != WORLD_SIZE was an error under torchrun)."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    from distributeddeeplearningspark_amd import trainers as T
+
+    monkeypatch.setenv("DDL_REPLICA_GROUPS", "0")
+    base = Sequential([Dense(4, activation="relu", input_shape=(5,)), Dense(1)])
+    base.set_weights([np.full_like(w, 0.05 * (i + 1)) + np.linspace(-0.1, 0.1, w.size, dtype=np.float32).reshape(w.shape)
+                      for i, w in enumerate(base.get_weights())])
+    tr = getattr(T, algo)(keras_model=base, worker_optimizer="adam", loss="mean_squared_error", num_workers=4,
+                          batch_size=4, num_epoch=2, features_col="f", label_col="l", device="cpu",
+                          communication_window=3)
+    w_p = tr.train(_frame(spark)).get_weights()
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = tmp_path / "res.json"
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = {k: v for k, v in os.environ.items() if k not in ("DDL_REPLICA_GROUPS", "WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["PYTHONPATH"] = os.path.dirname(here)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port),
+                        os.path.join(here, "replica_torchrun_worker.py"), algo, str(out)],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(out.read_text())
+    assert [g["groups"] for g in res["replica_group"]] == [2, 2, 2, 2]
+    assert [g["group"] for g in res["replica_group"]] == [0, 0, 1, 1]
+    assert res["num_updates"] == tr.parameter_server.num_updates
+    for a, b in zip(tr.get_history(), res["history"]):
+        np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-6)
+    for a, b in zip(w_p, res["weights"]):
+        np.testing.assert_allclose(a, np.asarray(b, np.float32), rtol=1e-5, atol=1e-6)
