@@ -134,6 +134,9 @@ def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, bet
             tile = 0  # 128x128 + split-K slabs (see _SPLITK_SLABS_MODE)
         else:
             tile = choose_tile(M, N, bn_cap)
+    if (k_split is None and tile == 0 and epi == EPI_F32 and a_mode == RC and b_mode == RC and big_wgrad(M, N, K)
+            and _SPLITK_SLABS_MODE == "auto" and slabs is not False):
+        k_split = slab_split(M, N, K)
     if k_split is None:
         k_split = choose_split(M, N, K, tile, allow=(epi != EPI_BF16), rounds=split_rounds)
     split_stride = 0
@@ -179,9 +182,19 @@ _SPLITK_SLABS = _SPLITK_SLABS_MODE == "1"
 
 
 def big_wgrad(M: int, N: int, K: int) -> bool:
-    """An fp32 GEMM with more than 2^20 outputs over a long reduction (BERT's QKV / FFN weight gradients):
-    128x128 tiles split over K into partial slabs beat smaller tiles with fp32 atomics."""
-    return M * N > (1 << 20) and K >= 8192 and M >= 512 and N >= 512
+    """An fp32 GEMM with at least 2^19 outputs over a long reduction (BERT's QKV / FFN / attention-output weight
+    gradients): 128x128 tiles split over K into partial slabs beat smaller tiles with fp32 atomics."""
+    return M * N >= (1 << 19) and K >= 8192 and M >= 512 and N >= 512
+
+
+def slab_split(M: int, N: int, K: int) -> int:
+    """k_split of a 128x128 RC x RC partial-slab GEMM (weight gradient): as many splits as fill ONE round of
+    the kernel's 3 resident workgroups per CU, each split at least 18 K-tiles (1,152) deep.  BERT-base at
+    16,384 tokens (`scripts/r6/wgrad_splits.py`, TF/s incl. the slab reduce): QKV 7 splits 716 (was 10: 644),
+    FFN 5 splits 772 / 789 (was 8: 736 / 740), attention output 14 splits 513 (was 64x128 + atomics: 443)."""
+    tiles = math.ceil(M / 128) * math.ceil(N / 128)
+    splits = max(1, min((3 * _CU) // tiles, K // 1152))
+    return max(64, math.ceil(K / splits / 64) * 64)
 _SLAB_WS: dict = {}
 
 
