@@ -289,9 +289,18 @@ def linear_dgrad(dy, w, out=None, resid=None, gelu_pre=None, stats=None, resid_m
         # 30,522-word vocabulary ran on 240 workgroups of ~480 K-steps): split the reduction over
         # workgroups into an fp32 workspace, then round (+ statistics) in one finalize pass
         ws = splitk_workspace(M, K, dy.device)
-        splits = max(2, min(math.ceil(2048 / tiles), N // 512))
-        r = gemm(dy, w, ws, M, K, N, KC, RC, dy.stride(0), w.stride(0), K, EPI_F32, tile=3,
-                 k_split=math.ceil(N / splits / 64) * 64, defer_slabs=True)
+        t128 = math.ceil(M / 128) * math.ceil(K / 128)
+        if 2 * t128 <= 3 * _CU:
+            # 128x128 tiles on partial slabs, as many splits as fill one round of the kernel's 3 resident
+            # workgroups per CU (the decoder: 120 tiles x 6 splits): 205 -> 141 us vs 64x64 tiles + fp32
+            # atomics (scripts/r6/decoder_dgrad.py); the finalize sums the slabs in split order
+            splits = max(2, min((3 * _CU) // t128, N // 1152))
+            r = gemm(dy, w, ws, M, K, N, KC, RC, dy.stride(0), w.stride(0), K, EPI_F32, tile=0,
+                     k_split=math.ceil(N / splits / 64) * 64, defer_slabs=True, slabs=True)
+        else:
+            splits = max(2, min(math.ceil(2048 / tiles), N // 512))
+            r = gemm(dy, w, ws, M, K, N, KC, RC, dy.stride(0), w.stride(0), K, EPI_F32, tile=3,
+                     k_split=math.ceil(N / splits / 64) * 64, defer_slabs=True)
         if isinstance(r, tuple):  # partial slabs (DDL_SPLITK_SLABS): summed by the finalize itself
             C().splitk_finalize(r[0], out, K, None, False, stats, r[1])
         else:
