@@ -146,7 +146,7 @@ def gemm(a, b, c, M, N, K, a_mode, b_mode, lda, ldb, ldc, epi, *, alpha=1.0, bet
     if epi == EPI_F32 and k_split < K:
         if beta not in (0.0, 1.0):
             raise ValueError("split-K fp32 gemm supports beta in {0,1} (beta=0 needs a zeroed C)")
-        auto = _SPLITK_SLABS_MODE == "auto" and tile == 0 and big_wgrad(M, N, K) and math.ceil(K / k_split) <= 16
+        auto = _SPLITK_SLABS_MODE == "auto" and tile == 0 and big_wgrad(M, N, K) and math.ceil(K / k_split) <= 32
         use_slabs = (_det.enabled() or _SPLITK_SLABS or auto) if slabs is None else (slabs or _det.enabled())
         if tile in (0, 1, 2, 3) + _ONE_PER_CU and use_slabs:
             # partial slabs (plain stores) + an ordered reduce: deterministic, and the slab stores run at
