@@ -179,9 +179,18 @@ def conv_fwd_native(x, w, g: ConvGeometry, bias=None, relu=False, stats=None, bn
         ws = G.splitk_workspace(g.M, g.Co, x.device)
         K = g.T * g.Ci
         tiles = math.ceil(g.M / 64) * math.ceil(g.Co / 64)
-        splits = max(2, min(math.ceil(_SPLITK_WG / tiles), K // 512))  # ~4 workgroups per CU, >= 8 K-tiles each
-        r = G.gemm(x, w, ws, g.M, g.Co, K, G.KC_GATHER, G.KC, 0, K, g.Co, G.EPI_F32, geom=g.fwd_geom, tile=3,
-                   k_split=math.ceil(K / splits / 64) * 64, defer_slabs=True)
+        t128 = math.ceil(g.M / 128) * math.ceil(g.Co / 128)
+        s128 = min(768 // t128, K // 576)
+        if t128 >= 64 and s128 >= 6:
+            # enough 128x128 tiles and K depth for >= 6 splits of >= 9 K-tiles in one round at 3 workgroups
+            # per CU: partial slabs summed by the finalize (VGG-16's 4x4 512-channel layers: 52 -> 43 us,
+            # scripts/r6/vgg_splitk.py)
+            r = G.gemm(x, w, ws, g.M, g.Co, K, G.KC_GATHER, G.KC, 0, K, g.Co, G.EPI_F32, geom=g.fwd_geom, tile=0,
+                       k_split=math.ceil(K / s128 / 64) * 64, defer_slabs=True, slabs=True)
+        else:
+            splits = max(2, min(math.ceil(_SPLITK_WG / tiles), K // 512))  # ~4 workgroups per CU, >= 8 K-tiles
+            r = G.gemm(x, w, ws, g.M, g.Co, K, G.KC_GATHER, G.KC, 0, K, g.Co, G.EPI_F32, geom=g.fwd_geom, tile=3,
+                       k_split=math.ceil(K / splits / 64) * 64, defer_slabs=True)
         if isinstance(r, tuple):  # partial slabs (DDL_SPLITK_SLABS): summed by the finalize itself
             C().splitk_finalize(r[0], y2, g.Co, bias, bool(relu), stats, r[1])
         else:
