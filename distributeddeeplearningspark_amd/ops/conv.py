@@ -375,6 +375,18 @@ def conv_dgrad_native(dy, w, g: ConvGeometry, resid=None, resid_mask=None, bnr=N
     return dx
 
 
+def _slab_wgrad_splits(g: ConvGeometry) -> int:
+    """Split count of a gathered weight gradient on 128x128 partial slabs (0: not that path): one round of the
+    RC x RC_GATHER kernel's 3 resident workgroups per CU, >= 18 K-tiles per split, <= 32 slabs; only for
+    >= 24 output tiles whose 128-column blocks stay inside one tap (Ci % 128 == 0)."""
+    if g.Ci % 128 or _det.enabled():
+        return 0
+    t128 = math.ceil(g.Co / 128) * math.ceil(g.T * g.Ci / 128)
+    if t128 < 24:
+        return 0
+    return min((3 * G._CU) // t128, g.M // 1152, 32)
+
+
 def conv_wgrad_native(dy, x, g: ConvGeometry, gw):
     """gw[Co, KH, KW, Ci] (fp32) += dW."""
     gw2 = gw.view(g.Co, g.T * g.Ci)
@@ -392,6 +404,13 @@ def conv_wgrad_native(dy, x, g: ConvGeometry, gw):
         # 16-B vector (GATHER8) instead of per tile — twice the MFMA work per LDS fragment read
         G.gemm(dy, x, gw2, g.Co, g.T * g.Ci, g.M, G.RC, G.RC_GATHER8, g.Co, 0, g.T * g.Ci, G.EPI_F32, beta=1.0,
                geom=g.fwd_geom, bn_cap=128, split_rounds=_WGRAD_ROUNDS, tile=_wgrad_tile(g.Co, g.T * g.Ci, 128))
+    elif g.implicit_wgrad and _slab_wgrad_splits(g) >= 2:
+        # enough 128x128 output tiles (>= 24) for one round of 3 workgroups per CU with >= 2 splits: 128x128
+        # tiles on partial slabs, split count filling that round (ResNet-50's strided layers at 28^2 / 14^2:
+        # 3x3 115 -> 92 and 107 -> 83 us, 1x1 downsample 92 -> 77 and 92 -> 74 us; scripts/r6/gather_wgrad.py)
+        K = g.T * g.Ci
+        G.gemm(dy, x, gw2, g.Co, K, g.M, G.RC, G.RC_GATHER, g.Co, 0, K, G.EPI_F32, beta=1.0, geom=g.fwd_geom,
+               tile=0, k_split=math.ceil(g.M / _slab_wgrad_splits(g) / 64) * 64, slabs=True)
     elif g.implicit_wgrad:
         # gathered weight gradients are latency-bound per workgroup: 4 rounds of split-K workgroups
         # (measured: 3-16 % faster than 2 on the ResNet-50 3x3 / strided layers)

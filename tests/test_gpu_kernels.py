@@ -209,9 +209,29 @@ def test_linear_dgrad_splitk(M, slabs, monkeypatch):
     assert G.splitk_workspace(M, H, dy.device).abs().max().item() == 0.0
 
 
+@pytest.mark.parametrize("N,H,Ci,Co,k", [(64, 14, 512, 512, 3), (64, 14, 1024, 2048, 1), (32, 28, 256, 256, 3)])
+def test_gathered_wgrad_on_partial_slabs(N, H, Ci, Co, k):
+    """Strided weight gradients with >= 24 128x128 output tiles run on 128x128 partial slabs (one round of
+    3 workgroups per CU): against the fp32 reference, accumulating onto an existing gradient."""
+    from distributeddeeplearningspark_amd.ops import conv as CV
+
+    p = 1 if k == 3 else 0
+    g = CV.geometry(N, H, H, Ci, Co, k, k, (2, 2), (p, p), (1, 1))
+    assert CV._slab_wgrad_splits(g) >= 2
+    x = rnd(N, H, H, Ci, seed=70)
+    dy = rnd(N, g.Ho, g.Wo, Co, seed=71)
+    gw0 = torch.randn(Co, k, k, Ci, device=DEV)
+    gw = gw0.clone()
+    CV.conv_wgrad_native(dy, x, g, gw)
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (Co, Ci, k, k), dy.float().permute(0, 3, 1, 2),
+                                      stride=2, padding=p).permute(0, 2, 3, 1)
+    close(gw - gw0, ref, rtol=1e-2, atol=1e-2, what=f"slab wgrad {N}x{H}x{Ci}->{Co} k{k}")
+
+
 @pytest.mark.parametrize("slabs", [False, True])
 @pytest.mark.parametrize("relu", [False, True])
-def test_conv_splitk_forward_stats(relu, slabs, monkeypatch):
+@pytest.mark.parametrize("N,Co", [(16, 256), (256, 512)])
+def test_conv_splitk_forward_stats(relu, slabs, N, Co, monkeypatch):
     """Split-K forward of a small-grid conv: bias, ReLU and the fused per-channel statistics of the
     rounded bf16 output ([32, 2, C] sharded sums, as the GEMM epilogue writes them); with partial
     slabs the finalize sums them itself."""
@@ -220,7 +240,7 @@ def test_conv_splitk_forward_stats(relu, slabs, monkeypatch):
 
     monkeypatch.setattr(G, "_SPLITK_SLABS", slabs)
 
-    N, H, Ci, Co = 16, 4, 512, 256
+    H, Ci = 4, 512  # N = 256, Co = 512: VGG-16's 4x4 layer, 128x128 tiles on partial slabs (6 splits)
     g = CV.geometry(N, H, H, Ci, Co, 3, 3, (1, 1), (1, 1), (1, 1))
     assert CV.splitk_fwd_ok(g)
     x = rnd(N, H, H, Ci, seed=30)
