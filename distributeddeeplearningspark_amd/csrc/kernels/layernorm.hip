@@ -578,21 +578,42 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const int64_t* __restric
     for (int u = 0; u < 4; ++u)
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc[a][u][e] = 0.f;
-  for (long t = wave; t < T; t += nwaves) {
-    const long id = ids[t];
-    const int ty = types ? (int)types[t] : 0;
+  // four of the wave's tokens per trip: their row loads are issued together, then accumulated in token
+  // order (the same sums as one token at a time)
+  constexpr int TU = 4;
+  for (long t0 = wave; t0 < T; t0 += (long)TU * nwaves) {
+    uint4 raw[TU][4];
+    long id[TU];
+    int ty[TU];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int c = lane + 64 * u;
-      if (c < nv) {
-        float d[8];
-        unpack8(*reinterpret_cast<const uint4*>(ds + t * H + c * 8), d);
+    for (int j = 0; j < TU; ++j) {
+      const long t = t0 + (long)j * nwaves;
+      const bool ok = t < T;
+      id[j] = ok ? ids[t] : 0;
+      ty[j] = ok && types ? (int)types[t] : 0;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          if (gword) atomicAdd(gword + id * H + c * 8 + e, d[e]);
-          if (gpos) atomicAdd(gpos + (t % S) * H + c * 8 + e, d[e]);
-          if (ty == 0) acc[0][u][e] += d[e];
-          else acc[1][u][e] += d[e];
+      for (int u = 0; u < 4; ++u) {
+        const int c = lane + 64 * u;
+        if (ok && c < nv) raw[j][u] = *reinterpret_cast<const uint4*>(ds + t * H + c * 8);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < TU; ++j) {
+      const long t = t0 + (long)j * nwaves;
+      if (t >= T) break;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int c = lane + 64 * u;
+        if (c < nv) {
+          float d[8];
+          unpack8(raw[j][u], d);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            if (gword) atomicAdd(gword + id[j] * H + c * 8 + e, d[e]);
+            if (gpos) atomicAdd(gpos + (t % S) * H + c * 8 + e, d[e]);
+            if (ty[j] == 0) acc[0][u][e] += d[e];
+            else acc[1][u][e] += d[e];
+          }
         }
       }
     }
@@ -776,7 +797,19 @@ __global__ __launch_bounds__(256) void embed_pos_grad_kernel(const bf16_t* __res
   float a = 0.f, b = 0.f;
   const uint32_t* p = reinterpret_cast<const uint32_t*>(ds) + col;
   const long stride = (long)S * H / 2;
-  for (int r = 0; r < B; ++r) {
+  // 8 rows' loads in flight per lane, then summed in row order (the same sums as one row at a time)
+  int r = 0;
+  for (; r + 8 <= B; r += 8) {
+    uint32_t w[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) w[k] = p[(r + k) * stride];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      a += __uint_as_float(w[k] << 16);
+      b += __uint_as_float(w[k] & 0xffff0000u);
+    }
+  }
+  for (; r < B; ++r) {
     const uint32_t w = p[r * stride];
     a += __uint_as_float(w << 16);
     b += __uint_as_float(w & 0xffff0000u);
