@@ -24,9 +24,29 @@ Used by the dist-keras workers (``trainers.py``) whenever a worker trains on a G
 """
 from __future__ import annotations
 
+import contextlib
+import gc
 import os
 
 import torch
+
+
+@contextlib.contextmanager
+def graph_capture(g, stream):
+    """``torch.cuda.graph(g, stream=stream)`` with Python's cyclic garbage collector off for the capture: a
+    collection that starts inside a capture runs the destructors of unrelated garbage (events, graphs and
+    streams of finished models), and their HIP calls are illegal while a stream captures — the process
+    aborts (seen once in the GPU suite, a co-located replica capture collecting mid-window)."""
+    was = gc.isenabled()
+    gc.collect()
+    gc.disable()
+    try:
+        with torch.cuda.graph(g, stream=stream):
+            yield
+    finally:
+        if was:
+            gc.enable()
+
 
 
 def graphs_enabled() -> bool:
@@ -90,7 +110,7 @@ class CompiledTrainStep:
         s = torch.cuda.Stream(device=m.device)
         s.wait_stream(torch.cuda.current_stream(m.device))
         with torch.cuda.stream(s):
-            with torch.cuda.graph(g, stream=s):
+            with graph_capture(g, s):
                 loss = m.backward_step(self.static_x, self.static_y)
                 m.optimizer.captured_update(1.0)
                 self.static_loss = loss.detach().float()

@@ -33,6 +33,8 @@ import os
 
 import torch
 
+from ..models.step import graph_capture
+
 from ..models import optimizers as opt_mod
 
 
@@ -190,7 +192,7 @@ class BatchedReplicas:
             if os.environ.get("DDL_TEST_FAIL_CAPTURE") == "1":  # test hook: force the eager fallback
                 raise RuntimeError("capture forced to fail (DDL_TEST_FAIL_CAPTURE)")
             with torch.cuda.stream(s):
-                with torch.cuda.graph(g, stream=s):
+                with graph_capture(g, s):
                     for _ in range(k):
                         self._step()
         except Exception as e:

@@ -34,6 +34,8 @@ import os
 
 import torch
 
+from ..models.step import graph_capture
+
 from ..models import optimizers as opt_mod
 
 _MAX_R = 16  # kMaxBatchCopies / 2 (csrc/include/ddl_ops.h)
@@ -398,7 +400,7 @@ class SeqReplicas:
             if os.environ.get("DDL_TEST_FAIL_CAPTURE") == "1":
                 raise RuntimeError("capture forced to fail (DDL_TEST_FAIL_CAPTURE)")
             with torch.cuda.stream(s):
-                with torch.cuda.graph(g, stream=s):
+                with graph_capture(g, s):
                     for _ in range(k):
                         self._step()
         except Exception as e:

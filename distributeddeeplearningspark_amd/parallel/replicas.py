@@ -34,6 +34,8 @@ import time
 
 import torch
 
+from ..models.step import graph_capture
+
 COMMIT_RULES = ("adag", "dynsgd", "downpour", "easgd", "aeasgd", "eamsgd")
 ELASTIC = ("easgd", "aeasgd", "eamsgd")
 
@@ -150,7 +152,7 @@ class _Replica:
         m = self.model
         m.optimizer.enable_device_step()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=stream):
+        with graph_capture(g, stream):
             for i in range(k):
                 self._step_body(captured=True, more=i + 1 < k)
         from ..ops.norm import _POOL
