@@ -48,7 +48,6 @@ def graph_capture(g, stream):
             gc.enable()
 
 
-
 def graphs_enabled() -> bool:
     return os.environ.get("DDL_GRAPHS", "1") != "0"
 
