@@ -102,12 +102,69 @@ __device__ __forceinline__ void stage_a(const bf16_t* __restrict__ A, long lda, 
 
 }  // namespace gst
 
+// Side-operand loads of the residual / fused-BN-reduce epilogues (the residual rows, their ReLU mask, the BN
+// input x and its mask byte) as inline asm: like the LDS-DMA ring they are invisible to the compiler's
+// vmcnt model, so the only waits on them are the kernel's own counted ones.  Compiler-visible loads made
+// the compiler wait for them with a count that ignores the (invisible) ring DMAs issued after them, i.e.
+// it also drained the prefetch of the next A tile before every epilogue.
+typedef __attribute__((ext_vector_type(2))) unsigned u32x2_t;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
+__device__ __forceinline__ u32x4_t ald128(const void* p) {
+  u32x4_t v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ u32x2_t ald64(const void* p) {
+  u32x2_t v;
+  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ unsigned ald32(const void* p) {
+  unsigned v;
+  asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ unsigned ald16(const void* p) {
+  unsigned v;
+  asm volatile("global_load_ushort %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ unsigned ald8(const void* p) {
+  unsigned v;
+  asm volatile("global_load_ubyte %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+// ASM: the counted asm form (two-slot rings, K = 256: measured faster); otherwise plain loads the compiler
+// waits for itself (deeper rings, K = 64 / 128: the counted wait there also drained the older ring slots)
+template <bool ASM> __device__ __forceinline__ u32x4_t sld128(const void* p) {
+  if constexpr (ASM) return ald128(p);
+  return *reinterpret_cast<const u32x4_t*>(p);
+}
+template <bool ASM> __device__ __forceinline__ u32x2_t sld64(const void* p) {
+  if constexpr (ASM) return ald64(p);
+  return *reinterpret_cast<const u32x2_t*>(p);
+}
+template <bool ASM> __device__ __forceinline__ unsigned sld32(const void* p) {
+  if constexpr (ASM) return ald32(p);
+  return *reinterpret_cast<const uint32_t*>(p);
+}
+template <bool ASM> __device__ __forceinline__ unsigned sld16(const void* p) {
+  if constexpr (ASM) return ald16(p);
+  return *reinterpret_cast<const uint16_t*>(p);
+}
+template <bool ASM> __device__ __forceinline__ unsigned sld8(const void* p) {
+  if constexpr (ASM) return ald8(p);
+  return *reinterpret_cast<const uint8_t*>(p);
+}
+
+
 // BNR: 0 off; 1 the ReLU mask of the BN-backward reduce from GemmParams::bnr_mask (bits, or all ones);
 // 2 recomputed from the BN input as x * bnr_scale + bnr_shift > 0 (a BN without residual: mode 2)
 template <int WN, int K, int BMODE, bool RES, int BNR = 0>
 __global__ __launch_bounds__(gst::THREADS, 2) void gemm_stream_kernel(const GemmParams p) {
   using namespace gst;
   using CF = Cfg<WN, K>;
+  constexpr bool kAsmSide = CF::NBUF == 2;  // side-operand loads as counted asm (see sld128)
   // the ring and the output staging tile are separate objects: with one array the compiler cannot
   // tell the staging writes from the in-flight LDS-DMA and drains vmcnt(0) before them
   __shared__ __attribute__((aligned(16))) char smem[CF::LDS];  // [ring NBUF x TILE | staging tile]
@@ -182,49 +239,50 @@ __global__ __launch_bounds__(gst::THREADS, 2) void gemm_stream_kernel(const Gemm
     // staging barrier) with the tile NBUF - 1 iterations ahead
     const int m0 = tile_m0(i);
     // residual rows of this tile, issued ahead of the refill so their wait can be counted past it
-    uint2 rres[BM / 16][CF::RN];
+    // side operands (counted asm loads on two-slot rings, see sld128): issued ahead of the refill, so the DMA of
+    // the tile NBUF - 1 ahead is the youngest VMEM work when the epilogue waits for them (wait_vm<D>: the ring
+    // stays in flight)
+    u32x2_t rres[BM / 16][CF::RN];
     // residual ReLU mask (p.resid_mask): the 16 * RN columns this lane's row touches are 2 * RN
-    // consecutive mask bytes — one 2/4/8-byte load per row block; all ones when there is no mask
-    uint64_t rmsk[BM / 16];
+    // consecutive mask bytes — one 2/4/8-byte load per row block (from the residual itself when there is
+    // no mask: always issued, so the counted wait holds); rodd rows (stride-2 subgrid) add nothing
+    unsigned rmk32[BM / 16];
+    u32x2_t rmk64[CF::RN == 4 ? BM / 16 : 1];
+    unsigned rodd_bits = 0u;
+    const bool has_mask = p.resid_mask != nullptr;
     if constexpr (RES) {
-      const bool has_mask = p.resid_mask != nullptr;
 #pragma unroll
       for (int mb = 0; mb < BM / 16; ++mb) {
         const int m = min(m0 + 16 * mb + (lane & 15), p.M - 1);
         long rrow = m;  // stride-2 residual subgrid (GemmParams::rsub_h): odd rows add nothing
-        bool rodd = false;
         if (p.rsub_h) {
           int rn_, ri_, rj_;
           pix_decompose((uint32_t)m, p.rsub_h, p.rsub_w, rn_, ri_, rj_);
-          rodd = (ri_ | rj_) & 1;
+          const bool rodd = (ri_ | rj_) & 1;
+          rodd_bits |= (rodd ? 1u : 0u) << mb;
           rrow = rodd ? 0L : ((long)rn_ * ((p.rsub_h + 1) >> 1) + (ri_ >> 1)) * ((p.rsub_w + 1) >> 1) + (rj_ >> 1);
         }
         const long row = rrow * p.ldr + n0 + WN * w;
 #pragma unroll
         for (int rn = 0; rn < CF::RN; ++rn)
-          rres[mb][rn] = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(p.resid) + row + 16 * rn +
-                                                         4 * (lane >> 4));
-        rmsk[mb] = rodd ? 0ull : ~0ull;
-        if (has_mask && !rodd) {
-          const uint8_t* mp = p.resid_mask + (row >> 3);
-          if constexpr (CF::RN == 1) rmsk[mb] = *reinterpret_cast<const uint16_t*>(mp);
-          else if constexpr (CF::RN == 2) rmsk[mb] = *reinterpret_cast<const uint32_t*>(mp);
-          else rmsk[mb] = *reinterpret_cast<const uint64_t*>(mp);
-        }
+          rres[mb][rn] = sld64<kAsmSide>(reinterpret_cast<const bf16_t*>(p.resid) + row + 16 * rn + 4 * (lane >> 4));
+        const void* mp = has_mask ? (const void*)(p.resid_mask + (row >> 3)) : p.resid;
+        if constexpr (CF::RN == 1) rmk32[mb] = sld16<kAsmSide>(mp);
+        else if constexpr (CF::RN == 2) rmk32[mb] = sld32<kAsmSide>(mp);
+        else rmk64[mb] = sld64<kAsmSide>(mp);
       }
     }
-    // BNR: the BN input x and its ReLU-mask byte at this thread's read-out vectors (issued with the
-    // residual, ahead of the refill, for the same reason)
-    uint4 bx[BNR ? CF::S : 1];
-    uint32_t bm8[BNR ? CF::S : 1];
+    // BNR: the BN input x and its ReLU-mask byte at this thread's read-out vectors
+    u32x4_t bx[BNR ? CF::S : 1];
+    unsigned bm8[BNR == 1 ? CF::S : 1];
     if constexpr (BNR) {
 #pragma unroll
       for (int ps = 0; ps < CF::S; ++ps) {
         const int m = min(m0 + orow + ps * CF::RPP, p.M - 1);
         const long idx = (long)m * p.ldc + n0 + oc * 8;
-        bx[ps] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(p.bnr_x) + idx);
-        if constexpr (BNR == 1) bm8[ps] = p.bnr_mask ? (uint32_t)p.bnr_mask[idx >> 3] : 0xffu;
-        else bm8[ps] = 0xffu;
+        bx[ps] = sld128<kAsmSide>(reinterpret_cast<const bf16_t*>(p.bnr_x) + idx);
+        if constexpr (BNR == 1)
+          bm8[ps] = sld8<kAsmSide>(p.bnr_mask ? (const void*)(p.bnr_mask + (idx >> 3)) : (const void*)p.bnr_x);
       }
     }
     const int ahead = i + CF::NBUF - 1;
@@ -249,6 +307,28 @@ __global__ __launch_bounds__(gst::THREADS, 2) void gemm_stream_kernel(const Gemm
         for (int rn = 0; rn < CF::RN; ++rn) acc[mb][rn] = mfma16x16x32(bfr[rn][ks], a, acc[mb][rn]);
       }
 
+    if constexpr (kAsmSide && (RES || BNR)) {
+      // the side loads done, the refill DMA (the D youngest VMEM operations) still in flight; the empty asm
+      // redefines each loaded register here so no use can be scheduled above the wait
+      wait_vm<CF::D>();
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (RES) {
+#pragma unroll
+        for (int mb = 0; mb < BM / 16; ++mb) {
+#pragma unroll
+          for (int rn = 0; rn < CF::RN; ++rn) asm volatile("" : "+v"(rres[mb][rn]));
+          if constexpr (CF::RN == 4) asm volatile("" : "+v"(rmk64[mb]));
+          else asm volatile("" : "+v"(rmk32[mb]));
+        }
+      }
+      if constexpr (BNR) {
+#pragma unroll
+        for (int ps = 0; ps < CF::S; ++ps) {
+          asm volatile("" : "+v"(bx[ps]));
+          if constexpr (BNR == 1) asm volatile("" : "+v"(bm8[ps]));
+        }
+      }
+    }
     // epilogue math in the MFMA layout: acc[mb][rn][e] = C[m0 + 16mb + (lane&15)][n0 + WN*w + 16rn + 4(lane>>4) + e]
 #pragma unroll
     for (int mb = 0; mb < BM / 16; ++mb) {
@@ -260,8 +340,12 @@ __global__ __launch_bounds__(gst::THREADS, 2) void gemm_stream_kernel(const Gemm
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = fmaf(acc[mb][rn][e], p.alpha, bias_r[rn][e]);
         if constexpr (RES) {
-          const uint2 rv = rres[mb][rn];
-          const uint32_t mk = (uint32_t)(rmsk[mb] >> (16 * rn + 4 * (lane >> 4)));
+          const u32x2_t rv = rres[mb][rn];
+          uint64_t mraw;
+          if constexpr (CF::RN == 4) mraw = ((uint64_t)rmk64[mb].y << 32) | rmk64[mb].x;
+          else mraw = rmk32[mb];
+          const uint64_t rm = ((rodd_bits >> mb) & 1u) ? 0ull : (has_mask ? mraw : ~0ull);
+          const uint32_t mk = (uint32_t)(rm >> (16 * rn + 4 * (lane >> 4)));
           v[0] += (mk & 1u) ? __uint_as_float(rv.x << 16) : 0.f;
           v[1] += (mk & 2u) ? __uint_as_float(rv.x & 0xffff0000u) : 0.f;
           v[2] += (mk & 4u) ? __uint_as_float(rv.y << 16) : 0.f;
@@ -289,6 +373,8 @@ __global__ __launch_bounds__(gst::THREADS, 2) void gemm_stream_kernel(const Gemm
         if constexpr (BNR) {  // BN-backward partial sums of the stored gradient (see GemmParams)
           const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
           const uint32_t xv[4] = {bx[ps].x, bx[ps].y, bx[ps].z, bx[ps].w};
+          uint32_t bmk = 0xffu;
+          if constexpr (BNR == 1) bmk = p.bnr_mask ? bm8[ps] : 0xffu;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
 #pragma unroll
@@ -297,7 +383,7 @@ __global__ __launch_bounds__(gst::THREADS, 2) void gemm_stream_kernel(const Gemm
               const float xe = __uint_as_float(h ? (xv[q] & 0xffff0000u) : (xv[q] << 16));
               bool keep;
               if constexpr (BNR == 2) keep = xe * bsc[e] + bsh[e] > 0.f;  // the forward's own fmaf: same bits
-              else keep = (bm8[ps] >> e) & 1u;
+              else keep = (bmk >> e) & 1u;
               const float d = keep ? __uint_as_float(h ? (wv[q] & 0xffff0000u) : (wv[q] << 16)) : 0.f;
               s1[e] += d;
               s2[e] += d * (xe - bmu[e]);

@@ -71,3 +71,16 @@ def test_no_kernel_spills(rows):
 def test_matrix_kernels_do_not_spill(rows, family):
     for r in _pick(rows, family):
         assert r["scratch"] == 0, r
+
+
+def test_stream_side_loads_untouched_before_their_wait():
+    """The streaming kernel's counted asm side-operand loads (K = 256 rings): the compiler treats their
+    destination registers as ready at issue, so no instruction may touch them before the counted wait."""
+    import importlib.util
+
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts", "r6",
+                        "check_side_loads.py")
+    spec = importlib.util.spec_from_file_location("check_side_loads", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    assert mod.hazards(SO) == []
