@@ -134,8 +134,7 @@ __device__ __forceinline__ unsigned ald8(const void* p) {
   asm volatile("global_load_ubyte %0, %1, off" : "=v"(v) : "v"(p) : "memory");
   return v;
 }
-// ASM: the counted asm form (two-slot rings, K = 256: measured faster); otherwise plain loads the compiler
-// waits for itself (deeper rings, K = 64 / 128: the counted wait there also drained the older ring slots)
+// ASM: the counted asm form; otherwise plain loads the compiler waits for itself (kept for A/B)
 template <bool ASM> __device__ __forceinline__ u32x4_t sld128(const void* p) {
   if constexpr (ASM) return ald128(p);
   return *reinterpret_cast<const u32x4_t*>(p);
@@ -164,7 +163,10 @@ template <int WN, int K, int BMODE, bool RES, int BNR = 0>
 __global__ __launch_bounds__(gst::THREADS, 2) void gemm_stream_kernel(const GemmParams p) {
   using namespace gst;
   using CF = Cfg<WN, K>;
-  constexpr bool kAsmSide = CF::NBUF == 2;  // side-operand loads as counted asm (see sld128)
+  // side-operand loads as counted asm (see sld128) on every ring: on the two-slot K = 256 rings it keeps the
+  // refill DMA in flight through the epilogue (ResNet-50 +0.9 %); on the deeper rings it measured equal to
+  // compiler-tracked loads end to end (profiles/r6/stream_side_loads/)
+  constexpr bool kAsmSide = true;
   // the ring and the output staging tile are separate objects: with one array the compiler cannot
   // tell the staging writes from the in-flight LDS-DMA and drains vmcnt(0) before them
   __shared__ __attribute__((aligned(16))) char smem[CF::LDS];  // [ring NBUF x TILE | staging tile]
@@ -239,9 +241,8 @@ __global__ __launch_bounds__(gst::THREADS, 2) void gemm_stream_kernel(const Gemm
     // staging barrier) with the tile NBUF - 1 iterations ahead
     const int m0 = tile_m0(i);
     // residual rows of this tile, issued ahead of the refill so their wait can be counted past it
-    // side operands (counted asm loads on two-slot rings, see sld128): issued ahead of the refill, so the DMA of
-    // the tile NBUF - 1 ahead is the youngest VMEM work when the epilogue waits for them (wait_vm<D>: the ring
-    // stays in flight)
+    // side operands (counted asm loads, see sld128): issued ahead of the refill, so the DMA of the tile
+    // NBUF - 1 ahead is the youngest VMEM work when the epilogue waits for them (the ring stays in flight)
     u32x2_t rres[BM / 16][CF::RN];
     // residual ReLU mask (p.resid_mask): the 16 * RN columns this lane's row touches are 2 * RN
     // consecutive mask bytes — one 2/4/8-byte load per row block (from the residual itself when there is
@@ -307,26 +308,19 @@ __global__ __launch_bounds__(gst::THREADS, 2) void gemm_stream_kernel(const Gemm
         for (int rn = 0; rn < CF::RN; ++rn) acc[mb][rn] = mfma16x16x32(bfr[rn][ks], a, acc[mb][rn]);
       }
 
-    if constexpr (kAsmSide && (RES || BNR)) {
-      // the side loads done, the refill DMA (the D youngest VMEM operations) still in flight; the empty asm
-      // redefines each loaded register here so no use can be scheduled above the wait
-      wait_vm<CF::D>();
+    // counted waits (asm side loads): the residual before the epilogue math, with the BN-reduce loads (issued
+    // after it) and the refill DMA (the youngest) still in flight; the BN-reduce loads before the read-out.
+    // The empty asm redefines each loaded register after its wait, so no use is scheduled above it.
+    constexpr int kBnrLoads = BNR == 1 ? 2 * CF::S : (BNR == 2 ? CF::S : 0);
+    if constexpr (kAsmSide && RES) {
+      wait_vm<CF::D + kBnrLoads>();
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (RES) {
 #pragma unroll
-        for (int mb = 0; mb < BM / 16; ++mb) {
+      for (int mb = 0; mb < BM / 16; ++mb) {
 #pragma unroll
-          for (int rn = 0; rn < CF::RN; ++rn) asm volatile("" : "+v"(rres[mb][rn]));
-          if constexpr (CF::RN == 4) asm volatile("" : "+v"(rmk64[mb]));
-          else asm volatile("" : "+v"(rmk32[mb]));
-        }
-      }
-      if constexpr (BNR) {
-#pragma unroll
-        for (int ps = 0; ps < CF::S; ++ps) {
-          asm volatile("" : "+v"(bx[ps]));
-          if constexpr (BNR == 1) asm volatile("" : "+v"(bm8[ps]));
-        }
+        for (int rn = 0; rn < CF::RN; ++rn) asm volatile("" : "+v"(rres[mb][rn]));
+        if constexpr (CF::RN == 4) asm volatile("" : "+v"(rmk64[mb]));
+        else asm volatile("" : "+v"(rmk32[mb]));
       }
     }
     // epilogue math in the MFMA layout: acc[mb][rn][e] = C[m0 + 16mb + (lane&15)][n0 + WN*w + 16rn + 4(lane>>4) + e]
@@ -362,6 +356,15 @@ __global__ __launch_bounds__(gst::THREADS, 2) void gemm_stream_kernel(const Gemm
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): staging writes done before the barrier
     __builtin_amdgcn_s_barrier();
 
+    if constexpr (kAsmSide && BNR) {
+      wait_vm<CF::D>();
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ps = 0; ps < CF::S; ++ps) {
+        asm volatile("" : "+v"(bx[ps]));
+        if constexpr (BNR == 1) asm volatile("" : "+v"(bm8[ps]));
+      }
+    }
     // read-out: whole rows, 16 B per lane (each thread always owns the same 8 columns)
 #pragma unroll
     for (int ps = 0; ps < CF::S; ++ps) {

@@ -1,7 +1,7 @@
-"""ISA check of the streaming kernel's counted asm side-operand loads (two-slot rings, K = 256: residual rows,
+"""ISA check of the streaming kernel's counted asm side-operand loads (residual rows,
 their ReLU mask, the BN input x and its mask byte): no instruction reads or writes a load's destination
-registers between the load and the counted s_waitcnt after the tile barrier (the compiler does not know the
-loads are asynchronous).  Usage: python scripts/r6/check_side_loads.py (repo root, after the build)."""
+registers between the load and the first s_waitcnt after the tile barrier whose vmcnt is at most the number of
+VMEM operations issued after that load (the compiler does not know the loads are asynchronous).  Usage: python scripts/r6/check_side_loads.py (repo root, after the build)."""
 import os
 import re
 import subprocess
@@ -12,9 +12,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 from distributeddeeplearningspark_amd.utils.isa import code_objects  # noqa: E402
 
-KERNELS = [("ILi16ELi256ELi1ELb1ELi1E", 8), ("ILi16ELi256ELi0ELb1ELi1E", 8), ("ILi16ELi256ELi1ELb0ELi2E", 8),
-           ("ILi16ELi256ELi0ELb0ELi2E", 8), ("ILi16ELi256ELi1ELb0ELi1E", 8), ("ILi16ELi256ELi1ELb1ELi0E", 8),
-           ("ILi32ELi256ELi1ELb1ELi0E", 8), ("ILi32ELi256ELi0ELb1ELi0E", 8)]
+KERNELS = [(k, 0) for k in ("ILi16ELi256ELi1ELb1ELi1E", "ILi16ELi256ELi0ELb1ELi1E", "ILi16ELi256ELi1ELb0ELi2E",
+                            "ILi16ELi256ELi1ELb0ELi1E", "ILi16ELi256ELi1ELb1ELi0E", "ILi32ELi256ELi1ELb1ELi0E",
+                            "ILi16ELi64ELi1ELb1ELi1E", "ILi32ELi64ELi1ELb1ELi1E", "ILi16ELi128ELi1ELb1ELi1E",
+                            "ILi32ELi128ELi1ELb1ELi1E", "ILi32ELi64ELi1ELb0ELi2E", "ILi32ELi128ELi1ELb0ELi2E",
+                            "ILi32ELi64ELi1ELb1ELi0E", "ILi64ELi64ELi1ELb1ELi0E", "ILi32ELi128ELi1ELb1ELi0E",
+                            "ILi16ELi128ELi1ELb1ELi0E", "ILi32ELi64ELi0ELb1ELi1E", "ILi16ELi256ELi0ELb0ELi2E")]
 _LOAD = re.compile(r"\s*global_load_(?:ushort|ubyte|dwordx2|dwordx4|dword)\s+(v\[\d+:\d+\]|v\d+),")
 
 
@@ -52,16 +55,18 @@ def hazards(so=os.path.join(ROOT, "distributeddeeplearningspark_amd", "_C.so")):
             lm = _LOAD.match(lines[i])
             if not lm:
                 continue
-            rs, barrier = _regs(lm.group(1)), False
+            rs, barrier, younger = _regs(lm.group(1)), False, 0
             for j in range(i + 1, len(lines)):
                 if "s_barrier" in lines[j]:
                     barrier = True
                 w = re.search(r"s_waitcnt vmcnt\((\d+)\)", lines[j])
-                if barrier and w and int(w.group(1)) <= D:
+                if barrier and w and int(w.group(1)) <= younger:  # vmcnt(k) with k <= later VMEM ops: done
                     break
                 if rs & _regs(lines[j]):
                     found.append((name, lines[j].strip()))
                     break
+                if re.match(r"\s*(global_|buffer_)", lines[j]):
+                    younger += 1
     return found
 
 
