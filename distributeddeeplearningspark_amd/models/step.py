@@ -38,8 +38,7 @@ def graph_capture(g, stream):
     streams of finished models), and their HIP calls are illegal while a stream captures — the process
     aborts (seen once in the GPU suite, a co-located replica capture collecting mid-window)."""
     was = gc.isenabled()
-    gc.collect()
-    gc.disable()
+    gc.disable()  # no gc.collect() first: a full collection per capture cost the NYISO replica groups ~50 ms
     try:
         with torch.cuda.graph(g, stream=stream):
             yield
